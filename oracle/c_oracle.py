@@ -1,0 +1,97 @@
+"""ORACLE -- test infrastructure only (ctypes binding of oracle/c/rdfind_oracle.c).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may use this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liborc.so")
+_lib = None
+
+UNARY_CODES = (10, 12, 17, 20, 33, 34)
+BINARY_CODES = (14, 21, 35)
+
+
+class OrcCind(ctypes.Structure):
+    _fields_ = [("dep", ctypes.c_uint32), ("ref", ctypes.c_uint32), ("support", ctypes.c_uint32)]
+
+
+class OrcStats(ctypes.Structure):
+    _fields_ = [("n_freq_unary", ctypes.c_uint64 * 3), ("n_binary_keys", ctypes.c_uint64),
+                ("n_freq_binary", ctypes.c_uint64), ("n_records", ctypes.c_uint64),
+                ("n_unique", ctypes.c_uint64), ("n_groups", ctypes.c_uint64),
+                ("n_freq_captures", ctypes.c_uint64), ("n_raw_cinds", ctypes.c_uint64),
+                ("n_cinds", ctypes.c_uint64)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        lib = ctypes.CDLL(_LIB_PATH)
+        lib.orc_run.restype = ctypes.c_int
+        lib.orc_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                         ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                                         ctypes.POINTER(ctypes.POINTER(OrcCind)),
+                                                         ctypes.POINTER(ctypes.c_uint64),
+                                                         ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                                         ctypes.POINTER(ctypes.c_uint64),
+                                                         ctypes.POINTER(OrcStats)]
+        lib.orc_free.argtypes = [ctypes.c_void_p]
+        _lib = lib
+    return _lib
+
+
+def decode_capture(cap, num_terms, bin_keys):
+    """capture id -> (code, v1, v2|None)"""
+    V = num_terms
+    if cap < 6 * V:
+        return UNARY_CODES[cap // V], cap % V, None
+    key = int(bin_keys[cap - 6 * V])
+    return BINARY_CODES[key >> 62], (key >> 31) & 0x7FFFFFFF, key & 0x7FFFFFFF
+
+
+def run(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):
+    """Returns (set of (dt, dv1, dv2, rt, rv1, rv2, support), stats dict, raw arrays)."""
+    lib = _load()
+    s = np.ascontiguousarray(s, dtype=np.uint32)
+    p = np.ascontiguousarray(p, dtype=np.uint32)
+    o = np.ascontiguousarray(o, dtype=np.uint32)
+    out = ctypes.POINTER(OrcCind)()
+    n_out = ctypes.c_uint64()
+    bk = ctypes.POINTER(ctypes.c_uint64)()
+    nbk = ctypes.c_uint64()
+    st = OrcStats()
+    rc = lib.orc_run(s.ctypes.data, p.ctypes.data, o.ctypes.data, len(s), num_terms, min_support,
+                     strategy, int(clean), projection.encode(), ctypes.byref(out), ctypes.byref(n_out),
+                     ctypes.byref(bk), ctypes.byref(nbk), ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"orc_run failed with {rc}")
+    n = n_out.value
+    arr = np.ctypeslib.as_array(out, shape=(n,)).copy() if n else np.zeros(0, dtype=[("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])
+    keys = np.ctypeslib.as_array(bk, shape=(nbk.value,)).copy() if nbk.value else np.zeros(0, np.uint64)
+    lib.orc_free(out)
+    lib.orc_free(bk)
+    stats = {f: (list(getattr(st, f)) if f == "n_freq_unary" else getattr(st, f)) for f, _ in OrcStats._fields_}
+    return arr, keys, stats
+
+
+def run_set(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):
+    arr, keys, stats = run(s, p, o, num_terms, min_support, strategy, clean, projection)
+    out = set()
+    for dep, ref, sup in zip(arr["dep"].tolist(), arr["ref"].tolist(), arr["support"].tolist()):
+        dt, dv1, dv2 = decode_capture(dep, num_terms, keys)
+        rt, rv1, rv2 = decode_capture(ref, num_terms, keys)
+        out.add((dt, dv1, dv2, rt, rv1, rv2, sup))
+    return out, stats
