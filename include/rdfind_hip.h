@@ -1,0 +1,126 @@
+/*
+ * rdfind_hip.h -- C ABI of the MI355X-native RDFind CIND-discovery hot path (librdfind_hip.so).
+ *
+ * Plain C types only.  Each entry point replaces one operator boundary of the reference
+ * (stratosphere/rdfind; ALG/ = rdfind-algorithm/src/main/scala/de/hpi/isg/sodap/rdfind/):
+ *
+ *   rdf_set_triples            the DataSet[RDFTriple] handed to the plan
+ *                              (ALG/programs/RDFind.scala:220-237, RDFTriple ALG/data/RDFTriple.scala:7),
+ *                              dictionary-encoded: one uint32 id space for s, p and o.
+ *   rdf_frequent_conditions    FrequentConditionPlanner.constructFrequentConditionPlan
+ *                              (ALG/plan/FrequentConditionPlanner.scala:230-319), called at
+ *                              ALG/programs/RDFind.scala:290-296 (--use-fis).
+ *   rdf_build_capture_groups   CreateJoinPartners (RichFlatMapFunction, ALG/operators/CreateJoinPartners.scala:23-147)
+ *                              -> UnionJoinCandidates (ALG/operators/UnionJoinCandidates.scala:19-44)
+ *                              -> UnionCombinedJoinCandidates (ALG/operators/UnionCombinedJoinCandidates.scala:17-31),
+ *                              wired at ALG/programs/RDFind.scala:310-346.
+ *   rdf_discover_cinds         TraversalStrategy.enhanceFlinkPlan (ALG/plan/TraversalStrategy.scala:28-33),
+ *                              selected at ALG/programs/RDFind.scala:50-56 and called at :459, including
+ *                              splitAndCleanCindSets / removeImpliedCinds (ALG/plan/TraversalStrategy.scala:45-168).
+ *   rdf_copy_cinds             the DataSet[Cind] result (ALG/data/Cind.scala:12-31) before Cind.toString.
+ *
+ * Conventions (mirroring the reference's one-UDF-instance-per-task model):
+ *   - inputs are borrowed and copied to HBM before the call returns (rdf_set_triples), or borrowed
+ *     device pointers that must stay valid until the next rdf_set_triples* call;
+ *   - results are library-owned and device-resident until copied out or the next call;
+ *   - no exceptions cross the ABI: every call returns rdf_status (0 = OK, < 0 = error) and
+ *     rdf_last_error() describes the last failure; errors are sticky per call, not per context;
+ *   - a context is not thread-safe; different contexts (one per GPU) may run concurrently.
+ */
+#ifndef RDFIND_HIP_H
+#define RDFIND_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t rdf_status;
+#define RDF_OK 0
+#define RDF_ERR_ARG (-1)      /* invalid argument (IllegalArgumentException in the reference) */
+#define RDF_ERR_HIP (-2)      /* HIP runtime / device error */
+#define RDF_ERR_OOM (-3)      /* device memory exhausted */
+#define RDF_ERR_STATE (-4)    /* stage called out of order (IllegalStateException) */
+#define RDF_ERR_LIMIT (-5)    /* input exceeds an implementation limit (e.g. >= 2^30 terms) */
+
+/* rdf_discover_cinds flags */
+#define RDF_CLEAN_IMPLIED 1u          /* --clean-implied: R1-R4 minimality (TraversalStrategy.scala:126-168) */
+#define RDF_STRATEGY_ALL_AT_ONCE 2u   /* --traversal-strategy 0 semantics (literal Condition.isImpliedBy);
+                                         default is strategy 1 (S2L) */
+
+typedef struct rdf_ctx rdf_ctx;
+
+typedef struct {
+    uint32_t min_support;
+    uint32_t reserved;
+    uint64_t n_frequent_unary[3];   /* frequent s / p / o conditions */
+    uint64_t n_binary_keys;         /* distinct candidate binary conditions counted */
+    uint64_t n_frequent_binary;     /* frequent binary conditions */
+} rdf_fc_stats;
+
+typedef struct {
+    uint64_t n_records;             /* (join value, capture) join partners emitted */
+    uint64_t n_frequent_records;    /* distinct records of captures with support >= min_support */
+    uint64_t n_groups;              /* capture groups (join values) */
+    uint64_t n_captures;            /* captures with support >= min_support (dependent candidates) */
+    uint64_t n_unary_captures;
+    uint64_t n_heavy_groups;        /* groups tracked as bitmask columns */
+    uint64_t heavy_threshold;       /* minimum size of a heavy group */
+} rdf_group_stats;
+
+typedef struct {
+    uint64_t n_cinds;               /* CINDs in the result */
+    uint64_t n_explicit_raw;        /* raw CINDs of dependents with a light group */
+    uint64_t n_light_chunks;
+    uint64_t n_heavy_chunks;
+    float ms_pivot, ms_light, ms_rules, ms_heavy;  /* device time per K6/K7 kernel family */
+} rdf_cind_stats;
+
+/* One result row: capture ids (see rdf_decode_capture) and the support of the dependent. */
+typedef struct {
+    uint32_t dep;
+    uint32_t ref;
+    uint32_t support;
+} rdf_cind;
+
+rdf_status rdf_ctx_create(int device, rdf_ctx** out);
+void rdf_ctx_destroy(rdf_ctx* ctx);
+const char* rdf_last_error(const rdf_ctx* ctx);
+const char* rdf_version(void);
+
+rdf_status rdf_set_triples(rdf_ctx* ctx, const uint32_t* s, const uint32_t* p, const uint32_t* o,
+                           uint64_t n, uint32_t num_terms);
+rdf_status rdf_set_triples_device(rdf_ctx* ctx, const uint32_t* d_s, const uint32_t* d_p, const uint32_t* d_o,
+                                  uint64_t n, uint32_t num_terms);
+
+rdf_status rdf_frequent_conditions(rdf_ctx* ctx, uint32_t min_support, rdf_fc_stats* stats);
+/* projection: any combination of 's', 'p', 'o' (--projection, default "spo"). */
+rdf_status rdf_build_capture_groups(rdf_ctx* ctx, const char* projection, rdf_group_stats* stats);
+rdf_status rdf_discover_cinds(rdf_ctx* ctx, uint32_t flags, rdf_cind_stats* stats);
+
+/* Whole pipeline on the current triples (the three stages above). */
+rdf_status rdf_run(rdf_ctx* ctx, uint32_t min_support, const char* projection, uint32_t flags,
+                   rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs);
+
+rdf_status rdf_cind_count(rdf_ctx* ctx, uint64_t* n);
+/* Copies min(cap, count) rows to host memory; *n_copied receives the number copied. */
+rdf_status rdf_copy_cinds(rdf_ctx* ctx, rdf_cind* out, uint64_t cap, uint64_t* n_copied);
+
+/* Capture ids: unary type t (codes 10,12,17,20,33,34) with value v -> t*V + v; binary capture b
+ * (codes 14,21,35) -> 6V + b.  Decodes to the capture code and its condition values
+ * (value2 = UINT32_MAX for unary captures). */
+rdf_status rdf_decode_capture(rdf_ctx* ctx, uint32_t capture, uint32_t* code, uint32_t* value1, uint32_t* value2);
+/* Frequent binary condition keys (bt << 62 | v1 << 31 | v2), indexed by b. */
+rdf_status rdf_binary_key_count(rdf_ctx* ctx, uint64_t* n);
+rdf_status rdf_copy_binary_keys(rdf_ctx* ctx, uint64_t* out, uint64_t cap);
+
+/* Device time (ms) of the last call of each stage: [0] fc, [1] groups, [2] cinds. */
+rdf_status rdf_stage_times(rdf_ctx* ctx, float* ms3);
+/* Synchronise the context stream. */
+rdf_status rdf_sync(rdf_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RDFIND_HIP_H */

@@ -1,0 +1,255 @@
+"""ctypes binding of the C ABI in ``include/rdfind_hip.h`` (``rdfind_amd/librdfind_hip.so``).
+
+This is the product path: there is no CPU fallback.  If the HIP library is missing or no GPU is
+visible, :func:`load` / :class:`Context` raise immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import codes
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librdfind_hip.so")
+
+RDF_CLEAN_IMPLIED = 1
+RDF_STRATEGY_ALL_AT_ONCE = 2
+
+# every symbol declared in include/rdfind_hip.h
+EXPORTED_SYMBOLS = (
+    "rdf_ctx_create", "rdf_ctx_destroy", "rdf_last_error", "rdf_version", "rdf_set_triples",
+    "rdf_set_triples_device", "rdf_frequent_conditions", "rdf_build_capture_groups", "rdf_discover_cinds",
+    "rdf_run", "rdf_cind_count", "rdf_copy_cinds", "rdf_decode_capture", "rdf_binary_key_count",
+    "rdf_copy_binary_keys", "rdf_stage_times", "rdf_sync",
+)
+
+
+class FcStats(ctypes.Structure):
+    _fields_ = [("min_support", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("n_frequent_unary", ctypes.c_uint64 * 3), ("n_binary_keys", ctypes.c_uint64),
+                ("n_frequent_binary", ctypes.c_uint64)]
+
+
+class GroupStats(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("n_frequent_records", ctypes.c_uint64),
+                ("n_groups", ctypes.c_uint64), ("n_captures", ctypes.c_uint64),
+                ("n_unary_captures", ctypes.c_uint64), ("n_heavy_groups", ctypes.c_uint64),
+                ("heavy_threshold", ctypes.c_uint64)]
+
+
+class CindStats(ctypes.Structure):
+    _fields_ = [("n_cinds", ctypes.c_uint64), ("n_explicit_raw", ctypes.c_uint64),
+                ("n_light_chunks", ctypes.c_uint64), ("n_heavy_chunks", ctypes.c_uint64),
+                ("ms_pivot", ctypes.c_float), ("ms_light", ctypes.c_float), ("ms_rules", ctypes.c_float),
+                ("ms_heavy", ctypes.c_float)]
+
+
+CIND_DTYPE = np.dtype([("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])
+
+_lib = None
+
+
+class RdfError(RuntimeError):
+    pass
+
+
+def load():
+    """Load librdfind_hip.so (raises if it is missing: the product has no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RdfError(f"{LIB_PATH} not built; run __graft_entry__.build() (HIP extension missing)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    sig = {
+        "rdf_ctx_create": (i32, [ctypes.c_int, ctypes.POINTER(P)]),
+        "rdf_ctx_destroy": (None, [P]),
+        "rdf_last_error": (ctypes.c_char_p, [P]),
+        "rdf_version": (ctypes.c_char_p, []),
+        "rdf_set_triples": (i32, [P, P, P, P, u64, u32]),
+        "rdf_set_triples_device": (i32, [P, P, P, P, u64, u32]),
+        "rdf_frequent_conditions": (i32, [P, u32, ctypes.POINTER(FcStats)]),
+        "rdf_build_capture_groups": (i32, [P, ctypes.c_char_p, ctypes.POINTER(GroupStats)]),
+        "rdf_discover_cinds": (i32, [P, u32, ctypes.POINTER(CindStats)]),
+        "rdf_run": (i32, [P, u32, ctypes.c_char_p, u32, ctypes.POINTER(FcStats), ctypes.POINTER(GroupStats),
+                          ctypes.POINTER(CindStats)]),
+        "rdf_cind_count": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_copy_cinds": (i32, [P, P, u64, ctypes.POINTER(u64)]),
+        "rdf_decode_capture": (i32, [P, u32, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
+        "rdf_binary_key_count": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_copy_binary_keys": (i32, [P, P, u64]),
+        "rdf_stage_times": (i32, [P, ctypes.POINTER(ctypes.c_float)]),
+        "rdf_sync": (i32, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _struct_dict(st):
+    out = {}
+    for name, _ in st._fields_:
+        val = getattr(st, name)
+        out[name] = list(val) if isinstance(val, ctypes.Array) else val
+    return out
+
+
+class Context:
+    """One GPU context (one per device / rank), mirroring one Flink task instance."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.ptr = ctypes.c_void_p()
+        rc = self.lib.rdf_ctx_create(device, ctypes.byref(self.ptr))
+        if rc != 0:
+            raise RdfError(f"rdf_ctx_create(device={device}) failed ({rc}): is a GPU visible?")
+        self.num_terms = 0
+        self.fc = self.groups = self.cinds = None
+
+    def close(self):
+        if self.ptr:
+            self.lib.rdf_ctx_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.rdf_last_error(self.ptr)
+            raise RdfError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    # -- stages ------------------------------------------------------------------------------
+    def set_triples(self, s, p, o, num_terms: int):
+        s = np.ascontiguousarray(s, dtype=np.uint32)
+        p = np.ascontiguousarray(p, dtype=np.uint32)
+        o = np.ascontiguousarray(o, dtype=np.uint32)
+        if not (s.shape == p.shape == o.shape):
+            raise ValueError("s, p, o must have the same length")
+        self._check(self.lib.rdf_set_triples(self.ptr, s.ctypes.data, p.ctypes.data, o.ctypes.data, s.shape[0],
+                                             num_terms), "rdf_set_triples")
+        self.num_terms = num_terms
+
+    def set_triples_device(self, s_ptr: int, p_ptr: int, o_ptr: int, n: int, num_terms: int):
+        self._check(self.lib.rdf_set_triples_device(self.ptr, s_ptr, p_ptr, o_ptr, n, num_terms),
+                    "rdf_set_triples_device")
+        self.num_terms = num_terms
+
+    def frequent_conditions(self, min_support: int):
+        st = FcStats()
+        self._check(self.lib.rdf_frequent_conditions(self.ptr, min_support, ctypes.byref(st)),
+                    "rdf_frequent_conditions")
+        self.fc = _struct_dict(st)
+        return self.fc
+
+    def build_capture_groups(self, projection: str = "spo"):
+        st = GroupStats()
+        self._check(self.lib.rdf_build_capture_groups(self.ptr, projection.encode(), ctypes.byref(st)),
+                    "rdf_build_capture_groups")
+        self.groups = _struct_dict(st)
+        return self.groups
+
+    def discover_cinds(self, clean_implied: bool = True, traversal_strategy: int = 1):
+        flags = (RDF_CLEAN_IMPLIED if clean_implied else 0) | (RDF_STRATEGY_ALL_AT_ONCE if traversal_strategy == 0 else 0)
+        st = CindStats()
+        self._check(self.lib.rdf_discover_cinds(self.ptr, flags, ctypes.byref(st)), "rdf_discover_cinds")
+        self.cinds = _struct_dict(st)
+        return self.cinds
+
+    def run(self, min_support=10, projection="spo", clean_implied=True, traversal_strategy=1):
+        self.frequent_conditions(min_support)
+        self.build_capture_groups(projection)
+        return self.discover_cinds(clean_implied, traversal_strategy)
+
+    def sync(self):
+        self._check(self.lib.rdf_sync(self.ptr), "rdf_sync")
+
+    def stage_times(self):
+        arr = (ctypes.c_float * 3)()
+        self._check(self.lib.rdf_stage_times(self.ptr, arr), "rdf_stage_times")
+        return list(arr)
+
+    # -- results -----------------------------------------------------------------------------
+    def cind_count(self) -> int:
+        n = ctypes.c_uint64()
+        self._check(self.lib.rdf_cind_count(self.ptr, ctypes.byref(n)), "rdf_cind_count")
+        return n.value
+
+    def copy_cinds(self) -> np.ndarray:
+        n = self.cind_count()
+        out = np.empty(n, dtype=CIND_DTYPE)
+        copied = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_cinds(self.ptr, out.ctypes.data, n, ctypes.byref(copied)), "rdf_copy_cinds")
+        return out[: copied.value]
+
+    def binary_keys(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        self._check(self.lib.rdf_binary_key_count(self.ptr, ctypes.byref(n)), "rdf_binary_key_count")
+        out = np.empty(n.value, dtype=np.uint64)
+        if n.value:
+            self._check(self.lib.rdf_copy_binary_keys(self.ptr, out.ctypes.data, n.value), "rdf_copy_binary_keys")
+        return out
+
+    def decoded_cinds(self):
+        """Structured array with (dep_code, dep_v1, dep_v2, ref_code, ref_v1, ref_v2, support);
+        v2 = 0xFFFFFFFF for unary captures."""
+        rows = self.copy_cinds()
+        return decode_rows(rows, self.num_terms, self.binary_keys())
+
+
+DECODED_DTYPE = np.dtype([("dep_code", "u1"), ("dep_v1", "<u4"), ("dep_v2", "<u4"), ("ref_code", "u1"),
+                          ("ref_v1", "<u4"), ("ref_v2", "<u4"), ("support", "<u4")])
+
+
+def decode_captures(cap: np.ndarray, num_terms: int, bin_keys: np.ndarray):
+    """Vectorised capture id -> (code, v1, v2)."""
+    V = np.uint64(max(num_terms, 1))
+    cap = cap.astype(np.uint64)
+    unary = cap < np.uint64(6) * V
+    code = np.empty(cap.shape, np.uint8)
+    v1 = np.empty(cap.shape, np.uint32)
+    v2 = np.full(cap.shape, 0xFFFFFFFF, np.uint32)
+    ucodes = np.array(codes.UNARY_CODES, np.uint8)
+    code[unary] = ucodes[(cap[unary] // V).astype(np.int64)]
+    v1[unary] = (cap[unary] % V).astype(np.uint32)
+    if (~unary).any():
+        keys = bin_keys[(cap[~unary] - np.uint64(6) * V).astype(np.int64)]
+        bcodes = np.array(codes.BINARY_CODES, np.uint8)
+        code[~unary] = bcodes[(keys >> np.uint64(62)).astype(np.int64)]
+        v1[~unary] = ((keys >> np.uint64(31)) & np.uint64(0x7FFFFFFF)).astype(np.uint32)
+        v2[~unary] = (keys & np.uint64(0x7FFFFFFF)).astype(np.uint32)
+    return code, v1, v2
+
+
+def decode_rows(rows: np.ndarray, num_terms: int, bin_keys: np.ndarray) -> np.ndarray:
+    out = np.empty(rows.shape[0], dtype=DECODED_DTYPE)
+    out["dep_code"], out["dep_v1"], out["dep_v2"] = decode_captures(rows["dep"], num_terms, bin_keys)
+    out["ref_code"], out["ref_v1"], out["ref_v2"] = decode_captures(rows["ref"], num_terms, bin_keys)
+    out["support"] = rows["support"]
+    return out
+
+
+def decoded_to_set(dec: np.ndarray):
+    """Set of (dt, dv1, dv2|None, rt, rv1, rv2|None, support) -- the oracle's comparison form."""
+    none = 0xFFFFFFFF
+    out = set()
+    for r in dec.tolist():
+        dt, dv1, dv2, rt, rv1, rv2, sup = r
+        out.add((dt, dv1, None if dv2 == none else dv2, rt, rv1, None if rv2 == none else rv2, sup))
+    return out

@@ -1,0 +1,42 @@
+// Kernel declarations for the CIND-discovery pipeline.
+#pragma once
+#include "common.hpp"
+
+namespace rdf {
+
+static constexpr int LH_SLOTS = 4096;     // LDS hash slots (u32 keys) for unary counting
+static constexpr int LB_SLOTS = 2048;     // LDS hash slots (u64 keys) for binary counting
+static constexpr int HMAX = 64;           // heavy groups tracked as bit columns (one u64 per capture)
+static constexpr uint8_t LIGHT = 0xff;
+
+// per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
+struct __align__(16) CapInfo {
+    u64 hmask;     // bit j set <=> capture is in heavy group j
+    u32 support;   // number of capture groups containing it (distinct join values)
+    u32 meta;      // bit0 binary, bit1 has parents, bit2 heavy-only
+};
+static constexpr u32 META_BIN = 1u, META_PARENTS = 2u, META_HEAVY_ONLY = 4u;
+
+// Rule modes for K7 (TraversalStrategy.removeImpliedCinds, TraversalStrategy.scala:126-168)
+enum RuleMode : int { RULES_NONE = 0, RULES_S2L_RAW = 1, RULES_CLEAN = 2 };
+
+struct CindView {
+    // compact capture space [0, C); unary compact ids are [0, Cu), binary [Cu, C)
+    u32 C, Cu;
+    const CapInfo* info;
+    const u32* gcap;      // group members (compact ids), sorted within a group
+    const u64* goff;      // group offsets [G+1]
+    const uint8_t* hbit;  // heavy bit of a group or LIGHT
+    const u64* doff;      // dependent -> groups offsets [C+1]
+    const u32* dgrp;      // dependent -> group ids
+    const u32* bcomp;     // binary compact id b: components at [2*(b-Cu)], [2*(b-Cu)+1]
+    const u64* bkeyc;     // binary compact id b: bin key (bt, v1, v2)
+    const u64* poff;      // unary compact id -> parents offsets [Cu+1]
+    const u32* plist;     // parents (binary compact ids)
+    const u64* eoff;      // explicit CSR: dep -> refs [C+1]
+    const u64* epairs;    // explicit (dep << 32 | ref) pairs, sorted
+    int literal;          // strategy-0 Condition.isImpliedBy quirk
+    int mode;             // RuleMode
+};
+
+}  // namespace rdf

@@ -1,0 +1,243 @@
+// Device-wide primitives: exclusive scan and LSD radix sort of 64-bit keys (gfx950, wave64).
+//
+// The radix sort is the grouping engine that replaces Flink's sort-based groupBy on the join value
+// (ALG/programs/RDFind.scala:339-345 groupBy("joinValue") -> combineGroup -> reduceGroup): records are
+// packed as (join << capbits | capture) and sorted on exactly the needed bits, 8 bits per pass.
+// Per pass: (1) per-tile 256-bin digit histogram in LDS, (2) device exclusive scan of the digit-major
+// histogram, (3) stable scatter where each key's in-tile rank comes from wave ballots (8 ballots give
+// the peer mask of lanes with the same digit) plus per-wave running digit counters in LDS.
+#include "primitives.hpp"
+
+namespace rdf {
+
+// ------------------------------------------------------------------------------------------------
+// Block-level helpers
+
+template <typename T>
+__device__ inline T block_exclusive_scan(T v, T* lds_wave, T* total) {
+    const int lane = lane_id();
+    const int wave = threadIdx.x / RDF_WAVE;
+    T incl = v;
+#pragma unroll
+    for (int off = 1; off < RDF_WAVE; off <<= 1) {
+        T t = __shfl_up(incl, off, RDF_WAVE);
+        if (lane >= off) incl += t;
+    }
+    if (lane == RDF_WAVE - 1) lds_wave[wave] = incl;
+    __syncthreads();
+    T wave_off = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
+        T x = lds_wave[w];
+        if (w < wave) wave_off += x;
+        sum += x;
+    }
+    *total = sum;
+    __syncthreads();
+    return wave_off + incl - v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Exclusive scan: out[i] = sum_{j<i} in[j]   (reduce-then-scan, tile = 256 threads x 16 items)
+
+static constexpr int SCAN_ITEMS = 16;
+static constexpr int SCAN_TILE = RDF_BLOCK * SCAN_ITEMS;
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_reduce(const TI* __restrict__ in, u64 n, TO* __restrict__ tile_sums) {
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    TO acc = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        if (idx < n) acc += (TO)in[idx];
+    }
+    TO total;
+    block_exclusive_scan<TO>(acc, lds_wave, &total);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+template <typename TO>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_single(TO* __restrict__ a, u64 n, TO* __restrict__ grand_total) {
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    TO carry = 0;
+    for (u64 base = 0; base < n; base += SCAN_TILE) {
+        TO v[SCAN_ITEMS];
+        TO local = 0;
+        const u64 tb = base + (u64)threadIdx.x * SCAN_ITEMS;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            v[i] = (tb + i < n) ? a[tb + i] : (TO)0;
+            local += v[i];
+        }
+        TO total;
+        TO off = block_exclusive_scan<TO>(local, lds_wave, &total) + carry;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            if (tb + i < n) a[tb + i] = off;
+            off += v[i];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0 && grand_total) *grand_total = carry;
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply(const TI* __restrict__ in, TO* __restrict__ out, u64 n,
+                                                          const TO* __restrict__ tile_offsets) {
+    __shared__ TO lds[SCAN_TILE];
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        lds[i * RDF_BLOCK + threadIdx.x] = (idx < n) ? (TO)in[idx] : (TO)0;
+    }
+    __syncthreads();
+    TO v[SCAN_ITEMS];
+    TO local = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        v[i] = lds[threadIdx.x * SCAN_ITEMS + i];
+        local += v[i];
+    }
+    TO total;
+    TO off = block_exclusive_scan<TO>(local, lds_wave, &total) + tile_offsets[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        lds[threadIdx.x * SCAN_ITEMS + i] = off;
+        off += v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        if (idx < n) out[idx] = lds[i * RDF_BLOCK + threadIdx.x];
+    }
+}
+
+template <typename TI, typename TO>
+static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 n, TO* d_total, hipStream_t st) {
+    if (n == 0) {
+        if (d_total) return hipMemsetAsync(d_total, 0, sizeof(TO), st);
+        return hipSuccess;
+    }
+    u64 tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    TO* sums = (TO*)ws.scratch(tiles * sizeof(TO), 0);
+    if (!sums) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, n, sums);
+    hipLaunchKernelGGL((k_scan_single<TO>), dim3(1), dim3(RDF_BLOCK), 0, st, sums, tiles, d_total);
+    hipLaunchKernelGGL((k_scan_apply<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n, sums);
+    return hipGetLastError();
+}
+
+hipError_t exclusive_scan_u32_u64(Workspace& ws, const u32* in, u64* out, u64 n, u64* d_total, hipStream_t st) {
+    return exclusive_scan_impl<u32, u64>(ws, in, out, n, d_total, st);
+}
+hipError_t exclusive_scan_u64(Workspace& ws, const u64* in, u64* out, u64 n, u64* d_total, hipStream_t st) {
+    return exclusive_scan_impl<u64, u64>(ws, in, out, n, d_total, st);
+}
+hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32* d_total, hipStream_t st) {
+    return exclusive_scan_impl<u32, u32>(ws, in, out, n, d_total, st);
+}
+
+// ------------------------------------------------------------------------------------------------
+// LSD radix sort of u64 keys
+
+static constexpr int RS_ITEMS = 16;                              // keys per lane per tile
+static constexpr int RS_TILE = RDF_BLOCK * RS_ITEMS;             // 4096 keys per tile
+static constexpr int RS_WAVE_KEYS = RDF_WAVE * RS_ITEMS;         // 1024 keys per wave
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_radix_hist(const u64* __restrict__ keys, u64 n, int shift,
+                                                          u32* __restrict__ hist, u32 num_tiles) {
+    __shared__ u32 cnt[256];
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 base = (u64)blockIdx.x * RS_TILE;
+#pragma unroll
+    for (int i = 0; i < RS_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    hist[(u64)threadIdx.x * num_tiles + blockIdx.x] = cnt[threadIdx.x];
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
+                                                             int shift, const u32* __restrict__ offs, u32 num_tiles) {
+    __shared__ u32 wcount[RDF_WAVES_PER_BLOCK][256];
+    __shared__ u32 gbase[256];
+    const int lane = lane_id();
+    const int wave = threadIdx.x / RDF_WAVE;
+#pragma unroll
+    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) wcount[w][threadIdx.x] = 0;
+    gbase[threadIdx.x] = offs[(u64)threadIdx.x * num_tiles + blockIdx.x];
+    __syncthreads();
+
+    const u64 wbase = (u64)blockIdx.x * RS_TILE + (u64)wave * RS_WAVE_KEYS;
+    u64 k[RS_ITEMS];
+    u32 rank[RS_ITEMS];
+    const u64 lt = lanemask_lt();
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        u64 idx = wbase + (u64)r * RDF_WAVE + lane;
+        bool valid = idx < n;
+        k[r] = valid ? keys[idx] : 0;
+        u32 d = (u32)((k[r] >> shift) & 255);
+        // peer mask: lanes with the same digit (invalid lanes form their own group via a 9th bit)
+        u64 peers = __ballot(valid);
+        if (!valid) peers = ~peers;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            u64 bb = __ballot((d >> b) & 1);
+            peers &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        u32 before = (u32)__popcll(peers & lt);
+        u32 old = valid ? wcount[wave][d] : 0;
+        // the highest peer lane publishes the new running count (reads above precede this write)
+        bool last = valid && ((peers >> lane) >> 1) == 0;
+        if (last) wcount[wave][d] = old + before + 1;
+        rank[r] = old + before;
+    }
+    __syncthreads();
+    {   // exclusive prefix over waves per digit
+        u32 run = 0;
+#pragma unroll
+        for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
+            u32 c = wcount[w][threadIdx.x];
+            wcount[w][threadIdx.x] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        u64 idx = wbase + (u64)r * RDF_WAVE + lane;
+        if (idx < n) {
+            u32 d = (u32)((k[r] >> shift) & 255);
+            out[(u64)gbase[d] + wcount[wave][d] + rank[r]] = k[r];
+        }
+    }
+}
+
+hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st) {
+    if (n < 2 || bits <= 0) return hipSuccess;
+    if (n >= (1ull << 32)) return hipErrorInvalidValue;
+    const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
+    const u64 hn = (u64)tiles * 256;
+    u32* hist = (u32*)ws.scratch(hn * sizeof(u32), 1);
+    if (!hist) return hipErrorOutOfMemory;
+    for (int shift = 0; shift < bits; shift += 8) {
+        hipLaunchKernelGGL(k_radix_hist, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, hist, tiles);
+        hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, nullptr, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_radix_scatter, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, hist, tiles);
+        u64* t = keys;
+        keys = tmp;
+        tmp = t;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rdf

@@ -1,0 +1,60 @@
+// Device memory + primitive declarations.
+#pragma once
+#include "common.hpp"
+
+namespace rdf {
+
+// Grow-only device buffer.  Re-allocation only happens when a call needs more than before, so a
+// steady-state pipeline (the bench's repeated steps) allocates nothing.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        cap = want;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T* as() const { return (T*)p; }
+};
+
+struct Workspace {
+    static constexpr int kSlots = 8;
+    DevBuf slot[kSlots];
+    void* scratch(size_t bytes, int s) {
+        if (s < 0 || s >= kSlots) return nullptr;
+        if (slot[s].ensure(bytes) != hipSuccess) return nullptr;
+        return slot[s].p;
+    }
+    void release() {
+        for (auto& b : slot) b.release();
+    }
+};
+
+// out[i] = sum_{j<i} in[j]; *d_total (device, optional) = sum of all.  In-place allowed.
+hipError_t exclusive_scan_u32_u64(Workspace& ws, const u32* in, u64* out, u64 n, u64* d_total, hipStream_t st);
+hipError_t exclusive_scan_u64(Workspace& ws, const u64* in, u64* out, u64 n, u64* d_total, hipStream_t st);
+hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32* d_total, hipStream_t st);
+
+// LSD radix sort on the low `bits` bits; keys/tmp are swapped so that `keys` holds the result.
+// Uses workspace slots 0 and 1.  Requires n < 2^32.
+hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st);
+
+}  // namespace rdf

@@ -1,0 +1,707 @@
+// librdfind_hip.so: C-ABI host orchestration of the MI355X CIND-discovery pipeline.
+// See include/rdfind_hip.h for the boundary and DESIGN.md for the data layout in HBM.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rdfind_hip.h"
+#include "primitives.hpp"
+#include "kernels.inl"
+
+using namespace rdf;
+
+#define RDF_VERSION "rdfind_amd 0.1 (gfx950)"
+
+struct rdf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    Workspace ws;
+
+    // device scalars + pinned host mirror
+    DevBuf scal;
+    u64* hscal = nullptr;
+
+    // triples
+    DevBuf ts, tp, to;
+    const u32 *s = nullptr, *p = nullptr, *o = nullptr;
+    u64 n = 0;
+    u32 V = 0;
+    int stage = 0;  // 0 none, 1 triples, 2 fc, 3 groups, 4 cinds
+
+    // frequent conditions
+    u32 ms = 1;
+    DevBuf cnt, tkeys, tcnt, bkeys, bkeys_tmp, lkeys, lvals, flags, pos;
+    u64 B = 0, lcap = 0;
+    std::vector<u64> h_bkeys;
+
+    // capture groups
+    DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, gflag, gexcl, goff, gcap, gid, csup, doff, dcur, dgrp;
+    DevBuf hist, heavy_list, hbit, bcomp, bkeyc, pcnt, poff, pcur, plist;
+    u64 J = 0, Jf = 0, G = 0;
+    u32 C = 0, Cu = 0, nheavy = 0;
+    u64 heavy_threshold = 0;
+    int capbits = 0;
+    u64 *rec_sorted = nullptr;
+
+    // cinds
+    DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, out, stage_rows;
+    u64 n_out = 0;
+    u64* out_ptr = nullptr;
+    std::vector<u32> h_fcap;
+    std::vector<u32> h_csup;
+
+    hipEvent_t ev[8] = {};
+    float stage_ms[3] = {0, 0, 0};
+};
+
+static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                          \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess)                                                                       \
+            return fail(ctx, _e == hipErrorOutOfMemory ? RDF_ERR_OOM : RDF_ERR_HIP,                 \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                        \
+    } while (0)
+
+#define ENSURE(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.ensure((size_t)(bytes)))
+
+static int bits_for(u64 maxval) {  // bits needed to represent values in [0, maxval]
+    int b = 0;
+    while (b < 64 && (maxval >> b)) ++b;
+    return b < 1 ? 1 : b;
+}
+
+static u64 next_pow2(u64 x) {
+    u64 p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+static rdf_status read_scalars(rdf_ctx* c, int count) {
+    HIP_TRY(c, hipMemcpyAsync(c->hscal, c->scal.p, count * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RDF_OK;
+}
+
+static rdf_status read_u64(rdf_ctx* c, const void* dptr, u64* out) {
+    HIP_TRY(c, hipMemcpyAsync(c->hscal + 15, dptr, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *out = c->hscal[15];
+    return RDF_OK;
+}
+
+static rdf_status read_u32(rdf_ctx* c, const void* dptr, u32* out) {
+    HIP_TRY(c, hipMemcpyAsync(c->hscal + 15, dptr, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *out = (u32)(c->hscal[15] & 0xffffffffu);
+    return RDF_OK;
+}
+
+static u64* dscal(rdf_ctx* c, int i) { return c->scal.as<u64>() + i; }
+
+static const unsigned kGrid = 2048;  // grid-stride kernels: 8 blocks of 256 threads per CU
+
+extern "C" {
+
+const char* rdf_version(void) { return RDF_VERSION; }
+
+rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
+    if (!out) return RDF_ERR_ARG;
+    *out = nullptr;
+    rdf_ctx* c = new rdf_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
+    for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e != hipSuccess) {
+        rdf_ctx_destroy(c);
+        return RDF_ERR_HIP;
+    }
+    *out = c;
+    return RDF_OK;
+}
+
+void rdf_ctx_destroy(rdf_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->scal, &c->ts, &c->tp, &c->to, &c->cnt, &c->tkeys, &c->tcnt, &c->bkeys, &c->bkeys_tmp,
+                      &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
+                      &c->fcap, &c->info, &c->fk, &c->gflag, &c->gexcl, &c->goff, &c->gcap, &c->gid, &c->csup,
+                      &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
+                      &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
+                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->out,
+                      &c->stage_rows};
+    for (DevBuf* b : bufs) b->release();
+    c->ws.release();
+    if (c->hscal) (void)hipHostFree(c->hscal);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rdf_last_error(const rdf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+rdf_status rdf_sync(rdf_ctx* c) {
+    if (!c) return RDF_ERR_ARG;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RDF_OK;
+}
+
+static rdf_status check_terms(rdf_ctx* c, u64 n, u32 num_terms) {
+    if (num_terms >= (1u << 30)) return fail(c, RDF_ERR_LIMIT, "num_terms must be < 2^30");
+    if (n >= (1ull << 32) / 9) return fail(c, RDF_ERR_LIMIT, "n must be < 2^32/9 triples per GPU (shard larger inputs)");
+    return RDF_OK;
+}
+
+rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, const uint32_t* o, uint64_t n,
+                           uint32_t num_terms) {
+    if (!c || (n && (!s || !p || !o))) return fail(c, RDF_ERR_ARG, "null triple arrays");
+    rdf_status st = check_terms(c, n, num_terms);
+    if (st) return st;
+    HIP_TRY(c, hipSetDevice(c->device));
+    ENSURE(c, ts, n * 4);
+    ENSURE(c, tp, n * 4);
+    ENSURE(c, to, n * 4);
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(c->ts.p, s, n * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->tp.p, p, n * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->to.p, o, n * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->s = c->ts.as<u32>();
+    c->p = c->tp.as<u32>();
+    c->o = c->to.as<u32>();
+    c->n = n;
+    c->V = num_terms;
+    c->stage = 1;
+    return RDF_OK;
+}
+
+rdf_status rdf_set_triples_device(rdf_ctx* c, const uint32_t* s, const uint32_t* p, const uint32_t* o, uint64_t n,
+                                  uint32_t num_terms) {
+    if (!c || (n && (!s || !p || !o))) return fail(c, RDF_ERR_ARG, "null triple arrays");
+    rdf_status st = check_terms(c, n, num_terms);
+    if (st) return st;
+    c->s = s;
+    c->p = p;
+    c->o = o;
+    c->n = n;
+    c->V = num_terms;
+    c->stage = 1;
+    return RDF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage 1: frequent conditions (FrequentConditionPlanner.constructFrequentConditionPlan)
+
+rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const u32 V = c->V ? c->V : 1;
+    c->ms = min_support ? min_support : 1;  // a support of 0 admits exactly the captures that exist
+    HIP_TRY(c, hipEventRecord(c->ev[0], st));
+    HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
+    ENSURE(c, cnt, 3ull * V * 4);
+    HIP_TRY(c, hipMemsetAsync(c->cnt.p, 0, 3ull * V * 4, st));
+    if (n) {
+        hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
+                           st, c->s, c->p, c->o, n, V, c->cnt.as<u32>());
+        hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p,
+                           c->o, n, V, c->ms, c->cnt.as<u32>(), dscal(c, 3));
+    }
+    hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->cnt.as<u32>(), V, c->ms, dscal(c, 0));
+    rdf_status rs = read_scalars(c, 4);
+    if (rs) return rs;
+    u64 nfreq[3] = {c->hscal[0], c->hscal[1], c->hscal[2]};
+    const u64 E = c->hscal[3];
+    const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
+    ENSURE(c, tkeys, tcap * 8);
+    ENSURE(c, tcnt, tcap * 4);
+    HIP_TRY(c, hipMemsetAsync(c->tkeys.p, 0xff, tcap * 8, st));
+    HIP_TRY(c, hipMemsetAsync(c->tcnt.p, 0, tcap * 4, st));
+    if (E)
+        hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
+                           st, c->s, c->p, c->o, n, V, c->ms, c->cnt.as<u32>(), c->tkeys.as<u64>(), c->tcnt.as<u32>(),
+                           tcap - 1);
+    hipLaunchKernelGGL(k_count_nonempty, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->tkeys.as<u64>(), tcap, dscal(c, 4));
+    ENSURE(c, flags, tcap * 4);
+    ENSURE(c, pos, tcap * 8);
+    hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
+    rs = read_scalars(c, 6);
+    if (rs) return rs;
+    const u64 nkeys = c->hscal[4];
+    const u64 B = c->hscal[5];
+    c->B = B;
+    ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
+    ENSURE(c, bkeys_tmp, std::max<u64>(B, 1) * 8);
+    hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->tkeys.as<u64>(), c->flags.as<u32>(), c->pos.as<u64>(), tcap, c->bkeys.as<u64>());
+    {
+        u64* k = c->bkeys.as<u64>();
+        u64* t = c->bkeys_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, 64, st));
+        if (k != c->bkeys.as<u64>()) std::swap(c->bkeys, c->bkeys_tmp);
+    }
+    c->lcap = next_pow2(2 * B + 16);
+    ENSURE(c, lkeys, c->lcap * 8);
+    ENSURE(c, lvals, c->lcap * 4);
+    HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, c->lcap * 8, st));
+    if (B)
+        hipLaunchKernelGGL(k_bin_lookup_build, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->bkeys.as<u64>(), B, c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1);
+    c->h_bkeys.resize(B);
+    if (B) HIP_TRY(c, hipMemcpyAsync(c->h_bkeys.data(), c->bkeys.p, B * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipEventRecord(c->ev[1], st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->min_support = c->ms;
+        for (int i = 0; i < 3; ++i) stats->n_frequent_unary[i] = nfreq[i];
+        stats->n_binary_keys = nkeys;
+        stats->n_frequent_binary = B;
+    }
+    c->stage = 2;
+    return RDF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage 2: capture groups (CreateJoinPartners -> UnionJoinCandidates -> UnionCombinedJoinCandidates)
+
+static int heavy_threshold_from_hist(const u32* hist, u64 min_size) {
+    // smallest bucket such that all groups in buckets >= it number at most HMAX
+    u64 cum = 0;
+    int best = -1;
+    for (int b = 255; b >= 0; --b) {
+        cum += hist[b];
+        if (cum > (u64)HMAX) break;
+        if (hist[b]) best = b;
+    }
+    (void)min_size;
+    return best;
+}
+
+static u64 bucket_min_size(int b) {
+    for (u64 s = 1; s < 64; ++s)
+        if (size_bucket(s) == b) return s;
+    int msb = b / 4, frac = b % 4;
+    return (u64)(4 + frac) << (msb - 2);
+}
+
+rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_group_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 2) return fail(c, RDF_ERR_STATE, "rdf_frequent_conditions must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const char* pr = projection ? projection : "spo";
+    int proj = 0;
+    for (const char* q = pr; *q; ++q) {
+        if (*q == 's') proj |= 1;
+        else if (*q == 'p') proj |= 2;
+        else if (*q == 'o') proj |= 4;
+        else return fail(c, RDF_ERR_ARG, std::string("invalid projection attribute in '") + pr + "'");
+    }
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const u32 V = c->V ? c->V : 1;
+    const u64 ncap = 6ull * V + c->B;
+    const int capbits = bits_for(ncap - 1);
+    const int joinbits = bits_for(V - 1);
+    if (capbits + joinbits > 64) return fail(c, RDF_ERR_LIMIT, "join+capture bits exceed 64");
+    if (ncap >= (1ull << 32)) return fail(c, RDF_ERR_LIMIT, "capture id space exceeds 2^32");
+    c->capbits = capbits;
+    HIP_TRY(c, hipEventRecord(c->ev[2], st));
+    HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
+
+    // K3 join partners
+    const u64 cap_rec = std::max<u64>(9 * n, 1);
+    ENSURE(c, rec, cap_rec * 8);
+    ENSURE(c, rec_tmp, cap_rec * 8);
+    if (n)
+        hipLaunchKernelGGL(k_emit_records, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n,
+                           V, c->ms, c->cnt.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits,
+                           c->rec.as<u64>(), dscal(c, 0));
+    rdf_status rs = read_scalars(c, 1);
+    if (rs) return rs;
+    const u64 J = c->hscal[0];
+    c->J = J;
+
+    // K4 sort by (join, capture)
+    u64* keys = c->rec.as<u64>();
+    u64* tmp = c->rec_tmp.as<u64>();
+    HIP_TRY(c, radix_sort_u64(c->ws, keys, tmp, J, capbits + joinbits, st));
+    c->rec_sorted = keys;
+
+    // K5 supports (distinct join values per capture)
+    ENSURE(c, support, ncap * 4);
+    HIP_TRY(c, hipMemsetAsync(c->support.p, 0, ncap * 4, st));
+    const u64 capmask = (capbits >= 64) ? ~0ull : ((1ull << capbits) - 1);
+    if (J)
+        hipLaunchKernelGGL(k_unique_support, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capmask,
+                           c->support.as<u32>());
+    ENSURE(c, flags, std::max(J, ncap) * 4);
+    ENSURE(c, fidx, (ncap + 1) * 4);
+    hipLaunchKernelGGL(k_support_flags, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fidx.as<u32>(), ncap, c->fidx.as<u32>() + ncap, st));
+    u32 C = 0, Cu = 0;
+    rs = read_u32(c, c->fidx.as<u32>() + ncap, &C);
+    if (rs) return rs;
+    rs = read_u32(c, c->fidx.as<u32>() + 6ull * V, &Cu);
+    if (rs) return rs;
+    c->C = C;
+    c->Cu = Cu;
+    ENSURE(c, fcap, std::max<u64>(C, 1) * 4);
+    ENSURE(c, info, std::max<u64>(C, 1) * sizeof(CapInfo));
+    hipLaunchKernelGGL(k_compact_captures, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->support.as<u32>(), c->fidx.as<u32>(), ncap, c->ms, c->fcap.as<u32>(), c->info.as<CapInfo>());
+
+    // distinct records of frequent captures, capture ids made compact
+    ENSURE(c, pos, std::max<u64>(J, 1) * 8);
+    if (J) {
+        hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capmask,
+                           c->support.as<u32>(), c->ms, c->flags.as<u32>());
+    }
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), J, dscal(c, 1), st));
+    rs = read_scalars(c, 2);
+    if (rs) return rs;
+    const u64 Jf = c->hscal[1];
+    c->Jf = Jf;
+    ENSURE(c, fk, std::max<u64>(Jf, 1) * 8);
+    if (J)
+        hipLaunchKernelGGL(k_keep_scatter, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capbits,
+                           capmask, c->flags.as<u32>(), c->pos.as<u64>(), c->fidx.as<u32>(), c->fk.as<u64>());
+
+    // groups
+    ENSURE(c, gflag, std::max<u64>(Jf, 1) * 4);
+    ENSURE(c, gexcl, (Jf + 1) * 4);
+    if (Jf)
+        hipLaunchKernelGGL(k_group_flags, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fk.as<u64>(), Jf,
+                           c->gflag.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), Jf, c->gexcl.as<u32>() + Jf, st));
+    u32 G32 = 0;
+    rs = read_u32(c, c->gexcl.as<u32>() + Jf, &G32);
+    if (rs) return rs;
+    const u64 G = G32;
+    c->G = G;
+    ENSURE(c, goff, (G + 1) * 8);
+    ENSURE(c, gcap, std::max<u64>(Jf, 1) * 4);
+    ENSURE(c, gid, std::max<u64>(Jf, 1) * 4);
+    if (Jf)
+        hipLaunchKernelGGL(k_group_build, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fk.as<u64>(), Jf,
+                           c->gflag.as<u32>(), c->gexcl.as<u32>(), c->goff.as<u64>(), c->gcap.as<u32>(), c->gid.as<u32>());
+    c->hscal[14] = Jf;
+    HIP_TRY(c, hipMemcpyAsync(c->goff.as<u64>() + G, c->hscal + 14, 8, hipMemcpyHostToDevice, st));
+
+    // dependent -> groups
+    ENSURE(c, csup, std::max<u64>(C, 1) * 4);
+    ENSURE(c, doff, (C + 1ull) * 8);
+    ENSURE(c, dcur, (C + 1ull) * 8);
+    ENSURE(c, dgrp, std::max<u64>(Jf, 1) * 4);
+    if (C)
+        hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->info.as<CapInfo>(), C, c->csup.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->csup.as<u32>(), c->doff.as<u64>(), C, c->doff.as<u64>() + C, st));
+    HIP_TRY(c, hipMemcpyAsync(c->dcur.p, c->doff.p, (C + 1ull) * 8, hipMemcpyDeviceToDevice, st));
+    if (Jf)
+        hipLaunchKernelGGL(k_dep_scatter, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
+                           c->gid.as<u32>(), Jf, c->dcur.as<u64>(), c->dgrp.as<u32>());
+
+    // heavy groups -> bitmask columns
+    ENSURE(c, hist, 256 * 4 + 64);
+    HIP_TRY(c, hipMemsetAsync(c->hist.p, 0, 256 * 4 + 64, st));
+    if (G)
+        hipLaunchKernelGGL(k_group_size_hist, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(),
+                           G, c->hist.as<u32>());
+    std::vector<u32> h_hist(256);
+    HIP_TRY(c, hipMemcpyAsync(h_hist.data(), c->hist.p, 256 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    const u64 kHeavyMin = 64;  // smaller groups are cheaper to verify by binary search than as bit columns
+    int tb = heavy_threshold_from_hist(h_hist.data(), kHeavyMin);
+    u64 thr = tb >= 0 ? std::max<u64>(bucket_min_size(tb), kHeavyMin) : 0;
+    c->heavy_threshold = thr;
+    ENSURE(c, heavy_list, HMAX * 4);
+    ENSURE(c, hbit, std::max<u64>(G, 1));
+    u32* d_nheavy = c->hist.as<u32>() + 256;
+    if (G)
+        hipLaunchKernelGGL(k_heavy_select, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), G,
+                           thr, d_nheavy, c->heavy_list.as<u32>(), c->hbit.as<uint8_t>());
+    u32 nh = 0;
+    rs = read_u32(c, d_nheavy, &nh);
+    if (rs) return rs;
+    nh = std::min<u32>(nh, HMAX);
+    c->nheavy = nh;
+    if (nh)
+        hipLaunchKernelGGL(k_heavy_mask, dim3(64, nh), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), c->gcap.as<u32>(),
+                           c->heavy_list.as<u32>(), c->info.as<CapInfo>());
+
+    // binary components, parents (unary -> binary captures having it as a component)
+    const u32 Cb = C - Cu;
+    ENSURE(c, bcomp, std::max<u64>(2ull * Cb, 1) * 4);
+    ENSURE(c, bkeyc, std::max<u64>(Cb, 1) * 8);
+    ENSURE(c, pcnt, std::max<u64>(Cu, 1) * 4);
+    ENSURE(c, poff, (Cu + 1ull) * 8);
+    ENSURE(c, pcur, (Cu + 1ull) * 8);
+    ENSURE(c, plist, std::max<u64>(2ull * Cb, 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->pcnt.p, 0, std::max<u64>(Cu, 1) * 4, st));
+    if (Cb)
+        hipLaunchKernelGGL(k_binary_info, dim3(grid_for(Cb, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fcap.as<u32>(),
+                           c->fidx.as<u32>(), c->bkeys.as<u64>(), C, Cu, V, c->bcomp.as<u32>(), c->bkeyc.as<u64>(),
+                           c->pcnt.as<u32>(), c->info.as<CapInfo>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->pcnt.as<u32>(), c->poff.as<u64>(), Cu, c->poff.as<u64>() + Cu, st));
+    HIP_TRY(c, hipMemcpyAsync(c->pcur.p, c->poff.p, (Cu + 1ull) * 8, hipMemcpyDeviceToDevice, st));
+    if (Cb)
+        hipLaunchKernelGGL(k_parents_scatter, dim3(grid_for(Cb, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->bcomp.as<u32>(),
+                           C, Cu, c->pcur.as<u64>(), c->plist.as<u32>());
+    if (Cu)
+        hipLaunchKernelGGL(k_parent_meta, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pcnt.as<u32>(), Cu,
+                           c->info.as<CapInfo>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(c->ev[3], st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[1], c->ev[2], c->ev[3]));
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->n_records = J;
+        stats->n_frequent_records = Jf;
+        stats->n_groups = G;
+        stats->n_captures = C;
+        stats->n_unary_captures = Cu;
+        stats->n_heavy_groups = nh;
+        stats->heavy_threshold = thr;
+    }
+    c->stage = 3;
+    return RDF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage 3: CIND extraction + minimality (TraversalStrategy.enhanceFlinkPlan)
+
+rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    CindView v;
+    v.C = C;
+    v.Cu = c->Cu;
+    v.info = c->info.as<CapInfo>();
+    v.gcap = c->gcap.as<u32>();
+    v.goff = c->goff.as<u64>();
+    v.hbit = c->hbit.as<uint8_t>();
+    v.doff = c->doff.as<u64>();
+    v.dgrp = c->dgrp.as<u32>();
+    v.bcomp = c->bcomp.as<u32>();
+    v.bkeyc = c->bkeyc.as<u64>();
+    v.poff = c->poff.as<u64>();
+    v.plist = c->plist.as<u32>();
+    v.literal = (flags & RDF_STRATEGY_ALL_AT_ONCE) ? 1 : 0;
+    v.mode = (flags & RDF_CLEAN_IMPLIED) ? RULES_CLEAN : (v.literal ? RULES_NONE : RULES_S2L_RAW);
+    HIP_TRY(c, hipEventRecord(c->ev[4], st));
+    HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
+
+    // pivots and work chunks
+    ENSURE(c, pivot, std::max<u64>(C, 1) * 4);
+    ENSURE(c, nchl, std::max<u64>(C, 1) * 4);
+    ENSURE(c, nchh, std::max<u64>(C, 1) * 4);
+    ENSURE(c, choffl, (C + 1ull) * 8);
+    ENSURE(c, choffh, (C + 1ull) * 8);
+    hipEvent_t e0 = c->ev[5], e1 = c->ev[6], e2 = c->ev[7];
+    HIP_TRY(c, hipEventRecord(e0, st));
+    if (C)
+        hipLaunchKernelGGL(k_pivot, dim3((unsigned)((C + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK), 0,
+                           st, v, c->pivot.as<u32>(), c->nchl.as<u32>(), c->nchh.as<u32>(), c->info.as<CapInfo>());
+    HIP_TRY(c, hipEventRecord(e1, st));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchl.as<u32>(), c->choffl.as<u64>(), C, c->choffl.as<u64>() + C, st));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
+    u64 WL = 0, WH = 0;
+    rdf_status rs = read_u64(c, c->choffl.as<u64>() + C, &WL);
+    if (rs) return rs;
+    rs = read_u64(c, c->choffh.as<u64>() + C, &WH);
+    if (rs) return rs;
+    float ms_pivot = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms_pivot, e0, e1));
+
+    // light dependents -> explicit raw pairs
+    const u64 cap_pairs = std::max<u64>(WL * RDF_WAVE, 1);
+    ENSURE(c, epairs, cap_pairs * 8);
+    ENSURE(c, epairs_tmp, cap_pairs * 8);
+    HIP_TRY(c, hipEventRecord(e0, st));
+    if (WL)
+        hipLaunchKernelGGL(k_light, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
+                           0, st, v, c->pivot.as<u32>(), c->choffl.as<u64>(), WL, c->epairs.as<u64>(), dscal(c, 0));
+    HIP_TRY(c, hipEventRecord(e1, st));
+    rs = read_scalars(c, 1);
+    if (rs) return rs;
+    const u64 E = c->hscal[0];
+    float ms_light = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms_light, e0, e1));
+    {
+        u64* k = c->epairs.as<u64>();
+        u64* t = c->epairs_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, E, 32 + bits_for(C ? C - 1 : 0), st));
+        if (k != c->epairs.as<u64>()) std::swap(c->epairs, c->epairs_tmp);
+    }
+    ENSURE(c, eoff, (C + 1ull) * 8);
+    hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->epairs.as<u64>(), E, C, c->eoff.as<u64>());
+    v.eoff = c->eoff.as<u64>();
+    v.epairs = c->epairs.as<u64>();
+
+    // heavy-only dependents: count pass
+    ENSURE(c, hcounts, std::max<u64>(WH, 1) * 4);
+    ENSURE(c, hoff, (WH + 1) * 8);
+    HIP_TRY(c, hipEventRecord(e0, st));
+    if (WH)
+        hipLaunchKernelGGL((k_heavy<false>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, c->hcounts.as<u32>(),
+                           (const u64*)nullptr, (u64)0, (u64*)nullptr);
+    HIP_TRY(c, hipEventRecord(e1, st));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->hcounts.as<u32>(), c->hoff.as<u64>(), WH, c->hoff.as<u64>() + WH, st));
+    u64 H = 0;
+    rs = read_u64(c, c->hoff.as<u64>() + WH, &H);
+    if (rs) return rs;
+    float ms_heavy = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms_heavy, e0, e1));
+
+    // minimality on the explicit pairs, then heavy write pass
+    ENSURE(c, out, std::max<u64>(E + H, 1) * 8);
+    HIP_TRY(c, hipEventRecord(e0, st));
+    if (E)
+        hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                           c->epairs.as<u64>(), E, c->out.as<u64>(), dscal(c, 1));
+    HIP_TRY(c, hipEventRecord(e1, st));
+    rs = read_scalars(c, 2);
+    if (rs) return rs;
+    const u64 K = c->hscal[1];
+    float ms_rules = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms_rules, e0, e1));
+    HIP_TRY(c, hipEventRecord(e0, st));
+    if (WH)
+        hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, (u32*)nullptr,
+                           c->hoff.as<u64>(), K, c->out.as<u64>());
+    HIP_TRY(c, hipEventRecord(e2, st));
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    float ms_hw = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms_hw, e0, e2));
+    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], e2));
+    c->n_out = K + H;
+    c->out_ptr = c->out.as<u64>();
+    // host copies for result decoding
+    c->h_fcap.resize(C);
+    c->h_csup.resize(C);
+    if (C) {
+        HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fcap.p, (u64)C * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
+    }
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->n_cinds = c->n_out;
+        stats->n_explicit_raw = E;
+        stats->n_light_chunks = WL;
+        stats->n_heavy_chunks = WH;
+        stats->ms_pivot = ms_pivot;
+        stats->ms_light = ms_light;
+        stats->ms_rules = ms_rules;
+        stats->ms_heavy = ms_heavy + ms_hw;
+    }
+    c->stage = 4;
+    return RDF_OK;
+}
+
+rdf_status rdf_run(rdf_ctx* c, uint32_t min_support, const char* projection, uint32_t flags, rdf_fc_stats* fc,
+                   rdf_group_stats* gs, rdf_cind_stats* cs) {
+    rdf_status r = rdf_frequent_conditions(c, min_support, fc);
+    if (r) return r;
+    r = rdf_build_capture_groups(c, projection, gs);
+    if (r) return r;
+    return rdf_discover_cinds(c, flags, cs);
+}
+
+rdf_status rdf_cind_count(rdf_ctx* c, uint64_t* n) {
+    if (!c || !n) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    *n = c->n_out;
+    return RDF_OK;
+}
+
+rdf_status rdf_copy_cinds(rdf_ctx* c, rdf_cind* out, uint64_t cap, uint64_t* n_copied) {
+    if (!c || (cap && !out)) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 total = std::min<u64>(cap, c->n_out);
+    const u64 chunk = 1ull << 24;
+    std::vector<u64> buf(std::min<u64>(chunk, std::max<u64>(total, 1)));
+    for (u64 b = 0; b < total; b += chunk) {
+        const u64 m = std::min(chunk, total - b);
+        HIP_TRY(c, hipMemcpy(buf.data(), c->out_ptr + b, m * 8, hipMemcpyDeviceToHost));
+        for (u64 i = 0; i < m; ++i) {
+            const u32 d = (u32)(buf[i] >> 32), r = (u32)buf[i];
+            out[b + i].dep = c->h_fcap[d];
+            out[b + i].ref = c->h_fcap[r];
+            out[b + i].support = c->h_csup[d];
+        }
+    }
+    if (n_copied) *n_copied = total;
+    return RDF_OK;
+}
+
+rdf_status rdf_decode_capture(rdf_ctx* c, uint32_t capture, uint32_t* code, uint32_t* value1, uint32_t* value2) {
+    if (!c || !code || !value1 || !value2) return RDF_ERR_ARG;
+    static const uint32_t UN[6] = {10, 12, 17, 20, 33, 34}, BI[3] = {14, 21, 35};
+    const u64 V = c->V ? c->V : 1;
+    if (capture < 6 * V) {
+        *code = UN[capture / V];
+        *value1 = (u32)(capture % V);
+        *value2 = 0xffffffffu;
+        return RDF_OK;
+    }
+    const u64 b = capture - 6 * V;
+    if (b >= c->h_bkeys.size()) return fail(c, RDF_ERR_ARG, "capture id out of range");
+    const u64 k = c->h_bkeys[b];
+    *code = BI[bin_key_type(k)];
+    *value1 = bin_key_v1(k);
+    *value2 = bin_key_v2(k);
+    return RDF_OK;
+}
+
+rdf_status rdf_binary_key_count(rdf_ctx* c, uint64_t* n) {
+    if (!c || !n) return RDF_ERR_ARG;
+    *n = c->h_bkeys.size();
+    return RDF_OK;
+}
+
+rdf_status rdf_copy_binary_keys(rdf_ctx* c, uint64_t* out, uint64_t cap) {
+    if (!c || (cap && !out)) return RDF_ERR_ARG;
+    const u64 m = std::min<u64>(cap, c->h_bkeys.size());
+    if (m) memcpy(out, c->h_bkeys.data(), m * 8);
+    return RDF_OK;
+}
+
+rdf_status rdf_stage_times(rdf_ctx* c, float* ms3) {
+    if (!c || !ms3) return RDF_ERR_ARG;
+    for (int i = 0; i < 3; ++i) ms3[i] = c->stage_ms[i];
+    return RDF_OK;
+}
+
+}  // extern "C"
