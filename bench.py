@@ -1,0 +1,162 @@
+"""Benchmark: CIND-discovery triples/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--scale 1.0]
+
+A *step* is one pass of the hot path over one batch: rdf_run = frequent conditions -> capture groups
+-> CIND extraction + --clean-implied minimality (strategy 1, the reference default), with the
+dictionary-encoded triples already resident in HBM and the CIND id-records left in HBM (the
+PCIe-inclusive rate is reported separately in DESIGN.md).  Workload: BASELINE configs[1] =
+LUBM-100-shaped synthetic triples (~13.4M), support 10, one MI355X.
+
+For N > 1 (launched by torch.distributed.run) every rank runs its own LUBM-100-shaped replica on its
+own GPU (weak scaling, no data-path collective); `value` is the triples of all ranks divided by the
+max-over-ranks time.  `roofline` is computed for the dominant kernel family from HIP events recorded on
+the library's stream; `cpu_baseline` times the C restatement (oracle/) on a bounded sample on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
+
+
+def algorithmic_bytes(name, d, gs, cs, kt_counts):
+    """Minimal HBM bytes a kernel family must move per launch (DESIGN.md 'Kernels and rooflines')."""
+    n = d.n
+    J = gs["n_records"]
+    if name == "unary":
+        return 12 * n                                   # read s, p, o once
+    if name == "emit":
+        return 12 * n + 8 * J                           # read triples, write (join, capture) records
+    if name == "sort":
+        return 16 * kt_counts["sort_passes_records"]    # read + write each record once per 8-bit pass
+    if name in ("hwrite", "hcount"):
+        cand = cs["n_heavy_candidates"]
+        out = 8 * cs["n_cinds"] if name == "hwrite" else 4 * cs["n_heavy_chunks"]
+        return 20 * cand + out                          # candidate ids + 16-B capture info, output records
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    from rdfind_amd import _lib, synth
+
+    d = synth.config(args.config, args.scale, seed=None if rank == 0 else 1000 + rank)
+    ms = d.min_support
+    ctx = _lib.Context(local_rank)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ctx.run(ms)
+    ctx.sync()
+    barrier()
+    kt_sum = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cs = ctx.run(ms)
+        for k, v in ctx.kernel_times().items():
+            kt_sum[k] = kt_sum.get(k, 0.0) + v
+    ctx.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([float(d.n)], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(tot)
+        total_triples = float(tot.item())
+    else:
+        total_triples = float(d.n)
+    steps = max(args.steps, 1)
+    ms_per_step = elapsed * 1000.0 / steps
+    value = total_triples * steps / elapsed
+
+    gs, fc = ctx.groups, ctx.fc
+    kt = {k: v / steps for k, v in kt_sum.items()}
+    counts = {"sort_passes_records": 0}
+    # passes of the record sort (bits = join bits + capture bits, 8 per pass)
+    V = d.num_terms
+    capbits = int(6 * V + fc["n_frequent_binary"] - 1).bit_length()
+    joinbits = int(V - 1).bit_length()
+    counts["sort_passes_records"] = ((capbits + joinbits + 7) // 8) * gs["n_records"]
+    dominant = max(kt, key=lambda k: kt[k])
+    roof = None
+    for name in [dominant] + sorted(kt, key=lambda k: -kt[k]):
+        b = algorithmic_bytes(name, d, gs, cs, counts)
+        if b is not None and kt[name] > 0:
+            achieved = b / (kt[name] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "ms": round(kt[name], 4), "bytes_per_launch": int(b), "dominant_kernel": dominant,
+                    "dominant_ms": round(kt[dominant], 4)}
+            break
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import c_oracle
+
+        sd = synth.config(args.config, args.cpu_sample_scale)
+        t = time.perf_counter()
+        _, _, st = c_oracle.run(sd.s, sd.p, sd.o, sd.num_terms, sd.min_support, 1, True)
+        ct = time.perf_counter() - t
+        cpu = {"value": round(sd.n / ct, 1), "unit": "triples/s", "cores": 1, "kind": "port",
+               "sample": f"{args.config} scale {args.cpu_sample_scale} ({sd.n} triples, {st['n_cinds']} CINDs) "
+                         f"through oracle/c/rdfind_oracle.c single-threaded, {ct:.1f}s"}
+
+    if rank == 0:
+        line = {
+            "metric": "CIND-discovery triples/sec", "value": round(value, 1), "unit": "triples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"{args.config} ({'LUBM-100-shaped' if args.config == 'c2' else args.config}, "
+                                   f"scale {args.scale}, support {ms}, strategy 1 --use-fis --clean-implied)",
+                       "triples_per_gpu": d.n, "global_triples": int(total_triples), "cinds": cs["n_cinds"],
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -75,7 +75,26 @@ typedef struct {
     uint64_t n_light_chunks;
     uint64_t n_heavy_chunks;
     float ms_pivot, ms_light, ms_rules, ms_heavy;  /* device time per K6/K7 kernel family */
+    uint64_t n_heavy_candidates;    /* pivot members scanned for dependents whose groups are all heavy */
 } rdf_cind_stats;
+
+/* Kernel-family device timers (HIP events on the context stream), see rdf_kernel_times. */
+enum {
+    RDF_T_UNARY = 0,    /* K1 unary condition counts (+ frequent-value count) */
+    RDF_T_BINARY,       /* K2 binary condition counts + frequent-key extraction */
+    RDF_T_EMIT,         /* K3 join-partner emission */
+    RDF_T_SORT,         /* K4 radix sort of (join, capture) records */
+    RDF_T_SUPPORT,      /* K5 distinct records, supports, frequent-capture compaction */
+    RDF_T_GROUPS,       /* capture-group CSR + dependent -> group CSR */
+    RDF_T_HEAVYMASK,    /* heavy-group selection, bitmask columns, binary components/parents */
+    RDF_T_PIVOT,        /* K6 pivot selection */
+    RDF_T_LIGHT,        /* K6 light-dependent intersection */
+    RDF_T_ESORT,        /* sort of explicit pairs + CSR offsets */
+    RDF_T_HCOUNT,       /* K6 heavy-only count pass (minimality fused) */
+    RDF_T_RULES,        /* K7 minimality on explicit pairs */
+    RDF_T_HWRITE,       /* K6 heavy-only write pass (minimality fused) */
+    RDF_NUM_TIMERS
+};
 
 /* One result row: capture ids (see rdf_decode_capture) and the support of the dependent. */
 typedef struct {
@@ -107,6 +126,11 @@ rdf_status rdf_cind_count(rdf_ctx* ctx, uint64_t* n);
 /* Copies min(cap, count) rows to host memory; *n_copied receives the number copied. */
 rdf_status rdf_copy_cinds(rdf_ctx* ctx, rdf_cind* out, uint64_t cap, uint64_t* n_copied);
 
+/* Copies rows [offset, offset+count) of the result (clipped); *n_copied receives the number copied. */
+rdf_status rdf_copy_cinds_range(rdf_ctx* ctx, uint64_t offset, rdf_cind* out, uint64_t count, uint64_t* n_copied);
+/* Order-independent checksum of the result set (sum of a 64-bit mix of (dep, ref) capture ids). */
+rdf_status rdf_cind_checksum(rdf_ctx* ctx, uint64_t* checksum);
+
 /* Capture ids: unary type t (codes 10,12,17,20,33,34) with value v -> t*V + v; binary capture b
  * (codes 14,21,35) -> 6V + b.  Decodes to the capture code and its condition values
  * (value2 = UINT32_MAX for unary captures). */
@@ -117,6 +141,8 @@ rdf_status rdf_copy_binary_keys(rdf_ctx* ctx, uint64_t* out, uint64_t cap);
 
 /* Device time (ms) of the last call of each stage: [0] fc, [1] groups, [2] cinds. */
 rdf_status rdf_stage_times(rdf_ctx* ctx, float* ms3);
+/* Device time (ms) of each kernel family (RDF_T_*) in the last calls; count <= RDF_NUM_TIMERS. */
+rdf_status rdf_kernel_times(rdf_ctx* ctx, float* ms, int count);
 /* Synchronise the context stream. */
 rdf_status rdf_sync(rdf_ctx* ctx);
 

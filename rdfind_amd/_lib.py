@@ -23,8 +23,13 @@ EXPORTED_SYMBOLS = (
     "rdf_ctx_create", "rdf_ctx_destroy", "rdf_last_error", "rdf_version", "rdf_set_triples",
     "rdf_set_triples_device", "rdf_frequent_conditions", "rdf_build_capture_groups", "rdf_discover_cinds",
     "rdf_run", "rdf_cind_count", "rdf_copy_cinds", "rdf_decode_capture", "rdf_binary_key_count",
-    "rdf_copy_binary_keys", "rdf_stage_times", "rdf_sync",
+    "rdf_copy_binary_keys", "rdf_stage_times", "rdf_kernel_times", "rdf_sync",
+    "rdf_copy_cinds_range", "rdf_cind_checksum",
 )
+
+# RDF_T_* kernel-family timers (include/rdfind_hip.h)
+TIMER_NAMES = ("unary", "binary", "emit", "sort", "support", "groups", "heavymask", "pivot", "light", "esort",
+               "hcount", "rules", "hwrite")
 
 
 class FcStats(ctypes.Structure):
@@ -44,7 +49,7 @@ class CindStats(ctypes.Structure):
     _fields_ = [("n_cinds", ctypes.c_uint64), ("n_explicit_raw", ctypes.c_uint64),
                 ("n_light_chunks", ctypes.c_uint64), ("n_heavy_chunks", ctypes.c_uint64),
                 ("ms_pivot", ctypes.c_float), ("ms_light", ctypes.c_float), ("ms_rules", ctypes.c_float),
-                ("ms_heavy", ctypes.c_float)]
+                ("ms_heavy", ctypes.c_float), ("n_heavy_candidates", ctypes.c_uint64)]
 
 
 CIND_DTYPE = np.dtype([("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])
@@ -83,7 +88,10 @@ def load():
         "rdf_binary_key_count": (i32, [P, ctypes.POINTER(u64)]),
         "rdf_copy_binary_keys": (i32, [P, P, u64]),
         "rdf_stage_times": (i32, [P, ctypes.POINTER(ctypes.c_float)]),
+        "rdf_kernel_times": (i32, [P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
         "rdf_sync": (i32, [P]),
+        "rdf_copy_cinds_range": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
+        "rdf_cind_checksum": (i32, [P, ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -185,6 +193,11 @@ class Context:
         self._check(self.lib.rdf_stage_times(self.ptr, arr), "rdf_stage_times")
         return list(arr)
 
+    def kernel_times(self):
+        arr = (ctypes.c_float * len(TIMER_NAMES))()
+        self._check(self.lib.rdf_kernel_times(self.ptr, arr, len(TIMER_NAMES)), "rdf_kernel_times")
+        return dict(zip(TIMER_NAMES, list(arr)))
+
     # -- results -----------------------------------------------------------------------------
     def cind_count(self) -> int:
         n = ctypes.c_uint64()
@@ -197,6 +210,18 @@ class Context:
         copied = ctypes.c_uint64()
         self._check(self.lib.rdf_copy_cinds(self.ptr, out.ctypes.data, n, ctypes.byref(copied)), "rdf_copy_cinds")
         return out[: copied.value]
+
+    def copy_cinds_range(self, offset: int, count: int) -> np.ndarray:
+        out = np.empty(count, dtype=CIND_DTYPE)
+        copied = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_cinds_range(self.ptr, offset, out.ctypes.data, count, ctypes.byref(copied)),
+                    "rdf_copy_cinds_range")
+        return out[: copied.value]
+
+    def checksum(self) -> int:
+        v = ctypes.c_uint64()
+        self._check(self.lib.rdf_cind_checksum(self.ptr, ctypes.byref(v)), "rdf_cind_checksum")
+        return v.value
 
     def binary_keys(self) -> np.ndarray:
         n = ctypes.c_uint64()

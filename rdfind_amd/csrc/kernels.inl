@@ -421,7 +421,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_parent_meta(const u32* __restrict
 
 // pivot pass: one wave per dependent
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot(CindView v, u32* pivot, u32* nchunk_light, u32* nchunk_heavy,
-                                                     CapInfo* info) {
+                                                     CapInfo* info, u64* heavy_candidates) {
     const int lane = lane_id();
     const u64 d = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (d >= v.C) return;
@@ -448,7 +448,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot(CindView v, u32* pivot, u32
         pivot[d] = g;
         nchunk_light[d] = nlight ? nch : 0;
         nchunk_heavy[d] = nlight ? 0 : nch;
-        if (!nlight) info[d].meta |= META_HEAVY_ONLY;
+        if (!nlight) {
+            info[d].meta |= META_HEAVY_ONLY;
+            atomicAdd(heavy_candidates, sz);
+        }
     }
 }
 
@@ -647,4 +650,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy(CindView v, const u32* __re
     }
 }
 
+}  // namespace rdf
+
+namespace rdf {
+// order-independent checksum of the result set (capture ids, so it is comparable across runs)
+__global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u64* __restrict__ pairs, u64 n, const u32* __restrict__ fcap,
+                                                        u64* sum) {
+    u64 acc = 0;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 pr = pairs[i];
+        acc += mix64(((u64)fcap[pr >> 32] << 32) | fcap[(u32)pr]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, RDF_WAVE);
+    if (lane_id() == 0 && acc) atomicAdd(sum, acc);
+}
 }  // namespace rdf

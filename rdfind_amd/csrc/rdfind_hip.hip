@@ -55,7 +55,28 @@ struct rdf_ctx {
 
     hipEvent_t ev[8] = {};
     float stage_ms[3] = {0, 0, 0};
+    // per kernel-family device timers (events on the context stream)
+    hipEvent_t tev[2 * RDF_NUM_TIMERS] = {};
+    bool tused[RDF_NUM_TIMERS] = {};
+    float tms[RDF_NUM_TIMERS] = {};
+    u64 sort_passes_records = 0, sort_passes_pairs = 0;
+    u64 heavy_candidates = 0;
 };
+
+static void tbegin(rdf_ctx* c, int id) {
+    (void)hipEventRecord(c->tev[2 * id], c->stream);
+    c->tused[id] = true;
+}
+static void tend(rdf_ctx* c, int id) { (void)hipEventRecord(c->tev[2 * id + 1], c->stream); }
+// call after a stream sync: fold recorded timers of [lo, hi) into tms
+static void tcollect(rdf_ctx* c, int lo, int hi) {
+    for (int i = lo; i < hi; ++i) {
+        float ms = 0;
+        if (c->tused[i] && hipEventElapsedTime(&ms, c->tev[2 * i], c->tev[2 * i + 1]) == hipSuccess) c->tms[i] = ms;
+        else c->tms[i] = 0;
+        c->tused[i] = false;
+    }
+}
 
 static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
     if (c) c->err = msg;
@@ -122,6 +143,7 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
     for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    for (int i = 0; i < 2 * RDF_NUM_TIMERS && e == hipSuccess; ++i) e = hipEventCreate(&c->tev[i]);
     if (e != hipSuccess) {
         rdf_ctx_destroy(c);
         return RDF_ERR_HIP;
@@ -145,6 +167,8 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
     for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -217,12 +241,14 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
     ENSURE(c, cnt, 3ull * V * 4);
     HIP_TRY(c, hipMemsetAsync(c->cnt.p, 0, 3ull * V * 4, st));
-    if (n) {
+    tbegin(c, RDF_T_UNARY);
+    if (n)
         hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                            st, c->s, c->p, c->o, n, V, c->cnt.as<u32>());
+    tend(c, RDF_T_UNARY);
+    if (n)
         hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p,
                            c->o, n, V, c->ms, c->cnt.as<u32>(), dscal(c, 3));
-    }
     hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->cnt.as<u32>(), V, c->ms, dscal(c, 0));
     rdf_status rs = read_scalars(c, 4);
@@ -234,6 +260,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     ENSURE(c, tcnt, tcap * 4);
     HIP_TRY(c, hipMemsetAsync(c->tkeys.p, 0xff, tcap * 8, st));
     HIP_TRY(c, hipMemsetAsync(c->tcnt.p, 0, tcap * 4, st));
+    tbegin(c, RDF_T_BINARY);
     if (E)
         hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                            st, c->s, c->p, c->o, n, V, c->ms, c->cnt.as<u32>(), c->tkeys.as<u64>(), c->tcnt.as<u32>(),
@@ -245,6 +272,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
+    tend(c, RDF_T_BINARY);
     rs = read_scalars(c, 6);
     if (rs) return rs;
     const u64 nkeys = c->hscal[4];
@@ -272,6 +300,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     HIP_TRY(c, hipEventRecord(c->ev[1], st));
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
+    tcollect(c, RDF_T_UNARY, RDF_T_BINARY + 1);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->min_support = c->ms;
@@ -334,10 +363,12 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     const u64 cap_rec = std::max<u64>(9 * n, 1);
     ENSURE(c, rec, cap_rec * 8);
     ENSURE(c, rec_tmp, cap_rec * 8);
+    tbegin(c, RDF_T_EMIT);
     if (n)
         hipLaunchKernelGGL(k_emit_records, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n,
                            V, c->ms, c->cnt.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits,
                            c->rec.as<u64>(), dscal(c, 0));
+    tend(c, RDF_T_EMIT);
     rdf_status rs = read_scalars(c, 1);
     if (rs) return rs;
     const u64 J = c->hscal[0];
@@ -346,11 +377,15 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     // K4 sort by (join, capture)
     u64* keys = c->rec.as<u64>();
     u64* tmp = c->rec_tmp.as<u64>();
+    tbegin(c, RDF_T_SORT);
     HIP_TRY(c, radix_sort_u64(c->ws, keys, tmp, J, capbits + joinbits, st));
+    tend(c, RDF_T_SORT);
     c->rec_sorted = keys;
+    c->sort_passes_records = (u64)((capbits + joinbits + 7) / 8) * J;
 
     // K5 supports (distinct join values per capture)
     ENSURE(c, support, ncap * 4);
+    tbegin(c, RDF_T_SUPPORT);
     HIP_TRY(c, hipMemsetAsync(c->support.p, 0, ncap * 4, st));
     const u64 capmask = (capbits >= 64) ? ~0ull : ((1ull << capbits) - 1);
     if (J)
@@ -389,7 +424,9 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
         hipLaunchKernelGGL(k_keep_scatter, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capbits,
                            capmask, c->flags.as<u32>(), c->pos.as<u64>(), c->fidx.as<u32>(), c->fk.as<u64>());
 
+    tend(c, RDF_T_SUPPORT);
     // groups
+    tbegin(c, RDF_T_GROUPS);
     ENSURE(c, gflag, std::max<u64>(Jf, 1) * 4);
     ENSURE(c, gexcl, (Jf + 1) * 4);
     if (Jf)
@@ -424,7 +461,9 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
         hipLaunchKernelGGL(k_dep_scatter, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
                            c->gid.as<u32>(), Jf, c->dcur.as<u64>(), c->dgrp.as<u32>());
 
+    tend(c, RDF_T_GROUPS);
     // heavy groups -> bitmask columns
+    tbegin(c, RDF_T_HEAVYMASK);
     ENSURE(c, hist, 256 * 4 + 64);
     HIP_TRY(c, hipMemsetAsync(c->hist.p, 0, 256 * 4 + 64, st));
     if (G)
@@ -474,9 +513,11 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
         hipLaunchKernelGGL(k_parent_meta, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pcnt.as<u32>(), Cu,
                            c->info.as<CapInfo>());
     HIP_TRY(c, hipGetLastError());
+    tend(c, RDF_T_HEAVYMASK);
     HIP_TRY(c, hipEventRecord(c->ev[3], st));
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[1], c->ev[2], c->ev[3]));
+    tcollect(c, RDF_T_EMIT, RDF_T_HEAVYMASK + 1);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->n_records = J;
@@ -524,12 +565,12 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     ENSURE(c, nchh, std::max<u64>(C, 1) * 4);
     ENSURE(c, choffl, (C + 1ull) * 8);
     ENSURE(c, choffh, (C + 1ull) * 8);
-    hipEvent_t e0 = c->ev[5], e1 = c->ev[6], e2 = c->ev[7];
-    HIP_TRY(c, hipEventRecord(e0, st));
+    tbegin(c, RDF_T_PIVOT);
     if (C)
         hipLaunchKernelGGL(k_pivot, dim3((unsigned)((C + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK), 0,
-                           st, v, c->pivot.as<u32>(), c->nchl.as<u32>(), c->nchh.as<u32>(), c->info.as<CapInfo>());
-    HIP_TRY(c, hipEventRecord(e1, st));
+                           st, v, c->pivot.as<u32>(), c->nchl.as<u32>(), c->nchh.as<u32>(), c->info.as<CapInfo>(),
+                           dscal(c, 2));
+    tend(c, RDF_T_PIVOT);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchl.as<u32>(), c->choffl.as<u64>(), C, c->choffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
     u64 WL = 0, WH = 0;
@@ -537,23 +578,22 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (rs) return rs;
     rs = read_u64(c, c->choffh.as<u64>() + C, &WH);
     if (rs) return rs;
-    float ms_pivot = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms_pivot, e0, e1));
+    rs = read_u64(c, dscal(c, 2), &c->heavy_candidates);
+    if (rs) return rs;
 
     // light dependents -> explicit raw pairs
     const u64 cap_pairs = std::max<u64>(WL * RDF_WAVE, 1);
     ENSURE(c, epairs, cap_pairs * 8);
     ENSURE(c, epairs_tmp, cap_pairs * 8);
-    HIP_TRY(c, hipEventRecord(e0, st));
+    tbegin(c, RDF_T_LIGHT);
     if (WL)
         hipLaunchKernelGGL(k_light, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
                            0, st, v, c->pivot.as<u32>(), c->choffl.as<u64>(), WL, c->epairs.as<u64>(), dscal(c, 0));
-    HIP_TRY(c, hipEventRecord(e1, st));
+    tend(c, RDF_T_LIGHT);
     rs = read_scalars(c, 1);
     if (rs) return rs;
     const u64 E = c->hscal[0];
-    float ms_light = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms_light, e0, e1));
+    tbegin(c, RDF_T_ESORT);
     {
         u64* k = c->epairs.as<u64>();
         u64* t = c->epairs_tmp.as<u64>();
@@ -563,48 +603,46 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     ENSURE(c, eoff, (C + 1ull) * 8);
     hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->epairs.as<u64>(), E, C, c->eoff.as<u64>());
+    tend(c, RDF_T_ESORT);
+    c->sort_passes_pairs = (u64)((32 + bits_for(C ? C - 1 : 0) + 7) / 8) * E;
     v.eoff = c->eoff.as<u64>();
     v.epairs = c->epairs.as<u64>();
 
     // heavy-only dependents: count pass
     ENSURE(c, hcounts, std::max<u64>(WH, 1) * 4);
     ENSURE(c, hoff, (WH + 1) * 8);
-    HIP_TRY(c, hipEventRecord(e0, st));
+    tbegin(c, RDF_T_HCOUNT);
     if (WH)
         hipLaunchKernelGGL((k_heavy<false>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, c->hcounts.as<u32>(),
                            (const u64*)nullptr, (u64)0, (u64*)nullptr);
-    HIP_TRY(c, hipEventRecord(e1, st));
+    tend(c, RDF_T_HCOUNT);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->hcounts.as<u32>(), c->hoff.as<u64>(), WH, c->hoff.as<u64>() + WH, st));
     u64 H = 0;
     rs = read_u64(c, c->hoff.as<u64>() + WH, &H);
     if (rs) return rs;
-    float ms_heavy = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms_heavy, e0, e1));
 
     // minimality on the explicit pairs, then heavy write pass
     ENSURE(c, out, std::max<u64>(E + H, 1) * 8);
-    HIP_TRY(c, hipEventRecord(e0, st));
+    tbegin(c, RDF_T_RULES);
     if (E)
         hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
                            c->epairs.as<u64>(), E, c->out.as<u64>(), dscal(c, 1));
-    HIP_TRY(c, hipEventRecord(e1, st));
+    tend(c, RDF_T_RULES);
     rs = read_scalars(c, 2);
     if (rs) return rs;
     const u64 K = c->hscal[1];
-    float ms_rules = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms_rules, e0, e1));
-    HIP_TRY(c, hipEventRecord(e0, st));
+    tbegin(c, RDF_T_HWRITE);
     if (WH)
         hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, (u32*)nullptr,
                            c->hoff.as<u64>(), K, c->out.as<u64>());
-    HIP_TRY(c, hipEventRecord(e2, st));
+    tend(c, RDF_T_HWRITE);
+    HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(st));
-    float ms_hw = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms_hw, e0, e2));
-    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], e2));
+    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], c->ev[5]));
+    tcollect(c, RDF_T_PIVOT, RDF_T_HWRITE + 1);
     c->n_out = K + H;
     c->out_ptr = c->out.as<u64>();
     // host copies for result decoding
@@ -620,10 +658,11 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
         stats->n_explicit_raw = E;
         stats->n_light_chunks = WL;
         stats->n_heavy_chunks = WH;
-        stats->ms_pivot = ms_pivot;
-        stats->ms_light = ms_light;
-        stats->ms_rules = ms_rules;
-        stats->ms_heavy = ms_heavy + ms_hw;
+        stats->ms_pivot = c->tms[RDF_T_PIVOT];
+        stats->ms_light = c->tms[RDF_T_LIGHT];
+        stats->ms_rules = c->tms[RDF_T_RULES];
+        stats->ms_heavy = c->tms[RDF_T_HCOUNT] + c->tms[RDF_T_HWRITE];
+        stats->n_heavy_candidates = c->heavy_candidates;
     }
     c->stage = 4;
     return RDF_OK;
@@ -666,6 +705,37 @@ rdf_status rdf_copy_cinds(rdf_ctx* c, rdf_cind* out, uint64_t cap, uint64_t* n_c
     return RDF_OK;
 }
 
+rdf_status rdf_copy_cinds_range(rdf_ctx* c, uint64_t offset, rdf_cind* out, uint64_t count, uint64_t* n_copied) {
+    if (!c || (count && !out)) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
+    std::vector<u64> buf(std::max<u64>(m, 1));
+    if (m) HIP_TRY(c, hipMemcpy(buf.data(), c->out_ptr + offset, m * 8, hipMemcpyDeviceToHost));
+    for (u64 i = 0; i < m; ++i) {
+        const u32 d = (u32)(buf[i] >> 32), r = (u32)buf[i];
+        out[i].dep = c->h_fcap[d];
+        out[i].ref = c->h_fcap[r];
+        out[i].support = c->h_csup[d];
+    }
+    if (n_copied) *n_copied = m;
+    return RDF_OK;
+}
+
+rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
+    if (!c || !checksum) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 7), 0, 8, c->stream));
+    if (c->n_out)
+        hipLaunchKernelGGL(k_checksum, dim3(grid_for(c->n_out, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
+                           c->out_ptr, c->n_out, c->fcap.as<u32>(), dscal(c, 7));
+    u64 v = 0;
+    rdf_status rs = read_u64(c, dscal(c, 7), &v);
+    *checksum = v;
+    return rs;
+}
+
 rdf_status rdf_decode_capture(rdf_ctx* c, uint32_t capture, uint32_t* code, uint32_t* value1, uint32_t* value2) {
     if (!c || !code || !value1 || !value2) return RDF_ERR_ARG;
     static const uint32_t UN[6] = {10, 12, 17, 20, 33, 34}, BI[3] = {14, 21, 35};
@@ -695,6 +765,12 @@ rdf_status rdf_copy_binary_keys(rdf_ctx* c, uint64_t* out, uint64_t cap) {
     if (!c || (cap && !out)) return RDF_ERR_ARG;
     const u64 m = std::min<u64>(cap, c->h_bkeys.size());
     if (m) memcpy(out, c->h_bkeys.data(), m * 8);
+    return RDF_OK;
+}
+
+rdf_status rdf_kernel_times(rdf_ctx* c, float* ms, int count) {
+    if (!c || !ms || count < 0) return RDF_ERR_ARG;
+    for (int i = 0; i < count; ++i) ms[i] = i < RDF_NUM_TIMERS ? c->tms[i] : 0.f;
     return RDF_OK;
 }
 

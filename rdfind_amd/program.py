@@ -1,0 +1,154 @@
+"""RDFind-compatible driver: same flags, same plan stages, same ``Cind.toString`` output.
+
+Mirrors ``RDFind.createFlinkPlan`` (ALG/programs/RDFind.scala:196-580) for the hot path:
+read + parse N-Triples -> (optional) distinct triples -> frequent conditions (--use-fis) -> capture
+groups -> traversal strategy (0 AllAtOnce, 1 S2L) incl. --clean-implied -> output.  The three middle
+stages run on the GPU through the C ABI (``include/rdfind_hip.h``); there is no CPU fallback.
+
+Flag names follow ``RDFind.Parameters`` (RDFind.scala:639-721).  Flags that only change how Flink
+executes (and not the result) are accepted and ignored; flags whose semantics are out of scope for
+this build raise ``NotImplementedError`` instead of silently producing a different result.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+from . import _lib, codes, ntriples
+
+# flags accepted for compatibility that do not change the CIND result
+_RESULT_NEUTRAL = {
+    "--frequent-condition-strategy": int, "--no-combinable-join": None, "--no-bulk-merge": None,
+    "--rebalance-join": None, "--rebalance-strategy": int, "--rebalance-split": int,
+    "--rebalance-threshold": float, "--rebalance-max-load": int, "--merge-window-size": int,
+    "--counters": int, "--print-plan": None, "--rmi-server": str, "--no-clean-up": None,
+    "--configuration": str, "--wait": None, "--flink-verbose": None, "-jar": str, "-rex": str,
+}
+# flags whose semantics this build does not implement (SURVEY.md 8f "next" rows or out of scope)
+_UNSUPPORTED = ["--use-ars", "--ar-output", "--prefixes", "--asciify-triples", "--apply-hash", "--hash-dictionary",
+                "--hash-function", "--hash-bytes", "--any-binary-captures", "--find-frequent-captures",
+                "--explicit-threshold", "--sbf-bytes", "--balanced-overlap-candidates"]
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(prog="rdfind", description="CIND discovery on RDF (MI355X)")
+    ap.add_argument("inputs", nargs="*", help="input files to process")
+    ap.add_argument("--support", type=int, default=10, help="minimum support for conditions involved in CINDs")
+    ap.add_argument("--traversal-strategy", type=int, default=1, help="ID of CIND search space traversal strategy")
+    ap.add_argument("--use-fis", action="store_true", help="whether to find and use frequent item sets")
+    ap.add_argument("--clean-implied", action="store_true", help="whether to remove implied CINDs")
+    ap.add_argument("--output", default=None, help="an output file to save the CINDs to")
+    ap.add_argument("--projection", default="spo", help="what shall be used as projection for captures")
+    ap.add_argument("--distinct-triples", action="store_true", help="whether to ensure that triples are distinct")
+    ap.add_argument("--tabs", action="store_true", help="if input file is tab-separated")
+    ap.add_argument("--collect-result", action="store_true", help="whether to collect the results locally")
+    ap.add_argument("--debug-level", type=int, default=0, help="0: no debug prints, 1: some, ...")
+    ap.add_argument("--find-only-fcs", type=int, default=0)
+    ap.add_argument("--do-only-join", action="store_true")
+    ap.add_argument("--only-read", action="store_true")
+    ap.add_argument("--create-join-histogram", action="store_true")
+    ap.add_argument("-dop", "--gpus", dest="dop", type=int, default=-1, help="degree of parallelism (GPUs)")
+    ap.add_argument("--device", type=int, default=0)
+    for flag, typ in _RESULT_NEUTRAL.items():
+        if typ is None:
+            ap.add_argument(flag, action="store_true", help="accepted; does not change the result")
+        else:
+            ap.add_argument(flag, type=typ, default=None, help="accepted; does not change the result")
+    for flag in _UNSUPPORTED:
+        ap.add_argument(flag, nargs="?", const=True, default=None, help="not supported by this build")
+    return ap
+
+
+class RDFind:
+    """Program lifecycle (AbstractProgram.run: FLK/jobs/AbstractProgram.java:112-139)."""
+
+    def __init__(self, argv):
+        self.args = build_parser().parse_args(argv)
+        for flag in _UNSUPPORTED:
+            if getattr(self.args, flag.lstrip("-").replace("-", "_")) is not None:
+                raise NotImplementedError(f"{flag} is not supported by this build (SURVEY.md section 8f)")
+        if self.args.traversal_strategy not in (0, 1):
+            raise NotImplementedError(f"traversal strategy {self.args.traversal_strategy} is not supported (0 or 1)")
+        if self.args.traversal_strategy == 1 and not self.args.use_fis:
+            # RDFind.scala:290-296 leaves frequentDoubleConditions null without --use-fis and
+            # SmallToLargeTraversalStrategy.scala:534 dereferences it.
+            raise ValueError("traversal strategy 1 (S2L) requires --use-fis")
+        self.timings = {}
+
+    def log(self, msg):
+        print(msg, file=sys.stderr)
+
+    def run(self, out=sys.stdout):
+        a = self.args
+        t0 = time.time()
+        paths = ntriples.resolve_paths(a.inputs)
+        if not paths:
+            raise ValueError("no input files")
+        s, p, o, dic = ntriples.read_triples(paths, tabs=a.tabs)
+        if a.distinct_triples:
+            key = np.unique(np.stack([s, p, o], axis=1), axis=0)
+            s, p, o = key[:, 0].copy(), key[:, 1].copy(), key[:, 2].copy()
+        self.timings["read"] = time.time() - t0
+        if a.only_read:
+            return []
+        t1 = time.time()
+        with _lib.Context(a.device) as ctx:
+            ctx.set_triples(s, p, o, dic.size)
+            fc = ctx.frequent_conditions(a.support)
+            if a.debug_level >= 1:
+                self.log(f"Found {sum(fc['n_frequent_unary'])} frequent single-conditions.")
+                self.log(f"Found {fc['n_frequent_binary']} frequent double-conditions.")
+            if a.find_only_fcs >= 1:
+                return []
+            gs = ctx.build_capture_groups(a.projection)
+            if a.do_only_join:
+                return []
+            cs = ctx.discover_cinds(clean_implied=a.clean_implied, traversal_strategy=a.traversal_strategy)
+            ctx.sync()
+            self.timings["discover"] = time.time() - t1
+            self.timings["device_ms"] = ctx.stage_times()
+            rows = ctx.decoded_cinds()
+        self.stats = {"fc": fc, "groups": gs, "cinds": cs}
+        t2 = time.time()
+        lines = format_rows(rows, dic.term)
+        self.timings["format"] = time.time() - t2
+        if a.debug_level >= 1:
+            self.log(f"Found {len(lines)} CINDs in total.")
+        if a.output:
+            path = a.output[5:] if a.output.startswith("file:") else a.output
+            while path.startswith("//"):
+                path = path[1:]
+            d = os.path.dirname(os.path.abspath(path))
+            os.makedirs(d, exist_ok=True)
+            with open(path, "w", encoding="utf-8") as f:
+                for ln in lines:
+                    f.write(ln)
+                    f.write("\n")
+            self.log(f"Outputting CINDs to {os.path.abspath(path)}.")
+        if a.collect_result or a.debug_level >= 3:
+            for ln in lines:
+                print(ln, file=out)
+        if not a.output and not a.collect_result:
+            print(f"Detected {len(lines)} CINDs.", file=out)
+        return lines
+
+
+def format_rows(rows, term):
+    """``Cind.toString`` for decoded rows (ALG/data/Cind.scala:29-31)."""
+    none = 0xFFFFFFFF
+    out = []
+    for dc, d1, d2, rc, r1, r2, sup in rows.tolist():
+        dep = codes.pretty_print(dc, term(d1), None if d2 == none else term(d2))
+        ref = codes.pretty_print(rc, term(r1), None if r2 == none else term(r2))
+        out.append(f"{dep} < {ref} (support={sup})")
+    return out
+
+
+def main(argv=None):
+    prog = RDFind(sys.argv[1:] if argv is None else argv)
+    prog.run()
+    return 0

@@ -137,7 +137,7 @@ _N_RESEARCH = 30             # researchInterest literal pool "Research{i}"
 _NAME_POOL = 2000            # name literals "UndergraduateStudent{i}" etc. repeat across departments
 
 
-def lubm(n_universities: int = 100, seed: int = 0, min_support: int = 10) -> Dataset:
+def lubm(n_universities: int = 100, seed: int = 0, min_support: int = 10, max_departments: int | None = None) -> Dataset:
     """LUBM(n)-shaped triples (~133k per university).  Term ids are allocated in ranges so that
     :class:`TermTable` can print them; literals such as names repeat across departments as in UBA."""
     rng = np.random.default_rng(seed)
@@ -159,7 +159,10 @@ def lubm(n_universities: int = 100, seed: int = 0, min_support: int = 10) -> Dat
     # Plan all departments first so that entity id ranges can be allocated contiguously.
     depts = []
     for u in range(n_universities):
-        for d in range(int(rng.integers(15, 26))):
+        n_dep = int(rng.integers(15, 26))
+        if max_departments is not None:
+            n_dep = min(n_dep, max_departments)
+        for d in range(n_dep):
             fac = [int(rng.integers(lo, hi + 1)) for (_, lo, hi, _, _) in _FAC]
             nf = sum(fac)
             depts.append(dict(u=u, d=d, fac=fac, nf=nf, ug=nf * int(rng.integers(8, 15)),

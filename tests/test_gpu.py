@@ -1,0 +1,160 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+* bit-exact CIND sets vs the C/Python restatements on random inputs, edge cases and scaled BASELINE
+  configs, in every mode (strategy 0/1 x --clean-implied on/off);
+* the golden fixtures through the full program (N-Triples -> GPU -> Cind.toString lines);
+* at the bench size (c2 = LUBM-100 shape), size-independent properties: determinism, rule
+  monotonicity (clean <= S2L-raw <= V), and direct verification of sampled CINDs against the triples.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import c_oracle as C, rdfind_oracle as R
+from rdfind_amd import _lib, ntriples, program, synth
+from tests.conftest import GOLDEN
+from tests.test_oracle import KAT_PEOPLE, KAT_PEOPLE_CLEAN, KAT_PEOPLE_RAW, read_golden
+
+pytestmark = pytest.mark.gpu
+
+MODES = [(1, True), (0, True), (0, False), (1, False)]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = _lib.Context(0)
+    yield c
+    c.close()
+
+
+def expected_set(arr, nv, ms, strategy, clean):
+    if strategy == 1 and not clean:  # exact-candidate S2L raw output (oracle.s2l_exact_raw)
+        tr = [tuple(x) for x in arr.tolist()]
+        uf = R.frequent_unary_conditions(tr, ms)
+        v = R.all_at_once(R.join_lines(tr, uf, R.frequent_binary_conditions(tr, uf, ms)), ms, False,
+                          literal_implies=False)
+        return R.cind_set(R.s2l_exact_raw(v))
+    got, _ = C.run_set(arr[:, 0], arr[:, 1], arr[:, 2], nv, ms, strategy, clean)
+    return got
+
+
+def gpu_set(ctx, arr, nv, ms, strategy, clean, projection="spo"):
+    ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+    ctx.run(ms, projection, clean, strategy)
+    return _lib.decoded_to_set(ctx.decoded_cinds())
+
+
+def test_random_parity_all_modes(ctx):
+    rng = random.Random(11)
+    for _ in range(150):
+        n = rng.randrange(1, 250)
+        nv = rng.randrange(2, 40)
+        ms = rng.randrange(1, 5)
+        arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                       dtype=np.uint32)
+        for strategy, clean in MODES:
+            assert gpu_set(ctx, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
+                (n, nv, ms, strategy, clean)
+
+
+def test_projection_subsets(ctx):
+    rng = random.Random(5)
+    for proj in ("s", "p", "o", "sp", "so", "po"):
+        arr = np.array([(rng.randrange(12), rng.randrange(4), rng.randrange(12)) for _ in range(200)], dtype=np.uint32)
+        exp, _ = C.run_set(arr[:, 0], arr[:, 1], arr[:, 2], 12, 2, 1, True, proj)
+        assert gpu_set(ctx, arr, 12, 2, 1, True, proj) == exp, proj
+
+
+def test_edge_cases(ctx):
+    empty = np.zeros((0, 3), np.uint32)
+    assert gpu_set(ctx, empty, 1, 1, 1, True) == set()
+    one = np.array([[0, 1, 2]], np.uint32)
+    assert gpu_set(ctx, one, 3, 1, 1, True) == expected_set(one, 3, 1, 1, True)
+    dup = np.array([[0, 1, 2]] * 50, np.uint32)  # duplicates count for conditions, not for support
+    for strategy, clean in MODES:
+        assert gpu_set(ctx, dup, 3, 2, strategy, clean) == expected_set(dup, 3, 2, strategy, clean)
+    same = np.array([[4, 4, 4], [4, 4, 4], [1, 4, 4], [4, 1, 1]], np.uint32)  # equal values across positions
+    for strategy, clean in MODES:
+        assert gpu_set(ctx, same, 5, 1, strategy, clean) == expected_set(same, 5, 1, strategy, clean)
+    big_ms = np.array([[0, 1, 2], [1, 1, 2]], np.uint32)
+    assert gpu_set(ctx, big_ms, 3, 1000, 1, True) == set()
+    assert gpu_set(ctx, big_ms, 3, 0, 1, True) == expected_set(big_ms, 3, 1, 1, True)  # support 0 == 1
+
+
+def test_kat_people(ctx):
+    dic = ntriples.Dictionary()
+    arr = np.array([[dic.encode(a), dic.encode(b), dic.encode(c)] for a, b, c in KAT_PEOPLE], np.uint32)
+    for clean, expected in ((True, KAT_PEOPLE_CLEAN), (False, None)):
+        ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], dic.size)
+        ctx.run(2, "spo", clean, 0)
+        lines = sorted(program.format_rows(ctx.decoded_cinds(), dic.term))
+        assert lines == (expected if expected is not None else KAT_PEOPLE_RAW)
+
+
+@pytest.mark.parametrize("name", ["zipf_small", "lubm_small", "skew_small"])
+@pytest.mark.parametrize("mode,flags", [("s1_clean", ["--use-fis", "--clean-implied"]),
+                                        ("s0_clean", ["--traversal-strategy", "0", "--clean-implied"]),
+                                        ("s0_raw", ["--traversal-strategy", "0"])])
+def test_program_reproduces_golden(tmp_path, name, mode, flags):
+    ms, expected = read_golden(name, mode)
+    out = tmp_path / "cinds.txt"
+    prog = program.RDFind(flags + ["--support", str(ms), "--output", f"file://{out}",
+                                   os.path.join(GOLDEN, f"{name}.nt.gz")])
+    prog.run()
+    assert sorted(out.read_text().splitlines()) == expected
+
+
+@pytest.mark.parametrize("cfg,scale", [("c1", 0.3), ("c2", 0.05), ("c3", 0.002), ("c4", 0.0003), ("c5", 0.01)])
+def test_synthetic_configs_vs_oracle(ctx, cfg, scale):
+    d = synth.config(cfg, scale)
+    exp, st = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support)
+    # intermediate stages agree with the restatement too
+    assert ctx.fc["n_frequent_unary"] == st["n_freq_unary"]
+    assert ctx.fc["n_frequent_binary"] == st["n_freq_binary"]
+    assert ctx.groups["n_records"] == st["n_records"]
+    assert ctx.groups["n_captures"] == st["n_freq_captures"]
+    assert _lib.decoded_to_set(ctx.decoded_cinds()) == exp
+
+
+def _capture_joins(d, code, v1, v2):
+    """Distinct join values of a capture, straight from the triples (the definition of its groups)."""
+    cols = {1: d.s, 2: d.p, 4: d.o}
+    prim, proj = code & 7, (code >> 3) & 7
+    first = prim & -prim
+    second = prim & ~first
+    mask = cols[first] == v1
+    if second:
+        mask &= cols[second] == v2
+    return np.unique(cols[proj][mask])
+
+
+def test_bench_size_properties(ctx):
+    """c2 at full size (the bench workload): determinism, rule monotonicity, sampled verification."""
+    d = synth.config("c2", 1.0)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support, "spo", True, 1)
+    n_clean = ctx.cind_count()
+    sum_clean = ctx.checksum()
+    rng = np.random.default_rng(0)
+    offsets = rng.choice(n_clean, size=min(40, n_clean), replace=False)
+    sample = np.concatenate([ctx.copy_cinds_range(int(off), 1) for off in offsets])
+    bkeys = ctx.binary_keys()
+    ctx.run(d.min_support, "spo", True, 1)
+    assert ctx.cind_count() == n_clean and ctx.checksum() == sum_clean  # deterministic set
+    ctx.run(d.min_support, "spo", False, 1)
+    n_s2l_raw = ctx.cind_count()
+    ctx.run(d.min_support, "spo", False, 0)
+    n_v_literal = ctx.cind_count()
+    assert 0 < n_clean <= n_s2l_raw and n_v_literal > 0
+    # verify sampled CINDs directly: every join value of dep is a join value of ref; support = #joins(dep)
+    dec = _lib.decode_rows(sample, d.num_terms, bkeys)
+    for r in dec.tolist():
+        dc, d1, d2, rc, r1, r2, sup = r
+        jd = _capture_joins(d, dc, d1, d2)
+        jr = _capture_joins(d, rc, r1, r2)
+        assert len(jd) == sup
+        assert np.isin(jd, jr).all()
