@@ -39,6 +39,9 @@ def algorithmic_bytes(name, d, gs, cs, kt_counts):
         return 12 * n + 8 * J                           # read triples, write (join, capture) records
     if name == "sort":
         return 16 * kt_counts["sort_passes_records"]    # read + write each record once per 8-bit pass
+    if name == "cemit":
+        n_out = cs["n_class_cinds"]
+        return 8 * n_out + 4 * n_out // 16            # 8-B (dep, ref) records written; list re-read once per 16 deps
     if name in ("hwrite", "hcount"):
         cand = cs["n_heavy_candidates"]
         out = 8 * cs["n_cinds"] if name == "hwrite" else 4 * cs["n_heavy_chunks"]

@@ -75,7 +75,10 @@ typedef struct {
     uint64_t n_light_chunks;
     uint64_t n_heavy_chunks;
     float ms_pivot, ms_light, ms_rules, ms_heavy;  /* device time per K6/K7 kernel family */
-    uint64_t n_heavy_candidates;    /* pivot members scanned for dependents whose groups are all heavy */
+    uint64_t n_heavy_candidates;    /* pivot members scanned for binary dependents whose groups are all heavy */
+    uint64_t n_class_members;       /* unary dependents whose groups are all heavy (emitted per mask class) */
+    uint64_t n_classes;             /* distinct heavy bitmasks among them */
+    uint64_t n_class_cinds;         /* CINDs emitted by the class path */
 } rdf_cind_stats;
 
 /* Kernel-family device timers (HIP events on the context stream), see rdf_kernel_times. */
@@ -93,6 +96,8 @@ enum {
     RDF_T_HCOUNT,       /* K6 heavy-only count pass (minimality fused) */
     RDF_T_RULES,        /* K7 minimality on explicit pairs */
     RDF_T_HWRITE,       /* K6 heavy-only write pass (minimality fused) */
+    RDF_T_CLASS,        /* K6c mask classes of unary heavy-only dependents + filtered shared ref lists */
+    RDF_T_CEMIT,        /* K6c streaming emission of the class ref lists */
     RDF_NUM_TIMERS
 };
 

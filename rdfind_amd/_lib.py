@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
 
 # RDF_T_* kernel-family timers (include/rdfind_hip.h)
 TIMER_NAMES = ("unary", "binary", "emit", "sort", "support", "groups", "heavymask", "pivot", "light", "esort",
-               "hcount", "rules", "hwrite")
+               "hcount", "rules", "hwrite", "class", "cemit")
 
 
 class FcStats(ctypes.Structure):
@@ -49,7 +49,8 @@ class CindStats(ctypes.Structure):
     _fields_ = [("n_cinds", ctypes.c_uint64), ("n_explicit_raw", ctypes.c_uint64),
                 ("n_light_chunks", ctypes.c_uint64), ("n_heavy_chunks", ctypes.c_uint64),
                 ("ms_pivot", ctypes.c_float), ("ms_light", ctypes.c_float), ("ms_rules", ctypes.c_float),
-                ("ms_heavy", ctypes.c_float), ("n_heavy_candidates", ctypes.c_uint64)]
+                ("ms_heavy", ctypes.c_float), ("n_heavy_candidates", ctypes.c_uint64),
+                ("n_class_members", ctypes.c_uint64), ("n_classes", ctypes.c_uint64), ("n_class_cinds", ctypes.c_uint64)]
 
 
 CIND_DTYPE = np.dtype([("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])

@@ -8,6 +8,7 @@ static constexpr int LH_SLOTS = 4096;     // LDS hash slots (u32 keys) for unary
 static constexpr int LB_SLOTS = 2048;     // LDS hash slots (u64 keys) for binary counting
 static constexpr int HMAX = 64;           // heavy groups tracked as bit columns (one u64 per capture)
 static constexpr uint8_t LIGHT = 0xff;
+static constexpr u64 LIGHT_SEG = 2048;   // groups of one dependent verified by one light work item
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
 struct __align__(16) CapInfo {
@@ -35,6 +36,7 @@ struct CindView {
     const u32* plist;     // parents (binary compact ids)
     const u64* eoff;      // explicit CSR: dep -> refs [C+1]
     const u64* epairs;    // explicit (dep << 32 | ref) pairs, sorted
+    const u64* ebin;      // first explicit pair of a dep whose ref is binary
     int literal;          // strategy-0 Condition.isImpliedBy quirk
     int mode;             // RuleMode
 };

@@ -42,8 +42,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_unary_count(const u32* __restrict
         lcnt[i] = 0;
     }
     __syncthreads();
-    const u64 stride = (u64)gridDim.x * RDF_BLOCK;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += stride) {
+    // one contiguous chunk per block so that runs of equal values (e.g. subjects) aggregate in LDS
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
         lds_count_u32(lkey, lcnt, s[i], cnt);
         lds_count_u32(lkey, lcnt, V + p[i], cnt);
         lds_count_u32(lkey, lcnt, 2u * V + o[i], cnt);
@@ -202,6 +204,26 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
     }
 }
 
+// Block-aggregated append: one global atomic per block iteration instead of one per wave.
+__device__ inline u64 block_append(u64* counter, u32 want, u32* lds_wave, u64* lds_base) {
+    const int wave = threadIdx.x / RDF_WAVE;
+    const u32 incl = wave_inclusive_scan(want);
+    if (lane_id() == RDF_WAVE - 1) lds_wave[wave] = incl;
+    __syncthreads();
+    u32 woff = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
+        const u32 x = lds_wave[w];
+        woff += w < wave ? x : 0u;
+        total += x;
+    }
+    if (threadIdx.x == 0) *lds_base = total ? atomicAdd(counter, (u64)total) : 0ull;
+    __syncthreads();
+    const u64 base = *lds_base + woff + incl - want;
+    __syncthreads();  // lds_wave / lds_base are reused by the next iteration
+    return base;
+}
+
 // ================================================================================================
 // K3: join partners  (CreateJoinPartners.flatMap, ALG/operators/CreateJoinPartners.scala:86-147)
 // Per triple and projection: unary captures of the frequent condition values and, when the binary
@@ -214,8 +236,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             const u32* __restrict__ cnt, const u64* __restrict__ lkeys,
                                                             const u32* __restrict__ lvals, u64 lmask, int proj,
                                                             int capbits, u64* out, u64* counter) {
+    __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
+    __shared__ u64 lds_base;
     const u64 stride = (u64)gridDim.x * RDF_BLOCK;
-    const u64 n_round = (n + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;  // all lanes of a wave iterate together
+    const u64 n_round = (n + RDF_BLOCK - 1) / RDF_BLOCK * RDF_BLOCK;  // all threads of a block iterate together
     const u64 B6 = 6ull * V;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n_round; i += stride) {
         u64 rec[9];
@@ -252,7 +276,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                 }
             }
         }
-        u64 base = wave_append(counter, c);
+        u64 base = block_append(counter, c, lds_wave, &lds_base);
         for (u32 k = 0; k < c; ++k) out[base + k] = rec[k];
     }
 }
@@ -263,12 +287,26 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
 //     captures per join value) and capture supports (depCount summed per group,
 //     ALG/operators/candidate_merging/BulkMergeDependencies.scala:78-84)
 
+// Hot captures (e.g. s[p=rdf:type]) appear once in almost every group: LDS-hash pre-aggregation over a
+// contiguous chunk of groups turns ~|groups| global atomics on one address into one per block.
 __global__ __launch_bounds__(RDF_BLOCK) void k_unique_support(const u64* __restrict__ keys, u64 n, u64 capmask,
                                                               u32* support) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        u64 k = keys[i];
-        if (i == 0 || keys[i - 1] != k) atomicAdd(&support[k & capmask], 1u);
+    __shared__ u32 lkey[LH_SLOTS];
+    __shared__ u32 lcnt[LH_SLOTS];
+    for (int i = threadIdx.x; i < LH_SLOTS; i += RDF_BLOCK) {
+        lkey[i] = EMPTY32;
+        lcnt[i] = 0;
     }
+    __syncthreads();
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
+        u64 k = keys[i];
+        if (i == 0 || keys[i - 1] != k) lds_count_u32(lkey, lcnt, (u32)(k & capmask), support);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < LH_SLOTS; i += RDF_BLOCK)
+        if (lkey[i] != EMPTY32) atomicAdd(&support[lkey[i]], lcnt[i]);
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_support_flags(const u32* __restrict__ support, u64 ncap, u32 ms, u32* flags) {
@@ -333,13 +371,16 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_info_support_u32(const CapInfo* _
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < C; i += (u64)gridDim.x * RDF_BLOCK) out[i] = info[i].support;
 }
 
-// dependent -> groups (transposed CSR); order inside a list is irrelevant
-__global__ __launch_bounds__(RDF_BLOCK) void k_dep_scatter(const u32* __restrict__ gcap, const u32* __restrict__ gid, u64 n,
-                                                           u64* cursor, u32* dgrp) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        u64 pos = atomicAdd(&cursor[gcap[i]], 1ull);
-        dgrp[pos] = gid[i];
-    }
+// dependent -> groups (transposed CSR) by radix-sorting (capture << 32 | group): no per-capture cursor
+// atomics (a hot capture sits in ~every group), and every dependent's group list comes out sorted.
+__global__ __launch_bounds__(RDF_BLOCK) void k_make_tkeys(const u32* __restrict__ gcap, const u32* __restrict__ gid, u64 n,
+                                                          u64* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        out[i] = ((u64)gcap[i] << 32) | gid[i];
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_low32(const u64* __restrict__ keys, u64 n, u32* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) out[i] = (u32)keys[i];
 }
 
 // ---- heavy groups: quarter-octave size buckets, then the top groups become bit columns
@@ -351,8 +392,13 @@ __device__ __host__ inline int size_bucket(u64 size) {
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_group_size_hist(const u64* __restrict__ goff, u64 G, u32* hist) {
+    __shared__ u32 lh[256];
+    lh[threadIdx.x] = 0;
+    __syncthreads();
     for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK)
-        atomicAdd(&hist[size_bucket(goff[g + 1] - goff[g])], 1u);
+        atomicAdd(&lh[size_bucket(goff[g + 1] - goff[g])], 1u);
+    __syncthreads();
+    if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restrict__ goff, u64 G, u64 threshold, u32* nheavy,
@@ -419,13 +465,38 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_parent_meta(const u32* __restrict
 //     groups are verified by binary search with one lane per group.  Deps whose groups are all heavy
 //     ("heavy-only") need no verification: their refs are the pivot members passing the mask test.
 
-// pivot pass: one wave per dependent
-__global__ __launch_bounds__(RDF_BLOCK) void k_pivot(CindView v, u32* pivot, u32* nchunk_light, u32* nchunk_heavy,
-                                                     CapInfo* info, u64* heavy_candidates) {
+// pivot pass, itemised: a work item is (dependent, segment of PIVOT_SEG of its groups), one wave each, so a
+// dependent in ~every group (s[p=rdf:type]) is spread over many waves.  Items of a multi-segment dependent
+// combine with atomicMin/atomicAdd; k_pivot_final derives the chunk counts.
+static constexpr u64 PIVOT_SEG = 4096;
+
+__device__ inline u32 find_dep(const u64* chunk_off, u32 C, u64 w) {
+    // largest d with chunk_off[d] <= w
+    u32 lo = 0, hi = C;
+    while (lo < hi) {
+        u32 mid = (lo + hi + 1) >> 1;
+        if (chunk_off[mid] <= w) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_nseg(const u64* __restrict__ doff, u32 C, u32* nseg) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 len = doff[d + 1] - doff[d];
+        nseg[d] = (u32)((len + PIVOT_SEG - 1) / PIVOT_SEG);
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, const u64* __restrict__ segoff, u64 W, u64* best_out,
+                                                         u32* nlight_out) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
     const int lane = lane_id();
-    const u64 d = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (d >= v.C) return;
-    const u64 b = v.doff[d], e = v.doff[d + 1];
+    const u32 d = find_dep(segoff, v.C, w);
+    const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
+    const u64 b = b0 + (w - segoff[d]) * PIVOT_SEG;
+    const u64 e = b + PIVOT_SEG < e0 ? b + PIVOT_SEG : e0;
     u64 best = ~0ull;  // (size << 32 | group)
     u32 nlight = 0;
     for (u64 j = b + lane; j < e; j += RDF_WAVE) {
@@ -442,16 +513,41 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot(CindView v, u32* pivot, u32
     }
     nlight = wave_sum(nlight);
     if (lane == 0) {
-        u32 g = (u32)(best & 0xffffffffu);
-        u64 sz = best >> 32;
-        u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
-        pivot[d] = g;
-        nchunk_light[d] = nlight ? nch : 0;
-        nchunk_heavy[d] = nlight ? 0 : nch;
-        if (!nlight) {
-            info[d].meta |= META_HEAVY_ONLY;
-            atomicAdd(heavy_candidates, sz);
+        if (e0 - b0 <= PIVOT_SEG) {
+            best_out[d] = best;
+            nlight_out[d] = nlight;
+        } else {
+            atomicMin(&best_out[d], best);
+            atomicAdd(&nlight_out[d], nlight);
         }
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64* __restrict__ best_in,
+                                                           const u32* __restrict__ nlight_in, u32* pivot, u32* nchunk_light,
+                                                           u32* nitem_light, u32* nchunk_heavy, CapInfo* info,
+                                                           u64* heavy_candidates) {
+    const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
+        u32 hc = 0;
+        if (d < v.C) {
+            const u64 best = best_in[d];
+            const u32 nlight = nlight_in[d];
+            const u64 sz = best >> 32;
+            const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
+            pivot[d] = (u32)(best & 0xffffffffu);
+            nchunk_light[d] = nlight ? nch : 0;
+            nitem_light[d] = nlight ? nch * (u32)((v.doff[d + 1] - v.doff[d] + LIGHT_SEG - 1) / LIGHT_SEG) : 0;
+            // unary heavy-only dependents are emitted per bitmask class (k_class_*), binary ones by k_heavy
+            nchunk_heavy[d] = (nlight || d < v.Cu) ? 0 : nch;
+            if (!nlight) {
+                info[d].meta |= META_HEAVY_ONLY;
+                if (d >= v.Cu) hc = (u32)sz;
+            }
+        }
+        u64 tot = wave_inclusive_scan64(hc);
+        tot = __shfl(tot, RDF_WAVE - 1, RDF_WAVE);
+        if (lane_id() == 0 && tot) atomicAdd(heavy_candidates, tot);
     }
 }
 
@@ -511,36 +607,37 @@ __device__ inline bool member(const CindView& v, u32 x, u32 y) {
 //   R3 drop 1/1 A<R if A<X in V12, R in comp(X)
 //   R4 drop 2/2 D<X if comp(D)<X in V12
 // RULES_S2L_RAW applies only R1 and R4: the exact-candidate S2L output without --clean-implied.
+// exists a binary X with a < X (raw) and r a component of X?  Iterates the shorter of parents(r) and,
+// for a dependent with explicit refs, its binary refs (a suffix of its sorted explicit list).
+__device__ inline bool implied_via_binary_ref(const CindView& v, u32 a, u32 r) {
+    if (!(v.info[r].meta & META_PARENTS)) return false;
+    const u64 pb = v.poff[r], pe = v.poff[r + 1];
+    if (!(v.info[a].meta & META_HEAVY_ONLY)) {
+        const u64 xb = v.ebin[a], xe = v.eoff[a + 1];
+        if (xe - xb <= pe - pb) {
+            for (u64 j = xb; j < xe; ++j) {
+                const u32* bc = v.bcomp + 2ull * ((u32)v.epairs[j] - v.Cu);
+                if (bc[0] == r || bc[1] == r) return true;
+            }
+            return false;
+        }
+    }
+    for (u64 j = pb; j < pe; ++j)
+        if (member(v, a, v.plist[j])) return true;
+    return false;
+}
+
 __device__ inline bool rule_keep(const CindView& v, u32 a, u32 r) {
     if (v.mode == RULES_NONE) return true;
     const bool ab = a >= v.Cu, rb = r >= v.Cu;
     if (!ab && rb) return true;
-    if (!ab && !rb) {
-        if (v.mode != RULES_CLEAN) return true;
-        if (!(v.info[r].meta & META_PARENTS)) return true;
-        for (u64 j = v.poff[r]; j < v.poff[r + 1]; ++j)
-            if (member(v, a, v.plist[j])) return false;
-        return true;
-    }
+    if (!ab && !rb) return v.mode != RULES_CLEAN || !implied_via_binary_ref(v, a, r);  // R3
     const u32* bc = v.bcomp + 2ull * (a - v.Cu);
-    if (member(v, bc[0], r) || member(v, bc[1], r)) return false;  // R1 / R4
+    if (member(v, bc[0], r) || member(v, bc[1], r)) return false;                     // R1 / R4
     if (rb || v.mode != RULES_CLEAN) return true;
-    if (!(v.info[r].meta & META_PARENTS)) return true;
-    for (u64 j = v.poff[r]; j < v.poff[r + 1]; ++j)  // R2
-        if (member(v, a, v.plist[j])) return false;
-    return true;
+    return !implied_via_binary_ref(v, a, r);                                            // R2
 }
 
-__device__ inline u32 find_dep(const u64* chunk_off, u32 C, u64 w) {
-    // largest d with chunk_off[d] <= w
-    u32 lo = 0, hi = C;
-    while (lo < hi) {
-        u32 mid = (lo + hi + 1) >> 1;
-        if (chunk_off[mid] <= w) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
 
 // candidate filter for a chunk of the pivot group: returns this lane's candidate (or NONE)
 __device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 chunk) {
@@ -556,19 +653,36 @@ __device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& i
     return r;
 }
 
-// light dependents: verify light groups, write explicit (dep << 32 | ref) pairs
-__global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ choff,
-                                                     u64 W, u64* pairs, u64* npairs) {
+__device__ inline void emit_pairs(u32 d, u32 cand, u64 alive, u64* pairs, u64* npairs) {
+    if (!alive) return;
+    const u32 cnt = (u32)__popcll(alive);
+    u64 base = 0;
+    if (lane_id() == 0) base = atomicAdd(npairs, (u64)cnt);
+    base = __shfl(base, 0, RDF_WAVE);
+    if ((alive >> lane_id()) & 1ull) pairs[base + __popcll(alive & lanemask_lt())] = ((u64)d << 32) | cand;
+}
+
+// light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
+// dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
+// multi-segment ones publish the candidates they kill with atomicOr and k_light_final emits the survivors.
+__global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
+                                                     const u64* __restrict__ choff, u64 W, u64* dead, u64* pairs,
+                                                     u64* npairs) {
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
-    const u32 d = find_dep(choff, v.C, w);
-    const u64 chunk = w - choff[d];
+    const u32 d = find_dep(itemoff, v.C, w);
+    const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
+    const u64 nseg = (e0 - b0 + LIGHT_SEG - 1) / LIGHT_SEG;
+    const u64 item = w - itemoff[d];
+    const u64 chunk = item / nseg, seg = item % nseg;
     const u32 piv = pivot[d];
     const CapInfo id = v.info[d];
     const u32 cand = chunk_candidate(v, d, id, piv, chunk);
-    u64 alive = __ballot(cand != NONE32);
-    const u64 b = v.doff[d], e = v.doff[d + 1];
+    const u64 alive0 = __ballot(cand != NONE32);
+    u64 alive = alive0;
+    const u64 b = b0 + seg * LIGHT_SEG;
+    const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
     for (u64 j0 = b; j0 < e && alive; j0 += RDF_WAVE) {
         const u64 j = j0 + lane;
         u32 g = NONE32;
@@ -591,24 +705,43 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
             if (!__all(ok)) alive &= ~(1ull << bit);
         }
     }
-    if (!alive) return;
-    const u32 cnt = (u32)__popcll(alive);
-    u64 base = 0;
-    if (lane == 0) base = atomicAdd(npairs, (u64)cnt);
-    base = __shfl(base, 0, RDF_WAVE);
-    if ((alive >> lane) & 1ull) pairs[base + __popcll(alive & lanemask_lt())] = ((u64)d << 32) | cand;
+    if (nseg == 1) {
+        emit_pairs(d, cand, alive, pairs, npairs);
+    } else if (lane == 0 && (alive0 & ~alive)) {
+        atomicOr(&dead[choff[d] + chunk], alive0 & ~alive);
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_final(CindView v, const u32* __restrict__ pivot,
+                                                           const u64* __restrict__ choff, u64 W,
+                                                           const u64* __restrict__ dead, u64* pairs, u64* npairs) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 d = find_dep(choff, v.C, w);
+    if (v.doff[d + 1] - v.doff[d] <= LIGHT_SEG) return;  // single segment: already emitted
+    const u64 chunk = w - choff[d];
+    const u32 cand = chunk_candidate(v, d, v.info[d], pivot[d], chunk);
+    const u64 alive = __ballot(cand != NONE32) & ~dead[w];
+    emit_pairs(d, cand, alive, pairs, npairs);
 }
 
 // explicit CSR offsets: eoff[d] = first pair with dep >= d
-__global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restrict__ pairs, u64 E, u32 C, u64* eoff) {
+__device__ inline u64 lower_bound_u64(const u64* a, u64 n, u64 key) {
+    u64 lo = 0, hi = n;
+    while (lo < hi) {
+        u64 mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ebin[d] = first explicit pair of d with a binary ref (ref >= Cu)
+__global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restrict__ pairs, u64 E, u32 C, u32 Cu, u64* eoff,
+                                                            u64* ebin) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d <= C; d += (u64)gridDim.x * RDF_BLOCK) {
-        u64 key = d << 32, lo = 0, hi = E;
-        while (lo < hi) {
-            u64 mid = (lo + hi) >> 1;
-            if (pairs[mid] < key) lo = mid + 1;
-            else hi = mid;
-        }
-        eoff[d] = lo;
+        eoff[d] = lower_bound_u64(pairs, E, d << 32);
+        if (d < C) ebin[d] = lower_bound_u64(pairs, E, (d << 32) | Cu);
     }
 }
 
@@ -629,30 +762,221 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const 
 }
 
 // heavy-only dependents: refs = pivot members passing the mask test; minimality fused.
-// WRITE=false: count per work item; WRITE=true: write at the scanned offsets.
+// WRITE=false: count per work item; WRITE=true: write at the scanned offsets.  Each wave walks HEAVY_TILE
+// consecutive work items (chunks of 64 candidates), so the dependent lookup is amortised.
+static constexpr u32 HEAVY_TILE = 1;  // 8 measured 60% slower (fewer independent waves in flight)
+
 template <bool WRITE>
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ choff,
                                                      u64 W, u32* counts, const u64* __restrict__ woff, u64 out_base,
                                                      u64* out) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
+    const u64 w0 = ((u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE) * HEAVY_TILE;
+    if (w0 >= W) return;
     const int lane = lane_id();
-    const u32 d = find_dep(choff, v.C, w);
-    const u64 chunk = w - choff[d];
-    const CapInfo id = v.info[d];
-    const u32 cand = chunk_candidate(v, d, id, pivot[d], chunk);
-    const bool keep = cand != NONE32 && rule_keep(v, d, cand);
-    const u64 kept = __ballot(keep);
-    if (!WRITE) {
-        if (lane == 0) counts[w] = (u32)__popcll(kept);
-    } else if (keep) {
-        out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = ((u64)d << 32) | cand;
+    u32 d = find_dep(choff, v.C, w0);
+    u64 dend = choff[d + 1];
+    CapInfo id = v.info[d];
+    u32 piv = pivot[d];
+    for (u32 t = 0; t < HEAVY_TILE; ++t) {
+        const u64 w = w0 + t;
+        if (w >= W) break;
+        if (w >= dend) {  // next dependent with chunks
+            do {
+                ++d;
+                dend = choff[d + 1];
+            } while (w >= dend);
+            id = v.info[d];
+            piv = pivot[d];
+        }
+        const u64 chunk = w - choff[d];
+        const u32 cand = chunk_candidate(v, d, id, piv, chunk);
+        const bool keep = cand != NONE32 && rule_keep(v, d, cand);
+        const u64 kept = __ballot(keep);
+        if (!WRITE) {
+            if (lane == 0) counts[w] = (u32)__popcll(kept);
+        } else if (keep) {
+            out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = ((u64)d << 32) | cand;
+        }
     }
 }
 
-}  // namespace rdf
 
-namespace rdf {
+// ================================================================================================
+// K6c: unary heavy-only dependents by bitmask class.  A dependent A whose groups are all heavy has
+// support(A) = popcount(hmask(A)) and refs(A) = {B : hmask(B) covers hmask(A)} \ {A}; every dependent with
+// the same mask shares the pivot group and therefore the ref list L(m).  Under --clean-implied, R3 removes
+// from a unary A's 1/1 refs every R that is a component of a binary ref X of A -- for heavy-only A that is
+// "R has a parent binary whose mask covers m", again a class property.  So L'(m) is built once per class
+// and each dependent's output is L'(m) minus itself: a streaming copy bound by the HBM write rate.
+
+// member-free R3 test for a heavy-only unary dependent with mask m
+__device__ inline bool r3_dropped_for_mask(const CindView& v, u32 r, u64 m) {
+    if (r >= v.Cu || !(v.info[r].meta & META_PARENTS)) return false;
+    for (u64 j = v.poff[r]; j < v.poff[r + 1]; ++j) {
+        const u64 mx = v.info[v.plist[j]].hmask;
+        if ((mx & m) == m) return true;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u64* tkeys, u64 tmask, u64* nmembers) {
+    u32 cnt = 0;
+    const u64 n_round = ((u64)v.Cu + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
+        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY)) {
+            const u64 m = v.info[d].hmask;  // never 0 for a heavy-only dependent
+            u64 h = mix64(m) & tmask;
+            for (;;) {
+                u64 k = tkeys[h];
+                if (k == m) break;
+                if (k == 0) {
+                    u64 prev = atomicCAS(&tkeys[h], 0ull, m);
+                    if (prev == 0 || prev == m) break;
+                }
+                h = (h + 1) & tmask;
+            }
+            cnt++;
+        }
+    }
+    cnt = wave_sum(cnt);
+    if (lane_id() == 0 && cnt) atomicAdd(nmembers, (u64)cnt);
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_nonzero_flags(const u64* __restrict__ a, u64 n, u32* flags) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) flags[i] = a[i] != 0;
+}
+
+// (class << 32 | dep) keys for all unary heavy-only dependents
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_keys(CindView v, const u64* __restrict__ tkeys, const u32* __restrict__ cid,
+                                                          u64 tmask, u64* out, u64* counter) {
+    const u64 n_round = ((u64)v.Cu + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
+        u32 want = 0;
+        u64 key = 0;
+        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY)) {
+            const u64 m = v.info[d].hmask;
+            u64 h = mix64(m) & tmask;
+            while (tkeys[h] != m) h = (h + 1) & tmask;
+            key = ((u64)cid[h] << 32) | d;
+            want = 1;
+        }
+        u64 pos = wave_append(counter, want);
+        if (want) out[pos] = key;
+    }
+}
+
+// per class: member offsets, mask, pivot, pivot-chunk count
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_info(CindView v, const u64* __restrict__ keys, u64 nkeys, u32 ncls,
+                                                          const u32* __restrict__ pivot, u64* coff, u64* cmask, u32* cpiv,
+                                                          u32* cnch) {
+    for (u64 m = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; m <= ncls; m += (u64)gridDim.x * RDF_BLOCK) {
+        u64 lo = lower_bound_u64(keys, nkeys, m << 32);
+        coff[m] = lo;
+        if (m < ncls) {
+            const u32 rep = (u32)keys[lo];
+            const u32 g = pivot[rep];
+            cmask[m] = v.info[rep].hmask;
+            cpiv[m] = g;
+            cnch[m] = (u32)((v.goff[g + 1] - v.goff[g] + RDF_WAVE - 1) / RDF_WAVE);
+        }
+    }
+}
+
+// L'(m): filter the class pivot group (count pass, then write pass at scanned offsets -> sorted lists)
+template <bool WRITE>
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_filter(CindView v, const u64* __restrict__ cchoff, u32 ncls,
+                                                            u64 W, const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
+                                                            u32* counts, const u64* __restrict__ woff, u32* lists) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 m = find_dep(cchoff, ncls, w);
+    const u64 chunk = w - cchoff[m];
+    const u32 g = cpiv[m];
+    const u64 mask = cmask[m];
+    const u64 idx = v.goff[g] + chunk * RDF_WAVE + lane_id();
+    bool keep = false;
+    u32 r = 0;
+    if (idx < v.goff[g + 1]) {
+        r = v.gcap[idx];
+        keep = (v.info[r].hmask & mask) == mask;
+        if (keep && v.mode == RULES_CLEAN) keep = !r3_dropped_for_mask(v, r, mask);
+    }
+    const u64 kept = __ballot(keep);
+    if (!WRITE) {
+        if (lane_id() == 0) counts[w] = (u32)__popcll(kept);
+    } else if (keep) {
+        lists[woff[w] + __popcll(kept & lanemask_lt())] = r;
+    }
+}
+
+// per member dependent: position of itself in L'(m) (or NONE) and its output count
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_members(const u64* __restrict__ keys, u64 nkeys,
+                                                             const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
+                                                             const u32* __restrict__ lists, u32* selfpos, u32* cnt) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < nkeys; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 m = (u32)(keys[i] >> 32), d = (u32)keys[i];
+        const u64 b = lwoff[cchoff[m]], e = lwoff[cchoff[m + 1]];
+        u64 lo = b, hi = e;
+        while (lo < hi) {
+            u64 mid = (lo + hi) >> 1;
+            if (lists[mid] < d) lo = mid + 1;
+            else hi = mid;
+        }
+        const bool self = lo < e && lists[lo] == d;
+        selfpos[i] = self ? (u32)(lo - b) : NONE32;
+        cnt[i] = (u32)(e - b) - (self ? 1u : 0u);
+    }
+}
+
+// per class: number of emission tiles = ceil(members / CLS_DT) * ceil(|L'| / CLS_LS)
+static constexpr u32 CLS_DT = 16;                    // dependents per tile
+static constexpr u32 CLS_LS = RDF_BLOCK * 4;         // list elements per tile (4 per thread, in registers)
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict__ coff, const u64* __restrict__ cchoff,
+                                                           const u64* __restrict__ lwoff, u32 ncls, u32* ntiles) {
+    for (u64 m = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; m < ncls; m += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = coff[m + 1] - coff[m];
+        const u64 len = lwoff[cchoff[m + 1]] - lwoff[cchoff[m]];
+        ntiles[m] = (u32)(((k + CLS_DT - 1) / CLS_DT) * ((len + CLS_LS - 1) / CLS_LS));
+    }
+}
+
+// streaming emission: each block loads CLS_LS list entries once and writes them for CLS_DT dependents
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict__ keys, const u64* __restrict__ coff,
+                                                          const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
+                                                          const u32* __restrict__ lists, const u64* __restrict__ toff,
+                                                          u32 ncls, const u32* __restrict__ selfpos,
+                                                          const u64* __restrict__ obase, u64 out_base, u64* out) {
+    __shared__ u32 s_m;
+    if (threadIdx.x == 0) s_m = find_dep(toff, ncls, blockIdx.x);
+    __syncthreads();
+    const u32 m = s_m;
+    const u64 lb = lwoff[cchoff[m]], len = lwoff[cchoff[m + 1]] - lb;
+    const u64 nseg = (len + CLS_LS - 1) / CLS_LS;
+    const u64 t = blockIdx.x - toff[m];
+    const u64 dt = t / nseg, seg = t % nseg;
+    const u64 k0 = coff[m] + dt * CLS_DT, k1 = k0 + CLS_DT < coff[m + 1] ? k0 + CLS_DT : coff[m + 1];
+    u32 val[4];
+    u64 pos[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        pos[q] = seg * CLS_LS + (u64)q * RDF_BLOCK + threadIdx.x;
+        val[q] = pos[q] < len ? lists[lb + pos[q]] : 0u;
+    }
+    for (u64 i = k0; i < k1; ++i) {
+        const u64 d = (u32)keys[i];
+        const u32 sp = selfpos[i];
+        const u64 base = out_base + obase[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (pos[q] < len && pos[q] != sp) {
+                const u64 o = base + pos[q] - ((sp != NONE32 && pos[q] > sp) ? 1u : 0u);
+                out[o] = (d << 32) | val[q];
+            }
+        }
+    }
+}
+
 // order-independent checksum of the result set (capture ids, so it is comparable across runs)
 __global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u64* __restrict__ pairs, u64 n, const u32* __restrict__ fcap,
                                                         u64* sum) {

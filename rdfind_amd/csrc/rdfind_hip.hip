@@ -48,6 +48,10 @@ struct rdf_ctx {
 
     // cinds
     DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, out, stage_rows;
+    DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
+    DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
+        ctiles, ctoff;
+    u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
     u64 n_out = 0;
     u64* out_ptr = nullptr;
     std::vector<u32> h_fcap;
@@ -162,7 +166,10 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->out,
-                      &c->stage_rows};
+                      &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
+                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -456,10 +463,15 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
         hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->info.as<CapInfo>(), C, c->csup.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->csup.as<u32>(), c->doff.as<u64>(), C, c->doff.as<u64>() + C, st));
-    HIP_TRY(c, hipMemcpyAsync(c->dcur.p, c->doff.p, (C + 1ull) * 8, hipMemcpyDeviceToDevice, st));
-    if (Jf)
-        hipLaunchKernelGGL(k_dep_scatter, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
-                           c->gid.as<u32>(), Jf, c->dcur.as<u64>(), c->dgrp.as<u32>());
+    if (Jf) {
+        // (capture << 32 | group) keys in fk, sorted with rec_tmp as scratch (both hold >= Jf u64)
+        u64* tk = c->fk.as<u64>();
+        u64* tt = c->rec_tmp.as<u64>();
+        hipLaunchKernelGGL(k_make_tkeys, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
+                           c->gid.as<u32>(), Jf, tk);
+        HIP_TRY(c, radix_sort_u64(c->ws, tk, tt, Jf, 32 + bits_for(C ? C - 1 : 0), st));
+        hipLaunchKernelGGL(k_low32, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, c->dgrp.as<u32>());
+    }
 
     tend(c, RDF_T_GROUPS);
     // heavy groups -> bitmask columns
@@ -565,13 +577,35 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     ENSURE(c, nchh, std::max<u64>(C, 1) * 4);
     ENSURE(c, choffl, (C + 1ull) * 8);
     ENSURE(c, choffh, (C + 1ull) * 8);
+    ENSURE(c, nitl, std::max<u64>(C, 1) * 4);
+    ENSURE(c, itoffl, (C + 1ull) * 8);
+    ENSURE(c, pseg, std::max<u64>(C, 1) * 4);
+    ENSURE(c, psegoff, (C + 1ull) * 8);
+    ENSURE(c, pbest, std::max<u64>(C, 1) * 8);
+    ENSURE(c, pnl, std::max<u64>(C, 1) * 4);
     tbegin(c, RDF_T_PIVOT);
-    if (C)
-        hipLaunchKernelGGL(k_pivot, dim3((unsigned)((C + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK), 0,
-                           st, v, c->pivot.as<u32>(), c->nchl.as<u32>(), c->nchh.as<u32>(), c->info.as<CapInfo>(),
-                           dscal(c, 2));
+    if (C) {
+        hipLaunchKernelGGL(k_pivot_nseg, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), C,
+                           c->pseg.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->pseg.as<u32>(), c->psegoff.as<u64>(), C, c->psegoff.as<u64>() + C, st));
+        HIP_TRY(c, hipMemsetAsync(c->pbest.p, 0xff, (u64)C * 8, st));
+        HIP_TRY(c, hipMemsetAsync(c->pnl.p, 0, (u64)C * 4, st));
+    }
+    tend(c, RDF_T_PIVOT);
+    u64 WS = 0;
+    rdf_status rs0 = C ? read_u64(c, c->psegoff.as<u64>() + C, &WS) : RDF_OK;
+    if (rs0) return rs0;
+    tbegin(c, RDF_T_PIVOT);
+    if (C) {
+        hipLaunchKernelGGL(k_pivot_seg, dim3((unsigned)((WS + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
+                           0, st, v, c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
+        hipLaunchKernelGGL(k_pivot_final, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
+                           c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(),
+                           c->info.as<CapInfo>(), dscal(c, 2));
+    }
     tend(c, RDF_T_PIVOT);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchl.as<u32>(), c->choffl.as<u64>(), C, c->choffl.as<u64>() + C, st));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
     u64 WL = 0, WH = 0;
     rdf_status rs = read_u64(c, c->choffl.as<u64>() + C, &WL);
@@ -580,15 +614,25 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (rs) return rs;
     rs = read_u64(c, dscal(c, 2), &c->heavy_candidates);
     if (rs) return rs;
+    u64 WI = 0;
+    rs = read_u64(c, c->itoffl.as<u64>() + C, &WI);
+    if (rs) return rs;
 
     // light dependents -> explicit raw pairs
     const u64 cap_pairs = std::max<u64>(WL * RDF_WAVE, 1);
     ENSURE(c, epairs, cap_pairs * 8);
     ENSURE(c, epairs_tmp, cap_pairs * 8);
+    ENSURE(c, dead, std::max<u64>(WL, 1) * 8);
+    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, std::max<u64>(WL, 1) * 8, st));
     tbegin(c, RDF_T_LIGHT);
-    if (WL)
-        hipLaunchKernelGGL(k_light, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
-                           0, st, v, c->pivot.as<u32>(), c->choffl.as<u64>(), WL, c->epairs.as<u64>(), dscal(c, 0));
+    if (WI)
+        hipLaunchKernelGGL(k_light, dim3((unsigned)((WI + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
+                           0, st, v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->choffl.as<u64>(), WI, c->dead.as<u64>(),
+                           c->epairs.as<u64>(), dscal(c, 0));
+    if (WI > WL)  // some dependent spans several segments
+        hipLaunchKernelGGL(k_light_final, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffl.as<u64>(), WL, c->dead.as<u64>(),
+                           c->epairs.as<u64>(), dscal(c, 0));
     tend(c, RDF_T_LIGHT);
     rs = read_scalars(c, 1);
     if (rs) return rs;
@@ -601,19 +645,21 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
         if (k != c->epairs.as<u64>()) std::swap(c->epairs, c->epairs_tmp);
     }
     ENSURE(c, eoff, (C + 1ull) * 8);
+    ENSURE(c, ebin, std::max<u64>(C, 1) * 8);
     hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                       c->epairs.as<u64>(), E, C, c->eoff.as<u64>());
+                       c->epairs.as<u64>(), E, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
     tend(c, RDF_T_ESORT);
     c->sort_passes_pairs = (u64)((32 + bits_for(C ? C - 1 : 0) + 7) / 8) * E;
     v.eoff = c->eoff.as<u64>();
     v.epairs = c->epairs.as<u64>();
+    v.ebin = c->ebin.as<u64>();
 
     // heavy-only dependents: count pass
     ENSURE(c, hcounts, std::max<u64>(WH, 1) * 4);
     ENSURE(c, hoff, (WH + 1) * 8);
     tbegin(c, RDF_T_HCOUNT);
     if (WH)
-        hipLaunchKernelGGL((k_heavy<false>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+        hipLaunchKernelGGL((k_heavy<false>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, c->hcounts.as<u32>(),
                            (const u64*)nullptr, (u64)0, (u64*)nullptr);
     tend(c, RDF_T_HCOUNT);
@@ -622,8 +668,87 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     rs = read_u64(c, c->hoff.as<u64>() + WH, &H);
     if (rs) return rs;
 
+    // unary heavy-only dependents: bitmask classes, shared filtered ref lists
+    tbegin(c, RDF_T_CLASS);
+    const u32 Cu = c->Cu;
+    const u64 tcapc = next_pow2(2ull * Cu + 16);
+    ENSURE(c, ctab, tcapc * 8);
+    ENSURE(c, cflag, tcapc * 4);
+    ENSURE(c, ccid, (tcapc + 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->ctab.p, 0, tcapc * 8, st));
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 2 * 8, st));
+    if (Cu)
+        hipLaunchKernelGGL(k_class_insert, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
+                           tcapc - 1, dscal(c, 3));
+    hipLaunchKernelGGL(k_nonzero_flags, dim3(grid_for(tcapc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ctab.as<u64>(),
+                       tcapc, c->cflag.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->cflag.as<u32>(), c->ccid.as<u32>(), tcapc, c->ccid.as<u32>() + tcapc, st));
+    u64 nmem = 0;
+    u32 ncls = 0;
+    rs = read_u64(c, dscal(c, 3), &nmem);
+    if (rs) return rs;
+    rs = read_u32(c, c->ccid.as<u32>() + tcapc, &ncls);
+    if (rs) return rs;
+    u64 HC = 0, NT = 0;
+    if (nmem) {
+        ENSURE(c, ckeys, nmem * 8);
+        ENSURE(c, ckeys_tmp, nmem * 8);
+        hipLaunchKernelGGL(k_class_keys, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
+                           c->ccid.as<u32>(), tcapc - 1, c->ckeys.as<u64>(), dscal(c, 4));
+        {
+            u64* k = c->ckeys.as<u64>();
+            u64* t = c->ckeys_tmp.as<u64>();
+            HIP_TRY(c, radix_sort_u64(c->ws, k, t, nmem, 32 + bits_for(ncls ? ncls - 1 : 0), st));
+            if (k != c->ckeys.as<u64>()) std::swap(c->ckeys, c->ckeys_tmp);
+        }
+        ENSURE(c, coff, (ncls + 1ull) * 8);
+        ENSURE(c, cmask, std::max<u64>(ncls, 1) * 8);
+        ENSURE(c, cpiv, std::max<u64>(ncls, 1) * 4);
+        ENSURE(c, cnch, std::max<u64>(ncls, 1) * 4);
+        ENSURE(c, cchoff, (ncls + 1ull) * 8);
+        hipLaunchKernelGGL(k_class_info, dim3(grid_for(ncls + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                           c->ckeys.as<u64>(), nmem, ncls, c->pivot.as<u32>(), c->coff.as<u64>(), c->cmask.as<u64>(),
+                           c->cpiv.as<u32>(), c->cnch.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cnch.as<u32>(), c->cchoff.as<u64>(), ncls, c->cchoff.as<u64>() + ncls, st));
+        u64 WC = 0;
+        rs = read_u64(c, c->cchoff.as<u64>() + ncls, &WC);
+        if (rs) return rs;
+        ENSURE(c, ccnt, std::max<u64>(WC, 1) * 4);
+        ENSURE(c, lwoff, (WC + 1) * 8);
+        hipLaunchKernelGGL((k_class_filter<false>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
+                           c->ccnt.as<u32>(), (const u64*)nullptr, (u32*)nullptr);
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ccnt.as<u32>(), c->lwoff.as<u64>(), WC, c->lwoff.as<u64>() + WC, st));
+        u64 LT = 0;
+        rs = read_u64(c, c->lwoff.as<u64>() + WC, &LT);
+        if (rs) return rs;
+        ENSURE(c, clists, std::max<u64>(LT, 1) * 4);
+        hipLaunchKernelGGL((k_class_filter<true>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
+                           (u32*)nullptr, c->lwoff.as<u64>(), c->clists.as<u32>());
+        ENSURE(c, cself, nmem * 4);
+        ENSURE(c, cmcnt, nmem * 4);
+        ENSURE(c, cobase, (nmem + 1) * 8);
+        hipLaunchKernelGGL(k_class_members, dim3(grid_for(nmem, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ckeys.as<u64>(),
+                           nmem, c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->cself.as<u32>(),
+                           c->cmcnt.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cmcnt.as<u32>(), c->cobase.as<u64>(), nmem, c->cobase.as<u64>() + nmem, st));
+        ENSURE(c, ctiles, std::max<u64>(ncls, 1) * 4);
+        ENSURE(c, ctoff, (ncls + 1ull) * 8);
+        hipLaunchKernelGGL(k_class_tiles, dim3(grid_for(ncls, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->coff.as<u64>(),
+                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), ncls, c->ctiles.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ctiles.as<u32>(), c->ctoff.as<u64>(), ncls, c->ctoff.as<u64>() + ncls, st));
+        rs = read_u64(c, c->cobase.as<u64>() + nmem, &HC);
+        if (rs) return rs;
+        rs = read_u64(c, c->ctoff.as<u64>() + ncls, &NT);
+        if (rs) return rs;
+    }
+    tend(c, RDF_T_CLASS);
+    c->n_class_members = nmem;
+    c->n_classes = ncls;
+
     // minimality on the explicit pairs, then heavy write pass
-    ENSURE(c, out, std::max<u64>(E + H, 1) * 8);
+    ENSURE(c, out, std::max<u64>(E + H + HC, 1) * 8);
     tbegin(c, RDF_T_RULES);
     if (E)
         hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
@@ -634,16 +759,23 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     const u64 K = c->hscal[1];
     tbegin(c, RDF_T_HWRITE);
     if (WH)
-        hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+        hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, (u32*)nullptr,
                            c->hoff.as<u64>(), K, c->out.as<u64>());
     tend(c, RDF_T_HWRITE);
+    tbegin(c, RDF_T_CEMIT);
+    if (NT)
+        hipLaunchKernelGGL(k_class_emit, dim3((unsigned)NT), dim3(RDF_BLOCK), 0, st, c->ckeys.as<u64>(), c->coff.as<u64>(),
+                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(), ncls,
+                           c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u64>());
+    tend(c, RDF_T_CEMIT);
     HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], c->ev[5]));
-    tcollect(c, RDF_T_PIVOT, RDF_T_HWRITE + 1);
-    c->n_out = K + H;
+    tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS);
+    c->n_out = K + H + HC;
+    c->n_class_out = HC;
     c->out_ptr = c->out.as<u64>();
     // host copies for result decoding
     c->h_fcap.resize(C);
@@ -663,6 +795,9 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
         stats->ms_rules = c->tms[RDF_T_RULES];
         stats->ms_heavy = c->tms[RDF_T_HCOUNT] + c->tms[RDF_T_HWRITE];
         stats->n_heavy_candidates = c->heavy_candidates;
+        stats->n_class_members = c->n_class_members;
+        stats->n_classes = c->n_classes;
+        stats->n_class_cinds = c->n_class_out;
     }
     c->stage = 4;
     return RDF_OK;
