@@ -6,6 +6,16 @@
 
 namespace rdf {
 
+__device__ inline u64 lower_bound_u64(const u64* a, u64 n, u64 key) {
+    u64 lo = 0, hi = n;
+    while (lo < hi) {
+        u64 mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // ================================================================================================
 // K1: unary condition counts  (FrequentConditionPlanner.findFrequentSingleConditions,
 //     ALG/plan/FrequentConditionPlanner.scala:488-508: flatMap 3 x (type, value, 1) -> groupBy.sum)
@@ -427,9 +437,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mask(const u64* __restrict_
 }
 
 // binary captures: components (unary compact ids) and keys; unary captures: parent counts
+// binary captures: components (unary compact ids) and keys; parent edges (component << 32 | binary)
+// are radix-sorted into the parents CSR (no per-unary cursor atomics: s[p=name] has thousands of parents)
 __global__ __launch_bounds__(RDF_BLOCK) void k_binary_info(const u32* __restrict__ fcap, const u32* __restrict__ fidx,
                                                            const u64* __restrict__ bkeys, u32 C, u32 Cu, u32 V,
-                                                           u32* bcomp, u64* bkeyc, u32* pcnt, CapInfo* info) {
+                                                           u32* bcomp, u64* bkeyc, u64* pedges, CapInfo* info) {
     for (u64 c = Cu + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < C; c += (u64)gridDim.x * RDF_BLOCK) {
         u64 key = bkeys[fcap[c] - 6ull * V];
         int bt = bin_key_type(key);
@@ -438,23 +450,22 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_binary_info(const u32* __restrict
         bcomp[2 * (c - Cu)] = c1;
         bcomp[2 * (c - Cu) + 1] = c2;
         bkeyc[c - Cu] = key;
-        atomicAdd(&pcnt[c1], 1u);
-        atomicAdd(&pcnt[c2], 1u);
+        pedges[2 * (c - Cu)] = ((u64)c1 << 32) | c;
+        pedges[2 * (c - Cu) + 1] = ((u64)c2 << 32) | c;
         info[c].meta |= META_BIN;
     }
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_parents_scatter(const u32* __restrict__ bcomp, u32 C, u32 Cu,
-                                                               u64* cursor, u32* plist) {
-    for (u64 c = Cu + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < C; c += (u64)gridDim.x * RDF_BLOCK) {
-        plist[atomicAdd(&cursor[bcomp[2 * (c - Cu)]], 1ull)] = (u32)c;
-        plist[atomicAdd(&cursor[bcomp[2 * (c - Cu) + 1]], 1ull)] = (u32)c;
+// poff[u] = first edge of unary u; plist = low words; META_PARENTS for unary captures with parents
+__global__ __launch_bounds__(RDF_BLOCK) void k_parents_csr(const u64* __restrict__ pedges, u64 npe, u32 Cu, u64* poff,
+                                                           u32* plist, CapInfo* info) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < npe; i += (u64)gridDim.x * RDF_BLOCK)
+        plist[i] = (u32)pedges[i];
+    for (u64 u = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; u <= Cu; u += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 lo = lower_bound_u64(pedges, npe, u << 32);
+        poff[u] = lo;
+        if (u < Cu && lo < npe && (u32)(pedges[lo] >> 32) == u) info[u].meta |= META_PARENTS;
     }
-}
-
-__global__ __launch_bounds__(RDF_BLOCK) void k_parent_meta(const u32* __restrict__ pcnt, u32 Cu, CapInfo* info) {
-    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < Cu; c += (u64)gridDim.x * RDF_BLOCK)
-        if (pcnt[c]) info[c].meta |= META_PARENTS;
 }
 
 // ================================================================================================
@@ -726,16 +737,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_final(CindView v, const u32
 }
 
 // explicit CSR offsets: eoff[d] = first pair with dep >= d
-__device__ inline u64 lower_bound_u64(const u64* a, u64 n, u64 key) {
-    u64 lo = 0, hi = n;
-    while (lo < hi) {
-        u64 mid = (lo + hi) >> 1;
-        if (a[mid] < key) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
 // ebin[d] = first explicit pair of d with a binary ref (ref >= Cu)
 __global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restrict__ pairs, u64 E, u32 C, u32 Cu, u64* eoff,
                                                             u64* ebin) {

@@ -52,6 +52,7 @@ struct rdf_ctx {
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
         ctiles, ctoff;
     u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
+    DevBuf pedges, pedges_tmp;
     u64 n_out = 0;
     u64* out_ptr = nullptr;
     std::vector<u32> h_fcap;
@@ -169,7 +170,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
-                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff};
+                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -511,19 +512,19 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     ENSURE(c, poff, (Cu + 1ull) * 8);
     ENSURE(c, pcur, (Cu + 1ull) * 8);
     ENSURE(c, plist, std::max<u64>(2ull * Cb, 1) * 4);
-    HIP_TRY(c, hipMemsetAsync(c->pcnt.p, 0, std::max<u64>(Cu, 1) * 4, st));
-    if (Cb)
+    ENSURE(c, pedges, std::max<u64>(2ull * Cb, 1) * 8);
+    ENSURE(c, pedges_tmp, std::max<u64>(2ull * Cb, 1) * 8);
+    if (Cb) {
         hipLaunchKernelGGL(k_binary_info, dim3(grid_for(Cb, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fcap.as<u32>(),
                            c->fidx.as<u32>(), c->bkeys.as<u64>(), C, Cu, V, c->bcomp.as<u32>(), c->bkeyc.as<u64>(),
-                           c->pcnt.as<u32>(), c->info.as<CapInfo>());
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->pcnt.as<u32>(), c->poff.as<u64>(), Cu, c->poff.as<u64>() + Cu, st));
-    HIP_TRY(c, hipMemcpyAsync(c->pcur.p, c->poff.p, (Cu + 1ull) * 8, hipMemcpyDeviceToDevice, st));
-    if (Cb)
-        hipLaunchKernelGGL(k_parents_scatter, dim3(grid_for(Cb, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->bcomp.as<u32>(),
-                           C, Cu, c->pcur.as<u64>(), c->plist.as<u32>());
-    if (Cu)
-        hipLaunchKernelGGL(k_parent_meta, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pcnt.as<u32>(), Cu,
-                           c->info.as<CapInfo>());
+                           c->pedges.as<u64>(), c->info.as<CapInfo>());
+        u64* k = c->pedges.as<u64>();
+        u64* t = c->pedges_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, 2ull * Cb, 32 + bits_for(Cu ? Cu - 1 : 0), st));
+        if (k != c->pedges.as<u64>()) std::swap(c->pedges, c->pedges_tmp);
+    }
+    hipLaunchKernelGGL(k_parents_csr, dim3(grid_for(std::max<u64>(2ull * Cb, Cu + 1ull), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0,
+                       st, c->pedges.as<u64>(), 2ull * Cb, Cu, c->poff.as<u64>(), c->plist.as<u32>(), c->info.as<CapInfo>());
     HIP_TRY(c, hipGetLastError());
     tend(c, RDF_T_HEAVYMASK);
     HIP_TRY(c, hipEventRecord(c->ev[3], st));
