@@ -8,9 +8,11 @@ dictionary-encoded triples already resident in HBM and the CIND id-records left 
 PCIe-inclusive rate is reported separately in DESIGN.md).  Workload: BASELINE configs[1] =
 LUBM-100-shaped synthetic triples (~13.4M), support 10, one MI355X.
 
-For N > 1 (launched by torch.distributed.run) every rank runs its own LUBM-100-shaped replica on its
-own GPU (weak scaling, no data-path collective); `value` is the triples of all ranks divided by the
-max-over-ranks time.  `roofline` is computed for the dominant kernel family from HIP events recorded on
+For N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL over xGMI) the SAME workload is
+sharded (rdfind_amd/distributed.py): every rank holds the triples, owns the capture groups
+of its join-value hash shard and the dependents d % N, and the eight collectives of the protocol run
+inside the timed region.  `value` is the workload's triples divided by the max-over-ranks time per
+step (strong scaling).  `roofline` is computed for the dominant kernel family from HIP events recorded on
 the library's stream; `cpu_baseline` times the C restatement (oracle/) on a bounded sample on rank 0.
 """
 from __future__ import annotations
@@ -58,6 +60,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.2)
+    ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
+                    "exchanges, to rehearse several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -68,15 +72,26 @@ def main():
         import torch
         import torch.distributed as dist
 
+        local_rank %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.backend)
 
     from rdfind_amd import _lib, synth
 
-    d = synth.config(args.config, args.scale, seed=None if rank == 0 else 1000 + rank)
+    d = synth.config(args.config, args.scale)  # same seeded workload on every rank
     ms = d.min_support
     ctx = _lib.Context(local_rank)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
+
+    if dist is not None:
+        from rdfind_amd import distributed
+
+        def step():
+            distributed.run_sharded(ctx, ms)
+            return ctx.cinds
+    else:
+        def step():
+            return ctx.run(ms)
 
     def barrier():
         if dist is not None:
@@ -85,13 +100,13 @@ def main():
             torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        ctx.run(ms)
+        step()
     ctx.sync()
     barrier()
     kt_sum = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        cs = ctx.run(ms)
+        cs = step()
         for k, v in ctx.kernel_times().items():
             kt_sum[k] = kt_sum.get(k, 0.0) + v
     ctx.sync()
@@ -99,14 +114,16 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dev = f"cuda:{local_rank}" if args.backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([float(d.n)], device=f"cuda:{local_rank}", dtype=torch.float64)
+        tot = torch.tensor([cs["n_cinds"]], device=dev, dtype=torch.int64)
         dist.all_reduce(tot)
-        total_triples = float(tot.item())
+        total_cinds = int(tot.item())
     else:
-        total_triples = float(d.n)
+        total_cinds = cs["n_cinds"]
+    total_triples = float(d.n)
     steps = max(args.steps, 1)
     ms_per_step = elapsed * 1000.0 / steps
     value = total_triples * steps / elapsed
@@ -147,11 +164,11 @@ def main():
         line = {
             "metric": "CIND-discovery triples/sec", "value": round(value, 1), "unit": "triples/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": f"{args.config} ({'LUBM-100-shaped' if args.config == 'c2' else args.config}, "
                                    f"scale {args.scale}, support {ms}, strategy 1 --use-fis --clean-implied)",
-                       "triples_per_gpu": d.n, "global_triples": int(total_triples), "cinds": cs["n_cinds"],
-                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+                       "triples": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
+                       "parallelism": f"join-hash shards x{world} (RCCL)" if world > 1 else "single"},
             "roofline": roof, "cpu_baseline": cpu,
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
         }

@@ -144,6 +144,52 @@ rdf_status rdf_decode_capture(rdf_ctx* ctx, uint32_t capture, uint32_t* code, ui
 rdf_status rdf_binary_key_count(rdf_ctx* ctx, uint64_t* n);
 rdf_status rdf_copy_binary_keys(rdf_ctx* ctx, uint64_t* out, uint64_t cap);
 
+/* Statistics of the last completed run (single-GPU or sharded). */
+rdf_status rdf_last_stats(rdf_ctx* ctx, rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs);
+
+/*
+ * Sharded multi-GPU mode (the reference's --dop parallelism over Flink task slots).
+ * Every rank holds all triples; rank r owns the capture groups of the join values with
+ * hash(join) % nranks == r, and the dependents d with d % nranks == r.  The library stops at every
+ * collective and describes it in an rdf_exchange; the caller performs it (torch.distributed over RCCL,
+ * see rdfind_amd/distributed.py) and hands the result back:
+ *
+ *     rdf_shard_begin(ctx, rank, nranks, min_support, projection, flags);
+ *     for (;;) {
+ *         rdf_shard_step(ctx, &x);               // runs device work up to the next collective
+ *         if (x.op == RDF_X_DONE) break;
+ *         rdf_shard_export(ctx, send);           // x.count elements of x.elem_bytes (device or host memory)
+ *         ... collective(send -> recv) ...
+ *         rdf_shard_import(ctx, recv, n_recv);   // all-reduce: x.count; all-gather: concatenation in rank
+ *     }                                          // order; all-to-all: concatenation of what each rank sent here
+ *
+ * Afterwards rdf_cind_count / rdf_copy_cinds* return this rank's CINDs (those of its own dependents);
+ * the union over ranks equals the single-GPU result.  Replaces the reference's hash-partitioned
+ * shuffles between the capture-group, candidate-merging and minimality operators
+ * (ALG/plan/AllAtOnceTraversalStrategy.scala:62-65 combine, ALG/plan/TraversalStrategy.scala:126-168).
+ */
+#define RDF_MAX_RANKS 64
+enum {
+    RDF_X_DONE = 0,
+    RDF_X_ALLREDUCE_SUM_U32 = 1,   /* element-wise sum, uint32 */
+    RDF_X_ALLREDUCE_SUM_U64 = 2,   /* element-wise sum, uint64 */
+    RDF_X_ALLREDUCE_MIN_U64 = 3,   /* element-wise minimum, values < 2^63 */
+    RDF_X_ALLGATHERV_U64 = 4,      /* variable-length all-gather, uint64 */
+    RDF_X_ALLTOALLV_U64 = 5        /* variable-length all-to-all, uint64; send_counts per destination */
+};
+typedef struct {
+    int32_t op;
+    uint32_t elem_bytes;
+    uint64_t count;                          /* elements this rank contributes */
+    uint64_t send_counts[RDF_MAX_RANKS];     /* RDF_X_ALLTOALLV_U64: elements for rank r, consecutive */
+} rdf_exchange;
+
+rdf_status rdf_shard_begin(rdf_ctx* ctx, uint32_t rank, uint32_t nranks, uint32_t min_support, const char* projection,
+                           uint32_t flags);
+rdf_status rdf_shard_step(rdf_ctx* ctx, rdf_exchange* x);
+rdf_status rdf_shard_export(rdf_ctx* ctx, void* dst);
+rdf_status rdf_shard_import(rdf_ctx* ctx, const void* src, uint64_t count);
+
 /* Device time (ms) of the last call of each stage: [0] fc, [1] groups, [2] cinds. */
 rdf_status rdf_stage_times(rdf_ctx* ctx, float* ms3);
 /* Device time (ms) of each kernel family (RDF_T_*) in the last calls; count <= RDF_NUM_TIMERS. */

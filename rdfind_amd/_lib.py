@@ -24,8 +24,13 @@ EXPORTED_SYMBOLS = (
     "rdf_set_triples_device", "rdf_frequent_conditions", "rdf_build_capture_groups", "rdf_discover_cinds",
     "rdf_run", "rdf_cind_count", "rdf_copy_cinds", "rdf_decode_capture", "rdf_binary_key_count",
     "rdf_copy_binary_keys", "rdf_stage_times", "rdf_kernel_times", "rdf_sync",
-    "rdf_copy_cinds_range", "rdf_cind_checksum",
+    "rdf_copy_cinds_range", "rdf_cind_checksum", "rdf_last_stats", "rdf_shard_begin", "rdf_shard_step",
+    "rdf_shard_export", "rdf_shard_import",
 )
+
+# rdf_exchange ops (sharded mode, include/rdfind_hip.h)
+X_DONE, X_ALLREDUCE_SUM_U32, X_ALLREDUCE_SUM_U64, X_ALLREDUCE_MIN_U64, X_ALLGATHERV_U64, X_ALLTOALLV_U64 = range(6)
+MAX_RANKS = 64
 
 # RDF_T_* kernel-family timers (include/rdfind_hip.h)
 TIMER_NAMES = ("unary", "binary", "emit", "sort", "support", "groups", "heavymask", "pivot", "light", "esort",
@@ -51,6 +56,22 @@ class CindStats(ctypes.Structure):
                 ("ms_pivot", ctypes.c_float), ("ms_light", ctypes.c_float), ("ms_rules", ctypes.c_float),
                 ("ms_heavy", ctypes.c_float), ("n_heavy_candidates", ctypes.c_uint64),
                 ("n_class_members", ctypes.c_uint64), ("n_classes", ctypes.c_uint64), ("n_class_cinds", ctypes.c_uint64)]
+
+
+class Exchange(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("elem_bytes", ctypes.c_uint32), ("count", ctypes.c_uint64),
+                ("send_counts", ctypes.c_uint64 * MAX_RANKS)]
+
+
+class ExchangeRequest:
+    """A collective the sharded library asks its caller to perform (see rdfind_amd/distributed.py)."""
+
+    def __init__(self, op: int, elem_bytes: int, count: int, send_counts=None):
+        self.op, self.elem_bytes, self.count = op, elem_bytes, count
+        self.send_counts = list(send_counts or [])
+
+    def __repr__(self):
+        return f"ExchangeRequest(op={self.op}, count={self.count}, send_counts={self.send_counts})"
 
 
 CIND_DTYPE = np.dtype([("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])
@@ -93,6 +114,11 @@ def load():
         "rdf_sync": (i32, [P]),
         "rdf_copy_cinds_range": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_cind_checksum": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_last_stats": (i32, [P, ctypes.POINTER(FcStats), ctypes.POINTER(GroupStats), ctypes.POINTER(CindStats)]),
+        "rdf_shard_begin": (i32, [P, u32, u32, u32, ctypes.c_char_p, u32]),
+        "rdf_shard_step": (i32, [P, ctypes.POINTER(Exchange)]),
+        "rdf_shard_export": (i32, [P, P]),
+        "rdf_shard_import": (i32, [P, P, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -188,6 +214,32 @@ class Context:
 
     def sync(self):
         self._check(self.lib.rdf_sync(self.ptr), "rdf_sync")
+
+    def last_stats(self):
+        fc, gs, cs = FcStats(), GroupStats(), CindStats()
+        self._check(self.lib.rdf_last_stats(self.ptr, ctypes.byref(fc), ctypes.byref(gs), ctypes.byref(cs)),
+                    "rdf_last_stats")
+        self.fc, self.groups, self.cinds = _struct_dict(fc), _struct_dict(gs), _struct_dict(cs)
+        return self.groups, self.cinds
+
+    # -- sharded mode (driven by rdfind_amd.distributed.run_sharded) ---------------------------
+    def shard_begin(self, rank: int, nranks: int, min_support: int, projection="spo", clean_implied=True,
+                    traversal_strategy=1):
+        flags = (RDF_CLEAN_IMPLIED if clean_implied else 0) | (RDF_STRATEGY_ALL_AT_ONCE if traversal_strategy == 0 else 0)
+        self._nranks = nranks
+        self._check(self.lib.rdf_shard_begin(self.ptr, rank, nranks, min_support, projection.encode(), flags),
+                    "rdf_shard_begin")
+
+    def shard_step(self) -> ExchangeRequest:
+        x = Exchange()
+        self._check(self.lib.rdf_shard_step(self.ptr, ctypes.byref(x)), "rdf_shard_step")
+        return ExchangeRequest(x.op, x.elem_bytes, x.count, list(x.send_counts)[: self._nranks])
+
+    def shard_export(self, dst_ptr: int):
+        self._check(self.lib.rdf_shard_export(self.ptr, dst_ptr), "rdf_shard_export")
+
+    def shard_import(self, src_ptr: int, count: int):
+        self._check(self.lib.rdf_shard_import(self.ptr, src_ptr, count), "rdf_shard_import")
 
     def stage_times(self):
         arr = (ctypes.c_float * 3)()

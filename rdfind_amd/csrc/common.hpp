@@ -37,6 +37,11 @@ __host__ __device__ inline u64 mix64(u64 x) {
     return x;
 }
 
+// owner rank of a join value (capture groups are sharded by join-value hash)
+__host__ __device__ inline u32 shard_of(u32 join, u32 nranks) {
+    return nranks <= 1 ? 0u : (u32)((((u64)join * 0x9E3779B97F4A7C15ull) >> 32) % nranks);
+}
+
 __device__ inline u32 hash32(u32 x) {
     x ^= x >> 16;
     x *= 0x7feb352dU;

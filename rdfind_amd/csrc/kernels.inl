@@ -245,7 +245,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             const u32* __restrict__ o, u64 n, u32 V, u32 ms,
                                                             const u32* __restrict__ cnt, const u64* __restrict__ lkeys,
                                                             const u32* __restrict__ lvals, u64 lmask, int proj,
-                                                            int capbits, u64* out, u64* counter) {
+                                                            int capbits, u32 rank, u32 nranks, u64* out, u64* counter) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
     __shared__ u64 lds_base;
     const u64 stride = (u64)gridDim.x * RDF_BLOCK;
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
             const u32 ts = s[i], tp = p[i], to = o[i];
             bool fs, fp, fo;
             freq_flags(cnt, V, ms, ts, tp, to, fs, fp, fo);
-            if (proj & 4) {  // project objects: o[s], o[p], o[s,p]
+            if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s], o[p], o[s,p]
                 const u64 j = (u64)to << capbits;
                 if (fs) rec[c++] = j | (4ull * V + ts);
                 if (fp) rec[c++] = j | (5ull * V + tp);
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                     if (b != NONE32) rec[c++] = j | (B6 + b);
                 }
             }
-            if (proj & 2) {  // project predicates: p[s], p[o], p[s,o]
+            if ((proj & 2) && shard_of(tp, nranks) == rank) {  // project predicates: p[s], p[o], p[s,o]
                 const u64 j = (u64)tp << capbits;
                 if (fs) rec[c++] = j | (2ull * V + ts);
                 if (fo) rec[c++] = j | (3ull * V + to);
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                     if (b != NONE32) rec[c++] = j | (B6 + b);
                 }
             }
-            if (proj & 1) {  // project subjects: s[p], s[o], s[p,o]
+            if ((proj & 1) && shard_of(ts, nranks) == rank) {  // project subjects: s[p], s[o], s[p,o]
                 const u64 j = (u64)ts << capbits;
                 if (fp) rec[c++] = j | (0ull * V + tp);
                 if (fo) rec[c++] = j | (1ull * V + to);
@@ -389,6 +389,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_make_tkeys(const u32* __restrict_
         out[i] = ((u64)gcap[i] << 32) | gid[i];
 }
 
+// offsets of a sorted (id << 32 | x) key array: off[d] = first key with id >= d, d in [0, C]
+__global__ __launch_bounds__(RDF_BLOCK) void k_key_offsets(const u64* __restrict__ keys, u64 n, u32 C, u64* off) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d <= C; d += (u64)gridDim.x * RDF_BLOCK)
+        off[d] = lower_bound_u64(keys, n, d << 32);
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_low32(const u64* __restrict__ keys, u64 n, u32* out) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) out[i] = (u32)keys[i];
 }
@@ -411,15 +417,15 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_size_hist(const u64* __rest
     if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restrict__ goff, u64 G, u64 threshold, u32* nheavy,
-                                                            u32* heavy_list, uint8_t* hbit) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restrict__ goff, u64 G, u64 threshold, u32 base,
+                                                            u32* nheavy, u32* heavy_list, uint8_t* hbit) {
     for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
         u64 sz = goff[g + 1] - goff[g];
         uint8_t b = LIGHT;
         if (threshold && sz >= threshold) {
             u32 j = atomicAdd(nheavy, 1u);
-            if (j < (u32)HMAX) {
-                b = (uint8_t)j;
+            if (base + j < (u32)HMAX) {
+                b = (uint8_t)(base + j);
                 heavy_list[j] = (u32)g;
             }
         }
@@ -428,12 +434,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restric
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mask(const u64* __restrict__ goff, const u32* __restrict__ gcap,
-                                                          const u32* __restrict__ heavy_list, CapInfo* info) {
+                                                          const u32* __restrict__ heavy_list, u32 base, CapInfo* info) {
     const u32 h = blockIdx.y;
     const u32 g = heavy_list[h];
     const u64 b = goff[g], e = goff[g + 1];
     for (u64 i = b + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < e; i += (u64)gridDim.x * RDF_BLOCK)
-        atomicOr(&info[gcap[i]].hmask, 1ull << h);
+        atomicOr(&info[gcap[i]].hmask, 1ull << (base + h));
 }
 
 // binary captures: components (unary compact ids) and keys; unary captures: parent counts
@@ -747,15 +753,16 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restric
 }
 
 // minimality on explicit pairs -> output
-__global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const u64* __restrict__ pairs, u64 E, u64* out,
-                                                              u64* nout) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const u64* __restrict__ pairs, u64 E, u32 rank,
+                                                              u32 nranks, u64* out, u64* nout) {
     const u64 n_round = (E + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n_round; i += (u64)gridDim.x * RDF_BLOCK) {
         u32 keep = 0;
         u64 pr = 0;
         if (i < E) {
             pr = pairs[i];
-            keep = rule_keep(v, (u32)(pr >> 32), (u32)pr) ? 1u : 0u;
+            const u32 d = (u32)(pr >> 32);
+            keep = (d % nranks == rank && rule_keep(v, d, (u32)pr)) ? 1u : 0u;
         }
         u64 pos = wave_append(nout, keep);
         if (keep) out[pos] = pr;
@@ -849,12 +856,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_nonzero_flags(const u64* __restri
 
 // (class << 32 | dep) keys for all unary heavy-only dependents
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_keys(CindView v, const u64* __restrict__ tkeys, const u32* __restrict__ cid,
-                                                          u64 tmask, u64* out, u64* counter) {
+                                                          u64 tmask, u32 rank, u32 nranks, u64* out, u64* counter) {
     const u64 n_round = ((u64)v.Cu + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
         u32 want = 0;
         u64 key = 0;
-        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY)) {
+        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY) && (u32)d % nranks == rank) {
             const u64 m = v.info[d].hmask;
             u64 h = mix64(m) & tmask;
             while (tkeys[h] != m) h = (h + 1) & tmask;
@@ -887,7 +894,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_info(CindView v, const u64*
 template <bool WRITE>
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_filter(CindView v, const u64* __restrict__ cchoff, u32 ncls,
                                                             u64 W, const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
-                                                            u32* counts, const u64* __restrict__ woff, u32* lists) {
+                                                            u32* counts, const u64* __restrict__ woff, u32* lists,
+                                                            u64* cpairs) {
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 m = find_dep(cchoff, ncls, w);
@@ -906,7 +914,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_filter(CindView v, const u6
     if (!WRITE) {
         if (lane_id() == 0) counts[w] = (u32)__popcll(kept);
     } else if (keep) {
-        lists[woff[w] + __popcll(kept & lanemask_lt())] = r;
+        const u64 o = woff[w] + __popcll(kept & lanemask_lt());
+        if (cpairs) cpairs[o] = ((u64)m << 32) | r;  // sharded mode: (class, ref) pairs for the all-gather
+        else lists[o] = r;
     }
 }
 
@@ -989,5 +999,160 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u64* __restrict__ 
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, RDF_WAVE);
     if (lane_id() == 0 && acc) atomicAdd(sum, acc);
+}
+// ================================================================================================
+// Sharded mode: capture groups partitioned by join-value hash over R ranks.  Global
+// quantities (supports, group-size histogram, heavy masks, pivot sizes, light-group counts) are combined
+// by the caller's collectives; light dependents' local survivors are routed to the dependent's owner
+// (dep % R), which keeps a ref iff every rank holding a light group of the dependent reported it.
+
+// MIN-allreduce keys of the local pivot: (size << 32 | rank), INT64_MAX where the rank has no group
+__global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __restrict__ best, u32 C, u32 rank, u64* out) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 b = best[d];
+        out[d] = b == ~0ull ? 0x7fffffffffffffffull : ((b >> 32) << 32) | rank;
+    }
+}
+
+// SUM-allreduce word of the local light-group count: nlight | (nlight > 0) << 40
+__global__ __launch_bounds__(RDF_BLOCK) void k_shard_light_words(const u32* __restrict__ nl, u32 C, u64* out) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
+        out[d] = (u64)nl[d] | ((u64)(nl[d] != 0) << 40);
+}
+
+// pivot final, sharded: the pivot is the rank-local smallest group; light dependents verify their local
+// light groups; a heavy-only dependent (no light group on any rank) is handled by the rank holding its
+// globally smallest group.  nrl[d] = ranks holding a light group of d.
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, const u64* __restrict__ best_in,
+                                                                 const u32* __restrict__ nlight_in,
+                                                                 const u64* __restrict__ gbest, const u64* __restrict__ glight,
+                                                                 u32 rank, u32* pivot, u32* nchunk_light, u32* nitem_light,
+                                                                 u32* nchunk_heavy, u32* nrl, CapInfo* info,
+                                                                 u64* heavy_candidates) {
+    const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
+        u32 hc = 0;
+        if (d < v.C) {
+            const u64 best = best_in[d];
+            const u32 nlight = nlight_in[d];
+            const u64 gl = glight[d];
+            const bool heavy_only = (gl & ((1ull << 40) - 1)) == 0;
+            const bool holder = (u32)gbest[d] == rank && best != ~0ull;
+            const u64 sz = best == ~0ull ? 0 : best >> 32;
+            const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
+            pivot[d] = (u32)(best & 0xffffffffu);
+            nchunk_light[d] = nlight ? nch : 0;
+            nitem_light[d] = nlight ? nch * (u32)((v.doff[d + 1] - v.doff[d] + LIGHT_SEG - 1) / LIGHT_SEG) : 0;
+            nchunk_heavy[d] = (heavy_only && d >= v.Cu && holder) ? nch : 0;
+            nrl[d] = (u32)(gl >> 40);
+            if (heavy_only) {
+                info[d].meta |= META_HEAVY_ONLY;
+                if (d >= v.Cu && holder) hc = (u32)sz;
+            }
+        }
+        u64 tot = wave_inclusive_scan64(hc);
+        tot = __shfl(tot, RDF_WAVE - 1, RDF_WAVE);
+        if (lane_id() == 0 && tot) atomicAdd(heavy_candidates, tot);
+    }
+}
+
+// (dep << 32 | ref) -> (owner << 2cb | dep << cb | ref), so one radix sort groups the pairs by owner
+__global__ __launch_bounds__(RDF_BLOCK) void k_owner_pack(u64* pairs, u64 n, u32 nranks, int cb) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 pr = pairs[i];
+        const u64 d = pr >> 32, r = pr & 0xffffffffull;
+        pairs[i] = ((d % nranks) << (2 * cb)) | (d << cb) | r;
+    }
+}
+
+// first packed pair of each owner (bounds[R] = n)
+__global__ __launch_bounds__(RDF_BLOCK) void k_owner_bounds(const u64* __restrict__ pairs, u64 n, int cb, u32 nranks,
+                                                            u64* bounds) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= nranks; i += (u64)gridDim.x * RDF_BLOCK)
+        bounds[i] = lower_bound_u64(pairs, n, (u64)i << (2 * cb));
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_owner_strip(u64* pairs, u64 n, int cb) {
+    const u64 m = (1ull << cb) - 1;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = pairs[i];
+        pairs[i] = (((k >> cb) & m) << 32) | (k & m);
+    }
+}
+
+// owner side: sorted reported pairs; keep the first of each run whose length equals the number of
+// ranks that hold a light group of the dependent (each rank reports a pair at most once)
+__global__ __launch_bounds__(RDF_BLOCK) void k_mult_flags(const u64* __restrict__ a, u64 n, const u32* __restrict__ nrl,
+                                                          u32* flags) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = a[i];
+        u32 f = 0;
+        if (i == 0 || a[i - 1] != k) {
+            const u32 need = nrl[k >> 32];
+            f = (need >= 1 && i + need - 1 < n && a[i + need - 1] == k) ? 1u : 0u;
+        }
+        flags[i] = f;
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_compact_u64(const u64* __restrict__ a, u64 n, const u32* __restrict__ flags,
+                                                           const u64* __restrict__ pos, u64* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        if (flags[i]) out[pos[i]] = a[i];
+}
+
+// mask classes with deterministic ids: masks sorted ascending, id = rank in that order
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_rank(const u64* __restrict__ tkeys, u64 tmask,
+                                                          const u64* __restrict__ smask, u32 ncls, u32* cid) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < ncls; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 m = smask[i];
+        u64 h = mix64(m) & tmask;
+        while (tkeys[h] != m) h = (h + 1) & tmask;
+        cid[h] = (u32)i;
+    }
+}
+
+// per class: owned-member offsets and mask
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_info_shard(const u64* __restrict__ keys, u64 nkeys, u32 ncls,
+                                                                const u64* __restrict__ smask, u64* coff, u64* cmask) {
+    for (u64 m = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; m <= ncls; m += (u64)gridDim.x * RDF_BLOCK) {
+        coff[m] = lower_bound_u64(keys, nkeys, m << 32);
+        if (m < ncls) cmask[m] = smask[m];
+    }
+}
+
+// classes whose pivot group (the globally smallest group of every member) lives on this rank
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_pivot_shard(CindView v, const u64* __restrict__ tkeys, u64 tmask,
+                                                                 const u32* __restrict__ cid, const u32* __restrict__ pivot,
+                                                                 const u64* __restrict__ gbest, u32 rank, u32* cpiv,
+                                                                 u32* cnch) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.Cu; d += (u64)gridDim.x * RDF_BLOCK) {
+        if (!(v.info[d].meta & META_HEAVY_ONLY) || (u32)gbest[d] != rank) continue;
+        const u64 m = v.info[d].hmask;
+        u64 h = mix64(m) & tmask;
+        while (tkeys[h] != m) h = (h + 1) & tmask;
+        const u32 c = cid[h];
+        const u32 g = pivot[d];  // members of a class have the same groups, hence the same pivot
+        cpiv[c] = g;
+        cnch[c] = (u32)((v.goff[g + 1] - v.goff[g] + RDF_WAVE - 1) / RDF_WAVE);
+    }
+}
+
+// gathered (class << 32 | ref) pairs, sorted -> per-class lists; cchoff becomes the identity map
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_lists(const u64* __restrict__ pairs, u64 n, u32 ncls, u32* lists,
+                                                           u64* loff, u64* ident) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) lists[i] = (u32)pairs[i];
+    for (u64 m = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; m <= ncls; m += (u64)gridDim.x * RDF_BLOCK) {
+        loff[m] = lower_bound_u64(pairs, n, m << 32);
+        ident[m] = m;
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_extract_hmask(const CapInfo* __restrict__ info, u32 C, u64* out) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) out[d] = info[d].hmask;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_set_hmask(const u64* __restrict__ in, u32 C, CapInfo* info) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) info[d].hmask = in[d];
 }
 }  // namespace rdf

@@ -53,6 +53,24 @@ struct rdf_ctx {
         ctiles, ctoff;
     u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
     DevBuf pedges, pedges_tmp;
+    u64 ncap = 0;
+    u64 n_explicit_raw = 0, n_light_chunks = 0;
+    rdf_fc_stats fstats = {};
+    rdf_group_stats gstats = {};
+    rdf_cind_stats cstats = {};
+
+    // sharded mode: this rank's share of the join values, and the pending exchange
+    u32 rank = 0, nranks = 1;
+    u32 sh_rank = 0, sh_nranks = 1, sh_ms = 1, sh_flags = 0;
+    int sh_proj = 7, sh_phase = -1;
+    u64 sh_WH = 0, sh_H = 0, sh_E = 0, sh_tcapc = 0;
+    u32 h_hist_local[256] = {};
+    int x_op = RDF_X_DONE;
+    const void* x_src = nullptr;
+    u64 x_count = 0, x_recv_count = 0;
+    u32 x_bytes = 8;
+    bool x_imported = true;
+    DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0;
     u64* out_ptr = nullptr;
     std::vector<u32> h_fcap;
@@ -170,7 +188,9 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
-                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp};
+                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
+                      &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->obounds};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -309,13 +329,12 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
     tcollect(c, RDF_T_UNARY, RDF_T_BINARY + 1);
-    if (stats) {
-        memset(stats, 0, sizeof(*stats));
-        stats->min_support = c->ms;
-        for (int i = 0; i < 3; ++i) stats->n_frequent_unary[i] = nfreq[i];
-        stats->n_binary_keys = nkeys;
-        stats->n_frequent_binary = B;
-    }
+    memset(&c->fstats, 0, sizeof(c->fstats));
+    c->fstats.min_support = c->ms;
+    for (int i = 0; i < 3; ++i) c->fstats.n_frequent_unary[i] = nfreq[i];
+    c->fstats.n_binary_keys = nkeys;
+    c->fstats.n_frequent_binary = B;
+    if (stats) *stats = c->fstats;
     c->stage = 2;
     return RDF_OK;
 }
@@ -343,18 +362,27 @@ static u64 bucket_min_size(int b) {
     return (u64)(4 + frac) << (msb - 2);
 }
 
-rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_group_stats* stats) {
-    if (!c) return RDF_ERR_ARG;
-    if (c->stage < 2) return fail(c, RDF_ERR_STATE, "rdf_frequent_conditions must be called first");
-    HIP_TRY(c, hipSetDevice(c->device));
+static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj) {
     const char* pr = projection ? projection : "spo";
-    int proj = 0;
+    int m = 0;
     for (const char* q = pr; *q; ++q) {
-        if (*q == 's') proj |= 1;
-        else if (*q == 'p') proj |= 2;
-        else if (*q == 'o') proj |= 4;
+        if (*q == 's') m |= 1;
+        else if (*q == 'p') m |= 2;
+        else if (*q == 'o') m |= 4;
         else return fail(c, RDF_ERR_ARG, std::string("invalid projection attribute in '") + pr + "'");
     }
+    *proj = m;
+    return RDF_OK;
+}
+
+#define TRY(expr)                    \
+    do {                             \
+        rdf_status _r = (expr);      \
+        if (_r != RDF_OK) return _r; \
+    } while (0)
+
+// K3 emission of this rank's join shard, K4 sort by (join, capture), K5 local supports -> c->support[ncap]
+static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
@@ -364,10 +392,9 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     if (capbits + joinbits > 64) return fail(c, RDF_ERR_LIMIT, "join+capture bits exceed 64");
     if (ncap >= (1ull << 32)) return fail(c, RDF_ERR_LIMIT, "capture id space exceeds 2^32");
     c->capbits = capbits;
+    c->ncap = ncap;
     HIP_TRY(c, hipEventRecord(c->ev[2], st));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
-
-    // K3 join partners
     const u64 cap_rec = std::max<u64>(9 * n, 1);
     ENSURE(c, rec, cap_rec * 8);
     ENSURE(c, rec_tmp, cap_rec * 8);
@@ -375,14 +402,11 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     if (n)
         hipLaunchKernelGGL(k_emit_records, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n,
                            V, c->ms, c->cnt.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits,
-                           c->rec.as<u64>(), dscal(c, 0));
+                           c->rank, c->nranks, c->rec.as<u64>(), dscal(c, 0));
     tend(c, RDF_T_EMIT);
-    rdf_status rs = read_scalars(c, 1);
-    if (rs) return rs;
+    TRY(read_scalars(c, 1));
     const u64 J = c->hscal[0];
     c->J = J;
-
-    // K4 sort by (join, capture)
     u64* keys = c->rec.as<u64>();
     u64* tmp = c->rec_tmp.as<u64>();
     tbegin(c, RDF_T_SORT);
@@ -390,8 +414,6 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     tend(c, RDF_T_SORT);
     c->rec_sorted = keys;
     c->sort_passes_records = (u64)((capbits + joinbits + 7) / 8) * J;
-
-    // K5 supports (distinct join values per capture)
     ENSURE(c, support, ncap * 4);
     tbegin(c, RDF_T_SUPPORT);
     HIP_TRY(c, hipMemsetAsync(c->support.p, 0, ncap * 4, st));
@@ -399,41 +421,47 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     if (J)
         hipLaunchKernelGGL(k_unique_support, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capmask,
                            c->support.as<u32>());
+    tend(c, RDF_T_SUPPORT);
+    return RDF_OK;
+}
+
+// frequent-capture compaction (c->support = global supports), capture groups, dependent -> groups CSR
+static rdf_status g_compact_groups(rdf_ctx* c) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 ncap = c->ncap, J = c->J;
+    const int capbits = c->capbits;
+    const u64 capmask = (capbits >= 64) ? ~0ull : ((1ull << capbits) - 1);
+    u64* keys = c->rec_sorted;
+    tbegin(c, RDF_T_SUPPORT);
     ENSURE(c, flags, std::max(J, ncap) * 4);
     ENSURE(c, fidx, (ncap + 1) * 4);
     hipLaunchKernelGGL(k_support_flags, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fidx.as<u32>(), ncap, c->fidx.as<u32>() + ncap, st));
     u32 C = 0, Cu = 0;
-    rs = read_u32(c, c->fidx.as<u32>() + ncap, &C);
-    if (rs) return rs;
-    rs = read_u32(c, c->fidx.as<u32>() + 6ull * V, &Cu);
-    if (rs) return rs;
+    TRY(read_u32(c, c->fidx.as<u32>() + ncap, &C));
+    TRY(read_u32(c, c->fidx.as<u32>() + 6ull * V, &Cu));
     c->C = C;
     c->Cu = Cu;
     ENSURE(c, fcap, std::max<u64>(C, 1) * 4);
     ENSURE(c, info, std::max<u64>(C, 1) * sizeof(CapInfo));
     hipLaunchKernelGGL(k_compact_captures, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->support.as<u32>(), c->fidx.as<u32>(), ncap, c->ms, c->fcap.as<u32>(), c->info.as<CapInfo>());
-
     // distinct records of frequent captures, capture ids made compact
     ENSURE(c, pos, std::max<u64>(J, 1) * 8);
-    if (J) {
+    if (J)
         hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capmask,
                            c->support.as<u32>(), c->ms, c->flags.as<u32>());
-    }
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), J, dscal(c, 1), st));
-    rs = read_scalars(c, 2);
-    if (rs) return rs;
+    TRY(read_scalars(c, 2));
     const u64 Jf = c->hscal[1];
     c->Jf = Jf;
     ENSURE(c, fk, std::max<u64>(Jf, 1) * 8);
     if (J)
         hipLaunchKernelGGL(k_keep_scatter, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capbits,
                            capmask, c->flags.as<u32>(), c->pos.as<u64>(), c->fidx.as<u32>(), c->fk.as<u64>());
-
     tend(c, RDF_T_SUPPORT);
-    // groups
     tbegin(c, RDF_T_GROUPS);
     ENSURE(c, gflag, std::max<u64>(Jf, 1) * 4);
     ENSURE(c, gexcl, (Jf + 1) * 4);
@@ -442,8 +470,7 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
                            c->gflag.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), Jf, c->gexcl.as<u32>() + Jf, st));
     u32 G32 = 0;
-    rs = read_u32(c, c->gexcl.as<u32>() + Jf, &G32);
-    if (rs) return rs;
+    TRY(read_u32(c, c->gexcl.as<u32>() + Jf, &G32));
     const u64 G = G32;
     c->G = G;
     ENSURE(c, goff, (G + 1) * 8);
@@ -454,63 +481,88 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
                            c->gflag.as<u32>(), c->gexcl.as<u32>(), c->goff.as<u64>(), c->gcap.as<u32>(), c->gid.as<u32>());
     c->hscal[14] = Jf;
     HIP_TRY(c, hipMemcpyAsync(c->goff.as<u64>() + G, c->hscal + 14, 8, hipMemcpyHostToDevice, st));
-
     // dependent -> groups
     ENSURE(c, csup, std::max<u64>(C, 1) * 4);
     ENSURE(c, doff, (C + 1ull) * 8);
-    ENSURE(c, dcur, (C + 1ull) * 8);
     ENSURE(c, dgrp, std::max<u64>(Jf, 1) * 4);
     if (C)
         hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->info.as<CapInfo>(), C, c->csup.as<u32>());
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->csup.as<u32>(), c->doff.as<u64>(), C, c->doff.as<u64>() + C, st));
     if (Jf) {
-        // (capture << 32 | group) keys in fk, sorted with rec_tmp as scratch (both hold >= Jf u64)
+        // (capture << 32 | group) keys in fk, sorted with rec_tmp as scratch (both hold >= Jf u64); the
+        // dependent offsets come from the sorted keys (a sharded rank holds only part of each support)
         u64* tk = c->fk.as<u64>();
         u64* tt = c->rec_tmp.as<u64>();
         hipLaunchKernelGGL(k_make_tkeys, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
                            c->gid.as<u32>(), Jf, tk);
         HIP_TRY(c, radix_sort_u64(c->ws, tk, tt, Jf, 32 + bits_for(C ? C - 1 : 0), st));
         hipLaunchKernelGGL(k_low32, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, c->dgrp.as<u32>());
+        hipLaunchKernelGGL(k_key_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, C,
+                           c->doff.as<u64>());
+    } else {
+        HIP_TRY(c, hipMemsetAsync(c->doff.p, 0, (C + 1ull) * 8, st));
     }
-
     tend(c, RDF_T_GROUPS);
-    // heavy groups -> bitmask columns
+    return RDF_OK;
+}
+
+// local group-size histogram (quarter-octave buckets) -> h_hist (host)
+static rdf_status g_size_hist(rdf_ctx* c, u32* h_hist) {
+    hipStream_t st = c->stream;
     tbegin(c, RDF_T_HEAVYMASK);
     ENSURE(c, hist, 256 * 4 + 64);
     HIP_TRY(c, hipMemsetAsync(c->hist.p, 0, 256 * 4 + 64, st));
-    if (G)
-        hipLaunchKernelGGL(k_group_size_hist, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(),
-                           G, c->hist.as<u32>());
-    std::vector<u32> h_hist(256);
-    HIP_TRY(c, hipMemcpyAsync(h_hist.data(), c->hist.p, 256 * 4, hipMemcpyDeviceToHost, st));
+    if (c->G)
+        hipLaunchKernelGGL(k_group_size_hist, dim3(grid_for(c->G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->goff.as<u64>(), c->G, c->hist.as<u32>());
+    tend(c, RDF_T_HEAVYMASK);
+    HIP_TRY(c, hipMemcpyAsync(h_hist, c->hist.p, 256 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    const u64 kHeavyMin = 64;  // smaller groups are cheaper to verify by binary search than as bit columns
-    int tb = heavy_threshold_from_hist(h_hist.data(), kHeavyMin);
-    u64 thr = tb >= 0 ? std::max<u64>(bucket_min_size(tb), kHeavyMin) : 0;
+    return RDF_OK;
+}
+
+static const u64 kHeavyMin = 64;  // smaller groups are cheaper to verify by binary search than as bit columns
+
+// heavy threshold from the (global) histogram; 0 = no heavy groups
+static u64 heavy_threshold(const u32* hist) {
+    int tb = heavy_threshold_from_hist(hist, kHeavyMin);
+    return tb >= 0 ? std::max<u64>(bucket_min_size(tb), kHeavyMin) : 0;
+}
+
+// groups of a histogram at or above the threshold (exact: kHeavyMin starts a bucket)
+static u64 heavy_count(const u32* hist, u64 thr) {
+    if (!thr) return 0;
+    u64 n = 0;
+    for (int b = size_bucket(thr); b < 256; ++b) n += hist[b];
+    return n;
+}
+
+// heavy groups -> bitmask columns base.. (this rank's), binary components and parents CSR
+static rdf_status g_heavy_binary(rdf_ctx* c, u64 thr, u32 base) {
+    hipStream_t st = c->stream;
+    const u64 G = c->G;
+    const u32 C = c->C, Cu = c->Cu;
+    const u32 V = c->V ? c->V : 1;
+    tbegin(c, RDF_T_HEAVYMASK);
     c->heavy_threshold = thr;
     ENSURE(c, heavy_list, HMAX * 4);
     ENSURE(c, hbit, std::max<u64>(G, 1));
     u32* d_nheavy = c->hist.as<u32>() + 256;
+    HIP_TRY(c, hipMemsetAsync(d_nheavy, 0, 4, st));
     if (G)
         hipLaunchKernelGGL(k_heavy_select, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), G,
-                           thr, d_nheavy, c->heavy_list.as<u32>(), c->hbit.as<uint8_t>());
+                           thr, base, d_nheavy, c->heavy_list.as<u32>(), c->hbit.as<uint8_t>());
     u32 nh = 0;
-    rs = read_u32(c, d_nheavy, &nh);
-    if (rs) return rs;
-    nh = std::min<u32>(nh, HMAX);
+    TRY(read_u32(c, d_nheavy, &nh));
+    nh = base >= (u32)HMAX ? 0 : std::min<u32>(nh, HMAX - base);
     c->nheavy = nh;
     if (nh)
         hipLaunchKernelGGL(k_heavy_mask, dim3(64, nh), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), c->gcap.as<u32>(),
-                           c->heavy_list.as<u32>(), c->info.as<CapInfo>());
-
-    // binary components, parents (unary -> binary captures having it as a component)
+                           c->heavy_list.as<u32>(), base, c->info.as<CapInfo>());
     const u32 Cb = C - Cu;
     ENSURE(c, bcomp, std::max<u64>(2ull * Cb, 1) * 4);
     ENSURE(c, bkeyc, std::max<u64>(Cb, 1) * 8);
-    ENSURE(c, pcnt, std::max<u64>(Cu, 1) * 4);
     ENSURE(c, poff, (Cu + 1ull) * 8);
-    ENSURE(c, pcur, (Cu + 1ull) * 8);
     ENSURE(c, plist, std::max<u64>(2ull * Cb, 1) * 4);
     ENSURE(c, pedges, std::max<u64>(2ull * Cb, 1) * 8);
     ENSURE(c, pedges_tmp, std::max<u64>(2ull * Cb, 1) * 8);
@@ -527,35 +579,54 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
                        st, c->pedges.as<u64>(), 2ull * Cb, Cu, c->poff.as<u64>(), c->plist.as<u32>(), c->info.as<CapInfo>());
     HIP_TRY(c, hipGetLastError());
     tend(c, RDF_T_HEAVYMASK);
-    HIP_TRY(c, hipEventRecord(c->ev[3], st));
-    HIP_TRY(c, hipStreamSynchronize(st));
+    return RDF_OK;
+}
+
+static void fill_group_stats(rdf_ctx* c) {
+    rdf_group_stats& s = c->gstats;
+    memset(&s, 0, sizeof(s));
+    s.n_records = c->J;
+    s.n_frequent_records = c->Jf;
+    s.n_groups = c->G;
+    s.n_captures = c->C;
+    s.n_unary_captures = c->Cu;
+    s.n_heavy_groups = c->nheavy;
+    s.heavy_threshold = c->heavy_threshold;
+}
+
+static rdf_status g_finish(rdf_ctx* c, rdf_group_stats* stats) {
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[1], c->ev[2], c->ev[3]));
     tcollect(c, RDF_T_EMIT, RDF_T_HEAVYMASK + 1);
-    if (stats) {
-        memset(stats, 0, sizeof(*stats));
-        stats->n_records = J;
-        stats->n_frequent_records = Jf;
-        stats->n_groups = G;
-        stats->n_captures = C;
-        stats->n_unary_captures = Cu;
-        stats->n_heavy_groups = nh;
-        stats->heavy_threshold = thr;
-    }
+    fill_group_stats(c);
+    if (stats) *stats = c->gstats;
     c->stage = 3;
     return RDF_OK;
+}
+
+rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_group_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 2) return fail(c, RDF_ERR_STATE, "rdf_frequent_conditions must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    int proj = 0;
+    TRY(parse_projection(c, projection, &proj));
+    c->rank = 0;
+    c->nranks = 1;
+    TRY(g_emit_sort_support(c, proj));
+    TRY(g_compact_groups(c));
+    u32 h_hist[256];
+    TRY(g_size_hist(c, h_hist));
+    TRY(g_heavy_binary(c, heavy_threshold(h_hist), 0));
+    return g_finish(c, stats);
 }
 
 // ------------------------------------------------------------------------------------------------
 // Stage 3: CIND extraction + minimality (TraversalStrategy.enhanceFlinkPlan)
 
-rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats) {
-    if (!c) return RDF_ERR_ARG;
-    if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
-    HIP_TRY(c, hipSetDevice(c->device));
-    hipStream_t st = c->stream;
-    const u32 C = c->C;
+static CindView make_view(rdf_ctx* c, uint32_t flags) {
     CindView v;
-    v.C = C;
+    v.C = c->C;
     v.Cu = c->Cu;
     v.info = c->info.as<CapInfo>();
     v.gcap = c->gcap.as<u32>();
@@ -567,12 +638,20 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     v.bkeyc = c->bkeyc.as<u64>();
     v.poff = c->poff.as<u64>();
     v.plist = c->plist.as<u32>();
+    v.eoff = nullptr;
+    v.epairs = nullptr;
+    v.ebin = nullptr;
     v.literal = (flags & RDF_STRATEGY_ALL_AT_ONCE) ? 1 : 0;
     v.mode = (flags & RDF_CLEAN_IMPLIED) ? RULES_CLEAN : (v.literal ? RULES_NONE : RULES_S2L_RAW);
+    return v;
+}
+
+// local pivot statistics: pbest[d] = (size << 32 | group) of d's smallest local group, pnl[d] = local light groups
+static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
     HIP_TRY(c, hipEventRecord(c->ev[4], st));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
-
-    // pivots and work chunks
     ENSURE(c, pivot, std::max<u64>(C, 1) * 4);
     ENSURE(c, nchl, std::max<u64>(C, 1) * 4);
     ENSURE(c, nchh, std::max<u64>(C, 1) * 4);
@@ -594,37 +673,38 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
-    rdf_status rs0 = C ? read_u64(c, c->psegoff.as<u64>() + C, &WS) : RDF_OK;
-    if (rs0) return rs0;
+    if (C) TRY(read_u64(c, c->psegoff.as<u64>() + C, &WS));
     tbegin(c, RDF_T_PIVOT);
-    if (C) {
+    if (WS)
         hipLaunchKernelGGL(k_pivot_seg, dim3((unsigned)((WS + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
                            0, st, v, c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
-        hipLaunchKernelGGL(k_pivot_final, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
-                           c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(),
-                           c->info.as<CapInfo>(), dscal(c, 2));
-    }
     tend(c, RDF_T_PIVOT);
+    return RDF_OK;
+}
+
+// work-chunk offsets after the pivot final pass
+static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchl.as<u32>(), c->choffl.as<u64>(), C, c->choffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
-    u64 WL = 0, WH = 0;
-    rdf_status rs = read_u64(c, c->choffl.as<u64>() + C, &WL);
-    if (rs) return rs;
-    rs = read_u64(c, c->choffh.as<u64>() + C, &WH);
-    if (rs) return rs;
-    rs = read_u64(c, dscal(c, 2), &c->heavy_candidates);
-    if (rs) return rs;
-    u64 WI = 0;
-    rs = read_u64(c, c->itoffl.as<u64>() + C, &WI);
-    if (rs) return rs;
+    TRY(read_u64(c, c->choffl.as<u64>() + C, WL));
+    TRY(read_u64(c, c->choffh.as<u64>() + C, WH));
+    TRY(read_u64(c, dscal(c, 2), &c->heavy_candidates));
+    TRY(read_u64(c, c->itoffl.as<u64>() + C, WI));
+    return RDF_OK;
+}
 
-    // light dependents -> explicit raw pairs
+// light dependents -> explicit raw (dep << 32 | ref) pairs in epairs (unsorted); *E = count
+static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64* E) {
+    hipStream_t st = c->stream;
     const u64 cap_pairs = std::max<u64>(WL * RDF_WAVE, 1);
     ENSURE(c, epairs, cap_pairs * 8);
     ENSURE(c, epairs_tmp, cap_pairs * 8);
     ENSURE(c, dead, std::max<u64>(WL, 1) * 8);
     HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, std::max<u64>(WL, 1) * 8, st));
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 0), 0, 8, st));
     tbegin(c, RDF_T_LIGHT);
     if (WI)
         hipLaunchKernelGGL(k_light, dim3((unsigned)((WI + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
@@ -635,9 +715,15 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffl.as<u64>(), WL, c->dead.as<u64>(),
                            c->epairs.as<u64>(), dscal(c, 0));
     tend(c, RDF_T_LIGHT);
-    rs = read_scalars(c, 1);
-    if (rs) return rs;
-    const u64 E = c->hscal[0];
+    TRY(read_u64(c, dscal(c, 0), E));
+    return RDF_OK;
+}
+
+// sort the explicit pairs (epairs[0, E)) and index them: v.eoff / v.ebin / v.epairs
+static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
     tbegin(c, RDF_T_ESORT);
     {
         u64* k = c->epairs.as<u64>();
@@ -654,8 +740,12 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     v.eoff = c->eoff.as<u64>();
     v.epairs = c->epairs.as<u64>();
     v.ebin = c->ebin.as<u64>();
+    return RDF_OK;
+}
 
-    // heavy-only dependents: count pass
+// heavy-only binary dependents: count pass -> hoff, *H
+static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
+    hipStream_t st = c->stream;
     ENSURE(c, hcounts, std::max<u64>(WH, 1) * 4);
     ENSURE(c, hoff, (WH + 1) * 8);
     tbegin(c, RDF_T_HCOUNT);
@@ -665,14 +755,16 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
                            (const u64*)nullptr, (u64)0, (u64*)nullptr);
     tend(c, RDF_T_HCOUNT);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->hcounts.as<u32>(), c->hoff.as<u64>(), WH, c->hoff.as<u64>() + WH, st));
-    u64 H = 0;
-    rs = read_u64(c, c->hoff.as<u64>() + WH, &H);
-    if (rs) return rs;
+    TRY(read_u64(c, c->hoff.as<u64>() + WH, H));
+    return RDF_OK;
+}
 
-    // unary heavy-only dependents: bitmask classes, shared filtered ref lists
-    tbegin(c, RDF_T_CLASS);
+// mask-class hash table of the unary heavy-only dependents; *nmem members, *ncls classes, *tcapc table size
+static rdf_status d_class_table(rdf_ctx* c, const CindView& v, u64* nmem, u32* ncls, u64* tcapc_out) {
+    hipStream_t st = c->stream;
     const u32 Cu = c->Cu;
     const u64 tcapc = next_pow2(2ull * Cu + 16);
+    *tcapc_out = tcapc;
     ENSURE(c, ctab, tcapc * 8);
     ENSURE(c, cflag, tcapc * 4);
     ENSURE(c, ccid, (tcapc + 1) * 4);
@@ -684,18 +776,49 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     hipLaunchKernelGGL(k_nonzero_flags, dim3(grid_for(tcapc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ctab.as<u64>(),
                        tcapc, c->cflag.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->cflag.as<u32>(), c->ccid.as<u32>(), tcapc, c->ccid.as<u32>() + tcapc, st));
-    u64 nmem = 0;
+    TRY(read_u64(c, dscal(c, 3), nmem));
+    TRY(read_u32(c, c->ccid.as<u32>() + tcapc, ncls));
+    return RDF_OK;
+}
+
+// class emission tiles (members -> selfpos / output bases; per-class tile offsets); lists at
+// lwoff[cchoff[m]] .. lwoff[cchoff[m+1]]
+static rdf_status d_class_tiles(rdf_ctx* c, u64 nmem, u32 ncls, u64* HC, u64* NT) {
+    hipStream_t st = c->stream;
+    *HC = 0;
+    *NT = 0;
+    if (!nmem) return RDF_OK;
+    ENSURE(c, cself, nmem * 4);
+    ENSURE(c, cmcnt, nmem * 4);
+    ENSURE(c, cobase, (nmem + 1) * 8);
+    hipLaunchKernelGGL(k_class_members, dim3(grid_for(nmem, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ckeys.as<u64>(),
+                       nmem, c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->cself.as<u32>(),
+                       c->cmcnt.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cmcnt.as<u32>(), c->cobase.as<u64>(), nmem, c->cobase.as<u64>() + nmem, st));
+    ENSURE(c, ctiles, std::max<u64>(ncls, 1) * 4);
+    ENSURE(c, ctoff, (ncls + 1ull) * 8);
+    hipLaunchKernelGGL(k_class_tiles, dim3(grid_for(std::max<u32>(ncls, 1), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->coff.as<u64>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(), ncls, c->ctiles.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ctiles.as<u32>(), c->ctoff.as<u64>(), ncls, c->ctoff.as<u64>() + ncls, st));
+    TRY(read_u64(c, c->cobase.as<u64>() + nmem, HC));
+    TRY(read_u64(c, c->ctoff.as<u64>() + ncls, NT));
+    return RDF_OK;
+}
+
+// single-rank class path: table -> keys -> per-class pivot -> filtered lists -> tiles
+static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* NT) {
+    hipStream_t st = c->stream;
+    tbegin(c, RDF_T_CLASS);
+    u64 nmem = 0, tcapc = 0;
     u32 ncls = 0;
-    rs = read_u64(c, dscal(c, 3), &nmem);
-    if (rs) return rs;
-    rs = read_u32(c, c->ccid.as<u32>() + tcapc, &ncls);
-    if (rs) return rs;
-    u64 HC = 0, NT = 0;
+    TRY(d_class_table(c, v, &nmem, &ncls, &tcapc));
+    *HC = 0;
+    *NT = 0;
     if (nmem) {
         ENSURE(c, ckeys, nmem * 8);
         ENSURE(c, ckeys_tmp, nmem * 8);
-        hipLaunchKernelGGL(k_class_keys, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
-                           c->ccid.as<u32>(), tcapc - 1, c->ckeys.as<u64>(), dscal(c, 4));
+        hipLaunchKernelGGL(k_class_keys, dim3(grid_for(c->Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
+                           c->ccid.as<u32>(), tcapc - 1, 0u, 1u, c->ckeys.as<u64>(), dscal(c, 4));
         {
             u64* k = c->ckeys.as<u64>();
             u64* t = c->ckeys_tmp.as<u64>();
@@ -712,52 +835,41 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
                            c->cpiv.as<u32>(), c->cnch.as<u32>());
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cnch.as<u32>(), c->cchoff.as<u64>(), ncls, c->cchoff.as<u64>() + ncls, st));
         u64 WC = 0;
-        rs = read_u64(c, c->cchoff.as<u64>() + ncls, &WC);
-        if (rs) return rs;
+        TRY(read_u64(c, c->cchoff.as<u64>() + ncls, &WC));
         ENSURE(c, ccnt, std::max<u64>(WC, 1) * 4);
         ENSURE(c, lwoff, (WC + 1) * 8);
-        hipLaunchKernelGGL((k_class_filter<false>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
-                           c->ccnt.as<u32>(), (const u64*)nullptr, (u32*)nullptr);
+        if (WC)
+            hipLaunchKernelGGL((k_class_filter<false>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                               dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
+                               c->ccnt.as<u32>(), (const u64*)nullptr, (u32*)nullptr, (u64*)nullptr);
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ccnt.as<u32>(), c->lwoff.as<u64>(), WC, c->lwoff.as<u64>() + WC, st));
         u64 LT = 0;
-        rs = read_u64(c, c->lwoff.as<u64>() + WC, &LT);
-        if (rs) return rs;
+        TRY(read_u64(c, c->lwoff.as<u64>() + WC, &LT));
         ENSURE(c, clists, std::max<u64>(LT, 1) * 4);
-        hipLaunchKernelGGL((k_class_filter<true>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
-                           (u32*)nullptr, c->lwoff.as<u64>(), c->clists.as<u32>());
-        ENSURE(c, cself, nmem * 4);
-        ENSURE(c, cmcnt, nmem * 4);
-        ENSURE(c, cobase, (nmem + 1) * 8);
-        hipLaunchKernelGGL(k_class_members, dim3(grid_for(nmem, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ckeys.as<u64>(),
-                           nmem, c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->cself.as<u32>(),
-                           c->cmcnt.as<u32>());
-        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cmcnt.as<u32>(), c->cobase.as<u64>(), nmem, c->cobase.as<u64>() + nmem, st));
-        ENSURE(c, ctiles, std::max<u64>(ncls, 1) * 4);
-        ENSURE(c, ctoff, (ncls + 1ull) * 8);
-        hipLaunchKernelGGL(k_class_tiles, dim3(grid_for(ncls, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->coff.as<u64>(),
-                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), ncls, c->ctiles.as<u32>());
-        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ctiles.as<u32>(), c->ctoff.as<u64>(), ncls, c->ctoff.as<u64>() + ncls, st));
-        rs = read_u64(c, c->cobase.as<u64>() + nmem, &HC);
-        if (rs) return rs;
-        rs = read_u64(c, c->ctoff.as<u64>() + ncls, &NT);
-        if (rs) return rs;
+        if (WC)
+            hipLaunchKernelGGL((k_class_filter<true>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                               dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
+                               (u32*)nullptr, c->lwoff.as<u64>(), c->clists.as<u32>(), (u64*)nullptr);
+        TRY(d_class_tiles(c, nmem, ncls, HC, NT));
     }
     tend(c, RDF_T_CLASS);
     c->n_class_members = nmem;
     c->n_classes = ncls;
+    return RDF_OK;
+}
 
-    // minimality on the explicit pairs, then heavy write pass
+// K7 minimality on the (owned) explicit pairs, heavy-only binary write pass, class emission -> out
+static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
+    hipStream_t st = c->stream;
     ENSURE(c, out, std::max<u64>(E + H + HC, 1) * 8);
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 1), 0, 8, st));
     tbegin(c, RDF_T_RULES);
     if (E)
         hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
-                           c->epairs.as<u64>(), E, c->out.as<u64>(), dscal(c, 1));
+                           c->epairs.as<u64>(), E, c->rank, c->nranks, c->out.as<u64>(), dscal(c, 1));
     tend(c, RDF_T_RULES);
-    rs = read_scalars(c, 2);
-    if (rs) return rs;
-    const u64 K = c->hscal[1];
+    u64 K = 0;
+    TRY(read_u64(c, dscal(c, 1), &K));
     tbegin(c, RDF_T_HWRITE);
     if (WH)
         hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
@@ -767,8 +879,8 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     tbegin(c, RDF_T_CEMIT);
     if (NT)
         hipLaunchKernelGGL(k_class_emit, dim3((unsigned)NT), dim3(RDF_BLOCK), 0, st, c->ckeys.as<u64>(), c->coff.as<u64>(),
-                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(), ncls,
-                           c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u64>());
+                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(),
+                           (u32)c->n_classes, c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u64>());
     tend(c, RDF_T_CEMIT);
     HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipGetLastError());
@@ -778,29 +890,55 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     c->n_out = K + H + HC;
     c->n_class_out = HC;
     c->out_ptr = c->out.as<u64>();
-    // host copies for result decoding
+    const u32 C = c->C;
     c->h_fcap.resize(C);
     c->h_csup.resize(C);
     if (C) {
         HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fcap.p, (u64)C * 4, hipMemcpyDeviceToHost));
         HIP_TRY(c, hipMemcpy(c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
     }
-    if (stats) {
-        memset(stats, 0, sizeof(*stats));
-        stats->n_cinds = c->n_out;
-        stats->n_explicit_raw = E;
-        stats->n_light_chunks = WL;
-        stats->n_heavy_chunks = WH;
-        stats->ms_pivot = c->tms[RDF_T_PIVOT];
-        stats->ms_light = c->tms[RDF_T_LIGHT];
-        stats->ms_rules = c->tms[RDF_T_RULES];
-        stats->ms_heavy = c->tms[RDF_T_HCOUNT] + c->tms[RDF_T_HWRITE];
-        stats->n_heavy_candidates = c->heavy_candidates;
-        stats->n_class_members = c->n_class_members;
-        stats->n_classes = c->n_classes;
-        stats->n_class_cinds = c->n_class_out;
-    }
+    rdf_cind_stats& s = c->cstats;
+    memset(&s, 0, sizeof(s));
+    s.n_cinds = c->n_out;
+    s.n_explicit_raw = c->n_explicit_raw;
+    s.n_light_chunks = c->n_light_chunks;
+    s.n_heavy_chunks = WH;
+    s.ms_pivot = c->tms[RDF_T_PIVOT];
+    s.ms_light = c->tms[RDF_T_LIGHT];
+    s.ms_rules = c->tms[RDF_T_RULES];
+    s.ms_heavy = c->tms[RDF_T_HCOUNT] + c->tms[RDF_T_HWRITE];
+    s.n_heavy_candidates = c->heavy_candidates;
+    s.n_class_members = c->n_class_members;
+    s.n_classes = c->n_classes;
+    s.n_class_cinds = c->n_class_out;
     c->stage = 4;
+    return RDF_OK;
+}
+
+rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
+    if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    CindView v = make_view(c, flags);
+    TRY(d_pivot_local(c, v));
+    tbegin(c, RDF_T_PIVOT);
+    if (c->C)
+        hipLaunchKernelGGL(k_pivot_final, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
+                           c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(),
+                           c->info.as<CapInfo>(), dscal(c, 2));
+    tend(c, RDF_T_PIVOT);
+    u64 WL = 0, WH = 0, WI = 0, E = 0, H = 0, HC = 0, NT = 0;
+    TRY(d_chunks(c, &WL, &WH, &WI));
+    TRY(d_light(c, v, WI, WL, &E));
+    c->n_explicit_raw = E;
+    c->n_light_chunks = WL;
+    TRY(d_explicit_index(c, v, E));
+    TRY(d_heavy_count(c, v, WH, &H));
+    TRY(d_classes_single(c, v, &HC, &NT));
+    TRY(d_emit(c, v, E, WH, H, HC, NT));
+    if (stats) *stats = c->cstats;
     return RDF_OK;
 }
 
@@ -811,6 +949,359 @@ rdf_status rdf_run(rdf_ctx* c, uint32_t min_support, const char* projection, uin
     r = rdf_build_capture_groups(c, projection, gs);
     if (r) return r;
     return rdf_discover_cinds(c, flags, cs);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sharded mode: a state machine that stops at every collective; the caller performs it
+// (torch.distributed over RCCL, rdfind_amd/distributed.py) and hands the result back.
+
+static rdf_status x_request(rdf_ctx* c, rdf_exchange* req, int op, const void* src, u64 count, int next_phase) {
+    memset(req, 0, sizeof(*req));
+    req->op = op;
+    req->elem_bytes = op == RDF_X_ALLREDUCE_SUM_U32 ? 4 : 8;
+    req->count = count;
+    c->x_op = op;
+    c->x_src = src;
+    c->x_count = count;
+    c->x_bytes = req->elem_bytes;
+    c->x_imported = false;
+    c->sh_phase = next_phase;
+    return RDF_OK;
+}
+
+static rdf_status sh_phase0(rdf_ctx* c, rdf_exchange* req) {
+    TRY(rdf_frequent_conditions(c, c->sh_ms, nullptr));
+    c->rank = c->sh_rank;
+    c->nranks = c->sh_nranks;
+    TRY(g_emit_sort_support(c, c->sh_proj));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U32, c->support.p, c->ncap, 1);
+}
+
+static rdf_status sh_phase1(rdf_ctx* c, rdf_exchange* req) {
+    HIP_TRY(c, hipMemcpyAsync(c->support.p, c->xrecv.p, c->ncap * 4, hipMemcpyDeviceToDevice, c->stream));
+    TRY(g_compact_groups(c));
+    TRY(g_size_hist(c, c->h_hist_local));
+    ENSURE(c, xsend, 256 * 8);
+    std::vector<u64> w(256);
+    for (int i = 0; i < 256; ++i) w[i] = c->h_hist_local[i];
+    HIP_TRY(c, hipMemcpy(c->xsend.p, w.data(), 256 * 8, hipMemcpyHostToDevice));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, 256, 2);
+}
+
+static rdf_status sh_phase2(rdf_ctx* c, rdf_exchange* req) {
+    const u32 R = c->nranks;
+    if (c->x_recv_count != 256ull * R) return fail(c, RDF_ERR_ARG, "histogram all-gather: wrong element count");
+    std::vector<u64> all(256ull * R);
+    HIP_TRY(c, hipMemcpy(all.data(), c->xrecv.p, all.size() * 8, hipMemcpyDeviceToHost));
+    u32 gh[256] = {};
+    for (u32 r = 0; r < R; ++r)
+        for (int b = 0; b < 256; ++b) gh[b] += (u32)all[256ull * r + b];
+    const u64 thr = heavy_threshold(gh);
+    u32 base = 0;
+    for (u32 r = 0; r < c->rank; ++r) {
+        u32 lh[256];
+        for (int b = 0; b < 256; ++b) lh[b] = (u32)all[256ull * r + b];
+        base += (u32)heavy_count(lh, thr);
+    }
+    TRY(g_heavy_binary(c, thr, base));
+    TRY(g_finish(c, nullptr));
+    c->gstats.n_heavy_groups = heavy_count(gh, thr);
+    ENSURE(c, xsend, std::max<u64>(c->C, 1) * 8);
+    if (c->C)
+        hipLaunchKernelGGL(k_extract_hmask, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
+                           c->info.as<CapInfo>(), c->C, c->xsend.as<u64>());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U64, c->xsend.p, c->C, 3);  // heavy bits are disjoint: sum == or
+}
+
+static rdf_status sh_phase3(rdf_ctx* c, rdf_exchange* req) {
+    if (c->C)
+        hipLaunchKernelGGL(k_set_hmask, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
+                           c->xrecv.as<u64>(), c->C, c->info.as<CapInfo>());
+    CindView v = make_view(c, c->sh_flags);
+    TRY(d_pivot_local(c, v));
+    ENSURE(c, xsend, std::max<u64>(c->C, 1) * 8);
+    if (c->C)
+        hipLaunchKernelGGL(k_shard_best_keys, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
+                           c->pbest.as<u64>(), c->C, c->rank, c->xsend.as<u64>());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return x_request(c, req, RDF_X_ALLREDUCE_MIN_U64, c->xsend.p, c->C, 4);
+}
+
+static rdf_status sh_phase4(rdf_ctx* c, rdf_exchange* req) {
+    ENSURE(c, gbest, std::max<u64>(c->C, 1) * 8);
+    HIP_TRY(c, hipMemcpyAsync(c->gbest.p, c->xrecv.p, (u64)c->C * 8, hipMemcpyDeviceToDevice, c->stream));
+    if (c->C)
+        hipLaunchKernelGGL(k_shard_light_words, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
+                           c->pnl.as<u32>(), c->C, c->xsend.as<u64>());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U64, c->xsend.p, c->C, 5);
+}
+
+static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C, R = c->nranks;
+    CindView v = make_view(c, c->sh_flags);
+    ENSURE(c, nrl, std::max<u64>(C, 1) * 4);
+    tbegin(c, RDF_T_PIVOT);
+    if (C)
+        hipLaunchKernelGGL(k_pivot_final_shard, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                           c->pbest.as<u64>(), c->pnl.as<u32>(), c->gbest.as<u64>(), c->xrecv.as<u64>(), c->rank,
+                           c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(), c->nrl.as<u32>(),
+                           c->info.as<CapInfo>(), dscal(c, 2));
+    tend(c, RDF_T_PIVOT);
+    u64 WL = 0, WH = 0, WI = 0, E = 0;
+    TRY(d_chunks(c, &WL, &WH, &WI));
+    c->sh_WH = WH;
+    TRY(d_light(c, v, WI, WL, &E));
+    c->n_explicit_raw = E;
+    c->n_light_chunks = WL;
+    // group the local survivors by owner rank (dep % R): pack, sort, find bounds, unpack
+    const int cb = bits_for(C ? C - 1 : 0);
+    const int ob = bits_for(R);
+    if (2 * cb + ob > 64) return fail(c, RDF_ERR_LIMIT, "sharded mode: too many captures for the owner sort key");
+    ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
+    ENSURE(c, obounds, (RDF_MAX_RANKS + 1) * 8);
+    tbegin(c, RDF_T_ESORT);
+    if (E) {
+        hipLaunchKernelGGL(k_owner_pack, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E, R, cb);
+        u64* k = c->epairs.as<u64>();
+        u64* t = c->epairs_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, E, 2 * cb + ob, st));
+        if (k != c->epairs.as<u64>()) std::swap(c->epairs, c->epairs_tmp);
+    }
+    hipLaunchKernelGGL(k_owner_bounds, dim3(1), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E, cb, R, c->obounds.as<u64>());
+    if (E) hipLaunchKernelGGL(k_owner_strip, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E, cb);
+    tend(c, RDF_T_ESORT);
+    std::vector<u64> bounds(R + 1);
+    HIP_TRY(c, hipMemcpyAsync(bounds.data(), c->obounds.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->epairs.p, E, 6));
+    for (u32 r = 0; r < R; ++r) req->send_counts[r] = bounds[r + 1] - bounds[r];
+    return RDF_OK;
+}
+
+static rdf_status sh_phase6(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 n = c->x_recv_count;
+    const u32 C = c->C;
+    ENSURE(c, epairs, std::max<u64>(n, 1) * 8);
+    ENSURE(c, epairs_tmp, std::max<u64>(n, 1) * 8);
+    HIP_TRY(c, hipMemcpyAsync(c->epairs.p, c->xrecv.p, n * 8, hipMemcpyDeviceToDevice, st));
+    tbegin(c, RDF_T_ESORT);
+    {
+        u64* k = c->epairs.as<u64>();
+        u64* t = c->epairs_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, n, 32 + bits_for(C ? C - 1 : 0), st));
+        if (k != c->epairs.as<u64>()) std::swap(c->epairs, c->epairs_tmp);
+    }
+    ENSURE(c, flags, std::max<u64>(n, 1) * 4);
+    ENSURE(c, pos, (n + 1) * 8);
+    if (n)
+        hipLaunchKernelGGL(k_mult_flags, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), n,
+                           c->nrl.as<u32>(), c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), n, c->pos.as<u64>() + n, st));
+    u64 E = 0;
+    TRY(read_u64(c, c->pos.as<u64>() + n, &E));
+    ENSURE(c, xsend, std::max<u64>(E, 1) * 8);
+    if (n)
+        hipLaunchKernelGGL(k_compact_u64, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), n,
+                           c->flags.as<u32>(), c->pos.as<u64>(), c->xsend.as<u64>());
+    tend(c, RDF_T_ESORT);
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, E, 7);
+}
+
+static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 E = c->x_recv_count;  // every rank's final explicit pairs
+    ENSURE(c, epairs, std::max<u64>(E, 1) * 8);
+    HIP_TRY(c, hipMemcpyAsync(c->epairs.p, c->xrecv.p, E * 8, hipMemcpyDeviceToDevice, st));
+    c->sh_E = E;
+    CindView v = make_view(c, c->sh_flags);
+    TRY(d_explicit_index(c, v, E));
+    u64 H = 0;
+    TRY(d_heavy_count(c, v, c->sh_WH, &H));
+    c->sh_H = H;
+    // classes: deterministic ids (sorted masks), owned members, lists of the classes pivoted here
+    tbegin(c, RDF_T_CLASS);
+    u64 nmem_all = 0, tcapc = 0;
+    u32 ncls = 0;
+    TRY(d_class_table(c, v, &nmem_all, &ncls, &tcapc));
+    c->sh_tcapc = tcapc;
+    c->n_classes = ncls;
+    ENSURE(c, smask, std::max<u64>(ncls, 1) * 8);
+    ENSURE(c, smask_tmp, std::max<u64>(ncls, 1) * 8);
+    ENSURE(c, pos, (tcapc + 1) * 8);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cflag.as<u32>(), c->pos.as<u64>(), tcapc, c->pos.as<u64>() + tcapc, st));
+    hipLaunchKernelGGL(k_compact_u64, dim3(grid_for(tcapc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ctab.as<u64>(), tcapc,
+                       c->cflag.as<u32>(), c->pos.as<u64>(), c->smask.as<u64>());
+    {
+        u64* k = c->smask.as<u64>();
+        u64* t = c->smask_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, ncls, 64, st));
+        if (k != c->smask.as<u64>()) std::swap(c->smask, c->smask_tmp);
+    }
+    if (ncls)
+        hipLaunchKernelGGL(k_class_rank, dim3(grid_for(ncls, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ctab.as<u64>(),
+                           tcapc - 1, c->smask.as<u64>(), ncls, c->ccid.as<u32>());
+    // owned members
+    ENSURE(c, ckeys, std::max<u64>(nmem_all, 1) * 8);
+    ENSURE(c, ckeys_tmp, std::max<u64>(nmem_all, 1) * 8);
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 4), 0, 8, st));
+    if (c->Cu)
+        hipLaunchKernelGGL(k_class_keys, dim3(grid_for(c->Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
+                           c->ccid.as<u32>(), tcapc - 1, c->rank, c->nranks, c->ckeys.as<u64>(), dscal(c, 4));
+    u64 nmem = 0;
+    TRY(read_u64(c, dscal(c, 4), &nmem));
+    {
+        u64* k = c->ckeys.as<u64>();
+        u64* t = c->ckeys_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, nmem, 32 + bits_for(ncls ? ncls - 1 : 0), st));
+        if (k != c->ckeys.as<u64>()) std::swap(c->ckeys, c->ckeys_tmp);
+    }
+    c->n_class_members = nmem;
+    ENSURE(c, coff, (ncls + 1ull) * 8);
+    ENSURE(c, cmask, std::max<u64>(ncls, 1) * 8);
+    ENSURE(c, cpiv, std::max<u64>(ncls, 1) * 4);
+    ENSURE(c, cnch, std::max<u64>(ncls, 1) * 4);
+    ENSURE(c, cchoff, (ncls + 1ull) * 8);
+    hipLaunchKernelGGL(k_class_info_shard, dim3(grid_for(ncls + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->ckeys.as<u64>(), nmem, ncls, c->smask.as<u64>(), c->coff.as<u64>(), c->cmask.as<u64>());
+    HIP_TRY(c, hipMemsetAsync(c->cnch.p, 0, std::max<u64>(ncls, 1) * 4, st));
+    if (c->Cu && ncls)
+        hipLaunchKernelGGL(k_class_pivot_shard, dim3(grid_for(c->Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                           c->ctab.as<u64>(), tcapc - 1, c->ccid.as<u32>(), c->pivot.as<u32>(), c->gbest.as<u64>(), c->rank,
+                           c->cpiv.as<u32>(), c->cnch.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cnch.as<u32>(), c->cchoff.as<u64>(), ncls, c->cchoff.as<u64>() + ncls, st));
+    u64 WC = 0;
+    TRY(read_u64(c, c->cchoff.as<u64>() + ncls, &WC));
+    ENSURE(c, ccnt, std::max<u64>(WC, 1) * 4);
+    ENSURE(c, lwoff, (WC + 1) * 8);
+    if (WC)
+        hipLaunchKernelGGL((k_class_filter<false>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
+                           c->ccnt.as<u32>(), (const u64*)nullptr, (u32*)nullptr, (u64*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ccnt.as<u32>(), c->lwoff.as<u64>(), WC, c->lwoff.as<u64>() + WC, st));
+    u64 LT = 0;
+    TRY(read_u64(c, c->lwoff.as<u64>() + WC, &LT));
+    ENSURE(c, xsend, std::max<u64>(LT, 1) * 8);
+    if (WC)
+        hipLaunchKernelGGL((k_class_filter<true>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
+                           (u32*)nullptr, c->lwoff.as<u64>(), (u32*)nullptr, c->xsend.as<u64>());
+    tend(c, RDF_T_CLASS);
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, LT, 8);
+}
+
+static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 n = c->x_recv_count;  // (class << 32 | ref) pairs of every class
+    const u32 ncls = (u32)c->n_classes;
+    ENSURE(c, cpairs, std::max<u64>(n, 1) * 8);
+    ENSURE(c, cpairs_tmp, std::max<u64>(n, 1) * 8);
+    HIP_TRY(c, hipMemcpyAsync(c->cpairs.p, c->xrecv.p, n * 8, hipMemcpyDeviceToDevice, st));
+    tbegin(c, RDF_T_CLASS);
+    {
+        u64* k = c->cpairs.as<u64>();
+        u64* t = c->cpairs_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, n, 32 + bits_for(ncls ? ncls - 1 : 0), st));
+        if (k != c->cpairs.as<u64>()) std::swap(c->cpairs, c->cpairs_tmp);
+    }
+    ENSURE(c, clists, std::max<u64>(n, 1) * 4);
+    ENSURE(c, lwoff, (ncls + 1ull) * 8);
+    ENSURE(c, cchoff, (ncls + 1ull) * 8);
+    hipLaunchKernelGGL(k_class_lists, dim3(grid_for(std::max<u64>(n, ncls + 1ull), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->cpairs.as<u64>(), n, ncls, c->clists.as<u32>(), c->lwoff.as<u64>(), c->cchoff.as<u64>());
+    u64 HC = 0, NT = 0;
+    TRY(d_class_tiles(c, c->n_class_members, ncls, &HC, &NT));
+    tend(c, RDF_T_CLASS);
+    CindView v = make_view(c, c->sh_flags);
+    v.eoff = c->eoff.as<u64>();
+    v.epairs = c->epairs.as<u64>();
+    v.ebin = c->ebin.as<u64>();
+    TRY(d_emit(c, v, c->sh_E, c->sh_WH, c->sh_H, HC, NT));
+    memset(req, 0, sizeof(*req));
+    req->op = RDF_X_DONE;
+    c->sh_phase = 9;
+    return RDF_OK;
+}
+
+rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t min_support, const char* projection,
+                           uint32_t flags) {
+    if (!c) return RDF_ERR_ARG;
+    if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
+    if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    int proj = 0;
+    TRY(parse_projection(c, projection, &proj));
+    c->sh_rank = rank;
+    c->sh_nranks = nranks;
+    c->sh_ms = min_support;
+    c->sh_proj = proj;
+    c->sh_flags = flags;
+    c->sh_phase = 0;
+    c->x_imported = true;
+    c->stage = std::min(c->stage, 1);
+    return RDF_OK;
+}
+
+rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
+    if (!c || !req) return RDF_ERR_ARG;
+    if (c->sh_phase < 0 || c->sh_phase > 8) return fail(c, RDF_ERR_STATE, "rdf_shard_begin must be called first");
+    if (!c->x_imported) return fail(c, RDF_ERR_STATE, "rdf_shard_import must supply the pending exchange first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    rdf_status r = RDF_OK;
+    switch (c->sh_phase) {
+        case 0: r = sh_phase0(c, req); break;
+        case 1: r = sh_phase1(c, req); break;
+        case 2: r = sh_phase2(c, req); break;
+        case 3: r = sh_phase3(c, req); break;
+        case 4: r = sh_phase4(c, req); break;
+        case 5: r = sh_phase5(c, req); break;
+        case 6: r = sh_phase6(c, req); break;
+        case 7: r = sh_phase7(c, req); break;
+        case 8: r = sh_phase8(c, req); break;
+    }
+    if (r != RDF_OK) c->sh_phase = -1;  // a failed machine must be restarted with rdf_shard_begin
+    return r;
+}
+
+rdf_status rdf_shard_export(rdf_ctx* c, void* dst) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->x_imported || c->sh_phase < 1 || c->sh_phase > 8) return fail(c, RDF_ERR_STATE, "no pending exchange");
+    if (c->x_count && !dst) return fail(c, RDF_ERR_ARG, "null exchange buffer");
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->x_count)
+        HIP_TRY(c, hipMemcpyAsync(dst, c->x_src, c->x_count * c->x_bytes, hipMemcpyDefault, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RDF_OK;
+}
+
+rdf_status rdf_shard_import(rdf_ctx* c, const void* src, uint64_t count) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->x_imported || c->sh_phase < 1 || c->sh_phase > 8) return fail(c, RDF_ERR_STATE, "no pending exchange");
+    if (count && !src) return fail(c, RDF_ERR_ARG, "null exchange buffer");
+    const bool reduce = c->x_op == RDF_X_ALLREDUCE_SUM_U32 || c->x_op == RDF_X_ALLREDUCE_SUM_U64 ||
+                        c->x_op == RDF_X_ALLREDUCE_MIN_U64;
+    if (reduce && count != c->x_count) return fail(c, RDF_ERR_ARG, "all-reduce result has the wrong element count");
+    HIP_TRY(c, hipSetDevice(c->device));
+    ENSURE(c, xrecv, std::max<u64>(count, 1) * c->x_bytes);
+    if (count) HIP_TRY(c, hipMemcpyAsync(c->xrecv.p, src, count * c->x_bytes, hipMemcpyDefault, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->x_recv_count = count;
+    c->x_imported = true;
+    return RDF_OK;
+}
+
+rdf_status rdf_last_stats(rdf_ctx* c, rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "no completed run");
+    if (fc) *fc = c->fstats;
+    if (gs) *gs = c->gstats;
+    if (cs) *cs = c->cstats;
+    return RDF_OK;
 }
 
 rdf_status rdf_cind_count(rdf_ctx* c, uint64_t* n) {

@@ -1,0 +1,119 @@
+"""Sharded multi-GPU CIND discovery: one process per GPU, torch.distributed over RCCL.
+
+Every rank holds all triples.  Rank r builds only the capture groups of the join values it owns
+(``hash(join) % R == r``), so join partners never cross the fabric.  The global quantities are
+combined by collectives that the library requests one at a time (``rdf_shard_step``):
+
+  1. all-reduce(sum)  capture supports (distinct join values per capture)
+  2. all-gather       group-size histograms -> global heavy threshold + this rank's heavy bit base
+  3. all-reduce(sum)  heavy-group bitmasks (bits of different ranks are disjoint, so sum == or)
+  4. all-reduce(min)  (pivot size, rank) per dependent
+  5. all-reduce(sum)  light-group counts and the number of ranks holding light groups per dependent
+  6. all-to-all       local survivors (dep, ref) of light dependents -> the dependent's owner (dep % R);
+                      the owner keeps a ref iff every rank with a light group of dep reported it.  This is
+                      the reference's combiner-side intersection (AllAtOnceTraversalStrategy.scala:62-65)
+                      followed by the shuffle to the IntersectCindCandidates reducer.
+  7. all-gather       the final explicit CIND pairs (the minimality rules R1-R4 probe other dependents)
+  8. all-gather       filtered ref lists of the bitmask classes pivoted on each rank
+
+Each rank then emits the CINDs of its own dependents; the union over ranks is the single-GPU result.
+
+``run_sharded`` drives any object with ``shard_begin/shard_step/shard_export/shard_import`` (the HIP
+``Context``); ``run_protocol`` is the backend-neutral loop, also used by the CPU protocol tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+_DTYPES = {_lib.X_ALLREDUCE_SUM_U32: torch.int32}
+
+
+def _dtype(op):
+    return _DTYPES.get(op, torch.int64)
+
+
+def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
+    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts) if counts else 0
+    if m == 0:
+        return send.new_empty(0)
+    padded = send.new_zeros(m)
+    padded[: send.numel()] = send
+    parts = [send.new_empty(m) for _ in range(world)]
+    dist.all_gather(parts, padded, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+def alltoallv(send: torch.Tensor, send_counts, group=None) -> torch.Tensor:
+    """Variable-length all-to-all: ``send`` holds consecutive slices for ranks 0..R-1."""
+    world = dist.get_world_size(group)
+    sc = torch.tensor(list(send_counts) + [0] * (world - len(send_counts)), dtype=torch.int64, device=send.device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.tolist()]
+    out = send.new_empty(sum(recv_counts))
+    dist.all_to_all_single(out, send, output_split_sizes=recv_counts, input_split_sizes=[int(x) for x in sc.tolist()],
+                           group=group)
+    return out
+
+
+def exchange(req: _lib.ExchangeRequest, send: torch.Tensor, group=None) -> torch.Tensor:
+    """Perform the collective ``req`` describes on ``send`` and return the result tensor."""
+    op = req.op
+    if op in (_lib.X_ALLREDUCE_SUM_U32, _lib.X_ALLREDUCE_SUM_U64):
+        dist.all_reduce(send, op=dist.ReduceOp.SUM, group=group)  # two's-complement sums == unsigned sums
+        return send
+    if op == _lib.X_ALLREDUCE_MIN_U64:
+        dist.all_reduce(send, op=dist.ReduceOp.MIN, group=group)  # values < 2^63 by contract
+        return send
+    if op == _lib.X_ALLGATHERV_U64:
+        return allgatherv(send, group)
+    if op == _lib.X_ALLTOALLV_U64:
+        return alltoallv(send, req.send_counts, group)
+    raise ValueError(f"unknown exchange op {op}")
+
+
+def exchange_device(group=None) -> torch.device:
+    """Where exchange buffers live: HBM for RCCL, host memory for gloo (a CPU-only process group)."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def run_protocol(machine, group=None, device=None):
+    """Drive a shard machine to completion.  ``machine.shard_step()`` returns an ExchangeRequest;
+    ``machine.shard_export(ptr)`` fills ``count`` elements at ``ptr``; ``machine.shard_import(ptr, n)``
+    takes the result.  Returns the number of collectives performed."""
+    device = device or exchange_device(group)
+    n = 0
+    while True:
+        req = machine.shard_step()
+        if req.op == _lib.X_DONE:
+            return n
+        send = torch.empty(req.count, dtype=_dtype(req.op), device=device)
+        machine.shard_export(send.data_ptr())
+        if device.type == "cuda":
+            torch.cuda.current_stream(device).synchronize()
+        recv = exchange(req, send, group).contiguous()
+        if device.type == "cuda":
+            torch.cuda.current_stream(device).synchronize()
+        machine.shard_import(recv.data_ptr(), recv.numel())
+        n += 1
+
+
+def run_sharded(ctx, min_support: int, projection="spo", clean_implied=True, traversal_strategy=1, group=None,
+                device=None):
+    """Sharded CIND discovery on this rank's context; returns (group_stats, cind_stats) of this rank."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy)
+    run_protocol(ctx, group, device)
+    return ctx.last_stats()

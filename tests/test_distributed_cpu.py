@@ -1,0 +1,126 @@
+"""Sharded protocol on the CPU: real gloo collectives, world size 2 (and 3), driven by the same
+``rdfind_amd.distributed.run_protocol`` loop as the GPU path, with ``tests/shard_sim.ShardSim`` standing in
+for the HIP library.  The union of the ranks' CINDs must equal the single-process oracle result, and the
+ranks' outputs must be disjoint (each dependent has exactly one owner)."""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import rdfind_oracle as R
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, cases, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import distributed
+    from tests.shard_sim import ShardSim
+
+    try:
+        out = []
+        for arr, ms, strategy, clean in cases:
+            sim = ShardSim(arr)
+            sim.shard_begin(rank, world, ms, "spo", clean, strategy)
+            n = distributed.run_protocol(sim)
+            out.append((n, sorted(R.cind_set(sim.result))))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, cases):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return results
+
+
+def _cases(seed, count):
+    rng = random.Random(seed)
+    cases = []
+    for i in range(count):
+        nv = rng.randrange(4, 30)
+        n = rng.randrange(10, 160)
+        arr = [(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)]
+        strategy, clean = [(1, True), (0, True), (0, False), (1, False)][i % 4]
+        cases.append((arr, rng.randrange(1, 4), strategy, clean))
+    return cases
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_protocol_matches_oracle(world):
+    cases = _cases(world, 12)
+    res = _run(world, cases)
+    for k, (arr, ms, strategy, clean) in enumerate(cases):
+        tr = [tuple(t) for t in arr]
+        if strategy == 1 and not clean:
+            uf = R.frequent_unary_conditions(tr, ms)
+            v = R.all_at_once(R.join_lines(tr, uf, R.frequent_binary_conditions(tr, uf, ms)), ms, False,
+                              literal_implies=False)
+            expected = R.cind_set(R.s2l_exact_raw(v))
+        else:
+            expected = R.cind_set(R.rdfind(tr, ms, strategy, clean))
+        parts = [set(res[r][k][1]) for r in range(world)]
+        assert all(res[r][k][0] == 8 for r in range(world))  # the library's eight collectives
+        union = set().union(*parts)
+        assert sum(len(p) for p in parts) == len(union)      # every dependent has one owner
+        assert union == expected, (k, ms, strategy, clean)
+
+
+def test_exchange_helpers_gloo():
+    """allgatherv / alltoallv with ragged and empty contributions."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_helpers_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0]["ag"] == [0, 1, 2, 10] and got[1]["ag"] == [0, 1, 2, 10]
+    assert got[0]["empty"] == [] and got[1]["empty"] == []
+    # rank 0 sends [100] to 0 and [101, 102] to 1; rank 1 sends [] to 0 and [200] to 1
+    assert got[0]["a2a"] == [100] and got[1]["a2a"] == [101, 102, 200]
+
+
+def _helpers_worker(rank, world, port, q):
+    import torch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import distributed
+
+    try:
+        send = torch.tensor([0, 1, 2] if rank == 0 else [10], dtype=torch.int64)
+        ag = distributed.allgatherv(send).tolist()
+        empty = distributed.allgatherv(torch.zeros(0, dtype=torch.int64)).tolist()
+        if rank == 0:
+            a2a = distributed.alltoallv(torch.tensor([100, 101, 102], dtype=torch.int64), [1, 2]).tolist()
+        else:
+            a2a = distributed.alltoallv(torch.tensor([200], dtype=torch.int64), [0, 1]).tolist()
+        q.put((rank, {"ag": ag, "empty": empty, "a2a": a2a}))
+    finally:
+        dist.destroy_process_group()

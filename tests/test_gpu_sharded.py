@@ -1,0 +1,138 @@
+"""GPU parity of the sharded (multi-GPU) mode: 2 and 3 ranks, each with its own context on the one GPU of
+the test box, exchanging through gloo (host-staged buffers; the bench uses RCCL over xGMI with one GPU per
+rank).  The union of the ranks' CINDs must equal the single-GPU result and the C oracle, bit-exact, and the
+ranks' outputs must be disjoint."""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, cases, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import _lib, distributed
+
+    out = []
+    try:
+        ctx = _lib.Context(0)
+        for s, p, o, nv, ms, strategy, clean in cases:
+            ctx.set_triples(s, p, o, nv)
+            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy)
+            n = ctx.cind_count()
+            rows = ctx.copy_cinds() if n <= 2_000_000 else None
+            out.append({"n": n, "checksum": ctx.checksum(), "rows": rows, "heavy": gs["n_heavy_groups"],
+                        "class_members": cs["n_class_members"]})
+        ctx.close()
+        q.put((rank, out))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_sharded(world, cases):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+    return res
+
+
+def _single(cases):
+    from rdfind_amd import _lib
+
+    out = []
+    with _lib.Context(0) as ctx:
+        for s, p, o, nv, ms, strategy, clean in cases:
+            ctx.set_triples(s, p, o, nv)
+            ctx.run(ms, "spo", clean, strategy)
+            n = ctx.cind_count()
+            rows = ctx.copy_cinds() if n <= 2_000_000 else None
+            out.append({"n": n, "checksum": ctx.checksum(), "rows": rows})
+    return out
+
+
+def _rowset(rows):
+    return set(map(tuple, np.stack([rows["dep"], rows["ref"], rows["support"]], 1).tolist()))
+
+
+def _check(world, cases):
+    single = _single(cases)
+    res = _run_sharded(world, cases)
+    for k, exp in enumerate(single):
+        parts = [res[r][k] for r in range(world)]
+        assert sum(p["n"] for p in parts) == exp["n"], k
+        assert sum(p["checksum"] for p in parts) % (1 << 64) == exp["checksum"], k
+        if exp["rows"] is not None:
+            union = set()
+            for p in parts:
+                union |= _rowset(p["rows"])
+            assert union == _rowset(exp["rows"]), k
+    return res
+
+
+def _random_cases(seed, count):
+    rng = random.Random(seed)
+    cases = []
+    for i in range(count):
+        nv = rng.randrange(4, 60)
+        n = rng.randrange(1, 400)
+        arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                       dtype=np.uint32)
+        strategy, clean = [(1, True), (0, True), (0, False), (1, False)][i % 4]
+        cases.append((arr[:, 0], arr[:, 1], arr[:, 2], nv, rng.randrange(1, 4), strategy, clean))
+    return cases
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_random_matches_single(world):
+    _check(world, _random_cases(100 + world, 24))
+
+
+def test_sharded_synthetic_configs_match_oracle():
+    """Scaled BASELINE configs (heavy groups and mask classes exercised) vs single GPU and the C oracle."""
+    from oracle import c_oracle as C
+    from rdfind_amd import synth
+
+    cases = []
+    for cfg, scale in (("c2", 0.05), ("c1", 0.1), ("c5", 0.01), ("c3", 0.002)):
+        d = synth.config(cfg, scale)
+        cases.append((d.s, d.p, d.o, d.num_terms, d.min_support, 1, True))
+    res = _check(2, cases)
+    assert sum(res[r][0]["heavy"] for r in range(2)) >= 0
+    assert any(res[r][0]["class_members"] > 0 for r in range(2))  # c2 exercises the class exchange
+    # the single-GPU result is pinned against the C restatement in test_gpu.py; pin one case here too
+    s, p, o, nv, ms, _, _ = cases[1]
+    exp, _ = C.run_set(s, p, o, nv, ms, 1, True)
+    assert sum(res[r][1]["n"] for r in range(2)) == len(exp)
+
+
+def test_sharded_bench_size_properties():
+    """c2 at full size over 2 ranks: CIND count and set checksum equal the single-GPU run."""
+    from rdfind_amd import synth
+
+    d = synth.config("c2", 1.0)
+    _check(2, [(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)])
