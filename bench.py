@@ -133,7 +133,7 @@ def main():
     counts = {"sort_passes_records": 0}
     # passes of the record sort (bits = join bits + capture bits, 8 per pass)
     V = d.num_terms
-    capbits = int(6 * V + fc["n_frequent_binary"] - 1).bit_length()
+    capbits = int(2 * sum(fc["n_frequent_unary"]) + fc["n_frequent_binary"] - 1).bit_length()  # compact capture ids
     joinbits = int(V - 1).bit_length()
     counts["sort_passes_records"] = ((capbits + joinbits + 7) // 8) * gs["n_records"]
     dominant = max(kt, key=lambda k: kt[k])
@@ -171,6 +171,10 @@ def main():
                        "parallelism": f"join-hash shards x{world} (RCCL)" if world > 1 else "single"},
             "roofline": roof, "cpu_baseline": cpu,
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+            "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
+                     "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],
+                     "explicit_raw": cs["n_explicit_raw"], "class_members": cs["n_class_members"],
+                     "classes": cs["n_classes"], "class_cinds": cs["n_class_cinds"]},
         }
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -13,7 +13,7 @@ import numpy as np
 from . import codes
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librdfind_hip.so")
+LIB_PATH = os.environ.get("RDFIND_HIP_LIB") or os.path.join(_HERE, "librdfind_hip.so")  # env: dev variants only
 
 RDF_CLEAN_IMPLIED = 1
 RDF_STRATEGY_ALL_AT_ONCE = 2

@@ -77,6 +77,47 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_count_frequent(const u32* __restr
     }
 }
 
+// frequent-condition ranks: frank[i] (i = pos * V + value, pos 0 s / 1 p / 2 o) = index of the condition
+// among all frequent conditions, NONE if infrequent; fval[index] = value.  They give the compact candidate
+// capture space: unary capture (type t, value v) -> 2 * frank[cap_pos(t) * V + v] + (t >= 3), binary
+// capture b -> 2U + b (U = frequent conditions), so sort keys and support arrays scale with U, not |V|.
+__global__ __launch_bounds__(RDF_BLOCK) void k_frank_flags(const u32* __restrict__ cnt, u64 n3, u32 ms, u32* flags) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n3; i += (u64)gridDim.x * RDF_BLOCK) flags[i] = cnt[i] >= ms;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_frank_final(const u32* __restrict__ cnt, u64 n3, u32 V, u32 ms, u32* frank,
+                                                           u32* fval) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n3; i += (u64)gridDim.x * RDF_BLOCK) {
+        if (cnt[i] >= ms) fval[frank[i]] = (u32)(i % V);
+        else frank[i] = NONE32;
+    }
+}
+
+// condition position (0 s, 1 p, 2 o) of unary capture type t (0 s[p], 1 s[o], 2 p[s], 3 p[o], 4 o[s], 5 o[p])
+__host__ __device__ inline int cap_pos(int t) { return (t == 2 || t == 4) ? 0 : ((t == 0 || t == 5) ? 1 : 2); }
+
+// candidate capture id of unary capture (t, v); NONE if its condition is infrequent
+__device__ inline u32 ucap(const u32* frank, u32 V, int t, u32 v) {
+    const u32 r = frank[(u64)cap_pos(t) * V + v];
+    return r == NONE32 ? NONE32 : 2u * r + (t >= 3 ? 1u : 0u);
+}
+
+// external capture id (t * V + v for unary, 6V + b for binary) of a candidate id
+__global__ __launch_bounds__(RDF_BLOCK) void k_external_ids(const u32* __restrict__ fcap, u32 C, u32 twoU, u32 V,
+                                                            const u32* __restrict__ fval, u32 Us, u32 Up, u32* ext) {
+    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < C; c += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 id = fcap[c];
+        if (id < twoU) {
+            const u32 u = id >> 1, j = id & 1u;
+            const int pos = u < Us ? 0 : (u < Us + Up ? 1 : 2);
+            const u32 t = pos == 0 ? (j ? 4u : 2u) : (pos == 1 ? (j ? 5u : 0u) : (j ? 3u : 1u));
+            ext[c] = t * V + fval[u];
+        } else {
+            ext[c] = 6u * V + (id - twoU);
+        }
+    }
+}
+
 // ================================================================================================
 // K2: binary condition counts  (CreatedReducedDoubleConditionCounts.flatMap,
 //     ALG/operators/candidate_extraction/CreatedReducedDoubleConditionCounts.scala:45-86, + groupBy.sum
@@ -215,23 +256,22 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
 }
 
 // Block-aggregated append: one global atomic per block iteration instead of one per wave.
-__device__ inline u64 block_append(u64* counter, u32 want, u32* lds_wave, u64* lds_base) {
+// block-wide exclusive scan of one u32 per thread; *total = block sum (all threads must call it)
+__device__ inline u32 block_exclusive_scan_u32(u32 v, u32* lds_wave, u32* total) {
     const int wave = threadIdx.x / RDF_WAVE;
-    const u32 incl = wave_inclusive_scan(want);
+    const u32 incl = wave_inclusive_scan(v);
     if (lane_id() == RDF_WAVE - 1) lds_wave[wave] = incl;
     __syncthreads();
-    u32 woff = 0, total = 0;
+    u32 woff = 0, sum = 0;
 #pragma unroll
     for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
         const u32 x = lds_wave[w];
         woff += w < wave ? x : 0u;
-        total += x;
+        sum += x;
     }
-    if (threadIdx.x == 0) *lds_base = total ? atomicAdd(counter, (u64)total) : 0ull;
-    __syncthreads();
-    const u64 base = *lds_base + woff + incl - want;
-    __syncthreads();  // lds_wave / lds_base are reused by the next iteration
-    return base;
+    *total = sum;
+    __syncthreads();  // lds_wave is reused by the next call
+    return woff + incl - v;
 }
 
 // ================================================================================================
@@ -241,54 +281,71 @@ __device__ inline u64 block_append(u64* counter, u32 want, u32* lds_wave, u64* l
 // components, which is what every consumer reconstructs (CreateDependencyCandidates.scala:157-186,
 // splitAndCollectUnaryCaptures).  Record = join << capbits | capture id.
 
+// records of triple i (at most 9); returns the count
+__device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
+                                     u32 V, u32 twoU, const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                     const u32* __restrict__ lvals, u64 lmask, int proj, int capbits, u32 rank, u32 nranks,
+                                     u64 (&rec)[9]) {
+    u32 c = 0;
+    const u32 ts = s[i], tp = p[i], to = o[i];
+    const u32 rs = frank[ts], rp = frank[V + tp], ro = frank[2ull * V + to];  // condition ranks (or NONE)
+    const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
+    if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
+        const u64 j = (u64)to << capbits;
+        if (fs) rec[c++] = j | (2ull * rs + 1);
+        if (fp) rec[c++] = j | (2ull * rp + 1);
+        if (fs && fp) {
+            u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
+            if (b != NONE32) rec[c++] = j | ((u64)twoU + b);
+        }
+    }
+    if ((proj & 2) && shard_of(tp, nranks) == rank) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
+        const u64 j = (u64)tp << capbits;
+        if (fs) rec[c++] = j | (2ull * rs);
+        if (fo) rec[c++] = j | (2ull * ro + 1);
+        if (fs && fo) {
+            u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
+            if (b != NONE32) rec[c++] = j | ((u64)twoU + b);
+        }
+    }
+    if ((proj & 1) && shard_of(ts, nranks) == rank) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
+        const u64 j = (u64)ts << capbits;
+        if (fp) rec[c++] = j | (2ull * rp);
+        if (fo) rec[c++] = j | (2ull * ro);
+        if (fp && fo) {
+            u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
+            if (b != NONE32) rec[c++] = j | ((u64)twoU + b);
+        }
+    }
+    return c;
+}
+
+// two passes over contiguous per-block chunks of triples: COUNT writes each block's record count, the
+// write pass places records at the scanned block offset + block-local prefix (no shared counter, and the
+// record order is deterministic)
+template <bool WRITE>
 __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                            const u32* __restrict__ o, u64 n, u32 V, u32 ms,
-                                                            const u32* __restrict__ cnt, const u64* __restrict__ lkeys,
+                                                            const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
+                                                            const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                             const u32* __restrict__ lvals, u64 lmask, int proj,
-                                                            int capbits, u32 rank, u32 nranks, u64* out, u64* counter) {
+                                                            int capbits, u32 rank, u32 nranks, u64* block_counts,
+                                                            const u64* __restrict__ block_offsets, u64* out) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
-    __shared__ u64 lds_base;
-    const u64 stride = (u64)gridDim.x * RDF_BLOCK;
-    const u64 n_round = (n + RDF_BLOCK - 1) / RDF_BLOCK * RDF_BLOCK;  // all threads of a block iterate together
-    const u64 B6 = 6ull * V;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n_round; i += stride) {
+    const u64 b = (u64)blockIdx.x * per;
+    const u64 e = b + per < n ? b + per : n;
+    u64 run = WRITE ? block_offsets[blockIdx.x] : 0;
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
         u64 rec[9];
         u32 c = 0;
-        if (i < n) {
-            const u32 ts = s[i], tp = p[i], to = o[i];
-            bool fs, fp, fo;
-            freq_flags(cnt, V, ms, ts, tp, to, fs, fp, fo);
-            if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s], o[p], o[s,p]
-                const u64 j = (u64)to << capbits;
-                if (fs) rec[c++] = j | (4ull * V + ts);
-                if (fp) rec[c++] = j | (5ull * V + tp);
-                if (fs && fp) {
-                    u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
-                    if (b != NONE32) rec[c++] = j | (B6 + b);
-                }
-            }
-            if ((proj & 2) && shard_of(tp, nranks) == rank) {  // project predicates: p[s], p[o], p[s,o]
-                const u64 j = (u64)tp << capbits;
-                if (fs) rec[c++] = j | (2ull * V + ts);
-                if (fo) rec[c++] = j | (3ull * V + to);
-                if (fs && fo) {
-                    u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
-                    if (b != NONE32) rec[c++] = j | (B6 + b);
-                }
-            }
-            if ((proj & 1) && shard_of(ts, nranks) == rank) {  // project subjects: s[p], s[o], s[p,o]
-                const u64 j = (u64)ts << capbits;
-                if (fp) rec[c++] = j | (0ull * V + tp);
-                if (fo) rec[c++] = j | (1ull * V + to);
-                if (fp && fo) {
-                    u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
-                    if (b != NONE32) rec[c++] = j | (B6 + b);
-                }
-            }
-        }
-        u64 base = block_append(counter, c, lds_wave, &lds_base);
-        for (u32 k = 0; k < c; ++k) out[base + k] = rec[k];
+        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, capbits, rank, nranks, rec);
+        u32 total;
+        const u32 off = block_exclusive_scan_u32(c, lds_wave, &total);
+        if (WRITE)
+            for (u32 k = 0; k < c; ++k) out[run + off + k] = rec[k];
+        run += total;
     }
+    if (!WRITE && threadIdx.x == 0) block_counts[blockIdx.x] = run;
 }
 
 // ================================================================================================
@@ -446,13 +503,16 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mask(const u64* __restrict_
 // binary captures: components (unary compact ids) and keys; parent edges (component << 32 | binary)
 // are radix-sorted into the parents CSR (no per-unary cursor atomics: s[p=name] has thousands of parents)
 __global__ __launch_bounds__(RDF_BLOCK) void k_binary_info(const u32* __restrict__ fcap, const u32* __restrict__ fidx,
-                                                           const u64* __restrict__ bkeys, u32 C, u32 Cu, u32 V,
-                                                           u32* bcomp, u64* bkeyc, u64* pedges, CapInfo* info) {
+                                                           const u64* __restrict__ bkeys, const u32* __restrict__ frank,
+                                                           u32 C, u32 Cu, u32 V, u32 twoU, u32* bcomp, u64* bkeyc,
+                                                           u64* pedges, CapInfo* info) {
     for (u64 c = Cu + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < C; c += (u64)gridDim.x * RDF_BLOCK) {
-        u64 key = bkeys[fcap[c] - 6ull * V];
+        u64 key = bkeys[fcap[c] - twoU];
         int bt = bin_key_type(key);
-        u32 c1 = fidx[(u64)bin_comp1(bt) * V + bin_key_v1(key)];
-        u32 c2 = fidx[(u64)bin_comp2(bt) * V + bin_key_v2(key)];
+        // a frequent binary condition has frequent unary conditions, and its captures' components are
+        // in every group the binary capture is in, so they are frequent captures too
+        u32 c1 = fidx[ucap(frank, V, bin_comp1(bt), bin_key_v1(key))];
+        u32 c2 = fidx[ucap(frank, V, bin_comp2(bt), bin_key_v2(key))];
         bcomp[2 * (c - Cu)] = c1;
         bcomp[2 * (c - Cu) + 1] = c2;
         bkeyc[c - Cu] = key;
@@ -498,10 +558,36 @@ __device__ inline u32 find_dep(const u64* chunk_off, u32 C, u64 w) {
     return lo;
 }
 
+static constexpr u64 PIVOT_SHORT = 32;  // dependents with at most this many groups: one lane each
+
+// segments of the long dependents (the short ones are done lane-per-dependent by k_pivot_short)
+// owner[w] = d for every work item w in [off[d], off[d+1]) (replaces a binary search per work item)
+__global__ __launch_bounds__(RDF_BLOCK) void k_expand_owner(const u64* __restrict__ off, u32 C, u32* owner) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
+        for (u64 w = off[d]; w < off[d + 1]; ++w) owner[w] = (u32)d;
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_nseg(const u64* __restrict__ doff, u32 C, u32* nseg) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 len = doff[d + 1] - doff[d];
-        nseg[d] = (u32)((len + PIVOT_SEG - 1) / PIVOT_SEG);
+        nseg[d] = len > PIVOT_SHORT ? (u32)((len + PIVOT_SEG - 1) / PIVOT_SEG) : 0u;
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u64* best_out, u32* nlight_out) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 b = v.doff[d], e = v.doff[d + 1];
+        if (e - b > PIVOT_SHORT) continue;
+        u64 best = ~0ull;
+        u32 nlight = 0;
+        for (u64 j = b; j < e; ++j) {
+            const u32 g = v.dgrp[j];
+            const u64 key = ((v.goff[g + 1] - v.goff[g]) << 32) | g;
+            best = key < best ? key : best;
+            nlight += v.hbit[g] == LIGHT;
+        }
+        best_out[d] = best;
+        nlight_out[d] = nlight;
     }
 }
 
@@ -670,25 +756,40 @@ __device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& i
     return r;
 }
 
-__device__ inline void emit_pairs(u32 d, u32 cand, u64 alive, u64* pairs, u64* npairs) {
-    if (!alive) return;
-    const u32 cnt = (u32)__popcll(alive);
-    u64 base = 0;
-    if (lane_id() == 0) base = atomicAdd(npairs, (u64)cnt);
-    base = __shfl(base, 0, RDF_WAVE);
-    if ((alive >> lane_id()) & 1ull) pairs[base + __popcll(alive & lanemask_lt())] = ((u64)d << 32) | cand;
+// survivors of a chunk go to the chunk's own 64-entry slot (no shared counter: a single global append
+// counter serialises at the memory side); k_slot_compact packs the slots afterwards
+__device__ inline void slot_emit(u64 slot, u32 d, u32 cand, u64 alive, u64* slots, u32* counts) {
+    if (lane_id() == 0) counts[slot] = (u32)__popcll(alive);
+    if ((alive >> lane_id()) & 1ull) slots[slot * RDF_WAVE + __popcll(alive & lanemask_lt())] = ((u64)d << 32) | cand;
 }
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(const u64* __restrict__ slots, const u32* __restrict__ counts,
+                                                            const u64* __restrict__ pos, u64 W, u64* out) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 lane = (u32)lane_id();
+    if (lane < counts[w]) out[pos[w] + lane] = slots[w * RDF_WAVE + lane];
+}
+
+#ifdef RDF_LIGHT_STATS
+// dev instrumentation (make STATS=1): [0] items [1] wave iterations [2] candidate checks [3] groups visited
+// [4] sum of log2 sizes of searched groups [5] initially alive candidates [6] items with nseg > 1
+__device__ unsigned long long g_light_stats[8];
+#define LSTAT(i, v) do { if (lane_id() == 0) atomicAdd(&g_light_stats[i], (unsigned long long)(v)); } while (0)
+#else
+#define LSTAT(i, v) do { } while (0)
+#endif
 
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
-// multi-segment ones publish the candidates they kill with atomicOr and k_light_final emits the survivors.
+// multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
 __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
-                                                     const u64* __restrict__ choff, u64 W, u64* dead, u64* pairs,
-                                                     u64* npairs) {
+                                                     const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
+                                                     u64* dead, u32* arrive, u64* slots, u32* counts) {
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
-    const u32 d = find_dep(itemoff, v.C, w);
+    const u32 d = item_dep[w];
     const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
     const u64 nseg = (e0 - b0 + LIGHT_SEG - 1) / LIGHT_SEG;
     const u64 item = w - itemoff[d];
@@ -700,46 +801,80 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     u64 alive = alive0;
     const u64 b = b0 + seg * LIGHT_SEG;
     const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
-    for (u64 j0 = b; j0 < e && alive; j0 += RDF_WAVE) {
-        const u64 j = j0 + lane;
-        u32 g = NONE32;
-        if (j < e) {
-            g = v.dgrp[j];
-            if (g == piv || v.hbit[g] != LIGHT) g = NONE32;
+    LSTAT(0, 1);
+    LSTAT(5, __popcll(alive0));
+    LSTAT(6, nseg > 1);
+    // Few groups, many candidates (the common case: most dependents have a handful of groups): every lane
+    // tests its own candidate against the groups one after the other, so the serial chain is the number of
+    // groups rather than the number of candidates.
+    if (e - b <= (u64)__popcll(alive0) * ((e - b + RDF_WAVE - 1) / RDF_WAVE)) {
+        bool ok = cand != NONE32;
+        for (u64 j = b; j < e; ++j) {
+            if (!__any(ok)) break;
+            const u32 g = v.dgrp[j];
+            if (g == piv || v.hbit[g] != LIGHT) continue;
+            LSTAT(1, 1);
+            LSTAT(2, __popcll(__ballot(ok)));
+            if (ok) ok = bsearch_u32(v.gcap + v.goff[g], v.goff[g + 1] - v.goff[g], cand);
         }
-        const u32* gm = nullptr;
-        u64 gsz = 0;
-        if (g != NONE32) {
-            gm = v.gcap + v.goff[g];
-            gsz = v.goff[g + 1] - v.goff[g];
-        }
-        u64 todo = alive;
-        while (todo) {
-            const int bit = __ffsll((long long)todo) - 1;
-            todo &= todo - 1;
-            const u32 c = __shfl(cand, bit, RDF_WAVE);
-            const bool ok = (g == NONE32) || bsearch_u32(gm, gsz, c);
-            if (!__all(ok)) alive &= ~(1ull << bit);
+        alive = __ballot(ok);
+    } else {
+        // many groups: lanes take one group each and the alive candidates are tested one after the other
+        for (u64 j0 = b; j0 < e && alive; j0 += RDF_WAVE) {
+#ifdef RDF_LIGHT_STATS
+            {
+                const u64 jj = j0 + lane;
+                u32 gg = jj < e ? v.dgrp[jj] : NONE32;
+                const bool vis = gg != NONE32 && gg != piv && v.hbit[gg] == LIGHT;
+                const u32 lg = vis ? 64 - __builtin_clzll(v.goff[gg + 1] - v.goff[gg]) : 0;
+                LSTAT(1, 1);
+                LSTAT(2, __popcll(alive));
+                LSTAT(3, __popcll(__ballot(vis)));
+                LSTAT(4, (u64)wave_sum(lg) * __popcll(alive));
+            }
+#endif
+            const u64 j = j0 + lane;
+            u32 g = NONE32;
+            if (j < e) {
+                g = v.dgrp[j];
+                if (g == piv || v.hbit[g] != LIGHT) g = NONE32;
+            }
+            const u32* gm = nullptr;
+            u64 gsz = 0;
+            if (g != NONE32) {
+                gm = v.gcap + v.goff[g];
+                gsz = v.goff[g + 1] - v.goff[g];
+            }
+            u64 todo = alive;
+            while (todo) {
+                const int bit = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const u32 c = __shfl(cand, bit, RDF_WAVE);
+                const bool ok = (g == NONE32) || bsearch_u32(gm, gsz, c);
+                if (!__all(ok)) alive &= ~(1ull << bit);
+            }
         }
     }
+    const u64 slot = choff[d] + chunk;
     if (nseg == 1) {
-        emit_pairs(d, cand, alive, pairs, npairs);
-    } else if (lane == 0 && (alive0 & ~alive)) {
-        atomicOr(&dead[choff[d] + chunk], alive0 & ~alive);
+        slot_emit(slot, d, cand, alive, slots, counts);
+        return;
     }
-}
-
-__global__ __launch_bounds__(RDF_BLOCK) void k_light_final(CindView v, const u32* __restrict__ pivot,
-                                                           const u64* __restrict__ choff, u64 W,
-                                                           const u64* __restrict__ dead, u64* pairs, u64* npairs) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
-    const u32 d = find_dep(choff, v.C, w);
-    if (v.doff[d + 1] - v.doff[d] <= LIGHT_SEG) return;  // single segment: already emitted
-    const u64 chunk = w - choff[d];
-    const u32 cand = chunk_candidate(v, d, v.info[d], pivot[d], chunk);
-    const u64 alive = __ballot(cand != NONE32) & ~dead[w];
-    emit_pairs(d, cand, alive, pairs, npairs);
+    // several segments: publish the killed candidates; the last segment to arrive emits the survivors
+    // (device-scope atomics execute at the memory side, so the returned OR is the final mask)
+    u32 last = 0;
+    if (lane == 0) {
+        if (alive0 & ~alive) atomicOr(&dead[slot], alive0 & ~alive);
+        __threadfence();
+        last = atomicAdd(&arrive[slot], 1u) == (u32)(nseg - 1);
+    }
+    if (__shfl(last, 0, RDF_WAVE)) {
+        __threadfence();
+        u64 dm = 0;
+        if (lane == 0) dm = atomicOr(&dead[slot], 0ull);
+        dm = __shfl(dm, 0, RDF_WAVE);
+        slot_emit(slot, d, cand, alive0 & ~dm, slots, counts);
+    }
 }
 
 // explicit CSR offsets: eoff[d] = first pair with dep >= d
@@ -754,18 +889,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restric
 
 // minimality on explicit pairs -> output
 __global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const u64* __restrict__ pairs, u64 E, u32 rank,
-                                                              u32 nranks, u64* out, u64* nout) {
-    const u64 n_round = (E + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n_round; i += (u64)gridDim.x * RDF_BLOCK) {
-        u32 keep = 0;
-        u64 pr = 0;
-        if (i < E) {
-            pr = pairs[i];
-            const u32 d = (u32)(pr >> 32);
-            keep = (d % nranks == rank && rule_keep(v, d, (u32)pr)) ? 1u : 0u;
-        }
-        u64 pos = wave_append(nout, keep);
-        if (keep) out[pos] = pr;
+                                                              u32 nranks, u32* keep) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < E; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 pr = pairs[i];
+        const u32 d = (u32)(pr >> 32);
+        keep[i] = (d % nranks == rank && rule_keep(v, d, (u32)pr)) ? 1u : 0u;
     }
 }
 
@@ -941,7 +1069,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_members(const u64* __restri
 
 // per class: number of emission tiles = ceil(members / CLS_DT) * ceil(|L'| / CLS_LS)
 static constexpr u32 CLS_DT = 16;                    // dependents per tile
-static constexpr u32 CLS_LS = RDF_BLOCK * 4;         // list elements per tile (4 per thread, in registers)
+static constexpr u32 CLS_LS = RDF_BLOCK * 4;         // list elements per tile (staged in LDS)
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict__ coff, const u64* __restrict__ cchoff,
                                                            const u64* __restrict__ lwoff, u32 ncls, u32* ntiles) {
@@ -952,12 +1080,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict
     }
 }
 
-// streaming emission: each block loads CLS_LS list entries once and writes them for CLS_DT dependents
+// streaming emission: each block stages CLS_LS list entries in LDS once and writes them for CLS_DT
+// dependents.  A dependent's output run starts at an arbitrary offset, so lanes cover aligned pairs of
+// output slots: 16-byte stores in the interior, 8-byte ones only at the two ends of a run.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict__ keys, const u64* __restrict__ coff,
                                                           const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
                                                           const u32* __restrict__ lists, const u64* __restrict__ toff,
                                                           u32 ncls, const u32* __restrict__ selfpos,
                                                           const u64* __restrict__ obase, u64 out_base, u64* out) {
+    __shared__ u32 sl[CLS_LS];
+    __shared__ u32 s_dep[CLS_DT], s_sp[CLS_DT];
+    __shared__ u64 s_base[CLS_DT];
     __shared__ u32 s_m;
     if (threadIdx.x == 0) s_m = find_dep(toff, ncls, blockIdx.x);
     __syncthreads();
@@ -967,22 +1102,37 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict_
     const u64 t = blockIdx.x - toff[m];
     const u64 dt = t / nseg, seg = t % nseg;
     const u64 k0 = coff[m] + dt * CLS_DT, k1 = k0 + CLS_DT < coff[m + 1] ? k0 + CLS_DT : coff[m + 1];
-    u32 val[4];
-    u64 pos[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        pos[q] = seg * CLS_LS + (u64)q * RDF_BLOCK + threadIdx.x;
-        val[q] = pos[q] < len ? lists[lb + pos[q]] : 0u;
+    const u64 p0 = seg * CLS_LS, p1 = p0 + CLS_LS < len ? p0 + CLS_LS : len;
+    for (u64 i = threadIdx.x; i < p1 - p0; i += RDF_BLOCK) sl[i] = lists[lb + p0 + i];
+    if (threadIdx.x < k1 - k0) {  // the tile's dependents, loaded once instead of one dependent load chain each
+        const u64 i = k0 + threadIdx.x;
+        s_dep[threadIdx.x] = (u32)keys[i];
+        s_sp[threadIdx.x] = selfpos[i];
+        s_base[threadIdx.x] = obase[i];
     }
+    __syncthreads();
     for (u64 i = k0; i < k1; ++i) {
-        const u64 d = (u32)keys[i];
-        const u32 sp = selfpos[i];
-        const u64 base = out_base + obase[i];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (pos[q] < len && pos[q] != sp) {
-                const u64 o = base + pos[q] - ((sp != NONE32 && pos[q] > sp) ? 1u : 0u);
-                out[o] = (d << 32) | val[q];
+        const u64 d = s_dep[i - k0];
+        const u32 sp = s_sp[i - k0];
+        const bool in_seg = sp != NONE32 && sp >= p0 && sp < p1;
+        const u64 ob = out_base + s_base[i - k0] + p0 - ((sp != NONE32 && sp < p0) ? 1 : 0);
+        const u64 oe = ob + (p1 - p0) - (in_seg ? 1 : 0);
+        const u64 skip = in_seg ? sp - p0 : ~0ull;  // index within the segment that is not emitted
+        for (u64 a = (ob >> 1) + threadIdx.x; 2 * a < oe; a += RDF_BLOCK) {
+            const u64 o0 = 2 * a, o1 = o0 + 1;
+            const bool in0 = o0 >= ob, in1 = o1 < oe;
+            const u64 q0 = o0 - ob, q1 = o1 - ob;  // k-th element of the run -> segment index k or k + 1
+            const u64 v0 = in0 ? ((d << 32) | sl[q0 + (q0 >= skip ? 1 : 0)]) : 0;
+            const u64 v1 = in1 ? ((d << 32) | sl[q1 + (q1 >= skip ? 1 : 0)]) : 0;
+            if (in0 && in1) {
+                u64x2 w;
+                w.x = v0;
+                w.y = v1;
+                *(u64x2*)(out + o0) = w;
+            } else if (in0) {
+                out[o0] = v0;
+            } else if (in1) {
+                out[o1] = v1;
             }
         }
     }

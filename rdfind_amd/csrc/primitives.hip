@@ -143,93 +143,155 @@ hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32
 }
 
 // ------------------------------------------------------------------------------------------------
-// LSD radix sort of u64 keys
+// LSD radix sort of u64 keys, 8-bit digits, reduce-then-scan per pass:
+//   count:   per-tile digit histogram (wave ballots give each lane its same-digit peers; one leader lane
+//            per digit adds the peer count -- no LDS atomics, so a skewed digit costs nothing extra)
+//   scan:    device exclusive scan of the digit-major [256][tiles] histogram
+//   scatter: stable in-tile ranks (peers + per-wave running counters), the tile is reordered by digit in
+//            LDS, then written out as contiguous per-digit runs (coalesced stores instead of 8-byte
+//            scattered ones).
 
 static constexpr int RS_ITEMS = 16;                              // keys per lane per tile
 static constexpr int RS_TILE = RDF_BLOCK * RS_ITEMS;             // 4096 keys per tile
 static constexpr int RS_WAVE_KEYS = RDF_WAVE * RS_ITEMS;         // 1024 keys per wave
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_radix_hist(const u64* __restrict__ keys, u64 n, int shift,
-                                                          u32* __restrict__ hist, u32 num_tiles) {
-    __shared__ u32 cnt[256];
-    cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const u64 base = (u64)blockIdx.x * RS_TILE;
+// lanes of the wave whose key is valid and has the same 8-bit digit as this lane (0 for invalid lanes)
+__device__ inline u64 digit_peers(u32 d, bool valid) {
+    u64 peers = __ballot(valid);
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; ++i) {
-        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
-        if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & 255], 1u);
+    for (int b = 0; b < 8; ++b) {
+        const u64 bb = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    return valid ? peers : 0ull;
+}
+
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+
+// 16-byte loads of a tile (two consecutive keys per lane and row); out-of-range keys read as 0
+__device__ inline void load_tile_pairs(const u64* __restrict__ keys, u64 n, u64 tbase, u64 (&k)[RS_ITEMS]) {
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS / 2; ++r) {
+        const u64 idx = tbase + 2ull * ((u64)r * RDF_BLOCK + threadIdx.x);
+        if (idx + 1 < n) {
+            const u64x2_t v = *(const u64x2_t*)(keys + idx);
+            k[2 * r] = v.x;
+            k[2 * r + 1] = v.y;
+        } else {
+            k[2 * r] = idx < n ? keys[idx] : 0;
+            k[2 * r + 1] = 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict__ keys, u64 n, int shift,
+                                                           u32* __restrict__ hist, u32 num_tiles) {
+    __shared__ u32 wcnt[RDF_WAVES_PER_BLOCK][256];
+    const int lane = lane_id();
+    const int wave = threadIdx.x / RDF_WAVE;
+#pragma unroll
+    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) wcnt[w][threadIdx.x] = 0;
+    __syncthreads();
+    const u64 tbase = (u64)blockIdx.x * RS_TILE;
+    u64 k[RS_ITEMS];
+    load_tile_pairs(keys, n, tbase, k);  // counting is order-free: any assignment of keys to lanes works
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const u64 idx = tbase + 2ull * ((u64)(r / 2) * RDF_BLOCK + threadIdx.x) + (r & 1);
+        const bool valid = idx < n;
+        const u32 d = (u32)((k[r] >> shift) & 255);
+        const u64 peers = digit_peers(d, valid);
+        if (valid && ((peers >> lane) >> 1) == 0) wcnt[wave][d] += (u32)__popcll(peers);
     }
     __syncthreads();
-    hist[(u64)threadIdx.x * num_tiles + blockIdx.x] = cnt[threadIdx.x];
+    u32 sum = 0;
+#pragma unroll
+    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) sum += wcnt[w][threadIdx.x];
+    hist[(u64)threadIdx.x * num_tiles + blockIdx.x] = sum;
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
                                                              int shift, const u32* __restrict__ offs, u32 num_tiles) {
+    __shared__ __align__(16) u64 skeys[RS_TILE];
     __shared__ u32 wcount[RDF_WAVES_PER_BLOCK][256];
+    __shared__ u32 tstart[256];
     __shared__ u32 gbase[256];
+    __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
     const int lane = lane_id();
     const int wave = threadIdx.x / RDF_WAVE;
 #pragma unroll
     for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) wcount[w][threadIdx.x] = 0;
     gbase[threadIdx.x] = offs[(u64)threadIdx.x * num_tiles + blockIdx.x];
+    const u64 tbase = (u64)blockIdx.x * RS_TILE;
+    const u64 tn = n - tbase < (u64)RS_TILE ? n - tbase : (u64)RS_TILE;
+    {   // stage the tile through LDS: 16-byte global loads, then each wave reads its contiguous sub-range
+        u64 kin[RS_ITEMS];
+        load_tile_pairs(keys, n, tbase, kin);
+#pragma unroll
+        for (int r = 0; r < RS_ITEMS / 2; ++r) {
+            const u32 p = 2u * ((u32)r * RDF_BLOCK + threadIdx.x);
+            *(u64x2_t*)(skeys + p) = u64x2_t{kin[2 * r], kin[2 * r + 1]};
+        }
+    }
     __syncthreads();
-
-    const u64 wbase = (u64)blockIdx.x * RS_TILE + (u64)wave * RS_WAVE_KEYS;
     u64 k[RS_ITEMS];
     u32 rank[RS_ITEMS];
     const u64 lt = lanemask_lt();
+    const u32 wofs = (u32)wave * RS_WAVE_KEYS;
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) k[r] = skeys[wofs + (u32)r * RDF_WAVE + lane];
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        u64 idx = wbase + (u64)r * RDF_WAVE + lane;
-        bool valid = idx < n;
-        k[r] = valid ? keys[idx] : 0;
-        u32 d = (u32)((k[r] >> shift) & 255);
-        // peer mask: lanes with the same digit (invalid lanes form their own group via a 9th bit)
-        u64 peers = __ballot(valid);
-        if (!valid) peers = ~peers;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            u64 bb = __ballot((d >> b) & 1);
-            peers &= ((d >> b) & 1) ? bb : ~bb;
-        }
-        u32 before = (u32)__popcll(peers & lt);
-        u32 old = valid ? wcount[wave][d] : 0;
+        const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn;
+        const u32 d = (u32)((k[r] >> shift) & 255);
+        const u64 peers = digit_peers(d, valid);
+        const u32 before = (u32)__popcll(peers & lt);
+        const u32 old = valid ? wcount[wave][d] : 0;
         // the highest peer lane publishes the new running count (reads above precede this write)
-        bool last = valid && ((peers >> lane) >> 1) == 0;
-        if (last) wcount[wave][d] = old + before + 1;
+        if (valid && ((peers >> lane) >> 1) == 0) wcount[wave][d] = old + before + 1;
         rank[r] = old + before;
     }
     __syncthreads();
-    {   // exclusive prefix over waves per digit
+    {   // exclusive prefix over waves per digit, then over digits for the tile
         u32 run = 0;
 #pragma unroll
         for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
-            u32 c = wcount[w][threadIdx.x];
+            const u32 c = wcount[w][threadIdx.x];
             wcount[w][threadIdx.x] = run;
             run += c;
         }
+        u32 total;
+        tstart[threadIdx.x] = block_exclusive_scan<u32>(run, lds_wave, &total);
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        u64 idx = wbase + (u64)r * RDF_WAVE + lane;
-        if (idx < n) {
-            u32 d = (u32)((k[r] >> shift) & 255);
-            out[(u64)gbase[d] + wcount[wave][d] + rank[r]] = k[r];
+        if (wofs + (u32)r * RDF_WAVE + lane < tn) {
+            const u32 d = (u32)((k[r] >> shift) & 255);
+            skeys[tstart[d] + wcount[wave][d] + rank[r]] = k[r];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RS_ITEMS; ++i) {
+        const u32 p = (u32)i * RDF_BLOCK + threadIdx.x;
+        if (p < tn) {
+            const u64 key = skeys[p];
+            const u32 d = (u32)((key >> shift) & 255);
+            out[(u64)gbase[d] + (p - tstart[d])] = key;
         }
     }
 }
 
-hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st) {
-    if (n < 2 || bits <= 0) return hipSuccess;
+hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st) {
+    if (n < 2 || hi <= lo) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
     const u64 hn = (u64)tiles * 256;
     u32* hist = (u32*)ws.scratch(hn * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
-    for (int shift = 0; shift < bits; shift += 8) {
-        hipLaunchKernelGGL(k_radix_hist, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, hist, tiles);
+    for (int shift = lo; shift < hi; shift += 8) {
+        hipLaunchKernelGGL(k_radix_count, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, hist, tiles);
         hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, nullptr, st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_radix_scatter, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, hist, tiles);
@@ -238,6 +300,10 @@ hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits,
         tmp = t;
     }
     return hipGetLastError();
+}
+
+hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st) {
+    return radix_sort_u64_bits(ws, keys, tmp, n, 0, bits, st);
 }
 
 }  // namespace rdf

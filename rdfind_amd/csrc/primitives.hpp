@@ -56,5 +56,8 @@ hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32
 // LSD radix sort on the low `bits` bits; keys/tmp are swapped so that `keys` holds the result.
 // Uses workspace slots 0 and 1.  Requires n < 2^32.
 hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st);
+// Stable sort on bits [lo, hi) only (8 bits per pass from lo; bits at or above the last pass's top must be
+// zero or already ordered).  Keys that arrive ordered by their low bits stay so within equal [lo, hi).
+hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st);
 
 }  // namespace rdf

@@ -33,6 +33,8 @@ struct rdf_ctx {
 
     // frequent conditions
     u32 ms = 1;
+    DevBuf frank, fval, fext;
+    u32 U = 0, Us = 0, Up = 0;
     DevBuf cnt, tkeys, tcnt, bkeys, bkeys_tmp, lkeys, lvals, flags, pos;
     u64 B = 0, lcap = 0;
     std::vector<u64> h_bkeys;
@@ -70,6 +72,7 @@ struct rdf_ctx {
     u64 x_count = 0, x_recv_count = 0;
     u32 x_bytes = 8;
     bool x_imported = true;
+    DevBuf item_dep, eblk, lslot;
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0;
     u64* out_ptr = nullptr;
@@ -79,25 +82,32 @@ struct rdf_ctx {
     hipEvent_t ev[8] = {};
     float stage_ms[3] = {0, 0, 0};
     // per kernel-family device timers (events on the context stream)
-    hipEvent_t tev[2 * RDF_NUM_TIMERS] = {};
-    bool tused[RDF_NUM_TIMERS] = {};
+    static constexpr int kTSeg = 6;  // segments per timer (a kernel family may run in several places)
+    hipEvent_t tev[2 * RDF_NUM_TIMERS * kTSeg] = {};
+    int tn[RDF_NUM_TIMERS] = {};
     float tms[RDF_NUM_TIMERS] = {};
     u64 sort_passes_records = 0, sort_passes_pairs = 0;
     u64 heavy_candidates = 0;
 };
 
 static void tbegin(rdf_ctx* c, int id) {
-    (void)hipEventRecord(c->tev[2 * id], c->stream);
-    c->tused[id] = true;
+    if (c->tn[id] < rdf_ctx::kTSeg) (void)hipEventRecord(c->tev[2 * (id * rdf_ctx::kTSeg + c->tn[id])], c->stream);
 }
-static void tend(rdf_ctx* c, int id) { (void)hipEventRecord(c->tev[2 * id + 1], c->stream); }
-// call after a stream sync: fold recorded timers of [lo, hi) into tms
+static void tend(rdf_ctx* c, int id) {
+    if (c->tn[id] < rdf_ctx::kTSeg) (void)hipEventRecord(c->tev[2 * (id * rdf_ctx::kTSeg + c->tn[id]) + 1], c->stream);
+    c->tn[id]++;
+}
+// call after a stream sync: fold the recorded segments of timers [lo, hi) into tms
 static void tcollect(rdf_ctx* c, int lo, int hi) {
     for (int i = lo; i < hi; ++i) {
-        float ms = 0;
-        if (c->tused[i] && hipEventElapsedTime(&ms, c->tev[2 * i], c->tev[2 * i + 1]) == hipSuccess) c->tms[i] = ms;
-        else c->tms[i] = 0;
-        c->tused[i] = false;
+        float total = 0;
+        for (int k = 0; k < std::min(c->tn[i], rdf_ctx::kTSeg); ++k) {
+            float ms = 0;
+            const int e = 2 * (i * rdf_ctx::kTSeg + k);
+            if (hipEventElapsedTime(&ms, c->tev[e], c->tev[e + 1]) == hipSuccess) total += ms;
+        }
+        c->tms[i] = total;
+        c->tn[i] = 0;
     }
 }
 
@@ -166,7 +176,7 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
     for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
-    for (int i = 0; i < 2 * RDF_NUM_TIMERS && e == hipSuccess; ++i) e = hipEventCreate(&c->tev[i]);
+    for (int i = 0; i < 2 * RDF_NUM_TIMERS * rdf_ctx::kTSeg && e == hipSuccess; ++i) e = hipEventCreate(&c->tev[i]);
     if (e != hipSuccess) {
         rdf_ctx_destroy(c);
         return RDF_ERR_HIP;
@@ -181,7 +191,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->scal, &c->ts, &c->tp, &c->to, &c->cnt, &c->tkeys, &c->tcnt, &c->bkeys, &c->bkeys_tmp,
                       &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
-                      &c->fcap, &c->info, &c->fk, &c->gflag, &c->gexcl, &c->goff, &c->gcap, &c->gid, &c->csup,
+                      &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->gflag, &c->gexcl, &c->goff, &c->gcap, &c->gid, &c->csup,
                       &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->out,
@@ -189,7 +199,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
-                      &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->item_dep, &c->eblk, &c->lslot, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
@@ -265,6 +275,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
     c->ms = min_support ? min_support : 1;  // a support of 0 admits exactly the captures that exist
+    for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
     HIP_TRY(c, hipEventRecord(c->ev[0], st));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
     ENSURE(c, cnt, 3ull * V * 4);
@@ -273,15 +284,26 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     if (n)
         hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                            st, c->s, c->p, c->o, n, V, c->cnt.as<u32>());
+    ENSURE(c, frank, 3ull * V * 4);
+    ENSURE(c, flags, 3ull * V * 4);
+    hipLaunchKernelGGL(k_frank_flags, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(),
+                       3ull * V, c->ms, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->frank.as<u32>(), 3ull * V, (u32*)dscal(c, 6), st));
     tend(c, RDF_T_UNARY);
     if (n)
         hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p,
                            c->o, n, V, c->ms, c->cnt.as<u32>(), dscal(c, 3));
     hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->cnt.as<u32>(), V, c->ms, dscal(c, 0));
-    rdf_status rs = read_scalars(c, 4);
+    rdf_status rs = read_scalars(c, 7);
     if (rs) return rs;
     u64 nfreq[3] = {c->hscal[0], c->hscal[1], c->hscal[2]};
+    c->U = (u32)c->hscal[6];
+    c->Us = (u32)nfreq[0];
+    c->Up = (u32)nfreq[1];
+    ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
+    hipLaunchKernelGGL(k_frank_final, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(),
+                       3ull * V, V, c->ms, c->frank.as<u32>(), c->fval.as<u32>());
     const u64 E = c->hscal[3];
     const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
     ENSURE(c, tkeys, tcap * 8);
@@ -386,11 +408,11 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
-    const u64 ncap = 6ull * V + c->B;
-    const int capbits = bits_for(ncap - 1);
+    const u64 ncap = 2ull * c->U + c->B;  // compact candidate captures (k_frank_final)
+    const int capbits = bits_for(ncap ? ncap - 1 : 0);
     const int joinbits = bits_for(V - 1);
     if (capbits + joinbits > 64) return fail(c, RDF_ERR_LIMIT, "join+capture bits exceed 64");
-    if (ncap >= (1ull << 32)) return fail(c, RDF_ERR_LIMIT, "capture id space exceeds 2^32");
+    if (6ull * V + c->B >= (1ull << 32)) return fail(c, RDF_ERR_LIMIT, "capture id space exceeds 2^32");
     c->capbits = capbits;
     c->ncap = ncap;
     HIP_TRY(c, hipEventRecord(c->ev[2], st));
@@ -399,10 +421,18 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     ENSURE(c, rec, cap_rec * 8);
     ENSURE(c, rec_tmp, cap_rec * 8);
     tbegin(c, RDF_T_EMIT);
-    if (n)
-        hipLaunchKernelGGL(k_emit_records, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n,
-                           V, c->ms, c->cnt.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits,
-                           c->rank, c->nranks, c->rec.as<u64>(), dscal(c, 0));
+    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const u64 per = n ? (n + eg - 1) / eg : 0;
+    ENSURE(c, eblk, (eg + 1ull) * 8);
+    if (n) {
+        hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits, c->rank,
+                           c->nranks, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr);
+        HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
+        hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits, c->rank,
+                           c->nranks, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>());
+    }
     tend(c, RDF_T_EMIT);
     TRY(read_scalars(c, 1));
     const u64 J = c->hscal[0];
@@ -441,13 +471,17 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fidx.as<u32>(), ncap, c->fidx.as<u32>() + ncap, st));
     u32 C = 0, Cu = 0;
     TRY(read_u32(c, c->fidx.as<u32>() + ncap, &C));
-    TRY(read_u32(c, c->fidx.as<u32>() + 6ull * V, &Cu));
+    TRY(read_u32(c, c->fidx.as<u32>() + 2ull * c->U, &Cu));
     c->C = C;
     c->Cu = Cu;
     ENSURE(c, fcap, std::max<u64>(C, 1) * 4);
     ENSURE(c, info, std::max<u64>(C, 1) * sizeof(CapInfo));
     hipLaunchKernelGGL(k_compact_captures, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->support.as<u32>(), c->fidx.as<u32>(), ncap, c->ms, c->fcap.as<u32>(), c->info.as<CapInfo>());
+    ENSURE(c, fext, std::max<u64>(C, 1) * 4);
+    if (C)
+        hipLaunchKernelGGL(k_external_ids, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fcap.as<u32>(), C,
+                           2u * c->U, V, c->fval.as<u32>(), c->Us, c->Up, c->fext.as<u32>());
     // distinct records of frequent captures, capture ids made compact
     ENSURE(c, pos, std::max<u64>(J, 1) * 8);
     if (J)
@@ -495,7 +529,8 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
         u64* tt = c->rec_tmp.as<u64>();
         hipLaunchKernelGGL(k_make_tkeys, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
                            c->gid.as<u32>(), Jf, tk);
-        HIP_TRY(c, radix_sort_u64(c->ws, tk, tt, Jf, 32 + bits_for(C ? C - 1 : 0), st));
+        // records are in group order, so a stable sort on the capture bits alone keeps each list sorted
+        HIP_TRY(c, radix_sort_u64_bits(c->ws, tk, tt, Jf, 32, 32 + bits_for(C ? C - 1 : 0), st));
         hipLaunchKernelGGL(k_low32, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, c->dgrp.as<u32>());
         hipLaunchKernelGGL(k_key_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, C,
                            c->doff.as<u64>());
@@ -568,11 +603,11 @@ static rdf_status g_heavy_binary(rdf_ctx* c, u64 thr, u32 base) {
     ENSURE(c, pedges_tmp, std::max<u64>(2ull * Cb, 1) * 8);
     if (Cb) {
         hipLaunchKernelGGL(k_binary_info, dim3(grid_for(Cb, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fcap.as<u32>(),
-                           c->fidx.as<u32>(), c->bkeys.as<u64>(), C, Cu, V, c->bcomp.as<u32>(), c->bkeyc.as<u64>(),
-                           c->pedges.as<u64>(), c->info.as<CapInfo>());
+                           c->fidx.as<u32>(), c->bkeys.as<u64>(), c->frank.as<u32>(), C, Cu, V, 2u * c->U,
+                           c->bcomp.as<u32>(), c->bkeyc.as<u64>(), c->pedges.as<u64>(), c->info.as<CapInfo>());
         u64* k = c->pedges.as<u64>();
         u64* t = c->pedges_tmp.as<u64>();
-        HIP_TRY(c, radix_sort_u64(c->ws, k, t, 2ull * Cb, 32 + bits_for(Cu ? Cu - 1 : 0), st));
+        HIP_TRY(c, radix_sort_u64_bits(c->ws, k, t, 2ull * Cb, 32, 32 + bits_for(Cu ? Cu - 1 : 0), st));  // edges in binary order
         if (k != c->pedges.as<u64>()) std::swap(c->pedges, c->pedges_tmp);
     }
     hipLaunchKernelGGL(k_parents_csr, dim3(grid_for(std::max<u64>(2ull * Cb, Cu + 1ull), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0,
@@ -670,6 +705,8 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->pseg.as<u32>(), c->psegoff.as<u64>(), C, c->psegoff.as<u64>() + C, st));
         HIP_TRY(c, hipMemsetAsync(c->pbest.p, 0xff, (u64)C * 8, st));
         HIP_TRY(c, hipMemsetAsync(c->pnl.p, 0, (u64)C * 4, st));
+        hipLaunchKernelGGL(k_pivot_short, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
+                           c->pnl.as<u32>());
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
@@ -700,32 +737,50 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI) {
 static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64* E) {
     hipStream_t st = c->stream;
     const u64 cap_pairs = std::max<u64>(WL * RDF_WAVE, 1);
-    ENSURE(c, epairs, cap_pairs * 8);
-    ENSURE(c, epairs_tmp, cap_pairs * 8);
-    ENSURE(c, dead, std::max<u64>(WL, 1) * 8);
-    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, std::max<u64>(WL, 1) * 8, st));
-    HIP_TRY(c, hipMemsetAsync(dscal(c, 0), 0, 8, st));
+    ENSURE(c, epairs_tmp, cap_pairs * 8);  // one 64-entry slot per chunk
+    ENSURE(c, dead, std::max<u64>(WL, 1) * 12);  // dead masks, then per-chunk arrival counters
+    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, std::max<u64>(WL, 1) * 12, st));
+    ENSURE(c, lslot, std::max<u64>(WL, 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, std::max<u64>(WL, 1) * 4, st));
+    ENSURE(c, item_dep, std::max<u64>(WI, 1) * 4);
     tbegin(c, RDF_T_LIGHT);
     if (WI)
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->itoffl.as<u64>(),
+                           c->C, c->item_dep.as<u32>());
+    if (WI)
         hipLaunchKernelGGL(k_light, dim3((unsigned)((WI + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
-                           0, st, v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->choffl.as<u64>(), WI, c->dead.as<u64>(),
-                           c->epairs.as<u64>(), dscal(c, 0));
-    if (WI > WL)  // some dependent spans several segments
-        hipLaunchKernelGGL(k_light_final, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffl.as<u64>(), WL, c->dead.as<u64>(),
-                           c->epairs.as<u64>(), dscal(c, 0));
+                           0, st, v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
+                           c->dead.as<u64>(),
+                           (u32*)(c->dead.as<u64>() + std::max<u64>(WL, 1)), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+    ENSURE(c, pos, (WL + 1) * 8);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
+    TRY(read_u64(c, c->pos.as<u64>() + WL, E));
+    ENSURE(c, epairs, std::max<u64>(*E, 1) * 8);
+    if (WL)
+        hipLaunchKernelGGL(k_slot_compact, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
+                           0, st, c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>());
     tend(c, RDF_T_LIGHT);
-    TRY(read_u64(c, dscal(c, 0), E));
+#ifdef RDF_LIGHT_STATS
+    {
+        unsigned long long h[8];
+        HIP_TRY(c, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_light_stats), sizeof(h)));
+        fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu E=%llu items=%llu iters=%llu checks=%llu groups=%llu logsum=%llu alive0=%llu multiseg=%llu\n",
+                (unsigned long long)WI, (unsigned long long)WL, (unsigned long long)*E, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+        memset(h, 0, sizeof(h));
+        HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_light_stats), h, sizeof(h)));
+    }
+#endif
     return RDF_OK;
 }
 
 // sort the explicit pairs (epairs[0, E)) and index them: v.eoff / v.ebin / v.epairs
-static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E) {
+// (presorted: the single-GPU light pass already emits them in (dep, ref) order, chunk by chunk)
+static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorted) {
     hipStream_t st = c->stream;
     const u32 C = c->C;
     ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
     tbegin(c, RDF_T_ESORT);
-    {
+    if (!presorted) {
         u64* k = c->epairs.as<u64>();
         u64* t = c->epairs_tmp.as<u64>();
         HIP_TRY(c, radix_sort_u64(c->ws, k, t, E, 32 + bits_for(C ? C - 1 : 0), st));
@@ -736,7 +791,7 @@ static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E) {
     hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->epairs.as<u64>(), E, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
     tend(c, RDF_T_ESORT);
-    c->sort_passes_pairs = (u64)((32 + bits_for(C ? C - 1 : 0) + 7) / 8) * E;
+    c->sort_passes_pairs = presorted ? 0 : (u64)((32 + bits_for(C ? C - 1 : 0) + 7) / 8) * E;
     v.eoff = c->eoff.as<u64>();
     v.epairs = c->epairs.as<u64>();
     v.ebin = c->ebin.as<u64>();
@@ -862,14 +917,19 @@ static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* 
 static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
     hipStream_t st = c->stream;
     ENSURE(c, out, std::max<u64>(E + H + HC, 1) * 8);
-    HIP_TRY(c, hipMemsetAsync(dscal(c, 1), 0, 8, st));
+    ENSURE(c, flags, std::max<u64>(E, 1) * 4);
+    ENSURE(c, pos, (E + 1) * 8);
     tbegin(c, RDF_T_RULES);
     if (E)
         hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
-                           c->epairs.as<u64>(), E, c->rank, c->nranks, c->out.as<u64>(), dscal(c, 1));
+                           c->epairs.as<u64>(), E, c->rank, c->nranks, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), E, c->pos.as<u64>() + E, st));
+    if (E)
+        hipLaunchKernelGGL(k_compact_u64, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E,
+                           c->flags.as<u32>(), c->pos.as<u64>(), c->out.as<u64>());
     tend(c, RDF_T_RULES);
     u64 K = 0;
-    TRY(read_u64(c, dscal(c, 1), &K));
+    TRY(read_u64(c, c->pos.as<u64>() + E, &K));
     tbegin(c, RDF_T_HWRITE);
     if (WH)
         hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
@@ -894,7 +954,7 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     c->h_fcap.resize(C);
     c->h_csup.resize(C);
     if (C) {
-        HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fcap.p, (u64)C * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fext.p, (u64)C * 4, hipMemcpyDeviceToHost));
         HIP_TRY(c, hipMemcpy(c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
     }
     rdf_cind_stats& s = c->cstats;
@@ -934,7 +994,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     TRY(d_light(c, v, WI, WL, &E));
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
-    TRY(d_explicit_index(c, v, E));
+    TRY(d_explicit_index(c, v, E, true));
     TRY(d_heavy_count(c, v, WH, &H));
     TRY(d_classes_single(c, v, &HC, &NT));
     TRY(d_emit(c, v, E, WH, H, HC, NT));
@@ -1120,7 +1180,7 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     HIP_TRY(c, hipMemcpyAsync(c->epairs.p, c->xrecv.p, E * 8, hipMemcpyDeviceToDevice, st));
     c->sh_E = E;
     CindView v = make_view(c, c->sh_flags);
-    TRY(d_explicit_index(c, v, E));
+    TRY(d_explicit_index(c, v, E, false));
     u64 H = 0;
     TRY(d_heavy_count(c, v, c->sh_WH, &H));
     c->sh_H = H;
@@ -1356,7 +1416,7 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     HIP_TRY(c, hipMemsetAsync(dscal(c, 7), 0, 8, c->stream));
     if (c->n_out)
         hipLaunchKernelGGL(k_checksum, dim3(grid_for(c->n_out, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
-                           c->out_ptr, c->n_out, c->fcap.as<u32>(), dscal(c, 7));
+                           c->out_ptr, c->n_out, c->fext.as<u32>(), dscal(c, 7));
     u64 v = 0;
     rdf_status rs = read_u64(c, dscal(c, 7), &v);
     *checksum = v;
