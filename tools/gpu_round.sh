@@ -1,0 +1,27 @@
+#!/bin/bash
+# usage (on the GPU box via gpurun): tools/gpu_round.sh <tag> [tests|bench|prof]...
+# Each GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+TAG=$1; shift
+mkdir -p gpurun_out
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/tests_$TAG.log; exit 1; } ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
+        || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
+      cat gpurun_out/bench_$TAG.json ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 \
+        || { echo "prof failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
+      find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG.kernel_stats.csv \;
+      head -25 gpurun_out/prof_$TAG.kernel_stats.csv ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps ok"
