@@ -30,6 +30,21 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
 
+# timer family -> the kernel whose rocprofv3 PMC traffic (profiles/pmc_<config>.json, tools/pmc.sh) is reported
+FAMILY_KERNEL = {"cemit": "k_class_emit", "light": "k_light", "unary": "k_unary_count", "emit": "k_emit_records",
+                 "sort": "k_radix_scatter", "hwrite": "k_heavy", "hcount": "k_heavy"}
+
+
+def pmc_traffic(config, family):
+    """HBM bytes per launch of the family's kernel from the committed PMC summary (FETCH_SIZE x2 + WRITE_SIZE,
+    corrected as MI355X_MICROARCH.md prescribes), or None when no summary for this config is committed."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    k = FAMILY_KERNEL.get(family)
+    if not k or not os.path.exists(path):
+        return None
+    ent = json.load(open(path)).get(k)
+    return int(ent["hbm_bytes"]) if ent else None
+
 
 def algorithmic_bytes(name, d, gs, cs, kt_counts):
     """Minimal HBM bytes a kernel family must move per launch (DESIGN.md 'Kernels and rooflines')."""
@@ -43,10 +58,11 @@ def algorithmic_bytes(name, d, gs, cs, kt_counts):
         return 16 * kt_counts["sort_passes_records"]    # read + write each record once per 8-bit pass
     if name == "cemit":
         n_out = cs["n_class_cinds"]
-        return 8 * n_out + 4 * n_out // 16            # 8-B (dep, ref) records written; list re-read once per 16 deps
+        return 4 * n_out                                # 4-B ref per CIND written (dependent-run output); the shared
+                                                        # class lists (< 1 MB) are read from L2
     if name in ("hwrite", "hcount"):
         cand = cs["n_heavy_candidates"]
-        out = 8 * cs["n_cinds"] if name == "hwrite" else 4 * cs["n_heavy_chunks"]
+        out = 4 * cs["n_cinds"] if name == "hwrite" else 4 * cs["n_heavy_chunks"]
         return 20 * cand + out                          # candidate ids + 16-B capture info, output records
     return None
 
@@ -143,7 +159,8 @@ def main():
         if b is not None and kt[name] > 0:
             achieved = b / (kt[name] * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_traffic(args.config, name) if args.scale == 1.0 and world == 1 else None,
                     "ms": round(kt[name], 4), "bytes_per_launch": int(b), "dominant_kernel": dominant,
                     "dominant_ms": round(kt[dominant], 4)}
             break

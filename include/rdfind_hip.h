@@ -22,7 +22,9 @@
  * Conventions (mirroring the reference's one-UDF-instance-per-task model):
  *   - inputs are borrowed and copied to HBM before the call returns (rdf_set_triples), or borrowed
  *     device pointers that must stay valid until the next rdf_set_triples* call;
- *   - results are library-owned and device-resident until copied out or the next call;
+ *   - results are library-owned and device-resident until copied out or the next call.  In HBM the
+ *     result is CindSet-shaped (ALG/data/CindSet.scala:9-13): one u32 ref per CIND, grouped in runs that
+ *     share a dependent (run table: start offset + dependent), 4 B per CIND; rdf_copy_cinds* expand it;
  *   - no exceptions cross the ABI: every call returns rdf_status (0 = OK, < 0 = error) and
  *     rdf_last_error() describes the last failure; errors are sticky per call, not per context;
  *   - a context is not thread-safe; different contexts (one per GPU) may run concurrently.

@@ -786,6 +786,7 @@ __device__ unsigned long long g_light_stats[8];
 __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
                                                      const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
                                                      u64* dead, u32* arrive, u64* slots, u32* counts) {
+    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_LDS];
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -807,15 +808,38 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     // Few groups, many candidates (the common case: most dependents have a handful of groups): every lane
     // tests its own candidate against the groups one after the other, so the serial chain is the number of
     // groups rather than the number of candidates.
+    // A group of at most LIGHT_LDS captures is staged into the wave's LDS slice with one coalesced load
+    // per lane, so the search costs one global round trip instead of log2(size) dependent ones.
     if (e - b <= (u64)__popcll(alive0) * ((e - b + RDF_WAVE - 1) / RDF_WAVE)) {
         bool ok = cand != NONE32;
+        u32* buf = s_light[threadIdx.x / RDF_WAVE];
         for (u64 j = b; j < e; ++j) {
             if (!__any(ok)) break;
             const u32 g = v.dgrp[j];
             if (g == piv || v.hbit[g] != LIGHT) continue;
             LSTAT(1, 1);
             LSTAT(2, __popcll(__ballot(ok)));
-            if (ok) ok = bsearch_u32(v.gcap + v.goff[g], v.goff[g + 1] - v.goff[g], cand);
+            const u64 gb = v.goff[g];
+            const u32 gsz = (u32)(v.goff[g + 1] - gb);
+            if (gsz <= LIGHT_LDS) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf before the refill
+                __builtin_amdgcn_wave_barrier();
+                for (u32 k = lane; k < gsz; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (ok) {
+                    u32 lo = 0, hi = gsz;
+                    while (lo < hi) {
+                        const u32 mid = (lo + hi) >> 1;
+                        if (buf[mid] < cand) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    ok = lo < gsz && buf[lo] == cand;
+                }
+            } else if (ok) {
+                ok = bsearch_u32(v.gcap + gb, gsz, cand);
+            }
         }
         alive = __ballot(ok);
     } else {
@@ -905,7 +929,7 @@ static constexpr u32 HEAVY_TILE = 1;  // 8 measured 60% slower (fewer independen
 template <bool WRITE>
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ choff,
                                                      u64 W, u32* counts, const u64* __restrict__ woff, u64 out_base,
-                                                     u64* out) {
+                                                     u32* out) {
     const u64 w0 = ((u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE) * HEAVY_TILE;
     if (w0 >= W) return;
     const int lane = lane_id();
@@ -931,7 +955,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy(CindView v, const u32* __re
         if (!WRITE) {
             if (lane == 0) counts[w] = (u32)__popcll(kept);
         } else if (keep) {
-            out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = ((u64)d << 32) | cand;
+            out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = cand;  // run of d (k_output_runs)
         }
     }
 }
@@ -1068,8 +1092,15 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_members(const u64* __restri
 }
 
 // per class: number of emission tiles = ceil(members / CLS_DT) * ceil(|L'| / CLS_LS)
-static constexpr u32 CLS_DT = 16;                    // dependents per tile
-static constexpr u32 CLS_LS = RDF_BLOCK * 4;         // list elements per tile (staged in LDS)
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+#ifndef RDF_CLS_DT
+#define RDF_CLS_DT 8
+#endif
+#ifndef RDF_CLS_LS
+#define RDF_CLS_LS 16384
+#endif
+static constexpr u32 CLS_DT = RDF_CLS_DT;            // dependents per tile
+static constexpr u32 CLS_LS = RDF_CLS_LS;            // list elements per tile (staged in LDS; power of two)
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict__ coff, const u64* __restrict__ cchoff,
                                                            const u64* __restrict__ lwoff, u32 ncls, u32* ntiles) {
@@ -1080,18 +1111,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict
     }
 }
 
-// streaming emission: each block stages CLS_LS list entries in LDS once and writes them for CLS_DT
-// dependents.  A dependent's output run starts at an arbitrary offset, so lanes cover aligned pairs of
-// output slots: 16-byte stores in the interior, 8-byte ones only at the two ends of a run.
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict__ keys, const u64* __restrict__ coff,
-                                                          const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
-                                                          const u32* __restrict__ lists, const u64* __restrict__ toff,
-                                                          u32 ncls, const u32* __restrict__ selfpos,
-                                                          const u64* __restrict__ obase, u64 out_base, u64* out) {
-    __shared__ u32 sl[CLS_LS];
-    __shared__ u32 s_dep[CLS_DT], s_sp[CLS_DT];
+// streaming emission into the dependent-run output (refs only; the run table names the dependent): each
+// block stages one list segment in LDS once and writes it for CLS_DT dependents.  HBM writes run at full
+// rate only for whole 128-B lines, so (1) a dependent's run is cut into segments at 128-B boundaries of the
+// OUTPUT (not of the list), so that no line is shared by two blocks, and (2) lanes own 16-B quads counted
+// from the 256-B boundary below the segment start, so every wave-wide store covers whole lines.  Segment s
+// of a run needs list entries [s*CLS_LS - 31, (s+1)*CLS_LS + 1), hence the staged halo.
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict__ coff, const u64* __restrict__ cchoff,
+                                                          const u64* __restrict__ lwoff, const u32* __restrict__ lists,
+                                                          const u64* __restrict__ toff, u32 ncls,
+                                                          const u32* __restrict__ selfpos, const u64* __restrict__ obase,
+                                                          u64 out_base, u32* out) {
+    __shared__ u32 sl[CLS_LS + 64];
+    __shared__ u32 s_sp[CLS_DT];
     __shared__ u64 s_base[CLS_DT];
     __shared__ u32 s_m;
     if (threadIdx.x == 0) s_m = find_dep(toff, ncls, blockIdx.x);
@@ -1102,49 +1134,119 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict_
     const u64 t = blockIdx.x - toff[m];
     const u64 dt = t / nseg, seg = t % nseg;
     const u64 k0 = coff[m] + dt * CLS_DT, k1 = k0 + CLS_DT < coff[m + 1] ? k0 + CLS_DT : coff[m + 1];
-    const u64 p0 = seg * CLS_LS, p1 = p0 + CLS_LS < len ? p0 + CLS_LS : len;
-    for (u64 i = threadIdx.x; i < p1 - p0; i += RDF_BLOCK) sl[i] = lists[lb + p0 + i];
+    const u64 p0 = seg * CLS_LS;
+    const u64 sb = p0 >= 32 ? p0 - 32 : 0;                                   // staged list range [sb, se)
+    const u64 se = p0 + CLS_LS + 1 < len ? p0 + CLS_LS + 1 : len;
+    for (u64 i = threadIdx.x; i < se - sb; i += RDF_BLOCK) sl[i] = lists[lb + sb + i];
     if (threadIdx.x < k1 - k0) {  // the tile's dependents, loaded once instead of one dependent load chain each
         const u64 i = k0 + threadIdx.x;
-        s_dep[threadIdx.x] = (u32)keys[i];
         s_sp[threadIdx.x] = selfpos[i];
         s_base[threadIdx.x] = obase[i];
     }
     __syncthreads();
-    for (u64 i = k0; i < k1; ++i) {
-        const u64 d = s_dep[i - k0];
-        const u32 sp = s_sp[i - k0];
-        const bool in_seg = sp != NONE32 && sp >= p0 && sp < p1;
-        const u64 ob = out_base + s_base[i - k0] + p0 - ((sp != NONE32 && sp < p0) ? 1 : 0);
-        const u64 oe = ob + (p1 - p0) - (in_seg ? 1 : 0);
-        const u64 skip = in_seg ? sp - p0 : ~0ull;  // index within the segment that is not emitted
-        for (u64 a = (ob >> 1) + threadIdx.x; 2 * a < oe; a += RDF_BLOCK) {
-            const u64 o0 = 2 * a, o1 = o0 + 1;
-            const bool in0 = o0 >= ob, in1 = o1 < oe;
-            const u64 q0 = o0 - ob, q1 = o1 - ob;  // k-th element of the run -> segment index k or k + 1
-            const u64 v0 = in0 ? ((d << 32) | sl[q0 + (q0 >= skip ? 1 : 0)]) : 0;
-            const u64 v1 = in1 ? ((d << 32) | sl[q1 + (q1 >= skip ? 1 : 0)]) : 0;
-            if (in0 && in1) {
-                u64x2 w;
-                w.x = v0;
-                w.y = v1;
-                *(u64x2*)(out + o0) = w;
-            } else if (in0) {
-                out[o0] = v0;
-            } else if (in1) {
-                out[o1] = v1;
+    for (u64 i = 0; i < k1 - k0; ++i) {
+        const u32 sp = s_sp[i];
+        const u64 n_run = len - (sp != NONE32 ? 1 : 0);
+        const u64 r0 = out_base + s_base[i];
+        // run element where segment s starts: the first 128-B boundary of the output at or below r0 + s*CLS_LS
+        auto bound = [&](u64 s) -> u64 {
+            if (s == 0) return 0;
+            if (s >= nseg) return n_run;
+            const u64 x = (r0 + s * CLS_LS) & ~31ull;
+            return x <= r0 ? 0 : (x - r0 < n_run ? x - r0 : n_run);
+        };
+        const u64 kb = bound(seg), ke = bound(seg + 1);
+        if (kb >= ke) continue;
+        const u64 ob = r0 + kb;
+        const int n = (int)(ke - kb);
+        const int lead = (int)(ob & 63);
+        const int nq = (lead + n + 3) >> 2;
+        u32* q_out = out + (ob - lead);                                       // 256-B aligned quad base
+        const int skip = sp != NONE32 ? (int)((u64)sp - kb) : 0x7fffffff;    // run element >= skip reads one further
+        const int base = (int)(kb - sb);                                     // run element kb at sl[base]
+        for (int t = threadIdx.x; t < nq; t += RDF_BLOCK) {
+            const int q0 = 4 * t - lead;                                      // segment element of the quad's first slot
+            u32 val[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int q = q0 + j;
+                const int li = base + q + (q >= skip ? 1 : 0);
+                val[j] = sl[li < 0 ? 0 : (li > (int)(CLS_LS + 63) ? (int)(CLS_LS + 63) : li)];
+            }
+            if (q0 >= 0 && q0 + 3 < n) {  // one 16-B store (the builtin keeps it from being split)
+                const u32x4 w = {val[0], val[1], val[2], val[3]};
+                __builtin_nontemporal_store(w, (u32x4*)(q_out + 4 * t));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (q0 + j >= 0 && q0 + j < n) q_out[4 * t + j] = val[j];
             }
         }
     }
 }
 
-// order-independent checksum of the result set (capture ids, so it is comparable across runs)
-__global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u64* __restrict__ pairs, u64 n, const u32* __restrict__ fcap,
+// output run table (dependent runs in output order): runs [0, C) are the explicit pairs of dependent d
+// (start pos[eoff[d]]), [C, C+WH) the heavy-only binary chunks, [C+WH, C+WH+nmem) the class members
+__global__ __launch_bounds__(RDF_BLOCK) void k_output_runs(u32 C, const u64* __restrict__ eoff, const u64* __restrict__ epos,
+                                                           u64 WH, const u64* __restrict__ choffh, const u64* __restrict__ hoff,
+                                                           u64 K, u64 nmem, const u64* __restrict__ ckeys,
+                                                           const u64* __restrict__ cobase, u64 H, u64 n_out, u64* runoff,
+                                                           u32* rundep) {
+    const u64 R = (u64)C + WH + nmem;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= R; i += (u64)gridDim.x * RDF_BLOCK) {
+        if (i == R) {
+            runoff[i] = n_out;
+        } else if (i < C) {
+            runoff[i] = epos[eoff[i]];
+            rundep[i] = (u32)i;
+        } else if (i < C + WH) {
+            const u64 w = i - C;
+            runoff[i] = K + hoff[w];
+            rundep[i] = find_dep(choffh, C, w);
+        } else {
+            const u64 j = i - C - WH;
+            runoff[i] = K + H + cobase[j];
+            rundep[i] = (u32)ckeys[j];
+        }
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_compact_refs(const u64* __restrict__ a, u64 n, const u32* __restrict__ flags,
+                                                            const u64* __restrict__ pos, u32* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        if (flags[i]) out[pos[i]] = (u32)a[i];
+}
+
+// run containing output element i: largest r with runoff[r] <= i, searched in [lo, hi]
+__device__ inline u64 run_of(const u64* __restrict__ runoff, u64 lo, u64 hi, u64 i) {
+    while (lo < hi) {
+        const u64 mid = (lo + hi + 1) >> 1;
+        if (runoff[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// order-independent checksum of the result set (external capture ids, so it is comparable across runs and
+// layouts).  Each block looks up the runs of its first and last element once; lanes search inside that range.
+__global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u32* __restrict__ refs, u64 n, const u64* __restrict__ runoff,
+                                                        const u32* __restrict__ rundep, u64 R, const u32* __restrict__ fcap,
                                                         u64* sum) {
+    __shared__ u64 s_lo, s_hi;
     u64 acc = 0;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 pr = pairs[i];
-        acc += mix64(((u64)fcap[pr >> 32] << 32) | fcap[(u32)pr]);
+    for (u64 b = (u64)blockIdx.x * RDF_BLOCK; b < n; b += (u64)gridDim.x * RDF_BLOCK) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const u64 last = b + RDF_BLOCK - 1 < n ? b + RDF_BLOCK - 1 : n - 1;
+            s_lo = run_of(runoff, 0, R - 1, b);
+            s_hi = run_of(runoff, s_lo, R - 1, last);
+        }
+        __syncthreads();
+        const u64 i = b + threadIdx.x;
+        if (i < n) {
+            const u32 d = rundep[run_of(runoff, s_lo, s_hi, i)];
+            acc += mix64(((u64)fcap[d] << 32) | fcap[refs[i]]);
+        }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, RDF_WAVE);

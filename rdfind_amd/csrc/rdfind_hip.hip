@@ -50,6 +50,7 @@ struct rdf_ctx {
 
     // cinds
     DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, out, stage_rows;
+    DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
         ctiles, ctoff;
@@ -74,8 +75,11 @@ struct rdf_ctx {
     bool x_imported = true;
     DevBuf item_dep, eblk, lslot;
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
-    u64 n_out = 0;
-    u64* out_ptr = nullptr;
+    u64 n_out = 0, n_runs = 0;
+    u32* out_ptr = nullptr;
+    bool h_runs_valid = false;  // host mirror of the run table (filled on the first copy)
+    std::vector<u64> h_runoff;
+    std::vector<u32> h_rundep;
     std::vector<u32> h_fcap;
     std::vector<u32> h_csup;
 
@@ -200,7 +204,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
-                      &c->obounds};
+                      &c->obounds, &c->runoff, &c->rundep};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -807,7 +811,7 @@ static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
     if (WH)
         hipLaunchKernelGGL((k_heavy<false>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, c->hcounts.as<u32>(),
-                           (const u64*)nullptr, (u64)0, (u64*)nullptr);
+                           (const u64*)nullptr, (u64)0, (u32*)nullptr);
     tend(c, RDF_T_HCOUNT);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->hcounts.as<u32>(), c->hoff.as<u64>(), WH, c->hoff.as<u64>() + WH, st));
     TRY(read_u64(c, c->hoff.as<u64>() + WH, H));
@@ -916,7 +920,7 @@ static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* 
 // K7 minimality on the (owned) explicit pairs, heavy-only binary write pass, class emission -> out
 static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
     hipStream_t st = c->stream;
-    ENSURE(c, out, std::max<u64>(E + H + HC, 1) * 8);
+    ENSURE(c, out, std::max<u64>(E + H + HC, 1) * 4);
     ENSURE(c, flags, std::max<u64>(E, 1) * 4);
     ENSURE(c, pos, (E + 1) * 8);
     tbegin(c, RDF_T_RULES);
@@ -925,8 +929,8 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
                            c->epairs.as<u64>(), E, c->rank, c->nranks, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), E, c->pos.as<u64>() + E, st));
     if (E)
-        hipLaunchKernelGGL(k_compact_u64, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E,
-                           c->flags.as<u32>(), c->pos.as<u64>(), c->out.as<u64>());
+        hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E,
+                           c->flags.as<u32>(), c->pos.as<u64>(), c->out.as<u32>());
     tend(c, RDF_T_RULES);
     u64 K = 0;
     TRY(read_u64(c, c->pos.as<u64>() + E, &K));
@@ -934,14 +938,24 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     if (WH)
         hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
                            dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, (u32*)nullptr,
-                           c->hoff.as<u64>(), K, c->out.as<u64>());
+                           c->hoff.as<u64>(), K, c->out.as<u32>());
     tend(c, RDF_T_HWRITE);
     tbegin(c, RDF_T_CEMIT);
     if (NT)
-        hipLaunchKernelGGL(k_class_emit, dim3((unsigned)NT), dim3(RDF_BLOCK), 0, st, c->ckeys.as<u64>(), c->coff.as<u64>(),
+        hipLaunchKernelGGL(k_class_emit, dim3((unsigned)NT), dim3(RDF_BLOCK), 0, st, c->coff.as<u64>(),
                            c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(),
-                           (u32)c->n_classes, c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u64>());
+                           (u32)c->n_classes, c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u32>());
     tend(c, RDF_T_CEMIT);
+    // run table: the dependent of every output ref (CindSet-shaped result, ALG/data/CindSet.scala:9-13)
+    const u64 nmem = HC ? c->n_class_members : 0;
+    const u64 R = (u64)c->C + WH + nmem;
+    ENSURE(c, runoff, (R + 1) * 8);
+    ENSURE(c, rundep, std::max<u64>(R, 1) * 4);
+    hipLaunchKernelGGL(k_output_runs, dim3(grid_for(R + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->C, v.eoff,
+                       c->pos.as<u64>(), WH, c->choffh.as<u64>(), c->hoff.as<u64>(), K, nmem, c->ckeys.as<u64>(),
+                       c->cobase.as<u64>(), H, K + H + HC, c->runoff.as<u64>(), c->rundep.as<u32>());
+    c->n_runs = R;
+    c->h_runs_valid = false;
     HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(st));
@@ -949,7 +963,7 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS);
     c->n_out = K + H + HC;
     c->n_class_out = HC;
-    c->out_ptr = c->out.as<u64>();
+    c->out_ptr = c->out.as<u32>();
     const u32 C = c->C;
     c->h_fcap.resize(C);
     c->h_csup.resize(C);
@@ -1371,23 +1385,45 @@ rdf_status rdf_cind_count(rdf_ctx* c, uint64_t* n) {
     return RDF_OK;
 }
 
+static rdf_status load_runs(rdf_ctx* c) {
+    if (c->h_runs_valid) return RDF_OK;
+    c->h_runoff.resize(c->n_runs + 1);
+    c->h_rundep.resize(c->n_runs);
+    HIP_TRY(c, hipMemcpy(c->h_runoff.data(), c->runoff.p, (c->n_runs + 1) * 8, hipMemcpyDeviceToHost));
+    if (c->n_runs) HIP_TRY(c, hipMemcpy(c->h_rundep.data(), c->rundep.p, c->n_runs * 4, hipMemcpyDeviceToHost));
+    c->h_runs_valid = true;
+    return RDF_OK;
+}
+
+// decode output elements [offset, offset + m) to caller records (external ids + dependent support)
+static rdf_status copy_decoded(rdf_ctx* c, u64 offset, u64 m, rdf_cind* out) {
+    TRY(load_runs(c));
+    const u64 chunk = 1ull << 24;
+    std::vector<u32> buf(std::min<u64>(chunk, std::max<u64>(m, 1)));
+    // first run holding element offset (largest r with runoff[r] <= offset)
+    u64 r = (u64)(std::upper_bound(c->h_runoff.begin(), c->h_runoff.begin() + c->n_runs, offset) - c->h_runoff.begin());
+    r = r ? r - 1 : 0;
+    for (u64 b = 0; b < m; b += chunk) {
+        const u64 k = std::min(chunk, m - b);
+        HIP_TRY(c, hipMemcpy(buf.data(), c->out_ptr + offset + b, k * 4, hipMemcpyDeviceToHost));
+        for (u64 i = 0; i < k; ++i) {
+            const u64 e = offset + b + i;
+            while (c->h_runoff[r + 1] <= e) ++r;
+            const u32 d = c->h_rundep[r];
+            out[b + i].dep = c->h_fcap[d];
+            out[b + i].ref = c->h_fcap[buf[i]];
+            out[b + i].support = c->h_csup[d];
+        }
+    }
+    return RDF_OK;
+}
+
 rdf_status rdf_copy_cinds(rdf_ctx* c, rdf_cind* out, uint64_t cap, uint64_t* n_copied) {
     if (!c || (cap && !out)) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
     const u64 total = std::min<u64>(cap, c->n_out);
-    const u64 chunk = 1ull << 24;
-    std::vector<u64> buf(std::min<u64>(chunk, std::max<u64>(total, 1)));
-    for (u64 b = 0; b < total; b += chunk) {
-        const u64 m = std::min(chunk, total - b);
-        HIP_TRY(c, hipMemcpy(buf.data(), c->out_ptr + b, m * 8, hipMemcpyDeviceToHost));
-        for (u64 i = 0; i < m; ++i) {
-            const u32 d = (u32)(buf[i] >> 32), r = (u32)buf[i];
-            out[b + i].dep = c->h_fcap[d];
-            out[b + i].ref = c->h_fcap[r];
-            out[b + i].support = c->h_csup[d];
-        }
-    }
+    if (total) TRY(copy_decoded(c, 0, total, out));
     if (n_copied) *n_copied = total;
     return RDF_OK;
 }
@@ -1397,14 +1433,7 @@ rdf_status rdf_copy_cinds_range(rdf_ctx* c, uint64_t offset, rdf_cind* out, uint
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
     const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
-    std::vector<u64> buf(std::max<u64>(m, 1));
-    if (m) HIP_TRY(c, hipMemcpy(buf.data(), c->out_ptr + offset, m * 8, hipMemcpyDeviceToHost));
-    for (u64 i = 0; i < m; ++i) {
-        const u32 d = (u32)(buf[i] >> 32), r = (u32)buf[i];
-        out[i].dep = c->h_fcap[d];
-        out[i].ref = c->h_fcap[r];
-        out[i].support = c->h_csup[d];
-    }
+    if (m) TRY(copy_decoded(c, offset, m, out));
     if (n_copied) *n_copied = m;
     return RDF_OK;
 }
@@ -1416,7 +1445,8 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     HIP_TRY(c, hipMemsetAsync(dscal(c, 7), 0, 8, c->stream));
     if (c->n_out)
         hipLaunchKernelGGL(k_checksum, dim3(grid_for(c->n_out, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
-                           c->out_ptr, c->n_out, c->fext.as<u32>(), dscal(c, 7));
+                           c->out_ptr, c->n_out, c->runoff.as<u64>(), c->rundep.as<u32>(), c->n_runs, c->fext.as<u32>(),
+                           dscal(c, 7));
     u64 v = 0;
     rdf_status rs = read_u64(c, dscal(c, 7), &v);
     *checksum = v;

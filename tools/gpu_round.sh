@@ -21,6 +21,16 @@ for step in "$@"; do
         || { echo "prof failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
       find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG.kernel_stats.csv \;
       head -25 gpurun_out/prof_$TAG.kernel_stats.csv ;;
+    pmc)
+      tools/pmc.sh $TAG || exit 1 ;;
+    lstats)
+      timeout -k 10 300 python -u tools/light_stats.py c2 1.0 > gpurun_out/lstats_$TAG.log 2>&1 \
+        || { echo "lstats failed"; tail -30 gpurun_out/lstats_$TAG.log; exit 1; }
+      grep LIGHT_STATS gpurun_out/lstats_$TAG.log ;;
+    quick)
+      timeout -k 10 300 python -u tools/gpu_quick.py > gpurun_out/quick_$TAG.log 2>&1 \
+        || { echo "quick failed"; tail -30 gpurun_out/quick_$TAG.log; exit 1; }
+      tail -5 gpurun_out/quick_$TAG.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
