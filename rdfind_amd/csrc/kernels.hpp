@@ -9,6 +9,7 @@ static constexpr int LB_SLOTS = 2048;     // LDS hash slots (u64 keys) for binar
 static constexpr int HMAX = 64;           // heavy groups tracked as bit columns (one u64 per capture)
 static constexpr uint8_t LIGHT = 0xff;
 static constexpr u64 LIGHT_SEG = 2048;   // groups of one dependent verified by one light work item
+static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
 static constexpr u32 LIGHT_LDS = 512;    // groups up to this size are searched in LDS (2 KiB per wave)
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load

@@ -626,9 +626,26 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, const u64* 
     }
 }
 
+// Light work plan of dependent d (nlight light groups, pivot of sz captures).  Output slots are octets (8
+// candidates of the pivot); noct[d] of them.  A dependent with few groups is "packed": one lane per
+// candidate in k_light_packed, with candidates of many dependents sharing a wave.  The others get
+// nitem[d] work items of k_light (chunk of 64 candidates x segment of LIGHT_SEG groups, one wave each).
+__device__ inline void light_plan(const CindView& v, u32 d, u32 nlight, u64 sz, u32* noct, u32* nitem, u32* npacked) {
+    if (!nlight) {
+        noct[d] = nitem[d] = npacked[d] = 0;
+        return;
+    }
+    const u64 ng = v.doff[d + 1] - v.doff[d];
+    const u32 oc = (u32)((sz + 7) / 8);
+    const bool packed = ng <= LIGHT_PACK_MAXG && ng <= (sz > 4 ? sz : 4);
+    noct[d] = oc;
+    nitem[d] = packed ? 0u : (u32)((sz + RDF_WAVE - 1) / RDF_WAVE) * (u32)((ng + LIGHT_SEG - 1) / LIGHT_SEG);
+    npacked[d] = packed ? oc : 0u;
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64* __restrict__ best_in,
                                                            const u32* __restrict__ nlight_in, u32* pivot, u32* nchunk_light,
-                                                           u32* nitem_light, u32* nchunk_heavy, CapInfo* info,
+                                                           u32* nitem_light, u32* npacked, u32* nchunk_heavy, CapInfo* info,
                                                            u64* heavy_candidates) {
     const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
@@ -639,8 +656,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64
             const u64 sz = best >> 32;
             const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
             pivot[d] = (u32)(best & 0xffffffffu);
-            nchunk_light[d] = nlight ? nch : 0;
-            nitem_light[d] = nlight ? nch * (u32)((v.doff[d + 1] - v.doff[d] + LIGHT_SEG - 1) / LIGHT_SEG) : 0;
+            light_plan(v, (u32)d, nlight, sz, nchunk_light, nitem_light, npacked);
             // unary heavy-only dependents are emitted per bitmask class (k_class_*), binary ones by k_heavy
             nchunk_heavy[d] = (nlight || d < v.Cu) ? 0 : nch;
             if (!nlight) {
@@ -742,10 +758,10 @@ __device__ inline bool rule_keep(const CindView& v, u32 a, u32 r) {
 }
 
 
-// candidate filter for a chunk of the pivot group: returns this lane's candidate (or NONE)
-__device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 chunk) {
+// candidate filter: the i-th member of the pivot group (or NONE)
+__device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 i) {
     const u64 gb = v.goff[piv], ge = v.goff[piv + 1];
-    const u64 idx = gb + chunk * RDF_WAVE + lane_id();
+    const u64 idx = gb + i;
     if (idx >= ge) return NONE32;
     const u32 r = v.gcap[idx];
     if (r == d) return NONE32;
@@ -756,28 +772,74 @@ __device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& i
     return r;
 }
 
-// survivors of a chunk go to the chunk's own 64-entry slot (no shared counter: a single global append
-// counter serialises at the memory side); k_slot_compact packs the slots afterwards
-__device__ inline void slot_emit(u64 slot, u32 d, u32 cand, u64 alive, u64* slots, u32* counts) {
-    if (lane_id() == 0) counts[slot] = (u32)__popcll(alive);
-    if ((alive >> lane_id()) & 1ull) slots[slot * RDF_WAVE + __popcll(alive & lanemask_lt())] = ((u64)d << 32) | cand;
+// candidate filter for a chunk of 64 pivot members: returns this lane's candidate (or NONE)
+__device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 chunk) {
+    return pivot_candidate(v, d, id, piv, chunk * RDF_WAVE + lane_id());
+}
+
+// Survivors go to per-octet slots (8 candidates of a pivot each; no shared counter: a single global append
+// counter serialises at the memory side); k_slot_compact packs the slots afterwards in slot order, which
+// is (dependent, ref) order.  Lanes [8o, 8o+8) of the wave own octet oct0 + o; octets >= nvalid belong to
+// the next dependent and are not touched.
+__device__ inline void slot_emit(u64 oct0, u32 nvalid, u32 d, u32 cand, u64 alive, u64* slots, u32* counts) {
+    const int lane = lane_id(), o = lane >> 3, j = lane & 7;
+    if ((u32)o >= nvalid) return;
+    const u32 om = (u32)(alive >> (o * 8)) & 0xffu;
+    if (j == 0) counts[oct0 + o] = (u32)__popc(om);
+    if ((om >> j) & 1u) slots[(oct0 + o) * 8 + __popc(om & ((1u << j) - 1u))] = ((u64)d << 32) | cand;
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(const u64* __restrict__ slots, const u32* __restrict__ counts,
                                                             const u64* __restrict__ pos, u64 W, u64* out) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
-    const u32 lane = (u32)lane_id();
-    if (lane < counts[w]) out[pos[w] + lane] = slots[w * RDF_WAVE + lane];
+    const u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x;
+    const u64 o = g >> 3;
+    if (o >= W) return;
+    const u32 j = (u32)(g & 7);
+    if (j < counts[o]) out[pos[o] + j] = slots[g];
+}
+
+// packed light dependents (few groups): one lane per pivot candidate, 8-lane octets, candidates of many
+// dependents per wave.  Each lane walks its dependent's groups and binary-searches its candidate in every
+// light one (the same test as k_light's few-groups path, without a mostly idle wave per dependent).
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(CindView v, const u32* __restrict__ pivot,
+                                                            const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep,
+                                                            u64 WP, const u64* __restrict__ choff, u64* slots, u32* counts) {
+    const u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x;
+    const u64 q = g >> 3;
+    if (q >= WP) return;  // whole octets only, so the octet ballots below see complete octets
+    const u32 d = pk_dep[q];
+    const u64 k = q - pkoff[d];
+    const u32 piv = pivot[d];
+    const CapInfo id = v.info[d];
+    const u32 cand = pivot_candidate(v, d, id, piv, k * 8 + (g & 7));
+    bool ok = cand != NONE32;
+    const u64 b = v.doff[d], e = v.doff[d + 1];
+    for (u64 j = b; ok && j < e; ++j) {
+        const u32 gr = v.dgrp[j];
+        if (gr == piv || v.hbit[gr] != LIGHT) continue;
+        ok = bsearch_u32(v.gcap + v.goff[gr], v.goff[gr + 1] - v.goff[gr], cand);
+    }
+    const u64 alive = __ballot(ok);
+    const int lane = lane_id(), o = lane >> 3, jj = lane & 7;
+    const u32 om = (u32)(alive >> (o * 8)) & 0xffu;
+    const u64 oct = choff[d] + k;
+    if (jj == 0) counts[oct] = (u32)__popc(om);
+    if (ok) slots[oct * 8 + __popc(om & ((1u << jj) - 1u))] = ((u64)d << 32) | cand;
 }
 
 #ifdef RDF_LIGHT_STATS
 // dev instrumentation (make STATS=1): [0] items [1] wave iterations [2] candidate checks [3] groups visited
 // [4] sum of log2 sizes of searched groups [5] initially alive candidates [6] items with nseg > 1
-__device__ unsigned long long g_light_stats[8];
+// [7] max wave cycles [8] cycles, few-groups path [9] cycles, many-groups path [10] cycles, multi-segment
+// items [11] max cycles of a multi-segment item [12] groups of multi-segment items [13] alive0 of those
+__device__ unsigned long long g_light_stats[16];
 #define LSTAT(i, v) do { if (lane_id() == 0) atomicAdd(&g_light_stats[i], (unsigned long long)(v)); } while (0)
+#define LSTAT_MAX(i, v) do { if (lane_id() == 0) atomicMax(&g_light_stats[i], (unsigned long long)(v)); } while (0)
+#define LSTAT_T0 const unsigned long long lstat_t0 = clock64()
 #else
 #define LSTAT(i, v) do { } while (0)
+#define LSTAT_MAX(i, v) do { } while (0)
+#define LSTAT_T0 do { } while (0)
 #endif
 
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
@@ -802,15 +864,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     u64 alive = alive0;
     const u64 b = b0 + seg * LIGHT_SEG;
     const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
+    LSTAT_T0;
     LSTAT(0, 1);
     LSTAT(5, __popcll(alive0));
     LSTAT(6, nseg > 1);
+    bool lstat_few = false;
+    (void)lstat_few;
     // Few groups, many candidates (the common case: most dependents have a handful of groups): every lane
     // tests its own candidate against the groups one after the other, so the serial chain is the number of
     // groups rather than the number of candidates.
     // A group of at most LIGHT_LDS captures is staged into the wave's LDS slice with one coalesced load
     // per lane, so the search costs one global round trip instead of log2(size) dependent ones.
     if (e - b <= (u64)__popcll(alive0) * ((e - b + RDF_WAVE - 1) / RDF_WAVE)) {
+        lstat_few = true;
         bool ok = cand != NONE32;
         u32* buf = s_light[threadIdx.x / RDF_WAVE];
         for (u64 j = b; j < e; ++j) {
@@ -879,9 +945,25 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
             }
         }
     }
-    const u64 slot = choff[d] + chunk;
+#ifdef RDF_LIGHT_STATS
+    {
+        const unsigned long long dt = clock64() - lstat_t0;
+        LSTAT_MAX(7, dt);
+        LSTAT(lstat_few ? 8 : 9, dt);
+        if (nseg > 1) {
+            LSTAT(10, dt);
+            LSTAT_MAX(11, dt);
+            LSTAT(12, e - b);
+            LSTAT(13, __popcll(alive0));
+        }
+    }
+#endif
+    const u64 oct0 = choff[d] + chunk * 8;  // first octet slot of this chunk
+    const u64 noct = choff[d + 1] - oct0;
+    const u32 nvalid = noct < 8 ? (u32)noct : 8u;
+    const u64 slot = oct0;                  // multi-segment bookkeeping is per chunk, keyed by its first octet
     if (nseg == 1) {
-        slot_emit(slot, d, cand, alive, slots, counts);
+        slot_emit(oct0, nvalid, d, cand, alive, slots, counts);
         return;
     }
     // several segments: publish the killed candidates; the last segment to arrive emits the survivors
@@ -897,7 +979,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
         u64 dm = 0;
         if (lane == 0) dm = atomicOr(&dead[slot], 0ull);
         dm = __shfl(dm, 0, RDF_WAVE);
-        slot_emit(slot, d, cand, alive0 & ~dm, slots, counts);
+        slot_emit(oct0, nvalid, d, cand, alive0 & ~dm, slots, counts);
     }
 }
 
@@ -1279,7 +1361,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
                                                                  const u32* __restrict__ nlight_in,
                                                                  const u64* __restrict__ gbest, const u64* __restrict__ glight,
                                                                  u32 rank, u32* pivot, u32* nchunk_light, u32* nitem_light,
-                                                                 u32* nchunk_heavy, u32* nrl, CapInfo* info,
+                                                                 u32* npacked, u32* nchunk_heavy, u32* nrl, CapInfo* info,
                                                                  u64* heavy_candidates) {
     const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
@@ -1293,8 +1375,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
             const u64 sz = best == ~0ull ? 0 : best >> 32;
             const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
             pivot[d] = (u32)(best & 0xffffffffu);
-            nchunk_light[d] = nlight ? nch : 0;
-            nitem_light[d] = nlight ? nch * (u32)((v.doff[d + 1] - v.doff[d] + LIGHT_SEG - 1) / LIGHT_SEG) : 0;
+            light_plan(v, (u32)d, nlight, sz, nchunk_light, nitem_light, npacked);
             nchunk_heavy[d] = (heavy_only && d >= v.Cu && holder) ? nch : 0;
             nrl[d] = (u32)(gl >> 40);
             if (heavy_only) {

@@ -73,7 +73,7 @@ struct rdf_ctx {
     u64 x_count = 0, x_recv_count = 0;
     u32 x_bytes = 8;
     bool x_imported = true;
-    DevBuf item_dep, eblk, lslot;
+    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep;
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
@@ -203,7 +203,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
-                      &c->item_dep, &c->eblk, &c->lslot, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
@@ -698,6 +698,8 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
     ENSURE(c, choffh, (C + 1ull) * 8);
     ENSURE(c, nitl, std::max<u64>(C, 1) * 4);
     ENSURE(c, itoffl, (C + 1ull) * 8);
+    ENSURE(c, npk, std::max<u64>(C, 1) * 4);
+    ENSURE(c, pkoff, (C + 1ull) * 8);
     ENSURE(c, pseg, std::max<u64>(C, 1) * 4);
     ENSURE(c, psegoff, (C + 1ull) * 8);
     ENSURE(c, pbest, std::max<u64>(C, 1) * 8);
@@ -724,52 +726,64 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
 }
 
 // work-chunk offsets after the pivot final pass
-static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI) {
+static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     hipStream_t st = c->stream;
     const u32 C = c->C;
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchl.as<u32>(), c->choffl.as<u64>(), C, c->choffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->npk.as<u32>(), c->pkoff.as<u64>(), C, c->pkoff.as<u64>() + C, st));
     TRY(read_u64(c, c->choffl.as<u64>() + C, WL));
+    TRY(read_u64(c, c->pkoff.as<u64>() + C, WP));
     TRY(read_u64(c, c->choffh.as<u64>() + C, WH));
     TRY(read_u64(c, dscal(c, 2), &c->heavy_candidates));
     TRY(read_u64(c, c->itoffl.as<u64>() + C, WI));
     return RDF_OK;
 }
 
-// light dependents -> explicit raw (dep << 32 | ref) pairs in epairs (unsorted); *E = count
-static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64* E) {
+// light dependents -> explicit raw (dep << 32 | ref) pairs in epairs, in (dep, ref) order; *E = count.
+// Output slots are octets (8 pivot candidates each): WL of them; WI k_light work items, WP packed octets.
+static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP, u64* E) {
     hipStream_t st = c->stream;
-    const u64 cap_pairs = std::max<u64>(WL * RDF_WAVE, 1);
-    ENSURE(c, epairs_tmp, cap_pairs * 8);  // one 64-entry slot per chunk
-    ENSURE(c, dead, std::max<u64>(WL, 1) * 12);  // dead masks, then per-chunk arrival counters
-    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, std::max<u64>(WL, 1) * 12, st));
-    ENSURE(c, lslot, std::max<u64>(WL, 1) * 4);
-    HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, std::max<u64>(WL, 1) * 4, st));
+    const u64 nslot = std::max<u64>(WL, 1);
+    ENSURE(c, epairs_tmp, nslot * 8 * 8);
+    ENSURE(c, dead, nslot * 12);  // dead masks (multi-segment chunks), then per-chunk arrival counters
+    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, nslot * 12, st));
+    ENSURE(c, lslot, nslot * 4);
+    HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, nslot * 4, st));
     ENSURE(c, item_dep, std::max<u64>(WI, 1) * 4);
+    ENSURE(c, pk_dep, std::max<u64>(WP, 1) * 4);
     tbegin(c, RDF_T_LIGHT);
     if (WI)
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->itoffl.as<u64>(),
                            c->C, c->item_dep.as<u32>());
+    if (WP)
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pkoff.as<u64>(),
+                           c->C, c->pk_dep.as<u32>());
+    if (WP)
+        hipLaunchKernelGGL(k_light_packed, dim3((unsigned)((WP * 8 + RDF_BLOCK - 1) / RDF_BLOCK)), dim3(RDF_BLOCK), 0, st, v,
+                           c->pivot.as<u32>(), c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
+                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     if (WI)
         hipLaunchKernelGGL(k_light, dim3((unsigned)((WI + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
                            0, st, v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
-                           c->dead.as<u64>(),
-                           (u32*)(c->dead.as<u64>() + std::max<u64>(WL, 1)), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+                           c->dead.as<u64>(), (u32*)(c->dead.as<u64>() + nslot), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     ENSURE(c, pos, (WL + 1) * 8);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
     TRY(read_u64(c, c->pos.as<u64>() + WL, E));
     ENSURE(c, epairs, std::max<u64>(*E, 1) * 8);
     if (WL)
-        hipLaunchKernelGGL(k_slot_compact, dim3((unsigned)((WL + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
-                           0, st, c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>());
+        hipLaunchKernelGGL(k_slot_compact, dim3((unsigned)((WL * 8 + RDF_BLOCK - 1) / RDF_BLOCK)), dim3(RDF_BLOCK), 0, st,
+                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>());
     tend(c, RDF_T_LIGHT);
 #ifdef RDF_LIGHT_STATS
     {
-        unsigned long long h[8];
+        unsigned long long h[16];
         HIP_TRY(c, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_light_stats), sizeof(h)));
-        fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu E=%llu items=%llu iters=%llu checks=%llu groups=%llu logsum=%llu alive0=%llu multiseg=%llu\n",
-                (unsigned long long)WI, (unsigned long long)WL, (unsigned long long)*E, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+        fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu WP=%llu E=%llu items=%llu iters=%llu checks=%llu groups=%llu logsum=%llu alive0=%llu multiseg=%llu"
+                " maxcyc=%llu cyc_few=%llu cyc_many=%llu cyc_mseg=%llu maxcyc_mseg=%llu grp_mseg=%llu alive_mseg=%llu\n",
+                (unsigned long long)WI, (unsigned long long)WL, (unsigned long long)WP, (unsigned long long)*E, h[0], h[1], h[2], h[3],
+                h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13]);
         memset(h, 0, sizeof(h));
         HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_light_stats), h, sizeof(h)));
     }
@@ -1000,12 +1014,12 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     tbegin(c, RDF_T_PIVOT);
     if (c->C)
         hipLaunchKernelGGL(k_pivot_final, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
-                           c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(),
-                           c->info.as<CapInfo>(), dscal(c, 2));
+                           c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>(),
+                           c->nchh.as<u32>(), c->info.as<CapInfo>(), dscal(c, 2));
     tend(c, RDF_T_PIVOT);
-    u64 WL = 0, WH = 0, WI = 0, E = 0, H = 0, HC = 0, NT = 0;
-    TRY(d_chunks(c, &WL, &WH, &WI));
-    TRY(d_light(c, v, WI, WL, &E));
+    u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0, H = 0, HC = 0, NT = 0;
+    TRY(d_chunks(c, &WL, &WH, &WI, &WP));
+    TRY(d_light(c, v, WI, WL, WP, &E));
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));
@@ -1122,13 +1136,14 @@ static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
     if (C)
         hipLaunchKernelGGL(k_pivot_final_shard, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
                            c->pbest.as<u64>(), c->pnl.as<u32>(), c->gbest.as<u64>(), c->xrecv.as<u64>(), c->rank,
-                           c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(), c->nrl.as<u32>(),
+                           c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>(), c->nchh.as<u32>(),
+                           c->nrl.as<u32>(),
                            c->info.as<CapInfo>(), dscal(c, 2));
     tend(c, RDF_T_PIVOT);
-    u64 WL = 0, WH = 0, WI = 0, E = 0;
-    TRY(d_chunks(c, &WL, &WH, &WI));
+    u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0;
+    TRY(d_chunks(c, &WL, &WH, &WI, &WP));
     c->sh_WH = WH;
-    TRY(d_light(c, v, WI, WL, &E));
+    TRY(d_light(c, v, WI, WL, WP, &E));
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     // group the local survivors by owner rank (dep % R): pack, sort, find bounds, unpack
