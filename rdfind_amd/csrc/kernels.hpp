@@ -8,9 +8,13 @@ static constexpr int LH_SLOTS = 4096;     // LDS hash slots (u32 keys) for unary
 static constexpr int LB_SLOTS = 2048;     // LDS hash slots (u64 keys) for binary counting
 static constexpr int HMAX = 64;           // heavy groups tracked as bit columns (one u64 per capture)
 static constexpr uint8_t LIGHT = 0xff;
-static constexpr u64 LIGHT_SEG = 2048;   // groups of one dependent verified by one light work item
+#ifndef RDF_LIGHT_SEG
+#define RDF_LIGHT_SEG 2048
+#endif
+static constexpr u64 LIGHT_SEG = RDF_LIGHT_SEG;  // groups of one dependent verified by one light work item
+static constexpr int LIGHT_IT = 4;             // groups per lane whose metadata is loaded together
 static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
-static constexpr u32 LIGHT_LDS = 512;    // groups up to this size are searched in LDS (2 KiB per wave)
+static constexpr int LIGHT_BATCH = 8;    // candidates searched together in k_light's many-groups path
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
 struct __align__(16) CapInfo {

@@ -22,25 +22,60 @@ __device__ inline u64 lower_bound_u64(const u64* a, u64 n, u64 key) {
 // Keys are type*V + value.  Per-block LDS hash table pre-aggregates hot keys (Zipf predicates /
 // classes) so only one global atomic per distinct key per block remains; table misses go global.
 
-__device__ inline void lds_count_u32(u32* lkey, u32* lcnt, u32 key, u32* gcnt) {
-    u32 h = hash32(key) & (LH_SLOTS - 1);
-#pragma unroll 1
-    for (int probe = 0; probe < 8; ++probe) {
-        u32 k = lkey[h];
-        if (k == key) {
-            atomicAdd(&lcnt[h], 1u);
-            return;
+// Wave-level merge of equal keys before counting (all lanes call it): runs of equal keys in adjacent lanes
+// collapse into their first lane (subject-ordered input, sorted records), then up to ROUNDS keys repeated
+// across the remaining run heads collapse into one lane each (hot predicates/classes).  Returns the count
+// this lane adds: 0 when inactive or merged into another lane.
+template <typename T, int ROUNDS>
+__device__ inline u32 wave_merge(T key, bool active) {
+    const int lane = lane_id();
+    const u64 A = __ballot(active);
+    const T prev = __shfl_up(key, 1, RDF_WAVE);
+    const bool head = active && (lane == 0 || !((A >> (lane - 1)) & 1ull) || prev != key);
+    const u64 H = __ballot(head);
+    const u64 stop = H | ~A;  // a run ends at the next head or inactive lane
+    u32 cnt = 0;
+    if (head) {
+        const u64 above = lane == RDF_WAVE - 1 ? 0ull : stop & (~0ull << (lane + 1));
+        cnt = (u32)((above ? __ffsll((long long)above) - 1 : RDF_WAVE) - lane);
+    }
+    u64 todo = H;
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (__popcll(todo) <= 1) break;
+        const int l = __ffsll((long long)todo) - 1;
+        const T kl = __shfl(key, l, RDF_WAVE);
+        const bool mine = ((todo >> lane) & 1ull) && key == kl;
+        const u64 m = __ballot(mine);
+        todo &= ~m;
+        if (__popcll(m) > 1) {
+            const u32 tot = wave_sum(mine ? cnt : 0u);
+            if (mine) cnt = lane == l ? tot : 0u;
         }
+    }
+    return cnt;
+}
+
+// LDS hash add with LDS_PROBES probes, then the global counter.  Few probes: once the table is full of
+// cold keys, probing further only delays the global atomic; hot keys claim their slots early.
+static constexpr int LDS_PROBES = 2;
+
+__device__ inline void lds_count_u32(u32* lkey, u32* lcnt, u32 key, u32 c, u32* gcnt) {
+    u32 h = hash32(key) & (LH_SLOTS - 1);
+#pragma unroll
+    for (int probe = 0; probe < LDS_PROBES; ++probe) {
+        u32 k = lkey[h];
         if (k == EMPTY32) {
-            u32 prev = atomicCAS(&lkey[h], EMPTY32, key);
-            if (prev == EMPTY32 || prev == key) {
-                atomicAdd(&lcnt[h], 1u);
-                return;
-            }
+            const u32 prev = atomicCAS(&lkey[h], EMPTY32, key);
+            k = prev == EMPTY32 ? key : prev;
+        }
+        if (k == key) {
+            atomicAdd(&lcnt[h], c);
+            return;
         }
         h = (h + 1) & (LH_SLOTS - 1);
     }
-    atomicAdd(&gcnt[key], 1u);
+    atomicAdd(&gcnt[key], c);
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_unary_count(const u32* __restrict__ s, const u32* __restrict__ p,
@@ -55,25 +90,45 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_unary_count(const u32* __restrict
     // one contiguous chunk per block so that runs of equal values (e.g. subjects) aggregate in LDS
     const u64 per = (n + gridDim.x - 1) / gridDim.x;
     const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
-    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
-        lds_count_u32(lkey, lcnt, s[i], cnt);
-        lds_count_u32(lkey, lcnt, V + p[i], cnt);
-        lds_count_u32(lkey, lcnt, 2u * V + o[i], cnt);
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        const bool act = i < e;
+        const u32 ks = act ? s[i] : 0u, kp = act ? V + p[i] : 0u, ko = act ? 2u * V + o[i] : 0u;
+        const u32 cs = wave_merge<u32, 2>(ks, act);
+        const u32 cp = wave_merge<u32, 4>(kp, act);
+        const u32 co = wave_merge<u32, 4>(ko, act);
+        if (cs) lds_count_u32(lkey, lcnt, ks, cs, cnt);
+        if (cp) lds_count_u32(lkey, lcnt, kp, cp, cnt);
+        if (co) lds_count_u32(lkey, lcnt, ko, co, cnt);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LH_SLOTS; i += RDF_BLOCK)
         if (lkey[i] != EMPTY32) atomicAdd(&cnt[lkey[i]], lcnt[i]);
 }
 
+// Block-reduced counter add (all threads of the block call it): device-scope atomics execute at the
+// memory side, ~11 ns apart on one address, so one per block instead of one per wave.
+__device__ inline void block_counter_add(u64* counter, u32 v) {
+    __shared__ u32 s_part[RDF_WAVES_PER_BLOCK];
+    v = wave_sum(v);
+    if (lane_id() == 0) s_part[threadIdx.x / RDF_WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 t = 0;
+#pragma unroll
+        for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) t += s_part[w];
+        if (t) atomicAdd(counter, t);
+    }
+    __syncthreads();
+}
+
 // number of frequent values per condition type (for stats)
 __global__ __launch_bounds__(RDF_BLOCK) void k_count_frequent(const u32* __restrict__ cnt, u32 V, u32 ms, u64* out3) {
-    const u64 total = 3ull * V;
-    u32 c[3] = {0, 0, 0};
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < total; i += (u64)gridDim.x * RDF_BLOCK)
-        if (cnt[i] >= ms) c[i / V]++;
     for (int t = 0; t < 3; ++t) {
-        u32 w = wave_sum(c[t]);
-        if (lane_id() == 0 && w) atomicAdd(&out3[t], (u64)w);
+        const u32* ct = cnt + (u64)t * V;
+        u32 c = 0;
+        for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < V; i += (u64)gridDim.x * RDF_BLOCK) c += ct[i] >= ms;
+        block_counter_add(&out3[t], c);
     }
 }
 
@@ -85,12 +140,14 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_frank_flags(const u32* __restrict
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n3; i += (u64)gridDim.x * RDF_BLOCK) flags[i] = cnt[i] >= ms;
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_frank_final(const u32* __restrict__ cnt, u64 n3, u32 V, u32 ms, u32* frank,
+__global__ __launch_bounds__(RDF_BLOCK) void k_frank_final(const u32* __restrict__ cnt, u32 V, u32 ms, u32* frank,
                                                            u32* fval) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n3; i += (u64)gridDim.x * RDF_BLOCK) {
-        if (cnt[i] >= ms) fval[frank[i]] = (u32)(i % V);
-        else frank[i] = NONE32;
-    }
+    for (int t = 0; t < 3; ++t)
+        for (u64 v = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; v < V; v += (u64)gridDim.x * RDF_BLOCK) {
+            const u64 i = (u64)t * V + v;
+            if (cnt[i] >= ms) fval[frank[i]] = (u32)v;
+            else frank[i] = NONE32;
+        }
 }
 
 // condition position (0 s, 1 p, 2 o) of unary capture type t (0 s[p], 1 s[o], 2 p[s], 3 p[o], 4 o[s], 5 o[p])
@@ -161,25 +218,22 @@ __device__ inline void global_hash_add(u64* tkeys, u32* tcnt, u64 mask, u64 key,
     }
 }
 
-__device__ inline void lds_count_u64(u64* lkey, u32* lcnt, u64 key, u64* tkeys, u32* tcnt, u64 tmask) {
+__device__ inline void lds_count_u64(u64* lkey, u32* lcnt, u64 key, u32 c, u64* tkeys, u32* tcnt, u64 tmask) {
     u32 h = (u32)mix64(key) & (LB_SLOTS - 1);
-#pragma unroll 1
-    for (int probe = 0; probe < 8; ++probe) {
+#pragma unroll
+    for (int probe = 0; probe < LDS_PROBES; ++probe) {
         u64 k = lkey[h];
-        if (k == key) {
-            atomicAdd(&lcnt[h], 1u);
-            return;
-        }
         if (k == EMPTY64) {
-            u64 prev = atomicCAS(&lkey[h], EMPTY64, key);
-            if (prev == EMPTY64 || prev == key) {
-                atomicAdd(&lcnt[h], 1u);
-                return;
-            }
+            const u64 prev = atomicCAS(&lkey[h], EMPTY64, key);
+            k = prev == EMPTY64 ? key : prev;
+        }
+        if (k == key) {
+            atomicAdd(&lcnt[h], c);
+            return;
         }
         h = (h + 1) & (LB_SLOTS - 1);
     }
-    global_hash_add(tkeys, tcnt, tmask, key, 1u);
+    global_hash_add(tkeys, tcnt, tmask, key, c);
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_binary_count(const u32* __restrict__ s, const u32* __restrict__ p,
@@ -193,39 +247,50 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_binary_count(const u32* __restric
         lcnt[i] = 0;
     }
     __syncthreads();
-    const u64 stride = (u64)gridDim.x * RDF_BLOCK;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += stride) {
-        u32 ts = s[i], tp = p[i], to = o[i];
-        bool fs, fp, fo;
-        freq_flags(cnt, V, ms, ts, tp, to, fs, fp, fo);
-        if (fs && fp) lds_count_u64(lkey, lcnt, bin_key(2, ts, tp), tkeys, tcnt, tmask);   // o[s,p] (35)
-        if (fs && fo) lds_count_u64(lkey, lcnt, bin_key(1, ts, to), tkeys, tcnt, tmask);   // p[s,o] (21)
-        if (fp && fo) lds_count_u64(lkey, lcnt, bin_key(0, tp, to), tkeys, tcnt, tmask);   // s[p,o] (14)
+    // one contiguous chunk per block (subject runs stay together for the wave merge)
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        const bool act = i < e;
+        u32 ts = 0, tp = 0, to = 0;
+        bool fs = false, fp = false, fo = false;
+        if (act) {
+            ts = s[i];
+            tp = p[i];
+            to = o[i];
+            freq_flags(cnt, V, ms, ts, tp, to, fs, fp, fo);
+        }
+        const u64 k_sp = bin_key(2, ts, tp), k_so = bin_key(1, ts, to), k_po = bin_key(0, tp, to);
+        const u32 c_sp = wave_merge<u64, 2>(k_sp, fs && fp);  // o[s,p] (35)
+        const u32 c_so = wave_merge<u64, 2>(k_so, fs && fo);  // p[s,o] (21)
+        const u32 c_po = wave_merge<u64, 4>(k_po, fp && fo);  // s[p,o] (14)
+        if (c_sp) lds_count_u64(lkey, lcnt, k_sp, c_sp, tkeys, tcnt, tmask);
+        if (c_so) lds_count_u64(lkey, lcnt, k_so, c_so, tkeys, tcnt, tmask);
+        if (c_po) lds_count_u64(lkey, lcnt, k_po, c_po, tkeys, tcnt, tmask);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < LB_SLOTS; i += RDF_BLOCK)
         if (lkey[i] != EMPTY64) global_hash_add(tkeys, tcnt, tmask, lkey[i], lcnt[i]);
 }
 
-// frequent binary conditions: filter >= minSupport (FrequentConditionPlanner.scala:587-589)
+// frequent binary conditions: filter >= minSupport (FrequentConditionPlanner.scala:587-589); *nonempty =
+// number of distinct binary keys (stats)
 __global__ __launch_bounds__(RDF_BLOCK) void k_bin_freq_flags(const u64* __restrict__ tkeys, const u32* __restrict__ tcnt,
-                                                              u64 cap, u32 ms, u32* flags) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < cap; i += (u64)gridDim.x * RDF_BLOCK)
-        flags[i] = (tkeys[i] != EMPTY64 && tcnt[i] >= ms) ? 1u : 0u;
+                                                              u64 cap, u32 ms, u32* flags, u64* nonempty) {
+    u32 c = 0;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < cap; i += (u64)gridDim.x * RDF_BLOCK) {
+        const bool used = tkeys[i] != EMPTY64;
+        c += used;
+        flags[i] = (used && tcnt[i] >= ms) ? 1u : 0u;
+    }
+    block_counter_add(nonempty, c);
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_bin_freq_scatter(const u64* __restrict__ tkeys, const u32* __restrict__ flags,
                                                                 const u64* __restrict__ pos, u64 cap, u64* out) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < cap; i += (u64)gridDim.x * RDF_BLOCK)
         if (flags[i]) out[pos[i]] = tkeys[i];
-}
-
-__global__ __launch_bounds__(RDF_BLOCK) void k_count_nonempty(const u64* __restrict__ tkeys, u64 cap, u64* total) {
-    u32 c = 0;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < cap; i += (u64)gridDim.x * RDF_BLOCK)
-        c += tkeys[i] != EMPTY64;
-    c = wave_sum(c);
-    if (lane_id() == 0 && c) atomicAdd(total, (u64)c);
 }
 
 // lookup table of frequent binary keys -> index b (keys sorted, so b is deterministic)
@@ -279,42 +344,40 @@ __device__ inline u32 block_exclusive_scan_u32(u32 v, u32* lds_wave, u32* total)
 // Per triple and projection: unary captures of the frequent condition values and, when the binary
 // condition is frequent, the binary capture.  Binary captures are emitted together with both unary
 // components, which is what every consumer reconstructs (CreateDependencyCandidates.scala:157-186,
-// splitAndCollectUnaryCaptures).  Record = join << capbits | capture id.
+// splitAndCollectUnaryCaptures).  Record = capture << joinbits | join: sorted, a capture's records are
+// contiguous, so its support is a run length (no atomics) and its join list is the dependent -> groups CSR.
 
 // records of triple i (at most 9); returns the count
 __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
                                      u32 V, u32 twoU, const u32* __restrict__ frank, const u64* __restrict__ lkeys,
-                                     const u32* __restrict__ lvals, u64 lmask, int proj, int capbits, u32 rank, u32 nranks,
+                                     const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, u32 rank, u32 nranks,
                                      u64 (&rec)[9]) {
     u32 c = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
     const u32 rs = frank[ts], rp = frank[V + tp], ro = frank[2ull * V + to];  // condition ranks (or NONE)
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
     if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
-        const u64 j = (u64)to << capbits;
-        if (fs) rec[c++] = j | (2ull * rs + 1);
-        if (fp) rec[c++] = j | (2ull * rp + 1);
+        if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
+        if (fp) rec[c++] = ((2ull * rp + 1) << joinbits) | to;
         if (fs && fp) {
             u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
-            if (b != NONE32) rec[c++] = j | ((u64)twoU + b);
+            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
         }
     }
     if ((proj & 2) && shard_of(tp, nranks) == rank) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
-        const u64 j = (u64)tp << capbits;
-        if (fs) rec[c++] = j | (2ull * rs);
-        if (fo) rec[c++] = j | (2ull * ro + 1);
+        if (fs) rec[c++] = ((2ull * rs) << joinbits) | tp;
+        if (fo) rec[c++] = ((2ull * ro + 1) << joinbits) | tp;
         if (fs && fo) {
             u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
-            if (b != NONE32) rec[c++] = j | ((u64)twoU + b);
+            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
         }
     }
     if ((proj & 1) && shard_of(ts, nranks) == rank) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
-        const u64 j = (u64)ts << capbits;
-        if (fp) rec[c++] = j | (2ull * rp);
-        if (fo) rec[c++] = j | (2ull * ro);
+        if (fp) rec[c++] = ((2ull * rp) << joinbits) | ts;
+        if (fo) rec[c++] = ((2ull * ro) << joinbits) | ts;
         if (fp && fo) {
             u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
-            if (b != NONE32) rec[c++] = j | ((u64)twoU + b);
+            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | ts;
         }
     }
     return c;
@@ -328,7 +391,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
                                                             const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                             const u32* __restrict__ lvals, u64 lmask, int proj,
-                                                            int capbits, u32 rank, u32 nranks, u64* block_counts,
+                                                            int joinbits, u32 rank, u32 nranks, u64* block_counts,
                                                             const u64* __restrict__ block_offsets, u64* out) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
     const u64 b = (u64)blockIdx.x * per;
@@ -338,7 +401,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
         u32 c = 0;
-        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, capbits, rank, nranks, rec);
+        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, rank, nranks, rec);
         u32 total;
         const u32 off = block_exclusive_scan_u32(c, lds_wave, &total);
         if (WRITE)
@@ -354,26 +417,27 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
 //     captures per join value) and capture supports (depCount summed per group,
 //     ALG/operators/candidate_merging/BulkMergeDependencies.scala:78-84)
 
-// Hot captures (e.g. s[p=rdf:type]) appear once in almost every group: LDS-hash pre-aggregation over a
-// contiguous chunk of groups turns ~|groups| global atomics on one address into one per block.
-__global__ __launch_bounds__(RDF_BLOCK) void k_unique_support(const u64* __restrict__ keys, u64 n, u64 capmask,
-                                                              u32* support) {
-    __shared__ u32 lkey[LH_SLOTS];
-    __shared__ u32 lcnt[LH_SLOTS];
-    for (int i = threadIdx.x; i < LH_SLOTS; i += RDF_BLOCK) {
-        lkey[i] = EMPTY32;
-        lcnt[i] = 0;
+// Sorted (capture << joinbits | join) records: fresh[i] = keys[i] differs from keys[i - 1] (a distinct
+// (capture, join) pair), and the capture runs' bounds: cstart[c] = first record of capture c, for every
+// c in [0, ncap] (captures without records get the next run's start; cstart[ncap] = n).
+__global__ __launch_bounds__(RDF_BLOCK) void k_fresh_bounds(const u64* __restrict__ keys, u64 n, u64 ncap, int joinbits,
+                                                            u32* fresh, u32* cstart) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = i < n ? keys[i] : 0ull, kp = i ? keys[i - 1] : 0ull;
+        if (i < n) fresh[i] = (i == 0 || kp != k) ? 1u : 0u;
+        const u64 c = i < n ? k >> joinbits : ncap;
+        const u64 cp = i ? (kp >> joinbits) + 1 : 0;
+        for (u64 x = cp; x <= c; ++x) cstart[x] = (u32)i;
     }
-    __syncthreads();
-    const u64 per = (n + gridDim.x - 1) / gridDim.x;
-    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
-    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
-        u64 k = keys[i];
-        if (i == 0 || keys[i - 1] != k) lds_count_u32(lkey, lcnt, (u32)(k & capmask), support);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < LH_SLOTS; i += RDF_BLOCK)
-        if (lkey[i] != EMPTY32) atomicAdd(&support[lkey[i]], lcnt[i]);
+}
+
+// support of capture c = distinct join values among its records = fresh records of its run; fpos = exclusive
+// scan of the fresh flags (fpos[n] = their total).  No atomics: a hot capture (s[p=rdf:type], in ~every
+// group) is one subtraction.
+__global__ __launch_bounds__(RDF_BLOCK) void k_run_support(const u32* __restrict__ cstart, u64 ncap,
+                                                           const u32* __restrict__ fpos, u32* support) {
+    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < ncap; c += (u64)gridDim.x * RDF_BLOCK)
+        support[c] = fpos[cstart[c + 1]] - fpos[cstart[c]];
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_support_flags(const u32* __restrict__ support, u64 ncap, u32 ms, u32* flags) {
@@ -399,22 +463,31 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_compact_captures(const u32* __res
 }
 
 // keep distinct records of frequent captures
-__global__ __launch_bounds__(RDF_BLOCK) void k_keep_flags(const u64* __restrict__ keys, u64 n, u64 capmask,
-                                                          const u32* __restrict__ support, u32 ms, u32* flags) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        u64 k = keys[i];
-        flags[i] = ((i == 0 || keys[i - 1] != k) && support[k & capmask] >= ms) ? 1u : 0u;
-    }
+// Fresh records of an infrequent capture are dropped; in (capture, join) order the kept ones of a capture
+// stay contiguous, so a kept record's position is its fresh rank minus the fresh records of the infrequent
+// captures before it.  skipv[c] = this rank's fresh records of c when c is infrequent (global support).
+__global__ __launch_bounds__(RDF_BLOCK) void k_skip_counts(const u32* __restrict__ cstart, const u32* __restrict__ fpos,
+                                                           const u32* __restrict__ support, u64 ncap, u32 ms, u32* skipv) {
+    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < ncap; c += (u64)gridDim.x * RDF_BLOCK)
+        skipv[c] = support[c] >= ms ? 0u : fpos[cstart[c + 1]] - fpos[cstart[c]];
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_keep_scatter(const u64* __restrict__ keys, u64 n, int capbits, u64 capmask,
-                                                            const u32* __restrict__ flags, const u64* __restrict__ pos,
-                                                            const u32* __restrict__ fidx, u64* out) {
+// kept records -> dk = (compact capture << 32 | join) in (capture, join) order (the dependent -> join CSR)
+// and fk = (join << 32 | compact capture) at the same position (sorted by join next, for the groups)
+__global__ __launch_bounds__(RDF_BLOCK) void k_keep_scatter(const u64* __restrict__ keys, u64 n, int joinbits,
+                                                            const u32* __restrict__ fpos, const u32* __restrict__ skip,
+                                                            const u32* __restrict__ support, u32 ms,
+                                                            const u32* __restrict__ fidx, u64* dk, u64* fk) {
+    const u64 jmask = (1ull << joinbits) - 1;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        if (flags[i]) {
-            u64 k = keys[i];
-            out[pos[i]] = ((k >> capbits) << 32) | fidx[k & capmask];
-        }
+        const u64 k = keys[i];
+        if (i && keys[i - 1] == k) continue;
+        const u64 cap = k >> joinbits;
+        if (support[cap] < ms) continue;
+        const u64 p = fpos[i] - skip[cap];
+        const u64 c = fidx[cap], j = k & jmask;
+        dk[p] = (c << 32) | j;
+        fk[p] = (j << 32) | c;
     }
 }
 
@@ -423,27 +496,29 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_flags(const u64* __restrict
         flags[i] = (i == 0 || (fk[i - 1] >> 32) != (fk[i] >> 32)) ? 1u : 0u;
 }
 
-// groups: goff[g] = first record; gcap[i] = compact capture id; gid[i] = group of record i
+// groups: goff[g] = first record; gcap[i] = compact capture id; gmap[join] = g (fk = join << 32 | capture)
 __global__ __launch_bounds__(RDF_BLOCK) void k_group_build(const u64* __restrict__ fk, u64 n, const u32* __restrict__ gflag,
-                                                           const u32* __restrict__ gexcl, u64* goff, u32* gcap, u32* gid) {
+                                                           const u32* __restrict__ gexcl, u64* goff, u32* gcap, u32* gmap) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        u32 g = gexcl[i] + gflag[i] - 1;
-        if (gflag[i]) goff[g] = i;
-        gcap[i] = (u32)(fk[i] & 0xffffffffu);
-        gid[i] = g;
+        const u64 k = fk[i];
+        gcap[i] = (u32)(k & 0xffffffffu);
+        if (gflag[i]) {
+            const u32 g = gexcl[i];
+            goff[g] = i;
+            gmap[k >> 32] = g;
+        }
     }
+}
+
+// dependent -> groups: dgrp[i] = group of the join value of dk[i].  A capture's joins ascend and group ids
+// are assigned in join order, so every dependent's group list comes out sorted.
+__global__ __launch_bounds__(RDF_BLOCK) void k_dgrp(const u64* __restrict__ dk, u64 n, const u32* __restrict__ gmap, u32* dgrp) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        dgrp[i] = gmap[(u32)dk[i]];
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_info_support_u32(const CapInfo* __restrict__ info, u32 C, u32* out) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < C; i += (u64)gridDim.x * RDF_BLOCK) out[i] = info[i].support;
-}
-
-// dependent -> groups (transposed CSR) by radix-sorting (capture << 32 | group): no per-capture cursor
-// atomics (a hot capture sits in ~every group), and every dependent's group list comes out sorted.
-__global__ __launch_bounds__(RDF_BLOCK) void k_make_tkeys(const u32* __restrict__ gcap, const u32* __restrict__ gid, u64 n,
-                                                          u64* out) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
-        out[i] = ((u64)gcap[i] << 32) | gid[i];
 }
 
 // offsets of a sorted (id << 32 | x) key array: off[d] = first key with id >= d, d in [0, C]
@@ -452,9 +527,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_key_offsets(const u64* __restrict
         off[d] = lower_bound_u64(keys, n, d << 32);
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_low32(const u64* __restrict__ keys, u64 n, u32* out) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) out[i] = (u32)keys[i];
-}
 
 // ---- heavy groups: quarter-octave size buckets, then the top groups become bit columns
 __device__ __host__ inline int size_bucket(u64 size) {
@@ -681,6 +753,27 @@ __device__ inline bool bsearch_u32(const u32* a, u64 n, u32 key) {
     return lo < n && a[lo] == key;
 }
 
+// K keys searched in one sorted array of n (> 0) distinct values; the K loads of a level are independent
+template <int K>
+__device__ inline void search_batch(const u32* __restrict__ a, u64 n, const u32 (&key)[K], bool (&found)[K]) {
+    u64 base[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) base[k] = 0;
+    if (!a) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) found[k] = false;
+        return;
+    }
+    while (n > 1) {
+        const u64 half = n >> 1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) base[k] = a[base[k] + half] <= key[k] ? base[k] + half : base[k];
+        n -= half;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) found[k] = a[base[k]] == key[k];
+}
+
 __device__ inline bool bsearch_u64(const u64* a, u64 n, u64 key) {
     u64 lo = 0, hi = n;
     while (lo < hi) {
@@ -848,7 +941,6 @@ __device__ unsigned long long g_light_stats[16];
 __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
                                                      const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
                                                      u64* dead, u32* arrive, u64* slots, u32* counts) {
-    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_LDS];
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -868,80 +960,61 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     LSTAT(0, 1);
     LSTAT(5, __popcll(alive0));
     LSTAT(6, nseg > 1);
-    bool lstat_few = false;
-    (void)lstat_few;
-    // Few groups, many candidates (the common case: most dependents have a handful of groups): every lane
-    // tests its own candidate against the groups one after the other, so the serial chain is the number of
-    // groups rather than the number of candidates.
-    // A group of at most LIGHT_LDS captures is staged into the wave's LDS slice with one coalesced load
-    // per lane, so the search costs one global round trip instead of log2(size) dependent ones.
-    if (e - b <= (u64)__popcll(alive0) * ((e - b + RDF_WAVE - 1) / RDF_WAVE)) {
-        lstat_few = true;
-        bool ok = cand != NONE32;
-        u32* buf = s_light[threadIdx.x / RDF_WAVE];
-        for (u64 j = b; j < e; ++j) {
-            if (!__any(ok)) break;
-            const u32 g = v.dgrp[j];
-            if (g == piv || v.hbit[g] != LIGHT) continue;
-            LSTAT(1, 1);
-            LSTAT(2, __popcll(__ballot(ok)));
-            const u64 gb = v.goff[g];
-            const u32 gsz = (u32)(v.goff[g + 1] - gb);
-            if (gsz <= LIGHT_LDS) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf before the refill
-                __builtin_amdgcn_wave_barrier();
-                for (u32 k = lane; k < gsz; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (ok) {
-                    u32 lo = 0, hi = gsz;
-                    while (lo < hi) {
-                        const u32 mid = (lo + hi) >> 1;
-                        if (buf[mid] < cand) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    ok = lo < gsz && buf[lo] == cand;
-                }
-            } else if (ok) {
-                ok = bsearch_u32(v.gcap + gb, gsz, cand);
+    // Lanes take one group each (LIGHT_IT per lane); dependents with few groups went to k_light_packed, so
+    // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
+    // independent gathers per level, so the serial chain is three round trips per segment, not per 64 groups.
+    for (u64 s0 = b; s0 < e && alive; s0 += (u64)LIGHT_IT * RDF_WAVE) {
+        u32 gg[LIGHT_IT];
+        u64 gbv[LIGHT_IT];
+        u32 gszv[LIGHT_IT];
+#pragma unroll
+        for (int it = 0; it < LIGHT_IT; ++it) {
+            const u64 j = s0 + (u64)it * RDF_WAVE + lane;
+            gg[it] = j < e ? v.dgrp[j] : NONE32;
+        }
+#pragma unroll
+        for (int it = 0; it < LIGHT_IT; ++it)
+            if (gg[it] != NONE32 && (gg[it] == piv || v.hbit[gg[it]] != LIGHT)) gg[it] = NONE32;
+#pragma unroll
+        for (int it = 0; it < LIGHT_IT; ++it) {
+            gbv[it] = 0;
+            gszv[it] = 0;
+            if (gg[it] != NONE32) {
+                gbv[it] = v.goff[gg[it]];
+                gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
             }
         }
-        alive = __ballot(ok);
-    } else {
-        // many groups: lanes take one group each and the alive candidates are tested one after the other
-        for (u64 j0 = b; j0 < e && alive; j0 += RDF_WAVE) {
+#pragma unroll
+        for (int it = 0; it < LIGHT_IT; ++it) {
+            if (s0 + (u64)it * RDF_WAVE >= e) break;
+            // a multi-segment item drops the candidates other segments have already killed
+            if (nseg > 1 && (it || s0 != b)) alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!alive) break;
 #ifdef RDF_LIGHT_STATS
-            {
-                const u64 jj = j0 + lane;
-                u32 gg = jj < e ? v.dgrp[jj] : NONE32;
-                const bool vis = gg != NONE32 && gg != piv && v.hbit[gg] == LIGHT;
-                const u32 lg = vis ? 64 - __builtin_clzll(v.goff[gg + 1] - v.goff[gg]) : 0;
-                LSTAT(1, 1);
-                LSTAT(2, __popcll(alive));
-                LSTAT(3, __popcll(__ballot(vis)));
-                LSTAT(4, (u64)wave_sum(lg) * __popcll(alive));
-            }
+            LSTAT(1, 1);
+            LSTAT(2, __popcll(alive));
+            LSTAT(3, __popcll(__ballot(gg[it] != NONE32)));
 #endif
-            const u64 j = j0 + lane;
-            u32 g = NONE32;
-            if (j < e) {
-                g = v.dgrp[j];
-                if (g == piv || v.hbit[g] != LIGHT) g = NONE32;
-            }
-            const u32* gm = nullptr;
-            u64 gsz = 0;
-            if (g != NONE32) {
-                gm = v.gcap + v.goff[g];
-                gsz = v.goff[g + 1] - v.goff[g];
-            }
+            const u32 g = gg[it];
+            const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
+            const u64 gsz = gszv[it];
+            // up to LIGHT_BATCH alive candidates are searched at once: their loads at one level of the
+            // search are independent, so the serial chain is one search, not one per candidate
             u64 todo = alive;
             while (todo) {
-                const int bit = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                const u32 c = __shfl(cand, bit, RDF_WAVE);
-                const bool ok = (g == NONE32) || bsearch_u32(gm, gsz, c);
-                if (!__all(ok)) alive &= ~(1ull << bit);
+                int bit[LIGHT_BATCH];
+                u32 key[LIGHT_BATCH];
+#pragma unroll
+                for (int k = 0; k < LIGHT_BATCH; ++k) {
+                    bit[k] = todo ? __ffsll((long long)todo) - 1 : -1;
+                    todo &= todo - 1;
+                    key[k] = __shfl(cand, bit[k] < 0 ? bit[0] : bit[k], RDF_WAVE);
+                }
+                bool ok[LIGHT_BATCH];
+                search_batch<LIGHT_BATCH>(gm, gsz, key, ok);
+#pragma unroll
+                for (int k = 0; k < LIGHT_BATCH; ++k)
+                    if (bit[k] >= 0 && !__all(g == NONE32 || ok[k])) alive &= ~(1ull << bit[k]);
             }
         }
     }
@@ -949,7 +1022,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     {
         const unsigned long long dt = clock64() - lstat_t0;
         LSTAT_MAX(7, dt);
-        LSTAT(lstat_few ? 8 : 9, dt);
+        LSTAT(9, dt);
         if (nseg > 1) {
             LSTAT(10, dt);
             LSTAT_MAX(11, dt);
@@ -1065,8 +1138,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u64* tke
     u32 cnt = 0;
     const u64 n_round = ((u64)v.Cu + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
-        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY)) {
-            const u64 m = v.info[d].hmask;  // never 0 for a heavy-only dependent
+        const bool member = d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY);
+        const u64 m = member ? v.info[d].hmask : 0ull;  // never 0 for a heavy-only dependent
+        cnt += member;
+        // few classes, many members: one lane per distinct mask of the wave inserts (one CAS per address)
+        if (wave_merge<u64, 4>(m, member)) {
             u64 h = mix64(m) & tmask;
             for (;;) {
                 u64 k = tkeys[h];
@@ -1077,11 +1153,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u64* tke
                 }
                 h = (h + 1) & tmask;
             }
-            cnt++;
         }
     }
-    cnt = wave_sum(cnt);
-    if (lane_id() == 0 && cnt) atomicAdd(nmembers, (u64)cnt);
+    block_counter_add(nmembers, cnt);
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_nonzero_flags(const u64* __restrict__ a, u64 n, u32* flags) {

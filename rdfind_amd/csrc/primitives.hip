@@ -2,7 +2,7 @@
 //
 // The radix sort is the grouping engine that replaces Flink's sort-based groupBy on the join value
 // (ALG/programs/RDFind.scala:339-345 groupBy("joinValue") -> combineGroup -> reduceGroup): records are
-// packed as (join << capbits | capture) and sorted on exactly the needed bits, 8 bits per pass.
+// packed as (capture << joinbits | join) and sorted on exactly the needed bits, 8 bits per pass.
 // Per pass: (1) per-tile 256-bin digit histogram in LDS, (2) device exclusive scan of the digit-major
 // histogram, (3) stable scatter where each key's in-tile rank comes from wave ballots (8 ballots give
 // the peer mask of lanes with the same digit) plus per-wave running digit counters in LDS.

@@ -40,12 +40,12 @@ struct rdf_ctx {
     std::vector<u64> h_bkeys;
 
     // capture groups
-    DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, gflag, gexcl, goff, gcap, gid, csup, doff, dcur, dgrp;
+    DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
     DevBuf hist, heavy_list, hbit, bcomp, bkeyc, pcnt, poff, pcur, plist;
     u64 J = 0, Jf = 0, G = 0;
     u32 C = 0, Cu = 0, nheavy = 0;
     u64 heavy_threshold = 0;
-    int capbits = 0;
+    int capbits = 0, joinbits = 0;
     u64 *rec_sorted = nullptr;
 
     // cinds
@@ -195,7 +195,8 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->scal, &c->ts, &c->tp, &c->to, &c->cnt, &c->tkeys, &c->tcnt, &c->bkeys, &c->bkeys_tmp,
                       &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
-                      &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->gflag, &c->gexcl, &c->goff, &c->gcap, &c->gid, &c->csup,
+                      &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
+                      &c->gcap, &c->gmap, &c->csup,
                       &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->out,
@@ -297,7 +298,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     if (n)
         hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p,
                            c->o, n, V, c->ms, c->cnt.as<u32>(), dscal(c, 3));
-    hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+    hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->cnt.as<u32>(), V, c->ms, dscal(c, 0));
     rdf_status rs = read_scalars(c, 7);
     if (rs) return rs;
@@ -306,8 +307,8 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     c->Us = (u32)nfreq[0];
     c->Up = (u32)nfreq[1];
     ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
-    hipLaunchKernelGGL(k_frank_final, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(),
-                       3ull * V, V, c->ms, c->frank.as<u32>(), c->fval.as<u32>());
+    hipLaunchKernelGGL(k_frank_final, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(), V, c->ms,
+                       c->frank.as<u32>(), c->fval.as<u32>());
     const u64 E = c->hscal[3];
     const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
     ENSURE(c, tkeys, tcap * 8);
@@ -319,12 +320,10 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
         hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                            st, c->s, c->p, c->o, n, V, c->ms, c->cnt.as<u32>(), c->tkeys.as<u64>(), c->tcnt.as<u32>(),
                            tcap - 1);
-    hipLaunchKernelGGL(k_count_nonempty, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                       c->tkeys.as<u64>(), tcap, dscal(c, 4));
     ENSURE(c, flags, tcap * 4);
     ENSURE(c, pos, tcap * 8);
     hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                       c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>());
+                       c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>(), dscal(c, 4));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
     tend(c, RDF_T_BINARY);
     rs = read_scalars(c, 6);
@@ -418,6 +417,7 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     if (capbits + joinbits > 64) return fail(c, RDF_ERR_LIMIT, "join+capture bits exceed 64");
     if (6ull * V + c->B >= (1ull << 32)) return fail(c, RDF_ERR_LIMIT, "capture id space exceeds 2^32");
     c->capbits = capbits;
+    c->joinbits = joinbits;
     c->ncap = ncap;
     HIP_TRY(c, hipEventRecord(c->ev[2], st));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
@@ -430,11 +430,11 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     ENSURE(c, eblk, (eg + 1ull) * 8);
     if (n) {
         hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits, c->rank,
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, c->rank,
                            c->nranks, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr);
         HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
         hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, capbits, c->rank,
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, c->rank,
                            c->nranks, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>());
     }
     tend(c, RDF_T_EMIT);
@@ -448,13 +448,18 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     tend(c, RDF_T_SORT);
     c->rec_sorted = keys;
     c->sort_passes_records = (u64)((capbits + joinbits + 7) / 8) * J;
-    ENSURE(c, support, ncap * 4);
+    // supports = distinct join values per capture: fresh (capture, join) records counted per key run
+    ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
+    ENSURE(c, flags, std::max<u64>(J, 1) * 4);
+    ENSURE(c, fpos, (J + 1) * 4);
+    ENSURE(c, cstart, (ncap + 1) * 4);
     tbegin(c, RDF_T_SUPPORT);
-    HIP_TRY(c, hipMemsetAsync(c->support.p, 0, ncap * 4, st));
-    const u64 capmask = (capbits >= 64) ? ~0ull : ((1ull << capbits) - 1);
-    if (J)
-        hipLaunchKernelGGL(k_unique_support, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capmask,
-                           c->support.as<u32>());
+    hipLaunchKernelGGL(k_fresh_bounds, dim3(grid_for(J + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, ncap, joinbits,
+                       c->flags.as<u32>(), c->cstart.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), J, c->fpos.as<u32>() + J, st));
+    if (ncap)
+        hipLaunchKernelGGL(k_run_support, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cstart.as<u32>(),
+                           ncap, c->fpos.as<u32>(), c->support.as<u32>());
     tend(c, RDF_T_SUPPORT);
     return RDF_OK;
 }
@@ -464,8 +469,7 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     hipStream_t st = c->stream;
     const u32 V = c->V ? c->V : 1;
     const u64 ncap = c->ncap, J = c->J;
-    const int capbits = c->capbits;
-    const u64 capmask = (capbits >= 64) ? ~0ull : ((1ull << capbits) - 1);
+    const int joinbits = c->joinbits;
     u64* keys = c->rec_sorted;
     tbegin(c, RDF_T_SUPPORT);
     ENSURE(c, flags, std::max(J, ncap) * 4);
@@ -486,21 +490,45 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     if (C)
         hipLaunchKernelGGL(k_external_ids, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fcap.as<u32>(), C,
                            2u * c->U, V, c->fval.as<u32>(), c->Us, c->Up, c->fext.as<u32>());
-    // distinct records of frequent captures, capture ids made compact
-    ENSURE(c, pos, std::max<u64>(J, 1) * 8);
-    if (J)
-        hipLaunchKernelGGL(k_keep_flags, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capmask,
-                           c->support.as<u32>(), c->ms, c->flags.as<u32>());
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), J, dscal(c, 1), st));
-    TRY(read_scalars(c, 2));
-    const u64 Jf = c->hscal[1];
+    // distinct records of frequent captures -> dk = (compact capture << 32 | join) in (capture, join) order,
+    // written to the record buffer that does not hold the sorted keys
+    ENSURE(c, skip, (ncap + 1) * 4);
+    if (ncap)
+        hipLaunchKernelGGL(k_skip_counts, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cstart.as<u32>(),
+                           c->fpos.as<u32>(), c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->skip.as<u32>(), ncap, c->skip.as<u32>() + ncap, st));
+    u32 nfresh = 0, nskip = 0;
+    TRY(read_u32(c, c->fpos.as<u32>() + J, &nfresh));
+    TRY(read_u32(c, c->skip.as<u32>() + ncap, &nskip));
+    const u64 Jf = (u64)nfresh - nskip;
     c->Jf = Jf;
+    u64* dk = keys == c->rec.as<u64>() ? c->rec_tmp.as<u64>() : c->rec.as<u64>();
     ENSURE(c, fk, std::max<u64>(Jf, 1) * 8);
+    ENSURE(c, fk_tmp, std::max<u64>(Jf, 1) * 8);
     if (J)
-        hipLaunchKernelGGL(k_keep_scatter, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, capbits,
-                           capmask, c->flags.as<u32>(), c->pos.as<u64>(), c->fidx.as<u32>(), c->fk.as<u64>());
+        hipLaunchKernelGGL(k_keep_scatter, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, joinbits,
+                           c->fpos.as<u32>(), c->skip.as<u32>(), c->support.as<u32>(), c->ms, c->fidx.as<u32>(), dk,
+                           c->fk.as<u64>());
     tend(c, RDF_T_SUPPORT);
     tbegin(c, RDF_T_GROUPS);
+    // dependent -> join offsets straight from dk; groups need the (join, capture) order: a stable sort of
+    // fk = (join << 32 | capture) on the join bits keeps each group's captures ascending
+    ENSURE(c, csup, std::max<u64>(C, 1) * 4);
+    ENSURE(c, doff, (C + 1ull) * 8);
+    ENSURE(c, dgrp, std::max<u64>(Jf, 1) * 4);
+    if (C)
+        hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->info.as<CapInfo>(), C, c->csup.as<u32>());
+    if (Jf) {
+        hipLaunchKernelGGL(k_key_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, dk, Jf, C,
+                           c->doff.as<u64>());
+        u64* tk = c->fk.as<u64>();
+        u64* tt = c->fk_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64_bits(c->ws, tk, tt, Jf, 32, 32 + joinbits, st));
+        if (tk != c->fk.as<u64>()) std::swap(c->fk, c->fk_tmp);
+    } else {
+        HIP_TRY(c, hipMemsetAsync(c->doff.p, 0, (C + 1ull) * 8, st));
+    }
     ENSURE(c, gflag, std::max<u64>(Jf, 1) * 4);
     ENSURE(c, gexcl, (Jf + 1) * 4);
     if (Jf)
@@ -513,34 +541,15 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     c->G = G;
     ENSURE(c, goff, (G + 1) * 8);
     ENSURE(c, gcap, std::max<u64>(Jf, 1) * 4);
-    ENSURE(c, gid, std::max<u64>(Jf, 1) * 4);
-    if (Jf)
+    ENSURE(c, gmap, (u64)V * 4);
+    if (Jf) {
         hipLaunchKernelGGL(k_group_build, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fk.as<u64>(), Jf,
-                           c->gflag.as<u32>(), c->gexcl.as<u32>(), c->goff.as<u64>(), c->gcap.as<u32>(), c->gid.as<u32>());
+                           c->gflag.as<u32>(), c->gexcl.as<u32>(), c->goff.as<u64>(), c->gcap.as<u32>(), c->gmap.as<u32>());
+        hipLaunchKernelGGL(k_dgrp, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, dk, Jf, c->gmap.as<u32>(),
+                           c->dgrp.as<u32>());
+    }
     c->hscal[14] = Jf;
     HIP_TRY(c, hipMemcpyAsync(c->goff.as<u64>() + G, c->hscal + 14, 8, hipMemcpyHostToDevice, st));
-    // dependent -> groups
-    ENSURE(c, csup, std::max<u64>(C, 1) * 4);
-    ENSURE(c, doff, (C + 1ull) * 8);
-    ENSURE(c, dgrp, std::max<u64>(Jf, 1) * 4);
-    if (C)
-        hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                           c->info.as<CapInfo>(), C, c->csup.as<u32>());
-    if (Jf) {
-        // (capture << 32 | group) keys in fk, sorted with rec_tmp as scratch (both hold >= Jf u64); the
-        // dependent offsets come from the sorted keys (a sharded rank holds only part of each support)
-        u64* tk = c->fk.as<u64>();
-        u64* tt = c->rec_tmp.as<u64>();
-        hipLaunchKernelGGL(k_make_tkeys, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gcap.as<u32>(),
-                           c->gid.as<u32>(), Jf, tk);
-        // records are in group order, so a stable sort on the capture bits alone keeps each list sorted
-        HIP_TRY(c, radix_sort_u64_bits(c->ws, tk, tt, Jf, 32, 32 + bits_for(C ? C - 1 : 0), st));
-        hipLaunchKernelGGL(k_low32, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, c->dgrp.as<u32>());
-        hipLaunchKernelGGL(k_key_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, tk, Jf, C,
-                           c->doff.as<u64>());
-    } else {
-        HIP_TRY(c, hipMemsetAsync(c->doff.p, 0, (C + 1ull) * 8, st));
-    }
     tend(c, RDF_T_GROUPS);
     return RDF_OK;
 }
