@@ -12,9 +12,15 @@ static constexpr uint8_t LIGHT = 0xff;
 #define RDF_LIGHT_SEG 2048
 #endif
 static constexpr u64 LIGHT_SEG = RDF_LIGHT_SEG;  // groups of one dependent verified by one light work item
-static constexpr int LIGHT_IT = 4;             // groups per lane whose metadata is loaded together
+#ifndef RDF_LIGHT_IT
+#define RDF_LIGHT_IT 4
+#endif
+static constexpr int LIGHT_IT = RDF_LIGHT_IT;  // groups per lane whose metadata is loaded together
 static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
-static constexpr int LIGHT_BATCH = 8;    // candidates searched together in k_light's many-groups path
+#ifndef RDF_LIGHT_BATCH
+#define RDF_LIGHT_BATCH 8
+#endif
+static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched together in k_light
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
 struct __align__(16) CapInfo {

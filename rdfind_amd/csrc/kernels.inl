@@ -940,7 +940,7 @@ __device__ unsigned long long g_light_stats[16];
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
 __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
                                                      const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
-                                                     u64* dead, u32* arrive, u64* slots, u32* counts) {
+                                                     u64* dead, u64* slots, u32* counts) {
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -1034,25 +1034,39 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     const u64 oct0 = choff[d] + chunk * 8;  // first octet slot of this chunk
     const u64 noct = choff[d + 1] - oct0;
     const u32 nvalid = noct < 8 ? (u32)noct : 8u;
-    const u64 slot = oct0;                  // multi-segment bookkeeping is per chunk, keyed by its first octet
     if (nseg == 1) {
         slot_emit(oct0, nvalid, d, cand, alive, slots, counts);
         return;
     }
-    // several segments: publish the killed candidates; the last segment to arrive emits the survivors
-    // (device-scope atomics execute at the memory side, so the returned OR is the final mask)
-    u32 last = 0;
-    if (lane == 0) {
-        if (alive0 & ~alive) atomicOr(&dead[slot], alive0 & ~alive);
-        __threadfence();
-        last = atomicAdd(&arrive[slot], 1u) == (u32)(nseg - 1);
-    }
-    if (__shfl(last, 0, RDF_WAVE)) {
-        __threadfence();
-        u64 dm = 0;
-        if (lane == 0) dm = atomicOr(&dead[slot], 0ull);
-        dm = __shfl(dm, 0, RDF_WAVE);
-        slot_emit(oct0, nvalid, d, cand, alive0 & ~dm, slots, counts);
+    // several segments: publish the killed candidates (a device-scope atomic, executed at the memory side);
+    // k_light_mseg_emit emits the survivors once this kernel has finished.  No fence and no arrival
+    // counter: an agent-scope release fence writes back the whole L2 of the XCD, per work item.
+    if (lane == 0 && (alive0 & ~alive)) atomicOr(&dead[oct0], alive0 & ~alive);
+}
+
+// chunks verified by several segments: survivors = candidates minus the union of the segments' kills
+// (launched after k_light; the kernel boundary orders the kills before these reads)
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(CindView v, const u32* __restrict__ pivot,
+                                                               const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep,
+                                                               u64 WM, const u64* __restrict__ choff,
+                                                               const u64* __restrict__ dead, u64* slots, u32* counts) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= WM) return;
+    const u32 d = mch_dep[w];
+    const u64 chunk = w - mchoff[d];
+    const u32 cand = chunk_candidate(v, d, v.info[d], pivot[d], chunk);
+    const u64 alive0 = __ballot(cand != NONE32);
+    const u64 oct0 = choff[d] + chunk * 8;
+    const u64 noct = choff[d + 1] - oct0;
+    slot_emit(oct0, noct < 8 ? (u32)noct : 8u, d, cand, alive0 & ~dead[oct0], slots, counts);
+}
+
+// multi-segment chunks per dependent: nitem / nseg when the dependent's groups span several segments
+__global__ __launch_bounds__(RDF_BLOCK) void k_mseg_chunks(const u64* __restrict__ doff, const u32* __restrict__ nitem, u32 C,
+                                                           u32* nmch) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 nseg = (doff[d + 1] - doff[d] + LIGHT_SEG - 1) / LIGHT_SEG;
+        nmch[d] = nseg > 1 ? (u32)(nitem[d] / nseg) : 0u;
     }
 }
 

@@ -73,7 +73,7 @@ struct rdf_ctx {
     u64 x_count = 0, x_recv_count = 0;
     u32 x_bytes = 8;
     bool x_imported = true;
-    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep;
+    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep;
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
@@ -204,7 +204,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
-                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
@@ -756,8 +756,8 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     hipStream_t st = c->stream;
     const u64 nslot = std::max<u64>(WL, 1);
     ENSURE(c, epairs_tmp, nslot * 8 * 8);
-    ENSURE(c, dead, nslot * 12);  // dead masks (multi-segment chunks), then per-chunk arrival counters
-    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, nslot * 12, st));
+    ENSURE(c, dead, nslot * 8);  // kill masks of multi-segment chunks, keyed by the chunk's first octet
+    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, nslot * 8, st));
     ENSURE(c, lslot, nslot * 4);
     HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, nslot * 4, st));
     ENSURE(c, item_dep, std::max<u64>(WI, 1) * 4);
@@ -776,7 +776,25 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     if (WI)
         hipLaunchKernelGGL(k_light, dim3((unsigned)((WI + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
                            0, st, v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
-                           c->dead.as<u64>(), (u32*)(c->dead.as<u64>() + nslot), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+                           c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+    // chunks of dependents whose groups span several segments: emitted once all their segments are done
+    u64 WM = 0;
+    if (WI) {
+        ENSURE(c, nmch, std::max<u64>(c->C, 1) * 4);
+        ENSURE(c, mchoff, (c->C + 1ull) * 8);
+        hipLaunchKernelGGL(k_mseg_chunks, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(),
+                           c->nitl.as<u32>(), c->C, c->nmch.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nmch.as<u32>(), c->mchoff.as<u64>(), c->C, c->mchoff.as<u64>() + c->C, st));
+        TRY(read_u64(c, c->mchoff.as<u64>() + c->C, &WM));
+    }
+    if (WM) {
+        ENSURE(c, mch_dep, WM * 4);
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->mchoff.as<u64>(),
+                           c->C, c->mch_dep.as<u32>());
+        hipLaunchKernelGGL(k_light_mseg_emit, dim3((unsigned)((WM + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->mchoff.as<u64>(), c->mch_dep.as<u32>(), WM,
+                           c->choffl.as<u64>(), c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+    }
     ENSURE(c, pos, (WL + 1) * 8);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
     TRY(read_u64(c, c->pos.as<u64>() + WL, E));

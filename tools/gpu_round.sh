@@ -21,6 +21,11 @@ for step in "$@"; do
         || { echo "prof failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
       find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG.kernel_stats.csv \;
       head -25 gpurun_out/prof_$TAG.kernel_stats.csv ;;
+    qprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/qprof_$TAG -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/qprof_$TAG.log 2>&1 \
+        || { echo "qprof failed"; tail -30 gpurun_out/qprof_$TAG.log; exit 1; }
+      python3 tools/trace_step.py gpurun_out/qprof_$TAG/run_kernel_trace.csv | awk '$2 > 40 || /total/' ;;
     pmc)
       tools/pmc.sh $TAG || exit 1 ;;
     lstats)
