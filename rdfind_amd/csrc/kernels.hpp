@@ -8,6 +8,7 @@ static constexpr int LH_SLOTS = 4096;     // LDS hash slots (u32 keys) for unary
 static constexpr int LB_SLOTS = 2048;     // LDS hash slots (u64 keys) for binary counting
 static constexpr int HMAX = 64;           // heavy groups tracked as bit columns (one u64 per capture)
 static constexpr uint8_t LIGHT = 0xff;
+static constexpr u32 DGRP_HEAVY = 0x80000000u;  // tag of a dependent -> group entry whose group is heavy
 #ifndef RDF_LIGHT_SEG
 #define RDF_LIGHT_SEG 2048
 #endif
@@ -17,6 +18,14 @@ static constexpr u64 LIGHT_SEG = RDF_LIGHT_SEG;  // groups of one dependent veri
 #endif
 static constexpr int LIGHT_IT = RDF_LIGHT_IT;  // groups per lane whose metadata is loaded together
 static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
+#ifndef RDF_PACK_MAXG2
+#define RDF_PACK_MAXG2 512
+#endif
+#ifndef RDF_PACK_NL
+#define RDF_PACK_NL 16
+#endif
+static constexpr u64 LIGHT_PACK_MAXG2 = RDF_PACK_MAXG2;  // ... and those with at most this many groups of
+static constexpr u32 LIGHT_PACK_NL = RDF_PACK_NL;        // which at most this many are light
 #ifndef RDF_LIGHT_BATCH
 #define RDF_LIGHT_BATCH 8
 #endif

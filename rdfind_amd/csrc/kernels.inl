@@ -646,25 +646,29 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_nseg(const u64* __restrict_
     }
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u64* best_out, u32* nlight_out) {
+// The pivot pass visits every (dependent, group) entry once and tags the entries of heavy groups in place
+// (DGRP_HEAVY): the light kernels then skip them without a per-group gather of hbit.
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp_tag, u64* best_out, u32* nlight_out) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = v.doff[d], e = v.doff[d + 1];
         if (e - b > PIVOT_SHORT) continue;
         u64 best = ~0ull;
         u32 nlight = 0;
         for (u64 j = b; j < e; ++j) {
-            const u32 g = v.dgrp[j];
+            const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
             const u64 key = ((v.goff[g + 1] - v.goff[g]) << 32) | g;
             best = key < best ? key : best;
-            nlight += v.hbit[g] == LIGHT;
+            const bool light = v.hbit[g] == LIGHT;
+            nlight += light;
+            dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
         }
         best_out[d] = best;
         nlight_out[d] = nlight;
     }
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, const u64* __restrict__ segoff, u64 W, u64* best_out,
-                                                         u32* nlight_out) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
+                                                         u64* best_out, u32* nlight_out) {
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -675,11 +679,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, const u64* 
     u64 best = ~0ull;  // (size << 32 | group)
     u32 nlight = 0;
     for (u64 j = b + lane; j < e; j += RDF_WAVE) {
-        u32 g = v.dgrp[j];
-        u64 sz = v.goff[g + 1] - v.goff[g];
-        u64 key = (sz << 32) | g;
+        const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
+        const u64 sz = v.goff[g + 1] - v.goff[g];
+        const u64 key = (sz << 32) | g;
         best = key < best ? key : best;
-        nlight += v.hbit[g] == LIGHT;
+        const bool light = v.hbit[g] == LIGHT;
+        nlight += light;
+        dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -709,7 +715,9 @@ __device__ inline void light_plan(const CindView& v, u32 d, u32 nlight, u64 sz, 
     }
     const u64 ng = v.doff[d + 1] - v.doff[d];
     const u32 oc = (u32)((sz + 7) / 8);
-    const bool packed = ng <= LIGHT_PACK_MAXG && ng <= (sz > 4 ? sz : 4);
+    // packed: each lane walks all ng group entries (heavy ones are skipped by their tag) and searches the
+    // light ones, so it pays when the groups are few or almost all heavy
+    const bool packed = (ng <= LIGHT_PACK_MAXG && ng <= (sz > 4 ? sz : 4)) || (ng <= LIGHT_PACK_MAXG2 && nlight <= LIGHT_PACK_NL);
     noct[d] = oc;
     nitem[d] = packed ? 0u : (u32)((sz + RDF_WAVE - 1) / RDF_WAVE) * (u32)((ng + LIGHT_SEG - 1) / LIGHT_SEG);
     npacked[d] = packed ? oc : 0u;
@@ -908,8 +916,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(CindView v, const u3
     bool ok = cand != NONE32;
     const u64 b = v.doff[d], e = v.doff[d + 1];
     for (u64 j = b; ok && j < e; ++j) {
-        const u32 gr = v.dgrp[j];
-        if (gr == piv || v.hbit[gr] != LIGHT) continue;
+        const u32 gr = v.dgrp[j];  // heavy entries carry DGRP_HEAVY (k_pivot_*)
+        if (gr == piv || (gr & DGRP_HEAVY)) continue;
         ok = bsearch_u32(v.gcap + v.goff[gr], v.goff[gr + 1] - v.goff[gr], cand);
     }
     const u64 alive = __ballot(ok);
@@ -974,7 +982,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
         }
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it)
-            if (gg[it] != NONE32 && (gg[it] == piv || v.hbit[gg[it]] != LIGHT)) gg[it] = NONE32;
+            if (gg[it] == piv || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY too
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it) {
             gbv[it] = 0;

@@ -720,8 +720,8 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->pseg.as<u32>(), c->psegoff.as<u64>(), C, c->psegoff.as<u64>() + C, st));
         HIP_TRY(c, hipMemsetAsync(c->pbest.p, 0xff, (u64)C * 8, st));
         HIP_TRY(c, hipMemsetAsync(c->pnl.p, 0, (u64)C * 4, st));
-        hipLaunchKernelGGL(k_pivot_short, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
-                           c->pnl.as<u32>());
+        hipLaunchKernelGGL(k_pivot_short, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->dgrp.as<u32>(),
+                           c->pbest.as<u64>(), c->pnl.as<u32>());
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
@@ -729,7 +729,7 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
     tbegin(c, RDF_T_PIVOT);
     if (WS)
         hipLaunchKernelGGL(k_pivot_seg, dim3((unsigned)((WS + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
-                           0, st, v, c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
+                           0, st, v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
     tend(c, RDF_T_PIVOT);
     return RDF_OK;
 }
