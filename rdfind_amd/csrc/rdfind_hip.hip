@@ -5,6 +5,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <utility>
+#include <initializer_list>
 
 #include "../../include/rdfind_hip.h"
 #include "primitives.hpp"
@@ -163,6 +165,32 @@ static rdf_status read_u32(rdf_ctx* c, const void* dptr, u32* out) {
 }
 
 static u64* dscal(rdf_ctx* c, int i) { return c->scal.as<u64>() + i; }
+
+// Several device scalars with ONE host round trip: a one-thread kernel gathers them into scal[8..13],
+// one copy brings them back (each separate read is a stream drain plus a copy, ~20-40 us).
+struct ScalarGather {
+    const void* p[6];
+    int bytes[6];
+    int n;
+};
+
+__global__ void k_gather_scalars(ScalarGather g, u64* dst) {
+    for (int i = 0; i < g.n; ++i) dst[i] = g.bytes[i] == 8 ? *(const u64*)g.p[i] : (u64) * (const u32*)g.p[i];
+}
+
+static rdf_status read_multi(rdf_ctx* c, std::initializer_list<std::pair<const void*, int>> refs, u64* out) {
+    ScalarGather g = {};
+    for (const auto& r : refs) {
+        g.p[g.n] = r.first;
+        g.bytes[g.n] = r.second;
+        ++g.n;
+    }
+    hipLaunchKernelGGL(k_gather_scalars, dim3(1), dim3(1), 0, c->stream, g, dscal(c, 8));
+    HIP_TRY(c, hipMemcpyAsync(c->hscal + 8, dscal(c, 8), g.n * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < g.n; ++i) out[i] = c->hscal[8 + i];
+    return RDF_OK;
+}
 
 static const unsigned kGrid = 2048;  // grid-stride kernels: 8 blocks of 256 threads per CU
 
@@ -478,8 +506,12 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
                        c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fidx.as<u32>(), ncap, c->fidx.as<u32>() + ncap, st));
     u32 C = 0, Cu = 0;
-    TRY(read_u32(c, c->fidx.as<u32>() + ncap, &C));
-    TRY(read_u32(c, c->fidx.as<u32>() + 2ull * c->U, &Cu));
+    {
+        u64 v[2];
+        TRY(read_multi(c, {{c->fidx.as<u32>() + ncap, 4}, {c->fidx.as<u32>() + 2ull * c->U, 4}}, v));
+        C = (u32)v[0];
+        Cu = (u32)v[1];
+    }
     c->C = C;
     c->Cu = Cu;
     ENSURE(c, fcap, std::max<u64>(C, 1) * 4);
@@ -497,10 +529,9 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
         hipLaunchKernelGGL(k_skip_counts, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cstart.as<u32>(),
                            c->fpos.as<u32>(), c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->skip.as<u32>(), ncap, c->skip.as<u32>() + ncap, st));
-    u32 nfresh = 0, nskip = 0;
-    TRY(read_u32(c, c->fpos.as<u32>() + J, &nfresh));
-    TRY(read_u32(c, c->skip.as<u32>() + ncap, &nskip));
-    const u64 Jf = (u64)nfresh - nskip;
+    u64 fs[2];
+    TRY(read_multi(c, {{c->fpos.as<u32>() + J, 4}, {c->skip.as<u32>() + ncap, 4}}, fs));
+    const u64 Jf = fs[0] - fs[1];
     c->Jf = Jf;
     u64* dk = keys == c->rec.as<u64>() ? c->rec_tmp.as<u64>() : c->rec.as<u64>();
     ENSURE(c, fk, std::max<u64>(Jf, 1) * 8);
@@ -742,11 +773,14 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->npk.as<u32>(), c->pkoff.as<u64>(), C, c->pkoff.as<u64>() + C, st));
-    TRY(read_u64(c, c->choffl.as<u64>() + C, WL));
-    TRY(read_u64(c, c->pkoff.as<u64>() + C, WP));
-    TRY(read_u64(c, c->choffh.as<u64>() + C, WH));
-    TRY(read_u64(c, dscal(c, 2), &c->heavy_candidates));
-    TRY(read_u64(c, c->itoffl.as<u64>() + C, WI));
+    u64 v[5];
+    TRY(read_multi(c, {{c->choffl.as<u64>() + C, 8}, {c->pkoff.as<u64>() + C, 8}, {c->choffh.as<u64>() + C, 8},
+                       {dscal(c, 2), 8}, {c->itoffl.as<u64>() + C, 8}}, v));
+    *WL = v[0];
+    *WP = v[1];
+    *WH = v[2];
+    c->heavy_candidates = v[3];
+    *WI = v[4];
     return RDF_OK;
 }
 
@@ -876,8 +910,10 @@ static rdf_status d_class_table(rdf_ctx* c, const CindView& v, u64* nmem, u32* n
     hipLaunchKernelGGL(k_nonzero_flags, dim3(grid_for(tcapc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ctab.as<u64>(),
                        tcapc, c->cflag.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->cflag.as<u32>(), c->ccid.as<u32>(), tcapc, c->ccid.as<u32>() + tcapc, st));
-    TRY(read_u64(c, dscal(c, 3), nmem));
-    TRY(read_u32(c, c->ccid.as<u32>() + tcapc, ncls));
+    u64 rv[2];
+    TRY(read_multi(c, {{dscal(c, 3), 8}, {c->ccid.as<u32>() + tcapc, 4}}, rv));
+    *nmem = rv[0];
+    *ncls = (u32)rv[1];
     return RDF_OK;
 }
 
@@ -900,8 +936,10 @@ static rdf_status d_class_tiles(rdf_ctx* c, u64 nmem, u32 ncls, u64* HC, u64* NT
     hipLaunchKernelGGL(k_class_tiles, dim3(grid_for(std::max<u32>(ncls, 1), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->coff.as<u64>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(), ncls, c->ctiles.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ctiles.as<u32>(), c->ctoff.as<u64>(), ncls, c->ctoff.as<u64>() + ncls, st));
-    TRY(read_u64(c, c->cobase.as<u64>() + nmem, HC));
-    TRY(read_u64(c, c->ctoff.as<u64>() + ncls, NT));
+    u64 v[2];
+    TRY(read_multi(c, {{c->cobase.as<u64>() + nmem, 8}, {c->ctoff.as<u64>() + ncls, 8}}, v));
+    *HC = v[0];
+    *NT = v[1];
     return RDF_OK;
 }
 
@@ -1005,13 +1043,6 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     c->n_out = K + H + HC;
     c->n_class_out = HC;
     c->out_ptr = c->out.as<u32>();
-    const u32 C = c->C;
-    c->h_fcap.resize(C);
-    c->h_csup.resize(C);
-    if (C) {
-        HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fext.p, (u64)C * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(c, hipMemcpy(c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
-    }
     rdf_cind_stats& s = c->cstats;
     memset(&s, 0, sizeof(s));
     s.n_cinds = c->n_out;
@@ -1427,12 +1458,21 @@ rdf_status rdf_cind_count(rdf_ctx* c, uint64_t* n) {
     return RDF_OK;
 }
 
+// host mirrors for copy-out (run table, external capture ids, supports): filled on the first copy after a
+// run, so a run whose results stay in HBM pays no device -> host traffic
 static rdf_status load_runs(rdf_ctx* c) {
     if (c->h_runs_valid) return RDF_OK;
     c->h_runoff.resize(c->n_runs + 1);
     c->h_rundep.resize(c->n_runs);
     HIP_TRY(c, hipMemcpy(c->h_runoff.data(), c->runoff.p, (c->n_runs + 1) * 8, hipMemcpyDeviceToHost));
     if (c->n_runs) HIP_TRY(c, hipMemcpy(c->h_rundep.data(), c->rundep.p, c->n_runs * 4, hipMemcpyDeviceToHost));
+    const u32 C = c->C;
+    c->h_fcap.resize(C);
+    c->h_csup.resize(C);
+    if (C) {
+        HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fext.p, (u64)C * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
+    }
     c->h_runs_valid = true;
     return RDF_OK;
 }
