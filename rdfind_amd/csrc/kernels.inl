@@ -106,6 +106,138 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_unary_count(const u32* __restrict
         if (lkey[i] != EMPTY32) atomicAdd(&cnt[lkey[i]], lcnt[i]);
 }
 
+// Weighted variant of the leader rounds of wave_merge: lanes holding the same key (anywhere in the wave)
+// collapse into one lane carrying the summed weight.
+template <typename T, int ROUNDS>
+__device__ inline u32 wave_merge_weighted(T key, bool active, u32 w) {
+    const int lane = lane_id();
+    u32 cnt = active ? w : 0u;
+    u64 todo = __ballot(active);
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (__popcll(todo) <= 1) break;
+        const int l = __ffsll((long long)todo) - 1;
+        const T kl = __shfl(key, l, RDF_WAVE);
+        const bool mine = ((todo >> lane) & 1ull) && key == kl;
+        const u64 m = __ballot(mine);
+        todo &= ~m;
+        if (__popcll(m) > 1) {
+            const u32 tot = wave_sum(mine ? cnt : 0u);
+            if (mine) cnt = lane == l ? tot : 0u;
+        }
+    }
+    return cnt;
+}
+
+// K1, partitioned (no per-key global atomics).  After the wave merge, every (key, count) pair goes to the
+// bucket of its key's high bits (UC_R = 2^UC_BITS counters, one LDS image); pass 1 histograms the buckets
+// per block, pass 2 scatters the pairs into bucket order (positions from LDS atomics: the order inside a
+// bucket is irrelevant to counting), then one block per bucket (a few slices for a hot bucket) counts its
+// pairs in LDS and writes the bucket's counters with plain coalesced stores.
+static constexpr int UC_BITS = 13;
+static constexpr u32 UC_R = 1u << UC_BITS;
+static constexpr u32 UC_MAXB = 4096;        // buckets: 3V <= 2^26
+static constexpr u64 UC_SLICE = 1ull << 15; // pairs per counting block
+#ifndef RDF_UCM
+#define RDF_UCM 0, 2, 1
+#endif
+static constexpr int UCM_ROUNDS[3] = {RDF_UCM};  // wave-merge leader rounds for the s / p / o keys
+static constexpr int UCM_S = UCM_ROUNDS[0], UCM_P = UCM_ROUNDS[1], UCM_O = UCM_ROUNDS[2];
+
+template <bool SCATTER>
+__global__ __launch_bounds__(RDF_BLOCK) void k_ucount_part(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                           const u32* __restrict__ o, u64 n, u32 V, u32 NB, u32* ghist,
+                                                           u64* __restrict__ pairs) {
+    __shared__ u32 lh[UC_MAXB];
+    for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
+    __syncthreads();
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    // the next iteration's triple is loaded before this one is processed (few waves per SIMD: the loads'
+    // latency would otherwise be paid once per iteration)
+    u32 ns = 0, np = 0, no = 0;
+    if (b + threadIdx.x < e) {
+        ns = s[b + threadIdx.x];
+        np = p[b + threadIdx.x];
+        no = o[b + threadIdx.x];
+    }
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        const bool act = i < e;
+        u32 key[3], c[3];
+        key[0] = ns;
+        key[1] = V + np;
+        key[2] = 2u * V + no;
+        if (i + RDF_BLOCK < e) {
+            ns = s[i + RDF_BLOCK];
+            np = p[i + RDF_BLOCK];
+            no = o[i + RDF_BLOCK];
+        }
+        c[0] = wave_merge<u32, UCM_S>(key[0], act);
+        c[1] = wave_merge<u32, UCM_P>(key[1], act);
+        c[2] = wave_merge<u32, UCM_O>(key[2], act);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            if (!c[t]) continue;
+            const u32 bk = key[t] >> UC_BITS;
+            if (SCATTER) pairs[atomicAdd(&lh[bk], 1u)] = ((u64)key[t] << 32) | c[t];
+            else atomicAdd(&lh[bk], 1u);
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
+    }
+}
+
+// slices per bucket: ceil(len / UC_SLICE) (at least 1, so every bucket's counters get written)
+__global__ __launch_bounds__(RDF_BLOCK) void k_ucount_nslices(const u32* __restrict__ ghist, u32 NB, u32 G, u32* nsl) {
+    for (u32 b = blockIdx.x * RDF_BLOCK + threadIdx.x; b < NB; b += gridDim.x * RDF_BLOCK) {
+        const u64 len = ghist[(u64)(b + 1) * G] - ghist[(u64)b * G];
+        const u64 k = (len + UC_SLICE - 1) / UC_SLICE;
+        nsl[b] = k < 1 ? 1u : (u32)k;
+    }
+}
+
+// one block per (bucket, slice) of the compact slice list soff (exclusive scan of nsl, soff[NB] = total);
+// ghist = exclusive scan of the bucket-major histogram (G blocks per bucket, ghist[NB * G] = total pairs)
+__global__ __launch_bounds__(RDF_BLOCK) void k_ucount_bucket(const u64* __restrict__ pairs, const u32* __restrict__ ghist,
+                                                             const u32* __restrict__ soff, u32 NB, u32 G, u64 K, u32* cnt) {
+    __shared__ u32 lc[UC_R];
+    const u32 x = blockIdx.x;
+    if (x >= soff[NB]) return;
+    u32 lo = 0, hi = NB;  // last bucket with soff[b] <= x
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (soff[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    const u32 bk = lo, j = x - soff[bk];
+    const u64 nsl = soff[bk + 1] - soff[bk];
+    const u64 start = ghist[(u64)bk * G], end = ghist[(u64)(bk + 1) * G];
+    const u64 len = end - start;
+    const u64 s0 = start + len * j / nsl, s1 = start + len * (j + 1) / nsl;
+    for (u32 i = threadIdx.x; i < UC_R; i += RDF_BLOCK) lc[i] = 0;
+    __syncthreads();
+    const u64 n_round = s0 + (s1 - s0 + RDF_BLOCK - 1) / RDF_BLOCK * RDF_BLOCK;
+    for (u64 i = s0 + threadIdx.x; i < n_round; i += RDF_BLOCK) {
+        const bool act = i < s1;
+        const u64 pr = act ? pairs[i] : 0ull;
+        const u32 key = (u32)(pr >> 32);
+        const u32 c = wave_merge_weighted<u32, 2>(key, act, (u32)pr);
+        if (c) atomicAdd(&lc[key & (UC_R - 1)], c);
+    }
+    __syncthreads();
+    const u64 base = (u64)bk << UC_BITS;
+    const u32 lim = K - base < UC_R ? (u32)(K - base) : UC_R;
+    if (nsl == 1) {
+        for (u32 i = threadIdx.x; i < lim; i += RDF_BLOCK) cnt[base + i] = lc[i];
+    } else {  // several slices share the bucket (cnt was zeroed)
+        for (u32 i = threadIdx.x; i < lim; i += RDF_BLOCK)
+            if (lc[i]) atomicAdd(&cnt[base + i], lc[i]);
+    }
+}
+
 // Block-reduced counter add (all threads of the block call it): device-scope atomics execute at the
 // memory side, ~11 ns apart on one address, so one per block instead of one per wave.
 __device__ inline void block_counter_add(u64* counter, u32 v) {

@@ -75,7 +75,7 @@ struct rdf_ctx {
     u64 x_count = 0, x_recv_count = 0;
     u32 x_bytes = 8;
     bool x_imported = true;
-    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep;
+    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep, uhist, upairs, usoff;
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
@@ -232,7 +232,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
-                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->upairs, &c->usoff, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
@@ -314,9 +314,30 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     ENSURE(c, cnt, 3ull * V * 4);
     HIP_TRY(c, hipMemsetAsync(c->cnt.p, 0, 3ull * V * 4, st));
     tbegin(c, RDF_T_UNARY);
-    if (n)
+    const u64 K = 3ull * V;
+    const u64 NB = (K + UC_R - 1) / UC_R;
+    if (n && NB <= UC_MAXB) {
+        // partitioned counting: bucket histogram, scatter of (key, count) pairs, per-bucket LDS counting
+        const unsigned G = std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024);
+        const u64 nh = NB * G;
+        ENSURE(c, uhist, (nh + 1) * 4);
+        ENSURE(c, upairs, 3 * n * 8);
+        hipLaunchKernelGGL((k_ucount_part<false>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V, (u32)NB,
+                           c->uhist.as<u32>(), (u64*)nullptr);
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
+        hipLaunchKernelGGL((k_ucount_part<true>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V, (u32)NB,
+                           c->uhist.as<u32>(), c->upairs.as<u64>());
+        ENSURE(c, usoff, (NB + 1) * 4);
+        hipLaunchKernelGGL(k_ucount_nslices, dim3(grid_for(NB, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(),
+                           (u32)NB, G, c->usoff.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->usoff.as<u32>(), c->usoff.as<u32>(), NB, c->usoff.as<u32>() + NB, st));
+        const u64 max_slices = NB + 3 * n / UC_SLICE + 1;  // >= sum over buckets of max(1, ceil(len / UC_SLICE))
+        hipLaunchKernelGGL(k_ucount_bucket, dim3((unsigned)max_slices), dim3(RDF_BLOCK), 0, st, c->upairs.as<u64>(),
+                           c->uhist.as<u32>(), c->usoff.as<u32>(), (u32)NB, (u32)G, K, c->cnt.as<u32>());
+    } else if (n) {
         hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                            st, c->s, c->p, c->o, n, V, c->cnt.as<u32>());
+    }
     ENSURE(c, frank, 3ull * V * 4);
     ENSURE(c, flags, 3ull * V * 4);
     hipLaunchKernelGGL(k_frank_flags, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(),

@@ -4,7 +4,7 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-first = sys.argv[2] if len(sys.argv) > 2 else "k_unary_count"
+first = sys.argv[2] if len(sys.argv) > 2 else "k_ucount_part"
 idx = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
 last = rows[idx[-1]:]
 tot = 0.0
