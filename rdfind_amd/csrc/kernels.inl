@@ -254,6 +254,24 @@ __device__ inline void block_counter_add(u64* counter, u32 v) {
     __syncthreads();
 }
 
+// block-wide exclusive scan of one u32 per thread; *total = block sum (all threads must call it)
+__device__ inline u32 block_exclusive_scan_u32(u32 v, u32* lds_wave, u32* total) {
+    const int wave = threadIdx.x / RDF_WAVE;
+    const u32 incl = wave_inclusive_scan(v);
+    if (lane_id() == RDF_WAVE - 1) lds_wave[wave] = incl;
+    __syncthreads();
+    u32 woff = 0, sum = 0;
+#pragma unroll
+    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
+        const u32 x = lds_wave[w];
+        woff += w < wave ? x : 0u;
+        sum += x;
+    }
+    *total = sum;
+    __syncthreads();  // lds_wave is reused by the next call
+    return woff + incl - v;
+}
+
 // number of frequent values per condition type (for stats)
 __global__ __launch_bounds__(RDF_BLOCK) void k_count_frequent(const u32* __restrict__ cnt, u32 V, u32 ms, u64* out3) {
     for (int t = 0; t < 3; ++t) {
@@ -327,8 +345,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_binary_emit_count(const u32* __re
         freq_flags(cnt, V, ms, s[i], p[i], o[i], fs, fp, fo);
         c += (fs && fp) + (fs && fo) + (fp && fo);
     }
-    c = wave_sum(c);
-    if (lane_id() == 0 && c) atomicAdd(total, (u64)c);
+    block_counter_add(total, c);
 }
 
 __device__ inline void global_hash_add(u64* tkeys, u32* tcnt, u64 mask, u64 key, u32 c) {
@@ -452,24 +469,6 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
     }
 }
 
-// Block-aggregated append: one global atomic per block iteration instead of one per wave.
-// block-wide exclusive scan of one u32 per thread; *total = block sum (all threads must call it)
-__device__ inline u32 block_exclusive_scan_u32(u32 v, u32* lds_wave, u32* total) {
-    const int wave = threadIdx.x / RDF_WAVE;
-    const u32 incl = wave_inclusive_scan(v);
-    if (lane_id() == RDF_WAVE - 1) lds_wave[wave] = incl;
-    __syncthreads();
-    u32 woff = 0, sum = 0;
-#pragma unroll
-    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
-        const u32 x = lds_wave[w];
-        woff += w < wave ? x : 0u;
-        sum += x;
-    }
-    *total = sum;
-    __syncthreads();  // lds_wave is reused by the next call
-    return woff + incl - v;
-}
 
 // ================================================================================================
 // K3: join partners  (CreateJoinPartners.flatMap, ALG/operators/CreateJoinPartners.scala:86-147)
@@ -526,6 +525,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             int joinbits, u32 rank, u32 nranks, u64* block_counts,
                                                             const u64* __restrict__ block_offsets, u64* out) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
+    __shared__ u64 stage[WRITE ? RDF_BLOCK * 9 : 1];  // the iteration's records, written out contiguously
     const u64 b = (u64)blockIdx.x * per;
     const u64 e = b + per < n ? b + per : n;
     u64 run = WRITE ? block_offsets[blockIdx.x] : 0;
@@ -536,8 +536,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, rank, nranks, rec);
         u32 total;
         const u32 off = block_exclusive_scan_u32(c, lds_wave, &total);
-        if (WRITE)
-            for (u32 k = 0; k < c; ++k) out[run + off + k] = rec[k];
+        if (WRITE) {
+            for (u32 k = 0; k < c; ++k) stage[off + k] = rec[k];
+            __syncthreads();
+            for (u32 k = threadIdx.x; k < total; k += RDF_BLOCK) out[run + k] = stage[k];
+            __syncthreads();
+        }
         run += total;
     }
     if (!WRITE && threadIdx.x == 0) block_counts[blockIdx.x] = run;

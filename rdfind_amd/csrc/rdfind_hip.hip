@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include <utility>
@@ -40,6 +41,8 @@ struct rdf_ctx {
     DevBuf cnt, tkeys, tcnt, bkeys, bkeys_tmp, lkeys, lvals, flags, pos;
     u64 B = 0, lcap = 0;
     std::vector<u64> h_bkeys;
+    bool h_bkeys_valid = false;
+    bool force_global_counts = false;
 
     // capture groups
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
@@ -130,6 +133,12 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
                         std::string(#expr) + ": " + hipGetErrorString(_e));                        \
     } while (0)
 
+#define TRY(expr)                    \
+    do {                             \
+        rdf_status _r = (expr);      \
+        if (_r != RDF_OK) return _r; \
+    } while (0)
+
 #define ENSURE(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.ensure((size_t)(bytes)))
 
 static int bits_for(u64 maxval) {  // bits needed to represent values in [0, maxval]
@@ -192,6 +201,14 @@ static rdf_status read_multi(rdf_ctx* c, std::initializer_list<std::pair<const v
     return RDF_OK;
 }
 
+static rdf_status load_bkeys(rdf_ctx* c) {
+    if (c->h_bkeys_valid) return RDF_OK;
+    c->h_bkeys.resize(c->B);
+    if (c->B) HIP_TRY(c, hipMemcpy(c->h_bkeys.data(), c->bkeys.p, c->B * 8, hipMemcpyDeviceToHost));
+    c->h_bkeys_valid = true;
+    return RDF_OK;
+}
+
 static const unsigned kGrid = 2048;  // grid-stride kernels: 8 blocks of 256 threads per CU
 
 extern "C" {
@@ -203,6 +220,10 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     *out = nullptr;
     rdf_ctx* c = new rdf_ctx();
     c->device = device;
+    // test hook: RDFIND_COUNT_PATHS=atomic selects the global-atomic unary counting kernel (the fallback of
+    // the partitioned K1 for |V| > 2^26 / 3), so the parity tests cover both paths
+    const char* paths = getenv("RDFIND_COUNT_PATHS");
+    c->force_global_counts = paths && !strcmp(paths, "atomic");
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -316,7 +337,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     tbegin(c, RDF_T_UNARY);
     const u64 K = 3ull * V;
     const u64 NB = (K + UC_R - 1) / UC_R;
-    if (n && NB <= UC_MAXB) {
+    if (n && NB <= UC_MAXB && !c->force_global_counts) {
         // partitioned counting: bucket histogram, scatter of (key, count) pairs, per-bucket LDS counting
         const unsigned G = std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024);
         const u64 nh = NB * G;
@@ -344,13 +365,14 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
                        3ull * V, c->ms, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->frank.as<u32>(), 3ull * V, (u32*)dscal(c, 6), st));
     tend(c, RDF_T_UNARY);
-    if (n)
+    if (n)  // binary keys emitted (sizes the K2 table)
         hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p,
                            c->o, n, V, c->ms, c->cnt.as<u32>(), dscal(c, 3));
     hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->cnt.as<u32>(), V, c->ms, dscal(c, 0));
     rdf_status rs = read_scalars(c, 7);
     if (rs) return rs;
+    const u64 E_emit = c->hscal[3];
     u64 nfreq[3] = {c->hscal[0], c->hscal[1], c->hscal[2]};
     c->U = (u32)c->hscal[6];
     c->Us = (u32)nfreq[0];
@@ -358,38 +380,42 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
     hipLaunchKernelGGL(k_frank_final, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(), V, c->ms,
                        c->frank.as<u32>(), c->fval.as<u32>());
-    const u64 E = c->hscal[3];
-    const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
-    ENSURE(c, tkeys, tcap * 8);
-    ENSURE(c, tcnt, tcap * 4);
-    HIP_TRY(c, hipMemsetAsync(c->tkeys.p, 0xff, tcap * 8, st));
-    HIP_TRY(c, hipMemsetAsync(c->tcnt.p, 0, tcap * 4, st));
+    // K2: wave-merged binary keys -> LDS hash per block -> one global open-addressing table
     tbegin(c, RDF_T_BINARY);
-    if (E)
-        hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
-                           st, c->s, c->p, c->o, n, V, c->ms, c->cnt.as<u32>(), c->tkeys.as<u64>(), c->tcnt.as<u32>(),
-                           tcap - 1);
-    ENSURE(c, flags, tcap * 4);
-    ENSURE(c, pos, tcap * 8);
-    hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                       c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>(), dscal(c, 4));
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
-    tend(c, RDF_T_BINARY);
-    rs = read_scalars(c, 6);
-    if (rs) return rs;
-    const u64 nkeys = c->hscal[4];
-    const u64 B = c->hscal[5];
+    u64 nkeys = 0, B = 0;
+    {
+        const u64 E = E_emit;
+        const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
+        ENSURE(c, tkeys, tcap * 8);
+        ENSURE(c, tcnt, tcap * 4);
+        HIP_TRY(c, hipMemsetAsync(c->tkeys.p, 0xff, tcap * 8, st));
+        HIP_TRY(c, hipMemsetAsync(c->tcnt.p, 0, tcap * 4, st));
+        if (E)
+            hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
+                               st, c->s, c->p, c->o, n, V, c->ms, c->cnt.as<u32>(), c->tkeys.as<u64>(), c->tcnt.as<u32>(),
+                               tcap - 1);
+        ENSURE(c, flags, tcap * 4);
+        ENSURE(c, pos, tcap * 8);
+        hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>(), dscal(c, 4));
+        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
+        rs = read_scalars(c, 6);
+        if (rs) return rs;
+        nkeys = c->hscal[4];
+        B = c->hscal[5];
+        ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
+        hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->tkeys.as<u64>(), c->flags.as<u32>(), c->pos.as<u64>(), tcap, c->bkeys.as<u64>());
+    }
     c->B = B;
-    ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
     ENSURE(c, bkeys_tmp, std::max<u64>(B, 1) * 8);
-    hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                       c->tkeys.as<u64>(), c->flags.as<u32>(), c->pos.as<u64>(), tcap, c->bkeys.as<u64>());
     {
         u64* k = c->bkeys.as<u64>();
         u64* t = c->bkeys_tmp.as<u64>();
         HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, 64, st));
         if (k != c->bkeys.as<u64>()) std::swap(c->bkeys, c->bkeys_tmp);
     }
+    tend(c, RDF_T_BINARY);
     c->lcap = next_pow2(2 * B + 16);
     ENSURE(c, lkeys, c->lcap * 8);
     ENSURE(c, lvals, c->lcap * 4);
@@ -397,8 +423,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     if (B)
         hipLaunchKernelGGL(k_bin_lookup_build, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->bkeys.as<u64>(), B, c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1);
-    c->h_bkeys.resize(B);
-    if (B) HIP_TRY(c, hipMemcpyAsync(c->h_bkeys.data(), c->bkeys.p, B * 8, hipMemcpyDeviceToHost, st));
+    c->h_bkeys_valid = false;  // host copy made on first use (decode / copy-out)
     HIP_TRY(c, hipEventRecord(c->ev[1], st));
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
@@ -449,11 +474,6 @@ static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj
     return RDF_OK;
 }
 
-#define TRY(expr)                    \
-    do {                             \
-        rdf_status _r = (expr);      \
-        if (_r != RDF_OK) return _r; \
-    } while (0)
 
 // K3 emission of this rank's join shard, K4 sort by (join, capture), K5 local supports -> c->support[ncap]
 static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
@@ -1567,6 +1587,7 @@ rdf_status rdf_decode_capture(rdf_ctx* c, uint32_t capture, uint32_t* code, uint
         return RDF_OK;
     }
     const u64 b = capture - 6 * V;
+    TRY(load_bkeys(c));
     if (b >= c->h_bkeys.size()) return fail(c, RDF_ERR_ARG, "capture id out of range");
     const u64 k = c->h_bkeys[b];
     *code = BI[bin_key_type(k)];
@@ -1577,12 +1598,13 @@ rdf_status rdf_decode_capture(rdf_ctx* c, uint32_t capture, uint32_t* code, uint
 
 rdf_status rdf_binary_key_count(rdf_ctx* c, uint64_t* n) {
     if (!c || !n) return RDF_ERR_ARG;
-    *n = c->h_bkeys.size();
+    *n = c->B;
     return RDF_OK;
 }
 
 rdf_status rdf_copy_binary_keys(rdf_ctx* c, uint64_t* out, uint64_t cap) {
     if (!c || (cap && !out)) return RDF_ERR_ARG;
+    TRY(load_bkeys(c));
     const u64 m = std::min<u64>(cap, c->h_bkeys.size());
     if (m) memcpy(out, c->h_bkeys.data(), m * 8);
     return RDF_OK;

@@ -120,6 +120,33 @@ def test_synthetic_configs_vs_oracle(ctx, cfg, scale):
     assert _lib.decoded_to_set(ctx.decoded_cinds()) == exp
 
 
+def test_global_count_paths(ctx, monkeypatch):
+    """The global-atomic unary counting kernel (fallback of the partitioned K1) agrees with the oracle and
+    with the partitioned path (condition statistics and the order-independent result checksum)."""
+    monkeypatch.setenv("RDFIND_COUNT_PATHS", "atomic")
+    g = _lib.Context(0)
+    try:
+        rng = random.Random(23)
+        for _ in range(30):
+            n = rng.randrange(1, 250)
+            nv = rng.randrange(2, 40)
+            ms = rng.randrange(1, 5)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            for strategy, clean in ((1, True), (0, False)):
+                assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean)
+        for cfg, scale in (("c1", 0.2), ("c5", 0.01)):
+            d = synth.config(cfg, scale)
+            stats = []
+            for c in (g, ctx):
+                c.set_triples(d.s, d.p, d.o, d.num_terms)
+                c.run(d.min_support)
+                stats.append((dict(c.fc), c.checksum()))
+            assert stats[0] == stats[1], cfg
+    finally:
+        g.close()
+
+
 def _capture_joins(d, code, v1, v2):
     """Distinct join values of a capture, straight from the triples (the definition of its groups)."""
     cols = {1: d.s, 2: d.p, 4: d.o}
