@@ -30,6 +30,11 @@ static constexpr u32 LIGHT_PACK_NL = RDF_PACK_NL;        // which at most this m
 #define RDF_LIGHT_BATCH 8
 #endif
 static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched together in k_light
+#ifndef RDF_LIGHT_SERIAL
+#define RDF_LIGHT_SERIAL 4
+#endif
+static constexpr int LIGHT_SERIAL = RDF_LIGHT_SERIAL;  // windows with at most this many light groups: lanes over candidates
+static constexpr u32 LIGHT_LDS = 512;                   // groups up to this size are searched in LDS (2 KiB per wave)
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
 struct __align__(16) CapInfo {

@@ -1085,6 +1085,7 @@ __device__ unsigned long long g_light_stats[16];
 __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
                                                      const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
                                                      u64* dead, u64* slots, u32* counts) {
+    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_LDS];
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -1140,6 +1141,44 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
             LSTAT(3, __popcll(__ballot(gg[it] != NONE32)));
 #endif
             const u32 g = gg[it];
+            const u64 lm = __ballot(g != NONE32);  // light groups of this window
+            if (__popcll(lm) <= LIGHT_SERIAL) {
+                // few light groups (the common case: most groups of a dependent are heavy and verified by the
+                // mask test): take them one at a time with the lanes over the candidates.  A group of at most
+                // LIGHT_LDS captures is staged into the wave's LDS slice by one coalesced load, so each
+                // candidate's search is one global round trip plus LDS probes.
+                u32* buf = s_light[threadIdx.x / RDF_WAVE];
+                u64 tg = lm;
+                while (tg && alive) {
+                    const int l = __ffsll((long long)tg) - 1;
+                    tg &= tg - 1;
+                    const u64 gb = __shfl(gbv[it], l, RDF_WAVE);
+                    const u32 gs = __shfl(gszv[it], l, RDF_WAVE);
+                    const bool mine = (alive >> lane) & 1ull;
+                    bool found = true;
+                    if (gs <= LIGHT_LDS) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
+                        __builtin_amdgcn_wave_barrier();
+                        for (u32 k = lane; k < gs; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        if (mine) {
+                            u32 lo = 0, hi = gs;
+                            while (lo < hi) {
+                                const u32 mid = (lo + hi) >> 1;
+                                if (buf[mid] < cand) lo = mid + 1;
+                                else hi = mid;
+                            }
+                            found = lo < gs && buf[lo] == cand;
+                        }
+                    } else if (mine) {
+                        found = bsearch_u32(v.gcap + gb, gs, cand);
+                    }
+                    alive &= __ballot(found);
+                }
+                continue;
+            }
             const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
             const u64 gsz = gszv[it];
             // up to LIGHT_BATCH alive candidates are searched at once: their loads at one level of the

@@ -21,6 +21,15 @@ for step in "$@"; do
         || { echo "prof failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
       find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG.kernel_stats.csv \;
       head -25 gpurun_out/prof_$TAG.kernel_stats.csv ;;
+    configs)  # the other BASELINE shapes on one GPU (c3 at half size: its generator runs ~2 min on the host)
+      for cfg in "c1 1.0" "c3 0.5" "c5 0.1" "c5 0.3"; do
+        set -- $cfg
+        echo "config $1 scale $2" >&2
+        timeout -k 10 400 python -u bench.py --config $1 --scale $2 --steps 3 --warmup 1 --no-cpu-baseline \
+          > gpurun_out/cfg_${TAG}_$1.json 2> gpurun_out/cfg_${TAG}_$1.err \
+          || { echo "config $1 failed"; tail -20 gpurun_out/cfg_${TAG}_$1.err; exit 1; }
+        cat gpurun_out/cfg_${TAG}_$1.json
+      done ;;
     qprof)
       timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/qprof_$TAG -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/qprof_$TAG.log 2>&1 \
