@@ -963,35 +963,28 @@ __device__ inline bool member(const CindView& v, u32 x, u32 y) {
 //   R3 drop 1/1 A<R if A<X in V12, R in comp(X)
 //   R4 drop 2/2 D<X if comp(D)<X in V12
 // RULES_S2L_RAW applies only R1 and R4: the exact-candidate S2L output without --clean-implied.
-// exists a binary X with a < X (raw) and r a component of X?  Iterates the shorter of parents(r) and,
-// for a dependent with explicit refs, its binary refs (a suffix of its sorted explicit list).
-__device__ inline bool implied_via_binary_ref(const CindView& v, u32 a, u32 r) {
-    if (!(v.info[r].meta & META_PARENTS)) return false;
-    const u64 pb = v.poff[r], pe = v.poff[r + 1];
-    if (!(v.info[a].meta & META_HEAVY_ONLY)) {
-        const u64 xb = v.ebin[a], xe = v.eoff[a + 1];
-        if (xe - xb <= pe - pb) {
-            for (u64 j = xb; j < xe; ++j) {
-                const u32* bc = v.bcomp + 2ull * ((u32)v.epairs[j] - v.Cu);
-                if (bc[0] == r || bc[1] == r) return true;
-            }
-            return false;
-        }
-    }
-    for (u64 j = pb; j < pe; ++j)
-        if (member(v, a, v.plist[j])) return true;
-    return false;
+// rule_keep tests R1/R4 per pair.  R2/R3 are applied by "mark" passes instead (k_rules_mark,
+// k_heavy_mark, k_class_mark): if a < X (raw) then joins(a) <= joins(X) <= joins(comp(X)), so every
+// component of a raw binary ref X of a is itself a raw ref of a (or trivial).  The unary refs R2/R3 drop
+// are therefore exactly the components of a's raw binary refs: each binary ref clears its (<= 2)
+// components in a's own sorted ref list -- O(binary refs x log) instead of a scan of parents(R) per pair.
+__device__ inline bool rule_keep(const CindView& v, u32 a, u32 r) {
+    if (v.mode == RULES_NONE || a < v.Cu) return true;
+    const u32* bc = v.bcomp + 2ull * (a - v.Cu);
+    return !(member(v, bc[0], r) || member(v, bc[1], r));                               // R1 / R4
 }
 
-__device__ inline bool rule_keep(const CindView& v, u32 a, u32 r) {
-    if (v.mode == RULES_NONE) return true;
-    const bool ab = a >= v.Cu, rb = r >= v.Cu;
-    if (!ab && rb) return true;
-    if (!ab && !rb) return v.mode != RULES_CLEAN || !implied_via_binary_ref(v, a, r);  // R3
-    const u32* bc = v.bcomp + 2ull * (a - v.Cu);
-    if (member(v, bc[0], r) || member(v, bc[1], r)) return false;                     // R1 / R4
-    if (rb || v.mode != RULES_CLEAN) return true;
-    return !implied_via_binary_ref(v, a, r);                                            // R2
+// position of capture x in the (ascending) member list of group g, or NONE
+__device__ inline u64 group_pos(const CindView& v, u32 g, u32 x) {
+    const u64 b = v.goff[g], n = v.goff[g + 1] - b;
+    const u32* a = v.gcap + b;
+    u64 lo = 0, hi = n;
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < n && a[lo] == x) ? lo : ~0ull;
 }
 
 
@@ -1263,7 +1256,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restric
     }
 }
 
-// minimality on explicit pairs -> output
+// minimality on explicit pairs -> output (R1/R4; R2/R3 by k_rules_mark afterwards)
 __global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const u64* __restrict__ pairs, u64 E, u32 rank,
                                                               u32 nranks, u32* keep) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < E; i += (u64)gridDim.x * RDF_BLOCK) {
@@ -1273,43 +1266,87 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const 
     }
 }
 
-// heavy-only dependents: refs = pivot members passing the mask test; minimality fused.
-// WRITE=false: count per work item; WRITE=true: write at the scanned offsets.  Each wave walks HEAVY_TILE
-// consecutive work items (chunks of 64 candidates), so the dependent lookup is amortised.
-static constexpr u32 HEAVY_TILE = 1;  // 8 measured 60% slower (fewer independent waves in flight)
-
-template <bool WRITE>
-__global__ __launch_bounds__(RDF_BLOCK) void k_heavy(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ choff,
-                                                     u64 W, u32* counts, const u64* __restrict__ woff, u64 out_base,
-                                                     u32* out) {
-    const u64 w0 = ((u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE) * HEAVY_TILE;
-    if (w0 >= W) return;
-    const int lane = lane_id();
-    u32 d = find_dep(choff, v.C, w0);
-    u64 dend = choff[d + 1];
-    CapInfo id = v.info[d];
-    u32 piv = pivot[d];
-    for (u32 t = 0; t < HEAVY_TILE; ++t) {
-        const u64 w = w0 + t;
-        if (w >= W) break;
-        if (w >= dend) {  // next dependent with chunks
-            do {
-                ++d;
-                dend = choff[d + 1];
-            } while (w >= dend);
-            id = v.info[d];
-            piv = pivot[d];
-        }
-        const u64 chunk = w - choff[d];
-        const u32 cand = chunk_candidate(v, d, id, piv, chunk);
-        const bool keep = cand != NONE32 && rule_keep(v, d, cand);
-        const u64 kept = __ballot(keep);
-        if (!WRITE) {
-            if (lane == 0) counts[w] = (u32)__popcll(kept);
-        } else if (keep) {
-            out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = cand;  // run of d (k_output_runs)
+// R2/R3 (--clean-implied) on explicit dependents: every binary raw pair (a, X) clears the components of X
+// in a's unary refs [eoff[a], ebin[a]).  Plain stores of 0 (idempotent; k_rules_explicit has finished).
+__global__ __launch_bounds__(RDF_BLOCK) void k_rules_mark(CindView v, const u64* __restrict__ pairs, u64 E, u32 rank,
+                                                          u32 nranks, u32* keep) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < E; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 pr = pairs[i];
+        const u32 a = (u32)(pr >> 32), x = (u32)pr;
+        if (x < v.Cu || a % nranks != rank) continue;
+        const u64 b = v.eoff[a], n = v.ebin[a] - b;
+        const u32* bc = v.bcomp + 2ull * (x - v.Cu);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const u64 key = ((u64)a << 32) | bc[k];
+            const u64 j = lower_bound_u64(pairs + b, n, key);
+            if (j < n && pairs[b + j] == key) keep[b + j] = 0u;
         }
     }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_popc_counts(const u64* __restrict__ bits, u64 W, u32* counts) {
+    for (u64 w = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; w < W; w += (u64)gridDim.x * RDF_BLOCK)
+        counts[w] = (u32)__popcll(bits[w]);
+}
+
+// heavy-only binary dependents: refs = pivot members passing the mask test.  One wave per work item (chunk of
+// 64 pivot members); bits[w] holds the surviving lanes: k_heavy_eval (candidate filter + R1/R4), then
+// k_heavy_mark (R2: the components of every raw binary ref are cleared, they sit in the same pivot group),
+// then k_heavy_write streams the survivors at the scanned offsets (popcounts of bits).
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_eval(CindView v, const u32* __restrict__ pivot,
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 d = owner[w];
+    const CapInfo id = v.info[d];
+    const u32 cand = chunk_candidate(v, d, id, pivot[d], w - choff[d]);
+    const bool keep = cand != NONE32 && rule_keep(v, d, cand);
+    const u64 kept = __ballot(keep);
+    if (lane_id() == 0) bits[w] = kept;
+}
+
+// clear bit p of a per-chunk survivor bitmap (all lanes call it).  Many binary refs share a component
+// (s[p=P,o=*] -> s[p=P]), so equal targets of a wave merge first and a target already cleared by another
+// wave is skipped by a plain load: only the first clear of a bit goes to the memory-side atomic.
+__device__ inline void mark_clear(u64* bits, u64 p, bool active) {
+    if (!wave_merge<u64, 4>(active ? p : ~0ull, active)) return;
+    u64* word = bits + p / RDF_WAVE;
+    const u64 m = 1ull << (p % RDF_WAVE);
+    if (!(*word & m)) return;
+    atomicAnd((unsigned long long*)word, ~m);
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(CindView v, const u32* __restrict__ pivot,
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 d = owner[w];
+    const CapInfo id = v.info[d];
+    const u32 piv = pivot[d];
+    const u32 x = chunk_candidate(v, d, id, piv, w - choff[d]);
+    const bool bin = x != NONE32 && x >= v.Cu;
+    if (!__ballot(bin)) return;
+    const u64 base = choff[d] * RDF_WAVE;  // bit index of pivot position 0
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const u64 p = bin ? group_pos(v, piv, v.bcomp[2ull * (x - v.Cu) + k]) : ~0ull;
+        mark_clear(bits, base + p, p != ~0ull);
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(CindView v, const u32* __restrict__ pivot,
+                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, const u64* __restrict__ bits,
+                                                           const u64* __restrict__ woff, u64 out_base, u32* out) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u64 kept = bits[w];
+    if (!kept) return;
+    const int lane = lane_id();
+    if (!((kept >> lane) & 1ull)) return;
+    const u32 d = owner[w];
+    const u64 idx = v.goff[pivot[d]] + (w - choff[d]) * RDF_WAVE + lane;
+    out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = v.gcap[idx];  // run of d (k_output_runs)
 }
 
 
@@ -1320,16 +1357,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy(CindView v, const u32* __re
 // from a unary A's 1/1 refs every R that is a component of a binary ref X of A -- for heavy-only A that is
 // "R has a parent binary whose mask covers m", again a class property.  So L'(m) is built once per class
 // and each dependent's output is L'(m) minus itself: a streaming copy bound by the HBM write rate.
-
-// member-free R3 test for a heavy-only unary dependent with mask m
-__device__ inline bool r3_dropped_for_mask(const CindView& v, u32 r, u64 m) {
-    if (r >= v.Cu || !(v.info[r].meta & META_PARENTS)) return false;
-    for (u64 j = v.poff[r]; j < v.poff[r + 1]; ++j) {
-        const u64 mx = v.info[v.plist[j]].hmask;
-        if ((mx & m) == m) return true;
-    }
-    return false;
-}
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u64* tkeys, u64 tmask, u64* nmembers) {
     u32 cnt = 0;
@@ -1395,34 +1422,56 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_info(CindView v, const u64*
     }
 }
 
-// L'(m): filter the class pivot group (count pass, then write pass at scanned offsets -> sorted lists)
-template <bool WRITE>
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_filter(CindView v, const u64* __restrict__ cchoff, u32 ncls,
-                                                            u64 W, const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
-                                                            u32* counts, const u64* __restrict__ woff, u32* lists,
-                                                            u64* cpairs) {
+// L'(m): the class pivot group filtered by the mask test (bits per chunk of 64 members), then, under
+// --clean-implied, R3 by k_class_mark: the components of the binary members of L(m) are cleared (a binary
+// X with hmask(X) >= m is a raw ref of every member; its components sit in the same pivot group).
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+                                                          const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
+                                                          u64* bits) {
     const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
-    const u32 m = find_dep(cchoff, ncls, w);
-    const u64 chunk = w - cchoff[m];
+    const u32 m = owner[w];
     const u32 g = cpiv[m];
     const u64 mask = cmask[m];
-    const u64 idx = v.goff[g] + chunk * RDF_WAVE + lane_id();
-    bool keep = false;
-    u32 r = 0;
-    if (idx < v.goff[g + 1]) {
-        r = v.gcap[idx];
-        keep = (v.info[r].hmask & mask) == mask;
-        if (keep && v.mode == RULES_CLEAN) keep = !r3_dropped_for_mask(v, r, mask);
-    }
+    const u64 idx = v.goff[g] + (w - cchoff[m]) * RDF_WAVE + lane_id();
+    const bool keep = idx < v.goff[g + 1] && (v.info[v.gcap[idx]].hmask & mask) == mask;
     const u64 kept = __ballot(keep);
-    if (!WRITE) {
-        if (lane_id() == 0) counts[w] = (u32)__popcll(kept);
-    } else if (keep) {
-        const u64 o = woff[w] + __popcll(kept & lanemask_lt());
-        if (cpairs) cpairs[o] = ((u64)m << 32) | r;  // sharded mode: (class, ref) pairs for the all-gather
-        else lists[o] = r;
+    if (lane_id() == 0) bits[w] = kept;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+                                                          const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
+                                                          u64* bits) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 m = owner[w];
+    const u32 g = cpiv[m];
+    const u64 mask = cmask[m];
+    const u64 idx = v.goff[g] + (w - cchoff[m]) * RDF_WAVE + lane_id();
+    const u32 x = idx < v.goff[g + 1] ? v.gcap[idx] : 0u;
+    const bool bin = x >= v.Cu && (v.info[x].hmask & mask) == mask;
+    if (!__ballot(bin)) return;
+    const u64 base = cchoff[m] * RDF_WAVE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const u64 p = bin ? group_pos(v, g, v.bcomp[2ull * (x - v.Cu) + k]) : ~0ull;
+        mark_clear(bits, base + p, p != ~0ull);
     }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_write(CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+                                                           const u32* __restrict__ cpiv, const u64* __restrict__ bits,
+                                                           const u64* __restrict__ woff, u32* lists, u64* cpairs) {
+    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u64 kept = bits[w];
+    const int lane = lane_id();
+    if (!((kept >> lane) & 1ull)) return;
+    const u32 m = owner[w];
+    const u32 r = v.gcap[v.goff[cpiv[m]] + (w - cchoff[m]) * RDF_WAVE + lane];
+    const u64 o = woff[w] + __popcll(kept & lanemask_lt());
+    if (cpairs) cpairs[o] = ((u64)m << 32) | r;  // sharded mode: (class, ref) pairs for the all-gather
+    else lists[o] = r;
 }
 
 // per member dependent: position of itself in L'(m) (or NONE) and its output count

@@ -54,7 +54,7 @@ struct rdf_ctx {
     u64 *rec_sorted = nullptr;
 
     // cinds
-    DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, out, stage_rows;
+    DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, hbits, cbits, hown, cown, out, stage_rows;
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
@@ -248,7 +248,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->gcap, &c->gmap, &c->csup,
                       &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
-                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->out,
+                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
@@ -923,11 +923,21 @@ static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
     hipStream_t st = c->stream;
     ENSURE(c, hcounts, std::max<u64>(WH, 1) * 4);
     ENSURE(c, hoff, (WH + 1) * 8);
+    ENSURE(c, hbits, std::max<u64>(WH, 1) * 8);
+    ENSURE(c, hown, std::max<u64>(WH, 1) * 4);
     tbegin(c, RDF_T_HCOUNT);
-    if (WH)
-        hipLaunchKernelGGL((k_heavy<false>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
-                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, c->hcounts.as<u32>(),
-                           (const u64*)nullptr, (u64)0, (u32*)nullptr);
+    if (WH) {
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->choffh.as<u64>(),
+                           c->C, c->hown.as<u32>());
+        const dim3 grid((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK));
+        hipLaunchKernelGGL(k_heavy_eval, grid, dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+                           c->hbits.as<u64>());
+        if (v.mode == RULES_CLEAN)
+            hipLaunchKernelGGL(k_heavy_mark, grid, dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+                               c->hbits.as<u64>());
+        hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WH, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->hbits.as<u64>(),
+                           WH, c->hcounts.as<u32>());
+    }
     tend(c, RDF_T_HCOUNT);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->hcounts.as<u32>(), c->hoff.as<u64>(), WH, c->hoff.as<u64>() + WH, st));
     TRY(read_u64(c, c->hoff.as<u64>() + WH, H));
@@ -1016,19 +1026,30 @@ static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* 
         u64 WC = 0;
         TRY(read_u64(c, c->cchoff.as<u64>() + ncls, &WC));
         ENSURE(c, ccnt, std::max<u64>(WC, 1) * 4);
+    ENSURE(c, cbits, std::max<u64>(WC, 1) * 8);
+    ENSURE(c, cown, std::max<u64>(WC, 1) * 4);
+    if (WC)
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(std::max<u32>(ncls, 1), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->cchoff.as<u64>(), ncls, c->cown.as<u32>());
         ENSURE(c, lwoff, (WC + 1) * 8);
-        if (WC)
-            hipLaunchKernelGGL((k_class_filter<false>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                               dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
-                               c->ccnt.as<u32>(), (const u64*)nullptr, (u32*)nullptr, (u64*)nullptr);
+        if (WC) {
+            const dim3 grid((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK));
+            hipLaunchKernelGGL(k_class_eval, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cmask.as<u64>(),
+                               c->cpiv.as<u32>(), c->cbits.as<u64>());
+            if (v.mode == RULES_CLEAN)
+                hipLaunchKernelGGL(k_class_mark, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
+                                   c->cmask.as<u64>(), c->cpiv.as<u32>(), c->cbits.as<u64>());
+            hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WC, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cbits.as<u64>(),
+                               WC, c->ccnt.as<u32>());
+        }
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ccnt.as<u32>(), c->lwoff.as<u64>(), WC, c->lwoff.as<u64>() + WC, st));
         u64 LT = 0;
         TRY(read_u64(c, c->lwoff.as<u64>() + WC, &LT));
         ENSURE(c, clists, std::max<u64>(LT, 1) * 4);
         if (WC)
-            hipLaunchKernelGGL((k_class_filter<true>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                               dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
-                               (u32*)nullptr, c->lwoff.as<u64>(), c->clists.as<u32>(), (u64*)nullptr);
+            hipLaunchKernelGGL(k_class_write, dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                               dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cpiv.as<u32>(), c->cbits.as<u64>(),
+                               c->lwoff.as<u64>(), c->clists.as<u32>(), (u64*)nullptr);
         TRY(d_class_tiles(c, nmem, ncls, HC, NT));
     }
     tend(c, RDF_T_CLASS);
@@ -1047,6 +1068,9 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     if (E)
         hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
                            c->epairs.as<u64>(), E, c->rank, c->nranks, c->flags.as<u32>());
+    if (E && v.mode == RULES_CLEAN)
+        hipLaunchKernelGGL(k_rules_mark, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->epairs.as<u64>(),
+                           E, c->rank, c->nranks, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), E, c->pos.as<u64>() + E, st));
     if (E)
         hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E,
@@ -1056,8 +1080,8 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     TRY(read_u64(c, c->pos.as<u64>() + E, &K));
     tbegin(c, RDF_T_HWRITE);
     if (WH)
-        hipLaunchKernelGGL((k_heavy<true>), dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK * HEAVY_TILE - 1) / (RDF_WAVES_PER_BLOCK * HEAVY_TILE))),
-                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), WH, (u32*)nullptr,
+        hipLaunchKernelGGL(k_heavy_write, dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH, c->hbits.as<u64>(),
                            c->hoff.as<u64>(), K, c->out.as<u32>());
     tend(c, RDF_T_HWRITE);
     tbegin(c, RDF_T_CEMIT);
@@ -1366,19 +1390,30 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     u64 WC = 0;
     TRY(read_u64(c, c->cchoff.as<u64>() + ncls, &WC));
     ENSURE(c, ccnt, std::max<u64>(WC, 1) * 4);
-    ENSURE(c, lwoff, (WC + 1) * 8);
+    ENSURE(c, cbits, std::max<u64>(WC, 1) * 8);
+    ENSURE(c, cown, std::max<u64>(WC, 1) * 4);
     if (WC)
-        hipLaunchKernelGGL((k_class_filter<false>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
-                           c->ccnt.as<u32>(), (const u64*)nullptr, (u32*)nullptr, (u64*)nullptr);
+        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(std::max<u32>(ncls, 1), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->cchoff.as<u64>(), ncls, c->cown.as<u32>());
+    ENSURE(c, lwoff, (WC + 1) * 8);
+    if (WC) {
+        const dim3 grid((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK));
+        hipLaunchKernelGGL(k_class_eval, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cmask.as<u64>(),
+                           c->cpiv.as<u32>(), c->cbits.as<u64>());
+        if (v.mode == RULES_CLEAN)
+            hipLaunchKernelGGL(k_class_mark, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
+                               c->cmask.as<u64>(), c->cpiv.as<u32>(), c->cbits.as<u64>());
+        hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WC, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cbits.as<u64>(),
+                           WC, c->ccnt.as<u32>());
+    }
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ccnt.as<u32>(), c->lwoff.as<u64>(), WC, c->lwoff.as<u64>() + WC, st));
     u64 LT = 0;
     TRY(read_u64(c, c->lwoff.as<u64>() + WC, &LT));
     ENSURE(c, xsend, std::max<u64>(LT, 1) * 8);
     if (WC)
-        hipLaunchKernelGGL((k_class_filter<true>), dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), ncls, WC, c->cmask.as<u64>(), c->cpiv.as<u32>(),
-                           (u32*)nullptr, c->lwoff.as<u64>(), (u32*)nullptr, c->xsend.as<u64>());
+        hipLaunchKernelGGL(k_class_write, dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
+                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cpiv.as<u32>(), c->cbits.as<u64>(),
+                           c->lwoff.as<u64>(), (u32*)nullptr, c->xsend.as<u64>());
     tend(c, RDF_T_CLASS);
     HIP_TRY(c, hipStreamSynchronize(st));
     return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, LT, 8);

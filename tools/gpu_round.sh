@@ -30,6 +30,14 @@ for step in "$@"; do
           || { echo "config $1 failed"; tail -20 gpurun_out/cfg_${TAG}_$1.err; exit 1; }
         cat gpurun_out/cfg_${TAG}_$1.json
       done ;;
+    cprof:*)  # cprof:<config>:<scale> -- kernel stats of one step of another BASELINE shape
+      IFS=: read -r _ CFG SC <<< "$step"
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/cprof_${TAG}_$CFG -o run --output-format csv \
+        -- python3 bench.py --config $CFG --scale $SC --steps 2 --warmup 1 --no-cpu-baseline \
+        > gpurun_out/cprof_${TAG}_$CFG.log 2>&1 \
+        || { echo "cprof $CFG failed"; tail -30 gpurun_out/cprof_${TAG}_$CFG.log; exit 1; }
+      find gpurun_out/cprof_${TAG}_$CFG -name "*kernel_stats.csv" -exec cp {} gpurun_out/cprof_${TAG}_$CFG.kernel_stats.csv \;
+      cut -c1-60,200- gpurun_out/cprof_${TAG}_$CFG.kernel_stats.csv | head -30 ;;
     qprof)
       timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/qprof_$TAG -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/qprof_$TAG.log 2>&1 \
