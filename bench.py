@@ -190,7 +190,8 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],
-                     "explicit_raw": cs["n_explicit_raw"], "class_members": cs["n_class_members"],
+                     "explicit_raw": cs["n_explicit_raw"], "heavy_chunks": cs["n_heavy_chunks"],
+                     "heavy_candidates": cs["n_heavy_candidates"], "class_members": cs["n_class_members"],
                      "classes": cs["n_classes"], "class_cinds": cs["n_class_cinds"]},
         }
         print(json.dumps(line), flush=True)

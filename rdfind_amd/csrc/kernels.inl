@@ -803,9 +803,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
     }
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
+__device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
                                                          u64* best_out, u32* nlight_out) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
     const u32 d = find_dep(segoff, v.C, w);
@@ -839,6 +839,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(CindView v, u32* dgrp_t
         }
     }
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(u64 nvblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
+                                                         u64* best_out, u32* nlight_out) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out);
+    }
+}
+
 
 // Light work plan of dependent d (nlight light groups, pivot of sz captures).  Output slots are octets (8
 // candidates of the pivot); noct[d] of them.  A dependent with few groups is "packed": one lane per
@@ -1019,22 +1026,29 @@ __device__ inline void slot_emit(u64 oct0, u32 nvalid, u32 d, u32 cand, u64 aliv
     if ((om >> j) & 1u) slots[(oct0 + o) * 8 + __popc(om & ((1u << j) - 1u))] = ((u64)d << 32) | cand;
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(const u64* __restrict__ slots, const u32* __restrict__ counts,
+__device__ inline void k_slot_compact_body(u64 vblk, const u64* __restrict__ slots, const u32* __restrict__ counts,
                                                             const u64* __restrict__ pos, u64 W, u64* out) {
-    const u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x;
+    const u64 g = (u64)vblk * RDF_BLOCK + threadIdx.x;
     const u64 o = g >> 3;
     if (o >= W) return;
     const u32 j = (u32)(g & 7);
     if (j < counts[o]) out[pos[o] + j] = slots[g];
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(u64 nvblk, const u64* __restrict__ slots, const u32* __restrict__ counts,
+                                                            const u64* __restrict__ pos, u64 W, u64* out) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_slot_compact_body(vb, slots, counts, pos, W, out);
+    }
+}
+
 
 // packed light dependents (few groups): one lane per pivot candidate, 8-lane octets, candidates of many
 // dependents per wave.  Each lane walks its dependent's groups and binary-searches its candidate in every
 // light one (the same test as k_light's few-groups path, without a mostly idle wave per dependent).
-__global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(CindView v, const u32* __restrict__ pivot,
+__device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                                             const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep,
                                                             u64 WP, const u64* __restrict__ choff, u64* slots, u32* counts) {
-    const u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x;
+    const u64 g = (u64)vblk * RDF_BLOCK + threadIdx.x;
     const u64 q = g >> 3;
     if (q >= WP) return;  // whole octets only, so the octet ballots below see complete octets
     const u32 d = pk_dep[q];
@@ -1056,6 +1070,14 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(CindView v, const u3
     if (jj == 0) counts[oct] = (u32)__popc(om);
     if (ok) slots[oct * 8 + __popc(om & ((1u << jj) - 1u))] = ((u64)d << 32) | cand;
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                            const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep,
+                                                            u64 WP, const u64* __restrict__ choff, u64* slots, u32* counts) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_light_packed_body(vb, v, pivot, pkoff, pk_dep, WP, choff, slots, counts);
+    }
+}
+
 
 #ifdef RDF_LIGHT_STATS
 // dev instrumentation (make STATS=1): [0] items [1] wave iterations [2] candidate checks [3] groups visited
@@ -1075,11 +1097,11 @@ __device__ unsigned long long g_light_stats[16];
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
-__global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
+__device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
                                                      const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
                                                      u64* dead, u64* slots, u32* counts) {
     __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_LDS];
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
     const u32 d = item_dep[w];
@@ -1219,14 +1241,22 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(CindView v, const u32* __re
     // counter: an agent-scope release fence writes back the whole L2 of the XCD, per work item.
     if (lane == 0 && (alive0 & ~alive)) atomicOr(&dead[oct0], alive0 & ~alive);
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
+                                                     const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
+                                                     u64* dead, u64* slots, u32* counts) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_light_body(vb, v, pivot, itemoff, item_dep, choff, W, dead, slots, counts);
+    }
+}
+
 
 // chunks verified by several segments: survivors = candidates minus the union of the segments' kills
 // (launched after k_light; the kernel boundary orders the kills before these reads)
-__global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(CindView v, const u32* __restrict__ pivot,
+__device__ inline void k_light_mseg_emit_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                                                const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep,
                                                                u64 WM, const u64* __restrict__ choff,
                                                                const u64* __restrict__ dead, u64* slots, u32* counts) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= WM) return;
     const u32 d = mch_dep[w];
     const u64 chunk = w - mchoff[d];
@@ -1236,6 +1266,15 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(CindView v, const
     const u64 noct = choff[d + 1] - oct0;
     slot_emit(oct0, noct < 8 ? (u32)noct : 8u, d, cand, alive0 & ~dead[oct0], slots, counts);
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                               const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep,
+                                                               u64 WM, const u64* __restrict__ choff,
+                                                               const u64* __restrict__ dead, u64* slots, u32* counts) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_light_mseg_emit_body(vb, v, pivot, mchoff, mch_dep, WM, choff, dead, slots, counts);
+    }
+}
+
 
 // multi-segment chunks per dependent: nitem / nseg when the dependent's groups span several segments
 __global__ __launch_bounds__(RDF_BLOCK) void k_mseg_chunks(const u64* __restrict__ doff, const u32* __restrict__ nitem, u32 C,
@@ -1294,17 +1333,28 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_popc_counts(const u64* __restrict
 // 64 pivot members); bits[w] holds the surviving lanes: k_heavy_eval (candidate filter + R1/R4), then
 // k_heavy_mark (R2: the components of every raw binary ref are cleared, they sit in the same pivot group),
 // then k_heavy_write streams the survivors at the scanned offsets (popcounts of bits).
-__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_eval(CindView v, const u32* __restrict__ pivot,
-                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+__device__ inline void k_heavy_eval_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
+                                                          u64* bits) {
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 d = owner[w];
     const CapInfo id = v.info[d];
-    const u32 cand = chunk_candidate(v, d, id, pivot[d], w - choff[d]);
+    const u32 piv = pivot[d];
+    const u64 chunk = w - choff[d];
+    const u32 cand = chunk_candidate(v, d, id, piv, chunk);
     const bool keep = cand != NONE32 && rule_keep(v, d, cand);
     const u64 kept = __ballot(keep);
     if (lane_id() == 0) bits[w] = kept;
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_eval(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
+                                                          u64* bits) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_heavy_eval_body(vb, v, pivot, choff, owner, W, bits);
+    }
+}
+
 
 // clear bit p of a per-chunk survivor bitmap (all lanes call it).  Many binary refs share a component
 // (s[p=P,o=*] -> s[p=P]), so equal targets of a wave merge first and a target already cleared by another
@@ -1317,9 +1367,9 @@ __device__ inline void mark_clear(u64* bits, u64 p, bool active) {
     atomicAnd((unsigned long long*)word, ~m);
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(CindView v, const u32* __restrict__ pivot,
+__device__ inline void k_heavy_mark_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 d = owner[w];
     const CapInfo id = v.info[d];
@@ -1330,24 +1380,47 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(CindView v, const u32*
     const u64 base = choff[d] * RDF_WAVE;  // bit index of pivot position 0
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const u64 p = bin ? group_pos(v, piv, v.bcomp[2ull * (x - v.Cu) + k]) : ~0ull;
+        const u32 t = bin ? v.bcomp[2ull * (x - v.Cu) + k] : NONE32;
+        const u32 tprev = __shfl_up(t, 1, RDF_WAVE);
+        const bool head = bin && (lane_id() == 0 || tprev != t);  // consecutive refs share component 0
+        const u64 p = head ? group_pos(v, piv, t) : ~0ull;
         mark_clear(bits, base + p, p != ~0ull);
     }
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_heavy_mark_body(vb, v, pivot, choff, owner, W, bits);
+    }
+}
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(CindView v, const u32* __restrict__ pivot,
-                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, const u64* __restrict__ bits,
-                                                           const u64* __restrict__ woff, u64 out_base, u32* out) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+
+// survivors of a heavy work item -> output run of its dependent; src[sbase[d] + i] is candidate i of d
+// (classed binary dependents: their class list; otherwise sbase = null and the pivot group is the source)
+__device__ inline void k_heavy_write_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
+                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
+                                                           const u64* __restrict__ bits, const u32* __restrict__ src,
+                                                           const u64* __restrict__ sbase, const u64* __restrict__ woff,
+                                                           u64 out_base, u32* out) {
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u64 kept = bits[w];
-    if (!kept) return;
     const int lane = lane_id();
     if (!((kept >> lane) & 1ull)) return;
     const u32 d = owner[w];
-    const u64 idx = v.goff[pivot[d]] + (w - choff[d]) * RDF_WAVE + lane;
-    out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = v.gcap[idx];  // run of d (k_output_runs)
+    const u64 base = sbase ? sbase[d] : v.goff[pivot[d]];
+    out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = src[base + (w - choff[d]) * RDF_WAVE + lane];
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
+                                                           const u64* __restrict__ bits, const u32* __restrict__ src,
+                                                           const u64* __restrict__ sbase, const u64* __restrict__ woff,
+                                                           u64 out_base, u32* out) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_heavy_write_body(vb, v, pivot, choff, owner, W, bits, src, sbase, woff, out_base, out);
+    }
+}
+
 
 
 // ================================================================================================
@@ -1358,13 +1431,14 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(CindView v, const u32
 // "R has a parent binary whose mask covers m", again a class property.  So L'(m) is built once per class
 // and each dependent's output is L'(m) minus itself: a streaming copy bound by the HBM write rate.
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u64* tkeys, u64 tmask, u64* nmembers) {
+// masks of the heavy-only dependents [0, cmax): cmax = Cu (unary only) or C (binary ones classed too)
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u32 cmax, u64* tkeys, u64 tmask, u64* nmembers) {
     u32 cnt = 0;
-    const u64 n_round = ((u64)v.Cu + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
+    const u64 n_round = ((u64)cmax + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
-        const bool member = d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY);
+        const bool member = d < cmax && (v.info[d].meta & META_HEAVY_ONLY);
         const u64 m = member ? v.info[d].hmask : 0ull;  // never 0 for a heavy-only dependent
-        cnt += member;
+        cnt += member && d < v.Cu;
         // few classes, many members: one lane per distinct mask of the wave inserts (one CAS per address)
         if (wave_merge<u64, 4>(m, member)) {
             u64 h = mix64(m) & tmask;
@@ -1405,15 +1479,78 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_keys(CindView v, const u64*
     }
 }
 
+// binary heavy-only dependents join the mask classes (single GPU, S2L semantics): class id per dependent and
+// the smallest member of every class (its representative: members of a class share the pivot group)
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_of(CindView v, const u64* __restrict__ tkeys, const u32* __restrict__ cid,
+                                                        u64 tmask, u32* dcls, u32* crep) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
+        u32 m = NONE32;
+        if (v.info[d].meta & META_HEAVY_ONLY) {
+            const u64 mk = v.info[d].hmask;
+            u64 h = mix64(mk) & tmask;
+            while (tkeys[h] != mk) h = (h + 1) & tmask;
+            m = cid[h];
+            atomicMin(&crep[m], (u32)d);
+        }
+        if (d >= v.Cu) dcls[d - v.Cu] = m;
+    }
+}
+
+// work items of a classed binary dependent: chunks of 64 of its class list L'(m); sbase = list start
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_bin_chunks(CindView v, const u32* __restrict__ dcls,
+                                                                const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
+                                                                u32* nchunk, u64* sbase) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
+        u32 n = 0;
+        if (d >= v.Cu && dcls[d - v.Cu] != NONE32) {
+            const u32 m = dcls[d - v.Cu];
+            const u64 b = lwoff[cchoff[m]], e = lwoff[cchoff[m + 1]];
+            sbase[d] = b;
+            n = (u32)((e - b + RDF_WAVE - 1) / RDF_WAVE);
+        }
+        nchunk[d] = n;
+    }
+}
+
+// classed binary dependent D: refs = L'(m) minus D, its components (trivial) and R1/R4 (comp(D) < R).
+// R2 is already in L'(m): D's binary raw refs are the binary members of L(m), the class marks cleared their
+// components.  Survivor bits per chunk, as k_heavy_eval.
+__device__ inline void k_class_bin_eval_body(u64 vblk, CindView v, const u64* __restrict__ choff,
+                                                              const u32* __restrict__ owner, u64 W, const u64* __restrict__ sbase,
+                                                              const u32* __restrict__ dcls, const u64* __restrict__ cchoff,
+                                                              const u64* __restrict__ lwoff, const u32* __restrict__ lists,
+                                                              u64* bits) {
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= W) return;
+    const u32 d = owner[w];
+    const u32 m = dcls[d - v.Cu];
+    const u64 i = sbase[d] + (w - choff[d]) * RDF_WAVE + lane_id();
+    bool keep = i < lwoff[cchoff[m + 1]];
+    const u32 r = keep ? lists[i] : 0u;
+    keep = keep && r != d && !is_trivial(v, d, r) && rule_keep(v, d, r);
+    const u64 kept = __ballot(keep);
+    if (lane_id() == 0) bits[w] = kept;
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_bin_eval(u64 nvblk, CindView v, const u64* __restrict__ choff,
+                                                              const u32* __restrict__ owner, u64 W, const u64* __restrict__ sbase,
+                                                              const u32* __restrict__ dcls, const u64* __restrict__ cchoff,
+                                                              const u64* __restrict__ lwoff, const u32* __restrict__ lists,
+                                                              u64* bits) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_class_bin_eval_body(vb, v, choff, owner, W, sbase, dcls, cchoff, lwoff, lists, bits);
+    }
+}
+
+
 // per class: member offsets, mask, pivot, pivot-chunk count
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_info(CindView v, const u64* __restrict__ keys, u64 nkeys, u32 ncls,
-                                                          const u32* __restrict__ pivot, u64* coff, u64* cmask, u32* cpiv,
-                                                          u32* cnch) {
+                                                          const u32* __restrict__ pivot, const u32* __restrict__ crep,
+                                                          u64* coff, u64* cmask, u32* cpiv, u32* cnch) {
     for (u64 m = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; m <= ncls; m += (u64)gridDim.x * RDF_BLOCK) {
         u64 lo = lower_bound_u64(keys, nkeys, m << 32);
         coff[m] = lo;
         if (m < ncls) {
-            const u32 rep = (u32)keys[lo];
+            const u32 rep = crep ? crep[m] : (u32)keys[lo];
             const u32 g = pivot[rep];
             cmask[m] = v.info[rep].hmask;
             cpiv[m] = g;
@@ -1425,10 +1562,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_info(CindView v, const u64*
 // L'(m): the class pivot group filtered by the mask test (bits per chunk of 64 members), then, under
 // --clean-implied, R3 by k_class_mark: the components of the binary members of L(m) are cleared (a binary
 // X with hmask(X) >= m is a raw ref of every member; its components sit in the same pivot group).
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+__device__ inline void k_class_eval_body(u64 vblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
                                                           const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
                                                           u64* bits) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 m = owner[w];
     const u32 g = cpiv[m];
@@ -1438,11 +1575,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(CindView v, const u64*
     const u64 kept = __ballot(keep);
     if (lane_id() == 0) bits[w] = kept;
 }
-
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(u64 nvblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
                                                           const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
                                                           u64* bits) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_class_eval_body(vb, v, cchoff, owner, W, cmask, cpiv, bits);
+    }
+}
+
+
+__device__ inline void k_class_mark_body(u64 vblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+                                                          const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
+                                                          u64* bits) {
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 m = owner[w];
     const u32 g = cpiv[m];
@@ -1454,15 +1599,26 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(CindView v, const u64*
     const u64 base = cchoff[m] * RDF_WAVE;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const u64 p = bin ? group_pos(v, g, v.bcomp[2ull * (x - v.Cu) + k]) : ~0ull;
+        const u32 t = bin ? v.bcomp[2ull * (x - v.Cu) + k] : NONE32;
+        const u32 tprev = __shfl_up(t, 1, RDF_WAVE);
+        const bool head = bin && (lane_id() == 0 || tprev != t);  // consecutive refs share component 0
+        const u64 p = head ? group_pos(v, g, t) : ~0ull;
         mark_clear(bits, base + p, p != ~0ull);
     }
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(u64 nvblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+                                                          const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
+                                                          u64* bits) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_class_mark_body(vb, v, cchoff, owner, W, cmask, cpiv, bits);
+    }
+}
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_write(CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+
+__device__ inline void k_class_write_body(u64 vblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
                                                            const u32* __restrict__ cpiv, const u64* __restrict__ bits,
                                                            const u64* __restrict__ woff, u32* lists, u64* cpairs) {
-    const u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u64 kept = bits[w];
     const int lane = lane_id();
@@ -1473,6 +1629,14 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_write(CindView v, const u64
     if (cpairs) cpairs[o] = ((u64)m << 32) | r;  // sharded mode: (class, ref) pairs for the all-gather
     else lists[o] = r;
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_write(u64 nvblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+                                                           const u32* __restrict__ cpiv, const u64* __restrict__ bits,
+                                                           const u64* __restrict__ woff, u32* lists, u64* cpairs) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_class_write_body(vb, v, cchoff, owner, W, cpiv, bits, woff, lists, cpairs);
+    }
+}
+
 
 // per member dependent: position of itself in L'(m) (or NONE) and its output count
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_members(const u64* __restrict__ keys, u64 nkeys,
@@ -1519,7 +1683,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict
 // OUTPUT (not of the list), so that no line is shared by two blocks, and (2) lanes own 16-B quads counted
 // from the 256-B boundary below the segment start, so every wave-wide store covers whole lines.  Segment s
 // of a run needs list entries [s*CLS_LS - 31, (s+1)*CLS_LS + 1), hence the staged halo.
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict__ coff, const u64* __restrict__ cchoff,
+__device__ inline void k_class_emit_body(u64 vblk, const u64* __restrict__ coff, const u64* __restrict__ cchoff,
                                                           const u64* __restrict__ lwoff, const u32* __restrict__ lists,
                                                           const u64* __restrict__ toff, u32 ncls,
                                                           const u32* __restrict__ selfpos, const u64* __restrict__ obase,
@@ -1528,12 +1692,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict_
     __shared__ u32 s_sp[CLS_DT];
     __shared__ u64 s_base[CLS_DT];
     __shared__ u32 s_m;
-    if (threadIdx.x == 0) s_m = find_dep(toff, ncls, blockIdx.x);
+    if (threadIdx.x == 0) s_m = find_dep(toff, ncls, vblk);
     __syncthreads();
     const u32 m = s_m;
     const u64 lb = lwoff[cchoff[m]], len = lwoff[cchoff[m + 1]] - lb;
     const u64 nseg = (len + CLS_LS - 1) / CLS_LS;
-    const u64 t = blockIdx.x - toff[m];
+    const u64 t = vblk - toff[m];
     const u64 dt = t / nseg, seg = t % nseg;
     const u64 k0 = coff[m] + dt * CLS_DT, k1 = k0 + CLS_DT < coff[m + 1] ? k0 + CLS_DT : coff[m + 1];
     const u64 p0 = seg * CLS_LS;
@@ -1586,6 +1750,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(const u64* __restrict_
         }
     }
 }
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(u64 nvblk, const u64* __restrict__ coff, const u64* __restrict__ cchoff,
+                                                          const u64* __restrict__ lwoff, const u32* __restrict__ lists,
+                                                          const u64* __restrict__ toff, u32 ncls,
+                                                          const u32* __restrict__ selfpos, const u64* __restrict__ obase,
+                                                          u64 out_base, u32* out) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_class_emit_body(vb, coff, cchoff, lwoff, lists, toff, ncls, selfpos, obase, out_base, out);
+        __syncthreads();  // shared staging is reused by the next virtual block
+    }
+}
+
 
 // output run table (dependent runs in output order): runs [0, C) are the explicit pairs of dependent d
 // (start pos[eoff[d]]), [C, C+WH) the heavy-only binary chunks, [C+WH, C+WH+nmem) the class members

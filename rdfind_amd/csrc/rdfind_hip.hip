@@ -43,6 +43,8 @@ struct rdf_ctx {
     std::vector<u64> h_bkeys;
     bool h_bkeys_valid = false;
     bool force_global_counts = false;
+    bool allow_hclass = true;
+    u64 heavy_min = 64;  // smaller groups are cheaper to verify by binary search than as bit columns
 
     // capture groups
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
@@ -54,12 +56,13 @@ struct rdf_ctx {
     u64 *rec_sorted = nullptr;
 
     // cinds
-    DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, hbits, cbits, hown, cown, out, stage_rows;
+    DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, hbits, cbits, hown, cown, sbase, dcls, crep, out, stage_rows;
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
         ctiles, ctoff;
     u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
+    bool hclassed = false;  // binary heavy-only dependents emitted from class lists (single GPU, S2L semantics)
     DevBuf pedges, pedges_tmp;
     u64 ncap = 0;
     u64 n_explicit_raw = 0, n_light_chunks = 0;
@@ -210,6 +213,11 @@ static rdf_status load_bkeys(rdf_ctx* c) {
 }
 
 static const unsigned kGrid = 2048;  // grid-stride kernels: 8 blocks of 256 threads per CU
+// work-item kernels loop over virtual blocks: a dispatch holds < 2^32 work-items in x, so grids are capped
+static const u64 kMaxBlocks = 1ull << 20;
+static inline unsigned vgrid(u64 blocks) { return (unsigned)std::min<u64>(std::max<u64>(blocks, 1), kMaxBlocks); }
+static inline u64 wave_blocks(u64 waves) { return (waves + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK; }
+static inline u64 thread_blocks(u64 threads) { return (threads + RDF_BLOCK - 1) / RDF_BLOCK; }
 
 extern "C" {
 
@@ -224,6 +232,12 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     // the partitioned K1 for |V| > 2^26 / 3), so the parity tests cover both paths
     const char* paths = getenv("RDFIND_COUNT_PATHS");
     c->force_global_counts = paths && !strcmp(paths, "atomic");
+    // test hook: RDFIND_HEAVY_MIN=<power of two> lowers the minimum heavy-group size (default 64), so small
+    // parity inputs exercise the bitmask / class / heavy-only paths
+    const char* hcl = getenv("RDFIND_HCLASS");
+    c->allow_hclass = !(hcl && !strcmp(hcl, "0"));
+    const char* hmin = getenv("RDFIND_HEAVY_MIN");
+    if (hmin && atoll(hmin) > 0) c->heavy_min = (u64)atoll(hmin);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -248,7 +262,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->gcap, &c->gmap, &c->csup,
                       &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
-                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->out,
+                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
@@ -641,15 +655,13 @@ static rdf_status g_size_hist(rdf_ctx* c, u32* h_hist) {
     return RDF_OK;
 }
 
-static const u64 kHeavyMin = 64;  // smaller groups are cheaper to verify by binary search than as bit columns
-
 // heavy threshold from the (global) histogram; 0 = no heavy groups
-static u64 heavy_threshold(const u32* hist) {
-    int tb = heavy_threshold_from_hist(hist, kHeavyMin);
-    return tb >= 0 ? std::max<u64>(bucket_min_size(tb), kHeavyMin) : 0;
+static u64 heavy_threshold(const rdf_ctx* c, const u32* hist) {
+    int tb = heavy_threshold_from_hist(hist, c->heavy_min);
+    return tb >= 0 ? std::max<u64>(bucket_min_size(tb), c->heavy_min) : 0;
 }
 
-// groups of a histogram at or above the threshold (exact: kHeavyMin starts a bucket)
+// groups of a histogram at or above the threshold (exact: a power-of-two heavy_min starts a bucket)
 static u64 heavy_count(const u32* hist, u64 thr) {
     if (!thr) return 0;
     u64 n = 0;
@@ -737,7 +749,7 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     TRY(g_compact_groups(c));
     u32 h_hist[256];
     TRY(g_size_hist(c, h_hist));
-    TRY(g_heavy_binary(c, heavy_threshold(h_hist), 0));
+    TRY(g_heavy_binary(c, heavy_threshold(c, h_hist), 0));
     return g_finish(c, stats);
 }
 
@@ -800,8 +812,8 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
     if (C) TRY(read_u64(c, c->psegoff.as<u64>() + C, &WS));
     tbegin(c, RDF_T_PIVOT);
     if (WS)
-        hipLaunchKernelGGL(k_pivot_seg, dim3((unsigned)((WS + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
-                           0, st, v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
+        hipLaunchKernelGGL(k_pivot_seg, dim3(vgrid(wave_blocks(WS))), dim3(RDF_BLOCK),
+                           0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
     tend(c, RDF_T_PIVOT);
     return RDF_OK;
 }
@@ -845,12 +857,12 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pkoff.as<u64>(),
                            c->C, c->pk_dep.as<u32>());
     if (WP)
-        hipLaunchKernelGGL(k_light_packed, dim3((unsigned)((WP * 8 + RDF_BLOCK - 1) / RDF_BLOCK)), dim3(RDF_BLOCK), 0, st, v,
+        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), v,
                            c->pivot.as<u32>(), c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
                            c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     if (WI)
-        hipLaunchKernelGGL(k_light, dim3((unsigned)((WI + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)), dim3(RDF_BLOCK),
-                           0, st, v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
+        hipLaunchKernelGGL(k_light, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
+                           0, st, (u64)wave_blocks(WI), v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
                            c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     // chunks of dependents whose groups span several segments: emitted once all their segments are done
     u64 WM = 0;
@@ -866,8 +878,8 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
         ENSURE(c, mch_dep, WM * 4);
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->mchoff.as<u64>(),
                            c->C, c->mch_dep.as<u32>());
-        hipLaunchKernelGGL(k_light_mseg_emit, dim3((unsigned)((WM + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->mchoff.as<u64>(), c->mch_dep.as<u32>(), WM,
+        hipLaunchKernelGGL(k_light_mseg_emit, dim3(vgrid(wave_blocks(WM))),
+                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, c->pivot.as<u32>(), c->mchoff.as<u64>(), c->mch_dep.as<u32>(), WM,
                            c->choffl.as<u64>(), c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     }
     ENSURE(c, pos, (WL + 1) * 8);
@@ -875,7 +887,7 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     TRY(read_u64(c, c->pos.as<u64>() + WL, E));
     ENSURE(c, epairs, std::max<u64>(*E, 1) * 8);
     if (WL)
-        hipLaunchKernelGGL(k_slot_compact, dim3((unsigned)((WL * 8 + RDF_BLOCK - 1) / RDF_BLOCK)), dim3(RDF_BLOCK), 0, st,
+        hipLaunchKernelGGL(k_slot_compact, dim3(vgrid(thread_blocks(WL * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WL * 8),
                            c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>());
     tend(c, RDF_T_LIGHT);
 #ifdef RDF_LIGHT_STATS
@@ -919,6 +931,7 @@ static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorte
 }
 
 // heavy-only binary dependents: count pass -> hoff, *H
+// (classed: the work items are chunks of class lists, sbase/dcls from d_class_bin; else chunks of pivot groups)
 static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
     hipStream_t st = c->stream;
     ENSURE(c, hcounts, std::max<u64>(WH, 1) * 4);
@@ -929,11 +942,17 @@ static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
     if (WH) {
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->choffh.as<u64>(),
                            c->C, c->hown.as<u32>());
-        const dim3 grid((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK));
-        hipLaunchKernelGGL(k_heavy_eval, grid, dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
-                           c->hbits.as<u64>());
-        if (v.mode == RULES_CLEAN)
-            hipLaunchKernelGGL(k_heavy_mark, grid, dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+        const u64 nvb = wave_blocks(WH);
+        const dim3 grid(vgrid(nvb));
+        if (c->hclassed)
+            hipLaunchKernelGGL(k_class_bin_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+                               c->sbase.as<u64>(), c->dcls.as<u32>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(),
+                               c->clists.as<u32>(), c->hbits.as<u64>());
+        else
+            hipLaunchKernelGGL(k_heavy_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(),
+                               c->hown.as<u32>(), WH, c->hbits.as<u64>());
+        if (v.mode == RULES_CLEAN && !c->hclassed)
+            hipLaunchKernelGGL(k_heavy_mark, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
                                c->hbits.as<u64>());
         hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WH, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->hbits.as<u64>(),
                            WH, c->hcounts.as<u32>());
@@ -945,19 +964,19 @@ static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
 }
 
 // mask-class hash table of the unary heavy-only dependents; *nmem members, *ncls classes, *tcapc table size
-static rdf_status d_class_table(rdf_ctx* c, const CindView& v, u64* nmem, u32* ncls, u64* tcapc_out) {
+// (cmax = C also classes the binary heavy-only dependents; *nmem counts the unary members only)
+static rdf_status d_class_table(rdf_ctx* c, const CindView& v, u32 cmax, u64* nmem, u32* ncls, u64* tcapc_out) {
     hipStream_t st = c->stream;
-    const u32 Cu = c->Cu;
-    const u64 tcapc = next_pow2(2ull * Cu + 16);
+    const u64 tcapc = next_pow2(2ull * cmax + 16);
     *tcapc_out = tcapc;
     ENSURE(c, ctab, tcapc * 8);
     ENSURE(c, cflag, tcapc * 4);
     ENSURE(c, ccid, (tcapc + 1) * 4);
     HIP_TRY(c, hipMemsetAsync(c->ctab.p, 0, tcapc * 8, st));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 2 * 8, st));
-    if (Cu)
-        hipLaunchKernelGGL(k_class_insert, dim3(grid_for(Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
-                           tcapc - 1, dscal(c, 3));
+    if (cmax)
+        hipLaunchKernelGGL(k_class_insert, dim3(grid_for(cmax, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, cmax,
+                           c->ctab.as<u64>(), tcapc - 1, dscal(c, 3));
     hipLaunchKernelGGL(k_nonzero_flags, dim3(grid_for(tcapc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ctab.as<u64>(),
                        tcapc, c->cflag.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->cflag.as<u32>(), c->ccid.as<u32>(), tcapc, c->ccid.as<u32>() + tcapc, st));
@@ -994,25 +1013,36 @@ static rdf_status d_class_tiles(rdf_ctx* c, u64 nmem, u32 ncls, u64* HC, u64* NT
     return RDF_OK;
 }
 
-// single-rank class path: table -> keys -> per-class pivot -> filtered lists -> tiles
+// single-rank class path: table -> keys -> per-class pivot -> filtered lists -> tiles.  With c->hclassed the
+// binary heavy-only dependents are classed too (their lists are filtered per dependent by d_class_bin).
 static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* NT) {
     hipStream_t st = c->stream;
     tbegin(c, RDF_T_CLASS);
     u64 nmem = 0, tcapc = 0;
     u32 ncls = 0;
-    TRY(d_class_table(c, v, &nmem, &ncls, &tcapc));
+    TRY(d_class_table(c, v, c->hclassed ? c->C : c->Cu, &nmem, &ncls, &tcapc));
     *HC = 0;
     *NT = 0;
-    if (nmem) {
-        ENSURE(c, ckeys, nmem * 8);
-        ENSURE(c, ckeys_tmp, nmem * 8);
-        hipLaunchKernelGGL(k_class_keys, dim3(grid_for(c->Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
-                           c->ccid.as<u32>(), tcapc - 1, 0u, 1u, c->ckeys.as<u64>(), dscal(c, 4));
-        {
+    if (ncls) {
+        ENSURE(c, ckeys, std::max<u64>(nmem, 1) * 8);
+        ENSURE(c, ckeys_tmp, std::max<u64>(nmem, 1) * 8);
+        if (nmem) {
+            hipLaunchKernelGGL(k_class_keys, dim3(grid_for(c->Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                               c->ctab.as<u64>(), c->ccid.as<u32>(), tcapc - 1, 0u, 1u, c->ckeys.as<u64>(), dscal(c, 4));
             u64* k = c->ckeys.as<u64>();
             u64* t = c->ckeys_tmp.as<u64>();
             HIP_TRY(c, radix_sort_u64(c->ws, k, t, nmem, 32 + bits_for(ncls ? ncls - 1 : 0), st));
             if (k != c->ckeys.as<u64>()) std::swap(c->ckeys, c->ckeys_tmp);
+        }
+        const u32* crep = nullptr;
+        if (c->hclassed) {
+            ENSURE(c, crep, (u64)ncls * 4);
+            ENSURE(c, dcls, std::max<u64>(c->C - c->Cu, 1) * 4);
+            HIP_TRY(c, hipMemsetAsync(c->crep.p, 0xff, (u64)ncls * 4, st));
+            if (c->C)
+                hipLaunchKernelGGL(k_class_of, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                                   c->ctab.as<u64>(), c->ccid.as<u32>(), tcapc - 1, c->dcls.as<u32>(), c->crep.as<u32>());
+            crep = c->crep.as<u32>();
         }
         ENSURE(c, coff, (ncls + 1ull) * 8);
         ENSURE(c, cmask, std::max<u64>(ncls, 1) * 8);
@@ -1020,24 +1050,24 @@ static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* 
         ENSURE(c, cnch, std::max<u64>(ncls, 1) * 4);
         ENSURE(c, cchoff, (ncls + 1ull) * 8);
         hipLaunchKernelGGL(k_class_info, dim3(grid_for(ncls + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
-                           c->ckeys.as<u64>(), nmem, ncls, c->pivot.as<u32>(), c->coff.as<u64>(), c->cmask.as<u64>(),
+                           c->ckeys.as<u64>(), nmem, ncls, c->pivot.as<u32>(), crep, c->coff.as<u64>(), c->cmask.as<u64>(),
                            c->cpiv.as<u32>(), c->cnch.as<u32>());
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cnch.as<u32>(), c->cchoff.as<u64>(), ncls, c->cchoff.as<u64>() + ncls, st));
         u64 WC = 0;
         TRY(read_u64(c, c->cchoff.as<u64>() + ncls, &WC));
         ENSURE(c, ccnt, std::max<u64>(WC, 1) * 4);
-    ENSURE(c, cbits, std::max<u64>(WC, 1) * 8);
-    ENSURE(c, cown, std::max<u64>(WC, 1) * 4);
-    if (WC)
-        hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(std::max<u32>(ncls, 1), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                           c->cchoff.as<u64>(), ncls, c->cown.as<u32>());
+        ENSURE(c, cbits, std::max<u64>(WC, 1) * 8);
+        ENSURE(c, cown, std::max<u64>(WC, 1) * 4);
         ENSURE(c, lwoff, (WC + 1) * 8);
         if (WC) {
-            const dim3 grid((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK));
-            hipLaunchKernelGGL(k_class_eval, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cmask.as<u64>(),
-                               c->cpiv.as<u32>(), c->cbits.as<u64>());
+            hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(ncls, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                               c->cchoff.as<u64>(), ncls, c->cown.as<u32>());
+            const u64 nvb = wave_blocks(WC);
+            const dim3 grid(vgrid(nvb));
+            hipLaunchKernelGGL(k_class_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
+                               c->cmask.as<u64>(), c->cpiv.as<u32>(), c->cbits.as<u64>());
             if (v.mode == RULES_CLEAN)
-                hipLaunchKernelGGL(k_class_mark, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
+                hipLaunchKernelGGL(k_class_mark, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
                                    c->cmask.as<u64>(), c->cpiv.as<u32>(), c->cbits.as<u64>());
             hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WC, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cbits.as<u64>(),
                                WC, c->ccnt.as<u32>());
@@ -1047,14 +1077,32 @@ static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* 
         TRY(read_u64(c, c->lwoff.as<u64>() + WC, &LT));
         ENSURE(c, clists, std::max<u64>(LT, 1) * 4);
         if (WC)
-            hipLaunchKernelGGL(k_class_write, dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                               dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cpiv.as<u32>(), c->cbits.as<u64>(),
-                               c->lwoff.as<u64>(), c->clists.as<u32>(), (u64*)nullptr);
+            hipLaunchKernelGGL(k_class_write, dim3(vgrid(wave_blocks(WC))),
+                               dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WC), v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cpiv.as<u32>(),
+                               c->cbits.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), (u64*)nullptr);
         TRY(d_class_tiles(c, nmem, ncls, HC, NT));
     }
     tend(c, RDF_T_CLASS);
     c->n_class_members = nmem;
     c->n_classes = ncls;
+    return RDF_OK;
+}
+
+// classed binary heavy-only dependents: work items = chunks of their class lists -> choffh, *WH
+static rdf_status d_class_bin(rdf_ctx* c, const CindView& v, u64* WH) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    ENSURE(c, sbase, std::max<u64>(C, 1) * 8);
+    tbegin(c, RDF_T_HCOUNT);
+    if (c->n_classes && C)
+        hipLaunchKernelGGL(k_class_bin_chunks, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                           c->dcls.as<u32>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->nchh.as<u32>(), c->sbase.as<u64>());
+    else
+        HIP_TRY(c, hipMemsetAsync(c->nchh.p, 0, std::max<u64>(C, 1) * 4, st));
+    tend(c, RDF_T_HCOUNT);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
+    TRY(read_u64(c, c->choffh.as<u64>() + C, WH));
+    c->heavy_candidates = *WH * RDF_WAVE;  // class-list entries scanned (upper bound)
     return RDF_OK;
 }
 
@@ -1080,13 +1128,14 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     TRY(read_u64(c, c->pos.as<u64>() + E, &K));
     tbegin(c, RDF_T_HWRITE);
     if (WH)
-        hipLaunchKernelGGL(k_heavy_write, dim3((unsigned)((WH + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH, c->hbits.as<u64>(),
-                           c->hoff.as<u64>(), K, c->out.as<u32>());
+        hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(WH))),
+                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WH), v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+                           c->hbits.as<u64>(), c->hclassed ? c->clists.as<u32>() : c->gcap.as<u32>(),
+                           c->hclassed ? c->sbase.as<u64>() : (const u64*)nullptr, c->hoff.as<u64>(), K, c->out.as<u32>());
     tend(c, RDF_T_HWRITE);
     tbegin(c, RDF_T_CEMIT);
     if (NT)
-        hipLaunchKernelGGL(k_class_emit, dim3((unsigned)NT), dim3(RDF_BLOCK), 0, st, c->coff.as<u64>(),
+        hipLaunchKernelGGL(k_class_emit, dim3(vgrid(NT)), dim3(RDF_BLOCK), 0, st, NT, c->coff.as<u64>(),
                            c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(),
                            (u32)c->n_classes, c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u32>());
     tend(c, RDF_T_CEMIT);
@@ -1146,8 +1195,11 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));
-    TRY(d_heavy_count(c, v, WH, &H));
+    // strategy 0's quirk filter is per dependent: keep the pivot scan there (RDFIND_HCLASS=0: test hook)
+    c->hclassed = !v.literal && c->allow_hclass;
     TRY(d_classes_single(c, v, &HC, &NT));
+    if (c->hclassed) TRY(d_class_bin(c, v, &WH));
+    TRY(d_heavy_count(c, v, WH, &H));
     TRY(d_emit(c, v, E, WH, H, HC, NT));
     if (stats) *stats = c->cstats;
     return RDF_OK;
@@ -1208,7 +1260,7 @@ static rdf_status sh_phase2(rdf_ctx* c, rdf_exchange* req) {
     u32 gh[256] = {};
     for (u32 r = 0; r < R; ++r)
         for (int b = 0; b < 256; ++b) gh[b] += (u32)all[256ull * r + b];
-    const u64 thr = heavy_threshold(gh);
+    const u64 thr = heavy_threshold(c, gh);
     u32 base = 0;
     for (u32 r = 0; r < c->rank; ++r) {
         u32 lh[256];
@@ -1340,7 +1392,7 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     tbegin(c, RDF_T_CLASS);
     u64 nmem_all = 0, tcapc = 0;
     u32 ncls = 0;
-    TRY(d_class_table(c, v, &nmem_all, &ncls, &tcapc));
+    TRY(d_class_table(c, v, c->Cu, &nmem_all, &ncls, &tcapc));
     c->sh_tcapc = tcapc;
     c->n_classes = ncls;
     ENSURE(c, smask, std::max<u64>(ncls, 1) * 8);
@@ -1397,11 +1449,12 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
                            c->cchoff.as<u64>(), ncls, c->cown.as<u32>());
     ENSURE(c, lwoff, (WC + 1) * 8);
     if (WC) {
-        const dim3 grid((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK));
-        hipLaunchKernelGGL(k_class_eval, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cmask.as<u64>(),
+        const u64 nvb = wave_blocks(WC);
+        const dim3 grid(vgrid(nvb));
+        hipLaunchKernelGGL(k_class_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cmask.as<u64>(),
                            c->cpiv.as<u32>(), c->cbits.as<u64>());
         if (v.mode == RULES_CLEAN)
-            hipLaunchKernelGGL(k_class_mark, grid, dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
+            hipLaunchKernelGGL(k_class_mark, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC,
                                c->cmask.as<u64>(), c->cpiv.as<u32>(), c->cbits.as<u64>());
         hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WC, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cbits.as<u64>(),
                            WC, c->ccnt.as<u32>());
@@ -1411,8 +1464,8 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     TRY(read_u64(c, c->lwoff.as<u64>() + WC, &LT));
     ENSURE(c, xsend, std::max<u64>(LT, 1) * 8);
     if (WC)
-        hipLaunchKernelGGL(k_class_write, dim3((unsigned)((WC + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK)),
-                           dim3(RDF_BLOCK), 0, st, v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cpiv.as<u32>(), c->cbits.as<u64>(),
+        hipLaunchKernelGGL(k_class_write, dim3(vgrid(wave_blocks(WC))),
+                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WC), v, c->cchoff.as<u64>(), c->cown.as<u32>(), WC, c->cpiv.as<u32>(), c->cbits.as<u64>(),
                            c->lwoff.as<u64>(), (u32*)nullptr, c->xsend.as<u64>());
     tend(c, RDF_T_CLASS);
     HIP_TRY(c, hipStreamSynchronize(st));
@@ -1457,6 +1510,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     if (!c) return RDF_ERR_ARG;
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    c->hclassed = false;
     int proj = 0;
     TRY(parse_projection(c, projection, &proj));
     c->sh_rank = rank;

@@ -185,3 +185,52 @@ def test_bench_size_properties(ctx):
         jr = _capture_joins(d, rc, r1, r2)
         assert len(jd) == sup
         assert np.isin(jd, jr).all()
+
+
+@pytest.mark.parametrize("heavy_min", [1, 2, 8])
+def test_heavy_paths_parity(monkeypatch, heavy_min):
+    """Small inputs with a lowered heavy-group minimum (RDFIND_HEAVY_MIN test hook), so the bitmask columns,
+    the mask classes (unary and binary heavy-only dependents) and the mark passes of R2/R3 carry most of the
+    result, in every mode."""
+    monkeypatch.setenv("RDFIND_HEAVY_MIN", str(heavy_min))
+    g = _lib.Context(0)
+    try:
+        rng = random.Random(100 + heavy_min)
+        for _ in range(60):
+            n = rng.randrange(20, 400)
+            nv = rng.randrange(4, 40)
+            ms = rng.randrange(1, 4)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            for strategy, clean in MODES:
+                assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
+                    (n, nv, ms, strategy, clean, heavy_min)
+        for cfg, scale in (("c5", 0.01), ("c1", 0.05)):
+            d = synth.config(cfg, scale)
+            exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+            g.set_triples(d.s, d.p, d.o, d.num_terms)
+            cs = g.run(d.min_support)
+            assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, heavy_min)
+            assert g.groups["n_heavy_groups"] > 0
+    finally:
+        g.close()
+
+
+def test_large_grids_two_paths(monkeypatch):
+    """c5 at scale 0.3 (8.7e9 CINDs): the heavy-only binary dependents take > 2^26 work items (a dispatch holds
+    < 2^32 work-items, so the kernels loop over virtual blocks).  The classed path and the pivot-scan path
+    (RDFIND_HCLASS=0) compute them independently and must agree on the count and the set checksum."""
+    d = synth.config("c5", 0.3)
+    got = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RDFIND_HCLASS", flag)
+        g = _lib.Context(0)
+        try:
+            g.set_triples(d.s, d.p, d.o, d.num_terms)
+            cs = g.run(d.min_support)
+            got.append((g.cind_count(), g.checksum()))
+            if flag == "0":
+                assert cs["n_heavy_chunks"] * 64 > 2 ** 32
+        finally:
+            g.close()
+    assert got[0] == got[1] and got[0][0] > 2 ** 32
