@@ -804,7 +804,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
 }
 
 __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
-                                                         u64* best_out, u32* nlight_out) {
+                                        u64* best_out, u32* nlight_out) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -839,8 +839,9 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
         }
     }
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(u64 nvblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
-                                                         u64* best_out, u32* nlight_out) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(u64 nvblk, CindView v, u32* dgrp_tag,
+                                                         const u64* __restrict__ segoff, u64 W, u64* best_out,
+                                                         u32* nlight_out) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out);
     }
@@ -1027,15 +1028,16 @@ __device__ inline void slot_emit(u64 oct0, u32 nvalid, u32 d, u32 cand, u64 aliv
 }
 
 __device__ inline void k_slot_compact_body(u64 vblk, const u64* __restrict__ slots, const u32* __restrict__ counts,
-                                                            const u64* __restrict__ pos, u64 W, u64* out) {
+                                           const u64* __restrict__ pos, u64 W, u64* out) {
     const u64 g = (u64)vblk * RDF_BLOCK + threadIdx.x;
     const u64 o = g >> 3;
     if (o >= W) return;
     const u32 j = (u32)(g & 7);
     if (j < counts[o]) out[pos[o] + j] = slots[g];
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(u64 nvblk, const u64* __restrict__ slots, const u32* __restrict__ counts,
-                                                            const u64* __restrict__ pos, u64 W, u64* out) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(u64 nvblk, const u64* __restrict__ slots,
+                                                            const u32* __restrict__ counts, const u64* __restrict__ pos,
+                                                            u64 W, u64* out) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_slot_compact_body(vb, slots, counts, pos, W, out);
     }
@@ -1046,8 +1048,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(u64 nvblk, const u64
 // dependents per wave.  Each lane walks its dependent's groups and binary-searches its candidate in every
 // light one (the same test as k_light's few-groups path, without a mostly idle wave per dependent).
 __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                                            const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep,
-                                                            u64 WP, const u64* __restrict__ choff, u64* slots, u32* counts) {
+                                           const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep, u64 WP,
+                                           const u64* __restrict__ choff, u64* slots, u32* counts) {
     const u64 g = (u64)vblk * RDF_BLOCK + threadIdx.x;
     const u64 q = g >> 3;
     if (q >= WP) return;  // whole octets only, so the octet ballots below see complete octets
@@ -1071,8 +1073,9 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     if (ok) slots[oct * 8 + __popc(om & ((1u << jj) - 1u))] = ((u64)d << 32) | cand;
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                            const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep,
-                                                            u64 WP, const u64* __restrict__ choff, u64* slots, u32* counts) {
+                                                            const u64* __restrict__ pkoff,
+                                                            const u32* __restrict__ pk_dep, u64 WP,
+                                                            const u64* __restrict__ choff, u64* slots, u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_light_packed_body(vb, v, pivot, pkoff, pk_dep, WP, choff, slots, counts);
     }
@@ -1097,9 +1100,9 @@ __device__ unsigned long long g_light_stats[16];
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
-__device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
-                                                     const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
-                                                     u64* dead, u64* slots, u32* counts) {
+__device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
+                                    const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
+                                    const u64* __restrict__ choff, u64 W, u64* dead, u64* slots, u32* counts) {
     __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_LDS];
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
@@ -1241,9 +1244,10 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // counter: an agent-scope release fence writes back the whole L2 of the XCD, per work item.
     if (lane == 0 && (alive0 & ~alive)) atomicOr(&dead[oct0], alive0 & ~alive);
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
-                                                     const u32* __restrict__ item_dep, const u64* __restrict__ choff, u64 W,
-                                                     u64* dead, u64* slots, u32* counts) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
+                                                     const u64* __restrict__ choff, u64 W, u64* dead, u64* slots,
+                                                     u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_light_body(vb, v, pivot, itemoff, item_dep, choff, W, dead, slots, counts);
     }
@@ -1253,9 +1257,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light(u64 nvblk, CindView v, cons
 // chunks verified by several segments: survivors = candidates minus the union of the segments' kills
 // (launched after k_light; the kernel boundary orders the kills before these reads)
 __device__ inline void k_light_mseg_emit_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                                               const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep,
-                                                               u64 WM, const u64* __restrict__ choff,
-                                                               const u64* __restrict__ dead, u64* slots, u32* counts) {
+                                              const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep, u64 WM,
+                                              const u64* __restrict__ choff, const u64* __restrict__ dead, u64* slots,
+                                              u32* counts) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= WM) return;
     const u32 d = mch_dep[w];
@@ -1267,8 +1271,9 @@ __device__ inline void k_light_mseg_emit_body(u64 vblk, CindView v, const u32* _
     slot_emit(oct0, noct < 8 ? (u32)noct : 8u, d, cand, alive0 & ~dead[oct0], slots, counts);
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                               const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep,
-                                                               u64 WM, const u64* __restrict__ choff,
+                                                               const u64* __restrict__ mchoff,
+                                                               const u32* __restrict__ mch_dep, u64 WM,
+                                                               const u64* __restrict__ choff,
                                                                const u64* __restrict__ dead, u64* slots, u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_light_mseg_emit_body(vb, v, pivot, mchoff, mch_dep, WM, choff, dead, slots, counts);
@@ -1334,8 +1339,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_popc_counts(const u64* __restrict
 // k_heavy_mark (R2: the components of every raw binary ref are cleared, they sit in the same pivot group),
 // then k_heavy_write streams the survivors at the scanned offsets (popcounts of bits).
 __device__ inline void k_heavy_eval_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
-                                                          u64* bits) {
+                                         const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 d = owner[w];
@@ -1348,8 +1352,8 @@ __device__ inline void k_heavy_eval_body(u64 vblk, CindView v, const u32* __rest
     if (lane_id() == 0) bits[w] = kept;
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_eval(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
-                                                          u64* bits) {
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner,
+                                                          u64 W, u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_heavy_eval_body(vb, v, pivot, choff, owner, W, bits);
     }
@@ -1368,7 +1372,7 @@ __device__ inline void mark_clear(u64* bits, u64 p, bool active) {
 }
 
 __device__ inline void k_heavy_mark_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
+                                         const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 d = owner[w];
@@ -1388,7 +1392,8 @@ __device__ inline void k_heavy_mark_body(u64 vblk, CindView v, const u32* __rest
     }
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
+                                                          const u64* __restrict__ choff, const u32* __restrict__ owner,
+                                                          u64 W, u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_heavy_mark_body(vb, v, pivot, choff, owner, W, bits);
     }
@@ -1398,10 +1403,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(u64 nvblk, CindView v,
 // survivors of a heavy work item -> output run of its dependent; src[sbase[d] + i] is candidate i of d
 // (classed binary dependents: their class list; otherwise sbase = null and the pivot group is the source)
 __device__ inline void k_heavy_write_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
-                                                           const u64* __restrict__ bits, const u32* __restrict__ src,
-                                                           const u64* __restrict__ sbase, const u64* __restrict__ woff,
-                                                           u64 out_base, u32* out) {
+                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
+                                          const u64* __restrict__ bits, const u32* __restrict__ src,
+                                          const u64* __restrict__ sbase, const u64* __restrict__ woff, u64 out_base,
+                                          u32* out) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u64 kept = bits[w];
@@ -1412,10 +1417,10 @@ __device__ inline void k_heavy_write_body(u64 vblk, CindView v, const u32* __res
     out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = src[base + (w - choff[d]) * RDF_WAVE + lane];
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                           const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
-                                                           const u64* __restrict__ bits, const u32* __restrict__ src,
-                                                           const u64* __restrict__ sbase, const u64* __restrict__ woff,
-                                                           u64 out_base, u32* out) {
+                                                           const u64* __restrict__ choff, const u32* __restrict__ owner,
+                                                           u64 W, const u64* __restrict__ bits,
+                                                           const u32* __restrict__ src, const u64* __restrict__ sbase,
+                                                           const u64* __restrict__ woff, u64 out_base, u32* out) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_heavy_write_body(vb, v, pivot, choff, owner, W, bits, src, sbase, woff, out_base, out);
     }
@@ -1480,7 +1485,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_keys(CindView v, const u64*
 }
 
 // binary heavy-only dependents join the mask classes (single GPU, S2L semantics): class id per dependent and
-// the smallest member of every class (its representative: members of a class share the pivot group)
+// a representative member of every class (members of a class share the pivot group)
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_of(CindView v, const u64* __restrict__ tkeys, const u32* __restrict__ cid,
                                                         u64 tmask, u32* dcls, u32* crep) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
@@ -1490,7 +1495,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_of(CindView v, const u64* _
             u64 h = mix64(mk) & tmask;
             while (tkeys[h] != mk) h = (h + 1) & tmask;
             m = cid[h];
-            atomicMin(&crep[m], (u32)d);
+            // any member represents its class (same groups, same pivot): a plain store once the slot is seen
+            // taken is skipped (thousands of members per class would otherwise serialise on one address)
+            if (crep[m] == NONE32) crep[m] = (u32)d;
         }
         if (d >= v.Cu) dcls[d - v.Cu] = m;
     }
@@ -1516,10 +1523,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_bin_chunks(CindView v, cons
 // R2 is already in L'(m): D's binary raw refs are the binary members of L(m), the class marks cleared their
 // components.  Survivor bits per chunk, as k_heavy_eval.
 __device__ inline void k_class_bin_eval_body(u64 vblk, CindView v, const u64* __restrict__ choff,
-                                                              const u32* __restrict__ owner, u64 W, const u64* __restrict__ sbase,
-                                                              const u32* __restrict__ dcls, const u64* __restrict__ cchoff,
-                                                              const u64* __restrict__ lwoff, const u32* __restrict__ lists,
-                                                              u64* bits) {
+                                             const u32* __restrict__ owner, u64 W, const u64* __restrict__ sbase,
+                                             const u32* __restrict__ dcls, const u64* __restrict__ cchoff,
+                                             const u64* __restrict__ lwoff, const u32* __restrict__ lists, u64* bits) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 d = owner[w];
@@ -1532,10 +1538,12 @@ __device__ inline void k_class_bin_eval_body(u64 vblk, CindView v, const u64* __
     if (lane_id() == 0) bits[w] = kept;
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_bin_eval(u64 nvblk, CindView v, const u64* __restrict__ choff,
-                                                              const u32* __restrict__ owner, u64 W, const u64* __restrict__ sbase,
-                                                              const u32* __restrict__ dcls, const u64* __restrict__ cchoff,
-                                                              const u64* __restrict__ lwoff, const u32* __restrict__ lists,
-                                                              u64* bits) {
+                                                              const u32* __restrict__ owner, u64 W,
+                                                              const u64* __restrict__ sbase,
+                                                              const u32* __restrict__ dcls,
+                                                              const u64* __restrict__ cchoff,
+                                                              const u64* __restrict__ lwoff,
+                                                              const u32* __restrict__ lists, u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_class_bin_eval_body(vb, v, choff, owner, W, sbase, dcls, cchoff, lwoff, lists, bits);
     }
@@ -1559,23 +1567,35 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_info(CindView v, const u64*
     }
 }
 
+// R3 for a unary ref with few parents is a scan of parents(r) in the eval pass (cheap, no atomics); the
+// components with long parent lists (s[p=P] under every s[p=P,o=*]) are cleared by the mark pass instead
+static constexpr u64 PARENT_SCAN_MAX = 32;
+__device__ inline bool short_parents(const CindView& v, u32 r) {
+    return !(v.info[r].meta & META_PARENTS) || v.poff[r + 1] - v.poff[r] <= PARENT_SCAN_MAX;
+}
+
 // L'(m): the class pivot group filtered by the mask test (bits per chunk of 64 members), then, under
-// --clean-implied, R3 by k_class_mark: the components of the binary members of L(m) are cleared (a binary
-// X with hmask(X) >= m is a raw ref of every member; its components sit in the same pivot group).
-__device__ inline void k_class_eval_body(u64 vblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
-                                                          const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
-                                                          u64* bits) {
+// --clean-implied, R3: the components of the binary members of L(m) are dropped (a binary X with
+// hmask(X) >= m is a raw ref of every member; its components sit in the same pivot group) -- by a scan of
+// parents(r) in the eval pass when that list is short, by k_class_mark otherwise.
+__device__ inline void k_class_eval_body(u64 vblk, CindView v, const u64* __restrict__ cchoff,
+                                         const u32* __restrict__ owner, u64 W, const u64* __restrict__ cmask,
+                                         const u32* __restrict__ cpiv, u64* bits) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 m = owner[w];
     const u32 g = cpiv[m];
     const u64 mask = cmask[m];
     const u64 idx = v.goff[g] + (w - cchoff[m]) * RDF_WAVE + lane_id();
-    const bool keep = idx < v.goff[g + 1] && (v.info[v.gcap[idx]].hmask & mask) == mask;
+    const u32 r = idx < v.goff[g + 1] ? v.gcap[idx] : 0u;
+    bool keep = idx < v.goff[g + 1] && (v.info[r].hmask & mask) == mask;
+    if (keep && v.mode == RULES_CLEAN && r < v.Cu && short_parents(v, r))  // R3 here; long lists: k_class_mark
+        for (u64 j = v.poff[r]; j < v.poff[r + 1] && keep; ++j) keep = (v.info[v.plist[j]].hmask & mask) != mask;
     const u64 kept = __ballot(keep);
     if (lane_id() == 0) bits[w] = kept;
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(u64 nvblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(u64 nvblk, CindView v, const u64* __restrict__ cchoff,
+                                                          const u32* __restrict__ owner, u64 W,
                                                           const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
                                                           u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
@@ -1584,9 +1604,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_eval(u64 nvblk, CindView v,
 }
 
 
-__device__ inline void k_class_mark_body(u64 vblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
-                                                          const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
-                                                          u64* bits) {
+__device__ inline void k_class_mark_body(u64 vblk, CindView v, const u64* __restrict__ cchoff,
+                                         const u32* __restrict__ owner, u64 W, const u64* __restrict__ cmask,
+                                         const u32* __restrict__ cpiv, u64* bits) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u32 m = owner[w];
@@ -1601,12 +1621,13 @@ __device__ inline void k_class_mark_body(u64 vblk, CindView v, const u64* __rest
     for (int k = 0; k < 2; ++k) {
         const u32 t = bin ? v.bcomp[2ull * (x - v.Cu) + k] : NONE32;
         const u32 tprev = __shfl_up(t, 1, RDF_WAVE);
-        const bool head = bin && (lane_id() == 0 || tprev != t);  // consecutive refs share component 0
+        const bool head = bin && (lane_id() == 0 || tprev != t) && !short_parents(v, t);  // consecutive refs share comp 0
         const u64 p = head ? group_pos(v, g, t) : ~0ull;
         mark_clear(bits, base + p, p != ~0ull);
     }
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(u64 nvblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(u64 nvblk, CindView v, const u64* __restrict__ cchoff,
+                                                          const u32* __restrict__ owner, u64 W,
                                                           const u64* __restrict__ cmask, const u32* __restrict__ cpiv,
                                                           u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
@@ -1615,9 +1636,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_mark(u64 nvblk, CindView v,
 }
 
 
-__device__ inline void k_class_write_body(u64 vblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
-                                                           const u32* __restrict__ cpiv, const u64* __restrict__ bits,
-                                                           const u64* __restrict__ woff, u32* lists, u64* cpairs) {
+__device__ inline void k_class_write_body(u64 vblk, CindView v, const u64* __restrict__ cchoff,
+                                          const u32* __restrict__ owner, u64 W, const u32* __restrict__ cpiv,
+                                          const u64* __restrict__ bits, const u64* __restrict__ woff, u32* lists,
+                                          u64* cpairs) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const u64 kept = bits[w];
@@ -1629,7 +1651,8 @@ __device__ inline void k_class_write_body(u64 vblk, CindView v, const u64* __res
     if (cpairs) cpairs[o] = ((u64)m << 32) | r;  // sharded mode: (class, ref) pairs for the all-gather
     else lists[o] = r;
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_write(u64 nvblk, CindView v, const u64* __restrict__ cchoff, const u32* __restrict__ owner, u64 W,
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_write(u64 nvblk, CindView v, const u64* __restrict__ cchoff,
+                                                           const u32* __restrict__ owner, u64 W,
                                                            const u32* __restrict__ cpiv, const u64* __restrict__ bits,
                                                            const u64* __restrict__ woff, u32* lists, u64* cpairs) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
@@ -1684,10 +1707,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_tiles(const u64* __restrict
 // from the 256-B boundary below the segment start, so every wave-wide store covers whole lines.  Segment s
 // of a run needs list entries [s*CLS_LS - 31, (s+1)*CLS_LS + 1), hence the staged halo.
 __device__ inline void k_class_emit_body(u64 vblk, const u64* __restrict__ coff, const u64* __restrict__ cchoff,
-                                                          const u64* __restrict__ lwoff, const u32* __restrict__ lists,
-                                                          const u64* __restrict__ toff, u32 ncls,
-                                                          const u32* __restrict__ selfpos, const u64* __restrict__ obase,
-                                                          u64 out_base, u32* out) {
+                                         const u64* __restrict__ lwoff, const u32* __restrict__ lists,
+                                         const u64* __restrict__ toff, u32 ncls, const u32* __restrict__ selfpos,
+                                         const u64* __restrict__ obase, u64 out_base, u32* out) {
     __shared__ u32 sl[CLS_LS + 64];
     __shared__ u32 s_sp[CLS_DT];
     __shared__ u64 s_base[CLS_DT];
@@ -1750,11 +1772,11 @@ __device__ inline void k_class_emit_body(u64 vblk, const u64* __restrict__ coff,
         }
     }
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(u64 nvblk, const u64* __restrict__ coff, const u64* __restrict__ cchoff,
-                                                          const u64* __restrict__ lwoff, const u32* __restrict__ lists,
-                                                          const u64* __restrict__ toff, u32 ncls,
-                                                          const u32* __restrict__ selfpos, const u64* __restrict__ obase,
-                                                          u64 out_base, u32* out) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(u64 nvblk, const u64* __restrict__ coff,
+                                                          const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
+                                                          const u32* __restrict__ lists, const u64* __restrict__ toff,
+                                                          u32 ncls, const u32* __restrict__ selfpos,
+                                                          const u64* __restrict__ obase, u64 out_base, u32* out) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
         k_class_emit_body(vb, coff, cchoff, lwoff, lists, toff, ncls, selfpos, obase, out_base, out);
         __syncthreads();  // shared staging is reused by the next virtual block
