@@ -13,7 +13,7 @@ sharded (rdfind_amd/distributed.py): every rank holds the triples,
 of its join-value hash shard and the dependents d % N, and the eight collectives of the protocol run
 inside the timed region.  `value` is the workload's triples divided by the max-over-ranks time per
 step (strong scaling).  `roofline` is computed for the dominant kernel family from HIP events recorded on
-the library's stream; `cpu_baseline` times the C restatement (oracle/) on a bounded sample on rank 0.
+the library's stream; `cpu_baseline` times the C restatement (oracle/, OpenMP) on a bounded sample on rank 0.
 """
 from __future__ import annotations
 
@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-scale", type=float, default=0.2)
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.3)
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
                     "exchanges, to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -173,9 +173,10 @@ def main():
         t = time.perf_counter()
         _, _, st = c_oracle.run(sd.s, sd.p, sd.o, sd.num_terms, sd.min_support, 1, True)
         ct = time.perf_counter() - t
-        cpu = {"value": round(sd.n / ct, 1), "unit": "triples/s", "cores": 1, "kind": "port",
+        nt = c_oracle.threads()
+        cpu = {"value": round(sd.n / ct, 1), "unit": "triples/s", "cores": nt, "kind": "port",
                "sample": f"{args.config} scale {args.cpu_sample_scale} ({sd.n} triples, {st['n_cinds']} CINDs) "
-                         f"through oracle/c/rdfind_oracle.c single-threaded, {ct:.1f}s"}
+                         f"through oracle/c/rdfind_oracle.c on {nt} OpenMP threads, {ct:.1f}s"}
 
     if rank == 0:
         line = {

@@ -1,10 +1,11 @@
 /*
  * ORACLE -- test infrastructure only.  Never linked into the product path.
  *
- * Scalar single-threaded C restatement of RDFind's CIND discovery on
- * dictionary-encoded triples.  It is the mid-size parity checker for the HIP
- * library (tests/, __graft_entry__.smoke()) and the "port" CPU baseline of
- * bench.py.  Cross-checked against the literal Python restatement
+ * Scalar C restatement of RDFind's CIND discovery on dictionary-encoded
+ * triples.  It is the mid-size parity checker for the HIP library (tests/,
+ * __graft_entry__.smoke()) and the "port" CPU baseline of bench.py.  Stages 5
+ * and 6 (per-dependent intersection, minimality) run on OpenMP threads
+ * (OMP_NUM_THREADS); the output order does not depend on the thread count.  Cross-checked against the literal Python restatement
  * (oracle/rdfind_oracle.py) by tests/test_oracle_c.py.
  *
  * Abbreviation: ALG/ = rdfind-algorithm/src/main/scala/de/hpi/isg/sodap/rdfind/
@@ -24,6 +25,7 @@
  * binary b (index into the sorted frequent binary keys) -> 6V+b.  Binary key =
  * bt<<62 | v1<<31 | v2, bt = 0 (s[p,o], code 14), 1 (p[s,o], 21), 2 (o[s,p], 35).
  */
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -48,24 +50,44 @@ typedef struct {
 
 static void *xmalloc(size_t n) { return malloc(n ? n : 1); }
 
+/* LSD radix sort, 11-bit digits; each pass: per-thread histograms of contiguous blocks, digit-major
+ * offsets, stable scatter (OpenMP threads; same result for any thread count) */
 static void radix_sort_u64(uint64_t *a, uint64_t n) {
     if (n < 2) return;
     uint64_t *tmp = (uint64_t *)xmalloc(n * sizeof(uint64_t));
     uint64_t *src = a, *dst = tmp;
+    const int nt = n < (1u << 16) ? 1 : omp_get_max_threads();
+    uint64_t *cnt = (uint64_t *)xmalloc((size_t)nt * 2048 * sizeof(uint64_t));
     for (int shift = 0; shift < 64; shift += 11) {
-        uint64_t cnt[2048];
-        memset(cnt, 0, sizeof(cnt));
-        for (uint64_t i = 0; i < n; ++i) cnt[(src[i] >> shift) & 2047]++;
+        memset(cnt, 0, (size_t)nt * 2048 * sizeof(uint64_t));
+#pragma omp parallel num_threads(nt)
+        {
+            const int t = omp_get_thread_num();
+            const uint64_t b0 = n * t / nt, b1 = n * (t + 1) / nt;
+            uint64_t *c = cnt + (size_t)t * 2048;
+            for (uint64_t i = b0; i < b1; ++i) c[(src[i] >> shift) & 2047]++;
+        }
         int trivial = 0;
-        for (int d = 0; d < 2048; ++d)
-            if (cnt[d] == n) { trivial = 1; break; }
+        for (int d = 0; d < 2048 && !trivial; ++d) {
+            uint64_t tot = 0;
+            for (int t = 0; t < nt; ++t) tot += cnt[(size_t)t * 2048 + d];
+            trivial = tot == n;
+        }
         if (trivial) continue;
         uint64_t sum = 0;
-        for (int d = 0; d < 2048; ++d) { uint64_t c = cnt[d]; cnt[d] = sum; sum += c; }
-        for (uint64_t i = 0; i < n; ++i) dst[cnt[(src[i] >> shift) & 2047]++] = src[i];
+        for (int d = 0; d < 2048; ++d)
+            for (int t = 0; t < nt; ++t) { uint64_t c = cnt[(size_t)t * 2048 + d]; cnt[(size_t)t * 2048 + d] = sum; sum += c; }
+#pragma omp parallel num_threads(nt)
+        {
+            const int t = omp_get_thread_num();
+            const uint64_t b0 = n * t / nt, b1 = n * (t + 1) / nt;
+            uint64_t *c = cnt + (size_t)t * 2048;
+            for (uint64_t i = b0; i < b1; ++i) dst[c[(src[i] >> shift) & 2047]++] = src[i];
+        }
         uint64_t *t = src; src = dst; dst = t;
     }
     if (src != a) memcpy(a, src, n * sizeof(uint64_t));
+    free(cnt);
     free(tmp);
 }
 
@@ -257,71 +279,96 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
     free(cur);
 
     /* 5. per dependent: ref set = intersection over its groups of (group \ implied)
-     *    (CreateAllCindCandidates.scala:106-121 + IntersectCindCandidates.scala:40-43) */
-    uint64_t ccap = 1 << 16, nc = 0;
-    orc_cind *cind = (orc_cind *)xmalloc(ccap * sizeof(orc_cind));
-    uint32_t *refs = NULL, *tmp = NULL;
-    uint64_t refs_cap = 0;
-    for (uint64_t a = 0; a < ncap; ++a) {
-        if (support[a] < ms) continue;
-        /* trivial refs of a binary dep: its two unary components (Condition.isImpliedBy) */
-        uint32_t triv1 = ~0u, triv2 = ~0u;
-        int dep_bt = -1;
-        uint32_t dv1 = 0, dv2 = 0;
-        if (a >= 6ull * V) {
-            uint64_t key = bkeys[a - 6ull * V];
-            dep_bt = (int)(key >> 62);
-            dv1 = (uint32_t)((key >> 31) & 0x7fffffff);
-            dv2 = (uint32_t)(key & 0x7fffffff);
-            int t1, t2;
-            binary_components(dep_bt, &t1, &t2);
-            triv1 = (uint32_t)((uint64_t)t1 * V + dv1);
-            triv2 = (uint32_t)((uint64_t)t2 * V + dv2);
-        }
-        uint64_t nref = 0;
-        for (uint64_t j = doff[a]; j < doff[a + 1]; ++j) {
-            uint64_t g = dgrp[j];
-            uint64_t k = goff[g + 1] - goff[g];
-            const uint32_t *gc = gcap + goff[g];
-            if (j == doff[a]) {
-                if (k > refs_cap) {
-                    refs_cap = k * 2;
-                    refs = (uint32_t *)realloc(refs, refs_cap * sizeof(uint32_t));
-                    tmp = (uint32_t *)realloc(tmp, refs_cap * sizeof(uint32_t));
+     *    (CreateAllCindCandidates.scala:106-121 + IntersectCindCandidates.scala:40-43).
+     *    Dependents are split into chunks processed by OpenMP threads; each chunk's CINDs go to its own
+     *    buffer and the buffers are concatenated in chunk (= dependent) order. */
+    const uint64_t nchunk = ncap < 4096 ? 1 : 4096;
+    orc_cind **cbuf = (orc_cind **)calloc(nchunk, sizeof(orc_cind *));
+    uint64_t *ccnt = (uint64_t *)calloc(nchunk + 1, sizeof(uint64_t));
+#pragma omp parallel
+    {
+        uint32_t *refs = NULL, *tmp = NULL;
+        uint64_t refs_cap = 0;
+#pragma omp for schedule(dynamic, 1)
+        for (uint64_t ch = 0; ch < nchunk; ++ch) {
+            uint64_t ccap = 256, nc = 0;
+            orc_cind *cind = (orc_cind *)xmalloc(ccap * sizeof(orc_cind));
+            const uint64_t a0 = ncap * ch / nchunk, a1 = ncap * (ch + 1) / nchunk;
+            for (uint64_t a = a0; a < a1; ++a) {
+                if (support[a] < ms) continue;
+                /* trivial refs of a binary dep: its two unary components (Condition.isImpliedBy) */
+                uint32_t triv1 = ~0u, triv2 = ~0u;
+                int dep_bt = -1;
+                uint32_t dv1 = 0, dv2 = 0;
+                if (a >= 6ull * V) {
+                    uint64_t key = bkeys[a - 6ull * V];
+                    dep_bt = (int)(key >> 62);
+                    dv1 = (uint32_t)((key >> 31) & 0x7fffffff);
+                    dv2 = (uint32_t)(key & 0x7fffffff);
+                    int t1, t2;
+                    binary_components(dep_bt, &t1, &t2);
+                    triv1 = (uint32_t)((uint64_t)t1 * V + dv1);
+                    triv2 = (uint32_t)((uint64_t)t2 * V + dv2);
                 }
-                for (uint64_t i = 0; i < k; ++i) {
-                    uint32_t r = gc[i];
-                    if (r == a || r == triv1 || r == triv2) continue;
-                    if (strategy == 0 && dep_bt >= 0 && r >= 6ull * V) {
-                        /* literal Condition.isImpliedBy quirk for same-type binary captures:
-                         * ref X is "implied" by dep D when X.v1 == D.v2 (Condition.scala:35-43) */
-                        uint64_t rk = bkeys[r - 6ull * V];
-                        if ((int)(rk >> 62) == dep_bt && (uint32_t)((rk >> 31) & 0x7fffffff) == dv2) continue;
+                uint64_t nref = 0;
+                for (uint64_t j = doff[a]; j < doff[a + 1]; ++j) {
+                    uint64_t g = dgrp[j];
+                    uint64_t k = goff[g + 1] - goff[g];
+                    const uint32_t *gc = gcap + goff[g];
+                    if (j == doff[a]) {
+                        if (k > refs_cap) {
+                            refs_cap = k * 2;
+                            refs = (uint32_t *)realloc(refs, refs_cap * sizeof(uint32_t));
+                            tmp = (uint32_t *)realloc(tmp, refs_cap * sizeof(uint32_t));
+                        }
+                        for (uint64_t i = 0; i < k; ++i) {
+                            uint32_t r = gc[i];
+                            if (r == a || r == triv1 || r == triv2) continue;
+                            if (strategy == 0 && dep_bt >= 0 && r >= 6ull * V) {
+                                /* literal Condition.isImpliedBy quirk for same-type binary captures:
+                                 * ref X is "implied" by dep D when X.v1 == D.v2 (Condition.scala:35-43) */
+                                uint64_t rk = bkeys[r - 6ull * V];
+                                if ((int)(rk >> 62) == dep_bt && (uint32_t)((rk >> 31) & 0x7fffffff) == dv2) continue;
+                            }
+                            refs[nref++] = r;
+                        }
+                    } else {
+                        /* merge-intersect sorted refs with sorted group */
+                        uint64_t x = 0, y = 0, m = 0;
+                        while (x < nref && y < k) {
+                            if (refs[x] < gc[y]) x++;
+                            else if (refs[x] > gc[y]) y++;
+                            else { tmp[m++] = refs[x]; x++; y++; }
+                        }
+                        uint32_t *t = refs; refs = tmp; tmp = t;
+                        nref = m;
                     }
-                    refs[nref++] = r;
+                    if (nref == 0) break;
                 }
-            } else {
-                /* merge-intersect sorted refs with sorted group */
-                uint64_t x = 0, y = 0, m = 0;
-                while (x < nref && y < k) {
-                    if (refs[x] < gc[y]) x++;
-                    else if (refs[x] > gc[y]) y++;
-                    else { tmp[m++] = refs[x]; x++; y++; }
+                for (uint64_t i = 0; i < nref; ++i) {
+                    if (nc == ccap) { ccap *= 2; cind = (orc_cind *)realloc(cind, ccap * sizeof(orc_cind)); }
+                    cind[nc].dep = (uint32_t)a;
+                    cind[nc].ref = refs[i];
+                    cind[nc].support = support[a];
+                    nc++;
                 }
-                uint32_t *t = refs; refs = tmp; tmp = t;
-                nref = m;
             }
-            if (nref == 0) break;
+            cbuf[ch] = cind;
+            ccnt[ch] = nc;
         }
-        for (uint64_t i = 0; i < nref; ++i) {
-            if (nc == ccap) { ccap *= 2; cind = (orc_cind *)realloc(cind, ccap * sizeof(orc_cind)); }
-            cind[nc].dep = (uint32_t)a;
-            cind[nc].ref = refs[i];
-            cind[nc].support = support[a];
-            nc++;
-        }
+        free(refs); free(tmp);
     }
-    free(refs); free(tmp); free(dgrp); free(doff); free(goff); free(gcap); free(support);
+    uint64_t nc = 0;
+    for (uint64_t ch = 0; ch < nchunk; ++ch) { uint64_t c = ccnt[ch]; ccnt[ch] = nc; nc += c; }
+    ccnt[nchunk] = nc;
+    orc_cind *cind = (orc_cind *)xmalloc(nc * sizeof(orc_cind));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (uint64_t ch = 0; ch < nchunk; ++ch) {
+        memcpy(cind + ccnt[ch], cbuf[ch], (ccnt[ch + 1] - ccnt[ch]) * sizeof(orc_cind));
+        free(cbuf[ch]);
+    }
+    free(cbuf); free(ccnt);
+    free(dgrp); free(doff); free(goff); free(gcap); free(support);
     st->n_raw_cinds = nc;
 
     /* 6. minimality (TraversalStrategy.removeImpliedCinds :126-168), rules on the raw sets */
@@ -349,7 +396,8 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
         }
         radix_sort_u64(s11, n11); radix_sort_u64(s12, n12);
         radix_sort_u64(s12c, n12c); radix_sort_u64(s22c, n22c);
-        uint64_t m = 0;
+        uint8_t *keep = (uint8_t *)xmalloc(nc);
+#pragma omp parallel for schedule(static)
         for (uint64_t i = 0; i < nc; ++i) {
             uint64_t d = cind[i].dep, r = cind[i].ref;
             int du = d < U, ru = r < U;
@@ -369,8 +417,12 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
                     drop = bsearch_u64(s12, n12, (c1 << 32) | r) || bsearch_u64(s12, n12, (c2 << 32) | r); /* R4 */
                 }
             }
-            if (!drop) cind[m++] = cind[i];
+            keep[i] = (uint8_t)!drop;
         }
+        uint64_t m = 0;
+        for (uint64_t i = 0; i < nc; ++i)
+            if (keep[i]) cind[m++] = cind[i];
+        free(keep);
         nc = m;
         free(s11); free(s12); free(s12c); free(s22c);
     }
@@ -383,3 +435,6 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
 }
 
 void orc_free(void *ptr) { free(ptr); }
+
+/* threads stages 4-6 use (OMP_NUM_THREADS, else all cores) */
+int orc_threads(void) { return omp_get_max_threads(); }

@@ -62,6 +62,13 @@ def decode_capture(cap, num_terms, bin_keys):
     return BINARY_CODES[key >> 62], (key >> 31) & 0x7FFFFFFF, key & 0x7FFFFFFF
 
 
+def threads():
+    """OpenMP threads the restatement runs on (OMP_NUM_THREADS, else all cores)."""
+    lib = _load()
+    lib.orc_threads.restype = ctypes.c_int
+    return int(lib.orc_threads())
+
+
 def run(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):
     """Returns (set of (dt, dv1, dv2, rt, rv1, rv2, support), stats dict, raw arrays)."""
     lib = _load()
