@@ -165,6 +165,14 @@ def main():
                     "dominant_ms": round(kt[dominant], 4)}
             break
 
+    # BASELINE metric also names "% HBM roofline of count kernels": K1 (unary) and K2 (binary condition counts)
+    count_roof = {}
+    for name, b in (("unary", 12 * d.n), ("binary", 12 * d.n + 12 * fc["n_binary_keys"])):
+        if kt.get(name, 0) > 0:
+            gbs = b / (kt[name] * 1e-3) / 1e9
+            count_roof[name] = {"bytes": int(b), "ms": round(kt[name], 4), "achieved": round(gbs, 1),
+                                "frac": round(gbs / HBM_PEAK_GBS, 4), "bound": "memory-side atomics"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import c_oracle
@@ -187,7 +195,7 @@ def main():
                                    f"scale {args.scale}, support {ms}, strategy 1 --use-fis --clean-implied)",
                        "triples": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
                        "parallelism": f"join-hash shards x{world} (RCCL)" if world > 1 else "single"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "count_kernels": count_roof, "cpu_baseline": cpu,
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],
