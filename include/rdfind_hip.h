@@ -146,6 +146,21 @@ rdf_status rdf_decode_capture(rdf_ctx* ctx, uint32_t capture, uint32_t* code, ui
 rdf_status rdf_binary_key_count(rdf_ctx* ctx, uint64_t* n);
 rdf_status rdf_copy_binary_keys(rdf_ctx* ctx, uint64_t* out, uint64_t cap);
 
+/*
+ * Output formatting on the device (replaces the host-side Cind.toString / TextOutputFormat write,
+ * ALG/data/Cind.scala:29-31 and ALG/programs/RDFind.scala:507-520).  The caller uploads its dictionary once:
+ * term t is heap[offsets[t], offsets[t+1]) (UTF-8 bytes, offsets[n_terms] == heap_bytes).  Lines are
+ * "<dep> < <ref> (support=<n>)\n" with ConditionCodes.prettyPrint captures ("s[p=<term>]",
+ * "o[s=<term>,p=<term>]"), for result rows [offset, offset+count) in result order.
+ */
+rdf_status rdf_set_dictionary(rdf_ctx* ctx, const char* heap, uint64_t heap_bytes, const uint64_t* offsets,
+                              uint64_t n_terms);
+/* Bytes the lines of rows [offset, offset+count) take. */
+rdf_status rdf_format_size(rdf_ctx* ctx, uint64_t offset, uint64_t count, uint64_t* bytes);
+/* Writes those lines to out (host memory, cap bytes); *bytes receives their size.  RDF_ERR_ARG if cap is
+ * smaller (nothing written). */
+rdf_status rdf_format_cinds(rdf_ctx* ctx, uint64_t offset, uint64_t count, char* out, uint64_t cap, uint64_t* bytes);
+
 /* Statistics of the last completed run (single-GPU or sharded). */
 rdf_status rdf_last_stats(rdf_ctx* ctx, rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs);
 

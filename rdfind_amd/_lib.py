@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "rdf_run", "rdf_cind_count", "rdf_copy_cinds", "rdf_decode_capture", "rdf_binary_key_count",
     "rdf_copy_binary_keys", "rdf_stage_times", "rdf_kernel_times", "rdf_sync",
     "rdf_copy_cinds_range", "rdf_cind_checksum", "rdf_last_stats", "rdf_shard_begin", "rdf_shard_step",
-    "rdf_shard_export", "rdf_shard_import",
+    "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
 )
 
 # rdf_exchange ops (sharded mode, include/rdfind_hip.h)
@@ -114,6 +114,9 @@ def load():
         "rdf_sync": (i32, [P]),
         "rdf_copy_cinds_range": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_cind_checksum": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
+        "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
+        "rdf_format_cinds": (i32, [P, u64, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_last_stats": (i32, [P, ctypes.POINTER(FcStats), ctypes.POINTER(GroupStats), ctypes.POINTER(CindStats)]),
         "rdf_shard_begin": (i32, [P, u32, u32, u32, ctypes.c_char_p, u32]),
         "rdf_shard_step": (i32, [P, ctypes.POINTER(Exchange)]),
@@ -283,6 +286,29 @@ class Context:
         if n.value:
             self._check(self.lib.rdf_copy_binary_keys(self.ptr, out.ctypes.data, n.value), "rdf_copy_binary_keys")
         return out
+
+    def set_dictionary(self, terms):
+        """Uploads the dictionary (term id -> string) for device-side formatting."""
+        enc = [t.encode("utf-8") for t in terms]
+        heap = b"".join(enc)
+        offsets = np.zeros(len(enc) + 1, dtype=np.uint64)
+        if enc:
+            np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.uint64, count=len(enc)), out=offsets[1:])
+        buf = ctypes.create_string_buffer(heap, max(len(heap), 1))
+        self._check(self.lib.rdf_set_dictionary(self.ptr, buf, len(heap), offsets.ctypes.data, len(enc)),
+                    "rdf_set_dictionary")
+
+    def format_cinds(self, offset=0, count=None) -> bytes:
+        """Cind.toString lines ("...\n" each) of result rows [offset, offset + count), formatted on the GPU."""
+        if count is None:
+            count = self.cind_count() - offset
+        need = ctypes.c_uint64()
+        self._check(self.lib.rdf_format_size(self.ptr, offset, count, ctypes.byref(need)), "rdf_format_size")
+        out = ctypes.create_string_buffer(max(need.value, 1))
+        got = ctypes.c_uint64()
+        self._check(self.lib.rdf_format_cinds(self.ptr, offset, count, out, need.value, ctypes.byref(got)),
+                    "rdf_format_cinds")
+        return out.raw[: got.value]
 
     def decoded_cinds(self):
         """Structured array with (dep_code, dep_v1, dep_v2, ref_code, ref_v1, ref_v2, support);

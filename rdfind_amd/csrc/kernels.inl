@@ -1244,7 +1244,12 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // counter: an agent-scope release fence writes back the whole L2 of the XCD, per work item.
     if (lane == 0 && (alive0 & ~alive)) atomicOr(&dead[oct0], alive0 & ~alive);
 }
-__global__ __launch_bounds__(RDF_BLOCK) void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+#ifdef RDF_LIGHT_WAVES
+#define RDF_LIGHT_ATTR __attribute__((amdgpu_waves_per_eu(RDF_LIGHT_WAVES)))
+#else
+#define RDF_LIGHT_ATTR
+#endif
+__global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_ATTR void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                      const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
                                                      const u64* __restrict__ choff, u64 W, u64* dead, u64* slots,
                                                      u32* counts) {
@@ -2005,4 +2010,142 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_extract_hmask(const CapInfo* __re
 __global__ __launch_bounds__(RDF_BLOCK) void k_set_hmask(const u64* __restrict__ in, u32 C, CapInfo* info) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) info[d].hmask = in[d];
 }
+// ================================================================================================
+// K8: Cind.toString output (ALG/data/Cind.scala:29-31, ConditionCodes.prettyPrint ALG/util/ConditionCodes.scala:102-107)
+// Byte work: every capture's pretty string ("s[p=<term>]", "o[s=<a>,p=<b>]") is built once per run into a
+// string table (the terms come from the caller's dictionary, uploaded by rdf_set_dictionary); each output
+// line "<dep> < <ref> (support=<n>)\n" is then assembled by one wave per 64 lines, the lanes copying 64 bytes
+// of a line per step (coalesced stores).
+
+// "s[p=" etc.: projection char, '[', first condition char, '=' -- per unary type t (UNARY_CODES order) and
+// binary type bt (BINARY_CODES order); the binary second part is ",o=" / ",o=" / ",p="
+__device__ __constant__ char kUnaryHead[6][4] = {{'s', '[', 'p', '='}, {'s', '[', 'o', '='}, {'p', '[', 's', '='},
+                                                {'p', '[', 'o', '='}, {'o', '[', 's', '='}, {'o', '[', 'p', '='}};
+__device__ __constant__ char kBinaryHead[3][4] = {{'s', '[', 'p', '='}, {'p', '[', 's', '='}, {'o', '[', 's', '='}};
+__device__ __constant__ char kBinaryMid[3][3] = {{',', 'o', '='}, {',', 'o', '='}, {',', 'p', '='}};
+
+struct CapStr {
+    const char* head;  // 4 chars
+    const char* mid;   // 3 chars or null (unary)
+    u32 v1, v2;
+};
+
+__device__ inline CapStr cap_str(u32 ext, u32 V, const u64* __restrict__ bkeys) {
+    CapStr c;
+    if (ext < 6u * V) {
+        const u32 t = ext / V;
+        c.head = kUnaryHead[t];
+        c.mid = nullptr;
+        c.v1 = ext - t * V;
+        c.v2 = 0;
+    } else {
+        const u64 k = bkeys[ext - 6u * V];
+        const u32 bt = bin_key_type(k);
+        c.head = kBinaryHead[bt];
+        c.mid = kBinaryMid[bt];
+        c.v1 = bin_key_v1(k);
+        c.v2 = bin_key_v2(k);
+    }
+    return c;
+}
+
+// length of the pretty string of every compact capture
+__global__ __launch_bounds__(RDF_BLOCK) void k_capstr_len(const u32* __restrict__ fext, u32 C, u32 V,
+                                                          const u64* __restrict__ bkeys, const u64* __restrict__ toff,
+                                                          u32* len) {
+    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < C; c += (u64)gridDim.x * RDF_BLOCK) {
+        const CapStr s = cap_str(fext[c], V, bkeys);
+        u64 n = 4 + (toff[s.v1 + 1] - toff[s.v1]) + 1;
+        if (s.mid) n += 3 + (toff[s.v2 + 1] - toff[s.v2]);
+        len[c] = (u32)n;
+    }
+}
+
+// one wave per capture string
+__global__ __launch_bounds__(RDF_BLOCK) void k_capstr_write(const u32* __restrict__ fext, u32 C, u32 V,
+                                                            const u64* __restrict__ bkeys, const u64* __restrict__ toff,
+                                                            const char* __restrict__ heap, const u64* __restrict__ soff,
+                                                            char* str) {
+    for (u64 c = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE; c < C;
+         c += (u64)gridDim.x * RDF_WAVES_PER_BLOCK) {
+        const CapStr s = cap_str(fext[c], V, bkeys);
+        const u64 a1 = toff[s.v1], n1 = toff[s.v1 + 1] - a1;
+        const u64 a2 = s.mid ? toff[s.v2] : 0, n2 = s.mid ? toff[s.v2 + 1] - a2 : 0;
+        const u64 n = soff[c + 1] - soff[c];
+        char* o = str + soff[c];
+        for (u64 j = lane_id(); j < n; j += RDF_WAVE) {
+            char ch;
+            if (j < 4) ch = s.head[j];
+            else if (j < 4 + n1) ch = heap[a1 + j - 4];
+            else if (!s.mid) ch = ']';
+            else if (j < 7 + n1) ch = s.mid[j - 4 - n1];
+            else if (j < 7 + n1 + n2) ch = heap[a2 + j - 7 - n1];
+            else ch = ']';
+            o[j] = ch;
+        }
+    }
+}
+
+__device__ inline u32 dec_digits(u32 x) {
+    u32 n = 1;
+    while (x >= 10) {
+        x /= 10;
+        ++n;
+    }
+    return n;
+}
+
+// line length of every CIND in [first, first + n)
+__global__ __launch_bounds__(RDF_BLOCK) void k_fmt_len(const u32* __restrict__ refs, u64 first, u64 n,
+                                                       const u64* __restrict__ runoff, const u32* __restrict__ rundep,
+                                                       u64 R, const u64* __restrict__ soff,
+                                                       const u32* __restrict__ csup, u32* len) {
+    for (u64 k = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; k < n; k += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 i = first + k;
+        const u32 d = rundep[run_of(runoff, 0, R - 1, i)], r = refs[i];
+        // "<dep> < <ref> (support=<n>)\n"
+        len[k] = (u32)((soff[d + 1] - soff[d]) + 3 + (soff[r + 1] - soff[r]) + 10 + dec_digits(csup[d]) + 2);
+    }
+}
+
+// lines at loff (exclusive scan of k_fmt_len); one wave per 64 consecutive lines
+__global__ __launch_bounds__(RDF_BLOCK) void k_fmt_write(const u32* __restrict__ refs, u64 first, u64 n,
+                                                         const u64* __restrict__ runoff, const u32* __restrict__ rundep,
+                                                         u64 R, const u64* __restrict__ soff, const char* __restrict__ str,
+                                                         const u32* __restrict__ csup, const u64* __restrict__ loff,
+                                                         char* out) {
+    const int lane = lane_id();
+    for (u64 base = ((u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE) * RDF_WAVE; base < n;
+         base += (u64)gridDim.x * RDF_WAVES_PER_BLOCK * RDF_WAVE) {
+        // lane j looks up line base + j, then the wave writes the lines one after another
+        u32 my_d = 0, my_r = 0;
+        if (base + lane < n) {
+            const u64 i = first + base + lane;
+            my_d = rundep[run_of(runoff, 0, R - 1, i)];
+            my_r = refs[i];
+        }
+        const u64 lines = n - base < RDF_WAVE ? n - base : RDF_WAVE;
+        for (u64 l = 0; l < lines; ++l) {
+            const u32 d = __shfl(my_d, (int)l, RDF_WAVE), r = __shfl(my_r, (int)l, RDF_WAVE);
+            const u64 da = soff[d], dn = soff[d + 1] - da, ra = soff[r], rn = soff[r + 1] - ra;
+            const u32 sup = csup[d], nd = dec_digits(sup);
+            const u64 o0 = loff[base + l], len = dn + 3 + rn + 10 + nd + 2;
+            for (u64 j = lane; j < len; j += RDF_WAVE) {
+                char ch;
+                if (j < dn) ch = str[da + j];
+                else if (j < dn + 3) ch = " < "[j - dn];
+                else if (j < dn + 3 + rn) ch = str[ra + j - dn - 3];
+                else if (j < dn + 13 + rn) ch = " (support="[j - dn - 3 - rn];
+                else if (j < dn + 13 + rn + nd) {
+                    u32 x = sup;
+                    for (u64 q = dn + 13 + rn + nd - 1 - j; q > 0; --q) x /= 10;  // digit j of sup
+                    ch = (char)('0' + x % 10);
+                } else if (j == len - 2) ch = ')';
+                else ch = '\n';
+                out[o0 + j] = ch;
+            }
+        }
+    }
+}
+
 }  // namespace rdf

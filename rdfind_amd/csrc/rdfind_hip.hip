@@ -57,6 +57,8 @@ struct rdf_ctx {
 
     // cinds
     DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, hbits, cbits, hown, cown, sbase, dcls, crep, out, stage_rows;
+    DevBuf dheap, dtoff, cslen, csoff, cstr, flen, floff, fbuf;  // output formatting (K8)
+    u64 dict_terms = 0, run_id = 0, capstr_run = ~0ull;
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
@@ -268,7 +270,8 @@ void rdf_ctx_destroy(rdf_ctx* c) {
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->upairs, &c->usoff, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
-                      &c->obounds, &c->runoff, &c->rundep};
+                      &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
+                      &c->cstr, &c->flen, &c->floff, &c->fbuf};
     for (DevBuf* b : bufs) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -1149,6 +1152,7 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
                        c->cobase.as<u64>(), H, K + H + HC, c->runoff.as<u64>(), c->rundep.as<u32>());
     c->n_runs = R;
     c->h_runs_valid = false;
+    ++c->run_id;
     HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(st));
@@ -1663,6 +1667,90 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     rdf_status rs = read_u64(c, dscal(c, 7), &v);
     *checksum = v;
     return rs;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Output formatting (K8): Cind.toString lines on the device from the caller's dictionary
+
+rdf_status rdf_set_dictionary(rdf_ctx* c, const char* heap, uint64_t heap_bytes, const uint64_t* offsets,
+                              uint64_t n_terms) {
+    if (!c || (heap_bytes && !heap) || !offsets) return RDF_ERR_ARG;
+    if (offsets[n_terms] != heap_bytes) return fail(c, RDF_ERR_ARG, "offsets[n_terms] must equal heap_bytes");
+    HIP_TRY(c, hipSetDevice(c->device));
+    ENSURE(c, dheap, std::max<u64>(heap_bytes, 1));
+    ENSURE(c, dtoff, (n_terms + 1) * 8);
+    if (heap_bytes) HIP_TRY(c, hipMemcpy(c->dheap.p, heap, heap_bytes, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->dtoff.p, offsets, (n_terms + 1) * 8, hipMemcpyHostToDevice));
+    c->dict_terms = n_terms;
+    c->capstr_run = ~0ull;
+    return RDF_OK;
+}
+
+// pretty strings of the run's compact captures (built once per run)
+static rdf_status ensure_capstr(rdf_ctx* c) {
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    if (c->dict_terms < c->V) return fail(c, RDF_ERR_STATE, "rdf_set_dictionary must cover every term id");
+    if (c->capstr_run == c->run_id) return RDF_OK;
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    ENSURE(c, cslen, std::max<u64>(C, 1) * 4);
+    ENSURE(c, csoff, (C + 1ull) * 8);
+    if (C)
+        hipLaunchKernelGGL(k_capstr_len, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fext.as<u32>(), C,
+                           c->V, c->bkeys.as<u64>(), c->dtoff.as<u64>(), c->cslen.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->cslen.as<u32>(), c->csoff.as<u64>(), C, c->csoff.as<u64>() + C, st));
+    u64 total = 0;
+    TRY(read_u64(c, c->csoff.as<u64>() + C, &total));
+    ENSURE(c, cstr, std::max<u64>(total, 1));
+    if (C)
+        hipLaunchKernelGGL(k_capstr_write, dim3(grid_for(C, RDF_WAVES_PER_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->fext.as<u32>(), C, c->V, c->bkeys.as<u64>(), c->dtoff.as<u64>(), c->dheap.as<char>(),
+                           c->csoff.as<u64>(), c->cstr.as<char>());
+    c->capstr_run = c->run_id;
+    return RDF_OK;
+}
+
+// line offsets of result rows [offset, offset + m) -> floff, *bytes
+static rdf_status fmt_prepare(rdf_ctx* c, u64 offset, u64 m, u64* bytes) {
+    hipStream_t st = c->stream;
+    TRY(ensure_capstr(c));
+    ENSURE(c, flen, std::max<u64>(m, 1) * 4);
+    ENSURE(c, floff, (m + 1) * 8);
+    if (m)
+        hipLaunchKernelGGL(k_fmt_len, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->out_ptr, offset, m,
+                           c->runoff.as<u64>(), c->rundep.as<u32>(), c->n_runs, c->csoff.as<u64>(), c->csup.as<u32>(),
+                           c->flen.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flen.as<u32>(), c->floff.as<u64>(), m, c->floff.as<u64>() + m, st));
+    return read_u64(c, c->floff.as<u64>() + m, bytes);
+}
+
+rdf_status rdf_format_size(rdf_ctx* c, uint64_t offset, uint64_t count, uint64_t* bytes) {
+    if (!c || !bytes) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
+    return fmt_prepare(c, offset, m, (u64*)bytes);
+}
+
+rdf_status rdf_format_cinds(rdf_ctx* c, uint64_t offset, uint64_t count, char* out, uint64_t cap, uint64_t* bytes) {
+    if (!c || !bytes || (cap && !out)) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
+    u64 total = 0;
+    TRY(fmt_prepare(c, offset, m, &total));
+    *bytes = total;
+    if (total > cap) return fail(c, RDF_ERR_ARG, "output buffer too small (see *bytes)");
+    ENSURE(c, fbuf, std::max<u64>(total, 1));
+    if (m)
+        hipLaunchKernelGGL(k_fmt_write, dim3(grid_for((m + RDF_WAVE - 1) / RDF_WAVE, RDF_WAVES_PER_BLOCK, kGrid)),
+                           dim3(RDF_BLOCK), 0, c->stream, c->out_ptr, offset, m, c->runoff.as<u64>(), c->rundep.as<u32>(),
+                           c->n_runs, c->csoff.as<u64>(), c->cstr.as<char>(), c->csup.as<u32>(), c->floff.as<u64>(),
+                           c->fbuf.as<char>());
+    HIP_TRY(c, hipGetLastError());
+    if (total) HIP_TRY(c, hipMemcpyAsync(out, c->fbuf.p, total, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RDF_OK;
 }
 
 rdf_status rdf_decode_capture(rdf_ctx* c, uint32_t capture, uint32_t* code, uint32_t* value1, uint32_t* value2) {

@@ -29,6 +29,9 @@ _RESULT_NEUTRAL = {
     "--configuration": str, "--wait": None, "--flink-verbose": None, "-jar": str, "-rex": str,
 }
 # flags whose semantics this build does not implement (SURVEY.md 8f "next" rows or out of scope)
+FORMAT_CHUNK = 1 << 23     # result rows formatted per device call
+KEEP_LINES_MAX = 1 << 24   # run() returns the lines as a list up to this many CINDs (None above)
+
 _UNSUPPORTED = ["--use-ars", "--ar-output", "--prefixes", "--asciify-triples", "--apply-hash", "--hash-dictionary",
                 "--hash-function", "--hash-bytes", "--any-binary-captures", "--find-frequent-captures",
                 "--explicit-threshold", "--sbf-bytes", "--balanced-overlap-candidates"]
@@ -111,34 +114,46 @@ class RDFind:
             ctx.sync()
             self.timings["discover"] = time.time() - t1
             self.timings["device_ms"] = ctx.stage_times()
-            rows = ctx.decoded_cinds()
-        self.stats = {"fc": fc, "groups": gs, "cinds": cs}
-        t2 = time.time()
-        lines = format_rows(rows, dic.term)
-        self.timings["format"] = time.time() - t2
+            self.stats = {"fc": fc, "groups": gs, "cinds": cs}
+            # Cind.toString lines are formatted on the GPU (rdf_format_cinds) in chunks of rows
+            t2 = time.time()
+            n = ctx.cind_count()
+            ctx.set_dictionary(dic.terms)
+            keep_lines = n <= KEEP_LINES_MAX or a.collect_result or a.debug_level >= 3
+            lines = [] if keep_lines else None
+            f = None
+            if a.output:
+                path = a.output[5:] if a.output.startswith("file:") else a.output
+                while path.startswith("//"):
+                    path = path[1:]
+                os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+                f = open(path, "wb")
+            try:
+                for off in range(0, n, FORMAT_CHUNK):
+                    text = ctx.format_cinds(off, FORMAT_CHUNK)
+                    if f is not None:
+                        f.write(text)
+                    if keep_lines:
+                        lines.extend(text.decode("utf-8").splitlines())
+            finally:
+                if f is not None:
+                    f.close()
+            self.timings["format"] = time.time() - t2
         if a.debug_level >= 1:
-            self.log(f"Found {len(lines)} CINDs in total.")
+            self.log(f"Found {n} CINDs in total.")
         if a.output:
-            path = a.output[5:] if a.output.startswith("file:") else a.output
-            while path.startswith("//"):
-                path = path[1:]
-            d = os.path.dirname(os.path.abspath(path))
-            os.makedirs(d, exist_ok=True)
-            with open(path, "w", encoding="utf-8") as f:
-                for ln in lines:
-                    f.write(ln)
-                    f.write("\n")
             self.log(f"Outputting CINDs to {os.path.abspath(path)}.")
         if a.collect_result or a.debug_level >= 3:
             for ln in lines:
                 print(ln, file=out)
         if not a.output and not a.collect_result:
-            print(f"Detected {len(lines)} CINDs.", file=out)
+            print(f"Detected {n} CINDs.", file=out)
         return lines
 
 
 def format_rows(rows, term):
-    """``Cind.toString`` for decoded rows (ALG/data/Cind.scala:29-31)."""
+    """``Cind.toString`` for decoded rows (ALG/data/Cind.scala:29-31), on the host: the reference formatting the
+    device formatter (rdf_format_cinds) is tested against."""
     none = 0xFFFFFFFF
     out = []
     for dc, d1, d2, rc, r1, r2, sup in rows.tolist():

@@ -234,3 +234,39 @@ def test_large_grids_two_paths(monkeypatch):
         finally:
             g.close()
     assert got[0] == got[1] and got[0][0] > 2 ** 32
+
+
+def test_device_formatting_matches_host(ctx):
+    """rdf_format_cinds (K8) writes exactly the host Cind.toString lines (program.format_rows), in result order,
+    for any row range; terms with multi-byte UTF-8, empty and long strings."""
+    rng = random.Random(7)
+    for it in range(20):
+        n = rng.randrange(30, 400)
+        nv = rng.randrange(4, 40)
+        ms = rng.randrange(1, 4)
+        arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                       dtype=np.uint32)
+        terms = [rng.choice(["<http://ex.org/e%d>" % i, '"l%d"' % i, "été-%d" % i, "", "x" * rng.randrange(1, 300)])
+                 for i in range(nv)]
+        strategy, clean = MODES[it % 4]
+        ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+        ctx.run(ms, "spo", clean, strategy)
+        ctx.set_dictionary(terms)
+        rows = ctx.decoded_cinds()
+        expected = program.format_rows(rows, terms.__getitem__)
+        text = ctx.format_cinds()
+        assert text.decode("utf-8").split("\n")[:-1] == expected if expected else text == b""
+        total = len(rows)
+        if total > 3:
+            a, b = total // 3, 2 * total // 3
+            parts = ctx.format_cinds(0, a) + ctx.format_cinds(a, b - a) + ctx.format_cinds(b, total)
+            assert parts == text
+    d = synth.config("c2", 0.05)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support)
+    terms = ["<http://www.Department%d.University%d.edu/t%d>" % (i % 15, i % 7, i) for i in range(d.num_terms)]
+    ctx.set_dictionary(terms)
+    n = ctx.cind_count()
+    rows = ctx.copy_cinds_range(n // 2, 20000)
+    dec = _lib.decode_rows(rows, d.num_terms, ctx.binary_keys())
+    assert ctx.format_cinds(n // 2, 20000).decode().split("\n")[:-1] == program.format_rows(dec, terms.__getitem__)
