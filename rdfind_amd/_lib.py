@@ -298,17 +298,22 @@ class Context:
         self._check(self.lib.rdf_set_dictionary(self.ptr, buf, len(heap), offsets.ctypes.data, len(enc)),
                     "rdf_set_dictionary")
 
-    def format_cinds(self, offset=0, count=None) -> bytes:
-        """Cind.toString lines ("...\n" each) of result rows [offset, offset + count), formatted on the GPU."""
+    def format_array(self, offset=0, count=None) -> np.ndarray:
+        """Cind.toString lines ("...\n" each) of result rows [offset, offset + count), formatted on the GPU, as a
+        uint8 array (no intermediate copies: write it to a file with ``arr.tofile`` / ``f.write(arr)``)."""
         if count is None:
             count = self.cind_count() - offset
         need = ctypes.c_uint64()
         self._check(self.lib.rdf_format_size(self.ptr, offset, count, ctypes.byref(need)), "rdf_format_size")
-        out = ctypes.create_string_buffer(max(need.value, 1))
+        out = np.empty(max(need.value, 1), dtype=np.uint8)
         got = ctypes.c_uint64()
-        self._check(self.lib.rdf_format_cinds(self.ptr, offset, count, out, need.value, ctypes.byref(got)),
+        self._check(self.lib.rdf_format_cinds(self.ptr, offset, count, out.ctypes.data, need.value, ctypes.byref(got)),
                     "rdf_format_cinds")
-        return out.raw[: got.value]
+        return out[: got.value]
+
+    def format_cinds(self, offset=0, count=None) -> bytes:
+        """As format_array, as bytes."""
+        return self.format_array(offset, count).tobytes()
 
     def decoded_cinds(self):
         """Structured array with (dep_code, dep_v1, dep_v2, ref_code, ref_v1, ref_v2, support);

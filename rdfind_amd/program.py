@@ -130,11 +130,11 @@ class RDFind:
                 f = open(path, "wb")
             try:
                 for off in range(0, n, FORMAT_CHUNK):
-                    text = ctx.format_cinds(off, FORMAT_CHUNK)
+                    text = ctx.format_array(off, FORMAT_CHUNK)
                     if f is not None:
-                        f.write(text)
+                        f.write(memoryview(text))
                     if keep_lines:
-                        lines.extend(text.decode("utf-8").splitlines())
+                        lines.extend(text.tobytes().decode("utf-8").splitlines())
             finally:
                 if f is not None:
                     f.close()
