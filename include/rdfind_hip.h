@@ -120,6 +120,14 @@ rdf_status rdf_set_triples(rdf_ctx* ctx, const uint32_t* s, const uint32_t* p, c
 rdf_status rdf_set_triples_device(rdf_ctx* ctx, const uint32_t* d_s, const uint32_t* d_p, const uint32_t* d_o,
                                   uint64_t n, uint32_t num_terms);
 
+/* --distinct-triples: `triples.distinct` (ALG/programs/RDFind.scala:284-287) on the resident triples, in HBM.
+ * Keeps the first occurrence of every triple in input order; *n_distinct receives the new count and *ms
+ * (optional) the device time.  The compacted triples are context-owned from then on. */
+rdf_status rdf_distinct_triples(rdf_ctx* ctx, uint64_t* n_distinct, float* ms);
+
+/* Copies min(cap, n) resident triples to host arrays (e.g. after rdf_distinct_triples). */
+rdf_status rdf_copy_triples(rdf_ctx* ctx, uint32_t* s, uint32_t* p, uint32_t* o, uint64_t cap, uint64_t* n_copied);
+
 rdf_status rdf_frequent_conditions(rdf_ctx* ctx, uint32_t min_support, rdf_fc_stats* stats);
 /* projection: any combination of 's', 'p', 'o' (--projection, default "spo"). */
 rdf_status rdf_build_capture_groups(rdf_ctx* ctx, const char* projection, rdf_group_stats* stats);

@@ -695,3 +695,49 @@ def s2l_exact_raw(cinds_v):
         if (t1, a) not in t and (t2, b) not in t:
             out.append(c)
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Input-side options
+
+def distinct_triples(s, p, o):
+    """``triples.distinct`` (ALG/programs/RDFind.scala:284-287): every triple once.  Flink's distinct
+    defines a set; this checker keeps first occurrences in input order (the GPU path's documented order)."""
+    import numpy as np
+    seen = set()
+    keep = []
+    for i, t in enumerate(zip(s.tolist(), p.tolist(), o.tolist())):
+        if t not in seen:
+            seen.add(t)
+            keep.append(i)
+    idx = np.array(keep, dtype=np.int64)
+    return s[idx], p[idx], o[idx]
+
+
+def parse_prefix_line(line):
+    """ParseRdfPrefixes.map (ALG/operators/ParseRdfPrefixes.scala:14-26): ``@prefix p: <url> .`` or
+    ``@prefix <url> .`` (prefix ""); anything else raises."""
+    import re
+    m = re.fullmatch(r"@prefix\s+(\S+): <(\S+)>\s*\.\n?", line)
+    if m:
+        return m.group(1), m.group(2)
+    m = re.fullmatch(r"@prefix\s+<(\S+)>\s*\.\n?", line)
+    if m:
+        return "", m.group(1)
+    raise ValueError(f"Could not parse the line {line!r} correctly.")
+
+
+def shorten_term(term, prefixes):
+    """ShortenUrls.shorten (ALG/operators/ShortenUrls.scala:36-44) with the trie of PrefixTrieCreator
+    (:55-60): key ``<url``, value ``prefix:``; the LONGEST key that is a prefix of the term wins
+    (StringTrie.getKeyAndValue, ALG/util/StringTrie.scala:44-54), by a linear scan here."""
+    if not term.endswith(">"):
+        return term
+    best = None
+    for prefix, url in prefixes:
+        key = "<" + url
+        if term.startswith(key) and (best is None or len(key) > len(best[0])):
+            best = (key, prefix + ":")
+    if best is None:
+        return term
+    return best[1] + term[len(best[0]):len(term) - 1]

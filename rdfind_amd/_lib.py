@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_binary_keys", "rdf_stage_times", "rdf_kernel_times", "rdf_sync",
     "rdf_copy_cinds_range", "rdf_cind_checksum", "rdf_last_stats", "rdf_shard_begin", "rdf_shard_step",
     "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
+    "rdf_distinct_triples", "rdf_copy_triples",
 )
 
 # rdf_exchange ops (sharded mode, include/rdfind_hip.h)
@@ -99,6 +100,8 @@ def load():
         "rdf_version": (ctypes.c_char_p, []),
         "rdf_set_triples": (i32, [P, P, P, P, u64, u32]),
         "rdf_set_triples_device": (i32, [P, P, P, P, u64, u32]),
+        "rdf_distinct_triples": (i32, [P, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_float)]),
+        "rdf_copy_triples": (i32, [P, P, P, P, u64, ctypes.POINTER(u64)]),
         "rdf_frequent_conditions": (i32, [P, u32, ctypes.POINTER(FcStats)]),
         "rdf_build_capture_groups": (i32, [P, ctypes.c_char_p, ctypes.POINTER(GroupStats)]),
         "rdf_discover_cinds": (i32, [P, u32, ctypes.POINTER(CindStats)]),
@@ -188,6 +191,22 @@ class Context:
         self._check(self.lib.rdf_set_triples_device(self.ptr, s_ptr, p_ptr, o_ptr, n, num_terms),
                     "rdf_set_triples_device")
         self.num_terms = num_terms
+
+    def distinct_triples(self):
+        """--distinct-triples on the resident triples (RDFind.scala:284-287); returns (kept, device ms)."""
+        n = ctypes.c_uint64()
+        ms = ctypes.c_float()
+        self._check(self.lib.rdf_distinct_triples(self.ptr, ctypes.byref(n), ctypes.byref(ms)),
+                    "rdf_distinct_triples")
+        return int(n.value), float(ms.value)
+
+    def copy_triples(self, n: int):
+        """The resident triples as three uint32 arrays (the first n of them)."""
+        s, p, o = (np.empty(n, np.uint32) for _ in range(3))
+        got = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_triples(self.ptr, s.ctypes.data, p.ctypes.data, o.ctypes.data, n,
+                                              ctypes.byref(got)), "rdf_copy_triples")
+        return s[:got.value], p[:got.value], o[:got.value]
 
     def frequent_conditions(self, min_support: int):
         st = FcStats()

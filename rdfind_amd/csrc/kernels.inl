@@ -2149,3 +2149,70 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_fmt_write(const u32* __restrict__
 }
 
 }  // namespace rdf
+
+namespace rdf {
+
+// ================================================================================================
+// Distinct triples (--distinct-triples: `triples.distinct`, ALG/programs/RDFind.scala:284-287).
+// One open-addressing table of triple indices (load <= 1/2).  A slot is claimed once by CAS and only ever
+// lowered afterwards (atomicMin) to another index of an equal triple, so it ends holding the FIRST
+// occurrence; the keep pass marks exactly the triples that are their slot's value.  Survivors keep their
+// input order (the result as a set is what the reference's distinct defines).
+
+__device__ inline u64 triple_slot(u32 a, u32 b, u32 c, u64 mask) {
+    return mix64((((u64)a << 32) | b) ^ mix64((u64)c + 0x9E3779B97F4A7C15ull)) & mask;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_distinct_insert(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                               const u32* __restrict__ o, u64 n, u32* table, u64 mask) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 a = s[i], b = p[i], c = o[i];
+        u64 h = triple_slot(a, b, c, mask);
+        for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+            u32 cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == EMPTY32) {
+                cur = atomicCAS(&table[h], EMPTY32, (u32)i);
+                if (cur == EMPTY32) break;
+            }
+            if (s[cur] == a && p[cur] == b && o[cur] == c) {
+                if (cur > (u32)i) atomicMin(&table[h], (u32)i);
+                break;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_distinct_keep(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                             const u32* __restrict__ o, u64 n,
+                                                             const u32* __restrict__ table, u64 mask, u32* keep) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 a = s[i], b = p[i], c = o[i];
+        u64 h = triple_slot(a, b, c, mask);
+        u32 k = 1;
+        for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+            const u32 cur = table[h];
+            if (cur == EMPTY32) break;  // unreachable: every triple's chain ends at its own slot
+            if (s[cur] == a && p[cur] == b && o[cur] == c) {
+                k = cur == (u32)i;
+                break;
+            }
+        }
+        keep[i] = k;
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_distinct_scatter(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                                const u32* __restrict__ o, u64 n,
+                                                                const u32* __restrict__ keep,
+                                                                const u32* __restrict__ pos, u32* ds, u32* dp, u32* dq) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        if (keep[i]) {
+            const u32 j = pos[i];
+            ds[j] = s[i];
+            dp[j] = p[i];
+            dq[j] = o[i];
+        }
+    }
+}
+
+}  // namespace rdf

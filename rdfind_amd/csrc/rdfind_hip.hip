@@ -29,6 +29,7 @@ struct rdf_ctx {
 
     // triples
     DevBuf ts, tp, to;
+    DevBuf dtab, dkeep, dpos, xs, xp, xo;  // --distinct-triples: slot table, keep flags, positions, compacted copy
     const u32 *s = nullptr, *p = nullptr, *o = nullptr;
     u64 n = 0;
     u32 V = 0;
@@ -332,6 +333,72 @@ rdf_status rdf_set_triples_device(rdf_ctx* c, const uint32_t* s, const uint32_t*
     c->n = n;
     c->V = num_terms;
     c->stage = 1;
+    return RDF_OK;
+}
+
+// --distinct-triples (`triples.distinct`, ALG/programs/RDFind.scala:284-287): removes duplicate triples
+// from the resident input in HBM (first occurrences kept, input order preserved).  The compacted triples
+// are context-owned afterwards, also after rdf_set_triples_device.
+rdf_status rdf_distinct_triples(rdf_ctx* c, uint64_t* n_distinct, float* ms) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    HIP_TRY(c, hipEventRecord(c->ev[6], st));
+    u64 kept = 0;
+    if (n) {
+        const u64 T = next_pow2(2 * n);
+        ENSURE(c, dtab, T * 4);
+        ENSURE(c, dkeep, n * 4);
+        ENSURE(c, dpos, n * 4);
+        ENSURE(c, xs, n * 4);
+        ENSURE(c, xp, n * 4);
+        ENSURE(c, xo, n * 4);
+        HIP_TRY(c, hipMemsetAsync(c->dtab.p, 0xff, T * 4, st));
+        const unsigned g = grid_for(n, RDF_BLOCK, kGrid);
+        hipLaunchKernelGGL(k_distinct_insert, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dtab.as<u32>(), T - 1);
+        hipLaunchKernelGGL(k_distinct_keep, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dtab.as<u32>(), T - 1,
+                           c->dkeep.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->dkeep.as<u32>(), c->dpos.as<u32>(), n, (u32*)dscal(c, 7), st));
+        hipLaunchKernelGGL(k_distinct_scatter, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dkeep.as<u32>(),
+                           c->dpos.as<u32>(), c->xs.as<u32>(), c->xp.as<u32>(), c->xo.as<u32>());
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipMemsetAsync((char*)dscal(c, 7) + 4, 0, 4, st));
+        HIP_TRY(c, hipEventRecord(c->ev[7], st));
+        rdf_status rs = read_u64(c, dscal(c, 7), &kept);
+        if (rs) return rs;
+        std::swap(c->ts, c->xs);
+        std::swap(c->tp, c->xp);
+        std::swap(c->to, c->xo);
+        c->s = c->ts.as<u32>();
+        c->p = c->tp.as<u32>();
+        c->o = c->to.as<u32>();
+    } else {
+        HIP_TRY(c, hipEventRecord(c->ev[7], st));
+        HIP_TRY(c, hipStreamSynchronize(st));
+    }
+    if (ms) HIP_TRY(c, hipEventElapsedTime(ms, c->ev[6], c->ev[7]));
+    c->n = kept;
+    c->stage = 1;
+    if (n_distinct) *n_distinct = kept;
+    return RDF_OK;
+}
+
+// Copies the resident triples (after rdf_distinct_triples: the compacted ones) to host arrays.
+rdf_status rdf_copy_triples(rdf_ctx* c, uint32_t* s, uint32_t* p, uint32_t* o, uint64_t cap, uint64_t* n_copied) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    const u64 n = std::min<u64>(cap, c->n);
+    if (n && (!s || !p || !o)) return fail(c, RDF_ERR_ARG, "null triple arrays");
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(s, c->s, n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(p, c->p, n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(o, c->o, n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (n_copied) *n_copied = n;
     return RDF_OK;
 }
 

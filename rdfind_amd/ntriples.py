@@ -17,6 +17,7 @@ from __future__ import annotations
 import gzip
 import io
 import os
+import re
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -168,3 +169,73 @@ def write_ntriples(path: str, lines):
         for ln in lines:
             f.write(ln)
             f.write("\n")
+
+
+# ------------------------------------------------------------------------------------------------
+# --prefixes: URL shortening (ALG/programs/RDFind.scala:243-267, ALG/operators/ShortenUrls.scala:16-61)
+
+_PREFIX_RE = re.compile(r"@prefix\s+(\S+): <(\S+)>\s*\.\n?")
+_BASE_RE = re.compile(r"@prefix\s+<(\S+)>\s*\.\n?")
+
+def parse_prefix_line(line: str):
+    """ParseRdfPrefixes.map (ALG/operators/ParseRdfPrefixes.scala:14-26): ``@prefix p: <url> .`` gives
+    (p, url), ``@prefix <url> .`` gives ("", url); any other line is an error."""
+    m = _PREFIX_RE.fullmatch(line)
+    if m:
+        return m.group(1), m.group(2)
+    m = _BASE_RE.fullmatch(line)
+    if m:
+        return "", m.group(1)
+    raise ValueError(f"Could not parse the line {line!r} correctly.")
+
+
+def read_prefixes(paths):
+    """Prefix files -> [(prefix, url)]; lines starting with '#' are comments (RDFind.scala:256-258)."""
+    out = []
+    for path in resolve_paths(paths):
+        with _open(path) as f:
+            for line in f.read().splitlines():
+                if line.startswith("#"):
+                    continue
+                out.append(parse_prefix_line(line))
+    return out
+
+
+class PrefixTable:
+    """The prefix trie of ShortenUrls.PrefixTrieCreator (ALG/operators/ShortenUrls.scala:55-60):
+    key ``<url`` -> value ``prefix:``, longest matching key wins (StringTrie.getKeyAndValue,
+    ALG/util/StringTrie.scala:44-54).  Held as one hash set per key length, probed longest first."""
+
+    def __init__(self, prefixes):
+        self.by_len = {}
+        for prefix, url in prefixes:
+            key = "<" + url
+            tab = self.by_len.setdefault(len(key), {})
+            if key in tab:  # StringTrie.+= (StringTrie.scala:36-38)
+                raise ValueError(f"Key already exists: {key}.")
+            tab[key] = prefix + ":"
+        self.lengths = sorted(self.by_len, reverse=True)
+
+    def shorten(self, term: str) -> str:
+        """ShortenUrls.shorten (ShortenUrls.scala:36-44)."""
+        if not term.endswith(">"):
+            return term
+        for n in self.lengths:
+            if n <= len(term):
+                v = self.by_len[n].get(term[:n])
+                if v is not None:
+                    if n > len(term) - 1:  # String.substring(n, len-1) with n > len-1 throws in the JVM
+                        raise ValueError(f"prefix key {term[:n]!r} covers the whole term {term!r}")
+                    return v + term[n:len(term) - 1]
+        return term
+
+
+def shorten_dictionary(s, p, o, dictionary: Dictionary, prefixes):
+    """Applies the URL shortening to every distinct term once (not to every triple, as the reference's
+    per-triple map does) and re-encodes: terms that shorten to the same string share one id afterwards,
+    exactly as they would have after a per-triple map followed by dictionary encoding."""
+    table = PrefixTable(prefixes)
+    short = Dictionary()
+    remap = np.fromiter((short.encode(table.shorten(t)) for t in dictionary.terms), dtype=np.uint32,
+                        count=dictionary.size)
+    return remap[s], remap[p], remap[o], short

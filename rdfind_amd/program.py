@@ -32,7 +32,7 @@ _RESULT_NEUTRAL = {
 FORMAT_CHUNK = 1 << 23     # result rows formatted per device call
 KEEP_LINES_MAX = 1 << 24   # run() returns the lines as a list up to this many CINDs (None above)
 
-_UNSUPPORTED = ["--use-ars", "--ar-output", "--prefixes", "--asciify-triples", "--apply-hash", "--hash-dictionary",
+_UNSUPPORTED = ["--use-ars", "--ar-output", "--asciify-triples", "--apply-hash", "--hash-dictionary",
                 "--hash-function", "--hash-bytes", "--any-binary-captures", "--find-frequent-captures",
                 "--explicit-threshold", "--sbf-bytes", "--balanced-overlap-candidates"]
 
@@ -48,6 +48,8 @@ def build_parser():
     ap.add_argument("--projection", default="spo", help="what shall be used as projection for captures")
     ap.add_argument("--distinct-triples", action="store_true", help="whether to ensure that triples are distinct")
     ap.add_argument("--tabs", action="store_true", help="if input file is tab-separated")
+    ap.add_argument("--prefixes", action="append", default=None,
+                    help="a list of nt-prefix files to apply on the input triple (repeatable or comma-separated)")
     ap.add_argument("--collect-result", action="store_true", help="whether to collect the results locally")
     ap.add_argument("--debug-level", type=int, default=0, help="0: no debug prints, 1: some, ...")
     ap.add_argument("--find-only-fcs", type=int, default=0)
@@ -92,15 +94,19 @@ class RDFind:
         if not paths:
             raise ValueError("no input files")
         s, p, o, dic = ntriples.read_triples(paths, tabs=a.tabs)
-        if a.distinct_triples:
-            key = np.unique(np.stack([s, p, o], axis=1), axis=0)
-            s, p, o = key[:, 0].copy(), key[:, 1].copy(), key[:, 2].copy()
+        if a.prefixes:  # Shorten URLs (RDFind.scala:243-267), once per distinct term
+            files = [x for arg in a.prefixes for x in arg.split(",") if x]
+            s, p, o, dic = ntriples.shorten_dictionary(s, p, o, dic, ntriples.read_prefixes(files))
         self.timings["read"] = time.time() - t0
         if a.only_read:
             return []
         t1 = time.time()
         with _lib.Context(a.device) as ctx:
             ctx.set_triples(s, p, o, dic.size)
+            if a.distinct_triples:  # Remove duplicate triples (RDFind.scala:284-287), in HBM
+                n_distinct, _ = ctx.distinct_triples()
+                if a.debug_level >= 1:
+                    self.log(f"{n_distinct} distinct triples of {s.shape[0]}.")
             fc = ctx.frequent_conditions(a.support)
             if a.debug_level >= 1:
                 self.log(f"Found {sum(fc['n_frequent_unary'])} frequent single-conditions.")

@@ -270,3 +270,48 @@ def test_device_formatting_matches_host(ctx):
     rows = ctx.copy_cinds_range(n // 2, 20000)
     dec = _lib.decode_rows(rows, d.num_terms, ctx.binary_keys())
     assert ctx.format_cinds(n // 2, 20000).decode().split("\n")[:-1] == program.format_rows(dec, terms.__getitem__)
+
+
+@pytest.mark.parametrize("n,nv", [(0, 1), (1, 3), (1000, 4), (200_000, 40), (300_000, 3000), (100_000, 1)])
+def test_distinct_triples_kernel(ctx, n, nv):
+    """rdf_distinct_triples (RDFind.scala:284-287) keeps exactly the first occurrence of every triple, in
+    input order (bit-exact vs the oracle), and the pipeline on the result equals the oracle on it."""
+    rng = np.random.default_rng(n + nv)
+    arr = rng.integers(0, nv, size=(n, 3), dtype=np.uint32)
+    ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+    kept, ms = ctx.distinct_triples()
+    es, ep, eo = R.distinct_triples(arr[:, 0], arr[:, 1], arr[:, 2])
+    assert kept == es.shape[0]
+    s, p, o = ctx.copy_triples(n)
+    assert s.shape[0] == kept
+    np.testing.assert_array_equal(s, es)
+    np.testing.assert_array_equal(p, ep)
+    np.testing.assert_array_equal(o, eo)
+    if n <= 1000:
+        ctx.run(2)
+        exp, _ = C.run_set(es, ep, eo, nv, 2, 1, True)
+        assert _lib.decoded_to_set(ctx.decoded_cinds()) == exp
+    kept2, _ = ctx.distinct_triples()  # idempotent
+    assert kept2 == kept
+
+
+def test_program_prefixes_and_distinct_triples(tmp_path):
+    """--prefixes + --distinct-triples through the program vs the oracle on per-triple shortened, distinct
+    string triples (ShortenUrls.map then triples.distinct, RDFind.scala:243-287)."""
+    rng = random.Random(17)
+    ents = [f"<http://ex.org/{'a/' if i % 3 else ''}e{i}>" for i in range(40)]
+    preds = [f"<http://ex.org/p{j}>" for j in range(5)]
+    objs = ents + ['"l1"', '"l2"', "ex:e1"]
+    tr = [(rng.choice(ents), rng.choice(preds), rng.choice(objs)) for _ in range(600)]
+    tr += tr[:200]  # duplicates: they change condition counts unless removed
+    (tmp_path / "in.nt").write_text("".join(f"{a} {b} {c} .\n" for a, b, c in tr))
+    (tmp_path / "pre.nt").write_text("@prefix ex: <http://ex.org/> .\n@prefix exa: <http://ex.org/a/> .\n")
+    prefixes = [("ex", "http://ex.org/"), ("exa", "http://ex.org/a/")]
+    short = [tuple(R.shorten_term(x, prefixes) for x in t) for t in tr]
+    for distinct in (False, True):
+        out = tmp_path / f"out{distinct}.txt"
+        argv = ["--use-fis", "--clean-implied", "--support", "3", "--prefixes", str(tmp_path / "pre.nt"),
+                "--output", f"file://{out}", str(tmp_path / "in.nt")] + (["--distinct-triples"] if distinct else [])
+        program.RDFind(argv).run()
+        expected = R.format_cinds(R.rdfind(short, 3, 1, True, distinct_triples=distinct))
+        assert sorted(out.read_text().splitlines()) == expected, distinct

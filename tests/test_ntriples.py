@@ -1,5 +1,6 @@
 import gzip
 
+import numpy as np
 import pytest
 
 from rdfind_amd import ntriples
@@ -30,3 +31,68 @@ def test_resolve_patterns(tmp_path):
         (tmp_path / n).write_text("<a> <p> <b> .\n")
     got = ntriples.resolve_paths([f"{tmp_path}/a*.nt"])
     assert [x.rsplit("/", 1)[1] for x in got] == ["a1.nt", "a2.nt"]
+
+
+# --prefixes (ALG/operators/ParseRdfPrefixes.scala, ShortenUrls.scala, util/StringTrie.scala) against the
+# oracle's linear-scan restatement
+from oracle import rdfind_oracle as R  # noqa: E402
+
+
+@pytest.mark.parametrize("line", [
+    "@prefix foaf: <http://xmlns.com/foaf/0.1/> .", "@prefix  ex:\t<http://ex.org/>.", "@prefix <http://base/> .",
+    "@prefix dc: <http://purl.org/dc/elements/1.1/> .\n", "@prefix x: <a>   .",
+    "@prefix : <http://empty/> .", "prefix ex: <http://ex.org/> .", "@prefix ex: http://ex.org/ .",
+    "@prefix ex: <http://ex.org/>", " @prefix ex: <http://ex.org/> .", "@prefix ex: <http://ex.org/> . #",
+])
+def test_prefix_line_parsing_matches_oracle(line):
+    try:
+        exp = R.parse_prefix_line(line)
+    except ValueError:
+        with pytest.raises(ValueError):
+            ntriples.parse_prefix_line(line)
+        return
+    assert ntriples.parse_prefix_line(line) == exp
+
+
+def test_shortening_matches_oracle():
+    import random
+    rng = random.Random(3)
+    alphabet = "ab/#:.x"
+    for _ in range(300):
+        urls = {"http://" + "".join(rng.choice(alphabet) for _ in range(rng.randrange(0, 6)))
+                for _ in range(rng.randrange(0, 6))}
+        prefixes = [(f"p{i}", u) for i, u in enumerate(sorted(urls))]
+        table = ntriples.PrefixTable(prefixes)
+        for _ in range(40):
+            body = "http://" + "".join(rng.choice(alphabet) for _ in range(rng.randrange(0, 9)))
+            term = rng.choice([f"<{body}>", f'"{body}"', f'"v"^^<{body}>', body, f"<{body}"])
+            assert table.shorten(term) == R.shorten_term(term, prefixes), (term, prefixes)
+
+
+def test_shorten_dictionary_equals_per_triple_shortening(tmp_path):
+    pref = tmp_path / "prefixes.nt"
+    pref.write_text("# comment\n@prefix ex: <http://ex.org/> .\n@prefix exa: <http://ex.org/a/> .\n"
+                    "@prefix <http://base.org/> .\n")
+    tr = [("<http://ex.org/a/x>", "<http://ex.org/p>", '"lit"'), ("<http://ex.org/b>", "<http://base.org/q>", "<other>"),
+          ("<http://ex.org/a/x>", "<http://ex.org/p>", "<http://ex.org/a/x>"), ("ex:b", "<http://base.org/q>", "<other>")]
+    d = ntriples.Dictionary()
+    arr = np.array([[d.encode(x) for x in t] for t in tr], np.uint32)
+    prefixes = ntriples.read_prefixes([str(pref)])
+    assert prefixes == [("ex", "http://ex.org/"), ("exa", "http://ex.org/a/"), ("", "http://base.org/")]
+    s, p, o, short = ntriples.shorten_dictionary(arr[:, 0], arr[:, 1], arr[:, 2], d, prefixes)
+    got = [(short.term(a), short.term(b), short.term(c)) for a, b, c in zip(s, p, o)]
+    exp = [tuple(R.shorten_term(x, prefixes) for x in t) for t in tr]
+    assert got == exp == [("exa:x", "ex:p", '"lit"'), ("ex:b", ":q", "<other>"), ("exa:x", "ex:p", "exa:x"),
+                          ("ex:b", ":q", "<other>")]
+    assert short.size == len({x for t in exp for x in t})  # "<http://ex.org/b>" and "ex:b" share one id
+
+
+def test_duplicate_prefix_key_rejected():
+    with pytest.raises(ValueError, match="Key already exists"):
+        ntriples.PrefixTable([("a", "http://x/"), ("b", "http://x/")])
+
+
+def test_prefixes_and_distinct_flags_accepted():
+    from rdfind_amd import program
+    prog = program.RDFind(["--use-fis", "--prefixes", "a.nt,b.nt", "--prefixes", "c.nt", "--distinct-triples", "x.nt"])
+    assert prog.args.prefixes == ["a.nt,b.nt", "c.nt"] and prog.args.distinct_triples

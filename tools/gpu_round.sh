@@ -53,6 +53,18 @@ for step in "$@"; do
       timeout -k 10 300 python -u tools/gpu_quick.py > gpurun_out/quick_$TAG.log 2>&1 \
         || { echo "quick failed"; tail -30 gpurun_out/quick_$TAG.log; exit 1; }
       tail -5 gpurun_out/quick_$TAG.log ;;
+    distinct)
+      timeout -k 10 300 python -u tools/distinct_bench.py > gpurun_out/distinct_$TAG.log 2>&1 \
+        || { echo "distinct failed"; tail -30 gpurun_out/distinct_$TAG.log; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/dprof_$TAG -o run --output-format csv \
+        -- python3 tools/distinct_bench.py > gpurun_out/dprof_$TAG.log 2>&1 \
+        || { echo "distinct prof failed"; tail -30 gpurun_out/dprof_$TAG.log; exit 1; }
+      find gpurun_out/dprof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/dprof_$TAG.kernel_stats.csv \;
+      grep DISTINCT gpurun_out/distinct_$TAG.log; grep distinct gpurun_out/dprof_$TAG.kernel_stats.csv | cut -c1-40,150- ;;
+    gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
+        > gpurun_out/gtest_$TAG.log 2>&1 || { echo "gtest failed"; tail -30 gpurun_out/gtest_$TAG.log; exit 1; }
+      tail -3 gpurun_out/gtest_$TAG.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
