@@ -2154,29 +2154,36 @@ namespace rdf {
 
 // ================================================================================================
 // Distinct triples (--distinct-triples: `triples.distinct`, ALG/programs/RDFind.scala:284-287).
-// One open-addressing table of triple indices (load <= 1/2).  A slot is claimed once by CAS and only ever
-// lowered afterwards (atomicMin) to another index of an equal triple, so it ends holding the FIRST
-// occurrence; the keep pass marks exactly the triples that are their slot's value.  Survivors keep their
-// input order (the result as a set is what the reference's distinct defines).
+// One open-addressing table (load <= 1/2) of 64-bit entries: a 32-bit fingerprint of the triple above the
+// triple's index.  A slot is claimed once by CAS and only ever lowered afterwards (atomicMin) to an entry
+// of an equal triple -- same fingerprint, smaller index -- so it ends holding the FIRST occurrence; the keep
+// pass marks exactly the triples that are their slot's index.  Triples are gathered for comparison only on
+// a fingerprint match, i.e. for duplicates and rare fingerprint collisions: a unique triple costs one
+// random table access per pass.  Survivors keep their input order (the reference's distinct defines a set).
 
-__device__ inline u64 triple_slot(u32 a, u32 b, u32 c, u64 mask) {
-    return mix64((((u64)a << 32) | b) ^ mix64((u64)c + 0x9E3779B97F4A7C15ull)) & mask;
+__device__ inline u64 triple_hash(u32 a, u32 b, u32 c) {
+    return mix64((((u64)a << 32) | b) ^ mix64((u64)c + 0x9E3779B97F4A7C15ull));
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_distinct_insert(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                               const u32* __restrict__ o, u64 n, u32* table, u64 mask) {
+                                                               const u32* __restrict__ o, u64 n, u64* table, u64 mask) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         const u32 a = s[i], b = p[i], c = o[i];
-        u64 h = triple_slot(a, b, c, mask);
+        const u64 hv = triple_hash(a, b, c);
+        const u64 e = (hv & 0xffffffff00000000ull) | i;  // entries never equal EMPTY64: i < 2^32 - 1
+        u64 h = hv & mask;
         for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
-            u32 cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cur == EMPTY32) {
-                cur = atomicCAS(&table[h], EMPTY32, (u32)i);
-                if (cur == EMPTY32) break;
+            u64 cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == EMPTY64) {
+                cur = atomicCAS(&table[h], EMPTY64, e);
+                if (cur == EMPTY64) break;
             }
-            if (s[cur] == a && p[cur] == b && o[cur] == c) {
-                if (cur > (u32)i) atomicMin(&table[h], (u32)i);
-                break;
+            if ((cur >> 32) == (e >> 32)) {
+                const u32 j = (u32)cur;
+                if (s[j] == a && p[j] == b && o[j] == c) {
+                    if (cur > e) atomicMin(&table[h], e);
+                    break;
+                }
             }
         }
     }
@@ -2184,17 +2191,22 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_distinct_insert(const u32* __rest
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_distinct_keep(const u32* __restrict__ s, const u32* __restrict__ p,
                                                              const u32* __restrict__ o, u64 n,
-                                                             const u32* __restrict__ table, u64 mask, u32* keep) {
+                                                             const u64* __restrict__ table, u64 mask, u32* keep) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         const u32 a = s[i], b = p[i], c = o[i];
-        u64 h = triple_slot(a, b, c, mask);
+        const u64 hv = triple_hash(a, b, c);
+        u64 h = hv & mask;
         u32 k = 1;
         for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
-            const u32 cur = table[h];
-            if (cur == EMPTY32) break;  // unreachable: every triple's chain ends at its own slot
-            if (s[cur] == a && p[cur] == b && o[cur] == c) {
-                k = cur == (u32)i;
-                break;
+            const u64 cur = table[h];
+            if (cur == EMPTY64) break;  // unreachable: every triple's chain ends at its own slot
+            if ((cur >> 32) == (hv >> 32)) {
+                const u32 j = (u32)cur;
+                if (j == (u32)i) break;  // this triple is its slot's first occurrence
+                if (s[j] == a && p[j] == b && o[j] == c) {
+                    k = 0;
+                    break;
+                }
             }
         }
         keep[i] = k;

@@ -349,16 +349,16 @@ rdf_status rdf_distinct_triples(rdf_ctx* c, uint64_t* n_distinct, float* ms) {
     u64 kept = 0;
     if (n) {
         const u64 T = next_pow2(2 * n);
-        ENSURE(c, dtab, T * 4);
+        ENSURE(c, dtab, T * 8);
         ENSURE(c, dkeep, n * 4);
         ENSURE(c, dpos, n * 4);
         ENSURE(c, xs, n * 4);
         ENSURE(c, xp, n * 4);
         ENSURE(c, xo, n * 4);
-        HIP_TRY(c, hipMemsetAsync(c->dtab.p, 0xff, T * 4, st));
+        HIP_TRY(c, hipMemsetAsync(c->dtab.p, 0xff, T * 8, st));
         const unsigned g = grid_for(n, RDF_BLOCK, kGrid);
-        hipLaunchKernelGGL(k_distinct_insert, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dtab.as<u32>(), T - 1);
-        hipLaunchKernelGGL(k_distinct_keep, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dtab.as<u32>(), T - 1,
+        hipLaunchKernelGGL(k_distinct_insert, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dtab.as<u64>(), T - 1);
+        hipLaunchKernelGGL(k_distinct_keep, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dtab.as<u64>(), T - 1,
                            c->dkeep.as<u32>());
         HIP_TRY(c, exclusive_scan_u32(c->ws, c->dkeep.as<u32>(), c->dpos.as<u32>(), n, (u32*)dscal(c, 7), st));
         hipLaunchKernelGGL(k_distinct_scatter, dim3(g), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, c->dkeep.as<u32>(),
