@@ -125,6 +125,17 @@ rdf_status rdf_set_triples_device(rdf_ctx* ctx, const uint32_t* d_s, const uint3
  * (optional) the device time.  The compacted triples are context-owned from then on. */
 rdf_status rdf_distinct_triples(rdf_ctx* ctx, uint64_t* n_distinct, float* ms);
 
+/* N-Triples ingest on the device: the `Parse triples` map (ALG/programs/RDFind.scala:196-237, rdf-converter's
+ * NTriplesParser) plus dictionary encoding, replacing the host parser (rdfind_amd/ntriples.py, same rules).
+ * text: the raw (decompressed) file bytes, '\n'-terminated lines; lines starting with '#' and blank lines are
+ * skipped.  Term ids follow first appearance (line-major, then s, p, o).  The parsed triples become the resident
+ * input; a malformed line fails with RDF_ERR_ARG naming it. */
+#define RDF_NT_TABS 1u                 /* --tabs: tab-separated terms */
+rdf_status rdf_parse_ntriples(rdf_ctx* ctx, const char* text, uint64_t nbytes, uint32_t flags, uint64_t* n_triples,
+                              uint32_t* num_terms, float* ms);
+/* The dictionary of the last rdf_parse_ntriples: term id i is text[offsets[i] .. offsets[i] + lengths[i]). */
+rdf_status rdf_copy_terms(rdf_ctx* ctx, uint64_t* offsets, uint32_t* lengths, uint64_t cap, uint64_t* n_copied);
+
 /* Copies min(cap, n) resident triples to host arrays (e.g. after rdf_distinct_triples). */
 rdf_status rdf_copy_triples(rdf_ctx* ctx, uint32_t* s, uint32_t* p, uint32_t* o, uint64_t cap, uint64_t* n_copied);
 

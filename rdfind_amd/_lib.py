@@ -26,8 +26,9 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_binary_keys", "rdf_stage_times", "rdf_kernel_times", "rdf_sync",
     "rdf_copy_cinds_range", "rdf_cind_checksum", "rdf_last_stats", "rdf_shard_begin", "rdf_shard_step",
     "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
-    "rdf_distinct_triples", "rdf_copy_triples",
+    "rdf_distinct_triples", "rdf_copy_triples", "rdf_parse_ntriples", "rdf_copy_terms",
 )
+RDF_NT_TABS = 1
 
 # rdf_exchange ops (sharded mode, include/rdfind_hip.h)
 X_DONE, X_ALLREDUCE_SUM_U32, X_ALLREDUCE_SUM_U64, X_ALLREDUCE_MIN_U64, X_ALLGATHERV_U64, X_ALLTOALLV_U64 = range(6)
@@ -102,6 +103,9 @@ def load():
         "rdf_set_triples_device": (i32, [P, P, P, P, u64, u32]),
         "rdf_distinct_triples": (i32, [P, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_float)]),
         "rdf_copy_triples": (i32, [P, P, P, P, u64, ctypes.POINTER(u64)]),
+        "rdf_parse_ntriples": (i32, [P, ctypes.c_char_p, u64, u32, ctypes.POINTER(u64), ctypes.POINTER(u32),
+                                     ctypes.POINTER(ctypes.c_float)]),
+        "rdf_copy_terms": (i32, [P, P, P, u64, ctypes.POINTER(u64)]),
         "rdf_frequent_conditions": (i32, [P, u32, ctypes.POINTER(FcStats)]),
         "rdf_build_capture_groups": (i32, [P, ctypes.c_char_p, ctypes.POINTER(GroupStats)]),
         "rdf_discover_cinds": (i32, [P, u32, ctypes.POINTER(CindStats)]),
@@ -199,6 +203,40 @@ class Context:
         self._check(self.lib.rdf_distinct_triples(self.ptr, ctypes.byref(n), ctypes.byref(ms)),
                     "rdf_distinct_triples")
         return int(n.value), float(ms.value)
+
+    def parse_ntriples(self, data: bytes, tabs: bool = False):
+        """N-Triples text -> resident dictionary-encoded triples, on the device (rdf_parse_ntriples).
+        Returns (n_triples, num_terms, device ms) and keeps ``data`` for :meth:`parsed_terms`."""
+        n, v, ms = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_float()
+        self._check(self.lib.rdf_parse_ntriples(self.ptr, data, len(data), RDF_NT_TABS if tabs else 0,
+                                                ctypes.byref(n), ctypes.byref(v), ctypes.byref(ms)),
+                    "rdf_parse_ntriples")
+        self.num_terms = int(v.value)
+        self._parsed = data
+        return int(n.value), int(v.value), float(ms.value)
+
+    def parsed_terms(self):
+        """The device dictionary of the last parse as (heap bytes, uint64 offsets[V + 1]): term i is
+        heap[offsets[i]:offsets[i + 1]] (UTF-8)."""
+        v = self.num_terms
+        off, ln = np.empty(v, np.uint64), np.empty(v, np.uint32)
+        got = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_terms(self.ptr, off.ctypes.data, ln.ctypes.data, v, ctypes.byref(got)),
+                    "rdf_copy_terms")
+        ln64 = ln.astype(np.int64)
+        offsets = np.zeros(v + 1, np.uint64)
+        np.cumsum(ln64, out=offsets[1:])
+        src = np.frombuffer(self._parsed, np.uint8)
+        pos = np.arange(int(offsets[-1]), dtype=np.int64) + np.repeat(off.astype(np.int64) - offsets[:-1].astype(np.int64),
+                                                                       ln64)
+        return src[pos].tobytes(), offsets
+
+    def set_dictionary_heap(self, heap: bytes, offsets):
+        """rdf_set_dictionary from a ready heap + offsets (e.g. :meth:`parsed_terms`)."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        buf = ctypes.create_string_buffer(heap, max(len(heap), 1))
+        self._check(self.lib.rdf_set_dictionary(self.ptr, buf, len(heap), offsets.ctypes.data, offsets.shape[0] - 1),
+                    "rdf_set_dictionary")
 
     def copy_triples(self, n: int):
         """The resident triples as three uint32 arrays (the first n of them)."""

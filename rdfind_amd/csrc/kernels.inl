@@ -2228,3 +2228,227 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_distinct_scatter(const u32* __res
 }
 
 }  // namespace rdf
+
+namespace rdf {
+
+// ================================================================================================
+// N-Triples ingest: the `Parse triples` map (ALG/programs/RDFind.scala:196-237) and the
+// dictionary encoding that the build puts in its place (one u32 id space for s, p, o; ids in order of first
+// appearance, line-major then s, p, o -- the host Dictionary's order, rdfind_amd/ntriples.py).
+//   lines    : '\n'-terminated; lines starting with '#' and all-whitespace lines are skipped;
+//   terms    : <IRI>, "literal" with \-escapes and an optional @lang / ^^<type> / ^^bare suffix, or a bare
+//              token up to whitespace; --tabs: the first three '\t'-separated fields.
+// Whitespace is ASCII (" \t\n\v\f\r" and 0x1c-0x1f, the ASCII part of Python's str.isspace).
+
+static constexpr u32 NT_CHUNK = 256;  // bytes per thread in the line-start pass
+
+__device__ inline bool nt_space(unsigned char ch) {
+    return ch == ' ' || (ch >= 9 && ch <= 13) || (ch >= 0x1c && ch <= 0x1f);
+}
+
+// pass 1: newlines per NT_CHUNK-byte chunk
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_count_lines(const unsigned char* __restrict__ text, u64 nbytes,
+                                                              u64 nchunks, u32* cnt) {
+    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < nchunks; c += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 b = c * NT_CHUNK, e = b + NT_CHUNK < nbytes ? b + NT_CHUNK : nbytes;
+        u32 k = 0;
+        for (u64 i = b; i < e; ++i) k += text[i] == '\n';
+        cnt[c] = k;
+    }
+}
+
+// pass 2: line start offsets (line 0 starts at 0; line j+1 starts after the j-th newline)
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_line_starts(const unsigned char* __restrict__ text, u64 nbytes,
+                                                              u64 nchunks, const u64* __restrict__ coff, u64* lstart) {
+    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < nchunks; c += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 b = c * NT_CHUNK, e = b + NT_CHUNK < nbytes ? b + NT_CHUNK : nbytes;
+        u64 j = coff[c];
+        if (c == 0) lstart[0] = 0;
+        for (u64 i = b; i < e; ++i)
+            if (text[i] == '\n') lstart[++j] = i + 1;
+    }
+}
+
+// per line: the three terms (tstart/tlen per occurrence 3*line+t), valid flag, first malformed line
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_tokenize(const unsigned char* __restrict__ text, u64 nbytes,
+                                                           const u64* __restrict__ lstart, u64 nlines, int tabs,
+                                                           u64* tstart, u32* tlen, u32* valid, u64* bad_line) {
+    for (u64 l = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; l < nlines; l += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 b = lstart[l];
+        u64 e = l + 1 < nlines ? lstart[l + 1] - 1 : nbytes;  // excludes the '\n'
+        if (l + 1 < nlines && e > b && text[e - 1] == '\r') --e;  // "\r\n" ends a line as one terminator
+        u32 ok = 0;
+        bool blank = true;
+        for (u64 i = b; i < e && blank; ++i) blank = nt_space(text[i]);
+        if (!(b < e && text[b] == '#') && !blank) {
+            u64 ts[3], te[3];
+            int nt = 0;
+            bool err = false;
+            if (tabs) {
+                u64 f = b;
+                for (u64 i = b; i <= e && nt < 3; ++i)
+                    if (i == e || text[i] == '\t') {
+                        ts[nt] = f;
+                        te[nt] = i;
+                        ++nt;
+                        f = i + 1;
+                    }
+                err = nt < 3;
+            } else {
+                u64 i = b;
+                while (nt < 3 && !err) {
+                    while (i < e && nt_space(text[i])) ++i;
+                    if (i >= e) {
+                        err = true;
+                        break;
+                    }
+                    u64 j;
+                    const unsigned char ch = text[i];
+                    if (ch == '<') {
+                        j = i + 1;
+                        while (j < e && text[j] != '>') ++j;
+                        if (j >= e) err = true;
+                        else ++j;
+                    } else if (ch == '"') {
+                        j = i + 1;
+                        while (j < e && text[j] != '"') j += text[j] == '\\' ? 2 : 1;
+                        if (j >= e) err = true;
+                        else {
+                            ++j;
+                            if (j < e && text[j] == '@') {
+                                while (j < e && !nt_space(text[j])) ++j;
+                            } else if (j + 1 < e && text[j] == '^' && text[j + 1] == '^') {
+                                j += 2;
+                                if (j < e && text[j] == '<') {
+                                    while (j < e && text[j] != '>') ++j;
+                                    if (j >= e) err = true;
+                                    else ++j;
+                                } else {
+                                    while (j < e && !nt_space(text[j])) ++j;
+                                }
+                            }
+                        }
+                    } else {
+                        j = i;
+                        while (j < e && !nt_space(text[j])) ++j;
+                    }
+                    if (err) break;
+                    ts[nt] = i;
+                    te[nt] = j;
+                    ++nt;
+                    i = j;
+                }
+            }
+            if (err) atomicMin(bad_line, l);
+            else {
+                ok = 1;
+                for (int t = 0; t < 3; ++t) {
+                    tstart[3 * l + t] = ts[t];
+                    tlen[3 * l + t] = (u32)(te[t] - ts[t]);
+                }
+            }
+        }
+        valid[l] = ok;
+    }
+}
+
+__device__ inline u64 nt_hash(const unsigned char* __restrict__ s, u32 n) {
+    u64 h = 0x243F6A8885A308D3ull ^ n;
+    u32 i = 0;
+    for (; i + 8 <= n; i += 8) {
+        u64 w = 0;
+        for (int k = 0; k < 8; ++k) w |= (u64)s[i + k] << (8 * k);
+        h = mix64(h ^ w);
+    }
+    u64 w = 0;
+    for (int k = 0; i + k < n; ++k) w |= (u64)s[i + k] << (8 * k);
+    return mix64(h ^ w ^ 0x9E3779B97F4A7C15ull);
+}
+
+__device__ inline bool nt_equal(const unsigned char* __restrict__ text, u64 a, u64 b, u32 n) {
+    for (u32 i = 0; i < n; ++i)
+        if (text[a + i] != text[b + i]) return false;
+    return true;
+}
+
+// dictionary table: entries fingerprint<<32 | occurrence; the slot of a term ends holding its first occurrence
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_insert(const unsigned char* __restrict__ text,
+                                                              const u64* __restrict__ tstart, const u32* __restrict__ tlen,
+                                                              const u32* __restrict__ valid, u64 nocc, u64* hv,
+                                                              u64* table, u64 mask) {
+    for (u64 k = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; k < nocc; k += (u64)gridDim.x * RDF_BLOCK) {
+        if (!valid[k / 3]) continue;
+        const u64 a = tstart[k];
+        const u32 n = tlen[k];
+        const u64 h0 = nt_hash(text + a, n);
+        hv[k] = h0;
+        const u64 e = (h0 & 0xffffffff00000000ull) | k;
+        u64 h = h0 & mask;
+        for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+            u64 cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == EMPTY64) {
+                cur = atomicCAS(&table[h], EMPTY64, e);
+                if (cur == EMPTY64) break;
+            }
+            if ((cur >> 32) == (e >> 32)) {
+                const u32 j = (u32)cur;
+                if (tlen[j] == n && nt_equal(text, tstart[j], a, n)) {
+                    if (cur > e) atomicMin(&table[h], e);
+                    break;
+                }
+            }
+        }
+    }
+}
+
+// per occurrence: its term's first occurrence (rep) and whether it is that first occurrence
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_rep(const unsigned char* __restrict__ text,
+                                                           const u64* __restrict__ tstart, const u32* __restrict__ tlen,
+                                                           const u32* __restrict__ valid, u64 nocc,
+                                                           const u64* __restrict__ hv, const u64* __restrict__ table,
+                                                           u64 mask, u32* rep, u32* first) {
+    for (u64 k = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; k < nocc; k += (u64)gridDim.x * RDF_BLOCK) {
+        u32 r = (u32)k, f = 0;
+        if (valid[k / 3]) {
+            const u64 h0 = hv[k], a = tstart[k];
+            const u32 n = tlen[k];
+            u64 h = h0 & mask;
+            for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+                const u64 cur = table[h];
+                if (cur == EMPTY64) break;  // unreachable
+                if ((cur >> 32) == (h0 >> 32)) {
+                    const u32 j = (u32)cur;
+                    if (j == (u32)k || (tlen[j] == n && nt_equal(text, tstart[j], a, n))) {
+                        r = j;
+                        break;
+                    }
+                }
+            }
+            f = r == (u32)k;
+        }
+        rep[k] = r;
+        first[k] = f;
+    }
+}
+
+// term ids (scan of `first` = id of each first occurrence) -> triples at their compacted line positions;
+// term table (first occurrence's offset and length per id)
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_assign(const u64* __restrict__ tstart, const u32* __restrict__ tlen,
+                                                         const u32* __restrict__ valid, const u32* __restrict__ lpos,
+                                                         u64 nocc, const u32* __restrict__ rep,
+                                                         const u32* __restrict__ first, const u32* __restrict__ fid,
+                                                         u32* s, u32* p, u32* o, u64* term_off, u32* term_len) {
+    for (u64 k = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; k < nocc; k += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 l = k / 3;
+        if (!valid[l]) continue;
+        const u32 id = fid[rep[k]];
+        const u32 t = (u32)(k - 3 * l), row = lpos[l];
+        (t == 0 ? s : t == 1 ? p : o)[row] = id;
+        if (first[k]) {
+            term_off[id] = tstart[k];
+            term_len[id] = tlen[k];
+        }
+    }
+}
+
+}  // namespace rdf

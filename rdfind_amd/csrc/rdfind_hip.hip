@@ -29,7 +29,9 @@ struct rdf_ctx {
 
     // triples
     DevBuf ts, tp, to;
-    DevBuf dtab, dkeep, dpos, xs, xp, xo;  // --distinct-triples: slot table, keep flags, positions, compacted copy
+    DevBuf dtab, dkeep, dpos, xs, xp, xo;
+    DevBuf ntext, ncnt, ncoff, nlstart, ntstart, ntlen, nvalid, nlpos, nhv, ntab, nrep, nfirst, nfid, nterm_off, nterm_len;
+    u64 n_terms_parsed = 0;  // rows of nterm_off/nterm_len (rdf_copy_terms)  // --distinct-triples: slot table, keep flags, positions, compacted copy
     const u32 *s = nullptr, *p = nullptr, *o = nullptr;
     u64 n = 0;
     u32 V = 0;
@@ -396,6 +398,104 @@ rdf_status rdf_copy_triples(rdf_ctx* c, uint32_t* s, uint32_t* p, uint32_t* o, u
         HIP_TRY(c, hipMemcpyAsync(s, c->s, n * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipMemcpyAsync(p, c->p, n * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipMemcpyAsync(o, c->o, n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (n_copied) *n_copied = n;
+    return RDF_OK;
+}
+
+// N-Triples ingest on the device (the `Parse triples` map of ALG/programs/RDFind.scala:196-237
+// plus dictionary encoding).  The parsed triples become the resident input (as after rdf_set_triples).
+rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uint32_t flags, uint64_t* n_triples,
+                              uint32_t* num_terms, float* ms) {
+    if (!c || (nbytes && !text)) return fail(c, RDF_ERR_ARG, "null text");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const unsigned char* dtext = nullptr;
+    ENSURE(c, ntext, nbytes + 1);
+    if (nbytes) HIP_TRY(c, hipMemcpyAsync(c->ntext.p, text, nbytes, hipMemcpyHostToDevice, st));
+    dtext = (const unsigned char*)c->ntext.p;
+    HIP_TRY(c, hipEventRecord(c->ev[6], st));
+    const u64 nchunks = std::max<u64>((nbytes + NT_CHUNK - 1) / NT_CHUNK, 1);
+    ENSURE(c, ncnt, nchunks * 4);
+    ENSURE(c, ncoff, nchunks * 8);
+    const unsigned gc = grid_for(nchunks, RDF_BLOCK, kGrid);
+    hipLaunchKernelGGL(k_nt_count_lines, dim3(gc), dim3(RDF_BLOCK), 0, st, dtext, nbytes, nchunks, c->ncnt.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ncnt.as<u32>(), c->ncoff.as<u64>(), nchunks, dscal(c, 0), st));
+    u64 newlines = 0;
+    rdf_status rs = read_u64(c, dscal(c, 0), &newlines);
+    if (rs) return rs;
+    const u64 nlines = newlines + 1, nocc = 3 * nlines;
+    if (nocc >= 0xffffffffull) return fail(c, RDF_ERR_LIMIT, "too many lines (3 * lines must be < 2^32)");
+    ENSURE(c, nlstart, nlines * 8);
+    hipLaunchKernelGGL(k_nt_line_starts, dim3(gc), dim3(RDF_BLOCK), 0, st, dtext, nbytes, nchunks, c->ncoff.as<u64>(),
+                       c->nlstart.as<u64>());
+    ENSURE(c, ntstart, nocc * 8);
+    ENSURE(c, ntlen, nocc * 4);
+    ENSURE(c, nvalid, nlines * 4);
+    ENSURE(c, nlpos, nlines * 4);
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 1), 0xff, 8, st));
+    const unsigned gl = grid_for(nlines, RDF_BLOCK, kGrid), go = grid_for(nocc, RDF_BLOCK, kGrid);
+    hipLaunchKernelGGL(k_nt_tokenize, dim3(gl), dim3(RDF_BLOCK), 0, st, dtext, nbytes, c->nlstart.as<u64>(), nlines,
+                       (int)(flags & RDF_NT_TABS), c->ntstart.as<u64>(), c->ntlen.as<u32>(), c->nvalid.as<u32>(),
+                       dscal(c, 1));
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 2), 0, 8, st));
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->nvalid.as<u32>(), c->nlpos.as<u32>(), nlines, (u32*)dscal(c, 2), st));
+    const u64 T = next_pow2(2 * nocc);
+    ENSURE(c, ntab, T * 8);
+    ENSURE(c, nhv, nocc * 8);
+    ENSURE(c, nrep, nocc * 4);
+    ENSURE(c, nfirst, nocc * 4);
+    ENSURE(c, nfid, nocc * 4);
+    HIP_TRY(c, hipMemsetAsync(c->ntab.p, 0xff, T * 8, st));
+    hipLaunchKernelGGL(k_nt_dict_insert, dim3(go), dim3(RDF_BLOCK), 0, st, dtext, c->ntstart.as<u64>(), c->ntlen.as<u32>(),
+                       c->nvalid.as<u32>(), nocc, c->nhv.as<u64>(), c->ntab.as<u64>(), T - 1);
+    hipLaunchKernelGGL(k_nt_dict_rep, dim3(go), dim3(RDF_BLOCK), 0, st, dtext, c->ntstart.as<u64>(), c->ntlen.as<u32>(),
+                       c->nvalid.as<u32>(), nocc, c->nhv.as<u64>(), c->ntab.as<u64>(), T - 1, c->nrep.as<u32>(),
+                       c->nfirst.as<u32>());
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 8, st));
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->nfirst.as<u32>(), c->nfid.as<u32>(), nocc, (u32*)dscal(c, 3), st));
+    u64 sc[3];
+    rs = read_multi(c, {{dscal(c, 1), 8}, {dscal(c, 2), 8}, {dscal(c, 3), 8}}, sc);
+    if (rs) return rs;
+    if (sc[0] != ~0ull) return fail(c, RDF_ERR_ARG, "malformed N-Triples line " + std::to_string(sc[0] + 1));
+    const u64 n = sc[1], V = sc[2];
+    rs = check_terms(c, n, (u32)std::min<u64>(V, 0xffffffffull));
+    if (rs) return rs;
+    ENSURE(c, ts, n * 4);
+    ENSURE(c, tp, n * 4);
+    ENSURE(c, to, n * 4);
+    ENSURE(c, nterm_off, V * 8);
+    ENSURE(c, nterm_len, V * 4);
+    hipLaunchKernelGGL(k_nt_assign, dim3(go), dim3(RDF_BLOCK), 0, st, c->ntstart.as<u64>(), c->ntlen.as<u32>(),
+                       c->nvalid.as<u32>(), c->nlpos.as<u32>(), nocc, c->nrep.as<u32>(), c->nfirst.as<u32>(),
+                       c->nfid.as<u32>(), c->ts.as<u32>(), c->tp.as<u32>(), c->to.as<u32>(), c->nterm_off.as<u64>(),
+                       c->nterm_len.as<u32>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(c->ev[7], st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    if (ms) HIP_TRY(c, hipEventElapsedTime(ms, c->ev[6], c->ev[7]));
+    c->s = c->ts.as<u32>();
+    c->p = c->tp.as<u32>();
+    c->o = c->to.as<u32>();
+    c->n = n;
+    c->V = (u32)V;
+    c->stage = 1;
+    c->n_terms_parsed = V;
+    if (n_triples) *n_triples = n;
+    if (num_terms) *num_terms = (u32)V;
+    return RDF_OK;
+}
+
+// Term table of the last rdf_parse_ntriples: byte offset (into the parsed text) and length of term id i.
+rdf_status rdf_copy_terms(rdf_ctx* c, uint64_t* offsets, uint32_t* lengths, uint64_t cap, uint64_t* n_copied) {
+    if (!c) return RDF_ERR_ARG;
+    const u64 n = std::min<u64>(cap, c->n_terms_parsed);
+    if (n && (!offsets || !lengths)) return fail(c, RDF_ERR_ARG, "null term arrays");
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (n) {
+        HIP_TRY(c, hipMemcpyAsync(offsets, c->nterm_off.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(lengths, c->nterm_len.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (n_copied) *n_copied = n;

@@ -239,3 +239,46 @@ def shorten_dictionary(s, p, o, dictionary: Dictionary, prefixes):
     remap = np.fromiter((short.encode(table.shorten(t)) for t in dictionary.terms), dtype=np.uint32,
                         count=dictionary.size)
     return remap[s], remap[p], remap[o], short
+
+
+# ------------------------------------------------------------------------------------------------
+# Device ingest (rdf_parse_ntriples): the host side only reads (and gunzips) the bytes
+
+def read_bytes(paths) -> bytes:
+    """The input files' bytes, concatenated with a line break between files (MultiFileTextInputFormat reads
+    every file's lines, FLK/persistence/MultiFileTextInputFormat.java:199-206)."""
+    parts = []
+    for path in paths:
+        if path.startswith("file:"):
+            path = path[5:]
+            while path.startswith("//"):
+                path = path[1:]
+        opener = gzip.open if path.endswith(".gz") else open
+        with opener(path, "rb") as f:
+            data = f.read()
+        parts.append(data)
+        if data and not data.endswith(b"\n"):
+            parts.append(b"\n")
+    return b"".join(parts)
+
+
+class HeapDictionary:
+    """Term id -> string over a (heap, offsets) pair, e.g. the device dictionary of rdf_parse_ntriples."""
+
+    def __init__(self, heap: bytes, offsets):
+        self.heap = heap
+        self.offsets = offsets
+        self._terms = None
+
+    @property
+    def size(self) -> int:
+        return len(self.offsets) - 1
+
+    def term(self, tid: int) -> str:
+        return self.heap[int(self.offsets[tid]):int(self.offsets[tid + 1])].decode("utf-8")
+
+    @property
+    def terms(self):
+        if self._terms is None:
+            self._terms = [self.term(i) for i in range(self.size)]
+        return self._terms

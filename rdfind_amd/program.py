@@ -48,6 +48,8 @@ def build_parser():
     ap.add_argument("--projection", default="spo", help="what shall be used as projection for captures")
     ap.add_argument("--distinct-triples", action="store_true", help="whether to ensure that triples are distinct")
     ap.add_argument("--tabs", action="store_true", help="if input file is tab-separated")
+    ap.add_argument("--host-parser", action="store_true",
+                    help="parse and dictionary-encode on the host instead of the device (same rules and ids)")
     ap.add_argument("--prefixes", action="append", default=None,
                     help="a list of nt-prefix files to apply on the input triple (repeatable or comma-separated)")
     ap.add_argument("--collect-result", action="store_true", help="whether to collect the results locally")
@@ -93,20 +95,29 @@ class RDFind:
         paths = ntriples.resolve_paths(a.inputs)
         if not paths:
             raise ValueError("no input files")
-        s, p, o, dic = ntriples.read_triples(paths, tabs=a.tabs)
-        if a.prefixes:  # Shorten URLs (RDFind.scala:243-267), once per distinct term
-            files = [x for arg in a.prefixes for x in arg.split(",") if x]
-            s, p, o, dic = ntriples.shorten_dictionary(s, p, o, dic, ntriples.read_prefixes(files))
-        self.timings["read"] = time.time() - t0
-        if a.only_read:
-            return []
-        t1 = time.time()
         with _lib.Context(a.device) as ctx:
-            ctx.set_triples(s, p, o, dic.size)
+            if a.host_parser:  # host tokenizer + dictionary (rdfind_amd/ntriples.py)
+                s, p, o, dic = ntriples.read_triples(paths, tabs=a.tabs)
+                n_in = s.shape[0]
+                ctx.set_triples(s, p, o, dic.size)
+            else:  # Parse triples on the device (rdf_parse_ntriples): the host only reads the bytes
+                n_in, _, _ = ctx.parse_ntriples(ntriples.read_bytes(paths), tabs=a.tabs)
+                dic = None  # device dictionary, fetched when needed
+            if a.prefixes:  # Shorten URLs (RDFind.scala:243-267), once per distinct term
+                if dic is None:
+                    dic = ntriples.HeapDictionary(*ctx.parsed_terms())
+                    s, p, o = ctx.copy_triples(n_in)
+                files = [x for arg in a.prefixes for x in arg.split(",") if x]
+                s, p, o, dic = ntriples.shorten_dictionary(s, p, o, dic, ntriples.read_prefixes(files))
+                ctx.set_triples(s, p, o, dic.size)
+            self.timings["read"] = time.time() - t0
+            if a.only_read:
+                return []
+            t1 = time.time()
             if a.distinct_triples:  # Remove duplicate triples (RDFind.scala:284-287), in HBM
                 n_distinct, _ = ctx.distinct_triples()
                 if a.debug_level >= 1:
-                    self.log(f"{n_distinct} distinct triples of {s.shape[0]}.")
+                    self.log(f"{n_distinct} distinct triples of {n_in}.")
             fc = ctx.frequent_conditions(a.support)
             if a.debug_level >= 1:
                 self.log(f"Found {sum(fc['n_frequent_unary'])} frequent single-conditions.")
@@ -124,7 +135,10 @@ class RDFind:
             # Cind.toString lines are formatted on the GPU (rdf_format_cinds) in chunks of rows
             t2 = time.time()
             n = ctx.cind_count()
-            ctx.set_dictionary(dic.terms)
+            if dic is None:
+                ctx.set_dictionary_heap(*ctx.parsed_terms())
+            else:
+                ctx.set_dictionary(dic.terms)
             keep_lines = n <= KEEP_LINES_MAX or a.collect_result or a.debug_level >= 3
             lines = [] if keep_lines else None
             f = None

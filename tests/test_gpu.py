@@ -315,3 +315,63 @@ def test_program_prefixes_and_distinct_triples(tmp_path):
         program.RDFind(argv).run()
         expected = R.format_cinds(R.rdfind(short, 3, 1, True, distinct_triples=distinct))
         assert sorted(out.read_text().splitlines()) == expected, distinct
+
+
+_NT_SAMPLE = (
+    "# comment line\n"
+    "<http://ex.org/a> <http://ex.org/p> \"plain\" .\n"
+    "\n   \t \n"
+    "<http://ex.org/a> <http://ex.org/p> \"esc \\\" quote\"@en-US .\n"
+    "_:b0 <http://ex.org/q> \"5\"^^<http://www.w3.org/2001/XMLSchema#int> .\r\n"
+    "<http://ex.org/b>\t<http://ex.org/p>   \"x\"^^xsd:int .\n"
+    "  <http://ex.org/a> <http://ex.org/q> _:b0 .\n"
+    "<http://ex.org/b> <http://ex.org/p> <http://ex.org/a> <http://ex.org/graph> .\n"
+    "#<http://ex.org/c> <http://ex.org/p> <http://ex.org/a> .\n"
+    "<http://ex.org/a> <http://ex.org/p> \"plain\" ."  # no final newline
+)
+
+
+def _host_parse(tmp_path, data: bytes, tabs=False):
+    f = tmp_path / "host.nt"
+    f.write_bytes(data)
+    return ntriples.read_triples([str(f)], tabs=tabs)
+
+
+def _device_parse(ctx, data: bytes, tabs=False):
+    n, v, _ = ctx.parse_ntriples(data, tabs=tabs)
+    s, p, o = ctx.copy_triples(n)
+    return s, p, o, ntriples.HeapDictionary(*ctx.parsed_terms())
+
+
+@pytest.mark.parametrize("case", ["sample", "empty", "only_comments", "tabs", "golden_lubm", "golden_zipf",
+                                  "synthetic_c1"])
+def test_device_parser_matches_host(ctx, tmp_path, case):
+    """rdf_parse_ntriples gives the host parser's triples and dictionary bit-exactly (same ids, same terms)."""
+    import gzip as _gz
+    tabs = case == "tabs"
+    if case == "sample":
+        data = _NT_SAMPLE.encode()
+    elif case == "empty":
+        data = b""
+    elif case == "only_comments":
+        data = b"# a\n\n#b\n"
+    elif case == "tabs":
+        data = b"<a>\t<p>\t\"x y\"\t.\n# c\n<b>\t<p>\t<a>\n\n<a> x\t<q>\t\"z\"\r\n"
+    elif case.startswith("golden"):
+        data = _gz.open(os.path.join(GOLDEN, f"{case.split('_')[1]}_small.nt.gz"), "rb").read()
+    else:
+        data = "".join(ln + "\n" for ln in synth.config("c1", 0.05).lines()).encode()
+    hs, hp, ho, hd = _host_parse(tmp_path, data, tabs)
+    ds, dp, do, dd = _device_parse(ctx, data, tabs)
+    assert dd.size == hd.size
+    assert dd.terms == hd.terms
+    np.testing.assert_array_equal(ds, hs)
+    np.testing.assert_array_equal(dp, hp)
+    np.testing.assert_array_equal(do, ho)
+
+
+def test_device_parser_rejects_malformed_line(ctx):
+    with pytest.raises(_lib.RdfError, match="line 2"):
+        ctx.parse_ntriples(b"<a> <p> <b> .\n<a> <p> \"unterminated .\n")
+    with pytest.raises(_lib.RdfError, match="line 1"):
+        ctx.parse_ntriples(b"<a> <p>\n")

@@ -61,6 +61,10 @@ for step in "$@"; do
         || { echo "distinct prof failed"; tail -30 gpurun_out/dprof_$TAG.log; exit 1; }
       find gpurun_out/dprof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/dprof_$TAG.kernel_stats.csv \;
       grep DISTINCT gpurun_out/distinct_$TAG.log; grep distinct gpurun_out/dprof_$TAG.kernel_stats.csv | cut -c1-40,150- ;;
+    parse)
+      timeout -k 10 400 python -u tools/parse_bench.py > gpurun_out/parse_$TAG.log 2>&1 \
+        || { echo "parse failed"; tail -30 gpurun_out/parse_$TAG.log; exit 1; }
+      grep -E "PARSE|text" gpurun_out/parse_$TAG.log ;;
     gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
         > gpurun_out/gtest_$TAG.log 2>&1 || { echo "gtest failed"; tail -30 gpurun_out/gtest_$TAG.log; exit 1; }
