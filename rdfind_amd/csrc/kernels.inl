@@ -2240,129 +2240,184 @@ namespace rdf {
 //              token up to whitespace; --tabs: the first three '\t'-separated fields.
 // Whitespace is ASCII (" \t\n\v\f\r" and 0x1c-0x1f, the ASCII part of Python's str.isspace).
 
-static constexpr u32 NT_CHUNK = 256;  // bytes per thread in the line-start pass
+static constexpr u32 NT_CHUNK = RDF_BLOCK * 16;  // bytes per block tile in the line-start passes (16 per thread)
+static constexpr u32 NT_TILE = 61440;           // LDS bytes for one block's lines in the tokenizer (2 blocks per CU)
 
 __device__ inline bool nt_space(unsigned char ch) {
     return ch == ' ' || (ch >= 9 && ch <= 13) || (ch >= 0x1c && ch <= 0x1f);
 }
 
-// pass 1: newlines per NT_CHUNK-byte chunk
+// newline bit mask of this thread's 16 bytes of tile c (one 16-B load; bytes past nbytes never count)
+__device__ inline u32 nt_newline_mask(const unsigned char* __restrict__ text, u64 nbytes, u64 c) {
+    const u64 b = c * NT_CHUNK + threadIdx.x * 16;
+    if (b >= nbytes) return 0;
+    const uint4 w = *(const uint4*)(text + b);
+    const u32 wd[4] = {w.x, w.y, w.z, w.w};
+    u32 m = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m |= (u32)(((wd[k >> 2] >> (8 * (k & 3))) & 0xff) == '\n') << k;
+    if (nbytes - b < 16) m &= (1u << (nbytes - b)) - 1u;
+    return m;
+}
+
+// pass 1: newlines per tile
 __global__ __launch_bounds__(RDF_BLOCK) void k_nt_count_lines(const unsigned char* __restrict__ text, u64 nbytes,
                                                               u64 nchunks, u32* cnt) {
-    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < nchunks; c += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 b = c * NT_CHUNK, e = b + NT_CHUNK < nbytes ? b + NT_CHUNK : nbytes;
-        u32 k = 0;
-        for (u64 i = b; i < e; ++i) k += text[i] == '\n';
-        cnt[c] = k;
+    __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
+    for (u64 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        u32 total;
+        (void)block_exclusive_scan_u32(__popc(nt_newline_mask(text, nbytes, c)), lds_wave, &total);
+        if (threadIdx.x == 0) cnt[c] = total;
     }
 }
 
 // pass 2: line start offsets (line 0 starts at 0; line j+1 starts after the j-th newline)
 __global__ __launch_bounds__(RDF_BLOCK) void k_nt_line_starts(const unsigned char* __restrict__ text, u64 nbytes,
                                                               u64 nchunks, const u64* __restrict__ coff, u64* lstart) {
-    for (u64 c = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; c < nchunks; c += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 b = c * NT_CHUNK, e = b + NT_CHUNK < nbytes ? b + NT_CHUNK : nbytes;
-        u64 j = coff[c];
-        if (c == 0) lstart[0] = 0;
-        for (u64 i = b; i < e; ++i)
-            if (text[i] == '\n') lstart[++j] = i + 1;
-    }
-}
-
-// per line: the three terms (tstart/tlen per occurrence 3*line+t), valid flag, first malformed line
-__global__ __launch_bounds__(RDF_BLOCK) void k_nt_tokenize(const unsigned char* __restrict__ text, u64 nbytes,
-                                                           const u64* __restrict__ lstart, u64 nlines, int tabs,
-                                                           u64* tstart, u32* tlen, u32* valid, u64* bad_line) {
-    for (u64 l = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; l < nlines; l += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 b = lstart[l];
-        u64 e = l + 1 < nlines ? lstart[l + 1] - 1 : nbytes;  // excludes the '\n'
-        if (l + 1 < nlines && e > b && text[e - 1] == '\r') --e;  // "\r\n" ends a line as one terminator
-        u32 ok = 0;
-        bool blank = true;
-        for (u64 i = b; i < e && blank; ++i) blank = nt_space(text[i]);
-        if (!(b < e && text[b] == '#') && !blank) {
-            u64 ts[3], te[3];
-            int nt = 0;
-            bool err = false;
-            if (tabs) {
-                u64 f = b;
-                for (u64 i = b; i <= e && nt < 3; ++i)
-                    if (i == e || text[i] == '\t') {
-                        ts[nt] = f;
-                        te[nt] = i;
-                        ++nt;
-                        f = i + 1;
-                    }
-                err = nt < 3;
-            } else {
-                u64 i = b;
-                while (nt < 3 && !err) {
-                    while (i < e && nt_space(text[i])) ++i;
-                    if (i >= e) {
-                        err = true;
-                        break;
-                    }
-                    u64 j;
-                    const unsigned char ch = text[i];
-                    if (ch == '<') {
-                        j = i + 1;
-                        while (j < e && text[j] != '>') ++j;
-                        if (j >= e) err = true;
-                        else ++j;
-                    } else if (ch == '"') {
-                        j = i + 1;
-                        while (j < e && text[j] != '"') j += text[j] == '\\' ? 2 : 1;
-                        if (j >= e) err = true;
-                        else {
-                            ++j;
-                            if (j < e && text[j] == '@') {
-                                while (j < e && !nt_space(text[j])) ++j;
-                            } else if (j + 1 < e && text[j] == '^' && text[j + 1] == '^') {
-                                j += 2;
-                                if (j < e && text[j] == '<') {
-                                    while (j < e && text[j] != '>') ++j;
-                                    if (j >= e) err = true;
-                                    else ++j;
-                                } else {
-                                    while (j < e && !nt_space(text[j])) ++j;
-                                }
-                            }
-                        }
-                    } else {
-                        j = i;
-                        while (j < e && !nt_space(text[j])) ++j;
-                    }
-                    if (err) break;
-                    ts[nt] = i;
-                    te[nt] = j;
-                    ++nt;
-                    i = j;
-                }
-            }
-            if (err) atomicMin(bad_line, l);
-            else {
-                ok = 1;
-                for (int t = 0; t < 3; ++t) {
-                    tstart[3 * l + t] = ts[t];
-                    tlen[3 * l + t] = (u32)(te[t] - ts[t]);
-                }
-            }
+    __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
+    if (blockIdx.x == 0 && threadIdx.x == 0) lstart[0] = 0;
+    for (u64 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        u32 m = nt_newline_mask(text, nbytes, c), total;
+        u64 j = coff[c] + block_exclusive_scan_u32(__popc(m), lds_wave, &total);
+        const u64 b = c * NT_CHUNK + threadIdx.x * 16;
+        while (m) {
+            const int k = __ffs(m) - 1;
+            m &= m - 1;
+            lstart[++j] = b + k + 1;
         }
-        valid[l] = ok;
     }
 }
 
-__device__ inline u64 nt_hash(const unsigned char* __restrict__ s, u32 n) {
+struct NtGlobal {
+    const unsigned char* t;
+    __device__ unsigned char operator[](u64 i) const { return t[i]; }
+};
+struct NtLds {
+    const unsigned char* tile;
+    u64 base;
+    __device__ unsigned char operator[](u64 i) const { return tile[i - base]; }
+};
+
+// one line [b, e): its three terms, or false (malformed)
+template <typename Src>
+__device__ inline bool nt_parse_line(Src text, u64 b, u64 e, int tabs, u64* ts, u64* te) {
+    int nt = 0;
+    if (tabs) {
+        u64 f = b;
+        for (u64 i = b; i <= e && nt < 3; ++i)
+            if (i == e || text[i] == '\t') {
+                ts[nt] = f;
+                te[nt] = i;
+                ++nt;
+                f = i + 1;
+            }
+        return nt == 3;
+    }
+    u64 i = b;
+    while (nt < 3) {
+        while (i < e && nt_space(text[i])) ++i;
+        if (i >= e) return false;
+        u64 j;
+        const unsigned char ch = text[i];
+        if (ch == '<') {
+            j = i + 1;
+            while (j < e && text[j] != '>') ++j;
+            if (j >= e) return false;
+            ++j;
+        } else if (ch == '"') {
+            j = i + 1;
+            while (j < e && text[j] != '"') j += text[j] == '\\' ? 2 : 1;
+            if (j >= e) return false;
+            ++j;
+            if (j < e && text[j] == '@') {
+                while (j < e && !nt_space(text[j])) ++j;
+            } else if (j + 1 < e && text[j] == '^' && text[j + 1] == '^') {
+                j += 2;
+                if (j < e && text[j] == '<') {
+                    while (j < e && text[j] != '>') ++j;
+                    if (j >= e) return false;
+                    ++j;
+                } else {
+                    while (j < e && !nt_space(text[j])) ++j;
+                }
+            }
+        } else {
+            j = i;
+            while (j < e && !nt_space(text[j])) ++j;
+        }
+        ts[nt] = i;
+        te[nt] = j;
+        ++nt;
+        i = j;
+    }
+    return true;
+}
+
+template <typename Src>
+__device__ inline u64 nt_hash(Src s, u64 a, u32 n) {
     u64 h = 0x243F6A8885A308D3ull ^ n;
     u32 i = 0;
     for (; i + 8 <= n; i += 8) {
         u64 w = 0;
-        for (int k = 0; k < 8; ++k) w |= (u64)s[i + k] << (8 * k);
+        for (int k = 0; k < 8; ++k) w |= (u64)s[a + i + k] << (8 * k);
         h = mix64(h ^ w);
     }
     u64 w = 0;
-    for (int k = 0; i + k < n; ++k) w |= (u64)s[i + k] << (8 * k);
+    for (int k = 0; i + k < n; ++k) w |= (u64)s[a + i + k] << (8 * k);
     return mix64(h ^ w ^ 0x9E3779B97F4A7C15ull);
+}
+
+template <typename Src>
+__device__ inline u32 nt_line(Src text, u64 b, u64 e, u64 l, int tabs, u64* tstart, u32* tlen, u64* hv, u64* bad_line) {
+    bool blank = true;
+    for (u64 i = b; i < e && blank; ++i) blank = nt_space(text[i]);
+    if ((b < e && text[b] == '#') || blank) return 0;
+    u64 ts[3], te[3];
+    if (!nt_parse_line(text, b, e, tabs, ts, te)) {
+        atomicMin(bad_line, l);
+        return 0;
+    }
+    for (int t = 0; t < 3; ++t) {
+        tstart[3 * l + t] = ts[t];
+        tlen[3 * l + t] = (u32)(te[t] - ts[t]);
+        hv[3 * l + t] = nt_hash(text, ts[t], (u32)(te[t] - ts[t]));
+    }
+    return 1;
+}
+
+// per line: the three terms (tstart/tlen per occurrence 3*line+t), valid flag, first malformed line.  A block's
+// RDF_BLOCK consecutive lines are one contiguous byte span: it is copied into LDS with coalesced 4-B loads and
+// each lane parses its line from there (spans over NT_TILE bytes parse from global memory).
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_tokenize(const unsigned char* __restrict__ text, u64 nbytes,
+                                                           const u64* __restrict__ lstart, u64 nlines, int tabs,
+                                                           u64* tstart, u32* tlen, u64* hv, u32* valid, u64* bad_line) {
+    __shared__ u32 tile[NT_TILE / 4 + 2];
+    for (u64 l0 = (u64)blockIdx.x * RDF_BLOCK; l0 < nlines; l0 += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 l1 = l0 + RDF_BLOCK < nlines ? l0 + RDF_BLOCK : nlines;
+        const u64 b0 = lstart[l0], b1 = l1 < nlines ? lstart[l1] : nbytes;
+        const u64 w0 = b0 & ~3ull, nw = (b1 - w0 + 3) / 4;
+        const bool in_lds = nw <= NT_TILE / 4;
+        __syncthreads();
+        if (in_lds)
+            for (u64 w = threadIdx.x; w < nw; w += RDF_BLOCK) tile[w] = *(const u32*)(text + w0 + 4 * w);
+        __syncthreads();
+        const u64 l = l0 + threadIdx.x;
+        if (l < l1) {
+            const u64 b = lstart[l];
+            u64 e = l + 1 < nlines ? lstart[l + 1] - 1 : nbytes;  // excludes the '\n'
+            u32 ok;
+            if (in_lds) {
+                NtLds src{(const unsigned char*)tile, w0};
+                if (l + 1 < nlines && e > b && src[e - 1] == '\r') --e;  // "\r\n" ends a line as one terminator
+                ok = nt_line(src, b, e, l, tabs, tstart, tlen, hv, bad_line);
+            } else {
+                NtGlobal src{text};
+                if (l + 1 < nlines && e > b && src[e - 1] == '\r') --e;
+                ok = nt_line(src, b, e, l, tabs, tstart, tlen, hv, bad_line);
+            }
+            valid[l] = ok;
+        }
+    }
 }
 
 __device__ inline bool nt_equal(const unsigned char* __restrict__ text, u64 a, u64 b, u32 n) {
@@ -2374,14 +2429,13 @@ __device__ inline bool nt_equal(const unsigned char* __restrict__ text, u64 a, u
 // dictionary table: entries fingerprint<<32 | occurrence; the slot of a term ends holding its first occurrence
 __global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_insert(const unsigned char* __restrict__ text,
                                                               const u64* __restrict__ tstart, const u32* __restrict__ tlen,
-                                                              const u32* __restrict__ valid, u64 nocc, u64* hv,
-                                                              u64* table, u64 mask) {
+                                                              const u32* __restrict__ valid, u64 nocc,
+                                                              const u64* __restrict__ hv, u64* table, u64 mask, u32* slot) {
     for (u64 k = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; k < nocc; k += (u64)gridDim.x * RDF_BLOCK) {
         if (!valid[k / 3]) continue;
         const u64 a = tstart[k];
         const u32 n = tlen[k];
-        const u64 h0 = nt_hash(text + a, n);
-        hv[k] = h0;
+        const u64 h0 = hv[k];
         const u64 e = (h0 & 0xffffffff00000000ull) | k;
         u64 h = h0 & mask;
         for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
@@ -2398,32 +2452,18 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_insert(const unsigned cha
                 }
             }
         }
+        slot[k] = (u32)h;  // the term's slot: after the pass it holds the term's first occurrence
     }
 }
 
 // per occurrence: its term's first occurrence (rep) and whether it is that first occurrence
-__global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_rep(const unsigned char* __restrict__ text,
-                                                           const u64* __restrict__ tstart, const u32* __restrict__ tlen,
-                                                           const u32* __restrict__ valid, u64 nocc,
-                                                           const u64* __restrict__ hv, const u64* __restrict__ table,
-                                                           u64 mask, u32* rep, u32* first) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_rep(const u32* __restrict__ valid, u64 nocc,
+                                                           const u32* __restrict__ slot, const u64* __restrict__ table,
+                                                           u32* rep, u32* first) {
     for (u64 k = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; k < nocc; k += (u64)gridDim.x * RDF_BLOCK) {
         u32 r = (u32)k, f = 0;
         if (valid[k / 3]) {
-            const u64 h0 = hv[k], a = tstart[k];
-            const u32 n = tlen[k];
-            u64 h = h0 & mask;
-            for (u64 probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
-                const u64 cur = table[h];
-                if (cur == EMPTY64) break;  // unreachable
-                if ((cur >> 32) == (h0 >> 32)) {
-                    const u32 j = (u32)cur;
-                    if (j == (u32)k || (tlen[j] == n && nt_equal(text, tstart[j], a, n))) {
-                        r = j;
-                        break;
-                    }
-                }
-            }
+            r = (u32)table[slot[k]];
             f = r == (u32)k;
         }
         rep[k] = r;

@@ -30,7 +30,7 @@ struct rdf_ctx {
     // triples
     DevBuf ts, tp, to;
     DevBuf dtab, dkeep, dpos, xs, xp, xo;
-    DevBuf ntext, ncnt, ncoff, nlstart, ntstart, ntlen, nvalid, nlpos, nhv, ntab, nrep, nfirst, nfid, nterm_off, nterm_len;
+    DevBuf ntext, ncnt, ncoff, nlstart, ntstart, ntlen, nvalid, nlpos, nhv, nslot, ntab, nrep, nfirst, nfid, nterm_off, nterm_len;
     u64 n_terms_parsed = 0;  // rows of nterm_off/nterm_len (rdf_copy_terms)  // --distinct-triples: slot table, keep flags, positions, compacted copy
     const u32 *s = nullptr, *p = nullptr, *o = nullptr;
     u64 n = 0;
@@ -412,14 +412,14 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t st = c->stream;
     const unsigned char* dtext = nullptr;
-    ENSURE(c, ntext, nbytes + 1);
+    ENSURE(c, ntext, nbytes + 16);  // 16-B loads of the last tile stay inside the buffer
     if (nbytes) HIP_TRY(c, hipMemcpyAsync(c->ntext.p, text, nbytes, hipMemcpyHostToDevice, st));
     dtext = (const unsigned char*)c->ntext.p;
     HIP_TRY(c, hipEventRecord(c->ev[6], st));
     const u64 nchunks = std::max<u64>((nbytes + NT_CHUNK - 1) / NT_CHUNK, 1);
     ENSURE(c, ncnt, nchunks * 4);
     ENSURE(c, ncoff, nchunks * 8);
-    const unsigned gc = grid_for(nchunks, RDF_BLOCK, kGrid);
+    const unsigned gc = (unsigned)std::min<u64>(nchunks, kGrid);  // one block per tile
     hipLaunchKernelGGL(k_nt_count_lines, dim3(gc), dim3(RDF_BLOCK), 0, st, dtext, nbytes, nchunks, c->ncnt.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ncnt.as<u32>(), c->ncoff.as<u64>(), nchunks, dscal(c, 0), st));
     u64 newlines = 0;
@@ -431,28 +431,29 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
     hipLaunchKernelGGL(k_nt_line_starts, dim3(gc), dim3(RDF_BLOCK), 0, st, dtext, nbytes, nchunks, c->ncoff.as<u64>(),
                        c->nlstart.as<u64>());
     ENSURE(c, ntstart, nocc * 8);
+    ENSURE(c, nhv, nocc * 8);
     ENSURE(c, ntlen, nocc * 4);
     ENSURE(c, nvalid, nlines * 4);
     ENSURE(c, nlpos, nlines * 4);
     HIP_TRY(c, hipMemsetAsync(dscal(c, 1), 0xff, 8, st));
     const unsigned gl = grid_for(nlines, RDF_BLOCK, kGrid), go = grid_for(nocc, RDF_BLOCK, kGrid);
     hipLaunchKernelGGL(k_nt_tokenize, dim3(gl), dim3(RDF_BLOCK), 0, st, dtext, nbytes, c->nlstart.as<u64>(), nlines,
-                       (int)(flags & RDF_NT_TABS), c->ntstart.as<u64>(), c->ntlen.as<u32>(), c->nvalid.as<u32>(),
-                       dscal(c, 1));
+                       (int)(flags & RDF_NT_TABS), c->ntstart.as<u64>(), c->ntlen.as<u32>(), c->nhv.as<u64>(),
+                       c->nvalid.as<u32>(), dscal(c, 1));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 2), 0, 8, st));
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->nvalid.as<u32>(), c->nlpos.as<u32>(), nlines, (u32*)dscal(c, 2), st));
     const u64 T = next_pow2(2 * nocc);
+    if (T > (1ull << 32)) return fail(c, RDF_ERR_LIMIT, "too many terms per parse call (split the input)");
     ENSURE(c, ntab, T * 8);
-    ENSURE(c, nhv, nocc * 8);
+    ENSURE(c, nslot, nocc * 4);
     ENSURE(c, nrep, nocc * 4);
     ENSURE(c, nfirst, nocc * 4);
     ENSURE(c, nfid, nocc * 4);
     HIP_TRY(c, hipMemsetAsync(c->ntab.p, 0xff, T * 8, st));
     hipLaunchKernelGGL(k_nt_dict_insert, dim3(go), dim3(RDF_BLOCK), 0, st, dtext, c->ntstart.as<u64>(), c->ntlen.as<u32>(),
-                       c->nvalid.as<u32>(), nocc, c->nhv.as<u64>(), c->ntab.as<u64>(), T - 1);
-    hipLaunchKernelGGL(k_nt_dict_rep, dim3(go), dim3(RDF_BLOCK), 0, st, dtext, c->ntstart.as<u64>(), c->ntlen.as<u32>(),
-                       c->nvalid.as<u32>(), nocc, c->nhv.as<u64>(), c->ntab.as<u64>(), T - 1, c->nrep.as<u32>(),
-                       c->nfirst.as<u32>());
+                       c->nvalid.as<u32>(), nocc, c->nhv.as<u64>(), c->ntab.as<u64>(), T - 1, c->nslot.as<u32>());
+    hipLaunchKernelGGL(k_nt_dict_rep, dim3(go), dim3(RDF_BLOCK), 0, st, c->nvalid.as<u32>(), nocc, c->nslot.as<u32>(),
+                       c->ntab.as<u64>(), c->nrep.as<u32>(), c->nfirst.as<u32>());
     HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 8, st));
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->nfirst.as<u32>(), c->nfid.as<u32>(), nocc, (u32*)dscal(c, 3), st));
     u64 sc[3];

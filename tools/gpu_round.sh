@@ -65,6 +65,12 @@ for step in "$@"; do
       timeout -k 10 400 python -u tools/parse_bench.py > gpurun_out/parse_$TAG.log 2>&1 \
         || { echo "parse failed"; tail -30 gpurun_out/parse_$TAG.log; exit 1; }
       grep -E "PARSE|text" gpurun_out/parse_$TAG.log ;;
+    pprof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/pprof_$TAG -o run --output-format csv \
+        -- python3 tools/parse_bench.py > gpurun_out/pprof_$TAG.log 2>&1 \
+        || { echo "parse prof failed"; tail -30 gpurun_out/pprof_$TAG.log; exit 1; }
+      find gpurun_out/pprof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/pprof_$TAG.kernel_stats.csv \;
+      grep -E "k_nt|scan" gpurun_out/pprof_$TAG.kernel_stats.csv | cut -c1-40,150- ;;
     gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
         > gpurun_out/gtest_$TAG.log 2>&1 || { echo "gtest failed"; tail -30 gpurun_out/gtest_$TAG.log; exit 1; }
