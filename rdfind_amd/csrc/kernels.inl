@@ -2420,9 +2420,24 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_nt_tokenize(const unsigned char* 
     }
 }
 
+// 4 text bytes starting at byte offset a, from aligned 4-B loads (the buffer is padded by 16 bytes)
+__device__ inline u32 nt_word(const u32* __restrict__ w, u64 a) {
+    const u64 i = a >> 2;
+    const u32 sh = (u32)(a & 3) * 8;
+    const u32 lo = w[i];
+    return sh ? (u32)((((u64)w[i + 1] << 32) | lo) >> sh) : lo;
+}
+
+// byte equality of text[a, a+n) and text[b, b+n), four bytes per step
 __device__ inline bool nt_equal(const unsigned char* __restrict__ text, u64 a, u64 b, u32 n) {
-    for (u32 i = 0; i < n; ++i)
-        if (text[a + i] != text[b + i]) return false;
+    const u32* w = (const u32*)text;
+    u32 i = 0;
+    for (; i + 4 <= n; i += 4)
+        if (nt_word(w, a + i) != nt_word(w, b + i)) return false;
+    if (i < n) {
+        const u32 m = (1u << (8 * (n - i))) - 1u;
+        if ((nt_word(w, a + i) ^ nt_word(w, b + i)) & m) return false;
+    }
     return true;
 }
 
