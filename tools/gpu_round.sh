@@ -25,7 +25,7 @@ for step in "$@"; do
       for cfg in "c1 1.0" "c3 0.5" "c5 0.1" "c5 0.3"; do
         set -- $cfg
         echo "config $1 scale $2" >&2
-        timeout -k 10 400 python -u bench.py --config $1 --scale $2 --steps 3 --warmup 1 --no-cpu-baseline \
+        timeout -k 10 400 python -u bench.py --config $1 --scale $2 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest \
           > gpurun_out/cfg_${TAG}_$1.json 2> gpurun_out/cfg_${TAG}_$1.err \
           || { echo "config $1 failed"; tail -20 gpurun_out/cfg_${TAG}_$1.err; exit 1; }
         cat gpurun_out/cfg_${TAG}_$1.json
@@ -33,7 +33,7 @@ for step in "$@"; do
     cprof:*)  # cprof:<config>:<scale> -- kernel stats of one step of another BASELINE shape
       IFS=: read -r _ CFG SC <<< "$step"
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/cprof_${TAG}_$CFG -o run --output-format csv \
-        -- python3 bench.py --config $CFG --scale $SC --steps 2 --warmup 1 --no-cpu-baseline \
+        -- python3 bench.py --config $CFG --scale $SC --steps 2 --warmup 1 --no-cpu-baseline --no-ingest \
         > gpurun_out/cprof_${TAG}_$CFG.log 2>&1 \
         || { echo "cprof $CFG failed"; tail -30 gpurun_out/cprof_${TAG}_$CFG.log; exit 1; }
       find gpurun_out/cprof_${TAG}_$CFG -name "*kernel_stats.csv" -exec cp {} gpurun_out/cprof_${TAG}_$CFG.kernel_stats.csv \;
