@@ -133,6 +133,9 @@ rdf_status rdf_distinct_triples(rdf_ctx* ctx, uint64_t* n_distinct, float* ms);
 #define RDF_NT_TABS 1u                 /* --tabs: tab-separated terms */
 rdf_status rdf_parse_ntriples(rdf_ctx* ctx, const char* text, uint64_t nbytes, uint32_t flags, uint64_t* n_triples,
                               uint32_t* num_terms, float* ms);
+/* Uses the dictionary of the last rdf_parse_ntriples as the formatting dictionary (rdf_set_dictionary without a
+ * host round trip); RDF_ERR_STATE if triples were set another way since. */
+rdf_status rdf_set_dictionary_parsed(rdf_ctx* ctx);
 /* The dictionary of the last rdf_parse_ntriples: term id i is text[offsets[i] .. offsets[i] + lengths[i]). */
 rdf_status rdf_copy_terms(rdf_ctx* ctx, uint64_t* offsets, uint32_t* lengths, uint64_t cap, uint64_t* n_copied);
 

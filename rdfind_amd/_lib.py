@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_cinds_range", "rdf_cind_checksum", "rdf_last_stats", "rdf_shard_begin", "rdf_shard_step",
     "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
     "rdf_distinct_triples", "rdf_copy_triples", "rdf_parse_ntriples", "rdf_copy_terms",
+    "rdf_set_dictionary_parsed",
 )
 RDF_NT_TABS = 1
 
@@ -106,6 +107,7 @@ def load():
         "rdf_parse_ntriples": (i32, [P, ctypes.c_char_p, u64, u32, ctypes.POINTER(u64), ctypes.POINTER(u32),
                                      ctypes.POINTER(ctypes.c_float)]),
         "rdf_copy_terms": (i32, [P, P, P, u64, ctypes.POINTER(u64)]),
+        "rdf_set_dictionary_parsed": (i32, [P]),
         "rdf_frequent_conditions": (i32, [P, u32, ctypes.POINTER(FcStats)]),
         "rdf_build_capture_groups": (i32, [P, ctypes.c_char_p, ctypes.POINTER(GroupStats)]),
         "rdf_discover_cinds": (i32, [P, u32, ctypes.POINTER(CindStats)]),
@@ -230,6 +232,10 @@ class Context:
         pos = np.arange(int(offsets[-1]), dtype=np.int64) + np.repeat(off.astype(np.int64) - offsets[:-1].astype(np.int64),
                                                                        ln64)
         return src[pos].tobytes(), offsets
+
+    def set_dictionary_parsed(self):
+        """The last parse's dictionary becomes the formatting dictionary, in HBM (rdf_set_dictionary_parsed)."""
+        self._check(self.lib.rdf_set_dictionary_parsed(self.ptr), "rdf_set_dictionary_parsed")
 
     def set_dictionary_heap(self, heap: bytes, offsets):
         """rdf_set_dictionary from a ready heap + offsets (e.g. :meth:`parsed_terms`)."""

@@ -2507,3 +2507,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_nt_assign(const u64* __restrict__
 }
 
 }  // namespace rdf
+
+namespace rdf {
+
+// parsed dictionary -> the formatter's contiguous term heap (term i at heap[off[i], off[i+1]))
+__global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_gather(const unsigned char* __restrict__ text,
+                                                              const u64* __restrict__ term_off,
+                                                              const u64* __restrict__ hoff, u64 V, char* heap) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < V; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 a = term_off[i], b = hoff[i], n = hoff[i + 1] - b;
+        for (u64 k = 0; k < n; ++k) heap[b + k] = (char)text[a + k];
+    }
+}
+
+}  // namespace rdf

@@ -29,9 +29,11 @@ struct rdf_ctx {
 
     // triples
     DevBuf ts, tp, to;
-    DevBuf dtab, dkeep, dpos, xs, xp, xo;
+    DevBuf dtab, dkeep, dpos, xs, xp, xo;  // --distinct-triples: slot table, keep flags, positions, compacted copy
+    // N-Triples ingest: text, line/term arrays, dictionary table, term table
     DevBuf ntext, ncnt, ncoff, nlstart, ntstart, ntlen, nvalid, nlpos, nhv, nslot, ntab, nrep, nfirst, nfid, nterm_off, nterm_len;
-    u64 n_terms_parsed = 0;  // rows of nterm_off/nterm_len (rdf_copy_terms)  // --distinct-triples: slot table, keep flags, positions, compacted copy
+    u64 n_terms_parsed = 0;  // rows of nterm_off/nterm_len (rdf_copy_terms)
+    bool parsed_dict = false;  // the resident triples' ids are the last parse's dictionary
     const u32 *s = nullptr, *p = nullptr, *o = nullptr;
     u64 n = 0;
     u32 V = 0;
@@ -321,6 +323,7 @@ rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, con
     c->n = n;
     c->V = num_terms;
     c->stage = 1;
+    c->parsed_dict = false;
     return RDF_OK;
 }
 
@@ -335,6 +338,7 @@ rdf_status rdf_set_triples_device(rdf_ctx* c, const uint32_t* s, const uint32_t*
     c->n = n;
     c->V = num_terms;
     c->stage = 1;
+    c->parsed_dict = false;
     return RDF_OK;
 }
 
@@ -483,6 +487,7 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
     c->V = (u32)V;
     c->stage = 1;
     c->n_terms_parsed = V;
+    c->parsed_dict = true;
     if (n_triples) *n_triples = n;
     if (num_terms) *num_terms = (u32)V;
     return RDF_OK;
@@ -1850,6 +1855,29 @@ rdf_status rdf_set_dictionary(rdf_ctx* c, const char* heap, uint64_t heap_bytes,
     if (heap_bytes) HIP_TRY(c, hipMemcpy(c->dheap.p, heap, heap_bytes, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->dtoff.p, offsets, (n_terms + 1) * 8, hipMemcpyHostToDevice));
     c->dict_terms = n_terms;
+    c->capstr_run = ~0ull;
+    return RDF_OK;
+}
+
+// The dictionary of the last rdf_parse_ntriples as the formatting dictionary, built in HBM (no host copy).
+rdf_status rdf_set_dictionary_parsed(rdf_ctx* c) {
+    if (!c) return RDF_ERR_ARG;
+    if (!c->parsed_dict) return fail(c, RDF_ERR_STATE, "the resident triples do not come from rdf_parse_ntriples");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const u64 V = c->n_terms_parsed;
+    ENSURE(c, dtoff, (V + 1) * 8);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nterm_len.as<u32>(), c->dtoff.as<u64>(), V, c->dtoff.as<u64>() + V, st));
+    u64 total = 0;
+    TRY(read_u64(c, c->dtoff.as<u64>() + V, &total));
+    ENSURE(c, dheap, std::max<u64>(total, 1));
+    if (V)
+        hipLaunchKernelGGL(k_nt_dict_gather, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           (const unsigned char*)c->ntext.p, c->nterm_off.as<u64>(), c->dtoff.as<u64>(), V,
+                           c->dheap.as<char>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->dict_terms = V;
     c->capstr_run = ~0ull;
     return RDF_OK;
 }

@@ -136,7 +136,7 @@ class RDFind:
             t2 = time.time()
             n = ctx.cind_count()
             if dic is None:
-                ctx.set_dictionary_heap(*ctx.parsed_terms())
+                ctx.set_dictionary_parsed()  # device dictionary straight into the formatter
             else:
                 ctx.set_dictionary(dic.terms)
             keep_lines = n <= KEEP_LINES_MAX or a.collect_result or a.debug_level >= 3

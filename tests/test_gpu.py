@@ -375,3 +375,20 @@ def test_device_parser_rejects_malformed_line(ctx):
         ctx.parse_ntriples(b"<a> <p> <b> .\n<a> <p> \"unterminated .\n")
     with pytest.raises(_lib.RdfError, match="line 1"):
         ctx.parse_ntriples(b"<a> <p>\n")
+
+
+def test_parsed_dictionary_formatting(ctx, tmp_path):
+    """rdf_set_dictionary_parsed (the parse's dictionary built into the formatter in HBM) formats the same bytes
+    as the host-uploaded dictionary; it is refused once triples were set another way."""
+    data = "".join(ln + "\n" for ln in synth.config("c1", 0.05).lines()).encode()
+    ctx.parse_ntriples(data)
+    ctx.run(5)
+    heap, offsets = ctx.parsed_terms()
+    ctx.set_dictionary_heap(heap, offsets)
+    host = ctx.format_array(0, 1 << 20).tobytes()
+    ctx.set_dictionary_parsed()
+    dev = ctx.format_array(0, 1 << 20).tobytes()
+    assert dev == host and len(dev) > 0
+    ctx.set_triples(np.zeros(1, np.uint32), np.zeros(1, np.uint32), np.zeros(1, np.uint32), 1)
+    with pytest.raises(_lib.RdfError, match="rdf_parse_ntriples"):
+        ctx.set_dictionary_parsed()
