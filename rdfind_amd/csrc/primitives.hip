@@ -117,6 +117,35 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply(const TI* __restrict__
     }
 }
 
+// small inputs (a few tiles): one block scans in -> out with a running carry (one launch instead of three)
+template <typename TI, typename TO>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* __restrict__ in, TO* __restrict__ out, u64 n,
+                                                          TO* __restrict__ grand_total) {
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    TO carry = 0;
+    for (u64 base = 0; base < n; base += SCAN_TILE) {
+        TO v[SCAN_ITEMS];
+        TO local = 0;
+        const u64 tb = base + (u64)threadIdx.x * SCAN_ITEMS;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            v[i] = (tb + i < n) ? (TO)in[tb + i] : (TO)0;
+            local += v[i];
+        }
+        TO total;
+        TO off = block_exclusive_scan<TO>(local, lds_wave, &total) + carry;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            if (tb + i < n) out[tb + i] = off;
+            off += v[i];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0 && grand_total) *grand_total = carry;
+}
+
+static constexpr u64 SCAN_SMALL_TILES = 4;
+
 template <typename TI, typename TO>
 static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 n, TO* d_total, hipStream_t st) {
     if (n == 0) {
@@ -124,6 +153,10 @@ static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 
         return hipSuccess;
     }
     u64 tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (tiles <= SCAN_SMALL_TILES) {
+        hipLaunchKernelGGL((k_scan_small<TI, TO>), dim3(1), dim3(RDF_BLOCK), 0, st, in, out, n, d_total);
+        return hipGetLastError();
+    }
     TO* sums = (TO*)ws.scratch(tiles * sizeof(TO), 0);
     if (!sums) return hipErrorOutOfMemory;
     hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, n, sums);
