@@ -392,3 +392,13 @@ def test_parsed_dictionary_formatting(ctx, tmp_path):
     ctx.set_triples(np.zeros(1, np.uint32), np.zeros(1, np.uint32), np.zeros(1, np.uint32), 1)
     with pytest.raises(_lib.RdfError, match="rdf_parse_ntriples"):
         ctx.set_dictionary_parsed()
+
+
+@pytest.mark.parametrize("name", ["lubm_small", "skew_small"])
+def test_program_host_parser_reproduces_golden(tmp_path, name):
+    """--host-parser (host tokenizer + dictionary) gives the same output as the default device ingest."""
+    ms, expected = read_golden(name, "s1_clean")
+    out = tmp_path / "cinds.txt"
+    program.RDFind(["--use-fis", "--clean-implied", "--host-parser", "--support", str(ms), "--output", f"file://{out}",
+                    os.path.join(GOLDEN, f"{name}.nt.gz")]).run()
+    assert sorted(out.read_text().splitlines()) == expected
