@@ -2241,7 +2241,7 @@ namespace rdf {
 // Whitespace is ASCII (" \t\n\v\f\r" and 0x1c-0x1f, the ASCII part of Python's str.isspace).
 
 static constexpr u32 NT_CHUNK = RDF_BLOCK * 16;  // bytes per block tile in the line-start passes (16 per thread)
-static constexpr u32 NT_TILE = 61440;           // LDS bytes for one block's lines in the tokenizer (2 blocks per CU)
+static constexpr u32 NT_TILE = 49152;           // LDS bytes for one block's lines in the tokenizer (3 blocks per CU)
 
 __device__ inline bool nt_space(unsigned char ch) {
     return ch == ' ' || (ch >= 9 && ch <= 13) || (ch >= 0x1c && ch <= 0x1f);
