@@ -81,6 +81,8 @@ typedef struct {
     uint64_t n_class_members;       /* unary dependents whose groups are all heavy (emitted per mask class) */
     uint64_t n_classes;             /* distinct heavy bitmasks among them */
     uint64_t n_class_cinds;         /* CINDs emitted by the class path */
+    uint64_t n_light_candidates;    /* pivot members of dependents with light groups (intersection candidates) */
+    uint64_t n_light_entries;       /* (dependent, group) entries of those dependents */
 } rdf_cind_stats;
 
 /* Kernel-family device timers (HIP events on the context stream), see rdf_kernel_times. */
@@ -155,9 +157,34 @@ rdf_status rdf_cind_count(rdf_ctx* ctx, uint64_t* n);
 /* Copies min(cap, count) rows to host memory; *n_copied receives the number copied. */
 rdf_status rdf_copy_cinds(rdf_ctx* ctx, rdf_cind* out, uint64_t cap, uint64_t* n_copied);
 
+/* The result as CindSet-shaped id-records (4 B per CIND): refs[n_refs] (compact capture ids), the run table
+ * (run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]; runoff has n_runs + 1 entries) and, per
+ * compact capture id, its external capture id (see rdf_decode_capture) and support.  Null pointers skip a part;
+ * pinned host memory lets the copies run at the link rate. */
+rdf_status rdf_result_sizes(rdf_ctx* ctx, uint64_t* n_refs, uint64_t* n_runs, uint64_t* n_captures);
+rdf_status rdf_copy_result_raw(rdf_ctx* ctx, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* capture_ids,
+                               uint32_t* supports);
+
+/* One result row in the reference's Cind shape (ALG/data/Cind.scala:12-15: depCaptureType, depConditionValue1/2,
+ * refCaptureType, refConditionValue1/2, support), with term ids for the condition values; value2 = UINT32_MAX
+ * stands for the reference's null (unary capture).  Seven uint32 fields, no padding. */
+typedef struct {
+    uint32_t dep_capture_type;
+    uint32_t dep_value1;
+    uint32_t dep_value2;
+    uint32_t ref_capture_type;
+    uint32_t ref_value1;
+    uint32_t ref_value2;
+    uint32_t support;
+} rdf_cind_row;
+/* Decoded rows [offset, offset+count) of the result (clipped), decoded on the device; *n_copied receives the number
+ * copied.  This is what a JNI/FFI caller turns into Cind objects (no capture-id arithmetic on the caller side). */
+rdf_status rdf_copy_cinds_decoded(rdf_ctx* ctx, uint64_t offset, rdf_cind_row* out, uint64_t count, uint64_t* n_copied);
+
 /* Copies rows [offset, offset+count) of the result (clipped); *n_copied receives the number copied. */
 rdf_status rdf_copy_cinds_range(rdf_ctx* ctx, uint64_t offset, rdf_cind* out, uint64_t count, uint64_t* n_copied);
-/* Order-independent checksum of the result set (sum of a 64-bit mix of (dep, ref) capture ids). */
+/* Order-independent checksum of the result set: sum over rows of mix64(((dep << 32) | ref) + support * 0x9E3779B97F4A7C15)
+ * (external capture ids; the C oracle's streamed mode computes the same sum without materializing rows). */
 rdf_status rdf_cind_checksum(rdf_ctx* ctx, uint64_t* checksum);
 
 /* Capture ids: unary type t (codes 10,12,17,20,33,34) with value v -> t*V + v; binary capture b
@@ -235,6 +262,8 @@ rdf_status rdf_stage_times(rdf_ctx* ctx, float* ms3);
 rdf_status rdf_kernel_times(rdf_ctx* ctx, float* ms, int count);
 /* Synchronise the context stream. */
 rdf_status rdf_sync(rdf_ctx* ctx);
+/* Device memory (bytes) the context holds right now (its HBM buffers and scratch). */
+rdf_status rdf_device_bytes(rdf_ctx* ctx, uint64_t* bytes);
 
 #ifdef __cplusplus
 }

@@ -155,14 +155,32 @@ static void binary_components(int bt, int *t1, int *t2) {
     *t2 = unary_index(rest | second);
 }
 
-/* ---------------------------------------------------------------- main */
+/* ---------------------------------------------------------------- stages 1-4 */
 
-int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n, uint32_t V,
-            uint32_t ms, int strategy, int clean, const char *projection,
-            orc_cind **out, uint64_t *n_out, uint64_t **bin_keys_out, uint64_t *n_bin_out,
-            orc_stats *st) {
+/* capture groups + dependent -> groups CSR of one input (stages 1-4) */
+typedef struct {
+    uint32_t V, ms;
+    uint64_t nb;          /* frequent binary conditions (sorted keys) */
+    uint64_t *bkeys;
+    uint64_t ncap, ng;    /* capture id space 6V + nb; groups */
+    uint32_t *support;    /* [ncap + 1] distinct join values per capture */
+    uint64_t *goff;       /* [ng + 1] */
+    uint32_t *gcap;       /* group members, ascending capture ids */
+    uint64_t *doff;       /* [ncap + 1] groups of each frequent capture */
+    uint32_t *dgrp;
+} orc_csr;
+
+static void csr_free(orc_csr *c) {
+    free(c->support); free(c->goff); free(c->gcap); free(c->doff); free(c->dgrp);
+}
+
+static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n, uint32_t V, uint32_t ms,
+                const char *projection, orc_csr *c, orc_stats *st) {
     memset(st, 0, sizeof(*st));
+    memset(c, 0, sizeof(*c));
     if (V >= (1u << 31)) return -1;
+    c->V = V;
+    c->ms = ms;
     int proj_s = strchr(projection, 's') != NULL;
     int proj_p = strchr(projection, 'p') != NULL;
     int proj_o = strchr(projection, 'o') != NULL;
@@ -265,9 +283,9 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
     /* transposed: capture -> groups (only captures with support >= ms can be dependents) */
     uint64_t *doff = (uint64_t *)xmalloc((ncap + 1) * sizeof(uint64_t));
     uint64_t acc = 0;
-    for (uint64_t c = 0; c < ncap; ++c) {
-        doff[c] = acc;
-        if (support[c] >= ms) { acc += support[c]; st->n_freq_captures++; }
+    for (uint64_t cc = 0; cc < ncap; ++cc) {
+        doff[cc] = acc;
+        if (support[cc] >= ms) { acc += support[cc]; st->n_freq_captures++; }
     }
     doff[ncap] = acc;
     uint32_t *dgrp = (uint32_t *)xmalloc(acc * sizeof(uint32_t));
@@ -277,18 +295,131 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
         for (uint64_t i = goff[g]; i < goff[g + 1]; ++i)
             if (support[gcap[i]] >= ms) dgrp[cur[gcap[i]]++] = (uint32_t)g;
     free(cur);
+    c->nb = nb; c->bkeys = bkeys; c->ncap = ncap; c->ng = ng; c->support = support;
+    c->goff = goff; c->gcap = gcap; c->doff = doff; c->dgrp = dgrp;
+    return 0;
+}
 
-    /* 5. per dependent: ref set = intersection over its groups of (group \ implied)
-     *    (CreateAllCindCandidates.scala:106-121 + IntersectCindCandidates.scala:40-43).
-     *    Dependents are split into chunks processed by OpenMP threads; each chunk's CINDs go to its own
-     *    buffer and the buffers are concatenated in chunk (= dependent) order. */
+/* ---------------------------------------------------------------- stage 5: raw refs of one dependent */
+
+typedef struct { uint32_t *refs, *tmp; uint64_t cap; } refbuf;
+
+static void refbuf_free(refbuf *b) { free(b->refs); free(b->tmp); b->refs = b->tmp = NULL; b->cap = 0; }
+
+/* unary components (capture ids) of binary capture x >= 6V */
+static void comps_of(const orc_csr *c, uint64_t x, uint32_t *c1, uint32_t *c2) {
+    uint64_t key = c->bkeys[x - 6ull * c->V];
+    int t1, t2;
+    binary_components((int)(key >> 62), &t1, &t2);
+    *c1 = (uint32_t)((uint64_t)t1 * c->V + ((key >> 31) & 0x7fffffff));
+    *c2 = (uint32_t)((uint64_t)t2 * c->V + (key & 0x7fffffff));
+}
+
+static uint64_t lower_bound_u32(const uint32_t *a, uint64_t n, uint32_t key) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+/* Raw ref set of dependent a (support >= ms), sorted ascending, in b->refs; returns its size.
+ * ref set = intersection over a's groups of (group \ {a} \ implied)
+ * (CreateAllCindCandidates.scala:106-121 + IntersectCindCandidates.scala:40-43).  The intersection starts
+ * from a's smallest group; a group much larger than the surviving set is probed by binary search, otherwise
+ * merged (the set is the same in any order; this only bounds the work by the smallest group). */
+static uint64_t raw_refs(const orc_csr *c, uint64_t a, int strategy, refbuf *b) {
+    const uint64_t V = c->V;
+    /* trivial refs of a binary dep: its two unary components (Condition.isImpliedBy) */
+    uint32_t triv1 = ~0u, triv2 = ~0u;
+    int dep_bt = -1;
+    uint32_t dv2 = 0;
+    if (a >= 6ull * V) {
+        uint64_t key = c->bkeys[a - 6ull * V];
+        dep_bt = (int)(key >> 62);
+        dv2 = (uint32_t)(key & 0x7fffffff);
+        comps_of(c, a, &triv1, &triv2);
+    }
+    const uint64_t j0 = c->doff[a], j1 = c->doff[a + 1];
+    if (j0 == j1) return 0;
+    uint64_t jp = j0;  /* pivot: smallest group */
+    for (uint64_t j = j0 + 1; j < j1; ++j) {
+        const uint64_t g = c->dgrp[j], gp = c->dgrp[jp];
+        if (c->goff[g + 1] - c->goff[g] < c->goff[gp + 1] - c->goff[gp]) jp = j;
+    }
+    {
+        const uint64_t g = c->dgrp[jp], k = c->goff[g + 1] - c->goff[g];
+        const uint32_t *gc = c->gcap + c->goff[g];
+        if (k > b->cap) {
+            b->cap = k * 2;
+            b->refs = (uint32_t *)realloc(b->refs, b->cap * sizeof(uint32_t));
+            b->tmp = (uint32_t *)realloc(b->tmp, b->cap * sizeof(uint32_t));
+        }
+        uint64_t nref = 0;
+        for (uint64_t i = 0; i < k; ++i) {
+            uint32_t r = gc[i];
+            if (r == a || r == triv1 || r == triv2) continue;
+            if (strategy == 0 && dep_bt >= 0 && r >= 6ull * V) {
+                /* literal Condition.isImpliedBy quirk for same-type binary captures:
+                 * ref X is "implied" by dep D when X.v1 == D.v2 (Condition.scala:35-43) */
+                uint64_t rk = c->bkeys[r - 6ull * V];
+                if ((int)(rk >> 62) == dep_bt && (uint32_t)((rk >> 31) & 0x7fffffff) == dv2) continue;
+            }
+            b->refs[nref++] = r;
+        }
+        for (uint64_t j = j0; j < j1 && nref; ++j) {
+            if (j == jp) continue;
+            const uint64_t gg = c->dgrp[j], kk = c->goff[gg + 1] - c->goff[gg];
+            const uint32_t *gm = c->gcap + c->goff[gg];
+            uint64_t m = 0;
+            if (kk > 16 * nref) {
+                uint64_t lo = 0;
+                for (uint64_t x = 0; x < nref; ++x) {
+                    lo += lower_bound_u32(gm + lo, kk - lo, b->refs[x]);
+                    if (lo < kk && gm[lo] == b->refs[x]) b->tmp[m++] = b->refs[x];
+                }
+            } else {
+                uint64_t x = 0, y = 0;
+                while (x < nref && y < kk) {
+                    if (b->refs[x] < gm[y]) x++;
+                    else if (b->refs[x] > gm[y]) y++;
+                    else { b->tmp[m++] = b->refs[x]; x++; y++; }
+                }
+            }
+            uint32_t *t = b->refs; b->refs = b->tmp; b->tmp = t;
+            nref = m;
+        }
+        return nref;
+    }
+}
+
+static int cmp_u32(const void *x, const void *y) {
+    const uint32_t a = *(const uint32_t *)x, b = *(const uint32_t *)y;
+    return a < b ? -1 : (a > b);
+}
+
+
+/* ---------------------------------------------------------------- materialized result */
+
+int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n, uint32_t V,
+            uint32_t ms, int strategy, int clean, const char *projection,
+            orc_cind **out, uint64_t *n_out, uint64_t **bin_keys_out, uint64_t *n_bin_out,
+            orc_stats *st) {
+    orc_csr c;
+    if (prep(s, p, o, n, V, ms, projection, &c, st)) return -1;
+    const uint64_t ncap = c.ncap;
+    const uint32_t *support = c.support;
+    const uint64_t *bkeys = c.bkeys;
+
+    /* 5. per dependent: raw ref set.  Dependents are split into chunks processed by OpenMP threads; each
+     *    chunk's CINDs go to its own buffer and the buffers are concatenated in chunk (= dependent) order. */
     const uint64_t nchunk = ncap < 4096 ? 1 : 4096;
     orc_cind **cbuf = (orc_cind **)calloc(nchunk, sizeof(orc_cind *));
     uint64_t *ccnt = (uint64_t *)calloc(nchunk + 1, sizeof(uint64_t));
 #pragma omp parallel
     {
-        uint32_t *refs = NULL, *tmp = NULL;
-        uint64_t refs_cap = 0;
+        refbuf rb = {NULL, NULL, 0};
 #pragma omp for schedule(dynamic, 1)
         for (uint64_t ch = 0; ch < nchunk; ++ch) {
             uint64_t ccap = 256, nc = 0;
@@ -296,59 +427,11 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
             const uint64_t a0 = ncap * ch / nchunk, a1 = ncap * (ch + 1) / nchunk;
             for (uint64_t a = a0; a < a1; ++a) {
                 if (support[a] < ms) continue;
-                /* trivial refs of a binary dep: its two unary components (Condition.isImpliedBy) */
-                uint32_t triv1 = ~0u, triv2 = ~0u;
-                int dep_bt = -1;
-                uint32_t dv1 = 0, dv2 = 0;
-                if (a >= 6ull * V) {
-                    uint64_t key = bkeys[a - 6ull * V];
-                    dep_bt = (int)(key >> 62);
-                    dv1 = (uint32_t)((key >> 31) & 0x7fffffff);
-                    dv2 = (uint32_t)(key & 0x7fffffff);
-                    int t1, t2;
-                    binary_components(dep_bt, &t1, &t2);
-                    triv1 = (uint32_t)((uint64_t)t1 * V + dv1);
-                    triv2 = (uint32_t)((uint64_t)t2 * V + dv2);
-                }
-                uint64_t nref = 0;
-                for (uint64_t j = doff[a]; j < doff[a + 1]; ++j) {
-                    uint64_t g = dgrp[j];
-                    uint64_t k = goff[g + 1] - goff[g];
-                    const uint32_t *gc = gcap + goff[g];
-                    if (j == doff[a]) {
-                        if (k > refs_cap) {
-                            refs_cap = k * 2;
-                            refs = (uint32_t *)realloc(refs, refs_cap * sizeof(uint32_t));
-                            tmp = (uint32_t *)realloc(tmp, refs_cap * sizeof(uint32_t));
-                        }
-                        for (uint64_t i = 0; i < k; ++i) {
-                            uint32_t r = gc[i];
-                            if (r == a || r == triv1 || r == triv2) continue;
-                            if (strategy == 0 && dep_bt >= 0 && r >= 6ull * V) {
-                                /* literal Condition.isImpliedBy quirk for same-type binary captures:
-                                 * ref X is "implied" by dep D when X.v1 == D.v2 (Condition.scala:35-43) */
-                                uint64_t rk = bkeys[r - 6ull * V];
-                                if ((int)(rk >> 62) == dep_bt && (uint32_t)((rk >> 31) & 0x7fffffff) == dv2) continue;
-                            }
-                            refs[nref++] = r;
-                        }
-                    } else {
-                        /* merge-intersect sorted refs with sorted group */
-                        uint64_t x = 0, y = 0, m = 0;
-                        while (x < nref && y < k) {
-                            if (refs[x] < gc[y]) x++;
-                            else if (refs[x] > gc[y]) y++;
-                            else { tmp[m++] = refs[x]; x++; y++; }
-                        }
-                        uint32_t *t = refs; refs = tmp; tmp = t;
-                        nref = m;
-                    }
-                    if (nref == 0) break;
-                }
+                const uint64_t nref = raw_refs(&c, a, strategy, &rb);
                 for (uint64_t i = 0; i < nref; ++i) {
                     if (nc == ccap) { ccap *= 2; cind = (orc_cind *)realloc(cind, ccap * sizeof(orc_cind)); }
                     cind[nc].dep = (uint32_t)a;
-                    cind[nc].ref = refs[i];
+                    cind[nc].ref = rb.refs[i];
                     cind[nc].support = support[a];
                     nc++;
                 }
@@ -356,10 +439,10 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
             cbuf[ch] = cind;
             ccnt[ch] = nc;
         }
-        free(refs); free(tmp);
+        refbuf_free(&rb);
     }
     uint64_t nc = 0;
-    for (uint64_t ch = 0; ch < nchunk; ++ch) { uint64_t c = ccnt[ch]; ccnt[ch] = nc; nc += c; }
+    for (uint64_t ch = 0; ch < nchunk; ++ch) { uint64_t cc = ccnt[ch]; ccnt[ch] = nc; nc += cc; }
     ccnt[nchunk] = nc;
     orc_cind *cind = (orc_cind *)xmalloc(nc * sizeof(orc_cind));
 #pragma omp parallel for schedule(dynamic, 16)
@@ -368,7 +451,6 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
         free(cbuf[ch]);
     }
     free(cbuf); free(ccnt);
-    free(dgrp); free(doff); free(goff); free(gcap); free(support);
     st->n_raw_cinds = nc;
 
     /* 6. minimality (TraversalStrategy.removeImpliedCinds :126-168), rules on the raw sets */
@@ -385,11 +467,8 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
             if (du && ru) s11[n11++] = pair;
             if (du && !ru) s12[n12++] = pair;
             if (!ru) {
-                uint64_t key = bkeys[r - U];
-                int t1, t2;
-                binary_components((int)(key >> 62), &t1, &t2);
-                uint64_t c1 = (uint64_t)t1 * V + ((key >> 31) & 0x7fffffff);
-                uint64_t c2 = (uint64_t)t2 * V + (key & 0x7fffffff);
+                uint32_t c1, c2;
+                comps_of(&c, r, &c1, &c2);
                 if (du) { s12c[n12c++] = (d << 32) | c1; s12c[n12c++] = (d << 32) | c2; }
                 else { s22c[n22c++] = (d << 32) | c1; s22c[n22c++] = (d << 32) | c2; }
             }
@@ -405,16 +484,13 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
             if (du && ru) {
                 drop = bsearch_u64(s12c, n12c, (d << 32) | r);                          /* R3 */
             } else if (!du) {
-                uint64_t key = bkeys[d - U];
-                int t1, t2;
-                binary_components((int)(key >> 62), &t1, &t2);
-                uint64_t c1 = (uint64_t)t1 * V + ((key >> 31) & 0x7fffffff);
-                uint64_t c2 = (uint64_t)t2 * V + (key & 0x7fffffff);
+                uint32_t c1, c2;
+                comps_of(&c, d, &c1, &c2);
                 if (ru) {
-                    drop = bsearch_u64(s11, n11, (c1 << 32) | r) || bsearch_u64(s11, n11, (c2 << 32) | r)  /* R1 */
+                    drop = bsearch_u64(s11, n11, ((uint64_t)c1 << 32) | r) || bsearch_u64(s11, n11, ((uint64_t)c2 << 32) | r)  /* R1 */
                         || bsearch_u64(s22c, n22c, (d << 32) | r);                                      /* R2 */
                 } else {
-                    drop = bsearch_u64(s12, n12, (c1 << 32) | r) || bsearch_u64(s12, n12, (c2 << 32) | r); /* R4 */
+                    drop = bsearch_u64(s12, n12, ((uint64_t)c1 << 32) | r) || bsearch_u64(s12, n12, ((uint64_t)c2 << 32) | r); /* R4 */
                 }
             }
             keep[i] = (uint8_t)!drop;
@@ -426,12 +502,148 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
         nc = m;
         free(s11); free(s12); free(s12c); free(s22c);
     }
+    (void)bkeys;
+    csr_free(&c);
     st->n_cinds = nc;
     *out = cind;
     *n_out = nc;
-    *bin_keys_out = bkeys;
-    *n_bin_out = nb;
+    *bin_keys_out = c.bkeys;
+    *n_bin_out = c.nb;
     return 0;
+}
+
+/* ---------------------------------------------------------------- streamed result */
+
+/* Order-independent checksum term of one result row (the same mix as the library's rdf_cind_checksum):
+ * external capture ids (unary t*V+v, binary 6V+b) and the dependent's support. */
+static inline uint64_t row_hash(uint32_t dep, uint32_t ref, uint32_t support) {
+    return mix64((((uint64_t)dep << 32) | ref) + (uint64_t)support * 0x9E3779B97F4A7C15ULL);
+}
+
+#define ORC_R1 1
+#define ORC_R2 2
+#define ORC_R3 4
+#define ORC_R4 8
+
+typedef struct {
+    uint64_t n_cinds;
+    uint64_t checksum;
+    uint64_t n_kind[4];   /* 1/1, 1/2, 2/1, 2/2 after the rules */
+    uint64_t n_raw;       /* |V| */
+} orc_stream_result;
+
+/* Count + checksum of the result without materializing it: every dependent's raw refs, then R1-R4 per
+ * dependent.  R2 and R3 only look at the dependent's own raw refs; R1 and R4 test membership of (comp(D), ref)
+ * in V11 / V12, i.e. in the raw refs of the two unary components of a binary dependent D, which are computed
+ * here (cached per thread: binary ids follow the sorted keys, so consecutive dependents share comp1).
+ * rules: ORC_R* mask (15 = --clean-implied, R1|R4 = strategy-1 raw output, 0 = strategy-0 raw). */
+int orc_stream(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n, uint32_t V, uint32_t ms,
+               int strategy, int rules, const char *projection, orc_stream_result *res, orc_stats *st) {
+    orc_csr c;
+    memset(res, 0, sizeof(*res));
+    if (prep(s, p, o, n, V, ms, projection, &c, st)) return -1;
+    const uint64_t ncap = c.ncap, U = 6ull * V;
+    const uint64_t nchunk = ncap < 4096 ? 1 : 65536;
+    uint64_t t_cnt = 0, t_sum = 0, t_raw = 0, t_kind[4] = {0, 0, 0, 0};
+#pragma omp parallel reduction(+ : t_cnt, t_sum, t_raw)
+    {
+        refbuf rb = {NULL, NULL, 0};
+        /* per-thread direct-mapped cache of the raw refs of binary dependents' unary components */
+        enum { NSLOT = 256 };
+        refbuf cache[NSLOT];
+        uint64_t ckey[NSLOT], cn[NSLOT];
+        memset(cache, 0, sizeof(cache));
+        for (int k = 0; k < NSLOT; ++k) ckey[k] = ~0ull, cn[k] = 0;
+        uint32_t *comp = NULL;
+        uint64_t comp_cap = 0;
+        uint64_t kind[4] = {0, 0, 0, 0};
+#pragma omp for schedule(dynamic, 1)
+        for (uint64_t ch = 0; ch < nchunk; ++ch) {
+            const uint64_t a0 = ncap * ch / nchunk, a1 = ncap * (ch + 1) / nchunk;
+            for (uint64_t a = a0; a < a1; ++a) {
+                if (c.support[a] < ms) continue;
+                const uint64_t nref = raw_refs(&c, a, strategy, &rb);
+                if (!nref) continue;
+                t_raw += nref;
+                const uint32_t sup = c.support[a];
+                /* first binary ref (refs are sorted: unary ids < 6V first) */
+                uint64_t nb0 = 0;
+                while (nb0 < nref && rb.refs[nb0] < U) nb0++;
+                /* components of the binary raw refs (R2 for binary deps, R3 for unary deps) */
+                uint64_t ncomp = 0;
+                const int mark = a < U ? (rules & ORC_R3) : (rules & ORC_R2);
+                if (mark && nref > nb0) {
+                    if (2 * (nref - nb0) > comp_cap) {
+                        comp_cap = 4 * (nref - nb0);
+                        comp = (uint32_t *)realloc(comp, comp_cap * sizeof(uint32_t));
+                    }
+                    for (uint64_t i = nb0; i < nref; ++i) comps_of(&c, rb.refs[i], &comp[ncomp], &comp[ncomp + 1]), ncomp += 2;
+                    qsort(comp, ncomp, sizeof(uint32_t), cmp_u32);
+                }
+                const uint32_t *r1 = NULL, *r2 = NULL;
+                uint64_t n1 = 0, n2 = 0;
+                if (a >= U && (rules & (ORC_R1 | ORC_R4))) {
+                    uint32_t cc[2];
+                    comps_of(&c, a, &cc[0], &cc[1]);
+                    const uint64_t k1 = mix64(cc[0]) % NSLOT;
+                    uint64_t k2 = mix64(cc[1]) % NSLOT;
+                    if (k2 == k1) k2 = (k2 + 1) % NSLOT;  /* both components stay resident */
+                    const uint64_t ks[2] = {k1, k2};
+                    for (int q = 0; q < 2; ++q) {
+                        const uint64_t k = ks[q];
+                        if (ckey[k] != cc[q]) { cn[k] = raw_refs(&c, cc[q], strategy, &cache[k]); ckey[k] = cc[q]; }
+                    }
+                    r1 = cache[k1].refs; n1 = cn[k1];
+                    r2 = cache[k2].refs; n2 = cn[k2];
+                }
+                /* refs, comp, r1 and r2 are all sorted: membership by forward-moving cursors */
+                uint64_t pc = 0, p1 = 0, p2 = 0;
+                for (uint64_t i = 0; i < nref; ++i) {
+                    const uint32_t r = rb.refs[i];
+                    const int ru = r < U;
+                    int drop = 0;
+                    if (ncomp && ru) {                                                           /* R3 / R2 */
+                        while (pc < ncomp && comp[pc] < r) pc++;
+                        drop = pc < ncomp && comp[pc] == r;
+                    }
+                    if (!drop && a >= U) {
+                        const int rule = ru ? (rules & ORC_R1) : (rules & ORC_R4);                  /* R1 / R4 */
+                        if (rule) {
+                            while (p1 < n1 && r1[p1] < r) p1++;
+                            while (p2 < n2 && r2[p2] < r) p2++;
+                            drop = (p1 < n1 && r1[p1] == r) || (p2 < n2 && r2[p2] == r);
+                        }
+                    }
+                    if (drop) continue;
+                    t_cnt++;
+                    t_sum += row_hash((uint32_t)a, r, sup);
+                    kind[(a >= U) * 2 + !ru]++;
+                }
+            }
+        }
+#pragma omp critical
+        for (int k = 0; k < 4; ++k) t_kind[k] += kind[k];
+        refbuf_free(&rb);
+        for (int k = 0; k < NSLOT; ++k) refbuf_free(&cache[k]);
+        free(comp);
+    }
+    res->n_cinds = t_cnt;
+    res->checksum = t_sum;
+    res->n_raw = t_raw;
+    for (int k = 0; k < 4; ++k) res->n_kind[k] = t_kind[k];
+    st->n_raw_cinds = t_raw;
+    st->n_cinds = t_cnt;
+    free(c.bkeys);
+    csr_free(&c);
+    return 0;
+}
+
+/* checksum of a materialized result (same row hash as orc_stream) */
+uint64_t orc_checksum(const orc_cind *rows, uint64_t n) {
+    uint64_t acc = 0;
+#pragma omp parallel for reduction(+ : acc) schedule(static)
+    for (uint64_t i = 0; i < n; ++i) acc += row_hash(rows[i].dep, rows[i].ref, rows[i].support);
+    return acc;
 }
 
 void orc_free(void *ptr) { free(ptr); }

@@ -30,6 +30,22 @@ class OrcStats(ctypes.Structure):
                 ("n_cinds", ctypes.c_uint64)]
 
 
+class OrcStream(ctypes.Structure):
+    _fields_ = [("n_cinds", ctypes.c_uint64), ("checksum", ctypes.c_uint64), ("n_kind", ctypes.c_uint64 * 4),
+                ("n_raw", ctypes.c_uint64)]
+
+
+# minimality rules of the streamed mode (oracle/c/rdfind_oracle.c ORC_R*)
+R1, R2, R3, R4 = 1, 2, 4, 8
+
+
+def rules_for(strategy, clean):
+    """--clean-implied: R1-R4; strategy-1 raw: the exact-candidate S2L output (R1 and R4); strategy-0 raw: V."""
+    if clean:
+        return R1 | R2 | R3 | R4
+    return R1 | R4 if strategy == 1 else 0
+
+
 def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
@@ -49,6 +65,12 @@ def _load():
                                                          ctypes.POINTER(ctypes.c_uint64),
                                                          ctypes.POINTER(OrcStats)]
         lib.orc_free.argtypes = [ctypes.c_void_p]
+        lib.orc_stream.restype = ctypes.c_int
+        lib.orc_stream.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                            ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                                            ctypes.POINTER(OrcStream), ctypes.POINTER(OrcStats)]
+        lib.orc_checksum.restype = ctypes.c_uint64
+        lib.orc_checksum.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         _lib = lib
     return _lib
 
@@ -92,6 +114,31 @@ def run(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo
     lib.orc_free(bk)
     stats = {f: (list(getattr(st, f)) if f == "n_freq_unary" else getattr(st, f)) for f, _ in OrcStats._fields_}
     return arr, keys, stats
+
+
+def stream(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):
+    """Count + order-independent checksum of the result without materializing it (the library's
+    rdf_cind_checksum mix).  Returns dict(n_cinds, checksum, n_kind=[11, 12, 21, 22], n_raw, stats)."""
+    lib = _load()
+    s = np.ascontiguousarray(s, dtype=np.uint32)
+    p = np.ascontiguousarray(p, dtype=np.uint32)
+    o = np.ascontiguousarray(o, dtype=np.uint32)
+    res = OrcStream()
+    st = OrcStats()
+    rc = lib.orc_stream(s.ctypes.data, p.ctypes.data, o.ctypes.data, len(s), num_terms, min_support, strategy,
+                        rules_for(strategy, clean), projection.encode(), ctypes.byref(res), ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"orc_stream failed with {rc}")
+    stats = {f: (list(getattr(st, f)) if f == "n_freq_unary" else getattr(st, f)) for f, _ in OrcStats._fields_}
+    return {"n_cinds": res.n_cinds, "checksum": res.checksum, "n_kind": list(res.n_kind), "n_raw": res.n_raw,
+            "stats": stats}
+
+
+def checksum_rows(arr):
+    """The streamed checksum of a materialized result (structured dep/ref/support array)."""
+    lib = _load()
+    a = np.ascontiguousarray(arr)
+    return int(lib.orc_checksum(a.ctypes.data, a.shape[0])) if a.shape[0] else 0
 
 
 def run_set(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):

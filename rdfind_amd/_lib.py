@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_cinds_range", "rdf_cind_checksum", "rdf_last_stats", "rdf_shard_begin", "rdf_shard_step",
     "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
     "rdf_distinct_triples", "rdf_copy_triples", "rdf_parse_ntriples", "rdf_copy_terms",
-    "rdf_set_dictionary_parsed",
+    "rdf_set_dictionary_parsed", "rdf_device_bytes", "rdf_copy_cinds_decoded", "rdf_result_sizes",
+    "rdf_copy_result_raw",
 )
 RDF_NT_TABS = 1
 
@@ -58,7 +59,8 @@ class CindStats(ctypes.Structure):
                 ("n_light_chunks", ctypes.c_uint64), ("n_heavy_chunks", ctypes.c_uint64),
                 ("ms_pivot", ctypes.c_float), ("ms_light", ctypes.c_float), ("ms_rules", ctypes.c_float),
                 ("ms_heavy", ctypes.c_float), ("n_heavy_candidates", ctypes.c_uint64),
-                ("n_class_members", ctypes.c_uint64), ("n_classes", ctypes.c_uint64), ("n_class_cinds", ctypes.c_uint64)]
+                ("n_class_members", ctypes.c_uint64), ("n_classes", ctypes.c_uint64), ("n_class_cinds", ctypes.c_uint64),
+                ("n_light_candidates", ctypes.c_uint64), ("n_light_entries", ctypes.c_uint64)]
 
 
 class Exchange(ctypes.Structure):
@@ -78,6 +80,9 @@ class ExchangeRequest:
 
 
 CIND_DTYPE = np.dtype([("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])
+# rdf_cind_row (include/rdfind_hip.h): the reference's Cind shape with term ids
+ROW_DTYPE = np.dtype([("dep_capture_type", "<u4"), ("dep_value1", "<u4"), ("dep_value2", "<u4"),
+                      ("ref_capture_type", "<u4"), ("ref_value1", "<u4"), ("ref_value2", "<u4"), ("support", "<u4")])
 
 _lib = None
 
@@ -121,8 +126,12 @@ def load():
         "rdf_stage_times": (i32, [P, ctypes.POINTER(ctypes.c_float)]),
         "rdf_kernel_times": (i32, [P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
         "rdf_sync": (i32, [P]),
+        "rdf_device_bytes": (i32, [P, ctypes.POINTER(u64)]),
         "rdf_copy_cinds_range": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_cind_checksum": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_copy_cinds_decoded": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
+        "rdf_result_sizes": (i32, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "rdf_copy_result_raw": (i32, [P, P, P, P, P, P]),
         "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
         "rdf_format_cinds": (i32, [P, u64, u64, P, u64, ctypes.POINTER(u64)]),
@@ -281,6 +290,12 @@ class Context:
     def sync(self):
         self._check(self.lib.rdf_sync(self.ptr), "rdf_sync")
 
+    def device_bytes(self) -> int:
+        """HBM bytes the context holds (rdf_device_bytes)."""
+        v = ctypes.c_uint64()
+        self._check(self.lib.rdf_device_bytes(self.ptr, ctypes.byref(v)), "rdf_device_bytes")
+        return int(v.value)
+
     def last_stats(self):
         fc, gs, cs = FcStats(), GroupStats(), CindStats()
         self._check(self.lib.rdf_last_stats(self.ptr, ctypes.byref(fc), ctypes.byref(gs), ctypes.byref(cs)),
@@ -335,6 +350,30 @@ class Context:
         copied = ctypes.c_uint64()
         self._check(self.lib.rdf_copy_cinds_range(self.ptr, offset, out.ctypes.data, count, ctypes.byref(copied)),
                     "rdf_copy_cinds_range")
+        return out[: copied.value]
+
+    def result_sizes(self):
+        """(n_refs, n_runs, n_captures) of the CindSet-shaped result (rdf_result_sizes)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.rdf_result_sizes(self.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                    "rdf_result_sizes")
+        return int(a.value), int(b.value), int(c.value)
+
+    def copy_result_raw(self, refs_ptr=None, runoff=None, rundep=None, capture_ids=None, supports=None):
+        """rdf_copy_result_raw into caller buffers (raw pointers or numpy arrays; None skips a part)."""
+        def ptr(x):
+            return None if x is None else (x if isinstance(x, int) else x.ctypes.data)
+        self._check(self.lib.rdf_copy_result_raw(self.ptr, ptr(refs_ptr), ptr(runoff), ptr(rundep), ptr(capture_ids),
+                                                 ptr(supports)), "rdf_copy_result_raw")
+
+    def copy_cinds_decoded(self, offset: int = 0, count: int | None = None) -> np.ndarray:
+        """Cind-shaped rows decoded on the device (rdf_copy_cinds_decoded), ROW_DTYPE."""
+        if count is None:
+            count = max(self.cind_count() - offset, 0)
+        out = np.empty(count, dtype=ROW_DTYPE)
+        copied = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_cinds_decoded(self.ptr, offset, out.ctypes.data, count, ctypes.byref(copied)),
+                    "rdf_copy_cinds_decoded")
         return out[: copied.value]
 
     def checksum(self) -> int:

@@ -873,7 +873,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64
                                                            u64* heavy_candidates) {
     const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
-        u32 hc = 0;
+        u32 hc = 0, lc = 0, le = 0;
         if (d < v.C) {
             const u64 best = best_in[d];
             const u32 nlight = nlight_in[d];
@@ -881,6 +881,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64
             const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
             pivot[d] = (u32)(best & 0xffffffffu);
             light_plan(v, (u32)d, nlight, sz, nchunk_light, nitem_light, npacked);
+            if (nlight && nchunk_light[d]) {
+                lc = (u32)sz;
+                le = (u32)(v.doff[d + 1] - v.doff[d]);
+            }
             // unary heavy-only dependents are emitted per bitmask class (k_class_*), binary ones by k_heavy
             nchunk_heavy[d] = (nlight || d < v.Cu) ? 0 : nch;
             if (!nlight) {
@@ -891,6 +895,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64
         u64 tot = wave_inclusive_scan64(hc);
         tot = __shfl(tot, RDF_WAVE - 1, RDF_WAVE);
         if (lane_id() == 0 && tot) atomicAdd(heavy_candidates, tot);
+        // light-intersection work of the chunk: pivot candidates and group entries of light dependents
+        u64 tl = wave_inclusive_scan64(lc), te = wave_inclusive_scan64(le);
+        tl = __shfl(tl, RDF_WAVE - 1, RDF_WAVE);
+        te = __shfl(te, RDF_WAVE - 1, RDF_WAVE);
+        if (lane_id() == 0 && tl) atomicAdd(heavy_candidates + 1, tl);
+        if (lane_id() == 0 && te) atomicAdd(heavy_candidates + 2, te);
     }
 }
 
@@ -1831,11 +1841,17 @@ __device__ inline u64 run_of(const u64* __restrict__ runoff, u64 lo, u64 hi, u64
     return lo;
 }
 
+// checksum term of one result row (external capture ids + the dependent's support); the C oracle's streamed
+// mode (oracle/c/rdfind_oracle.c row_hash) sums the same terms
+__device__ inline u64 row_hash(u32 dep, u32 ref, u32 support) {
+    return mix64((((u64)dep << 32) | ref) + (u64)support * 0x9E3779B97F4A7C15ull);
+}
+
 // order-independent checksum of the result set (external capture ids, so it is comparable across runs and
 // layouts).  Each block looks up the runs of its first and last element once; lanes search inside that range.
 __global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u32* __restrict__ refs, u64 n, const u64* __restrict__ runoff,
                                                         const u32* __restrict__ rundep, u64 R, const u32* __restrict__ fcap,
-                                                        u64* sum) {
+                                                        const u32* __restrict__ csup, u64* sum) {
     __shared__ u64 s_lo, s_hi;
     u64 acc = 0;
     for (u64 b = (u64)blockIdx.x * RDF_BLOCK; b < n; b += (u64)gridDim.x * RDF_BLOCK) {
@@ -1849,13 +1865,55 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u32* __restrict__ 
         const u64 i = b + threadIdx.x;
         if (i < n) {
             const u32 d = rundep[run_of(runoff, s_lo, s_hi, i)];
-            acc += mix64(((u64)fcap[d] << 32) | fcap[refs[i]]);
+            acc += row_hash(fcap[d], fcap[refs[i]], csup[d]);
         }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, RDF_WAVE);
     if (lane_id() == 0 && acc) atomicAdd(sum, acc);
 }
+// Cind-shaped rows (ALG/data/Cind.scala:12-15) of output elements [first, first + n): capture code and condition
+// values of dependent and referenced capture (value2 = NONE for unary captures) plus the support.
+__device__ inline void decode_capture(u32 ext, u32 V, const u64* __restrict__ bkeys, u32* code, u32* v1, u32* v2) {
+    const u64 six = 6ull * V;
+    if (ext < six) {
+        const u32 t = ext / V;
+        *code = t == 0 ? 10u : t == 1 ? 12u : t == 2 ? 17u : t == 3 ? 20u : t == 4 ? 33u : 34u;
+        *v1 = ext - t * V;
+        *v2 = NONE32;
+    } else {
+        const u64 k = bkeys[ext - six];
+        const int bt = bin_key_type(k);
+        *code = bt == 0 ? 14u : bt == 1 ? 21u : 35u;
+        *v1 = bin_key_v1(k);
+        *v2 = bin_key_v2(k);
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_decode_rows(const u32* __restrict__ refs, u64 first, u64 n,
+                                                           const u64* __restrict__ runoff, const u32* __restrict__ rundep,
+                                                           u64 R, const u32* __restrict__ fext, const u32* __restrict__ csup,
+                                                           u32 V, const u64* __restrict__ bkeys, u32* __restrict__ rows) {
+    __shared__ u64 s_lo, s_hi;
+    for (u64 b = (u64)blockIdx.x * RDF_BLOCK; b < n; b += (u64)gridDim.x * RDF_BLOCK) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const u64 last = b + RDF_BLOCK - 1 < n ? b + RDF_BLOCK - 1 : n - 1;
+            s_lo = run_of(runoff, 0, R - 1, first + b);
+            s_hi = run_of(runoff, s_lo, R - 1, first + last);
+        }
+        __syncthreads();
+        const u64 i = b + threadIdx.x;
+        if (i < n) {
+            const u32 d = rundep[run_of(runoff, s_lo, s_hi, first + i)];
+            u32* row = rows + 7 * i;
+            decode_capture(fext[d], V, bkeys, &row[0], &row[1], &row[2]);
+            decode_capture(fext[refs[first + i]], V, bkeys, &row[3], &row[4], &row[5]);
+            row[6] = csup[d];
+        }
+    }
+}
+
 // ================================================================================================
 // Sharded mode: capture groups partitioned by join-value hash over R ranks.  Global
 // quantities (supports, group-size histogram, heavy masks, pivot sizes, light-group counts) are combined
@@ -1887,7 +1945,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
                                                                  u64* heavy_candidates) {
     const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
-        u32 hc = 0;
+        u32 hc = 0, lc = 0, le = 0;
         if (d < v.C) {
             const u64 best = best_in[d];
             const u32 nlight = nlight_in[d];
@@ -1898,6 +1956,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
             const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
             pivot[d] = (u32)(best & 0xffffffffu);
             light_plan(v, (u32)d, nlight, sz, nchunk_light, nitem_light, npacked);
+            if (nlight && nchunk_light[d]) {
+                lc = (u32)sz;
+                le = (u32)(v.doff[d + 1] - v.doff[d]);
+            }
             nchunk_heavy[d] = (heavy_only && d >= v.Cu && holder) ? nch : 0;
             nrl[d] = (u32)(gl >> 40);
             if (heavy_only) {
@@ -1908,6 +1970,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
         u64 tot = wave_inclusive_scan64(hc);
         tot = __shfl(tot, RDF_WAVE - 1, RDF_WAVE);
         if (lane_id() == 0 && tot) atomicAdd(heavy_candidates, tot);
+        // light-intersection work of the chunk: pivot candidates and group entries of light dependents
+        u64 tl = wave_inclusive_scan64(lc), te = wave_inclusive_scan64(le);
+        tl = __shfl(tl, RDF_WAVE - 1, RDF_WAVE);
+        te = __shfl(te, RDF_WAVE - 1, RDF_WAVE);
+        if (lane_id() == 0 && tl) atomicAdd(heavy_candidates + 1, tl);
+        if (lane_id() == 0 && te) atomicAdd(heavy_candidates + 2, te);
     }
 }
 

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_single(TO* __restrict__ a, u
 }
 
 template <typename TI, typename TO>
-__global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply(const TI* __restrict__ in, TO* __restrict__ out, u64 n,
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply(const TI* in, TO* out, u64 n,
                                                           const TO* __restrict__ tile_offsets) {
     __shared__ TO lds[SCAN_TILE];
     __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply(const TI* __restrict__
 
 // small inputs (a few tiles): one block scans in -> out with a running carry (one launch instead of three)
 template <typename TI, typename TO>
-__global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* __restrict__ in, TO* __restrict__ out, u64 n,
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* in, TO* out, u64 n,
                                                           TO* __restrict__ grand_total) {
     __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
     TO carry = 0;

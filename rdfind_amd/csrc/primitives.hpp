@@ -46,6 +46,11 @@ struct Workspace {
     void release() {
         for (auto& b : slot) b.release();
     }
+    size_t bytes() const {
+        size_t t = 0;
+        for (const auto& b : slot) t += b.cap;
+        return t;
+    }
 };
 
 // out[i] = sum_{j<i} in[j]; *d_total (device, optional) = sum of all.  In-place allowed.

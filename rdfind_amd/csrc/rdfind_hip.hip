@@ -64,6 +64,7 @@ struct rdf_ctx {
     DevBuf pivot, nchl, nchh, choffl, choffh, epairs, epairs_tmp, eoff, hcounts, hoff, hbits, cbits, hown, cown, sbase, dcls, crep, out, stage_rows;
     DevBuf dheap, dtoff, cslen, csoff, cstr, flen, floff, fbuf;  // output formatting (K8)
     u64 dict_terms = 0, run_id = 0, capstr_run = ~0ull;
+    DevBuf drows;           // decoded Cind-shaped rows (rdf_copy_cinds_decoded)
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
@@ -107,6 +108,7 @@ struct rdf_ctx {
     float tms[RDF_NUM_TIMERS] = {};
     u64 sort_passes_records = 0, sort_passes_pairs = 0;
     u64 heavy_candidates = 0;
+    u64 light_candidates = 0, light_entries = 0;  // pivot members / group entries of dependents with light groups
 };
 
 static void tbegin(rdf_ctx* c, int id) {
@@ -185,11 +187,11 @@ static rdf_status read_u32(rdf_ctx* c, const void* dptr, u32* out) {
 
 static u64* dscal(rdf_ctx* c, int i) { return c->scal.as<u64>() + i; }
 
-// Several device scalars with ONE host round trip: a one-thread kernel gathers them into scal[8..13],
+// Several device scalars with ONE host round trip: a one-thread kernel gathers them into scal[8..15],
 // one copy brings them back (each separate read is a stream drain plus a copy, ~20-40 us).
 struct ScalarGather {
-    const void* p[6];
-    int bytes[6];
+    const void* p[8];
+    int bytes[8];
     int n;
 };
 
@@ -225,6 +227,24 @@ static const u64 kMaxBlocks = 1ull << 20;
 static inline unsigned vgrid(u64 blocks) { return (unsigned)std::min<u64>(std::max<u64>(blocks, 1), kMaxBlocks); }
 static inline u64 wave_blocks(u64 waves) { return (waves + RDF_WAVES_PER_BLOCK - 1) / RDF_WAVES_PER_BLOCK; }
 static inline u64 thread_blocks(u64 threads) { return (threads + RDF_BLOCK - 1) / RDF_BLOCK; }
+
+// every device buffer a context owns (release on destroy; rdf_device_bytes)
+static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
+    return {&c->scal, &c->ts, &c->tp, &c->to, &c->cnt, &c->tkeys, &c->tcnt, &c->bkeys, &c->bkeys_tmp,
+                      &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
+                      &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
+                      &c->gcap, &c->gmap, &c->csup,
+                      &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
+                      &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
+                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
+                      &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
+                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
+                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->upairs, &c->usoff, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
+                      &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows};
+}
 
 extern "C" {
 
@@ -263,21 +283,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->scal, &c->ts, &c->tp, &c->to, &c->cnt, &c->tkeys, &c->tcnt, &c->bkeys, &c->bkeys_tmp,
-                      &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
-                      &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
-                      &c->gcap, &c->gmap, &c->csup,
-                      &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
-                      &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
-                      &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
-                      &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
-                      &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
-                      &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
-                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->upairs, &c->usoff, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
-                      &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
-                      &c->cstr, &c->flen, &c->floff, &c->fbuf};
-    for (DevBuf* b : bufs) b->release();
+    for (DevBuf* b : ctx_buffers(c)) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
     for (auto& e : c->ev)
@@ -293,6 +299,14 @@ const char* rdf_last_error(const rdf_ctx* c) { return c ? c->err.c_str() : "null
 rdf_status rdf_sync(rdf_ctx* c) {
     if (!c) return RDF_ERR_ARG;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RDF_OK;
+}
+
+rdf_status rdf_device_bytes(rdf_ctx* c, uint64_t* bytes) {
+    if (!c || !bytes) return RDF_ERR_ARG;
+    u64 t = c->ws.bytes();
+    for (DevBuf* b : ctx_buffers(c)) t += b->cap;
+    *bytes = t;
     return RDF_OK;
 }
 
@@ -480,6 +494,11 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
     HIP_TRY(c, hipEventRecord(c->ev[7], st));
     HIP_TRY(c, hipStreamSynchronize(st));
     if (ms) HIP_TRY(c, hipEventElapsedTime(ms, c->ev[6], c->ev[7]));
+    // parse-only scratch (~36 B per term occurrence + the slot table): only the text and the term table stay,
+    // which rdf_set_dictionary_parsed needs, so discovery gets the HBM back
+    for (DevBuf* b : {&c->ncnt, &c->ncoff, &c->nlstart, &c->ntstart, &c->ntlen, &c->nvalid, &c->nlpos, &c->nhv,
+                      &c->nslot, &c->ntab, &c->nrep, &c->nfirst, &c->nfid})
+        b->release();
     c->s = c->ts.as<u32>();
     c->p = c->tp.as<u32>();
     c->o = c->to.as<u32>();
@@ -1002,14 +1021,16 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->npk.as<u32>(), c->pkoff.as<u64>(), C, c->pkoff.as<u64>() + C, st));
-    u64 v[5];
+    u64 v[7];
     TRY(read_multi(c, {{c->choffl.as<u64>() + C, 8}, {c->pkoff.as<u64>() + C, 8}, {c->choffh.as<u64>() + C, 8},
-                       {dscal(c, 2), 8}, {c->itoffl.as<u64>() + C, 8}}, v));
+                       {dscal(c, 2), 8}, {c->itoffl.as<u64>() + C, 8}, {dscal(c, 3), 8}, {dscal(c, 4), 8}}, v));
     *WL = v[0];
     *WP = v[1];
     *WH = v[2];
     c->heavy_candidates = v[3];
     *WI = v[4];
+    c->light_candidates = v[5];
+    c->light_entries = v[6];
     return RDF_OK;
 }
 
@@ -1348,6 +1369,8 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     s.n_class_members = c->n_class_members;
     s.n_classes = c->n_classes;
     s.n_class_cinds = c->n_class_out;
+    s.n_light_candidates = c->light_candidates;
+    s.n_light_entries = c->light_entries;
     c->stage = 4;
     return RDF_OK;
 }
@@ -1827,6 +1850,54 @@ rdf_status rdf_copy_cinds_range(rdf_ctx* c, uint64_t offset, rdf_cind* out, uint
     return RDF_OK;
 }
 
+// The CindSet-shaped result as id-records ("CIND id-records in host memory"): refs + run table +
+// the compact -> external capture ids and supports.  Plain async copies on the context stream (pinned caller
+// memory makes them DMA at the link rate).
+rdf_status rdf_result_sizes(rdf_ctx* c, uint64_t* n_refs, uint64_t* n_runs, uint64_t* n_captures) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    if (n_refs) *n_refs = c->n_out;
+    if (n_runs) *n_runs = c->n_runs;
+    if (n_captures) *n_captures = c->C;
+    return RDF_OK;
+}
+
+rdf_status rdf_copy_result_raw(rdf_ctx* c, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* capture_ids,
+                               uint32_t* supports) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    if (refs && c->n_out) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr, c->n_out * 4, hipMemcpyDeviceToHost, st));
+    if (runoff) HIP_TRY(c, hipMemcpyAsync(runoff, c->runoff.p, (c->n_runs + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (rundep && c->n_runs) HIP_TRY(c, hipMemcpyAsync(rundep, c->rundep.p, c->n_runs * 4, hipMemcpyDeviceToHost, st));
+    if (capture_ids && c->C) HIP_TRY(c, hipMemcpyAsync(capture_ids, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
+    if (supports && c->C) HIP_TRY(c, hipMemcpyAsync(supports, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return RDF_OK;
+}
+
+// Cind-shaped rows on the device (decode kernel), copied to the caller in chunks
+rdf_status rdf_copy_cinds_decoded(rdf_ctx* c, uint64_t offset, rdf_cind_row* out, uint64_t count, uint64_t* n_copied) {
+    if (!c || (count && !out)) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
+    const u64 kChunk = 1ull << 22;
+    if (m) ENSURE(c, drows, std::min<u64>(m, kChunk) * sizeof(rdf_cind_row));
+    for (u64 b = 0; b < m; b += kChunk) {
+        const u64 k = std::min(kChunk, m - b);
+        hipLaunchKernelGGL(k_decode_rows, dim3(grid_for(k, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream, c->out_ptr,
+                           offset + b, k, c->runoff.as<u64>(), c->rundep.as<u32>(), c->n_runs, c->fext.as<u32>(),
+                           c->csup.as<u32>(), c->V ? c->V : 1u, c->bkeys.as<u64>(), c->drows.as<u32>());
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipMemcpyAsync(out + b, c->drows.p, k * sizeof(rdf_cind_row), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // drows is reused by the next chunk
+    }
+    if (n_copied) *n_copied = m;
+    return RDF_OK;
+}
+
 rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     if (!c || !checksum) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
@@ -1835,7 +1906,7 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     if (c->n_out)
         hipLaunchKernelGGL(k_checksum, dim3(grid_for(c->n_out, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
                            c->out_ptr, c->n_out, c->runoff.as<u64>(), c->rundep.as<u32>(), c->n_runs, c->fext.as<u32>(),
-                           dscal(c, 7));
+                           c->csup.as<u32>(), dscal(c, 7));
     u64 v = 0;
     rdf_status rs = read_u64(c, dscal(c, 7), &v);
     *checksum = v;

@@ -82,9 +82,29 @@ def _zipf_ranks(rng: np.random.Generator, n_items: int, alpha: float, size: int)
 
 
 def _dedup(s, p, o):
-    key = np.stack([s, p, o], axis=1)
-    key = np.unique(key, axis=0)
-    return key[:, 0].copy(), key[:, 1].copy(), key[:, 2].copy()
+    """Distinct triples in lexicographic (s, p, o) order (== np.unique(axis=0), ~4x faster): one sort of
+    (s << 32 | p), then one of (rank of the (s, p) run << 32 | o)."""
+    n = s.shape[0]
+    if n == 0:
+        return s.copy(), p.copy(), o.copy()
+    k = (s.astype(np.uint64) << np.uint64(32)) | p.astype(np.uint64)
+    i1 = np.argsort(k)
+    ks = k[i1]
+    del k
+    run = np.empty(n, np.uint64)
+    run[0] = 0
+    np.cumsum(ks[1:] != ks[:-1], out=run[1:])
+    del ks
+    k2 = (run << np.uint64(32)) | o[i1].astype(np.uint64)
+    del run
+    i2 = np.argsort(k2)
+    order = i1[i2]
+    k2s = k2[i2]
+    del k2, i1, i2
+    keep = np.ones(n, bool)
+    keep[1:] = k2s[1:] != k2s[:-1]
+    order = order[keep]
+    return s[order], p[order], o[order]
 
 
 def zipf_rdf(name: str, n: int, n_entities: int, n_predicates: int, pred_alpha: float,
@@ -98,21 +118,33 @@ def zipf_rdf(name: str, n: int, n_entities: int, n_predicates: int, pred_alpha: 
     t_cls = terms.add(n_classes, lambda i: f"<http://ex.org/C{i}>")
     t_ent = terms.add(n_entities, lambda i: f"<http://ex.org/e{i}>")
     t_lit = terms.add(n_literals, lambda i: f'"l{i}"')
-    # oversample a little so that deduplication lands near n
+    def draw(m):
+        s = t_ent + _zipf_ranks(rng, n_entities, subj_alpha, m)
+        kind = rng.random(m)
+        is_cls = kind < class_frac
+        is_lit = (kind >= class_frac) & (kind < class_frac + literal_frac)
+        p = t_pred + _zipf_ranks(rng, n_predicates, pred_alpha, m)
+        p = np.where(is_cls, t_type, p)
+        o_ent = t_ent + _zipf_ranks(rng, n_entities, obj_alpha, m)
+        o_cls = t_cls + _zipf_ranks(rng, n_classes, class_alpha, m)
+        o_lit = t_lit + _zipf_ranks(rng, n_literals, lit_alpha, m)
+        o = np.where(is_cls, o_cls, np.where(is_lit, o_lit, o_ent))
+        return s.astype(np.uint32), p.astype(np.uint32), o.astype(np.uint32)
+
+    # oversample a little so that deduplication lands near n; draw more until n distinct triples exist
     m = int(n * 1.08) if dedup else n
-    s = t_ent + _zipf_ranks(rng, n_entities, subj_alpha, m)
-    kind = rng.random(m)
-    is_cls = kind < class_frac
-    is_lit = (kind >= class_frac) & (kind < class_frac + literal_frac)
-    p = t_pred + _zipf_ranks(rng, n_predicates, pred_alpha, m)
-    p = np.where(is_cls, t_type, p)
-    o_ent = t_ent + _zipf_ranks(rng, n_entities, obj_alpha, m)
-    o_cls = t_cls + _zipf_ranks(rng, n_classes, class_alpha, m)
-    o_lit = t_lit + _zipf_ranks(rng, n_literals, lit_alpha, m)
-    o = np.where(is_cls, o_cls, np.where(is_lit, o_lit, o_ent))
-    s, p, o = s.astype(np.uint32), p.astype(np.uint32), o.astype(np.uint32)
+    s, p, o = draw(m)
     if dedup:
         s, p, o = _dedup(s, p, o)
+        for _ in range(16):
+            got = s.shape[0]
+            if got >= n or got == 0:
+                break
+            extra = draw(int((n - got) * (m / got) * 1.25) + 1024)  # distinct yield of the draws so far
+            m += extra[0].shape[0]
+            s, p, o = _dedup(np.concatenate([s, extra[0]]), np.concatenate([p, extra[1]]),
+                             np.concatenate([o, extra[2]]))
+            del extra
         if s.shape[0] > n:
             idx = np.sort(rng.choice(s.shape[0], n, replace=False))
             s, p, o = s[idx], p[idx], o[idx]

@@ -402,3 +402,54 @@ def test_program_host_parser_reproduces_golden(tmp_path, name):
     program.RDFind(["--use-fis", "--clean-implied", "--host-parser", "--support", str(ms), "--output", f"file://{out}",
                     os.path.join(GOLDEN, f"{name}.nt.gz")]).run()
     assert sorted(out.read_text().splitlines()) == expected
+
+
+def test_copy_cinds_decoded_matches_host_decode(ctx):
+    """rdf_copy_cinds_decoded (Cind-shaped rows decoded on the device) equals the host decode of rdf_copy_cinds,
+    for the whole result and for ranges, in every mode."""
+    rng = random.Random(29)
+    for it in range(12):
+        n = rng.randrange(30, 400)
+        nv = rng.randrange(4, 40)
+        arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                       dtype=np.uint32)
+        strategy, clean = MODES[it % 4]
+        ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+        ctx.run(rng.randrange(1, 4), "spo", clean, strategy)
+        host = ctx.decoded_cinds()
+        dev = ctx.copy_cinds_decoded()
+        assert dev.shape[0] == host.shape[0]
+        for a, b in (("dep_capture_type", "dep_code"), ("dep_value1", "dep_v1"), ("dep_value2", "dep_v2"),
+                     ("ref_capture_type", "ref_code"), ("ref_value1", "ref_v1"), ("ref_value2", "ref_v2"),
+                     ("support", "support")):
+            np.testing.assert_array_equal(dev[a], host[b].astype(np.uint32))
+        if host.shape[0] > 5:
+            part = ctx.copy_cinds_decoded(2, 3)
+            np.testing.assert_array_equal(part, dev[2:5])
+    d = synth.config("c2", 0.05)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support)
+    n = ctx.cind_count()
+    dev = ctx.copy_cinds_decoded(n // 3, 1 << 21)
+    host = _lib.decode_rows(ctx.copy_cinds_range(n // 3, 1 << 21), d.num_terms, ctx.binary_keys())
+    np.testing.assert_array_equal(dev["ref_value1"], host["ref_v1"])
+    np.testing.assert_array_equal(dev["dep_capture_type"], host["dep_code"].astype(np.uint32))
+    np.testing.assert_array_equal(dev["support"], host["support"])
+
+
+def test_parse_scratch_released(ctx):
+    """After rdf_parse_ntriples only the text and the term table stay resident: the parse scratch (~36 B per term
+    occurrence + the slot table) is released before discovery (rdf_device_bytes)."""
+    c = _lib.Context(0)
+    try:
+        data = "".join(ln + "\n" for ln in synth.config("c1", 0.2).lines()).encode()
+        before = c.device_bytes()
+        n, v, _ = c.parse_ntriples(data)
+        held = c.device_bytes() - before
+        # text + triples (12 B each) + term table (12 B per term) + small scans; the scratch alone would be
+        # 3 * 36 B per line plus a 2^k * 8 B slot table
+        assert held < len(data) + 16 * n + 16 * v + (1 << 22), (held, len(data), n, v)
+        c.run(10)
+        assert c.cind_count() > 0
+    finally:
+        c.close()

@@ -1,0 +1,112 @@
+"""Full-size parity: the HIP path on BASELINE configs at the largest size one MI355X holds, against the C
+oracle's golden vectors (tests/golden/full_size.json, made by tools/make_full_golden.py with the streamed
+oracle: count + order-independent checksum of (dep, ref, support) rows + stage counts).
+
+* c1 at full size is also compared row by row with the materializing oracle (set equality);
+* c3 at full size additionally verifies sampled CINDs directly against the triples.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from rdfind_amd import _lib, synth
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(GOLDEN, "full_size.json")))
+_DATA = {}
+
+
+def dataset(cfg, scale):
+    key = (cfg, scale)
+    if key not in _DATA:
+        _DATA.clear()  # one full-size input at a time
+        _DATA[key] = synth.config(cfg, scale)
+    return _DATA[key]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = _lib.Context(0)
+    yield c
+    c.close()
+
+
+def fingerprint(d):
+    from tools.make_full_golden import fingerprint as fp
+    return fp(d)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("key", sorted(GOLD))
+def test_full_size_vs_oracle(ctx, key):
+    g = GOLD[key]
+    d = dataset(g["config"], g["scale"])
+    assert d.n == g["n_triples"] and d.num_terms == g["num_terms"]
+    assert str(fingerprint(d)) == g["fingerprint"], "synthetic generator drifted from the golden input"
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support, "spo", g["clean"], g["strategy"])
+    assert ctx.fc["n_frequent_unary"] == g["n_freq_unary"]
+    assert ctx.fc["n_frequent_binary"] == g["n_freq_binary"]
+    assert ctx.groups["n_records"] == g["n_records"]
+    assert ctx.groups["n_captures"] == g["n_freq_captures"]
+    assert ctx.cind_count() == g["n_cinds"]
+    assert ctx.checksum() == int(g["checksum"])
+
+
+def _packed(dep, ref, sup):
+    key = (dep.astype(np.uint64) << np.uint64(32)) | ref.astype(np.uint64)
+    order = np.argsort(key)
+    return key[order], sup[order]
+
+
+@pytest.mark.timeout(300)
+def test_c1_full_rows_vs_oracle(ctx):
+    """c1 (1M triples) at full size: every result row equals the materializing oracle's."""
+    from oracle import c_oracle as C
+    d = dataset("c1", 1.0)
+    for strategy, clean in ((1, True), (0, True), (0, False)):
+        rows, _, st = C.run(d.s, d.p, d.o, d.num_terms, d.min_support, strategy, clean)
+        ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+        ctx.run(d.min_support, "spo", clean, strategy)
+        got = ctx.copy_cinds()
+        assert got.shape[0] == rows.shape[0] == st["n_cinds"]
+        ek, es = _packed(rows["dep"], rows["ref"], rows["support"])
+        gk, gs = _packed(got["dep"], got["ref"], got["support"])
+        np.testing.assert_array_equal(gk, ek)
+        np.testing.assert_array_equal(gs, es)
+
+
+def _capture_joins(d, code, v1, v2):
+    cols = {1: d.s, 2: d.p, 4: d.o}
+    prim, proj = code & 7, (code >> 3) & 7
+    first = prim & -prim
+    second = prim & ~first
+    mask = cols[first] == v1
+    if second:
+        mask &= cols[second] == v2
+    return np.unique(cols[proj][mask])
+
+
+@pytest.mark.timeout(600)
+def test_c3_full_sampled_direct_verification(ctx):
+    """c3 (100M triples, support 25) at full size: sampled CINDs hold on the triples themselves (every join value
+    of the dependent is one of the referenced capture, support = the dependent's distinct join values)."""
+    g = GOLD["c3@1.0/s1_clean"]
+    d = dataset("c3", 1.0)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support)
+    n = ctx.cind_count()
+    assert n == g["n_cinds"]
+    rng = np.random.default_rng(3)
+    offs = rng.choice(n, size=min(16, n), replace=False)
+    sample = np.concatenate([ctx.copy_cinds_range(int(o), 1) for o in offs])
+    dec = _lib.decode_rows(sample, d.num_terms, ctx.binary_keys())
+    for dc, d1, d2, rc, r1, r2, sup in dec.tolist():
+        jd = _capture_joins(d, dc, d1, d2)
+        jr = _capture_joins(d, rc, r1, r2)
+        assert len(jd) == sup >= d.min_support
+        assert np.isin(jd, jr).all()
