@@ -46,25 +46,88 @@ def pmc_traffic(config, family):
     return int(ent["hbm_bytes"]) if ent else None
 
 
-def algorithmic_bytes(name, d, gs, cs, kt_counts):
-    """Minimal HBM bytes a kernel family must move per launch (DESIGN.md 'Kernels and rooflines')."""
-    n = d.n
-    J = gs["n_records"]
+def algorithmic_bytes(name, d, fc, gs, cs, counts):
+    """Minimal HBM bytes a kernel family must move per step ('Algorithmic bytes'), or None
+    for families without a formula (tiny bookkeeping kernels)."""
+    n, V = d.n, d.num_terms
+    J, Jf = gs["n_records"], gs["n_frequent_records"]
+    E = cs["n_explicit_raw"]
     if name == "unary":
-        return 12 * n                                   # read s, p, o once
+        return 12 * n + 12 * V                          # read s, p, o once; write 3 counters per term
+    if name == "binary":
+        return 12 * n + 12 * fc["n_binary_keys"]        # read the triples; one (8-B key, 4-B count) per distinct key
     if name == "emit":
         return 12 * n + 8 * J                           # read triples, write (join, capture) records
     if name == "sort":
-        return 16 * kt_counts["sort_passes_records"]    # read + write each record once per 8-bit pass
+        return 16 * counts["sort_passes_records"]       # read + write each record once per 8-bit pass
+    if name == "support":
+        return 12 * J + 16 * Jf                         # read records + write fresh flags; dk + fk per kept record
+    if name == "groups":
+        return 16 * Jf * counts["group_passes"] + 32 * Jf   # fk sort passes; flags/build/gcap/dgrp gathers
+    if name == "pivot":
+        return 12 * Jf                                  # per (dependent, group): group id + its bounds
+    if name == "light":
+        # every candidate (pivot member) and every group entry of a light dependent read once, each explicit pair
+        # written to its slot, read and written compacted
+        return 4 * cs["n_light_candidates"] + 4 * cs["n_light_entries"] + 24 * E
+    if name == "rules":
+        return 16 * E                                   # read each explicit pair, keep flag, compacted ref
     if name == "cemit":
-        n_out = cs["n_class_cinds"]
-        return 4 * n_out                                # 4-B ref per CIND written (dependent-run output); the shared
+        return 4 * cs["n_class_cinds"]                  # 4-B ref per CIND written (dependent-run output); the shared
                                                         # class lists (< 1 MB) are read from L2
     if name in ("hwrite", "hcount"):
         cand = cs["n_heavy_candidates"]
         out = 4 * cs["n_cinds"] if name == "hwrite" else 4 * cs["n_heavy_chunks"]
         return 20 * cand + out                          # candidate ids + 16-B capture info, output records
     return None
+
+
+def family_rooflines(d, fc, gs, cs, kt, counts):
+    out = {}
+    for name, ms in kt.items():
+        b = algorithmic_bytes(name, d, fc, gs, cs, counts)
+        if b is None or ms <= 0:
+            continue
+        gbs = b / (ms * 1e-3) / 1e9
+        out[name] = {"ms": round(ms, 4), "bytes": int(b), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    return out
+
+
+def t_disc_host(ctx, ms, reps=3):
+    """SURVEY.md 8(d) T_disc: triples resident in HBM -> CIND id-records in host memory (one step + the copy of the
+    CindSet-shaped result, rdf_copy_result_raw, into pinned host memory).  Returns (median ms, details)."""
+    import numpy as np
+    n_refs, n_runs, n_caps = ctx.result_sizes()
+    pinned = True
+    try:
+        import torch
+        refs = torch.empty(max(n_refs, 1), dtype=torch.int32, pin_memory=True)
+        refs_ptr = refs.data_ptr()
+    except Exception:  # no pinned pool: pageable numpy (slower link rate, stated in the line)
+        pinned = False
+        refs = np.empty(max(n_refs, 1), np.uint32)
+        refs_ptr = refs.ctypes.data
+    runoff = np.empty(n_runs + 1, np.uint64)
+    rundep = np.empty(max(n_runs, 1), np.uint32)
+    caps = np.empty(max(n_caps, 1), np.uint32)
+    sups = np.empty(max(n_caps, 1), np.uint32)
+    times, copy_ms = [], []
+    for _ in range(reps):
+        ctx.sync()
+        t0 = time.perf_counter()
+        ctx.run(ms)
+        ctx.sync()
+        t1 = time.perf_counter()
+        ctx.copy_result_raw(refs_ptr, runoff, rundep, caps, sups)
+        t2 = time.perf_counter()
+        times.append((t2 - t0) * 1e3)
+        copy_ms.append((t2 - t1) * 1e3)
+    med = sorted(times)[len(times) // 2]
+    cm = sorted(copy_ms)[len(copy_ms) // 2]
+    nbytes = 4 * n_refs + 12 * n_runs + 8 * n_caps
+    del refs
+    return med, {"ms": round(med, 3), "copy_ms": round(cm, 3), "bytes": nbytes,
+                 "link_gbs": round(nbytes / (cm * 1e-3) / 1e9, 1) if cm > 0 else None, "pinned": pinned}
 
 
 def main():
@@ -77,6 +140,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the N-Triples ingest leg (rank 0, N=1)")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.3)
+    ap.add_argument("--cpu-full-max", type=int, default=20_000_000,
+                    help="time the CPU baseline on the benchmarked workload itself up to this many triples")
+    ap.add_argument("--no-tdisc", action="store_true", help="skip the T_disc (id-records to host) leg")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
                     "exchanges, to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -147,67 +213,77 @@ def main():
 
     gs, fc = ctx.groups, ctx.fc
     kt = {k: v / steps for k, v in kt_sum.items()}
-    counts = {"sort_passes_records": 0}
-    # passes of the record sort (bits = join bits + capture bits, 8 per pass)
+    # passes of the record sort (bits = join bits + capture bits, 8 per pass) and of the group sort (join bits)
     V = d.num_terms
     capbits = int(2 * sum(fc["n_frequent_unary"]) + fc["n_frequent_binary"] - 1).bit_length()  # compact capture ids
-    joinbits = int(V - 1).bit_length()
-    counts["sort_passes_records"] = ((capbits + joinbits + 7) // 8) * gs["n_records"]
+    joinbits = max(int(V - 1).bit_length(), 1)
+    counts = {"sort_passes_records": ((capbits + joinbits + 7) // 8) * gs["n_records"],
+              "group_passes": (joinbits + 7) // 8}
+    fams = family_rooflines(d, fc, gs, cs, kt, counts)
     dominant = max(kt, key=lambda k: kt[k])
     roof = None
     for name in [dominant] + sorted(kt, key=lambda k: -kt[k]):
-        b = algorithmic_bytes(name, d, gs, cs, counts)
-        if b is not None and kt[name] > 0:
-            achieved = b / (kt[name] * 1e-3) / 1e9
-            roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(args.config, name) if args.scale == 1.0 and world == 1 else None,
-                    "ms": round(kt[name], 4), "bytes_per_launch": int(b), "dominant_kernel": dominant,
+        if name in fams:
+            f = fams[name]
+            roof = {"bound": "hbm", "kernel": name, "achieved": f["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": f["frac"], "traffic": pmc_traffic(args.config, name) if args.scale == 1.0 and world == 1 else None,
+                    "ms": f["ms"], "bytes_per_launch": f["bytes"], "dominant_kernel": dominant,
                     "dominant_ms": round(kt[dominant], 4)}
             break
 
     # BASELINE metric also names "% HBM roofline of count kernels": K1 (unary) and K2 (binary condition counts)
-    count_roof = {}
-    for name, b in (("unary", 12 * d.n), ("binary", 12 * d.n + 12 * fc["n_binary_keys"])):
-        if kt.get(name, 0) > 0:
-            gbs = b / (kt[name] * 1e-3) / 1e9
-            count_roof[name] = {"bytes": int(b), "ms": round(kt[name], 4), "achieved": round(gbs, 1),
-                                "frac": round(gbs / HBM_PEAK_GBS, 4), "bound": "memory-side atomics"}
+    count_roof = {k: dict(fams[k], bound="hbm") for k in ("unary", "binary") if k in fams}
+
+    tdisc = None
+    if rank == 0 and world == 1 and not args.no_tdisc:
+        tms, tdisc = t_disc_host(ctx, ms)
+        tdisc["triples_per_s"] = round(d.n / (tms * 1e-3), 1)
+        tdisc["note"] = ("SURVEY.md 8(d) T_disc: one step + copy of the CindSet-shaped id-records (4 B per CIND + run "
+                         "table) to host memory; median of 3")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import c_oracle
 
-        sd = synth.config(args.config, args.cpu_sample_scale)
+        # the same workload when the streamed C restatement finishes in ~30 s on the box's threads, else a sample
+        cpu_scale = args.scale if d.n <= args.cpu_full_max else args.cpu_sample_scale
+        sd = d if cpu_scale == args.scale else synth.config(args.config, cpu_scale)
         t = time.perf_counter()
-        _, _, st = c_oracle.run(sd.s, sd.p, sd.o, sd.num_terms, sd.min_support, 1, True)
+        r = c_oracle.stream(sd.s, sd.p, sd.o, sd.num_terms, sd.min_support, 1, True)
         ct = time.perf_counter() - t
         nt = c_oracle.threads()
+        same = cpu_scale == args.scale
         cpu = {"value": round(sd.n / ct, 1), "unit": "triples/s", "cores": nt, "kind": "port",
-               "sample": f"{args.config} scale {args.cpu_sample_scale} ({sd.n} triples, {st['n_cinds']} CINDs) "
-                         f"through oracle/c/rdfind_oracle.c on {nt} OpenMP threads, {ct:.1f}s"}
+               "sample": f"{args.config} scale {cpu_scale} ({sd.n} triples, {r['n_cinds']} CINDs"
+                         f"{', the benchmarked workload itself' if same else ''}) through oracle/c/rdfind_oracle.c "
+                         f"(streamed count + checksum, same stages incl. minimality) on {nt} OpenMP threads, {ct:.1f}s"}
+        if same:
+            cpu["matches_gpu"] = bool(r["n_cinds"] == cs["n_cinds"] and r["checksum"] == ctx.checksum())
 
     ingest = None
     if rank == 0 and world == 1 and not args.no_ingest:
         # parse/encode timed separately -- the same triples as N-Triples text through
-        # rdf_parse_ntriples (device time, text already uploaded; the ids/terms are checked by tests/)
+        # rdf_parse_ntriples (ids/terms are checked by tests/)
         import numpy as np
 
         tt = d.terms.term
         strs = np.array([tt(i) + " " for i in range(d.num_terms)], dtype=object)
         text = "".join(map("".join, zip(strs[d.s], strs[d.p], strs[d.o], [".\n"] * d.n))).encode()
         del strs
-        pt = []
+        pt, wt = [], []
         for _ in range(3):
+            t0 = time.perf_counter()
             n_parsed, n_terms, pms = ctx.parse_ntriples(text)
+            wt.append((time.perf_counter() - t0) * 1e3)
             pt.append(pms)
-        pms = sorted(pt)[1]
+        pms, wms = sorted(pt)[1], sorted(wt)[1]
         assert n_parsed == d.n
         ingest = {"ms": round(pms, 3), "text_bytes": len(text), "gbs_text": round(len(text) / pms / 1e6, 1),
                   "triples_per_s": round(d.n / pms * 1e3, 1), "terms": n_terms,
-                  "end_to_end_ms": round(pms + ms_per_step, 3),
-                  "note": "rdf_parse_ntriples device time (median of 3), excl. the text's H2D copy; end_to_end = "
-                          "ingest + one discovery step, both device-resident"}
+                  "wall_ms_incl_h2d": round(wms, 3), "device_resident_ms": round(pms + ms_per_step, 3),
+                  "note": "ms: rdf_parse_ntriples device time (median of 3), text already in HBM; wall_ms_incl_h2d: "
+                          "the same call timed on the host, including the text's upload from pageable memory; "
+                          "device_resident_ms = ingest + one discovery step, both device-resident"}
         del text
 
     if rank == 0:
@@ -219,7 +295,8 @@ def main():
                                    f"scale {args.scale}, support {ms}, strategy 1 --use-fis --clean-implied)",
                        "triples": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
                        "parallelism": f"join-hash shards x{world} (RCCL)" if world > 1 else "single"},
-            "roofline": roof, "count_kernels": count_roof, "cpu_baseline": cpu, "ingest": ingest,
+            "roofline": roof, "count_kernels": count_roof, "families": fams, "t_disc_host": tdisc,
+            "cpu_baseline": cpu, "ingest": ingest,
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],

@@ -1,0 +1,426 @@
+// Partitioned condition counting: K1 (unary) and K2 (binary) without per-key global atomics.
+// Included by kernels.inl after the wave-merge helpers.
+//
+// Both counts follow one shape: pass A histograms the keys of each block's contiguous chunk of triples over
+// key buckets (LDS counters), an exclusive scan turns the bucket-major histogram into write offsets, pass B
+// re-reads the chunk and scatters compact bucket-relative records, and one block per bucket (slice) counts
+// them in LDS and keeps what reaches the support.
+//
+//   K1 (FrequentConditionPlanner.findFrequentSingleConditions, ALG/plan/FrequentConditionPlanner.scala:291-311):
+//      key = pos * V + value, bucket = key >> bits (bits = 14, or 15 for a large |V|), record = the low key bits
+//      (u16).  The count block holds the bucket's counters in LDS and writes frank = the key's rank among the
+//      frequent keys of its 2^14-key rank block (or NONE), the block's frequent count (scanned into boff, so
+//      frank_at gives global ranks) and the frequency bitmap fbits (1 bit per key: 2.75 MB on LUBM-100, read
+//      from L2 by K2).
+//   K2 (CreatedReducedDoubleConditionCounts.scala:45-86 + groupBy(type, v1, v2).sum,
+//      FrequentConditionPlanner.scala:374-394): key = bt << 62 | v1 << 31 | v2 of triples whose two values are
+//      frequent (fbits), merged across the wave first (wave_merge, so a record counts <= 64 occurrences);
+//      bucket = hash(key) >> (64 - bits), record = (u64 key, u8 count).  The count blocks aggregate each bucket
+//      in an LDS hash table sized to the bucket and append the frequent keys.
+
+static constexpr int FR_BITS = 14;             // rank blocks: frank_at adds boff[key >> FR_BITS]
+static constexpr u32 FR_R = 1u << FR_BITS;
+static constexpr u32 U2_MAXB = 32768;          // K1 buckets (128 KB of LDS in the histogram passes)
+static constexpr u64 U2_SLICE = 1ull << 18;    // K1 records per counting block
+static constexpr int U2_CBLOCK = 1024;         // threads of a counting block
+static constexpr int B2_MAXBITS = 13;          // K2 buckets <= 8192 (32 KB of LDS in the histogram passes)
+static constexpr int B2_SLOTS = 4096;          // LDS hash slots of a K2 counting block (48 KB: 3 blocks per CU)
+static constexpr u64 B2_TARGET = 1024;         // target K2 records per bucket (sizes the bucket count)
+static constexpr int B2_PBLOCK = 1024;         // threads of a K2 histogram / scatter block
+
+// global rank of unary condition i (= pos * V + value) among all frequent conditions, or NONE
+__device__ inline u32 frank_at(const u32* __restrict__ frank, const u32* __restrict__ boff, u64 i) {
+    const u32 r = frank[i];
+    return r == NONE32 ? NONE32 : r + boff[i >> FR_BITS];
+}
+
+__device__ inline bool fbit(const u64* __restrict__ fbits, u64 i) { return (fbits[i >> 6] >> (i & 63)) & 1ull; }
+
+// One leader round of wave merging on a bucket index: lanes whose bucket equals the first active lane's take
+// consecutive positions from one LDS atomic; the other lanes take one atomic each.  Returns this lane's slot
+// (SCATTER pass) or adds to the histogram.  A bucket's records are counted in any order.
+__device__ inline u32 bucket_slot(u32* lh, u32 bk, bool active) {
+    const u64 A = __ballot(active);
+    u32 pos = 0;
+    if (A) {
+        const int l = __ffsll((long long)A) - 1;
+        const u32 bl = __shfl(bk, l, RDF_WAVE);
+        const bool mine = active && bk == bl;
+        const u64 m = __ballot(mine);
+        u32 base = 0;
+        if (lane_id() == l) base = atomicAdd(&lh[bl], (u32)__popcll(m));
+        base = __shfl(base, l, RDF_WAVE);
+        if (mine) pos = base + (u32)__popcll(m & lanemask_lt());
+        else if (active) pos = atomicAdd(&lh[bk], 1u);
+    }
+    return pos;
+}
+
+// ---- K1 ----------------------------------------------------------------------------------------
+
+template <bool SCATTER>
+__global__ __launch_bounds__(RDF_BLOCK) void k_u2_part(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                       const u32* __restrict__ o, u64 n, u32 V, u32 NB, int bits,
+                                                       u32* ghist, uint16_t* __restrict__ recs) {
+    extern __shared__ u32 lh[];
+    for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
+    __syncthreads();
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    const u64 lmask = (1ull << bits) - 1;
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        const bool act = i < e;
+        const u64 key[3] = {act ? (u64)s[i] : 0, act ? (u64)V + p[i] : 0, act ? 2ull * V + o[i] : 0};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const u32 pos = bucket_slot(lh, (u32)(key[t] >> bits), act);
+            if (SCATTER && act) recs[pos] = (uint16_t)(key[t] & lmask);
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
+    }
+}
+
+// slices per bucket (>= 1 so every bucket's ranks are written); multi-slice buckets get their global counter
+// range zeroed here (their slices add into it)
+__global__ __launch_bounds__(RDF_BLOCK) void k_u2_slices(const u32* __restrict__ ghist, u32 NB, u32 G, int bits, u64 K,
+                                                         u32* nsl, u32* cntg) {
+    const u32 b = blockIdx.x;
+    if (b >= NB) return;
+    const u64 len = ghist[(u64)(b + 1) * G] - ghist[(u64)b * G];
+    const u64 k = (len + U2_SLICE - 1) / U2_SLICE;
+    if (threadIdx.x == 0) nsl[b] = k < 1 ? 1u : (u32)k;
+    if (k > 1) {
+        const u64 base = (u64)b << bits, R = 1ull << bits;
+        const u32 lim = (u32)(K - base < R ? K - base : R);
+        for (u32 i = threadIdx.x; i < lim; i += RDF_BLOCK) cntg[base + i] = 0;
+    }
+}
+
+// counts of a bucket -> ranks.  Per 2^14-key rank block r: frank[key] = rank among r's keys with count >= ms
+// (NONE otherwise), bfreq[r] = their number, fstage[r * FR_R + rank] = key offset in r (for fval), fbits = the
+// flags.  nbound[t] (t = 1, 2) = frequent keys of the rank block holding t * V that lie below t * V.
+// Wave w owns keys [w * PER, (w + 1) * PER) of the bucket; two sweeps of 64-key ballots.
+template <int BITS>
+__device__ inline void u2_ranks(const u32* lc, u32 lim, u32 ms, u64 base, u64 V, u32* frank, u32* bfreq, u32* fstage,
+                                u64* fbits, u64* nbound) {
+    __shared__ u32 s_wtot[U2_CBLOCK / RDF_WAVE];
+    constexpr u32 NW = U2_CBLOCK / RDF_WAVE, PER = (1u << BITS) / NW, WPR = FR_R / PER;  // waves per rank block
+    const u32 w = threadIdx.x / RDF_WAVE, lane = lane_id();
+    u32 tot = 0;
+    for (u32 it = 0; it < PER; it += RDF_WAVE) {
+        const u32 k = w * PER + it + lane;
+        tot += (u32)__popcll(__ballot(k < lim && lc[k] >= ms));
+    }
+    if (lane == 0) s_wtot[w] = tot;
+    __syncthreads();
+    const u32 w0 = w / WPR * WPR;  // first wave of this rank block
+    u32 off = 0, all = 0;
+    for (u32 j = w0; j < w0 + WPR; ++j) {
+        off += j < w ? s_wtot[j] : 0u;
+        all += s_wtot[j];
+    }
+    const u64 rb = (base >> FR_BITS) + w / WPR;  // rank block index
+    for (u32 it = 0; it < PER; it += RDF_WAVE) {
+        const u32 k = w * PER + it + lane;
+        const bool f = k < lim && lc[k] >= ms;
+        const u64 m = __ballot(f);
+        if (k < lim) {
+            const u32 r = off + (u32)__popcll(m & lanemask_lt());
+            frank[base + k] = f ? r : NONE32;
+            if (f) fstage[(rb << FR_BITS) + r] = (u32)((base + k) & (FR_R - 1));
+        }
+        const u64 kb = base + w * PER + it;  // first key of this 64-key window (64-aligned)
+        if (lane == 0 && w * PER + it < lim) {
+            fbits[kb >> 6] = m;
+            for (int t = 1; t <= 2; ++t) {  // t * V inside the window: frequent keys of the rank block below it
+                const u64 bnd = (u64)t * V;
+                if (bnd >= kb && bnd < kb + RDF_WAVE) {
+                    const u32 below = (u32)(bnd - kb);
+                    nbound[t] = off + (u32)__popcll(m & ((1ull << below) - 1));
+                }
+            }
+        }
+        off += (u32)__popcll(m);
+    }
+    if (lane == 0 && w == w0) bfreq[rb] = all;
+}
+
+// one block per (bucket, slice) of the compact slice list soff (exclusive scan of nsl); ghist = scanned
+// bucket-major histogram (G blocks per bucket)
+template <int BITS>
+__global__ __launch_bounds__(U2_CBLOCK) void k_u2_count(const uint16_t* __restrict__ recs, const u32* __restrict__ ghist,
+                                                        const u32* __restrict__ soff, u32 NB, u32 G, u64 K, u32 V, u32 ms,
+                                                        u32* frank, u32* bfreq, u32* fstage, u64* fbits, u64* nbound,
+                                                        u32* cntg, int counts_only) {
+    constexpr u32 R = 1u << BITS;
+    __shared__ u32 lc[R];
+    const u32 x = blockIdx.x;
+    if (x >= soff[NB]) return;
+    u32 lo = 0, hi = NB;  // last bucket with soff[b] <= x
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (soff[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    const u32 bk = lo, j = x - soff[bk];
+    const u64 nsl = soff[bk + 1] - soff[bk];
+    const u64 start = ghist[(u64)bk * G], end = ghist[(u64)(bk + 1) * G];
+    const u64 len = end - start;
+    const u64 s0 = start + len * j / nsl, s1 = start + len * (j + 1) / nsl;
+    for (u32 i = threadIdx.x; i < R; i += U2_CBLOCK) lc[i] = 0;
+    __syncthreads();
+    // records in 16-B vectors (8 per lane) between the unaligned head and tail
+    const u64 a0 = (s0 + 7) & ~7ull, a1 = s1 & ~7ull;
+    if (a0 < a1) {
+        for (u64 i = s0 + threadIdx.x; i < a0; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
+        const uint4* v = (const uint4*)(recs + a0);
+        for (u64 q = threadIdx.x; q < (a1 - a0) / 8; q += U2_CBLOCK) {
+            const uint4 w = v[q];
+            const u32 ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                atomicAdd(&lc[ww[h] & 0xffffu], 1u);
+                atomicAdd(&lc[ww[h] >> 16], 1u);
+            }
+        }
+        for (u64 i = a1 + threadIdx.x; i < s1; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
+    } else {
+        for (u64 i = s0 + threadIdx.x; i < s1; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
+    }
+    __syncthreads();
+    const u64 base = (u64)bk << BITS;
+    const u32 lim = (u32)(K - base < R ? K - base : R);
+    if (nsl == 1 && counts_only) {  // sharded input: the dense local counts, summed over ranks before ranking
+        for (u32 i = threadIdx.x; i < lim; i += U2_CBLOCK) cntg[base + i] = lc[i];
+    } else if (nsl == 1) {
+        u2_ranks<BITS>(lc, lim, ms, base, V, frank, bfreq, fstage, fbits, nbound);
+    } else {  // several slices share the bucket: sum into its zeroed global counters, ranked by k_u2_finish
+        for (u32 i = threadIdx.x; i < lim; i += U2_CBLOCK)
+            if (lc[i]) atomicAdd(&cntg[base + i], lc[i]);
+    }
+}
+
+// ranks of the multi-slice buckets (one block each; single-slice buckets exit)
+template <int BITS>
+__global__ __launch_bounds__(U2_CBLOCK) void k_u2_finish(const u32* __restrict__ soff, u32 NB, u64 K, u32 V, u32 ms,
+                                                         const u32* __restrict__ cntg, u32* frank, u32* bfreq, u32* fstage,
+                                                         u64* fbits, u64* nbound) {
+    constexpr u32 R = 1u << BITS;
+    __shared__ u32 lc[R];
+    const u32 bk = blockIdx.x;
+    if (bk >= NB || soff[bk + 1] - soff[bk] <= 1) return;
+    const u64 base = (u64)bk << BITS;
+    const u32 lim = (u32)(K - base < R ? K - base : R);
+    for (u32 i = threadIdx.x; i < R; i += U2_CBLOCK) lc[i] = i < lim ? cntg[base + i] : 0u;
+    __syncthreads();
+    u2_ranks<BITS>(lc, lim, ms, base, V, frank, bfreq, fstage, fbits, nbound);
+}
+
+// fval[u] = value of the frequent condition with global rank u (boff = scanned rank-block totals, NR blocks), and
+// frank[key] = u: the block-local ranks become global, so later stages read frank directly
+__global__ __launch_bounds__(RDF_BLOCK) void k_u2_fval(const u32* __restrict__ boff, u32 NR, const u32* __restrict__ fstage,
+                                                       u32 V, u32* fval, u32* frank) {
+    const u32 U = boff[NR];
+    for (u64 u = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; u < U; u += (u64)gridDim.x * RDF_BLOCK) {
+        u32 lo = 0, hi = NR;  // last rank block with boff[r] <= u
+        while (hi - lo > 1) {
+            const u32 mid = (lo + hi) >> 1;
+            if (boff[mid] <= u) lo = mid;
+            else hi = mid;
+        }
+        const u64 key = ((u64)lo << FR_BITS) + fstage[((u64)lo << FR_BITS) + (u - boff[lo])];
+        fval[u] = (u32)(key % V);
+        frank[key] = (u32)u;
+    }
+}
+
+// fallback path (global-atomic counts): frequency bitmap from the counters
+__global__ __launch_bounds__(RDF_BLOCK) void k_fbits_from_counts(const u32* __restrict__ cnt, u64 K, u32 ms, u64* fbits) {
+    const u64 n_round = (K + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n_round; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 m = __ballot(i < K && cnt[i] >= ms);
+        if (lane_id() == 0) fbits[i >> 6] = m;
+    }
+}
+
+// ---- K2 ----------------------------------------------------------------------------------------
+
+static constexpr u64 B2_SLICE = 2560;          // K2 records per counting slice (table: next power of two >= 2x, <= B2_SLOTS)
+
+__device__ inline u32 b2_bucket(u64 key, int bits) { return (u32)(mix64(key) >> (64 - bits)); }
+
+// the binary keys of one triple window with runs of equal keys in adjacent lanes merged (the same merge in both
+// passes, so the histogram pass and the scatter pass agree; a record counts <= 64 occurrences)
+__device__ inline void b2_keys(const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o, u64 i,
+                               bool act, u32 V, const u64* __restrict__ fbits, u64 (&key)[3], u32 (&cnt)[3]) {
+    u32 ts = 0, tp = 0, to = 0;
+    bool fs = false, fp = false, fo = false;
+    if (act) {
+        ts = s[i];
+        tp = p[i];
+        to = o[i];
+        fs = fbit(fbits, ts);
+        fp = fbit(fbits, (u64)V + tp);
+        fo = fbit(fbits, 2ull * V + to);
+    }
+    key[0] = bin_key(2, ts, tp);  // o[s,p] (35)
+    key[1] = bin_key(1, ts, to);  // p[s,o] (21)
+    key[2] = bin_key(0, tp, to);  // s[p,o] (14)
+    cnt[0] = wave_merge<u64, 0>(key[0], fs && fp);
+    cnt[1] = wave_merge<u64, 0>(key[1], fs && fo);
+    cnt[2] = wave_merge<u64, 0>(key[2], fp && fo);
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                       const u32* __restrict__ o, u64 n, u32 V, const u64* __restrict__ fbits,
+                                                       int bits, u32* ghist, u64* __restrict__ rkeys,
+                                                       uint8_t* __restrict__ rcnt) {
+    extern __shared__ u32 lh[];
+    const u32 NB = 1u << bits;
+    for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
+    __syncthreads();
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (u64 i0 = b; i0 < e; i0 += B2_PBLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        u64 key[3];
+        u32 cnt[3];
+        b2_keys(s, p, o, i, i < e, V, fbits, key, cnt);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const bool a = cnt[t] != 0;
+            const u32 pos = bucket_slot(lh, a ? b2_bucket(key[t], bits) : 0u, a);
+            if (SCATTER && a) {
+                rkeys[pos] = key[t];
+                rcnt[pos] = (uint8_t)cnt[t];
+            }
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_b2_slices(const u32* __restrict__ ghist, u32 NB, u32 G, u32* nsl) {
+    for (u32 b = blockIdx.x * RDF_BLOCK + threadIdx.x; b < NB; b += gridDim.x * RDF_BLOCK) {
+        const u64 len = ghist[(u64)(b + 1) * G] - ghist[(u64)b * G];
+        const u64 k = (len + B2_SLICE - 1) / B2_SLICE;
+        nsl[b] = k < 1 ? 1u : (u32)k;
+    }
+}
+
+// Blocks loop over the (bucket, slice) list soff: LDS hash aggregation of a slice's (key, count) records in a table
+// of 2x the slice (<= B2_SLOTS).  A bucket held by one slice appends its frequent keys (count >= ms) to out and
+// counts its distinct keys; the slices of a larger bucket (hot keys) append all their (key, count) partials to the
+// spill list instead, which one global table then sums (as do records a crowded table refused).
+// counters: [0] frequent keys in out, [1] distinct keys, [2] spill entries.
+__global__ __launch_bounds__(RDF_BLOCK) void k_b2_count(const u64* __restrict__ rkeys, const uint8_t* __restrict__ rcnt,
+                                                        const u32* __restrict__ ghist, const u32* __restrict__ soff, u32 NB,
+                                                        u32 G, u32 ms, u64* out, u64* spill_keys, u32* spill_cnt,
+                                                        u64* counters, int all_to_spill) {
+    __shared__ u64 tk[B2_SLOTS];
+    __shared__ u32 tc[B2_SLOTS];
+    __shared__ u32 s_part[RDF_WAVES_PER_BLOCK];
+    __shared__ u64 s_base;
+    const u32 nslices = soff[NB];
+    u32 nd_acc = 0;
+    for (u32 x = blockIdx.x; x < nslices; x += gridDim.x) {
+        u32 lo = 0, hi = NB;  // last bucket with soff[b] <= x
+        while (hi - lo > 1) {
+            const u32 mid = (lo + hi) >> 1;
+            if (soff[mid] <= x) lo = mid;
+            else hi = mid;
+        }
+        const u32 bk = lo, j = x - soff[bk];
+        const u64 nsl = soff[bk + 1] - soff[bk];
+        const u64 start = ghist[(u64)bk * G], end = ghist[(u64)(bk + 1) * G];
+        const u64 len = end - start;
+        const u64 s0 = start + len * j / nsl, s1 = start + len * (j + 1) / nsl;
+        u32 T = 64;
+        while (T < B2_SLOTS && T < 2 * (s1 - s0)) T <<= 1;
+        for (u32 i = threadIdx.x; i < T; i += RDF_BLOCK) {
+            tk[i] = EMPTY64;
+            tc[i] = 0;
+        }
+        __syncthreads();
+        for (u64 i = s0 + threadIdx.x; i < s1; i += RDF_BLOCK) {
+            const u64 key = rkeys[i];
+            const u32 c = rcnt[i];
+            u32 h = (u32)mix64(key) & (T - 1);  // low hash bits (the bucket used the high ones)
+            bool done = false;
+            for (u32 probe = 0; probe < 32 && !done; ++probe) {
+                u64 k = tk[h];
+                if (k == EMPTY64) {
+                    const u64 prev = atomicCAS(&tk[h], EMPTY64, key);
+                    k = prev == EMPTY64 ? key : prev;
+                }
+                if (k == key) {
+                    atomicAdd(&tc[h], c);
+                    done = true;
+                }
+                h = (h + 1) & (T - 1);
+            }
+            if (!done) {  // a crowded table: the record goes to the spill list
+                const u64 at = atomicAdd(&counters[2], 1ull);
+                spill_keys[at] = key;
+                spill_cnt[at] = c;
+            }
+        }
+        __syncthreads();
+        const u32 per = (T + RDF_BLOCK - 1) / RDF_BLOCK;  // consecutive slots per thread
+        const bool single = nsl == 1 && !all_to_spill;  // all_to_spill: local partials for the sharded exchange
+        u32 nsel = 0, nd = 0;
+        for (u32 q = 0; q < per; ++q) {
+            const u32 slot = threadIdx.x * per + q;
+            if (slot < T && tk[slot] != EMPTY64) {
+                ++nd;
+                nsel += single ? (tc[slot] >= ms) : 1u;
+            }
+        }
+        if (single) nd_acc += nd;
+        // one reservation per slice
+        const u32 w = threadIdx.x / RDF_WAVE;
+        const u32 incl = wave_inclusive_scan(nsel);
+        if (lane_id() == RDF_WAVE - 1) s_part[w] = incl;
+        __syncthreads();
+        u32 woff = 0, tot = 0;
+        for (u32 k = 0; k < RDF_WAVES_PER_BLOCK; ++k) {
+            woff += k < w ? s_part[k] : 0u;
+            tot += s_part[k];
+        }
+        if (threadIdx.x == 0) s_base = tot ? atomicAdd(single ? &counters[0] : &counters[2], (u64)tot) : 0;
+        __syncthreads();
+        u64 pos = s_base + woff + incl - nsel;
+        for (u32 q = 0; q < per; ++q) {
+            const u32 slot = threadIdx.x * per + q;
+            if (slot >= T || tk[slot] == EMPTY64) continue;
+            if (single) {
+                if (tc[slot] >= ms) out[pos++] = tk[slot];
+            } else {
+                spill_keys[pos] = tk[slot];
+                spill_cnt[pos] = tc[slot];
+                ++pos;
+            }
+        }
+        __syncthreads();  // the table is reused by the next slice
+    }
+    nd_acc = wave_sum(nd_acc);
+    __shared__ u32 s_nd[RDF_WAVES_PER_BLOCK];
+    if (lane_id() == 0) s_nd[threadIdx.x / RDF_WAVE] = nd_acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 t = 0;
+        for (int k = 0; k < RDF_WAVES_PER_BLOCK; ++k) t += s_nd[k];
+        if (t) atomicAdd(&counters[1], t);
+    }
+}
+
+// spill entries -> one global open-addressing table (summed counts), then k_bin_freq_flags / k_bin_freq_scatter
+__global__ __launch_bounds__(RDF_BLOCK) void k_spill_insert(const u64* __restrict__ keys, const u32* __restrict__ cnt, u64 n,
+                                                            u64* tkeys, u32* tcnt, u64 tmask);

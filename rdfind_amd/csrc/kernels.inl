@@ -129,114 +129,7 @@ __device__ inline u32 wave_merge_weighted(T key, bool active, u32 w) {
     return cnt;
 }
 
-// K1, partitioned (no per-key global atomics).  After the wave merge, every (key, count) pair goes to the
-// bucket of its key's high bits (UC_R = 2^UC_BITS counters, one LDS image); pass 1 histograms the buckets
-// per block, pass 2 scatters the pairs into bucket order (positions from LDS atomics: the order inside a
-// bucket is irrelevant to counting), then one block per bucket (a few slices for a hot bucket) counts its
-// pairs in LDS and writes the bucket's counters with plain coalesced stores.
-static constexpr int UC_BITS = 13;
-static constexpr u32 UC_R = 1u << UC_BITS;
-static constexpr u32 UC_MAXB = 4096;        // buckets: 3V <= 2^26
-static constexpr u64 UC_SLICE = 1ull << 15; // pairs per counting block
-#ifndef RDF_UCM
-#define RDF_UCM 0, 2, 1
-#endif
-static constexpr int UCM_ROUNDS[3] = {RDF_UCM};  // wave-merge leader rounds for the s / p / o keys
-static constexpr int UCM_S = UCM_ROUNDS[0], UCM_P = UCM_ROUNDS[1], UCM_O = UCM_ROUNDS[2];
-
-template <bool SCATTER>
-__global__ __launch_bounds__(RDF_BLOCK) void k_ucount_part(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                           const u32* __restrict__ o, u64 n, u32 V, u32 NB, u32* ghist,
-                                                           u64* __restrict__ pairs) {
-    __shared__ u32 lh[UC_MAXB];
-    for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
-    __syncthreads();
-    const u64 per = (n + gridDim.x - 1) / gridDim.x;
-    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
-    // the next iteration's triple is loaded before this one is processed (few waves per SIMD: the loads'
-    // latency would otherwise be paid once per iteration)
-    u32 ns = 0, np = 0, no = 0;
-    if (b + threadIdx.x < e) {
-        ns = s[b + threadIdx.x];
-        np = p[b + threadIdx.x];
-        no = o[b + threadIdx.x];
-    }
-    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
-        const u64 i = i0 + threadIdx.x;
-        const bool act = i < e;
-        u32 key[3], c[3];
-        key[0] = ns;
-        key[1] = V + np;
-        key[2] = 2u * V + no;
-        if (i + RDF_BLOCK < e) {
-            ns = s[i + RDF_BLOCK];
-            np = p[i + RDF_BLOCK];
-            no = o[i + RDF_BLOCK];
-        }
-        c[0] = wave_merge<u32, UCM_S>(key[0], act);
-        c[1] = wave_merge<u32, UCM_P>(key[1], act);
-        c[2] = wave_merge<u32, UCM_O>(key[2], act);
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            if (!c[t]) continue;
-            const u32 bk = key[t] >> UC_BITS;
-            if (SCATTER) pairs[atomicAdd(&lh[bk], 1u)] = ((u64)key[t] << 32) | c[t];
-            else atomicAdd(&lh[bk], 1u);
-        }
-    }
-    if (!SCATTER) {
-        __syncthreads();
-        for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
-    }
-}
-
-// slices per bucket: ceil(len / UC_SLICE) (at least 1, so every bucket's counters get written)
-__global__ __launch_bounds__(RDF_BLOCK) void k_ucount_nslices(const u32* __restrict__ ghist, u32 NB, u32 G, u32* nsl) {
-    for (u32 b = blockIdx.x * RDF_BLOCK + threadIdx.x; b < NB; b += gridDim.x * RDF_BLOCK) {
-        const u64 len = ghist[(u64)(b + 1) * G] - ghist[(u64)b * G];
-        const u64 k = (len + UC_SLICE - 1) / UC_SLICE;
-        nsl[b] = k < 1 ? 1u : (u32)k;
-    }
-}
-
-// one block per (bucket, slice) of the compact slice list soff (exclusive scan of nsl, soff[NB] = total);
-// ghist = exclusive scan of the bucket-major histogram (G blocks per bucket, ghist[NB * G] = total pairs)
-__global__ __launch_bounds__(RDF_BLOCK) void k_ucount_bucket(const u64* __restrict__ pairs, const u32* __restrict__ ghist,
-                                                             const u32* __restrict__ soff, u32 NB, u32 G, u64 K, u32* cnt) {
-    __shared__ u32 lc[UC_R];
-    const u32 x = blockIdx.x;
-    if (x >= soff[NB]) return;
-    u32 lo = 0, hi = NB;  // last bucket with soff[b] <= x
-    while (hi - lo > 1) {
-        const u32 mid = (lo + hi) >> 1;
-        if (soff[mid] <= x) lo = mid;
-        else hi = mid;
-    }
-    const u32 bk = lo, j = x - soff[bk];
-    const u64 nsl = soff[bk + 1] - soff[bk];
-    const u64 start = ghist[(u64)bk * G], end = ghist[(u64)(bk + 1) * G];
-    const u64 len = end - start;
-    const u64 s0 = start + len * j / nsl, s1 = start + len * (j + 1) / nsl;
-    for (u32 i = threadIdx.x; i < UC_R; i += RDF_BLOCK) lc[i] = 0;
-    __syncthreads();
-    const u64 n_round = s0 + (s1 - s0 + RDF_BLOCK - 1) / RDF_BLOCK * RDF_BLOCK;
-    for (u64 i = s0 + threadIdx.x; i < n_round; i += RDF_BLOCK) {
-        const bool act = i < s1;
-        const u64 pr = act ? pairs[i] : 0ull;
-        const u32 key = (u32)(pr >> 32);
-        const u32 c = wave_merge_weighted<u32, 2>(key, act, (u32)pr);
-        if (c) atomicAdd(&lc[key & (UC_R - 1)], c);
-    }
-    __syncthreads();
-    const u64 base = (u64)bk << UC_BITS;
-    const u32 lim = K - base < UC_R ? (u32)(K - base) : UC_R;
-    if (nsl == 1) {
-        for (u32 i = threadIdx.x; i < lim; i += RDF_BLOCK) cnt[base + i] = lc[i];
-    } else {  // several slices share the bucket (cnt was zeroed)
-        for (u32 i = threadIdx.x; i < lim; i += RDF_BLOCK)
-            if (lc[i]) atomicAdd(&cnt[base + i], lc[i]);
-    }
-}
+#include "counts.inl"
 
 // Block-reduced counter add (all threads of the block call it): device-scope atomics execute at the
 // memory side, ~11 ns apart on one address, so one per block instead of one per wave.
@@ -330,19 +223,21 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_external_ids(const u32* __restric
 //     ALG/operators/candidate_extraction/CreatedReducedDoubleConditionCounts.scala:45-86, + groupBy.sum
 //     FrequentConditionPlanner.scala:571-591).  Only triples with >= 2 frequent values emit sp/so/po.
 
-__device__ inline void freq_flags(const u32* cnt, u32 V, u32 ms, u32 s, u32 p, u32 o, bool& fs, bool& fp, bool& fo) {
-    fs = cnt[s] >= ms;
-    fp = cnt[V + p] >= ms;
-    fo = cnt[2u * V + o] >= ms;
+__device__ inline void freq_flags(const u32* frank, const u32* boff, u32 V, u32 s, u32 p, u32 o, bool& fs, bool& fp,
+                                  bool& fo) {
+    fs = frank_at(frank, boff, s) != NONE32;
+    fp = frank_at(frank, boff, (u64)V + p) != NONE32;
+    fo = frank_at(frank, boff, 2ull * V + o) != NONE32;
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_binary_emit_count(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                                 const u32* __restrict__ o, u64 n, u32 V, u32 ms,
-                                                                 const u32* __restrict__ cnt, u64* total) {
+                                                                 const u32* __restrict__ o, u64 n, u32 V,
+                                                                 const u32* __restrict__ frank, const u32* __restrict__ boff,
+                                                                 u64* total) {
     u32 c = 0;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         bool fs, fp, fo;
-        freq_flags(cnt, V, ms, s[i], p[i], o[i], fs, fp, fo);
+        freq_flags(frank, boff, V, s[i], p[i], o[i], fs, fp, fo);
         c += (fs && fp) + (fs && fo) + (fp && fo);
     }
     block_counter_add(total, c);
@@ -367,6 +262,12 @@ __device__ inline void global_hash_add(u64* tkeys, u32* tcnt, u64 mask, u64 key,
     }
 }
 
+__global__ __launch_bounds__(RDF_BLOCK) void k_spill_insert(const u64* __restrict__ keys, const u32* __restrict__ cnt, u64 n,
+                                                            u64* tkeys, u32* tcnt, u64 tmask) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        global_hash_add(tkeys, tcnt, tmask, keys[i], cnt[i]);
+}
+
 __device__ inline void lds_count_u64(u64* lkey, u32* lcnt, u64 key, u32 c, u64* tkeys, u32* tcnt, u64 tmask) {
     u32 h = (u32)mix64(key) & (LB_SLOTS - 1);
 #pragma unroll
@@ -386,9 +287,9 @@ __device__ inline void lds_count_u64(u64* lkey, u32* lcnt, u64 key, u32 c, u64* 
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_binary_count(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                            const u32* __restrict__ o, u64 n, u32 V, u32 ms,
-                                                            const u32* __restrict__ cnt, u64* tkeys, u32* tcnt,
-                                                            u64 tmask) {
+                                                            const u32* __restrict__ o, u64 n, u32 V,
+                                                            const u32* __restrict__ frank, const u32* __restrict__ boff,
+                                                            u64* tkeys, u32* tcnt, u64 tmask) {
     __shared__ u64 lkey[LB_SLOTS];
     __shared__ u32 lcnt[LB_SLOTS];
     for (int i = threadIdx.x; i < LB_SLOTS; i += RDF_BLOCK) {
@@ -408,7 +309,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_binary_count(const u32* __restric
             ts = s[i];
             tp = p[i];
             to = o[i];
-            freq_flags(cnt, V, ms, ts, tp, to, fs, fp, fo);
+            freq_flags(frank, boff, V, ts, tp, to, fs, fp, fo);
         }
         const u64 k_sp = bin_key(2, ts, tp), k_so = bin_key(1, ts, to), k_po = bin_key(0, tp, to);
         const u32 c_sp = wave_merge<u64, 2>(k_sp, fs && fp);  // o[s,p] (35)
@@ -485,7 +386,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
                                      u64 (&rec)[9]) {
     u32 c = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
-    const u32 rs = frank[ts], rp = frank[V + tp], ro = frank[2ull * V + to];  // condition ranks (or NONE)
+    const u32 rs = frank[ts], rp = frank[(u64)V + tp], ro = frank[2ull * V + to];  // global condition ranks (or NONE)
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
     if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
         if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
@@ -753,6 +654,42 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_parents_csr(const u64* __restrict
 // pivot pass, itemised: a work item is (dependent, segment of PIVOT_SEG of its groups), one wave each, so a
 // dependent in ~every group (s[p=rdf:type]) is spread over many waves.  Items of a multi-segment dependent
 // combine with atomicMin/atomicAdd; k_pivot_final derives the chunk counts.
+// per-block partial sums of three counters -> part[3 * blockIdx.x + k] (reduced by k_sum_partials: one atomic per
+// block on one address would serialise at the memory side, ~11 ns each)
+__device__ inline void block_partials3(const u64 (&acc)[3], u64* part) {
+    __shared__ u64 s_acc[3][RDF_WAVES_PER_BLOCK];
+    for (int k = 0; k < 3; ++k) {
+        u64 v = acc[k];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, RDF_WAVE);
+        if (lane_id() == 0) s_acc[k][threadIdx.x / RDF_WAVE] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        u64 t = 0;
+        for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) t += s_acc[threadIdx.x][w];
+        part[3ull * blockIdx.x + threadIdx.x] = t;
+    }
+}
+
+// out[k] = sum over blocks of part[3 * b + k] (one block)
+__global__ __launch_bounds__(RDF_BLOCK) void k_sum_partials3(const u64* __restrict__ part, u32 nblocks, u64* out) {
+    __shared__ u64 s_acc[3][RDF_WAVES_PER_BLOCK];
+    for (int k = 0; k < 3; ++k) {
+        u64 v = 0;
+        for (u32 b = threadIdx.x; b < nblocks; b += RDF_BLOCK) v += part[3ull * b + k];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, RDF_WAVE);
+        if (lane_id() == 0) s_acc[k][threadIdx.x / RDF_WAVE] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        u64 t = 0;
+        for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) t += s_acc[threadIdx.x][w];
+        out[threadIdx.x] = t;
+    }
+}
+
 static constexpr u64 PIVOT_SEG = 4096;
 
 __device__ inline u32 find_dep(const u64* chunk_off, u32 C, u64 w) {
@@ -870,9 +807,9 @@ __device__ inline void light_plan(const CindView& v, u32 d, u32 nlight, u64 sz, 
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64* __restrict__ best_in,
                                                            const u32* __restrict__ nlight_in, u32* pivot, u32* nchunk_light,
                                                            u32* nitem_light, u32* npacked, u32* nchunk_heavy, CapInfo* info,
-                                                           u64* heavy_candidates) {
-    const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
-    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
+                                                           u64* heavy_candidates /* [3 * gridDim.x] partials */) {
+    u64 acc[3] = {0, 0, 0};  // heavy candidates, light candidates, light entries
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         u32 hc = 0, lc = 0, le = 0;
         if (d < v.C) {
             const u64 best = best_in[d];
@@ -892,16 +829,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64
                 if (d >= v.Cu) hc = (u32)sz;
             }
         }
-        u64 tot = wave_inclusive_scan64(hc);
-        tot = __shfl(tot, RDF_WAVE - 1, RDF_WAVE);
-        if (lane_id() == 0 && tot) atomicAdd(heavy_candidates, tot);
-        // light-intersection work of the chunk: pivot candidates and group entries of light dependents
-        u64 tl = wave_inclusive_scan64(lc), te = wave_inclusive_scan64(le);
-        tl = __shfl(tl, RDF_WAVE - 1, RDF_WAVE);
-        te = __shfl(te, RDF_WAVE - 1, RDF_WAVE);
-        if (lane_id() == 0 && tl) atomicAdd(heavy_candidates + 1, tl);
-        if (lane_id() == 0 && te) atomicAdd(heavy_candidates + 2, te);
+        acc[0] += hc;
+        acc[1] += lc;
+        acc[2] += le;
     }
+    block_partials3(acc, heavy_candidates);
 }
 
 __device__ inline bool bsearch_u32(const u32* a, u64 n, u32 key) {
@@ -1942,9 +1874,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
                                                                  const u64* __restrict__ gbest, const u64* __restrict__ glight,
                                                                  u32 rank, u32* pivot, u32* nchunk_light, u32* nitem_light,
                                                                  u32* npacked, u32* nchunk_heavy, u32* nrl, CapInfo* info,
-                                                                 u64* heavy_candidates) {
-    const u64 n_round = ((u64)v.C + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
-    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
+                                                                 u64* heavy_candidates /* [3 * gridDim.x] partials */) {
+    u64 acc[3] = {0, 0, 0};  // heavy candidates, light candidates, light entries
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         u32 hc = 0, lc = 0, le = 0;
         if (d < v.C) {
             const u64 best = best_in[d];
@@ -1967,16 +1899,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
                 if (d >= v.Cu && holder) hc = (u32)sz;
             }
         }
-        u64 tot = wave_inclusive_scan64(hc);
-        tot = __shfl(tot, RDF_WAVE - 1, RDF_WAVE);
-        if (lane_id() == 0 && tot) atomicAdd(heavy_candidates, tot);
-        // light-intersection work of the chunk: pivot candidates and group entries of light dependents
-        u64 tl = wave_inclusive_scan64(lc), te = wave_inclusive_scan64(le);
-        tl = __shfl(tl, RDF_WAVE - 1, RDF_WAVE);
-        te = __shfl(te, RDF_WAVE - 1, RDF_WAVE);
-        if (lane_id() == 0 && tl) atomicAdd(heavy_candidates + 1, tl);
-        if (lane_id() == 0 && te) atomicAdd(heavy_candidates + 2, te);
+        acc[0] += hc;
+        acc[1] += lc;
+        acc[2] += le;
     }
+    block_partials3(acc, heavy_candidates);
 }
 
 // (dep << 32 | ref) -> (owner << 2cb | dep << cb | ref), so one radix sort groups the pairs by owner
@@ -2587,5 +2514,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_gather(const unsigned cha
         for (u64 k = 0; k < n; ++k) heap[b + k] = (char)text[a + k];
     }
 }
+
+#include "shard.inl"
 
 }  // namespace rdf

@@ -31,6 +31,26 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
     }
+    // grow to at least bytes, keeping the contents (stream-ordered copy, then the old buffer is freed)
+    hipError_t grow_keep(size_t bytes, hipStream_t st) {
+        if (bytes <= cap && p) return hipSuccess;
+        void* q = nullptr;
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&q, want);
+        if (e != hipSuccess) return e;
+        if (p && cap) {
+            e = hipMemcpyAsync(q, p, cap, hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                (void)hipFree(q);
+                return e;
+            }
+            (void)hipFree(p);
+        }
+        p = q;
+        cap = want;
+        return hipSuccess;
+    }
     template <typename T>
     T* as() const { return (T*)p; }
 };

@@ -65,6 +65,7 @@ struct rdf_ctx {
     DevBuf dheap, dtoff, cslen, csoff, cstr, flen, floff, fbuf;  // output formatting (K8)
     u64 dict_terms = 0, run_id = 0, capstr_run = ~0ull;
     DevBuf drows;           // decoded Cind-shaped rows (rdf_copy_cinds_decoded)
+    DevBuf ppart;           // per-block partial sums of the pivot statistics
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
@@ -89,7 +90,8 @@ struct rdf_ctx {
     u64 x_count = 0, x_recv_count = 0;
     u32 x_bytes = 8;
     bool x_imported = true;
-    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep, uhist, upairs, usoff;
+    DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep;
+    DevBuf uhist, urecs, usl, cntg, fstage, bfreq, boff, fbits, brkeys, brcnt;  // partitioned K1 / K2 (counts.inl)
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
@@ -152,6 +154,7 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
     } while (0)
 
 #define ENSURE(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.ensure((size_t)(bytes)))
+#define ENSURE_KEEP(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.grow_keep((size_t)(bytes), (ctx)->stream))
 
 static int bits_for(u64 maxval) {  // bits needed to represent values in [0, maxval]
     int b = 0;
@@ -241,9 +244,10 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
-                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->upairs, &c->usoff, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
+                      &c->fbits, &c->brkeys, &c->brcnt, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
-                      &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows};
+                      &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart};
 }
 
 extern "C" {
@@ -530,93 +534,259 @@ rdf_status rdf_copy_terms(rdf_ctx* c, uint64_t* offsets, uint32_t* lengths, uint
 // ------------------------------------------------------------------------------------------------
 // Stage 1: frequent conditions (FrequentConditionPlanner.constructFrequentConditionPlan)
 
-rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stats* stats) {
-    if (!c) return RDF_ERR_ARG;
-    if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
-    HIP_TRY(c, hipSetDevice(c->device));
+// K1 partitioned over (s, p, o, n): bucket histogram, scatter of the low key bits, per-bucket LDS counting.
+// counts_only: the dense counts land in cntg (sharded input: summed over ranks, then fc_ranks_from_counts);
+// otherwise ranks, fbits and the rank-block totals bfreq are written (fc_unary_finish makes them global).
+static rdf_status fc_unary_part(rdf_ctx* c, const u32* s, const u32* p, const u32* o, u64 n, int ubits, u64 NB,
+                                bool counts_only) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 K = 3ull * V;
+    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>({1024, (n + 2047) / 2048, (1ull << 25) / NB}));
+    const u64 nh = NB * G;
+    ENSURE(c, uhist, (nh + 1) * 4);
+    ENSURE(c, urecs, 3 * n * 2 + 16);
+    ENSURE(c, usl, (NB + 1) * 4);
+    const size_t lds = NB * 4;
+    hipLaunchKernelGGL((k_u2_part<false>), dim3(G), dim3(RDF_BLOCK), lds, st, s, p, o, n, V, (u32)NB, ubits,
+                       c->uhist.as<u32>(), (uint16_t*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
+    hipLaunchKernelGGL((k_u2_part<true>), dim3(G), dim3(RDF_BLOCK), lds, st, s, p, o, n, V, (u32)NB, ubits,
+                       c->uhist.as<u32>(), c->urecs.as<uint16_t>());
+    hipLaunchKernelGGL(k_u2_slices, dim3((unsigned)NB), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(), (u32)NB, G, ubits, K,
+                       c->usl.as<u32>(), c->cntg.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->usl.as<u32>(), c->usl.as<u32>(), NB, c->usl.as<u32>() + NB, st));
+    const u64 max_slices = NB + 3 * n / U2_SLICE + 1;  // >= sum over buckets of max(1, ceil(len / U2_SLICE))
+    const int co = counts_only ? 1 : 0;
+    if (ubits == 14) {
+        hipLaunchKernelGGL(k_u2_count<14>, dim3((unsigned)max_slices), dim3(U2_CBLOCK), 0, st, c->urecs.as<uint16_t>(),
+                           c->uhist.as<u32>(), c->usl.as<u32>(), (u32)NB, G, K, V, c->ms, c->frank.as<u32>(),
+                           c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0), c->cntg.as<u32>(), co);
+        if (!counts_only)
+            hipLaunchKernelGGL(k_u2_finish<14>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, st, c->usl.as<u32>(), (u32)NB, K, V,
+                               c->ms, c->cntg.as<u32>(), c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(),
+                               c->fbits.as<u64>(), dscal(c, 0));
+    } else {
+        hipLaunchKernelGGL(k_u2_count<15>, dim3((unsigned)max_slices), dim3(U2_CBLOCK), 0, st, c->urecs.as<uint16_t>(),
+                           c->uhist.as<u32>(), c->usl.as<u32>(), (u32)NB, G, K, V, c->ms, c->frank.as<u32>(),
+                           c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0), c->cntg.as<u32>(), co);
+        if (!counts_only)
+            hipLaunchKernelGGL(k_u2_finish<15>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, st, c->usl.as<u32>(), (u32)NB, K, V,
+                               c->ms, c->cntg.as<u32>(), c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(),
+                               c->fbits.as<u64>(), dscal(c, 0));
+    }
+    return RDF_OK;
+}
+
+// rank-block totals -> boff, U, the s / p / o split (frequent keys below V and 2V = boff of their rank block +
+// the part below), fval, and global ranks in frank
+static rdf_status fc_unary_finish(rdf_ctx* c, u64 nfreq[3]) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 K = 3ull * V;
+    const u64 NR = (K + FR_R - 1) / FR_R;
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->bfreq.as<u32>(), c->boff.as<u32>(), NR, c->boff.as<u32>() + NR, st));
+    u64 sc[5];
+    TRY(read_multi(c, {{c->boff.as<u32>() + NR, 4}, {c->boff.as<u32>() + (V >> FR_BITS), 4}, {dscal(c, 1), 8},
+                       {c->boff.as<u32>() + ((2ull * V) >> FR_BITS), 4}, {dscal(c, 2), 8}}, sc));
+    c->U = (u32)sc[0];
+    const u64 b1 = sc[1] + sc[2], b2 = sc[3] + sc[4];
+    nfreq[0] = b1;
+    nfreq[1] = b2 - b1;
+    nfreq[2] = sc[0] - b2;
+    ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
+    if (c->U)
+        hipLaunchKernelGGL(k_u2_fval, dim3(grid_for(c->U, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->boff.as<u32>(),
+                           (u32)NR, c->fstage.as<u32>(), V, c->fval.as<u32>(), c->frank.as<u32>());
+    HIP_TRY(c, hipMemsetAsync(c->boff.p, 0, (NR + 2) * 4, st));  // frank holds global ranks now
+    return RDF_OK;
+}
+
+static rdf_status fc_unary_alloc(rdf_ctx* c) {
+    const u32 V = c->V ? c->V : 1;
+    const u64 K = 3ull * V;
+    const u64 NR = (K + FR_R - 1) / FR_R;
+    ENSURE(c, frank, K * 4);
+    ENSURE(c, boff, (NR + 2) * 4);
+    ENSURE(c, fbits, ((K + 63) / 64 + 1) * 8);
+    ENSURE(c, cntg, K * 4);
+    ENSURE(c, fstage, K * 4);
+    ENSURE(c, bfreq, (NR + 2) * 4);
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 0), 0, 3 * 8, c->stream));
+    return RDF_OK;
+}
+
+static int fc_ubits(u64 K) { return (K + (1ull << 14) - 1) >> 14 <= U2_MAXB ? 14 : 15; }
+
+// K1 on the resident triples: frank (global ranks), fval, fbits, U; nfreq = frequent s / p / o conditions
+static rdf_status fc_unary(rdf_ctx* c, u64 nfreq[3]) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
-    c->ms = min_support ? min_support : 1;  // a support of 0 admits exactly the captures that exist
-    for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
-    HIP_TRY(c, hipEventRecord(c->ev[0], st));
-    HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
-    ENSURE(c, cnt, 3ull * V * 4);
-    HIP_TRY(c, hipMemsetAsync(c->cnt.p, 0, 3ull * V * 4, st));
-    tbegin(c, RDF_T_UNARY);
     const u64 K = 3ull * V;
-    const u64 NB = (K + UC_R - 1) / UC_R;
-    if (n && NB <= UC_MAXB && !c->force_global_counts) {
-        // partitioned counting: bucket histogram, scatter of (key, count) pairs, per-bucket LDS counting
-        const unsigned G = std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024);
-        const u64 nh = NB * G;
-        ENSURE(c, uhist, (nh + 1) * 4);
-        ENSURE(c, upairs, 3 * n * 8);
-        hipLaunchKernelGGL((k_ucount_part<false>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V, (u32)NB,
-                           c->uhist.as<u32>(), (u64*)nullptr);
-        HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
-        hipLaunchKernelGGL((k_ucount_part<true>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V, (u32)NB,
-                           c->uhist.as<u32>(), c->upairs.as<u64>());
-        ENSURE(c, usoff, (NB + 1) * 4);
-        hipLaunchKernelGGL(k_ucount_nslices, dim3(grid_for(NB, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(),
-                           (u32)NB, G, c->usoff.as<u32>());
-        HIP_TRY(c, exclusive_scan_u32(c->ws, c->usoff.as<u32>(), c->usoff.as<u32>(), NB, c->usoff.as<u32>() + NB, st));
-        const u64 max_slices = NB + 3 * n / UC_SLICE + 1;  // >= sum over buckets of max(1, ceil(len / UC_SLICE))
-        hipLaunchKernelGGL(k_ucount_bucket, dim3((unsigned)max_slices), dim3(RDF_BLOCK), 0, st, c->upairs.as<u64>(),
-                           c->uhist.as<u32>(), c->usoff.as<u32>(), (u32)NB, (u32)G, K, c->cnt.as<u32>());
-    } else if (n) {
+    const u64 NR = (K + FR_R - 1) / FR_R;
+    TRY(fc_unary_alloc(c));
+    const int ubits = fc_ubits(K);
+    const u64 NB = (K + (1ull << ubits) - 1) >> ubits;
+    if (n && NB <= U2_MAXB && !c->force_global_counts) {
+        TRY(fc_unary_part(c, c->s, c->p, c->o, n, ubits, NB, false));
+        return fc_unary_finish(c, nfreq);
+    }
+    // fallback (|V| beyond the partitioned range; RDFIND_COUNT_PATHS=atomic test hook): global-atomic counts,
+    // then global ranks by one scan (boff = 0)
+    ENSURE(c, cnt, K * 4);
+    HIP_TRY(c, hipMemsetAsync(c->cnt.p, 0, K * 4, st));
+    HIP_TRY(c, hipMemsetAsync(c->boff.p, 0, (NR + 2) * 4, st));
+    if (n)
         hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                            st, c->s, c->p, c->o, n, V, c->cnt.as<u32>());
-    }
-    ENSURE(c, frank, 3ull * V * 4);
-    ENSURE(c, flags, 3ull * V * 4);
-    hipLaunchKernelGGL(k_frank_flags, dim3(grid_for(3ull * V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(),
-                       3ull * V, c->ms, c->flags.as<u32>());
-    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->frank.as<u32>(), 3ull * V, (u32*)dscal(c, 6), st));
-    tend(c, RDF_T_UNARY);
-    if (n)  // binary keys emitted (sizes the K2 table)
-        hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p,
-                           c->o, n, V, c->ms, c->cnt.as<u32>(), dscal(c, 3));
+    ENSURE(c, flags, K * 4);
+    hipLaunchKernelGGL(k_frank_flags, dim3(grid_for(K, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(), K,
+                       c->ms, c->flags.as<u32>());
+    hipLaunchKernelGGL(k_fbits_from_counts, dim3(grid_for(K, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->cnt.as<u32>(), K, c->ms, c->fbits.as<u64>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->frank.as<u32>(), K, (u32*)dscal(c, 6), st));
     hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->cnt.as<u32>(), V, c->ms, dscal(c, 0));
-    rdf_status rs = read_scalars(c, 7);
-    if (rs) return rs;
-    const u64 E_emit = c->hscal[3];
-    u64 nfreq[3] = {c->hscal[0], c->hscal[1], c->hscal[2]};
+    TRY(read_scalars(c, 7));
+    for (int t = 0; t < 3; ++t) nfreq[t] = c->hscal[t];
     c->U = (u32)c->hscal[6];
-    c->Us = (u32)nfreq[0];
-    c->Up = (u32)nfreq[1];
     ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
-    hipLaunchKernelGGL(k_frank_final, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(), V, c->ms,
-                       c->frank.as<u32>(), c->fval.as<u32>());
-    // K2: wave-merged binary keys -> LDS hash per block -> one global open-addressing table
-    tbegin(c, RDF_T_BINARY);
-    u64 nkeys = 0, B = 0;
-    {
-        const u64 E = E_emit;
-        const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
-        ENSURE(c, tkeys, tcap * 8);
-        ENSURE(c, tcnt, tcap * 4);
-        HIP_TRY(c, hipMemsetAsync(c->tkeys.p, 0xff, tcap * 8, st));
-        HIP_TRY(c, hipMemsetAsync(c->tcnt.p, 0, tcap * 4, st));
-        if (E)
-            hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
-                               st, c->s, c->p, c->o, n, V, c->ms, c->cnt.as<u32>(), c->tkeys.as<u64>(), c->tcnt.as<u32>(),
-                               tcap - 1);
-        ENSURE(c, flags, tcap * 4);
-        ENSURE(c, pos, tcap * 8);
-        hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                           c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>(), dscal(c, 4));
-        HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
-        rs = read_scalars(c, 6);
-        if (rs) return rs;
-        nkeys = c->hscal[4];
-        B = c->hscal[5];
-        ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
-        hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                           c->tkeys.as<u64>(), c->flags.as<u32>(), c->pos.as<u64>(), tcap, c->bkeys.as<u64>());
+    hipLaunchKernelGGL(k_frank_final, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cnt.as<u32>(), V,
+                       c->ms, c->frank.as<u32>(), c->fval.as<u32>());
+    return RDF_OK;
+}
+
+// ranks from dense, globally summed counts (sharded input)
+static rdf_status fc_ranks_from_counts(rdf_ctx* c, const u32* cnt, u64 nfreq[3]) {
+    const u32 V = c->V ? c->V : 1;
+    const u64 K = 3ull * V;
+    const int ubits = fc_ubits(K);
+    const u64 NB = (K + (1ull << ubits) - 1) >> ubits;
+    if (ubits == 14)
+        hipLaunchKernelGGL(k_u2_rank_counts<14>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, c->stream, (u32)NB, K, V, c->ms, cnt,
+                           c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0));
+    else
+        hipLaunchKernelGGL(k_u2_rank_counts<15>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, c->stream, (u32)NB, K, V, c->ms, cnt,
+                           c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0));
+    return fc_unary_finish(c, nfreq);
+}
+
+// sum (key, count) pairs in one global table (2x the pairs) and append the frequent keys at bkeys + *B; the pairs
+// are either two arrays (keys, cnt) or interleaved words (cnt == nullptr).  *nkeys += distinct keys.
+static rdf_status fc_sum_pairs(rdf_ctx* c, const u64* keys, const u32* cnt, u64 m, u64* B, u64* nkeys) {
+    hipStream_t st = c->stream;
+    const u64 tcap = next_pow2(std::max<u64>(1024, 2 * m));
+    ENSURE(c, lkeys, tcap * 8);  // lkeys / lvals are rebuilt afterwards (frequent-key lookup)
+    ENSURE(c, lvals, tcap * 4);
+    HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, tcap * 8, st));
+    HIP_TRY(c, hipMemsetAsync(c->lvals.p, 0, tcap * 4, st));
+    if (m) {
+        if (cnt)
+            hipLaunchKernelGGL(k_spill_insert, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, cnt, m,
+                               c->lkeys.as<u64>(), c->lvals.as<u32>(), tcap - 1);
+        else
+            hipLaunchKernelGGL(k_pairs_insert, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, m,
+                               c->lkeys.as<u64>(), c->lvals.as<u32>(), tcap - 1);
     }
+    ENSURE(c, flags, tcap * 4);
+    ENSURE(c, fpos, tcap * 8);
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 6), 0, 16, st));
+    hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->lkeys.as<u64>(),
+                       c->lvals.as<u32>(), tcap, c->ms, c->flags.as<u32>(), dscal(c, 6));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->fpos.as<u64>(), tcap, dscal(c, 7), st));
+    TRY(read_scalars(c, 8));
+    const u64 nf = c->hscal[7];
+    ENSURE_KEEP(c, bkeys, (*B + nf + 1) * 8);
+    hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->lkeys.as<u64>(),
+                       c->flags.as<u32>(), c->fpos.as<u64>(), tcap, c->bkeys.as<u64>() + *B);
+    *nkeys += c->hscal[6];
+    *B += nf;
+    return RDF_OK;
+}
+
+// K2 partitioned over (s, p, o, n): (key, run count) records by key-hash bucket, LDS hash count per bucket slice.
+// partials = false: frequent keys -> bkeys[0, *B), distinct count -> *nkeys (multi-slice buckets summed by
+// fc_sum_pairs).  partials = true (sharded input): every local (key, count) partial -> the spill list
+// (c->tkeys keys, c->pos counts), *S entries.
+static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u32* o, u64 n, bool partials, u64* B,
+                                 u64* nkeys, u64* S) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    int bits = 1;
+    while (bits < B2_MAXBITS && (1ull << bits) * B2_TARGET < 3 * n) ++bits;
+    const u32 NB2 = 1u << bits;
+    const unsigned G2 = (unsigned)std::max<u64>(1, std::min<u64>({512, (n + 4095) / 4096, (1ull << 22) / NB2}));
+    const u64 nh = (u64)NB2 * G2;
+    const u64 maxrec = std::max<u64>(3 * n, 1);
+    ENSURE(c, uhist, (nh + 1) * 4);
+    ENSURE(c, brkeys, maxrec * 8);
+    ENSURE(c, brcnt, maxrec);
+    ENSURE(c, usl, (NB2 + 1) * 4);
+    ENSURE(c, tkeys, maxrec * 8);  // spill list: keys
+    ENSURE(c, pos, maxrec * 4);    // spill list: counts
+    const u64 bmax = maxrec / std::max<u32>(c->ms, 1) + 1;  // frequent keys: each counts >= ms of <= 3n records
+    ENSURE(c, bkeys, bmax * 8);
+    const size_t lds = (size_t)NB2 * 4;
+    hipLaunchKernelGGL((k_b2_part<false>), dim3(G2), dim3(B2_PBLOCK), lds, st, s, p, o, n, V, c->fbits.as<u64>(), bits,
+                       c->uhist.as<u32>(), (u64*)nullptr, (uint8_t*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
+    hipLaunchKernelGGL((k_b2_part<true>), dim3(G2), dim3(B2_PBLOCK), lds, st, s, p, o, n, V, c->fbits.as<u64>(), bits,
+                       c->uhist.as<u32>(), c->brkeys.as<u64>(), c->brcnt.as<uint8_t>());
+    hipLaunchKernelGGL(k_b2_slices, dim3(grid_for(NB2, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(), NB2, G2,
+                       c->usl.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->usl.as<u32>(), c->usl.as<u32>(), NB2, c->usl.as<u32>() + NB2, st));
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 3 * 8, st));
+    hipLaunchKernelGGL(k_b2_count, dim3(256 * 3), dim3(RDF_BLOCK), 0, st, c->brkeys.as<u64>(), c->brcnt.as<uint8_t>(),
+                       c->uhist.as<u32>(), c->usl.as<u32>(), NB2, G2, c->ms, c->bkeys.as<u64>(), c->tkeys.as<u64>(),
+                       (u32*)c->pos.p, dscal(c, 3), partials ? 1 : 0);
+    TRY(read_scalars(c, 6));
+    *B = c->hscal[3];
+    *nkeys = c->hscal[4];
+    *S = c->hscal[5];
+    if (!partials && *S) TRY(fc_sum_pairs(c, c->tkeys.as<u64>(), (const u32*)c->pos.p, *S, B, nkeys));
+    return RDF_OK;
+}
+
+// K2 fallback: one global open-addressing table sized from the emitted keys
+static rdf_status fc_binary_global(rdf_ctx* c, u64* B, u64* nkeys) {
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const u32 V = c->V ? c->V : 1;
+    const u32* boff = c->boff.as<u32>();
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 8, st));
+    hipLaunchKernelGGL(k_binary_emit_count, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o,
+                       n, V, c->frank.as<u32>(), boff, dscal(c, 3));
+    TRY(read_scalars(c, 4));
+    const u64 E = c->hscal[3];
+    const u64 tcap = next_pow2(std::max<u64>(1024, E + E / 2 + 1));
+    ENSURE(c, tkeys, tcap * 8);
+    ENSURE(c, tcnt, tcap * 4);
+    HIP_TRY(c, hipMemsetAsync(c->tkeys.p, 0xff, tcap * 8, st));
+    HIP_TRY(c, hipMemsetAsync(c->tcnt.p, 0, tcap * 4, st));
+    if (E)
+        hipLaunchKernelGGL(k_binary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0, st,
+                           c->s, c->p, c->o, n, V, c->frank.as<u32>(), boff, c->tkeys.as<u64>(), c->tcnt.as<u32>(), tcap - 1);
+    ENSURE(c, flags, tcap * 4);
+    ENSURE(c, pos, tcap * 8);
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 4), 0, 16, st));
+    hipLaunchKernelGGL(k_bin_freq_flags, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->tkeys.as<u64>(),
+                       c->tcnt.as<u32>(), tcap, c->ms, c->flags.as<u32>(), dscal(c, 4));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), tcap, dscal(c, 5), st));
+    TRY(read_scalars(c, 6));
+    *nkeys = c->hscal[4];
+    *B = c->hscal[5];
+    ENSURE(c, bkeys, std::max<u64>(*B, 1) * 8);
+    hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->tkeys.as<u64>(),
+                       c->flags.as<u32>(), c->pos.as<u64>(), tcap, c->bkeys.as<u64>());
+    return RDF_OK;
+}
+
+// frequent binary keys bkeys[0, B) -> sorted (deterministic binary ids) + the key -> id lookup table
+static rdf_status fc_binary_index(rdf_ctx* c, u64 B) {
+    hipStream_t st = c->stream;
     c->B = B;
+    ENSURE_KEEP(c, bkeys, std::max<u64>(B, 1) * 8);
     ENSURE(c, bkeys_tmp, std::max<u64>(B, 1) * 8);
     {
         u64* k = c->bkeys.as<u64>();
@@ -624,7 +794,6 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
         HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, 64, st));
         if (k != c->bkeys.as<u64>()) std::swap(c->bkeys, c->bkeys_tmp);
     }
-    tend(c, RDF_T_BINARY);
     c->lcap = next_pow2(2 * B + 16);
     ENSURE(c, lkeys, c->lcap * 8);
     ENSURE(c, lvals, c->lcap * 4);
@@ -633,17 +802,54 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
         hipLaunchKernelGGL(k_bin_lookup_build, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->bkeys.as<u64>(), B, c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1);
     c->h_bkeys_valid = false;  // host copy made on first use (decode / copy-out)
-    HIP_TRY(c, hipEventRecord(c->ev[1], st));
-    HIP_TRY(c, hipStreamSynchronize(st));
-    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
-    tcollect(c, RDF_T_UNARY, RDF_T_BINARY + 1);
+    return RDF_OK;
+}
+
+static void fc_stats(rdf_ctx* c, const u64 nfreq[3], u64 nkeys, u64 B) {
+    c->Us = (u32)nfreq[0];
+    c->Up = (u32)nfreq[1];
     memset(&c->fstats, 0, sizeof(c->fstats));
     c->fstats.min_support = c->ms;
     for (int i = 0; i < 3; ++i) c->fstats.n_frequent_unary[i] = nfreq[i];
     c->fstats.n_binary_keys = nkeys;
     c->fstats.n_frequent_binary = B;
-    if (stats) *stats = c->fstats;
+}
+
+static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
+    c->ms = min_support ? min_support : 1;  // a support of 0 admits exactly the captures that exist
+    for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
+    HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), c->stream));
+    return RDF_OK;
+}
+
+static rdf_status fc_end(rdf_ctx* c) {
+    HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
+    tcollect(c, RDF_T_UNARY, RDF_T_BINARY + 1);
     c->stage = 2;
+    return RDF_OK;
+}
+
+rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    TRY(fc_begin(c, min_support));
+    u64 nfreq[3] = {0, 0, 0};
+    tbegin(c, RDF_T_UNARY);
+    TRY(fc_unary(c, nfreq));
+    tend(c, RDF_T_UNARY);
+    tbegin(c, RDF_T_BINARY);
+    u64 B = 0, nkeys = 0, S = 0;
+    if (c->n && !c->force_global_counts) TRY(fc_binary_part(c, c->s, c->p, c->o, c->n, false, &B, &nkeys, &S));
+    else if (c->n) TRY(fc_binary_global(c, &B, &nkeys));
+    TRY(fc_binary_index(c, B));
+    tend(c, RDF_T_BINARY);
+    TRY(fc_end(c));
+    fc_stats(c, nfreq, nkeys, B);
+    if (stats) *stats = c->fstats;
     return RDF_OK;
 }
 
@@ -1384,10 +1590,14 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     CindView v = make_view(c, flags);
     TRY(d_pivot_local(c, v));
     tbegin(c, RDF_T_PIVOT);
-    if (c->C)
-        hipLaunchKernelGGL(k_pivot_final, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
+    if (c->C) {
+        const unsigned gp = grid_for(c->C, RDF_BLOCK, kGrid);
+        ENSURE(c, ppart, 3ull * gp * 8);
+        hipLaunchKernelGGL(k_pivot_final, dim3(gp), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
                            c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>(),
-                           c->nchh.as<u32>(), c->info.as<CapInfo>(), dscal(c, 2));
+                           c->nchh.as<u32>(), c->info.as<CapInfo>(), c->ppart.as<u64>());
+        hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gp, dscal(c, 2));
+    }
     tend(c, RDF_T_PIVOT);
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0, H = 0, HC = 0, NT = 0;
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
@@ -1508,12 +1718,16 @@ static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
     CindView v = make_view(c, c->sh_flags);
     ENSURE(c, nrl, std::max<u64>(C, 1) * 4);
     tbegin(c, RDF_T_PIVOT);
-    if (C)
-        hipLaunchKernelGGL(k_pivot_final_shard, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+    if (C) {
+        const unsigned gp = grid_for(C, RDF_BLOCK, kGrid);
+        ENSURE(c, ppart, 3ull * gp * 8);
+        hipLaunchKernelGGL(k_pivot_final_shard, dim3(gp), dim3(RDF_BLOCK), 0, st, v,
                            c->pbest.as<u64>(), c->pnl.as<u32>(), c->gbest.as<u64>(), c->xrecv.as<u64>(), c->rank,
                            c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>(), c->nchh.as<u32>(),
                            c->nrl.as<u32>(),
-                           c->info.as<CapInfo>(), dscal(c, 2));
+                           c->info.as<CapInfo>(), c->ppart.as<u64>());
+        hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gp, dscal(c, 2));
+    }
     tend(c, RDF_T_PIVOT);
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0;
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
