@@ -8,12 +8,15 @@ dictionary-encoded triples already resident in HBM and the CIND id-records left 
 PCIe-inclusive rate is reported separately in DESIGN.md).  Workload: BASELINE configs[1] =
 LUBM-100-shaped synthetic triples (~13.4M), support 10, one MI355X.
 
-For N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL over xGMI) the SAME workload is
-sharded (rdfind_amd/distributed.py): every rank holds the triples, owns the capture groups
-of its join-value hash shard and the dependents d % N, and the eight collectives of the protocol run
-inside the timed region.  `value` is the workload's triples divided by the max-over-ranks time per
-step (strong scaling).  `roofline` is computed for the dominant kernel family from HIP events recorded on
-the library's stream; `cpu_baseline` times the C restatement (oracle/, OpenMP) on a bounded sample on rank 0.
+For N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL over xGMI) the workload is sharded
+(rdfind_amd/distributed.py): each rank holds only its slice of the triples
+(synth.config_slice), the condition counts are summed over ranks, every triple travels to the ranks owning
+its join values, each rank builds the capture groups of its join-value hash shard and owns the dependents
+d % N; the twelve collectives of the protocol run inside the timed region.  `value` is the workload's
+triples divided by the max-over-ranks time per step (the default c2 workload is split over the ranks:
+strong scaling; `--config c4` draws 1B/N rows per rank).  `roofline` is computed for the dominant kernel
+family from HIP events recorded on the library's stream; `cpu_baseline` times the C restatement (oracle/,
+OpenMP) on rank 0.
 """
 from __future__ import annotations
 
@@ -161,7 +164,11 @@ def main():
 
     from rdfind_amd import _lib, synth
 
-    d = synth.config(args.config, args.scale)  # same seeded workload on every rank
+    if dist is not None:  # each rank holds only its slice of the input (sharded input)
+        d, total_n = synth.config_slice(args.config, args.scale, rank, world)
+    else:
+        d = synth.config(args.config, args.scale)
+        total_n = d.n
     ms = d.min_support
     ctx = _lib.Context(local_rank)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
@@ -170,7 +177,7 @@ def main():
         from rdfind_amd import distributed
 
         def step():
-            distributed.run_sharded(ctx, ms)
+            distributed.run_sharded(ctx, ms, local_slice=True)
             return ctx.cinds
     else:
         def step():
@@ -206,7 +213,7 @@ def main():
         total_cinds = int(tot.item())
     else:
         total_cinds = cs["n_cinds"]
-    total_triples = float(d.n)
+    total_triples = float(total_n)
     steps = max(args.steps, 1)
     ms_per_step = elapsed * 1000.0 / steps
     value = total_triples * steps / elapsed
@@ -293,8 +300,8 @@ def main():
             "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": f"{args.config} ({'LUBM-100-shaped' if args.config == 'c2' else args.config}, "
                                    f"scale {args.scale}, support {ms}, strategy 1 --use-fis --clean-implied)",
-                       "triples": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
-                       "parallelism": f"join-hash shards x{world} (RCCL)" if world > 1 else "single"},
+                       "triples": total_n, "triples_rank0": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
+                       "parallelism": f"input slices + join-hash shards x{world} (RCCL)" if world > 1 else "single"},
             "roofline": roof, "count_kernels": count_roof, "families": fams, "t_disc_host": tdisc,
             "cpu_baseline": cpu, "ingest": ingest,
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},

@@ -215,8 +215,12 @@ rdf_status rdf_last_stats(rdf_ctx* ctx, rdf_fc_stats* fc, rdf_group_stats* gs, r
 
 /*
  * Sharded multi-GPU mode (the reference's --dop parallelism over Flink task slots).
- * Every rank holds all triples; rank r owns the capture groups of the join values with
- * hash(join) % nranks == r, and the dependents d with d % nranks == r.  The library stops at every
+ * With RDF_SHARD_LOCAL_SLICE the resident triples are this rank's slice of the input (any partition of the
+ * triples over the ranks, one dictionary); without it every rank holds all triples and takes rows
+ * [n * rank / nranks, n * (rank + 1) / nranks).  Condition counts are summed over ranks (unary: all-reduce of
+ * dense counts; binary: (key, count) partials all-to-all'd to the key's owner, frequent keys all-gathered), then
+ * each triple travels to the ranks owning its join values (hash(join) % nranks), so rank r builds the capture
+ * groups of its join values and owns the dependents d with d % nranks == r.  The library stops at every
  * collective and describes it in an rdf_exchange; the caller performs it (torch.distributed over RCCL,
  * see rdfind_amd/distributed.py) and hands the result back:
  *
@@ -235,6 +239,7 @@ rdf_status rdf_last_stats(rdf_ctx* ctx, rdf_fc_stats* fc, rdf_group_stats* gs, r
  * (ALG/plan/AllAtOnceTraversalStrategy.scala:62-65 combine, ALG/plan/TraversalStrategy.scala:126-168).
  */
 #define RDF_MAX_RANKS 64
+#define RDF_SHARD_LOCAL_SLICE 4u   /* rdf_shard_begin flags: the resident triples are this rank's input slice */
 enum {
     RDF_X_DONE = 0,
     RDF_X_ALLREDUCE_SUM_U32 = 1,   /* element-wise sum, uint32 */

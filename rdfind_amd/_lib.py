@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("RDFIND_HIP_LIB") or os.path.join(_HERE, "librdfind_hi
 
 RDF_CLEAN_IMPLIED = 1
 RDF_STRATEGY_ALL_AT_ONCE = 2
+RDF_SHARD_LOCAL_SLICE = 4
 
 # every symbol declared in include/rdfind_hip.h
 EXPORTED_SYMBOLS = (
@@ -305,8 +306,11 @@ class Context:
 
     # -- sharded mode (driven by rdfind_amd.distributed.run_sharded) ---------------------------
     def shard_begin(self, rank: int, nranks: int, min_support: int, projection="spo", clean_implied=True,
-                    traversal_strategy=1):
+                    traversal_strategy=1, local_slice=False):
+        """local_slice: the resident triples are this rank's slice of the input (else every rank holds all of
+        them and the library takes its row range)."""
         flags = (RDF_CLEAN_IMPLIED if clean_implied else 0) | (RDF_STRATEGY_ALL_AT_ONCE if traversal_strategy == 0 else 0)
+        flags |= RDF_SHARD_LOCAL_SLICE if local_slice else 0
         self._nranks = nranks
         self._check(self.lib.rdf_shard_begin(self.ptr, rank, nranks, min_support, projection.encode(), flags),
                     "rdf_shard_begin")

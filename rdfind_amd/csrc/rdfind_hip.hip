@@ -82,6 +82,8 @@ struct rdf_ctx {
     // sharded mode: this rank's share of the join values, and the pending exchange
     u32 rank = 0, nranks = 1;
     u32 sh_rank = 0, sh_nranks = 1, sh_ms = 1, sh_flags = 0;
+    u64 sh_nfreq[3] = {0, 0, 0}, sh_nkeys = 0;
+    DevBuf wts, wtp, wto;  // sharded input: the triples received for this rank's join shard
     int sh_proj = 7, sh_phase = -1;
     u64 sh_WH = 0, sh_H = 0, sh_E = 0, sh_tcapc = 0;
     u32 h_hist_local[256] = {};
@@ -247,7 +249,8 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
                       &c->fbits, &c->brkeys, &c->brcnt, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
-                      &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart};
+                      &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
+            &c->wto};
 }
 
 extern "C" {
@@ -659,10 +662,30 @@ static rdf_status fc_unary(rdf_ctx* c, u64 nfreq[3]) {
 
 // ranks from dense, globally summed counts (sharded input)
 static rdf_status fc_ranks_from_counts(rdf_ctx* c, const u32* cnt, u64 nfreq[3]) {
+    hipStream_t st = c->stream;
     const u32 V = c->V ? c->V : 1;
     const u64 K = 3ull * V;
     const int ubits = fc_ubits(K);
     const u64 NB = (K + (1ull << ubits) - 1) >> ubits;
+    if (NB > U2_MAXB) {  // |V| beyond the bucketed range: flags + one scan over the counts (boff = 0)
+        const u64 NR = (K + FR_R - 1) / FR_R;
+        HIP_TRY(c, hipMemsetAsync(c->boff.p, 0, (NR + 2) * 4, st));
+        ENSURE(c, flags, K * 4);
+        hipLaunchKernelGGL(k_frank_flags, dim3(grid_for(K, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, K, c->ms,
+                           c->flags.as<u32>());
+        hipLaunchKernelGGL(k_fbits_from_counts, dim3(grid_for(K, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, K, c->ms,
+                           c->fbits.as<u64>());
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->frank.as<u32>(), K, (u32*)dscal(c, 6), st));
+        hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, V, c->ms,
+                           dscal(c, 0));
+        TRY(read_scalars(c, 7));
+        for (int t = 0; t < 3; ++t) nfreq[t] = c->hscal[t];
+        c->U = (u32)c->hscal[6];
+        ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
+        hipLaunchKernelGGL(k_frank_final, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, V, c->ms,
+                           c->frank.as<u32>(), c->fval.as<u32>());
+        return RDF_OK;
+    }
     if (ubits == 14)
         hipLaunchKernelGGL(k_u2_rank_counts<14>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, c->stream, (u32)NB, K, V, c->ms, cnt,
                            c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0));
@@ -1642,12 +1665,151 @@ static rdf_status x_request(rdf_ctx* c, rdf_exchange* req, int op, const void* s
     return RDF_OK;
 }
 
-static rdf_status sh_phase0(rdf_ctx* c, rdf_exchange* req) {
-    TRY(rdf_frequent_conditions(c, c->sh_ms, nullptr));
+// ---- sharded input: condition counts as partial sums, then triples routed to their join owners ----
+
+// this rank's input slice: the resident triples (RDF_SHARD_LOCAL_SLICE), or its row range of replicated triples
+static void sh_slice(rdf_ctx* c, const u32** s, const u32** p, const u32** o, u64* n) {
+    u64 b = 0, e = c->n;
+    if (!(c->sh_flags & RDF_SHARD_LOCAL_SLICE)) {
+        b = c->n * c->sh_rank / c->sh_nranks;
+        e = c->n * (c->sh_rank + 1) / c->sh_nranks;
+    }
+    *s = c->s + b;
+    *p = c->p + b;
+    *o = c->o + b;
+    *n = e - b;
+}
+
+// local dense unary counts -> all-reduce(sum)
+static rdf_status sh_phase10(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    TRY(fc_begin(c, c->sh_ms));
+    TRY(fc_unary_alloc(c));
+    const u32 V = c->V ? c->V : 1;
+    const u64 K = 3ull * V;
+    const u32 *s, *p, *o;
+    u64 n;
+    sh_slice(c, &s, &p, &o, &n);
+    const int ubits = fc_ubits(K);
+    const u64 NB = (K + (1ull << ubits) - 1) >> ubits;
+    tbegin(c, RDF_T_UNARY);
+    if (n && NB <= U2_MAXB && !c->force_global_counts) {
+        TRY(fc_unary_part(c, s, p, o, n, ubits, NB, true));
+    } else {
+        HIP_TRY(c, hipMemsetAsync(c->cntg.p, 0, K * 4, st));
+        if (n)
+            hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
+                               st, s, p, o, n, V, c->cntg.as<u32>());
+    }
+    tend(c, RDF_T_UNARY);
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U32, c->cntg.p, K, 11);
+}
+
+// global counts -> ranks; local binary (key, count) partials -> all-to-all to the keys' owners
+static rdf_status sh_phase11(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    tbegin(c, RDF_T_UNARY);
+    TRY(fc_ranks_from_counts(c, c->xrecv.as<u32>(), c->sh_nfreq));
+    tend(c, RDF_T_UNARY);
+    const u32 *s, *p, *o;
+    u64 n;
+    sh_slice(c, &s, &p, &o, &n);
+    tbegin(c, RDF_T_BINARY);
+    u64 B = 0, nkeys = 0, S = 0;
+    if (n) TRY(fc_binary_part(c, s, p, o, n, true, &B, &nkeys, &S));
+    const u32 R = c->sh_nranks;
+    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>(1024, (S + 4095) / 4096));
+    ENSURE(c, uhist, ((u64)R * G + 1) * 4);
+    ENSURE(c, xsend, std::max<u64>(2 * S, 1) * 8);
+    hipLaunchKernelGGL((k_route_pairs<false>), dim3(G), dim3(RDF_BLOCK), 0, st, c->tkeys.as<u64>(), (const u32*)c->pos.p, S,
+                       R, c->uhist.as<u32>(), (u64*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), (u64)R * G, c->uhist.as<u32>() + (u64)R * G, st));
+    hipLaunchKernelGGL((k_route_pairs<true>), dim3(G), dim3(RDF_BLOCK), 0, st, c->tkeys.as<u64>(), (const u32*)c->pos.p, S,
+                       R, c->uhist.as<u32>(), c->xsend.as<u64>());
+    tend(c, RDF_T_BINARY);
+    std::vector<u32> h((u64)R * G + 1);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->uhist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->xsend.p, 2 * S, 12));
+    for (u32 r = 0; r < R; ++r) req->send_counts[r] = 2ull * (h[(u64)(r + 1) * G] - h[(u64)r * G]);
+    return RDF_OK;
+}
+
+// received partials of this rank's keys -> summed -> frequent keys -> all-gather
+static rdf_status sh_phase12(rdf_ctx* c, rdf_exchange* req) {
+    tbegin(c, RDF_T_BINARY);
+    u64 B = 0, nkeys = 0;
+    ENSURE(c, bkeys, 8);
+    TRY(fc_sum_pairs(c, c->xrecv.as<u64>(), nullptr, c->x_recv_count / 2, &B, &nkeys));
+    tend(c, RDF_T_BINARY);
+    c->sh_nkeys = nkeys;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->bkeys.p, B, 13);
+}
+
+// every rank's frequent keys -> sorted binary ids; the local triples -> the ranks owning their join values
+static rdf_status sh_phase13(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 B = c->x_recv_count;
+    tbegin(c, RDF_T_BINARY);
+    ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
+    if (B) HIP_TRY(c, hipMemcpyAsync(c->bkeys.p, c->xrecv.p, B * 8, hipMemcpyDeviceToDevice, st));
+    TRY(fc_binary_index(c, B));
+    tend(c, RDF_T_BINARY);
+    TRY(fc_end(c));
+    fc_stats(c, c->sh_nfreq, c->sh_nkeys, B);  // n_binary_keys: the distinct keys owned by this rank
+    const u32 *s, *p, *o;
+    u64 n;
+    sh_slice(c, &s, &p, &o, &n);
+    const u32 R = c->sh_nranks;
+    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>(1024, (n + 4095) / 4096));
+    ENSURE(c, uhist, ((u64)R * G + 1) * 4);
+    ENSURE(c, xsend, std::max<u64>(6 * n, 1) * 8);  // <= 3 copies of 2 words
+    tbegin(c, RDF_T_EMIT);
+    hipLaunchKernelGGL((k_route_triples<false>), dim3(G), dim3(RDF_BLOCK), 0, st, s, p, o, n, c->sh_proj, R,
+                       c->uhist.as<u32>(), (u64*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), (u64)R * G, c->uhist.as<u32>() + (u64)R * G, st));
+    hipLaunchKernelGGL((k_route_triples<true>), dim3(G), dim3(RDF_BLOCK), 0, st, s, p, o, n, c->sh_proj, R,
+                       c->uhist.as<u32>(), c->xsend.as<u64>());
+    tend(c, RDF_T_EMIT);
+    std::vector<u32> h((u64)R * G + 1);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->uhist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    const u64 copies = h[(u64)R * G];
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->xsend.p, 2 * copies, 14));
+    for (u32 r = 0; r < R; ++r) req->send_counts[r] = 2ull * (h[(u64)(r + 1) * G] - h[(u64)r * G]);
+    return RDF_OK;
+}
+
+// received triples (every triple with a join value owned here) -> join partners of this rank's shard, sort,
+// local supports -> all-reduce(sum) (then phases 1-8)
+static rdf_status sh_phase14(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 m = c->x_recv_count / 2;
+    ENSURE(c, wts, std::max<u64>(m, 1) * 4);
+    ENSURE(c, wtp, std::max<u64>(m, 1) * 4);
+    ENSURE(c, wto, std::max<u64>(m, 1) * 4);
+    if (m)
+        hipLaunchKernelGGL(k_unpack_triples, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->xrecv.as<u64>(), m,
+                           c->wts.as<u32>(), c->wtp.as<u32>(), c->wto.as<u32>());
+    if (m >= (1ull << 32) / 9) return fail(c, RDF_ERR_LIMIT, "join shard holds >= 2^32/9 triples (use more ranks)");
+    // K3 reads the received triples; the resident input stays this rank's slice for the next run
+    const u32 *s0 = c->s, *p0 = c->p, *o0 = c->o;
+    const u64 n0 = c->n;
+    c->s = c->wts.as<u32>();
+    c->p = c->wtp.as<u32>();
+    c->o = c->wto.as<u32>();
+    c->n = m;
     c->rank = c->sh_rank;
     c->nranks = c->sh_nranks;
-    TRY(g_emit_sort_support(c, c->sh_proj));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const rdf_status r = g_emit_sort_support(c, c->sh_proj);
+    c->s = s0;
+    c->p = p0;
+    c->o = o0;
+    c->n = n0;
+    TRY(r);
+    HIP_TRY(c, hipStreamSynchronize(st));
     return x_request(c, req, RDF_X_ALLREDUCE_SUM_U32, c->support.p, c->ncap, 1);
 }
 
@@ -1919,6 +2081,13 @@ static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
     return RDF_OK;
 }
 
+// phases: 10-14 (condition counts, routing of the triples), then 1-8; pending = a phase that follows a collective
+static bool sh_phase_valid(int ph, bool pending) {
+    if (ph >= 1 && ph <= 8) return true;
+    if (ph >= 11 && ph <= 14) return true;
+    return !pending && ph == 10;
+}
+
 rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t min_support, const char* projection,
                            uint32_t flags) {
     if (!c) return RDF_ERR_ARG;
@@ -1932,7 +2101,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     c->sh_ms = min_support;
     c->sh_proj = proj;
     c->sh_flags = flags;
-    c->sh_phase = 0;
+    c->sh_phase = 10;
     c->x_imported = true;
     c->stage = std::min(c->stage, 1);
     return RDF_OK;
@@ -1940,12 +2109,11 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
 
 rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
     if (!c || !req) return RDF_ERR_ARG;
-    if (c->sh_phase < 0 || c->sh_phase > 8) return fail(c, RDF_ERR_STATE, "rdf_shard_begin must be called first");
+    if (!sh_phase_valid(c->sh_phase, false)) return fail(c, RDF_ERR_STATE, "rdf_shard_begin must be called first");
     if (!c->x_imported) return fail(c, RDF_ERR_STATE, "rdf_shard_import must supply the pending exchange first");
     HIP_TRY(c, hipSetDevice(c->device));
     rdf_status r = RDF_OK;
     switch (c->sh_phase) {
-        case 0: r = sh_phase0(c, req); break;
         case 1: r = sh_phase1(c, req); break;
         case 2: r = sh_phase2(c, req); break;
         case 3: r = sh_phase3(c, req); break;
@@ -1954,6 +2122,11 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
         case 6: r = sh_phase6(c, req); break;
         case 7: r = sh_phase7(c, req); break;
         case 8: r = sh_phase8(c, req); break;
+        case 10: r = sh_phase10(c, req); break;
+        case 11: r = sh_phase11(c, req); break;
+        case 12: r = sh_phase12(c, req); break;
+        case 13: r = sh_phase13(c, req); break;
+        case 14: r = sh_phase14(c, req); break;
     }
     if (r != RDF_OK) c->sh_phase = -1;  // a failed machine must be restarted with rdf_shard_begin
     return r;
@@ -1961,7 +2134,7 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
 
 rdf_status rdf_shard_export(rdf_ctx* c, void* dst) {
     if (!c) return RDF_ERR_ARG;
-    if (c->x_imported || c->sh_phase < 1 || c->sh_phase > 8) return fail(c, RDF_ERR_STATE, "no pending exchange");
+    if (c->x_imported || !sh_phase_valid(c->sh_phase, true)) return fail(c, RDF_ERR_STATE, "no pending exchange");
     if (c->x_count && !dst) return fail(c, RDF_ERR_ARG, "null exchange buffer");
     HIP_TRY(c, hipSetDevice(c->device));
     if (c->x_count)
@@ -1972,7 +2145,7 @@ rdf_status rdf_shard_export(rdf_ctx* c, void* dst) {
 
 rdf_status rdf_shard_import(rdf_ctx* c, const void* src, uint64_t count) {
     if (!c) return RDF_ERR_ARG;
-    if (c->x_imported || c->sh_phase < 1 || c->sh_phase > 8) return fail(c, RDF_ERR_STATE, "no pending exchange");
+    if (c->x_imported || !sh_phase_valid(c->sh_phase, true)) return fail(c, RDF_ERR_STATE, "no pending exchange");
     if (count && !src) return fail(c, RDF_ERR_ARG, "null exchange buffer");
     const bool reduce = c->x_op == RDF_X_ALLREDUCE_SUM_U32 || c->x_op == RDF_X_ALLREDUCE_SUM_U64 ||
                         c->x_op == RDF_X_ALLREDUCE_MIN_U64;

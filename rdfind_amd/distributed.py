@@ -1,9 +1,13 @@
 """Sharded multi-GPU CIND discovery: one process per GPU, torch.distributed over RCCL.
 
-Every rank holds all triples.  Rank r builds only the capture groups of the join values it owns
-(``hash(join) % R == r``), so join partners never cross the fabric.  The global quantities are
-combined by collectives that the library requests one at a time (``rdf_shard_step``):
+Each rank holds a slice of the triples (or all of them, and the library takes its row range).  The collectives
+the library requests one at a time (``rdf_shard_step``):
 
+  a. all-reduce(sum)  dense unary condition counts of the slices (FrequentConditionPlanner.scala:293-309)
+  b. all-to-all       binary (key, count) partials to the key's owner rank, which sums them (:381-393)
+  c. all-gather       the frequent binary keys of every owner (sorted afterwards: deterministic ids)
+  d. all-to-all       every triple to the ranks owning its join values (RDFind.scala:339-345 groupBy(joinValue)),
+                      so rank r builds the capture groups of its join-value hash shard
   1. all-reduce(sum)  capture supports (distinct join values per capture)
   2. all-gather       group-size histograms -> global heavy threshold + this rank's heavy bit base
   3. all-reduce(sum)  heavy-group bitmasks (bits of different ranks are disjoint, so sum == or)
@@ -36,20 +40,24 @@ def _dtype(op):
 
 
 def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
-    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order."""
+    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order (one broadcast per rank
+    into its exact slice of the result: no padding to the largest contribution)."""
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n, group=group)
     counts = [int(c.item()) for c in counts]
-    m = max(counts) if counts else 0
-    if m == 0:
-        return send.new_empty(0)
-    padded = send.new_zeros(m)
-    padded[: send.numel()] = send
-    parts = [send.new_empty(m) for _ in range(world)]
-    dist.all_gather(parts, padded, group=group)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+    out = send.new_empty(sum(counts))
+    off = 0
+    for r, c in enumerate(counts):
+        if c:
+            part = out[off: off + c]
+            if r == rank:
+                part.copy_(send)
+            dist.broadcast(part, src=dist.get_global_rank(group, r) if group is not None else r, group=group)
+        off += c
+    return out
 
 
 def alltoallv(send: torch.Tensor, send_counts, group=None) -> torch.Tensor:
@@ -110,10 +118,11 @@ def run_protocol(machine, group=None, device=None):
 
 
 def run_sharded(ctx, min_support: int, projection="spo", clean_implied=True, traversal_strategy=1, group=None,
-                device=None):
-    """Sharded CIND discovery on this rank's context; returns (group_stats, cind_stats) of this rank."""
+                device=None, local_slice=False):
+    """Sharded CIND discovery on this rank's context; returns (group_stats, cind_stats) of this rank.
+    local_slice: the context's resident triples are this rank's slice of the input."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy)
+    ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy, local_slice)
     run_protocol(ctx, group, device)
     return ctx.last_stats()

@@ -360,6 +360,25 @@ def lubm(n_universities: int = 100, seed: int = 0, min_support: int = 10, max_de
 # ---------------------------------------------------------------------------
 # BASELINE configs
 
+def config_slice(name: str, scale: float, rank: int, nranks: int) -> tuple:
+    """This rank's slice of a BASELINE config for the sharded (multi-GPU) bench: (Dataset of the slice, total
+    triples).  c4 beyond scale 0.05 (1B triples at full size: no deduplication, i.i.d. rows) draws only its
+    own rows from a rank-specific seed, so no rank ever holds the whole input; the union of the slices is then
+    a function of nranks (same distribution and vocabulary).  Every other config is generated whole
+    (deterministically on every rank) and cut into contiguous row ranges."""
+    if name == "c4" and scale > 0.05:
+        n = int(1_000_000_000 * scale)
+        lo, hi = n * rank // nranks, n * (rank + 1) // nranks
+        seed = int(np.random.SeedSequence([4, rank, nranks]).generate_state(1)[0])
+        d = zipf_rdf("c4", hi - lo, max(int(100_000_000 * scale), 100), max(int(20_000 * scale), 20), 1.2, 1.0,
+                     0.10, 2000, 1.2, 0.35, max(int(150_000_000 * scale), 100), 1.0, 1.0, 100, seed, dedup=False)
+        return d, n
+    d = config(name, scale)
+    n = d.n
+    lo, hi = n * rank // nranks, n * (rank + 1) // nranks
+    return Dataset(d.name, d.s[lo:hi].copy(), d.p[lo:hi].copy(), d.o[lo:hi].copy(), d.terms, d.min_support), n
+
+
 def config(name: str, scale: float = 1.0, seed: int | None = None) -> Dataset:
     """c1..c5 of BASELINE.json; ``scale`` shrinks N (and the vocabularies) for tests."""
     if name == "c1":

@@ -1,13 +1,15 @@
 """CPU model of the sharded protocol (test infrastructure, built on the oracle).
 
 ``ShardSim`` answers the same ``shard_begin / shard_step / shard_export / shard_import`` calls as the HIP
-``Context`` in sharded mode, with the same sequence of collectives (rdfind_amd/distributed.py), but
-computes each rank's part with the Python oracle: join lines of the join values this rank owns, local
-intersections of the light dependents, owner-side multiplicity check, then minimality on the gathered
+``Context`` in sharded mode, with the same sequence of collectives and message layouts
+(rdfind_amd/distributed.py, rdfind_hip.hip sh_phase10-14 and 1-8), but computes each rank's part with the
+Python oracle: dense unary counts of the rank's slice (all-reduce), binary (key, count) partials routed to
+the key's owner (all-to-all, same key hash as shard.inl key_owner), the frequent keys all-gathered, every
+triple routed to the owners of its join values (all-to-all, two words per copy), join lines of the join
+values this rank owns, local intersections, owner-side multiplicity check, then minimality on the gathered
 explicit set.  It treats every group as light (no bitmask columns), so the class exchange is empty.
-It lets the CPU suite run the real collectives (gloo, world size 2) and check that the decomposition
--- shard by join hash, intersect locally, route by dependent, count reporters -- reproduces the
-single-process oracle result.
+It lets the CPU suite run the real collectives (gloo, world size 2 and 3) and check that the decomposition
+reproduces the single-process oracle result.
 """
 from __future__ import annotations
 
@@ -26,20 +28,59 @@ def shard_of(join: int, nranks: int) -> int:
     return (((join * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF) >> 32) % nranks
 
 
+M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def mix64(x: int) -> int:
+    """common.hpp mix64 (murmur3 finaliser)."""
+    x ^= x >> 33
+    x = (x * 0xFF51AFD7ED558CCD) & M64
+    x ^= x >> 33
+    x = (x * 0xC4CEB9FE1A85EC53) & M64
+    x ^= x >> 33
+    return x
+
+
+def key_owner(key: int, nranks: int) -> int:
+    """shard.inl key_owner: the rank that sums a binary condition's partial counts."""
+    return (mix64(key) & 0xFFFFFFFF) % nranks
+
+
+# binary condition type (S|P, S|O, P|O) <-> the library's key type bt (o[s,p] 2, p[s,o] 1, s[p,o] 0)
+_BT = {3: 2, 5: 1, 6: 0}
+_BT_INV = {v: k for k, v in _BT.items()}
+
+
+def bin_key(t, v1, v2):
+    return (_BT[t] << 62) | (v1 << 31) | v2
+
+
+def _i64(x: int) -> int:
+    """unsigned 64-bit word -> the int64 the exchange buffers hold"""
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
 def _view(ptr, n, dtype):
     ct = ctypes.c_int32 if dtype == np.int32 else ctypes.c_int64
     return np.ctypeslib.as_array((ct * n).from_address(ptr)) if n else np.zeros(0, dtype)
 
 
 class ShardSim:
-    def __init__(self, triples):
+    def __init__(self, triples, num_terms=None, local_slice=False):
         self.triples = [tuple(int(x) for x in t) for t in triples]
+        self.V = num_terms if num_terms is not None else 1 + max((max(t) for t in self.triples), default=0)
+        self.local_slice = local_slice
         self.result = None
 
-    def shard_begin(self, rank, nranks, min_support, projection="spo", clean_implied=True, traversal_strategy=1):
+    def shard_begin(self, rank, nranks, min_support, projection="spo", clean_implied=True, traversal_strategy=1,
+                    local_slice=None):
         self.rank, self.R, self.ms = rank, nranks, max(min_support, 1)
         self.proj, self.clean, self.strategy = projection, clean_implied, traversal_strategy
-        self.phase = 0
+        if local_slice is not None:
+            self.local_slice = local_slice
+        n = len(self.triples)
+        self.slice = self.triples if self.local_slice else self.triples[n * rank // nranks: n * (rank + 1) // nranks]
+        self.phase = 10
         self.pending = None
 
     # -- machine ----------------------------------------------------------------------------
@@ -61,19 +102,67 @@ class ShardSim:
         op, arr = self.pending
         self.recv = _view(ptr, n, arr.dtype).copy()
 
-    def _phase0(self):
-        tr = self.triples
-        self.uf = R.frequent_unary_conditions(tr, self.ms)
-        self.bf = R.frequent_binary_conditions(tr, self.uf, self.ms)
+    def _phase10(self):  # dense unary counts of the slice -> all-reduce
+        V = self.V
+        cnt = np.zeros(3 * V, np.int32)
+        for s, p, o in self.slice:
+            cnt[s] += 1
+            cnt[V + p] += 1
+            cnt[2 * V + o] += 1
+        return self._req(_lib.X_ALLREDUCE_SUM_U32, cnt, 11)
+
+    def _phase11(self):  # frequent unary conditions; binary partials -> owners
+        V, ms = self.V, self.ms
+        g = self.recv.astype(np.int64)
+        self.uf = {t: {v: int(g[i * V + v]) for v in range(V) if g[i * V + v] >= ms} for i, t in enumerate((R.S, R.P, R.O))}
+        part = R.frequent_binary_conditions(self.slice, self.uf, 1)  # local counts of every key (threshold 1)
+        out = [[] for _ in range(self.R)]
+        for (t, v1, v2), c in sorted(part.items()):
+            k = bin_key(t, v1, v2)
+            out[key_owner(k, self.R)] += [_i64(k), c]
+        send = np.array([x for o in out for x in o], np.int64)
+        return self._req(_lib.X_ALLTOALLV_U64, send, 12, [len(o) for o in out])
+
+    def _phase12(self):  # summed partials of the owned keys -> frequent keys -> all-gather
+        tot = {}
+        r = self.recv.astype(np.int64)
+        for k, c in zip(r[0::2].tolist(), r[1::2].tolist()):
+            tot[k] = tot.get(k, 0) + c
+        return self._req(_lib.X_ALLGATHERV_U64, np.array(sorted(k for k, c in tot.items() if c >= self.ms), np.int64), 13)
+
+    def _phase13(self):  # every owner's frequent keys; triples -> the owners of their join values
+        self.bf = {}
+        for k in self.recv.tolist():
+            k &= M64
+            self.bf[(_BT_INV[k >> 62], (k >> 31) & 0x7FFFFFFF, k & 0x7FFFFFFF)] = 1
+        out = [[] for _ in range(self.R)]
+        for s, p, o in self.slice:
+            dests = []
+            for pos, v in (("s", s), ("p", p), ("o", o)):
+                if pos in self.proj and shard_of(v, self.R) not in dests:
+                    dests.append(shard_of(v, self.R))
+            for d in dests:
+                out[d] += [(s << 32) | p, o]
+        send = np.array([x for o in out for x in o], np.int64)
+        return self._req(_lib.X_ALLTOALLV_U64, send, 14, [len(o) for o in out])
+
+    def _phase14(self):  # join lines of the owned join values; capture universe from the global conditions
+        r = self.recv.astype(np.int64)
+        tr = [(int(w0 >> 32), int(w0 & 0xFFFFFFFF), int(w1)) for w0, w1 in zip(r[0::2].tolist(), r[1::2].tolist())]
         lines = R.join_lines(tr, self.uf, self.bf, self.proj)
-        caps = set()
         self.local = []
         for jv, line in lines.items():
-            u, b = R.line_captures(line)
-            caps |= u | b
             if shard_of(jv, self.R) == self.rank:
+                u, b = R.line_captures(line)
                 self.local.append(u | b)
-        self.universe = sorted(caps, key=lambda c: c.key())  # identical on every rank (replicated triples)
+        caps = set()
+        for t, sec in ((R.S, (R.P, R.O)), (R.P, (R.S, R.O)), (R.O, (R.S, R.P))):
+            for v in self.uf[t]:
+                for q in sec:
+                    caps.add(R.Cond(v, None, R.create_code(t, secondary=q)))
+        for (t, v1, v2) in self.bf:
+            caps.add(R.Cond(v1, v2, R.add_secondary(t)))
+        self.universe = sorted(caps, key=lambda c: c.key())  # identical on every rank
         self.index = {c: i for i, c in enumerate(self.universe)}
         sup = np.zeros(len(self.universe), np.int32)
         for g in self.local:

@@ -22,7 +22,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, cases, q):
+def _worker(rank, world, port, cases, q, local_slice=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -32,7 +32,9 @@ def _worker(rank, world, port, cases, q):
     try:
         out = []
         for arr, ms, strategy, clean in cases:
-            sim = ShardSim(arr)
+            nv = 1 + max((max(t) for t in arr), default=0)  # one dictionary for all ranks
+            # local slices: an interleaved partition (slices need not be contiguous row ranges)
+            sim = ShardSim(arr[rank::world] if local_slice else arr, nv, local_slice)
             sim.shard_begin(rank, world, ms, "spo", clean, strategy)
             n = distributed.run_protocol(sim)
             out.append((n, sorted(R.cind_set(sim.result))))
@@ -41,11 +43,11 @@ def _worker(rank, world, port, cases, q):
         dist.destroy_process_group()
 
 
-def _run(world, cases):
+def _run(world, cases, local_slice=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice)) for r in range(world)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=300) for _ in procs)
@@ -67,10 +69,10 @@ def _cases(seed, count):
     return cases
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_protocol_matches_oracle(world):
+@pytest.mark.parametrize("world,local_slice", [(2, False), (3, False), (2, True), (3, True)])
+def test_sharded_protocol_matches_oracle(world, local_slice):
     cases = _cases(world, 12)
-    res = _run(world, cases)
+    res = _run(world, cases, local_slice)
     for k, (arr, ms, strategy, clean) in enumerate(cases):
         tr = [tuple(t) for t in arr]
         if strategy == 1 and not clean:
@@ -81,7 +83,7 @@ def test_sharded_protocol_matches_oracle(world):
         else:
             expected = R.cind_set(R.rdfind(tr, ms, strategy, clean))
         parts = [set(res[r][k][1]) for r in range(world)]
-        assert all(res[r][k][0] == 8 for r in range(world))  # the library's eight collectives
+        assert all(res[r][k][0] == 12 for r in range(world))  # the library's twelve collectives
         union = set().union(*parts)
         assert sum(len(p) for p in parts) == len(union)      # every dependent has one owner
         assert union == expected, (k, ms, strategy, clean)

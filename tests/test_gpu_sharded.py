@@ -22,7 +22,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, cases, q):
+def _worker(rank, world, port, cases, q, local_slice=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -32,8 +32,11 @@ def _worker(rank, world, port, cases, q):
     try:
         ctx = _lib.Context(0)
         for s, p, o, nv, ms, strategy, clean in cases:
-            ctx.set_triples(s, p, o, nv)
-            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy)
+            if local_slice:  # this rank holds only its slice (interleaved rows: slices need not be contiguous)
+                ctx.set_triples(s[rank::world], p[rank::world], o[rank::world], nv)
+            else:
+                ctx.set_triples(s, p, o, nv)
+            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy, local_slice=local_slice)
             n = ctx.cind_count()
             rows = ctx.copy_cinds() if n <= 2_000_000 else None
             out.append({"n": n, "checksum": ctx.checksum(), "rows": rows, "heavy": gs["n_heavy_groups"],
@@ -46,11 +49,11 @@ def _worker(rank, world, port, cases, q):
         dist.destroy_process_group()
 
 
-def _run_sharded(world, cases):
+def _run_sharded(world, cases, local_slice=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in procs)
@@ -79,9 +82,9 @@ def _rowset(rows):
     return set(map(tuple, np.stack([rows["dep"], rows["ref"], rows["support"]], 1).tolist()))
 
 
-def _check(world, cases):
+def _check(world, cases, local_slice=False):
     single = _single(cases)
-    res = _run_sharded(world, cases)
+    res = _run_sharded(world, cases, local_slice)
     for k, exp in enumerate(single):
         parts = [res[r][k] for r in range(world)]
         assert sum(p["n"] for p in parts) == exp["n"], k
@@ -107,9 +110,9 @@ def _random_cases(seed, count):
     return cases
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_random_matches_single(world):
-    _check(world, _random_cases(100 + world, 24))
+@pytest.mark.parametrize("world,local_slice", [(2, False), (3, False), (2, True), (3, True)])
+def test_sharded_random_matches_single(world, local_slice):
+    _check(world, _random_cases(100 + world, 24), local_slice)
 
 
 def test_sharded_synthetic_configs_match_oracle():
@@ -131,8 +134,28 @@ def test_sharded_synthetic_configs_match_oracle():
 
 
 def test_sharded_bench_size_properties():
-    """c2 at full size over 2 ranks: CIND count and set checksum equal the single-GPU run."""
+    """c2 at full size over 2 ranks, each holding only its half of the triples: CIND count and set checksum equal
+    the single-GPU run (and the golden vector of the C oracle)."""
+    import json
+    import os
+
     from rdfind_amd import synth
+    from tests.conftest import GOLDEN
 
     d = synth.config("c2", 1.0)
-    _check(2, [(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)])
+    res = _check(2, [(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)], local_slice=True)
+    g = json.load(open(os.path.join(GOLDEN, "full_size.json")))["c2@1.0/s1_clean"]
+    assert sum(res[r][0]["n"] for r in range(2)) == g["n_cinds"]
+    assert sum(res[r][0]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"])
+
+
+def test_shard_slice_limit_is_per_rank():
+    """The 2^32/9-triples-per-context limit applies to a rank's own slice and join shard, not to the input: a
+    sharded input of more triples than one context accepts is taken slice by slice (the size check only)."""
+    from rdfind_amd import _lib
+
+    with _lib.Context(0) as ctx:
+        n_total = (1 << 32) // 9 + 1000  # above the single-context limit
+        with pytest.raises(_lib.RdfError, match="2\\^32/9"):
+            ctx.set_triples_device(1 << 20, 1 << 20, 1 << 20, n_total, 1000)  # size check precedes any access
+        ctx.set_triples_device(1 << 20, 1 << 20, 1 << 20, n_total // 8, 1000)  # one rank of 8: accepted

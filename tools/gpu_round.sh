@@ -71,6 +71,9 @@ for step in "$@"; do
         || { echo "parse prof failed"; tail -30 gpurun_out/pprof_$TAG.log; exit 1; }
       find gpurun_out/pprof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/pprof_$TAG.kernel_stats.csv \;
       grep -E "k_nt|scan" gpurun_out/pprof_$TAG.kernel_stats.csv | cut -c1-40,150- ;;
+    rehearse:*)  # rehearse:<config>:<scale>:<ranks> -- sharded bench with several ranks on the one GPU (gloo)
+      IFS=: read -r _ CFG SC NR <<< "$step"
+      tools/shard_rehearsal.sh ${TAG}_${CFG}_$NR $CFG $SC $NR || exit 1 ;;
     gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
         > gpurun_out/gtest_$TAG.log 2>&1 || { echo "gtest failed"; tail -30 gpurun_out/gtest_$TAG.log; exit 1; }
