@@ -50,6 +50,7 @@ typedef int32_t rdf_status;
 #define RDF_CLEAN_IMPLIED 1u          /* --clean-implied: R1-R4 minimality (TraversalStrategy.scala:126-168) */
 #define RDF_STRATEGY_ALL_AT_ONCE 2u   /* --traversal-strategy 0 semantics (literal Condition.isImpliedBy);
                                          default is strategy 1 (S2L) */
+#define RDF_USE_ASSOCIATION_RULES 8u  /* rdf_run: --use-ars, rdf_association_rules between the first two stages */
 
 typedef struct rdf_ctx rdf_ctx;
 
@@ -145,6 +146,23 @@ rdf_status rdf_copy_terms(rdf_ctx* ctx, uint64_t* offsets, uint32_t* lengths, ui
 rdf_status rdf_copy_triples(rdf_ctx* ctx, uint32_t* s, uint32_t* p, uint32_t* o, uint64_t cap, uint64_t* n_copied);
 
 rdf_status rdf_frequent_conditions(rdf_ctx* ctx, uint32_t min_support, rdf_fc_stats* stats);
+/* --use-ars: exact association rules between frequent conditions (FrequentConditionPlanner.findAssociationRules,
+ * ALG/plan/FrequentConditionPlanner.scala:129-193).  Call between rdf_frequent_conditions and
+ * rdf_build_capture_groups: the AR-implied binary conditions then produce no captures (CreateJoinPartners.scala:
+ * 99-141), and rdf_discover_cinds leaves out the CINDs the reference does not produce with the rules
+ * (CreateAllCindCandidates.scala:108-115 for strategy 0; SmallToLargeTraversalStrategy.scala:80-85 and the
+ * candidate generation built on it for S2L).  Single-GPU only. */
+rdf_status rdf_association_rules(rdf_ctx* ctx, uint64_t* n_rules);
+/* One rule (AssociationRule, ALG/data/AssociationRule.scala:9-19; confidence is always 1): condition codes
+ * s = 1, p = 2, o = 4 and term ids; support = the triple count of the binary condition. */
+typedef struct {
+    uint32_t antecedent_type;
+    uint32_t consequent_type;
+    uint32_t antecedent;
+    uint32_t consequent;
+    uint32_t support;
+} rdf_assoc_rule;
+rdf_status rdf_copy_association_rules(rdf_ctx* ctx, rdf_assoc_rule* out, uint64_t cap, uint64_t* n_copied);
 /* projection: any combination of 's', 'p', 'o' (--projection, default "spo"). */
 rdf_status rdf_build_capture_groups(rdf_ctx* ctx, const char* projection, rdf_group_stats* stats);
 rdf_status rdf_discover_cinds(rdf_ctx* ctx, uint32_t flags, rdf_cind_stats* stats);

@@ -204,10 +204,58 @@ def frequent_binary_conditions(triples, unary_fc, min_support):
     return {k: c for k, c in counts.items() if c >= min_support}
 
 
+def association_rules(unary_fc, binary_fc):
+    """``FrequentConditionPlanner.findAssociationRules`` (FrequentConditionPlanner.scala:130-194, --use-ars):
+    a frequent unary condition A and a frequent binary condition {A, B} give the rule A -> B with confidence
+    count(A, B) / count(A); only confidence-1 rules are kept (:188-190).  Antecedents on the binary's first
+    value give s->p, s->o, p->o (:147-165), on its second value o->s, o->p, p->s (:167-185).
+
+    Returns [(antecedent type, consequent type, antecedent value, consequent value, support)].
+    """
+    rules = []
+    for (t, v1, v2), cb in binary_fc.items():
+        t1 = t & -t
+        t2 = t & ~t1
+        if unary_fc[t1].get(v1) == cb:
+            rules.append((t1, t2, v1, v2, cb))
+        if unary_fc[t2].get(v2) == cb:
+            rules.append((t2, t1, v2, v1, cb))
+    return rules
+
+
+def ar_implied_conditions(rules):
+    """``CreateJoinPartners.AssocationRuleBroadcastInitializer`` (CreateJoinPartners.scala:183-196): the binary
+    condition of every rule (values ordered by type); its capture equals the antecedent's, so it is not
+    emitted as a join partner (:100, :117, :134)."""
+    out = set()
+    for ta, tc, va, vc, _ in rules:
+        out.add((ta | tc, va, vc) if ta < tc else (ta | tc, vc, va))
+    return out
+
+
+def ar_implied_cinds(rules):
+    """``FilterAssociationRuleImpliedCinds.AssocationRuleBroadcastInitializer``
+    (FilterAssociationRuleImpliedCinds.scala:44-58): rule A -> B at the third position pi gives the 1/1 CIND
+    pi[A] < pi[B], which S2L drops before candidate generation (SmallToLargeTraversalStrategy.scala:80-85)."""
+    out = set()
+    for ta, tc, va, vc, _ in rules:
+        cond = ta | tc
+        proj = add_secondary(cond) & ~cond
+        out.add((ta | proj, va, tc | proj, vc))
+    return out
+
+
+def format_rules(rules, term=lambda v: v):
+    """``AssociationRule.toString`` (ALG/data/AssociationRule.scala:15-19), sorted: the --ar-output lines."""
+    chars = {S: "s", P: "p", O: "o"}
+    return sorted(f"[{chars[ta]}={term(va)}] -> [{chars[tc]}={term(vc)}] (support={n},confidence=100.00%)"
+                  for ta, tc, va, vc, n in rules)
+
+
 # ---------------------------------------------------------------------------
 # Join lines (capture groups)
 
-def create_join_partners(triple, unary_fc, binary_fc, projection="spo", use_fis=True):
+def create_join_partners(triple, unary_fc, binary_fc, projection="spo", use_fis=True, ar_implied=frozenset()):
     """``CreateJoinPartners.flatMap`` (ALG/operators/CreateJoinPartners.scala:86-147).
 
     Yields (join value, Cond).  With ``use_fis`` the unary/binary FC Bloom filters
@@ -220,8 +268,8 @@ def create_join_partners(triple, unary_fc, binary_fc, projection="spo", use_fis=
         p = tp if tp in unary_fc[P] else None
         o = to if to in unary_fc[O] else None
 
-        def freq2(v1, v2, t):
-            return (t, v1, v2) in binary_fc
+        def freq2(v1, v2, t):  # mightBeFrequent && !isAssociationRuleImplied (CreateJoinPartners.scala:100)
+            return (t, v1, v2) in binary_fc and (t, v1, v2) not in ar_implied
     else:
         s, p, o = ts, tp, to
 
@@ -258,7 +306,7 @@ def create_join_partners(triple, unary_fc, binary_fc, projection="spo", use_fis=
     return out
 
 
-def join_lines(triples, unary_fc, binary_fc, projection="spo", use_fis=True):
+def join_lines(triples, unary_fc, binary_fc, projection="spo", use_fis=True, ar_implied=frozenset()):
     """``UnionJoinCandidates`` + ``UnionCombinedJoinCandidates`` (UnionJoinCandidates.scala:27-44,
     UnionCombinedJoinCandidates.scala:21-31): group by join value, distinct conditions.
 
@@ -266,7 +314,7 @@ def join_lines(triples, unary_fc, binary_fc, projection="spo", use_fis=True):
     """
     groups = defaultdict(set)
     for t in triples:
-        for jv, cond in create_join_partners(t, unary_fc, binary_fc, projection, use_fis):
+        for jv, cond in create_join_partners(t, unary_fc, binary_fc, projection, use_fis, ar_implied):
             groups[jv].add(cond)
     return {jv: frozenset(c) for jv, c in groups.items()}
 
@@ -396,7 +444,7 @@ def trivially_implied(dep: Cond, ref: Cond) -> bool:
     return False
 
 
-def all_at_once(lines, min_support, clean_implied=True, literal_implies=True):
+def all_at_once(lines, min_support, clean_implied=True, literal_implies=True, ar_cinds=frozenset()):
     """``AllAtOnceTraversalStrategy.enhanceFlinkPlan`` (AllAtOnceTraversalStrategy.scala:42-84) with
     ``CreateAllCindCandidates`` (CreateAllCindCandidates.scala:71-121).
 
@@ -404,6 +452,8 @@ def all_at_once(lines, min_support, clean_implied=True, literal_implies=True):
     ``Condition.isImpliedBy`` (Condition.scala:35-43) also drops a *binary* ref ``X`` of the same type
     as a binary dep ``D`` whenever ``X.v1 == D.v2`` (it compares ``this.v1`` with ``that.v2``).
     ``literal_implies=False`` uses :func:`trivially_implied` instead: the set of all valid CINDs.
+    With --use-ars a unary dep also skips the ref its association rule implies (``findImpliedCondition``,
+    CreateDependencyCandidates.scala:125-129, used at CreateAllCindCandidates.scala:108-115): ``ar_cinds``.
     """
     inter = _Intersector()
     excluded = (lambda d, r: d.implies(r)) if literal_implies else trivially_implied
@@ -411,7 +461,8 @@ def all_at_once(lines, min_support, clean_implied=True, literal_implies=True):
         unary, binary = line_captures(line)
         allc = unary | binary
         for dep in allc:
-            refs = {r for r in allc if not excluded(dep, r)}
+            refs = {r for r in allc if not excluded(dep, r)
+                    and (dep.type, dep.v1, r.type, r.v1) not in ar_cinds}
             inter.add(dep, refs)
     cinds = []
     for dep, count, refs in inter.results():
@@ -449,7 +500,7 @@ def _ckey(dt, dv1, dv2, rt, rv1, rv2):
 
 
 def small_to_large(lines, binary_fc, min_support, clean_implied=True, bloom_fpp=0.0, prune_seed=None,
-                   full_prune=False):
+                   full_prune=False, ar_cinds=frozenset()):
     """``SmallToLargeTraversalStrategy.enhanceFlinkPlan`` (SmallToLargeTraversalStrategy.scala:38-171).
 
     ``binary_fc`` = frequent double conditions {(type, v1, v2): count} (needed by the 2/2 phase,
@@ -479,6 +530,8 @@ def small_to_large(lines, binary_fc, min_support, clean_implied=True, bloom_fpp=
     for a, na, b, nb, n in pairwise:  # :63-105
         (v11 if na == n else proper).append(norm_cind(a.type, a.v1, None, b.type, b.v1, None, n))
         (v11 if nb == n else proper).append(norm_cind(b.type, b.v1, None, a.type, a.v1, None, n))
+    if ar_cinds:  # --use-ars: FilterAssociationRuleImpliedCinds on the 1/1 CINDs (:80-85)
+        v11 = [c for c in v11 if (c.dt, c.dv1, c.rt, c.rv1) not in ar_cinds]
 
     # -- 1/2: GenerateUnaryBinaryCindCandidates (GenerateXxxBinaryCindCandidates.scala:26-65,
     #    GenerateUnaryBinaryCindCandidates.scala:16-41)
@@ -597,6 +650,52 @@ def small_to_large(lines, binary_fc, min_support, clean_implied=True, bloom_fpp=
     return v11 + v12 + v21 + v22
 
 
+def s2l_ars_closed_form(v, ar_cinds, clean_implied=True):
+    """S2L's result under --use-ars as a closed form over V (all valid CINDs of the AR-suppressed join lines),
+    derived from ``small_to_large`` above and cross-checked against it (tests/test_oracle.py):
+
+    * V11' = V11 minus the AR-implied 1/1 CINDs (FilterAssociationRuleImpliedCinds, :80-85);
+    * V12' = A < X in V12 such that every component Xk != A has A < Xk in V11' (1/2 candidates are generated
+      from pairs of V11' refs, or one V11' ref and A itself, GenerateUnaryBinaryCindCandidates.scala:16-41);
+    * V21s = D < R in V21 with no component c of D such that c < R in V11 (candidates: pairs of proper
+      overlaps, GenerateBinaryUnaryCindCandidates.scala:23-57);
+    * V22' = D < Y in V22 such that every component Yk of Y that is not a component of D has D < Yk in all21,
+      all21(D, R) = no component c of D with c < R in V11 and AR-implied (all21 = V21s plus the 2/1 CINDs
+      InferDoubleSingleCinds derives from V11' and proper overlaps, SmallToLargeTraversalStrategy.scala:497-562);
+    * --clean-implied: R1-R4 on (V11', V12', V21s, V22'); raw: V22' minus R4 (the full prune).
+    """
+    v11, v12, v21, v22 = split_by_arity(v)
+    s11 = {(c.dt, c.dv1, c.rt, c.rv1) for c in v11}
+    bad = ar_cinds & s11
+    v11p = [c for c in v11 if (c.dt, c.dv1, c.rt, c.rv1) not in bad]
+    v12p = []
+    for c in v12:
+        ok = True
+        for (t, val) in _comp_values(c.rt, c.rv1, c.rv2):
+            if (t, val) != (c.dt, c.dv1) and (c.dt, c.dv1, t, val) in bad:
+                ok = False
+        if ok:
+            v12p.append(c)
+    v21s = [c for c in v21 if not any((t, val, c.rt, c.rv1) in s11 for (t, val) in _comp_values(c.dt, c.dv1, c.dv2))]
+
+    def all21(dt, dv1, dv2, rt, rv1):
+        return not any((t, val, rt, rv1) in bad for (t, val) in _comp_values(dt, dv1, dv2))
+
+    v22p = []
+    for c in v22:
+        dcomps = set(_comp_values(c.dt, c.dv1, c.dv2))
+        if all(all21(c.dt, c.dv1, c.dv2, t, val) for (t, val) in _comp_values(c.rt, c.rv1, c.rv2) if (t, val) not in dcomps):
+            v22p.append(c)
+    if clean_implied:
+        return remove_implied(v11p, v12p, v21s, v22p)
+    deps_by_ref12 = defaultdict(set)
+    for c in v12p:
+        deps_by_ref12[(c.rt, c.rv1, c.rv2)].add((c.dt, c.dv1))
+    v22r = [c for c in v22p if not any(comp in deps_by_ref12.get((c.rt, c.rv1, c.rv2), set())
+                                       for comp in _comp_values(c.dt, c.dv1, c.dv2))]
+    return v11p + v12p + v21s + v22r
+
+
 def _gen_xxx_binary(group, out):
     """``GenerateXxxBinaryCindCandidates.reduce`` pair loop (GenerateXxxBinaryCindCandidates.scala:26-58)."""
     if len(group) <= 1:
@@ -635,7 +734,8 @@ def _infer_double_single(v11, proper):
 # Whole program (RDFind.createFlinkPlan, ALG/programs/RDFind.scala:196-580, hot-path portion)
 
 def rdfind(triples, min_support=10, traversal_strategy=1, clean_implied=True, use_fis=True,
-           projection="spo", bloom_fpp=0.0, prune_seed=None, distinct_triples=False, full_prune=False):
+           projection="spo", bloom_fpp=0.0, prune_seed=None, distinct_triples=False, full_prune=False,
+           use_ars=False):
     """Run the reference plan on in-memory triples; returns a list of :class:`Cind`."""
     triples = list(triples)
     if distinct_triples:
@@ -646,11 +746,13 @@ def rdfind(triples, min_support=10, traversal_strategy=1, clean_implied=True, us
         raise ValueError("S2L traversal requires --use-fis")
     unary_fc = frequent_unary_conditions(triples, min_support)
     binary_fc = frequent_binary_conditions(triples, unary_fc, min_support)
-    lines = join_lines(triples, unary_fc, binary_fc, projection, use_fis)
+    rules = association_rules(unary_fc, binary_fc) if use_ars else []  # needs --use-fis in the reference
+    lines = join_lines(triples, unary_fc, binary_fc, projection, use_fis, ar_implied_conditions(rules))
     if traversal_strategy == 0:
-        return all_at_once(lines, min_support, clean_implied)
+        return all_at_once(lines, min_support, clean_implied, ar_cinds=ar_implied_cinds(rules))
     if traversal_strategy == 1:
-        return small_to_large(lines, binary_fc, min_support, clean_implied, bloom_fpp, prune_seed, full_prune)
+        return small_to_large(lines, binary_fc, min_support, clean_implied, bloom_fpp, prune_seed, full_prune,
+                              ar_implied_cinds(rules))
     raise ValueError(f"unsupported traversal strategy {traversal_strategy}")
 
 

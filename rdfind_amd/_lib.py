@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("RDFIND_HIP_LIB") or os.path.join(_HERE, "librdfind_hi
 RDF_CLEAN_IMPLIED = 1
 RDF_STRATEGY_ALL_AT_ONCE = 2
 RDF_SHARD_LOCAL_SLICE = 4
+RDF_USE_ASSOCIATION_RULES = 8
 
 # every symbol declared in include/rdfind_hip.h
 EXPORTED_SYMBOLS = (
@@ -29,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
     "rdf_distinct_triples", "rdf_copy_triples", "rdf_parse_ntriples", "rdf_copy_terms",
     "rdf_set_dictionary_parsed", "rdf_device_bytes", "rdf_copy_cinds_decoded", "rdf_result_sizes",
-    "rdf_copy_result_raw",
+    "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules",
 )
 RDF_NT_TABS = 1
 
@@ -80,6 +81,9 @@ class ExchangeRequest:
         return f"ExchangeRequest(op={self.op}, count={self.count}, send_counts={self.send_counts})"
 
 
+# rdf_assoc_rule (include/rdfind_hip.h): condition codes s = 1, p = 2, o = 4, term ids, support
+RULE_DTYPE = np.dtype([("antecedent_type", "<u4"), ("consequent_type", "<u4"), ("antecedent", "<u4"),
+                       ("consequent", "<u4"), ("support", "<u4")])
 CIND_DTYPE = np.dtype([("dep", "<u4"), ("ref", "<u4"), ("support", "<u4")])
 # rdf_cind_row (include/rdfind_hip.h): the reference's Cind shape with term ids
 ROW_DTYPE = np.dtype([("dep_capture_type", "<u4"), ("dep_value1", "<u4"), ("dep_value2", "<u4"),
@@ -137,6 +141,8 @@ def load():
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
         "rdf_format_cinds": (i32, [P, u64, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_last_stats": (i32, [P, ctypes.POINTER(FcStats), ctypes.POINTER(GroupStats), ctypes.POINTER(CindStats)]),
+        "rdf_association_rules": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_copy_association_rules": (i32, [P, P, u64, ctypes.POINTER(u64)]),
         "rdf_shard_begin": (i32, [P, u32, u32, u32, ctypes.c_char_p, u32]),
         "rdf_shard_step": (i32, [P, ctypes.POINTER(Exchange)]),
         "rdf_shard_export": (i32, [P, P]),
@@ -269,6 +275,20 @@ class Context:
         self.fc = _struct_dict(st)
         return self.fc
 
+    def association_rules(self) -> int:
+        """--use-ars after frequent_conditions (rdf_association_rules); returns the number of rules."""
+        n = ctypes.c_uint64()
+        self._check(self.lib.rdf_association_rules(self.ptr, ctypes.byref(n)), "rdf_association_rules")
+        self.n_rules = int(n.value)
+        return self.n_rules
+
+    def copy_association_rules(self) -> np.ndarray:
+        out = np.empty(self.n_rules, dtype=RULE_DTYPE)
+        got = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_association_rules(self.ptr, out.ctypes.data, len(out), ctypes.byref(got)),
+                    "rdf_copy_association_rules")
+        return out[:got.value]
+
     def build_capture_groups(self, projection: str = "spo"):
         st = GroupStats()
         self._check(self.lib.rdf_build_capture_groups(self.ptr, projection.encode(), ctypes.byref(st)),
@@ -283,8 +303,10 @@ class Context:
         self.cinds = _struct_dict(st)
         return self.cinds
 
-    def run(self, min_support=10, projection="spo", clean_implied=True, traversal_strategy=1):
+    def run(self, min_support=10, projection="spo", clean_implied=True, traversal_strategy=1, use_ars=False):
         self.frequent_conditions(min_support)
+        if use_ars:
+            self.association_rules()
         self.build_capture_groups(projection)
         return self.discover_cinds(clean_implied, traversal_strategy)
 
@@ -306,11 +328,12 @@ class Context:
 
     # -- sharded mode (driven by rdfind_amd.distributed.run_sharded) ---------------------------
     def shard_begin(self, rank: int, nranks: int, min_support: int, projection="spo", clean_implied=True,
-                    traversal_strategy=1, local_slice=False):
+                    traversal_strategy=1, local_slice=False, use_ars=False):
         """local_slice: the resident triples are this rank's slice of the input (else every rank holds all of
-        them and the library takes its row range)."""
+        them and the library takes its row range).  use_ars: rejected (single-GPU only)."""
         flags = (RDF_CLEAN_IMPLIED if clean_implied else 0) | (RDF_STRATEGY_ALL_AT_ONCE if traversal_strategy == 0 else 0)
         flags |= RDF_SHARD_LOCAL_SLICE if local_slice else 0
+        flags |= RDF_USE_ASSOCIATION_RULES if use_ars else 0
         self._nranks = nranks
         self._check(self.lib.rdf_shard_begin(self.ptr, rank, nranks, min_support, projection.encode(), flags),
                     "rdf_shard_begin")

@@ -46,6 +46,9 @@ static constexpr u32 META_BIN = 1u, META_PARENTS = 2u, META_HEAVY_ONLY = 4u;
 
 // Rule modes for K7 (TraversalStrategy.removeImpliedCinds, TraversalStrategy.scala:126-168)
 enum RuleMode : int { RULES_NONE = 0, RULES_S2L_RAW = 1, RULES_CLEAN = 2 };
+// --use-ars on the discovery side (ars.inl ar_drop): strategy 0 drops the AR-implied 1/1 CINDs, S2L also the larger
+// CINDs its candidate generation cannot reach without them
+enum ArMode : int { AR_NONE = 0, AR_S0 = 1, AR_S2L = 2 };
 
 struct CindView {
     // compact capture space [0, C); unary compact ids are [0, Cu), binary [Cu, C)
@@ -65,6 +68,8 @@ struct CindView {
     const u64* ebin;      // first explicit pair of a dep whose ref is binary
     int literal;          // strategy-0 Condition.isImpliedBy quirk
     int mode;             // RuleMode
+    int ar;               // ArMode (--use-ars)
+    const u32* arref;     // unary compact id -> the ref its association rule implies, or NONE32 [Cu]
 };
 
 }  // namespace rdf

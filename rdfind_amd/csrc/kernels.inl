@@ -370,6 +370,8 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
     }
 }
 
+#include "ars.inl"
+
 
 // ================================================================================================
 // K3: join partners  (CreateJoinPartners.flatMap, ALG/operators/CreateJoinPartners.scala:86-147)
@@ -822,11 +824,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final(CindView v, const u64
                 lc = (u32)sz;
                 le = (u32)(v.doff[d + 1] - v.doff[d]);
             }
-            // unary heavy-only dependents are emitted per bitmask class (k_class_*), binary ones by k_heavy
-            nchunk_heavy[d] = (nlight || d < v.Cu) ? 0 : nch;
+            // unary heavy-only dependents are emitted per bitmask class (k_class_*), binary ones by k_heavy; with
+            // --use-ars every heavy-only dependent takes k_heavy (a class list is not per-dependent)
+            const bool classed = d < v.Cu && !v.ar;
+            nchunk_heavy[d] = (nlight || classed) ? 0 : nch;
             if (!nlight) {
                 info[d].meta |= META_HEAVY_ONLY;
-                if (d >= v.Cu) hc = (u32)sz;
+                if (!classed) hc = (u32)sz;
             }
         }
         acc[0] += hc;
@@ -901,7 +905,7 @@ __device__ inline bool member(const CindView& v, u32 x, u32 y) {
     const CapInfo ix = v.info[x];
     const u64 my = v.info[y].hmask;
     if ((ix.hmask & my) != ix.hmask) return false;
-    if (is_trivial(v, x, y) || is_quirk(v, x, y)) return false;
+    if (is_trivial(v, x, y) || is_quirk(v, x, y) || ar_drop(v, x, y)) return false;
     if (ix.meta & META_HEAVY_ONLY) return true;
     const u64 b = v.eoff[x], e = v.eoff[x + 1];
     return bsearch_u64(v.epairs + b, e - b, ((u64)x << 32) | y);
@@ -921,6 +925,8 @@ __device__ inline bool member(const CindView& v, u32 x, u32 y) {
 __device__ inline bool rule_keep(const CindView& v, u32 a, u32 r) {
     if (v.mode == RULES_NONE || a < v.Cu) return true;
     const u32* bc = v.bcomp + 2ull * (a - v.Cu);
+    if (v.ar == AR_S2L && r < v.Cu)  // S2L's 2/1 candidates avoid every 1/1 CIND, AR-implied ones included (R1)
+        return !(member(v, bc[0], r) || v.arref[bc[0]] == r || member(v, bc[1], r) || v.arref[bc[1]] == r);
     return !(member(v, bc[0], r) || member(v, bc[1], r));                               // R1 / R4
 }
 
@@ -948,7 +954,7 @@ __device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& i
     const CapInfo ir = v.info[r];
     if (ir.support < id.support) return NONE32;
     if ((ir.hmask & id.hmask) != id.hmask) return NONE32;
-    if (is_trivial(v, d, r) || is_quirk(v, d, r)) return NONE32;
+    if (is_trivial(v, d, r) || is_quirk(v, d, r) || ar_drop(v, d, r)) return NONE32;
     return r;
 }
 

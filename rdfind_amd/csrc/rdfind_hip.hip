@@ -50,6 +50,10 @@ struct rdf_ctx {
     bool force_global_counts = false;
     bool allow_hclass = true;
     u64 heavy_min = 64;  // smaller groups are cheaper to verify by binary search than as bit columns
+    // --use-ars (rdf_association_rules): rules (5 u32 each), per-condition counts, unary dependent -> implied ref
+    bool ar_on = false;
+    u64 n_rules = 0;
+    DevBuf ar_ucnt, ar_bcnt, ar_bits, ar_rules, arref;
 
     // capture groups
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
@@ -250,7 +254,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->brcnt, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto};
+            &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref};
 }
 
 extern "C" {
@@ -840,6 +844,8 @@ static void fc_stats(rdf_ctx* c, const u64 nfreq[3], u64 nkeys, u64 B) {
 
 static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
     c->ms = min_support ? min_support : 1;  // a support of 0 admits exactly the captures that exist
+    c->ar_on = false;
+    c->n_rules = 0;
     for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), c->stream));
@@ -873,6 +879,76 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     TRY(fc_end(c));
     fc_stats(c, nfreq, nkeys, B);
     if (stats) *stats = c->fstats;
+    return RDF_OK;
+}
+
+// Association rules (--use-ars, FrequentConditionPlanner.findAssociationRules, ALG/plan/FrequentConditionPlanner.scala:
+// 129-193): triple counts of the frequent conditions (k_ar_count), rule bits per frequent binary key, the rules, and
+// the frequent binary keys without the AR-implied ones (CreateJoinPartners.scala:99-141 never emits those captures).
+rdf_status rdf_association_rules(rdf_ctx* c, uint64_t* n_rules) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage != 2) return fail(c, RDF_ERR_STATE, "rdf_association_rules follows rdf_frequent_conditions");
+    if (c->ar_on) return fail(c, RDF_ERR_STATE, "association rules already applied to these frequent conditions");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 B = c->B, U = c->U;
+    ENSURE(c, ar_ucnt, std::max<u64>(U, 1) * 4);
+    ENSURE(c, ar_bcnt, std::max<u64>(B, 1) * 4);
+    ENSURE(c, ar_bits, std::max<u64>(B, 1) * 4);
+    ENSURE(c, flags, (B + 1) * 4);
+    ENSURE(c, fpos, (B + 1) * 4);
+    ENSURE(c, pos, (B + 1) * 4);
+    ENSURE(c, bkeys_tmp, std::max<u64>(B, 1) * 8);
+    HIP_TRY(c, hipMemsetAsync(c->ar_ucnt.p, 0, std::max<u64>(U, 1) * 4, st));
+    HIP_TRY(c, hipMemsetAsync(c->ar_bcnt.p, 0, std::max<u64>(B, 1) * 4, st));
+    if (c->n && B)
+        hipLaunchKernelGGL(k_ar_count, dim3(grid_for(c->n, RDF_BLOCK * 4, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o,
+                           c->n, V, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1,
+                           c->ar_ucnt.as<u32>(), c->ar_bcnt.as<u32>());
+    if (B)
+        hipLaunchKernelGGL(k_ar_flags, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, V,
+                           c->frank.as<u32>(), c->ar_ucnt.as<u32>(), c->ar_bcnt.as<u32>(), c->ar_bits.as<u32>(),
+                           c->flags.as<u32>(), (u32*)c->pos.p);
+    // rule slots (flags) and kept keys (pos) -> exclusive offsets fpos / pos (in place)
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), B, c->fpos.as<u32>() + B, st));
+    HIP_TRY(c, exclusive_scan_u32(c->ws, (u32*)c->pos.p, (u32*)c->pos.p, B, (u32*)c->pos.p + B, st));
+    u64 v[2];
+    TRY(read_multi(c, {{c->fpos.as<u32>() + B, 4}, {(u32*)c->pos.p + B, 4}}, v));
+    const u64 NR = v[0], Bk = v[1];
+    ENSURE(c, ar_rules, std::max<u64>(NR, 1) * 5 * 4);
+    if (B)
+        hipLaunchKernelGGL(k_ar_emit, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B,
+                           c->ar_bits.as<u32>(), c->ar_bcnt.as<u32>(), c->fpos.as<u32>(), (const u32*)c->pos.p,
+                           c->ar_rules.as<u32>(), c->bkeys_tmp.as<u64>());
+    std::swap(c->bkeys, c->bkeys_tmp);
+    TRY(fc_binary_index(c, Bk));  // already sorted: the radix passes keep the order
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->n_rules = NR;
+    c->ar_on = true;
+    if (n_rules) *n_rules = NR;
+    return RDF_OK;
+}
+
+// rules as rdf_assoc_rule rows (antecedent type, consequent type, antecedent, consequent, support)
+rdf_status rdf_copy_association_rules(rdf_ctx* c, rdf_assoc_rule* out, uint64_t cap, uint64_t* n_copied) {
+    if (!c || (!out && cap)) return RDF_ERR_ARG;
+    if (!c->ar_on) return fail(c, RDF_ERR_STATE, "rdf_association_rules must be called first");
+    const u64 m = std::min<u64>(cap, c->n_rules);
+    if (m) HIP_TRY(c, hipMemcpy(out, c->ar_rules.p, m * sizeof(rdf_assoc_rule), hipMemcpyDeviceToHost));
+    if (n_copied) *n_copied = m;
+    return RDF_OK;
+}
+
+// unary compact dependent -> its AR-implied ref (after the capture compaction)
+static rdf_status g_ar_refs(rdf_ctx* c) {
+    hipStream_t st = c->stream;
+    ENSURE(c, arref, std::max<u64>(c->Cu, 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->arref.p, 0xff, std::max<u64>(c->Cu, 1) * 4, st));
+    if (c->n_rules)
+        hipLaunchKernelGGL(k_ar_refs, dim3(grid_for(c->n_rules, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->ar_rules.as<u32>(), c->n_rules, c->V ? c->V : 1, c->frank.as<u32>(), c->support.as<u32>(),
+                           c->fidx.as<u32>(), c->ms, c->arref.as<u32>());
     return RDF_OK;
 }
 
@@ -1171,6 +1247,7 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     c->nranks = 1;
     TRY(g_emit_sort_support(c, proj));
     TRY(g_compact_groups(c));
+    if (c->ar_on) TRY(g_ar_refs(c));
     u32 h_hist[256];
     TRY(g_size_hist(c, h_hist));
     TRY(g_heavy_binary(c, heavy_threshold(c, h_hist), 0));
@@ -1199,6 +1276,8 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.ebin = nullptr;
     v.literal = (flags & RDF_STRATEGY_ALL_AT_ONCE) ? 1 : 0;
     v.mode = (flags & RDF_CLEAN_IMPLIED) ? RULES_CLEAN : (v.literal ? RULES_NONE : RULES_S2L_RAW);
+    v.ar = c->ar_on && c->nranks == 1 ? (v.literal ? AR_S0 : AR_S2L) : AR_NONE;
+    v.arref = c->arref.as<u32>();
     return v;
 }
 
@@ -1446,7 +1525,7 @@ static rdf_status d_classes_single(rdf_ctx* c, const CindView& v, u64* HC, u64* 
     tbegin(c, RDF_T_CLASS);
     u64 nmem = 0, tcapc = 0;
     u32 ncls = 0;
-    TRY(d_class_table(c, v, c->hclassed ? c->C : c->Cu, &nmem, &ncls, &tcapc));
+    TRY(d_class_table(c, v, v.ar ? 0u : (c->hclassed ? c->C : c->Cu), &nmem, &ncls, &tcapc));
     *HC = 0;
     *NT = 0;
     if (ncls) {
@@ -1629,7 +1708,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));
     // strategy 0's quirk filter is per dependent: keep the pivot scan there (RDFIND_HCLASS=0: test hook)
-    c->hclassed = !v.literal && c->allow_hclass;
+    c->hclassed = !v.literal && c->allow_hclass && !v.ar;
     TRY(d_classes_single(c, v, &HC, &NT));
     if (c->hclassed) TRY(d_class_bin(c, v, &WH));
     TRY(d_heavy_count(c, v, WH, &H));
@@ -1642,6 +1721,10 @@ rdf_status rdf_run(rdf_ctx* c, uint32_t min_support, const char* projection, uin
                    rdf_group_stats* gs, rdf_cind_stats* cs) {
     rdf_status r = rdf_frequent_conditions(c, min_support, fc);
     if (r) return r;
+    if (flags & RDF_USE_ASSOCIATION_RULES) {
+        r = rdf_association_rules(c, nullptr);
+        if (r) return r;
+    }
     r = rdf_build_capture_groups(c, projection, gs);
     if (r) return r;
     return rdf_discover_cinds(c, flags, cs);
@@ -2093,6 +2176,8 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     if (!c) return RDF_ERR_ARG;
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
+    if (flags & RDF_USE_ASSOCIATION_RULES)
+        return fail(c, RDF_ERR_ARG, "association rules are not supported in sharded mode (use rdf_run on one GPU)");
     c->hclassed = false;
     int proj = 0;
     TRY(parse_projection(c, projection, &proj));

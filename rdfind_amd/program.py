@@ -32,7 +32,7 @@ _RESULT_NEUTRAL = {
 FORMAT_CHUNK = 1 << 23     # result rows formatted per device call
 KEEP_LINES_MAX = 1 << 24   # run() returns the lines as a list up to this many CINDs (None above)
 
-_UNSUPPORTED = ["--use-ars", "--ar-output", "--asciify-triples", "--apply-hash", "--hash-dictionary",
+_UNSUPPORTED = ["--asciify-triples", "--apply-hash", "--hash-dictionary",
                 "--hash-function", "--hash-bytes", "--any-binary-captures", "--find-frequent-captures",
                 "--explicit-threshold", "--sbf-bytes", "--balanced-overlap-candidates"]
 
@@ -44,6 +44,8 @@ def build_parser():
     ap.add_argument("--traversal-strategy", type=int, default=1, help="ID of CIND search space traversal strategy")
     ap.add_argument("--use-fis", action="store_true", help="whether to find and use frequent item sets")
     ap.add_argument("--clean-implied", action="store_true", help="whether to remove implied CINDs")
+    ap.add_argument("--use-ars", action="store_true", help="whether to find and use association rules")
+    ap.add_argument("--ar-output", default=None, help="an output file to save the association rules to")
     ap.add_argument("--output", default=None, help="an output file to save the CINDs to")
     ap.add_argument("--projection", default="spo", help="what shall be used as projection for captures")
     ap.add_argument("--distinct-triples", action="store_true", help="whether to ensure that triples are distinct")
@@ -84,10 +86,20 @@ class RDFind:
             # RDFind.scala:290-296 leaves frequentDoubleConditions null without --use-fis and
             # SmallToLargeTraversalStrategy.scala:534 dereferences it.
             raise ValueError("traversal strategy 1 (S2L) requires --use-fis")
+        if (self.args.use_ars or self.args.ar_output) and not self.args.use_fis:
+            # the rules come out of the frequent-condition plan (FrequentConditionPlanner.scala:102), which only runs
+            # with --use-fis (RDFind.scala:290-296); without it their broadcast set is null
+            raise ValueError("--use-ars / --ar-output require --use-fis")
         self.timings = {}
 
     def log(self, msg):
         print(msg, file=sys.stderr)
+
+    def write_rules(self, spec, lines):
+        path = _output_path(spec)
+        self.log(f"Outputting assocation rules to {os.path.abspath(path)}.")
+        with open(path, "w", encoding="utf-8") as f:
+            f.writelines(ln + "\n" for ln in lines)
 
     def run(self, out=sys.stdout):
         a = self.args
@@ -124,6 +136,16 @@ class RDFind:
                 self.log(f"Found {fc['n_frequent_binary']} frequent double-conditions.")
             if a.find_only_fcs >= 1:
                 return []
+            if a.use_ars or a.ar_output:  # FrequentConditionPlanner.findAssociationRules (:129-193)
+                n_rules = ctx.association_rules()
+                if a.debug_level >= 1:
+                    self.log(f"Found {n_rules} frequent association rules.")
+                if a.ar_output:
+                    if dic is None:
+                        dic = ntriples.HeapDictionary(*ctx.parsed_terms())
+                    self.write_rules(a.ar_output, format_rules(ctx.copy_association_rules(), dic.term))
+                if not a.use_ars:  # rules printed only: frequent conditions again, without the suppression
+                    fc = ctx.frequent_conditions(a.support)
             gs = ctx.build_capture_groups(a.projection)
             if a.do_only_join:
                 return []
@@ -143,10 +165,7 @@ class RDFind:
             lines = [] if keep_lines else None
             f = None
             if a.output:
-                path = a.output[5:] if a.output.startswith("file:") else a.output
-                while path.startswith("//"):
-                    path = path[1:]
-                os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+                path = _output_path(a.output)
                 f = open(path, "wb")
             try:
                 for off in range(0, n, FORMAT_CHUNK):
@@ -169,6 +188,22 @@ class RDFind:
         if not a.output and not a.collect_result:
             print(f"Detected {n} CINDs.", file=out)
         return lines
+
+
+def _output_path(spec):
+    path = spec[5:] if spec.startswith("file:") else spec
+    while path.startswith("//"):
+        path = path[1:]
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    return path
+
+
+def format_rules(rules, term):
+    """``AssociationRule.toString`` (ALG/data/AssociationRule.scala:15-19) of rdf_assoc_rule rows, sorted (the
+    reference writes them in Flink's order, RDFind.scala:524-551)."""
+    chars = {1: "s", 2: "p", 4: "o"}
+    return sorted(f"[{chars[ta]}={term(va)}] -> [{chars[tc]}={term(vc)}] (support={n},confidence=100.00%)"
+                  for ta, tc, va, vc, n in rules.tolist())
 
 
 def format_rows(rows, term):
