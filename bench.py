@@ -33,20 +33,37 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
 
-# timer family -> the kernel whose rocprofv3 PMC traffic (profiles/pmc_<config>.json, tools/pmc.sh) is reported
-FAMILY_KERNEL = {"cemit": "k_class_emit", "light": "k_light", "unary": "k_unary_count", "emit": "k_emit_records",
-                 "sort": "k_radix_scatter", "hwrite": "k_heavy", "hcount": "k_heavy"}
+# timer family -> its kernels, whose rocprofv3 PMC traffic (profiles/pmc_<config>.json, tools/pmc.sh) is summed
+FAMILY_KERNELS = {
+    "unary": ["k_u2_part", "k_u2_slices", "k_u2_count", "k_u2_finish", "k_u2_fval"],
+    "binary": ["k_b2_part", "k_b2_slices", "k_b2_count", "k_spill_insert", "k_bin_freq_flags", "k_bin_freq_scatter",
+               "k_bin_lookup_build"],
+    "emit": ["k_emit_records"],
+    "support": ["k_fresh_bounds", "k_run_support", "k_support_flags", "k_compact_captures", "k_skip_counts",
+                "k_keep_scatter"],
+    "groups": ["k_key_offsets", "k_group_flags", "k_group_build", "k_dgrp"],
+    "pivot": ["k_pivot_nseg", "k_pivot_short", "k_pivot_seg", "k_pivot_final"],
+    "light": ["k_light", "k_light_packed", "k_light_mseg_emit", "k_mseg_chunks", "k_slot_compact"],
+    "rules": ["k_rules_explicit", "k_rules_mark", "k_compact_refs"],
+    "cemit": ["k_class_emit"],
+}
+PMC_STEP_KERNEL = "k_pivot_final"  # launched once per discovery step: the number of steps in the PMC run
 
 
 def pmc_traffic(config, family):
-    """HBM bytes per launch of the family's kernel from the committed PMC summary (FETCH_SIZE x2 + WRITE_SIZE,
-    corrected as MI355X_MICROARCH.md prescribes), or None when no summary for this config is committed."""
+    """HBM bytes per step of the family's kernels from the committed PMC summary (FETCH_SIZE x2 + WRITE_SIZE,
+    corrected as MI355X_MICROARCH.md prescribes; per-launch averages x launches / steps of that run), or None when
+    no summary for this config is committed.  The radix sort (shared by several sorts) has no per-family split."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
-    k = FAMILY_KERNEL.get(family)
-    if not k or not os.path.exists(path):
+    ks = FAMILY_KERNELS.get(family)
+    if not ks or not os.path.exists(path):
         return None
-    ent = json.load(open(path)).get(k)
-    return int(ent["hbm_bytes"]) if ent else None
+    pmc = json.load(open(path))
+    steps = pmc.get(PMC_STEP_KERNEL, {}).get("launches")
+    if not steps:
+        return None
+    tot = sum(pmc[k]["hbm_bytes"] * pmc[k]["launches"] for k in ks if k in pmc)
+    return int(tot / steps) if tot else None
 
 
 def algorithmic_bytes(name, d, fc, gs, cs, counts):
@@ -78,10 +95,10 @@ def algorithmic_bytes(name, d, fc, gs, cs, counts):
     if name == "cemit":
         return 4 * cs["n_class_cinds"]                  # 4-B ref per CIND written (dependent-run output); the shared
                                                         # class lists (< 1 MB) are read from L2
-    if name in ("hwrite", "hcount"):
-        cand = cs["n_heavy_candidates"]
-        out = 4 * cs["n_cinds"] if name == "hwrite" else 4 * cs["n_heavy_chunks"]
-        return 20 * cand + out                          # candidate ids + 16-B capture info, output records
+    if name == "hcount":
+        return 20 * cs["n_heavy_candidates"] + 12 * cs["n_heavy_chunks"]  # candidate id + 16-B info; chunk bits + counts
+    if name == "hwrite":
+        return 8 * cs["n_heavy_candidates"]             # candidate id read, <= one 4-B output per candidate
     return None
 
 
@@ -227,6 +244,12 @@ def main():
     counts = {"sort_passes_records": ((capbits + joinbits + 7) // 8) * gs["n_records"],
               "group_passes": (joinbits + 7) // 8}
     fams = family_rooflines(d, fc, gs, cs, kt, counts)
+    if args.scale == 1.0 and world == 1:  # HBM bytes per step from the committed PMC summary of this config
+        for name, f in fams.items():
+            t = pmc_traffic(args.config, name)
+            if t is not None:
+                f["traffic"] = t
+                f["traffic_x"] = round(t / f["bytes"], 2) if f["bytes"] else None
     dominant = max(kt, key=lambda k: kt[k])
     roof = None
     for name in [dominant] + sorted(kt, key=lambda k: -kt[k]):

@@ -36,23 +36,33 @@ __device__ inline u32 frank_at(const u32* __restrict__ frank, const u32* __restr
 
 __device__ inline bool fbit(const u64* __restrict__ fbits, u64 i) { return (fbits[i >> 6] >> (i & 63)) & 1ull; }
 
-// One leader round of wave merging on a bucket index: lanes whose bucket equals the first active lane's take
-// consecutive positions from one LDS atomic; the other lanes take one atomic each.  Returns this lane's slot
-// (SCATTER pass) or adds to the histogram.  A bucket's records are counted in any order.
+// Leader rounds of wave merging on a bucket index: in each round, the lanes whose bucket equals the first
+// remaining lane's take consecutive positions from one LDS atomic (hot buckets: predicates, Zipf objects); lanes
+// left after ROUNDS take one atomic each.  Returns this lane's slot (SCATTER pass) or adds to the histogram.
+// A bucket's records are counted in any order.  One round measured fastest on c2 (4 rounds: K1 passes +20 %).
+template <int ROUNDS = 1>
 __device__ inline u32 bucket_slot(u32* lh, u32 bk, bool active) {
-    const u64 A = __ballot(active);
+    u64 todo = __ballot(active);
     u32 pos = 0;
-    if (A) {
-        const int l = __ffsll((long long)A) - 1;
+    bool done = !active;
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        if (!todo) break;
+        const int l = __ffsll((long long)todo) - 1;
         const u32 bl = __shfl(bk, l, RDF_WAVE);
-        const bool mine = active && bk == bl;
+        const bool mine = !done && bk == bl;
         const u64 m = __ballot(mine);
         u32 base = 0;
         if (lane_id() == l) base = atomicAdd(&lh[bl], (u32)__popcll(m));
         base = __shfl(base, l, RDF_WAVE);
-        if (mine) pos = base + (u32)__popcll(m & lanemask_lt());
-        else if (active) pos = atomicAdd(&lh[bk], 1u);
+        if (mine) {
+            pos = base + (u32)__popcll(m & lanemask_lt());
+            done = true;
+        }
+        todo &= ~m;
+        if (__popcll(m) == 1) break;  // no repeats at the head of the wave: the rest take one atomic each
     }
+    if (!done) pos = atomicAdd(&lh[bk], 1u);
     return pos;
 }
 
@@ -178,7 +188,8 @@ __global__ __launch_bounds__(U2_CBLOCK) void k_u2_count(const uint16_t* __restri
     if (a0 < a1) {
         for (u64 i = s0 + threadIdx.x; i < a0; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
         const uint4* v = (const uint4*)(recs + a0);
-        for (u64 q = threadIdx.x; q < (a1 - a0) / 8; q += U2_CBLOCK) {
+        const u64 nq = (a1 - a0) / 8;
+        for (u64 q = threadIdx.x; q < nq; q += U2_CBLOCK) {
             const uint4 w = v[q];
             const u32 ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -253,8 +264,31 @@ static constexpr u64 B2_SLICE = 2560;          // K2 records per counting slice 
 
 __device__ inline u32 b2_bucket(u64 key, int bits) { return (u32)(mix64(key) >> (64 - bits)); }
 
+// K2 records carry their count (1..4) in the two key bits that are zero for every term id < 2^30 (bit 30 of v2,
+// bit 31 + 30 of v1): no separate count stream to scatter
+static constexpr u64 B2_CBITS = (1ull << 30) | (1ull << 61);
+__device__ inline u64 b2_pack(u64 key, u32 c) { return key | ((u64)((c - 1) & 1u) << 30) | ((u64)((c - 1) >> 1) << 61); }
+__device__ inline u32 b2_count_of(u64 rec) { return 1u + (u32)((rec >> 30) & 1ull) + 2u * (u32)((rec >> 61) & 1ull); }
+
+// runs of equal keys in adjacent active lanes, cut every 4 lanes: returns this lane's record count (0 if it is
+// inside a piece, else 1..4)
+__device__ inline u32 wave_runs4(u64 key, bool active) {
+    const int lane = lane_id();
+    const u64 A = __ballot(active);
+    const u64 prev = __shfl_up(key, 1, RDF_WAVE);
+    const bool head = active && (lane == 0 || !((A >> (lane - 1)) & 1ull) || prev != key);
+    const u64 H = __ballot(head);
+    if (!active) return 0;
+    const u64 le = lane == RDF_WAVE - 1 ? ~0ull : ((1ull << (lane + 1)) - 1);
+    const int start = 63 - __clzll((long long)(H & le));  // this lane's run head
+    if ((lane - start) & 3) return 0;
+    const u64 stop = (H | ~A) & ~le;  // next head or inactive lane above
+    const int end = stop ? __ffsll((long long)stop) - 1 : RDF_WAVE;
+    return (u32)min(4, end - lane);
+}
+
 // the binary keys of one triple window with runs of equal keys in adjacent lanes merged (the same merge in both
-// passes, so the histogram pass and the scatter pass agree; a record counts <= 64 occurrences)
+// passes, so the histogram pass and the scatter pass agree; a record counts <= 4 occurrences)
 __device__ inline void b2_keys(const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o, u64 i,
                                bool act, u32 V, const u64* __restrict__ fbits, u64 (&key)[3], u32 (&cnt)[3]) {
     u32 ts = 0, tp = 0, to = 0;
@@ -270,16 +304,15 @@ __device__ inline void b2_keys(const u32* __restrict__ s, const u32* __restrict_
     key[0] = bin_key(2, ts, tp);  // o[s,p] (35)
     key[1] = bin_key(1, ts, to);  // p[s,o] (21)
     key[2] = bin_key(0, tp, to);  // s[p,o] (14)
-    cnt[0] = wave_merge<u64, 0>(key[0], fs && fp);
-    cnt[1] = wave_merge<u64, 0>(key[1], fs && fo);
-    cnt[2] = wave_merge<u64, 0>(key[2], fp && fo);
+    cnt[0] = wave_runs4(key[0], fs && fp);
+    cnt[1] = wave_runs4(key[1], fs && fo);
+    cnt[2] = wave_runs4(key[2], fp && fo);
 }
 
 template <bool SCATTER>
 __global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s, const u32* __restrict__ p,
                                                        const u32* __restrict__ o, u64 n, u32 V, const u64* __restrict__ fbits,
-                                                       int bits, u32* ghist, u64* __restrict__ rkeys,
-                                                       uint8_t* __restrict__ rcnt) {
+                                                       int bits, u32* ghist, u64* __restrict__ rkeys) {
     extern __shared__ u32 lh[];
     const u32 NB = 1u << bits;
     for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
@@ -295,10 +328,7 @@ __global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s
         for (int t = 0; t < 3; ++t) {
             const bool a = cnt[t] != 0;
             const u32 pos = bucket_slot(lh, a ? b2_bucket(key[t], bits) : 0u, a);
-            if (SCATTER && a) {
-                rkeys[pos] = key[t];
-                rcnt[pos] = (uint8_t)cnt[t];
-            }
+            if (SCATTER && a) rkeys[pos] = b2_pack(key[t], cnt[t]);
         }
     }
     if (!SCATTER) {
@@ -320,8 +350,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_slices(const u32* __restrict__
 // counts its distinct keys; the slices of a larger bucket (hot keys) append all their (key, count) partials to the
 // spill list instead, which one global table then sums (as do records a crowded table refused).
 // counters: [0] frequent keys in out, [1] distinct keys, [2] spill entries.
-__global__ __launch_bounds__(RDF_BLOCK) void k_b2_count(const u64* __restrict__ rkeys, const uint8_t* __restrict__ rcnt,
-                                                        const u32* __restrict__ ghist, const u32* __restrict__ soff, u32 NB,
+__global__ __launch_bounds__(RDF_BLOCK) void k_b2_count(const u64* __restrict__ rkeys, const u32* __restrict__ ghist, const u32* __restrict__ soff, u32 NB,
                                                         u32 G, u32 ms, u64* out, u64* spill_keys, u32* spill_cnt,
                                                         u64* counters, int all_to_spill) {
     __shared__ u64 tk[B2_SLOTS];
@@ -350,8 +379,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_count(const u64* __restrict__ 
         }
         __syncthreads();
         for (u64 i = s0 + threadIdx.x; i < s1; i += RDF_BLOCK) {
-            const u64 key = rkeys[i];
-            const u32 c = rcnt[i];
+            const u64 rec = rkeys[i];
+            const u64 key = rec & ~B2_CBITS;
+            const u32 c = b2_count_of(rec);
             u32 h = (u32)mix64(key) & (T - 1);  // low hash bits (the bucket used the high ones)
             bool done = false;
             for (u32 probe = 0; probe < 32 && !done; ++probe) {

@@ -97,7 +97,7 @@ struct rdf_ctx {
     u32 x_bytes = 8;
     bool x_imported = true;
     DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep;
-    DevBuf uhist, urecs, usl, cntg, fstage, bfreq, boff, fbits, brkeys, brcnt;  // partitioned K1 / K2 (counts.inl)
+    DevBuf uhist, urecs, usl, cntg, fstage, bfreq, boff, fbits, brkeys;  // partitioned K1 / K2 (counts.inl)
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
@@ -251,7 +251,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
-                      &c->fbits, &c->brkeys, &c->brcnt, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
+                      &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
             &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref};
@@ -748,7 +748,6 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
     const u64 maxrec = std::max<u64>(3 * n, 1);
     ENSURE(c, uhist, (nh + 1) * 4);
     ENSURE(c, brkeys, maxrec * 8);
-    ENSURE(c, brcnt, maxrec);
     ENSURE(c, usl, (NB2 + 1) * 4);
     ENSURE(c, tkeys, maxrec * 8);  // spill list: keys
     ENSURE(c, pos, maxrec * 4);    // spill list: counts
@@ -756,16 +755,15 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
     ENSURE(c, bkeys, bmax * 8);
     const size_t lds = (size_t)NB2 * 4;
     hipLaunchKernelGGL((k_b2_part<false>), dim3(G2), dim3(B2_PBLOCK), lds, st, s, p, o, n, V, c->fbits.as<u64>(), bits,
-                       c->uhist.as<u32>(), (u64*)nullptr, (uint8_t*)nullptr);
+                       c->uhist.as<u32>(), (u64*)nullptr);
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
     hipLaunchKernelGGL((k_b2_part<true>), dim3(G2), dim3(B2_PBLOCK), lds, st, s, p, o, n, V, c->fbits.as<u64>(), bits,
-                       c->uhist.as<u32>(), c->brkeys.as<u64>(), c->brcnt.as<uint8_t>());
+                       c->uhist.as<u32>(), c->brkeys.as<u64>());
     hipLaunchKernelGGL(k_b2_slices, dim3(grid_for(NB2, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(), NB2, G2,
                        c->usl.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->usl.as<u32>(), c->usl.as<u32>(), NB2, c->usl.as<u32>() + NB2, st));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 3 * 8, st));
-    hipLaunchKernelGGL(k_b2_count, dim3(256 * 3), dim3(RDF_BLOCK), 0, st, c->brkeys.as<u64>(), c->brcnt.as<uint8_t>(),
-                       c->uhist.as<u32>(), c->usl.as<u32>(), NB2, G2, c->ms, c->bkeys.as<u64>(), c->tkeys.as<u64>(),
+    hipLaunchKernelGGL(k_b2_count, dim3(256 * 3), dim3(RDF_BLOCK), 0, st, c->brkeys.as<u64>(), c->uhist.as<u32>(), c->usl.as<u32>(), NB2, G2, c->ms, c->bkeys.as<u64>(), c->tkeys.as<u64>(),
                        (u32*)c->pos.p, dscal(c, 3), partials ? 1 : 0);
     TRY(read_scalars(c, 6));
     *B = c->hscal[3];

@@ -76,7 +76,9 @@ class RDFind:
     """Program lifecycle (AbstractProgram.run: FLK/jobs/AbstractProgram.java:112-139)."""
 
     def __init__(self, argv):
+        self.argv = list(argv)
         self.args = build_parser().parse_args(argv)
+        self.rank, self.world = 0, 1
         for flag in _UNSUPPORTED:
             if getattr(self.args, flag.lstrip("-").replace("-", "_")) is not None:
                 raise NotImplementedError(f"{flag} is not supported by this build (SURVEY.md section 8f)")
@@ -103,11 +105,29 @@ class RDFind:
 
     def run(self, out=sys.stdout):
         a = self.args
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if a.dop > 1 and world == 1:
+            return self.launch_ranks(a.dop)
+        self.rank, self.world = int(os.environ.get("RANK", "0")), world
+        if world > 1:
+            if a.use_ars:
+                raise NotImplementedError("--use-ars with -dop > 1: association rules run on one GPU only")
+            if a.find_only_fcs or a.do_only_join:
+                raise NotImplementedError("--find-only-fcs / --do-only-join with -dop > 1")
+            import torch
+            import torch.distributed as dist  # the ranks' exchange (rdfind_amd/distributed.py)
+            if not dist.is_initialized():  # RDFIND_DIST_BACKEND=gloo: host-staged exchange (rehearsals on one GPU)
+                dist.init_process_group(os.environ.get("RDFIND_DIST_BACKEND", "nccl"))
+            device = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+            if dist.get_backend() == "nccl":
+                torch.cuda.set_device(device)
+        else:
+            device = a.device
         t0 = time.time()
         paths = ntriples.resolve_paths(a.inputs)
         if not paths:
             raise ValueError("no input files")
-        with _lib.Context(a.device) as ctx:
+        with _lib.Context(device) as ctx:
             if a.host_parser:  # host tokenizer + dictionary (rdfind_amd/ntriples.py)
                 s, p, o, dic = ntriples.read_triples(paths, tabs=a.tabs)
                 n_in = s.shape[0]
@@ -130,6 +150,12 @@ class RDFind:
                 n_distinct, _ = ctx.distinct_triples()
                 if a.debug_level >= 1:
                     self.log(f"{n_distinct} distinct triples of {n_in}.")
+            if world > 1:  # -dop: every rank parsed the same bytes (same ids) and takes its share of the work
+                from . import distributed
+                gs, cs = distributed.run_sharded(ctx, a.support, a.projection, a.clean_implied,
+                                                 a.traversal_strategy)
+                fc = ctx.fc
+                return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
             fc = ctx.frequent_conditions(a.support)
             if a.debug_level >= 1:
                 self.log(f"Found {sum(fc['n_frequent_unary'])} frequent single-conditions.")
@@ -150,37 +176,47 @@ class RDFind:
             if a.do_only_join:
                 return []
             cs = ctx.discover_cinds(clean_implied=a.clean_implied, traversal_strategy=a.traversal_strategy)
-            ctx.sync()
-            self.timings["discover"] = time.time() - t1
-            self.timings["device_ms"] = ctx.stage_times()
-            self.stats = {"fc": fc, "groups": gs, "cinds": cs}
-            # Cind.toString lines are formatted on the GPU (rdf_format_cinds) in chunks of rows
-            t2 = time.time()
-            n = ctx.cind_count()
-            if dic is None:
-                ctx.set_dictionary_parsed()  # device dictionary straight into the formatter
-            else:
-                ctx.set_dictionary(dic.terms)
-            keep_lines = n <= KEEP_LINES_MAX or a.collect_result or a.debug_level >= 3
-            lines = [] if keep_lines else None
-            f = None
-            if a.output:
-                path = _output_path(a.output)
-                f = open(path, "wb")
-            try:
-                for off in range(0, n, FORMAT_CHUNK):
-                    text = ctx.format_array(off, FORMAT_CHUNK)
-                    if f is not None:
-                        f.write(memoryview(text))
-                    if keep_lines:
-                        lines.extend(text.tobytes().decode("utf-8").splitlines())
-            finally:
+            return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
+
+    def write_output(self, ctx, dic, stats, t1, out):
+        """Cind.toString lines formatted on the GPU (rdf_format_cinds) in chunks of rows, to --output and/or the
+        returned list.  With -dop > 1 every rank writes its own CINDs to a part file and rank 0 concatenates them
+        into the one output file (the reference writes file:// outputs with parallelism 1, RDFind.scala:507-520)."""
+        a = self.args
+        ctx.sync()
+        self.timings["discover"] = time.time() - t1
+        self.timings["device_ms"] = ctx.stage_times()
+        self.stats = stats
+        t2 = time.time()
+        n = ctx.cind_count()
+        if dic is None:
+            ctx.set_dictionary_parsed()  # device dictionary straight into the formatter
+        else:
+            ctx.set_dictionary(dic.terms)
+        keep_lines = n <= KEEP_LINES_MAX or a.collect_result or a.debug_level >= 3
+        lines = [] if keep_lines else None
+        f = None
+        path = _output_path(a.output) if a.output else None
+        if path:
+            f = open(path if self.world == 1 else f"{path}.part{self.rank}", "wb")
+        try:
+            for off in range(0, n, FORMAT_CHUNK):
+                text = ctx.format_array(off, FORMAT_CHUNK)
                 if f is not None:
-                    f.close()
-            self.timings["format"] = time.time() - t2
+                    f.write(memoryview(text))
+                if keep_lines:
+                    lines.extend(text.tobytes().decode("utf-8").splitlines())
+        finally:
+            if f is not None:
+                f.close()
+        if self.world > 1:
+            n, lines = self.merge_ranks(n, lines, path)
+            if self.rank != 0:
+                return lines
+        self.timings["format"] = time.time() - t2
         if a.debug_level >= 1:
             self.log(f"Found {n} CINDs in total.")
-        if a.output:
+        if path:
             self.log(f"Outputting CINDs to {os.path.abspath(path)}.")
         if a.collect_result or a.debug_level >= 3:
             for ln in lines:
@@ -188,6 +224,41 @@ class RDFind:
         if not a.output and not a.collect_result:
             print(f"Detected {n} CINDs.", file=out)
         return lines
+
+    def merge_ranks(self, n, lines, path):
+        """-dop > 1: total count (all-reduce), the part files concatenated by rank 0, the lines gathered on rank 0."""
+        import torch
+        import torch.distributed as dist
+        from .distributed import exchange_device
+        t = torch.tensor([n], dtype=torch.int64, device=exchange_device())
+        dist.all_reduce(t)
+        total = int(t.item())
+        gathered = [None] * self.world if self.rank == 0 else None
+        dist.gather_object(lines, gathered, dst=0)
+        if self.rank == 0:
+            lines = None if any(x is None for x in gathered) else [ln for part in gathered for ln in part]
+            if path:
+                with open(path, "wb") as dst:
+                    for r in range(self.world):
+                        with open(f"{path}.part{r}", "rb") as src:
+                            while chunk := src.read(1 << 24):
+                                dst.write(chunk)
+                        os.remove(f"{path}.part{r}")
+        dist.barrier()
+        return total, lines
+
+    def launch_ranks(self, nranks):
+        """-dop N (StratosphereParameters: the parallelism): one process per GPU under torch.distributed.run, started as
+        child processes before this process touches a GPU; returns their exit status."""
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "rdfind_amd"] + self.argv
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        return subprocess.run(cmd, env=env).returncode
 
 
 def _output_path(spec):
@@ -220,5 +291,5 @@ def format_rows(rows, term):
 
 def main(argv=None):
     prog = RDFind(sys.argv[1:] if argv is None else argv)
-    prog.run()
-    return 0
+    rc = prog.run()
+    return rc if isinstance(rc, int) else 0

@@ -159,3 +159,25 @@ def test_shard_slice_limit_is_per_rank():
         with pytest.raises(_lib.RdfError, match="2\\^32/9"):
             ctx.set_triples_device(1 << 20, 1 << 20, 1 << 20, n_total, 1000)  # size check precedes any access
         ctx.set_triples_device(1 << 20, 1 << 20, 1 << 20, n_total // 8, 1000)  # one rank of 8: accepted
+
+
+@pytest.mark.parametrize("name,mode,flags", [("lubm_small", "s1_clean", ["--use-fis", "--clean-implied"]),
+                                             ("skew_small", "s0_raw", ["--traversal-strategy", "0"])])
+def test_program_dop2_reproduces_golden(tmp_path, name, mode, flags):
+    """-dop 2 through the RDFind-compatible driver: two ranks (torch.distributed.run children of the driver, on
+    the one GPU of the box, gloo exchange), each parsing the input and running the sharded protocol; the part
+    files merge into the one output file, equal to the golden fixture."""
+    import subprocess
+    import sys
+    from tests.conftest import GOLDEN
+    from tests.test_oracle import read_golden
+    ms, expected = read_golden(name, mode)
+    out = tmp_path / "cinds.txt"
+    env = dict(os.environ, RDFIND_DIST_BACKEND="gloo")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "rdfind_amd", "-dop", "2", *flags, "--support", str(ms), "--output",
+                        f"file://{out}", os.path.join(GOLDEN, f"{name}.nt.gz")], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert sorted(out.read_text().splitlines()) == expected
+    assert not list(tmp_path.glob("cinds.txt.part*"))

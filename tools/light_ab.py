@@ -1,0 +1,34 @@
+"""A/B of light-kernel variants (dev tool): python tools/light_ab.py <cfg:scale>... ; each variant library
+(RDFIND_AB_LIBS, comma-separated .so names under rdfind_amd/) runs in its own process."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+if len(sys.argv) > 1 and sys.argv[1] == "--child":
+    sys.path.insert(0, ROOT)
+    from rdfind_amd import _lib, synth
+    out = {}
+    for spec in sys.argv[2:]:
+        cfg, sc = spec.split(":")
+        d = synth.config(cfg, float(sc))
+        with _lib.Context(0) as ctx:
+            ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+            best = None
+            for _ in range(3):
+                cs = ctx.run(d.min_support)
+                kt = ctx.kernel_times()
+                best = kt if best is None or kt["light"] < best["light"] else best
+            out[spec] = {"light": round(best["light"], 3), "pivot": round(best["pivot"], 3),
+                         "total": round(sum(best.values()), 3), "n": ctx.cind_count(), "sum": ctx.checksum()}
+    print("AB", json.dumps(out), flush=True)
+    sys.exit(0)
+
+for lib in os.environ.get("RDFIND_AB_LIBS", "librdfind_hip.so").split(","):
+    env = dict(os.environ, RDFIND_HIP_LIB=os.path.join(ROOT, "rdfind_amd", lib))
+    r = subprocess.run([sys.executable, __file__, "--child"] + sys.argv[1:], env=env, capture_output=True, text=True,
+                       timeout=900)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("AB")]
+    print(lib, line[0][3:] if line else r.stderr[-2000:], flush=True)
