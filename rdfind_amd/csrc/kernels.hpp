@@ -68,6 +68,8 @@ struct CindView {
     const u64* ebin;      // first explicit pair of a dep whose ref is binary
     int literal;          // strategy-0 Condition.isImpliedBy quirk
     int mode;             // RuleMode
+    const u64* vcoff;     // sharded verify pass: dependent -> offsets [C+1] into vpairs (null: pivot candidates)
+    const u64* vpairs;    // (dep << 32 | candidate) pairs sorted, the global pivot holder's survivors to verify
     int ar;               // ArMode (--use-ars)
     const u32* arref;     // unary compact id -> the ref its association rule implies, or NONE32 [Cu]
 };

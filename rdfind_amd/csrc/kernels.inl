@@ -946,6 +946,10 @@ __device__ inline u64 group_pos(const CindView& v, u32 g, u32 x) {
 
 // candidate filter: the i-th member of the pivot group (or NONE)
 __device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 i) {
+    if (v.vcoff) {  // sharded verify pass: the candidates are given (already filtered by the pivot holder)
+        const u64 idx = v.vcoff[d] + i;
+        return idx < v.vcoff[d + 1] ? (u32)v.vpairs[idx] : NONE32;
+    }
     const u64 gb = v.goff[piv], ge = v.goff[piv + 1];
     const u64 idx = gb + i;
     if (idx >= ge) return NONE32;
@@ -1866,15 +1870,64 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __rest
     }
 }
 
-// SUM-allreduce word of the local light-group count: nlight | (nlight > 0) << 40
-__global__ __launch_bounds__(RDF_BLOCK) void k_shard_light_words(const u32* __restrict__ nl, u32 C, u64* out) {
-    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
+// SUM-allreduce words of the local light groups: [d] = nlight | (nlight > 0) << 40, [C + d] = this rank's bit when
+// it holds a light group of d (bits of different ranks are disjoint: the sum is the rank mask)
+__global__ __launch_bounds__(RDF_BLOCK) void k_shard_light_words(const u32* __restrict__ nl, u32 C, u32 rank, u64* out) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
         out[d] = (u64)nl[d] | ((u64)(nl[d] != 0) << 40);
+        out[C + d] = nl[d] ? 1ull << rank : 0ull;
+    }
 }
 
-// pivot final, sharded: the pivot is the rank-local smallest group; light dependents verify their local
-// light groups; a heavy-only dependent (no light group on any rank) is handled by the rank holding its
-// globally smallest group.  nrl[d] = ranks holding a light group of d.
+// Holder-first light exchange (sharded): the rank holding d's globally smallest group (the pivot holder) checks
+// its candidates against its own light groups; each survivor goes to d's owner as the holder's report (tag 0)
+// and to every other rank holding a light group of d for verification (tag 1).  Output word:
+// dest << 58 | tag << (32 + cb) | dep << 32 | ref, so one 8-bit radix pass on bits 58.. groups by destination and
+// a sort on the low 33 + cb bits puts the reports before the (dep, ref)-ordered verify pairs.
+template <bool WRITE>
+__global__ __launch_bounds__(RDF_BLOCK) void k_route_survivors(const u64* __restrict__ pairs, u64 n,
+                                                               const u64* __restrict__ lmask, u32 rank, u32 nranks, int cb,
+                                                               u32* cnt, const u64* __restrict__ pos, u64* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 pr = pairs[i];
+        const u32 d = (u32)(pr >> 32);
+        const u64 others = lmask[d] & ~(1ull << rank);
+        if (!WRITE) {
+            cnt[i] = 1u + (u32)__popcll(others);
+            continue;
+        }
+        u64 o = pos[i];
+        out[o++] = ((u64)(d % nranks) << 58) | pr;
+        for (u64 m = others; m; m &= m - 1) {
+            const u64 r = (u64)(__ffsll((long long)m) - 1);
+            out[o++] = (r << 58) | (1ull << (32 + cb)) | pr;
+        }
+    }
+}
+
+// destination bounds of the dest-sorted words (dest in bits 58..63), then the destination bits cleared
+__global__ __launch_bounds__(RDF_BLOCK) void k_dest_bounds(const u64* __restrict__ words, u64 n, u32 nranks, u64* bounds) {
+    for (u64 r = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; r <= nranks; r += (u64)gridDim.x * RDF_BLOCK)
+        bounds[r] = lower_bound_u64(words, n, r << 58);
+}
+__global__ void k_lower_bound1(const u64* __restrict__ words, u64 n, u64 key, u64* out) { *out = lower_bound_u64(words, n, key); }
+__global__ __launch_bounds__(RDF_BLOCK) void k_clear_bits(u64* words, u64 n, u64 mask) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) words[i] &= ~mask;
+}
+
+// verify pass plan: candidates = the verify pairs of d, groups = all local light groups of d (no pivot skipped)
+__global__ __launch_bounds__(RDF_BLOCK) void k_verify_plan(CindView v, const u32* __restrict__ nlight_in, u32* nchunk_light,
+                                                           u32* nitem_light, u32* npacked) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 sz = v.vcoff[d + 1] - v.vcoff[d];
+        light_plan(v, (u32)d, sz ? nlight_in[d] : 0u, sz, nchunk_light, nitem_light, npacked);
+    }
+}
+
+// pivot final, sharded: the rank holding d's globally smallest group (the holder) takes its candidates from that
+// group and checks its own light groups; the other ranks with light groups of d verify the holder's survivors
+// (k_route_survivors, then a verify pass); a heavy-only dependent (no light group on any rank) is handled by the
+// holder alone.  nrl[d] = ranks holding a light group of d.
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, const u64* __restrict__ best_in,
                                                                  const u32* __restrict__ nlight_in,
                                                                  const u64* __restrict__ gbest, const u64* __restrict__ glight,
@@ -1893,8 +1946,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
             const u64 sz = best == ~0ull ? 0 : best >> 32;
             const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
             pivot[d] = (u32)(best & 0xffffffffu);
-            light_plan(v, (u32)d, nlight, sz, nchunk_light, nitem_light, npacked);
-            if (nlight && nchunk_light[d]) {
+            // only the pivot holder generates light candidates (holder-first exchange, k_route_survivors)
+            light_plan(v, (u32)d, holder ? nlight : 0u, sz, nchunk_light, nitem_light, npacked);
+            if (holder && nlight && nchunk_light[d]) {
                 lc = (u32)sz;
                 le = (u32)(v.doff[d + 1] - v.doff[d]);
             }

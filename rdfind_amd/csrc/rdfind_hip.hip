@@ -99,6 +99,8 @@ struct rdf_ctx {
     DevBuf item_dep, eblk, lslot, npk, pkoff, pk_dep, nmch, mchoff, mch_dep;
     DevBuf uhist, urecs, usl, cntg, fstage, bfreq, boff, fbits, brkeys;  // partitioned K1 / K2 (counts.inl)
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
+    DevBuf lmask, hrep, vpairs, vcoff, vpiv;  // holder-first light exchange (sh_phase5 / sh_phase15)
+    u64 n_hrep = 0;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
     bool h_runs_valid = false;  // host mirror of the run table (filled on the first copy)
@@ -252,7 +254,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
-                      &c->obounds, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
+                      &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
             &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref};
 }
@@ -1274,6 +1276,8 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.ebin = nullptr;
     v.literal = (flags & RDF_STRATEGY_ALL_AT_ONCE) ? 1 : 0;
     v.mode = (flags & RDF_CLEAN_IMPLIED) ? RULES_CLEAN : (v.literal ? RULES_NONE : RULES_S2L_RAW);
+    v.vcoff = nullptr;
+    v.vpairs = nullptr;
     v.ar = c->ar_on && c->nranks == 1 ? (v.literal ? AR_S0 : AR_S2L) : AR_NONE;
     v.arref = c->arref.as<u32>();
     return v;
@@ -1342,7 +1346,7 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
 
 // light dependents -> explicit raw (dep << 32 | ref) pairs in epairs, in (dep, ref) order; *E = count.
 // Output slots are octets (8 pivot candidates each): WL of them; WI k_light work items, WP packed octets.
-static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP, u64* E) {
+static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP, u64* E, const u32* pivot) {
     hipStream_t st = c->stream;
     const u64 nslot = std::max<u64>(WL, 1);
     ENSURE(c, epairs_tmp, nslot * 8 * 8);
@@ -1361,11 +1365,11 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
                            c->C, c->pk_dep.as<u32>());
     if (WP)
         hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), v,
-                           c->pivot.as<u32>(), c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
+                           pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
                            c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     if (WI)
         hipLaunchKernelGGL(k_light, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
-                           0, st, (u64)wave_blocks(WI), v, c->pivot.as<u32>(), c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
+                           0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
                            c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     // chunks of dependents whose groups span several segments: emitted once all their segments are done
     u64 WM = 0;
@@ -1382,7 +1386,7 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->mchoff.as<u64>(),
                            c->C, c->mch_dep.as<u32>());
         hipLaunchKernelGGL(k_light_mseg_emit, dim3(vgrid(wave_blocks(WM))),
-                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, c->pivot.as<u32>(), c->mchoff.as<u64>(), c->mch_dep.as<u32>(), WM,
+                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, pivot, c->mchoff.as<u64>(), c->mch_dep.as<u32>(), WM,
                            c->choffl.as<u64>(), c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     }
     ENSURE(c, pos, (WL + 1) * 8);
@@ -1701,7 +1705,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     tend(c, RDF_T_PIVOT);
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0, H = 0, HC = 0, NT = 0;
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
-    TRY(d_light(c, v, WI, WL, WP, &E));
+    TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));
@@ -1948,11 +1952,12 @@ static rdf_status sh_phase3(rdf_ctx* c, rdf_exchange* req) {
 static rdf_status sh_phase4(rdf_ctx* c, rdf_exchange* req) {
     ENSURE(c, gbest, std::max<u64>(c->C, 1) * 8);
     HIP_TRY(c, hipMemcpyAsync(c->gbest.p, c->xrecv.p, (u64)c->C * 8, hipMemcpyDeviceToDevice, c->stream));
+    ENSURE(c, xsend, std::max<u64>(2ull * c->C, 1) * 8);
     if (c->C)
         hipLaunchKernelGGL(k_shard_light_words, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
-                           c->pnl.as<u32>(), c->C, c->xsend.as<u64>());
+                           c->pnl.as<u32>(), c->C, c->rank, c->xsend.as<u64>());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U64, c->xsend.p, c->C, 5);
+    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U64, c->xsend.p, 2ull * c->C, 5);
 }
 
 static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
@@ -1975,10 +1980,55 @@ static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0;
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
     c->sh_WH = WH;
-    TRY(d_light(c, v, WI, WL, WP, &E));
+    TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
-    // group the local survivors by owner rank (dep % R): pack, sort, find bounds, unpack
+    // holder-first exchange: every survivor to d's owner (report) and to the other ranks holding light groups of d
+    // (verify), grouped by destination
+    const int cb = bits_for(C ? C - 1 : 0);
+    if (33 + cb > 58) return fail(c, RDF_ERR_LIMIT, "sharded mode: too many captures for the routing key");
+    ENSURE(c, lmask, std::max<u64>(C, 1) * 8);
+    HIP_TRY(c, hipMemcpyAsync(c->lmask.p, c->xrecv.as<u64>() + C, (u64)C * 8, hipMemcpyDeviceToDevice, st));
+    ENSURE(c, flags, std::max<u64>(E, 1) * 4);
+    ENSURE(c, pos, (E + 1) * 8);
+    tbegin(c, RDF_T_ESORT);
+    if (E)
+        hipLaunchKernelGGL((k_route_survivors<false>), dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->epairs.as<u64>(), E, c->lmask.as<u64>(), c->rank, R, cb, c->flags.as<u32>(), (const u64*)nullptr,
+                           (u64*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), E, c->pos.as<u64>() + E, st));
+    u64 T = 0;
+    TRY(read_u64(c, c->pos.as<u64>() + E, &T));
+    ENSURE(c, cpairs, std::max<u64>(T, 1) * 8);
+    ENSURE(c, cpairs_tmp, std::max<u64>(T, 1) * 8);
+    if (E)
+        hipLaunchKernelGGL((k_route_survivors<true>), dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->epairs.as<u64>(), E, c->lmask.as<u64>(), c->rank, R, cb, (u32*)nullptr, c->pos.as<u64>(),
+                           c->cpairs.as<u64>());
+    if (T) {
+        u64* k = c->cpairs.as<u64>();
+        u64* t = c->cpairs_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64_bits(c->ws, k, t, T, 58, 64, st));
+        if (k != c->cpairs.as<u64>()) std::swap(c->cpairs, c->cpairs_tmp);
+    }
+    ENSURE(c, obounds, (RDF_MAX_RANKS + 1) * 8);
+    hipLaunchKernelGGL(k_dest_bounds, dim3(1), dim3(RDF_BLOCK), 0, st, c->cpairs.as<u64>(), T, R, c->obounds.as<u64>());
+    if (T)
+        hipLaunchKernelGGL(k_clear_bits, dim3(grid_for(T, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cpairs.as<u64>(), T,
+                           63ull << 58);
+    tend(c, RDF_T_ESORT);
+    std::vector<u64> bounds(R + 1);
+    HIP_TRY(c, hipMemcpyAsync(bounds.data(), c->obounds.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->cpairs.p, T, 15));
+    for (u32 r = 0; r < R; ++r) req->send_counts[r] = bounds[r + 1] - bounds[r];
+    return RDF_OK;
+}
+
+// (dep << 32 | ref) pairs epairs[0, E) -> grouped by owner rank (dep % R) for an all-to-all to next_phase
+static rdf_status sh_to_owners(rdf_ctx* c, rdf_exchange* req, u64 E, int next_phase) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C, R = c->nranks;
     const int cb = bits_for(C ? C - 1 : 0);
     const int ob = bits_for(R);
     if (2 * cb + ob > 64) return fail(c, RDF_ERR_LIMIT, "sharded mode: too many captures for the owner sort key");
@@ -1998,18 +2048,79 @@ static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
     std::vector<u64> bounds(R + 1);
     HIP_TRY(c, hipMemcpyAsync(bounds.data(), c->obounds.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->epairs.p, E, 6));
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->epairs.p, E, next_phase));
     for (u32 r = 0; r < R; ++r) req->send_counts[r] = bounds[r + 1] - bounds[r];
     return RDF_OK;
 }
 
-static rdf_status sh_phase6(rdf_ctx* c, rdf_exchange* req) {
+// received holder words: reports for the dependents this rank owns (kept for phase 6) and verify pairs, checked
+// against this rank's light groups of the dependent (the light kernels with the given candidates and no pivot);
+// the survivors go to the owners as this rank's reports
+static rdf_status sh_phase15(rdf_ctx* c, rdf_exchange* req) {
     hipStream_t st = c->stream;
     const u64 n = c->x_recv_count;
     const u32 C = c->C;
+    const int cb = bits_for(C ? C - 1 : 0);
+    ENSURE(c, cpairs, std::max<u64>(n, 1) * 8);
+    ENSURE(c, cpairs_tmp, std::max<u64>(n, 1) * 8);
+    HIP_TRY(c, hipMemcpyAsync(c->cpairs.p, c->xrecv.p, n * 8, hipMemcpyDeviceToDevice, st));
+    tbegin(c, RDF_T_ESORT);
+    if (n) {
+        u64* k = c->cpairs.as<u64>();
+        u64* t = c->cpairs_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, n, 33 + cb, st));
+        if (k != c->cpairs.as<u64>()) std::swap(c->cpairs, c->cpairs_tmp);
+    }
+    ENSURE(c, obounds, (RDF_MAX_RANKS + 1) * 8);
+    // split point = first word with the verify tag: k_dest_bounds on the words shifted ... one lower bound
+    hipLaunchKernelGGL(k_lower_bound1, dim3(1), dim3(1), 0, st, c->cpairs.as<u64>(), n, 1ull << (32 + cb),
+                       c->obounds.as<u64>());
+    u64 nh = 0;
+    TRY(read_u64(c, c->obounds.as<u64>(), &nh));
+    const u64 nv = n - nh;
+    c->n_hrep = nh;
+    ENSURE(c, hrep, std::max<u64>(nh, 1) * 8);
+    ENSURE(c, vpairs, std::max<u64>(nv, 1) * 8);
+    if (nh) HIP_TRY(c, hipMemcpyAsync(c->hrep.p, c->cpairs.p, nh * 8, hipMemcpyDeviceToDevice, st));
+    if (nv) {
+        HIP_TRY(c, hipMemcpyAsync(c->vpairs.p, c->cpairs.as<u64>() + nh, nv * 8, hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_clear_bits, dim3(grid_for(nv, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->vpairs.as<u64>(), nv,
+                           1ull << (32 + cb));
+    }
+    ENSURE(c, vcoff, (C + 1ull) * 8);
+    ENSURE(c, ebin, std::max<u64>(C, 1) * 8);
+    hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->vpairs.as<u64>(), nv, C, c->Cu, c->vcoff.as<u64>(), c->ebin.as<u64>());
+    tend(c, RDF_T_ESORT);
+    CindView v = make_view(c, c->sh_flags);
+    v.vcoff = c->vcoff.as<u64>();
+    v.vpairs = c->vpairs.as<u64>();
+    ENSURE(c, vpiv, std::max<u64>(C, 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->vpiv.p, 0xff, std::max<u64>(C, 1) * 4, st));  // no pivot group to skip
+    tbegin(c, RDF_T_LIGHT);
+    if (C)
+        hipLaunchKernelGGL(k_verify_plan, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->pnl.as<u32>(),
+                           c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>());
+    tend(c, RDF_T_LIGHT);
+    const u64 hc = c->heavy_candidates, lc = c->light_candidates, le = c->light_entries;
+    u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0;
+    TRY(d_chunks(c, &WL, &WH, &WI, &WP));
+    c->heavy_candidates = hc;
+    c->light_candidates = lc;
+    c->light_entries = le;
+    TRY(d_light(c, v, WI, WL, WP, &E, c->vpiv.as<u32>()));
+    c->n_light_chunks += WL;
+    return sh_to_owners(c, req, E, 6);
+}
+
+static rdf_status sh_phase6(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 n6 = c->x_recv_count, nh = c->n_hrep, n = n6 + nh;  // verifiers' reports + the holders' reports
+    const u32 C = c->C;
     ENSURE(c, epairs, std::max<u64>(n, 1) * 8);
     ENSURE(c, epairs_tmp, std::max<u64>(n, 1) * 8);
-    HIP_TRY(c, hipMemcpyAsync(c->epairs.p, c->xrecv.p, n * 8, hipMemcpyDeviceToDevice, st));
+    if (n6) HIP_TRY(c, hipMemcpyAsync(c->epairs.p, c->xrecv.p, n6 * 8, hipMemcpyDeviceToDevice, st));
+    if (nh) HIP_TRY(c, hipMemcpyAsync(c->epairs.as<u64>() + n6, c->hrep.p, nh * 8, hipMemcpyDeviceToDevice, st));
     tbegin(c, RDF_T_ESORT);
     {
         u64* k = c->epairs.as<u64>();
@@ -2165,7 +2276,7 @@ static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
 // phases: 10-14 (condition counts, routing of the triples), then 1-8; pending = a phase that follows a collective
 static bool sh_phase_valid(int ph, bool pending) {
     if (ph >= 1 && ph <= 8) return true;
-    if (ph >= 11 && ph <= 14) return true;
+    if (ph >= 11 && ph <= 15) return true;
     return !pending && ph == 10;
 }
 
@@ -2202,6 +2313,7 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
         case 3: r = sh_phase3(c, req); break;
         case 4: r = sh_phase4(c, req); break;
         case 5: r = sh_phase5(c, req); break;
+        case 15: r = sh_phase15(c, req); break;
         case 6: r = sh_phase6(c, req); break;
         case 7: r = sh_phase7(c, req); break;
         case 8: r = sh_phase8(c, req); break;

@@ -12,13 +12,18 @@ the library requests one at a time (``rdf_shard_step``):
   2. all-gather       group-size histograms -> global heavy threshold + this rank's heavy bit base
   3. all-reduce(sum)  heavy-group bitmasks (bits of different ranks are disjoint, so sum == or)
   4. all-reduce(min)  (pivot size, rank) per dependent
-  5. all-reduce(sum)  light-group counts and the number of ranks holding light groups per dependent
-  6. all-to-all       local survivors (dep, ref) of light dependents -> the dependent's owner (dep % R);
-                      the owner keeps a ref iff every rank with a light group of dep reported it.  This is
-                      the reference's combiner-side intersection (AllAtOnceTraversalStrategy.scala:62-65)
-                      followed by the shuffle to the IntersectCindCandidates reducer.
-  7. all-gather       the final explicit CIND pairs (the minimality rules R1-R4 probe other dependents)
-  8. all-gather       filtered ref lists of the bitmask classes pivoted on each rank
+  5. all-reduce(sum)  light-group counts, the number of ranks holding light groups per dependent and their
+                      rank mask
+  6. all-to-all       holder-first light exchange: only the rank holding d's globally smallest group (the pivot
+                      holder) draws candidates from it and checks its own light groups; each survivor (dep, ref)
+                      goes to the owner (dep % R) as the holder's report and to every other rank with a light
+                      group of dep for verification
+  7. all-to-all       the verified survivors -> the owner, which keeps a ref iff every rank with a light group of
+                      dep reported it.  Together this is the reference's combiner-side intersection
+                      (AllAtOnceTraversalStrategy.scala:62-65) and the shuffle to the IntersectCindCandidates
+                      reducer, with candidate generation done once per dependent instead of once per rank.
+  8. all-gather       the final explicit CIND pairs (the minimality rules R1-R4 probe other dependents)
+  9. all-gather       filtered ref lists of the bitmask classes pivoted on each rank
 
 Each rank then emits the CINDs of its own dependents; the union over ranks is the single-GPU result.
 

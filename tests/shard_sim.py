@@ -196,28 +196,47 @@ class ShardSim:
 
     def _phase4(self):
         self.gbest = self.recv.copy()
-        words = np.array([len(gs) | ((1 if gs else 0) << 40) for gs in self.dep_groups], np.int64)
-        return self._req(_lib.X_ALLREDUCE_SUM_U64, words, 5)
+        words = [len(gs) | ((1 if gs else 0) << 40) for gs in self.dep_groups]
+        words += [(1 << self.rank) if gs else 0 for gs in self.dep_groups]
+        return self._req(_lib.X_ALLREDUCE_SUM_U64, np.array([_i64(w) for w in words], np.int64), 5)
 
     def _excluded(self, d, r):
         dc, rc = self.freq[d], self.freq[r]
         return dc.implies(rc) if self.strategy == 0 else R.trivially_implied(dc, rc)
 
-    def _phase5(self):
-        self.nrl = (self.recv >> 40).astype(np.int64)
+    def _phase5(self):  # holder-first: the pivot holder's survivors -> owner (report) + other light ranks (verify)
+        C = len(self.freq)
+        self.nrl = (self.recv[:C] >> 40).astype(np.int64)
+        lmask = [int(x) & ((1 << 64) - 1) for x in self.recv[C:].tolist()]
         out = [[] for _ in range(self.R)]
         for d, gs in enumerate(self.dep_groups):
-            if not gs:
+            if not gs or (int(self.gbest[d]) & 0xFFFFFFFF) != self.rank:
                 continue
             refs = set.intersection(*(set(g) for g in gs))
             for r in sorted(refs):
                 if r != d and not self._excluded(d, r):
+                    out[d % self.R].append((0, d, r))
+                    for q in range(self.R):
+                        if q != self.rank and (lmask[d] >> q) & 1:
+                            out[q].append((1, d, r))
+        send = np.array([(t << 63) | (d << 32) | r for part in out for t, d, r in part], np.uint64).view(np.int64)
+        return self._req(_lib.X_ALLTOALLV_U64, send, 15, [len(p) for p in out])
+
+    def _phase15(self):  # keep the reports; verify the other pairs against the local light groups -> owners
+        words = self.recv.view(np.uint64).tolist()
+        self.reports = [w for w in words if not w >> 63]
+        out = [[] for _ in range(self.R)]
+        for w in words:
+            if w >> 63:
+                d, r = (w >> 32) & 0x7FFFFFFF, w & 0xFFFFFFFF
+                if all(r in g for g in self.dep_groups[d]):
                     out[d % self.R].append((d << 32) | r)
         send = np.array([x for part in out for x in part], np.int64)
         return self._req(_lib.X_ALLTOALLV_U64, send, 6, [len(p) for p in out])
 
     def _phase6(self):
-        vals, cnt = np.unique(self.recv, return_counts=True)
+        allr = np.concatenate([self.recv.astype(np.int64), np.array(self.reports, np.int64)])
+        vals, cnt = np.unique(allr, return_counts=True)
         keep = [int(v) for v, c in zip(vals.tolist(), cnt.tolist()) if c == self.nrl[int(v) >> 32]]
         return self._req(_lib.X_ALLGATHERV_U64, np.array(keep, np.int64), 7)
 
