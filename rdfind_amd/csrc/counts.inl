@@ -23,9 +23,13 @@ static constexpr u32 FR_R = 1u << FR_BITS;
 static constexpr u32 U2_MAXB = 32768;          // K1 buckets (128 KB of LDS in the histogram passes)
 static constexpr u64 U2_SLICE = 1ull << 18;    // K1 records per counting block
 static constexpr int U2_CBLOCK = 1024;         // threads of a counting block
-static constexpr int B2_MAXBITS = 13;          // K2 buckets <= 8192 (32 KB of LDS in the histogram passes)
+#ifndef RDF_B2_MAXBITS
+#define RDF_B2_MAXBITS 15
+#endif
+static constexpr int B2_MAXBITS = RDF_B2_MAXBITS;  // K2 buckets <= 2^B2_MAXBITS (4 B of LDS each in the histogram passes)
 static constexpr int B2_SLOTS = 4096;          // LDS hash slots of a K2 counting block (48 KB: 3 blocks per CU)
-static constexpr u64 B2_TARGET = 1024;         // target K2 records per bucket (sizes the bucket count)
+static constexpr u64 B2_BIG = 64ull << 20;     // above 3n = 64M keys, one more bucket bit per doubling (fewer
+                                               // multi-slice buckets, which go to the spill table)
 static constexpr int B2_PBLOCK = 1024;         // threads of a K2 histogram / scatter block
 
 // global rank of unary condition i (= pos * V + value) among all frequent conditions, or NONE

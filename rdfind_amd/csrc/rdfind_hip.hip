@@ -742,10 +742,13 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
                                  u64* nkeys, u64* S) {
     hipStream_t st = c->stream;
     const u32 V = c->V ? c->V : 1;
+    // 2^13 buckets up to 3n = 64M keys (c2: 0.97 ms; 2^14: 1.16, 2^15: 1.46), then one bit per doubling up to
+    // 2^15 (c3 at half scale, 132M keys: 7.6 ms at 2^13, 3.9 ms at 2^15: its buckets no longer spill)
     int bits = 1;
-    while (bits < B2_MAXBITS && (1ull << bits) * B2_TARGET < 3 * n) ++bits;
+    while (bits < 13 && (1ull << bits) * 1024 < 3 * n) ++bits;
+    while (bits >= 13 && bits < B2_MAXBITS && 3 * n > (B2_BIG << (bits - 13))) ++bits;
     const u32 NB2 = 1u << bits;
-    const unsigned G2 = (unsigned)std::max<u64>(1, std::min<u64>({512, (n + 4095) / 4096, (1ull << 22) / NB2}));
+    const unsigned G2 = (unsigned)std::max<u64>(1, std::min<u64>({512, (n + 4095) / 4096, (1ull << 24) / NB2}));
     const u64 nh = (u64)NB2 * G2;
     const u64 maxrec = std::max<u64>(3 * n, 1);
     ENSURE(c, uhist, (nh + 1) * 4);
