@@ -17,6 +17,14 @@ static constexpr u64 LIGHT_SEG = RDF_LIGHT_SEG;  // groups of one dependent veri
 #define RDF_LIGHT_IT 4
 #endif
 static constexpr int LIGHT_IT = RDF_LIGHT_IT;  // groups per lane whose metadata is loaded together
+#ifndef RDF_SIG_W
+#define RDF_SIG_W 4
+#endif
+// Light-group signatures: bit h(g) of a 64*SIG_W-bit word set for every light group g of a capture.  G(d) <= G(c)
+// implies sig(d) <= sig(c), so a candidate whose signature misses a bit of the dependent's is not a ref; this kills
+// most doomed candidates before any group search (the heavy groups are exact bits of hmask already).
+static constexpr int SIG_W = RDF_SIG_W;
+static constexpr int SIG_LOG = SIG_W == 8 ? 9 : SIG_W == 4 ? 8 : SIG_W == 2 ? 7 : 6;
 static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
 #ifndef RDF_PACK_MAXG2
 #define RDF_PACK_MAXG2 512
@@ -72,6 +80,7 @@ struct CindView {
     const u64* vpairs;    // (dep << 32 | candidate) pairs sorted, the global pivot holder's survivors to verify
     int ar;               // ArMode (--use-ars)
     const u32* arref;     // unary compact id -> the ref its association rule implies, or NONE32 [Cu]
+    const u64* sig;       // light-group signature of each capture, SIG_W words (null: no signature test)
 };
 
 }  // namespace rdf

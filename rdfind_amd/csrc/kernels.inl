@@ -707,6 +707,13 @@ __device__ inline u32 find_dep(const u64* chunk_off, u32 C, u64 w) {
 
 static constexpr u64 PIVOT_SHORT = 32;  // dependents with at most this many groups: one lane each
 
+__device__ inline u32 sig_bit(u32 g) { return (g * 0x9E3779B1u) >> (32 - SIG_LOG); }
+__device__ inline void sig_add(u64 (&sg)[SIG_W], u32 g) {
+    const u32 h = sig_bit(g);
+#pragma unroll
+    for (int k = 0; k < SIG_W; ++k) sg[k] |= (h >> 6) == (u32)k ? 1ull << (h & 63) : 0ull;
+}
+
 // segments of the long dependents (the short ones are done lane-per-dependent by k_pivot_short)
 // owner[w] = d for every work item w in [off[d], off[d+1]) (replaces a binary search per work item)
 __global__ __launch_bounds__(RDF_BLOCK) void k_expand_owner(const u64* __restrict__ off, u32 C, u32* owner) {
@@ -723,27 +730,33 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_nseg(const u64* __restrict_
 
 // The pivot pass visits every (dependent, group) entry once and tags the entries of heavy groups in place
 // (DGRP_HEAVY): the light kernels then skip them without a per-group gather of hbit.
-__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp_tag, u64* best_out, u32* nlight_out) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp_tag, u64* best_out, u32* nlight_out,
+                                                           u64* sig) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = v.doff[d], e = v.doff[d + 1];
         if (e - b > PIVOT_SHORT) continue;
         u64 best = ~0ull;
         u32 nlight = 0;
+        u64 sg[SIG_W] = {};
         for (u64 j = b; j < e; ++j) {
             const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
             const u64 key = ((v.goff[g + 1] - v.goff[g]) << 32) | g;
             best = key < best ? key : best;
             const bool light = v.hbit[g] == LIGHT;
             nlight += light;
+            if (light) sig_add(sg, g);
             dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
         }
         best_out[d] = best;
         nlight_out[d] = nlight;
+        if (sig)
+#pragma unroll
+            for (int k = 0; k < SIG_W; ++k) sig[d * SIG_W + k] = sg[k];
     }
 }
 
 __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
-                                        u64* best_out, u32* nlight_out) {
+                                        u64* best_out, u32* nlight_out, u64* sig) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -753,6 +766,7 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
     const u64 e = b + PIVOT_SEG < e0 ? b + PIVOT_SEG : e0;
     u64 best = ~0ull;  // (size << 32 | group)
     u32 nlight = 0;
+    u64 sg[SIG_W] = {};
     for (u64 j = b + lane; j < e; j += RDF_WAVE) {
         const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
         const u64 sz = v.goff[g + 1] - v.goff[g];
@@ -760,16 +774,20 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
         best = key < best ? key : best;
         const bool light = v.hbit[g] == LIGHT;
         nlight += light;
+        if (light) sig_add(sg, g);
         dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         u64 o = __shfl_xor(best, off, RDF_WAVE);
         best = o < best ? o : best;
+#pragma unroll
+        for (int k = 0; k < SIG_W; ++k) sg[k] |= __shfl_xor(sg[k], off, RDF_WAVE);
     }
     nlight = wave_sum(nlight);
+    const bool single = e0 - b0 <= PIVOT_SEG;
     if (lane == 0) {
-        if (e0 - b0 <= PIVOT_SEG) {
+        if (single) {
             best_out[d] = best;
             nlight_out[d] = nlight;
         } else {
@@ -777,12 +795,19 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
             atomicAdd(&nlight_out[d], nlight);
         }
     }
+    if (sig && lane < SIG_W) {  // lane k writes word k (zeroed beforehand for the multi-segment dependents)
+        u64 x = 0;
+#pragma unroll
+        for (int k = 0; k < SIG_W; ++k) x = lane == k ? sg[k] : x;
+        if (single) sig[(u64)d * SIG_W + lane] = x;
+        else if (x) atomicOr((unsigned long long*)&sig[(u64)d * SIG_W + lane], (unsigned long long)x);
+    }
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(u64 nvblk, CindView v, u32* dgrp_tag,
                                                          const u64* __restrict__ segoff, u64 W, u64* best_out,
-                                                         u32* nlight_out) {
+                                                         u32* nlight_out, u64* sig) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out);
+        k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out, sig);
     }
 }
 
@@ -958,6 +983,14 @@ __device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& i
     const CapInfo ir = v.info[r];
     if (ir.support < id.support) return NONE32;
     if ((ir.hmask & id.hmask) != id.hmask) return NONE32;
+    if (v.sig && !(id.meta & META_HEAVY_ONLY)) {  // light-group signature containment (dependent's words: uniform loads)
+        const u64* sd = v.sig + (u64)d * SIG_W;
+        const u64* sr = v.sig + (u64)r * SIG_W;
+        u64 miss = 0;
+#pragma unroll
+        for (int k = 0; k < SIG_W; ++k) miss |= sd[k] & ~sr[k];
+        if (miss) return NONE32;
+    }
     if (is_trivial(v, d, r) || is_quirk(v, d, r) || ar_drop(v, d, r)) return NONE32;
     return r;
 }
@@ -1035,18 +1068,22 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(u64 nvblk, CindView 
 
 
 #ifdef RDF_LIGHT_STATS
-// dev instrumentation (make STATS=1): [0] items [1] wave iterations [2] candidate checks [3] groups visited
-// [4] sum of log2 sizes of searched groups [5] initially alive candidates [6] items with nseg > 1
-// [7] max wave cycles [8] cycles, few-groups path [9] cycles, many-groups path [10] cycles, multi-segment
-// items [11] max cycles of a multi-segment item [12] groups of multi-segment items [13] alive0 of those
-__device__ unsigned long long g_light_stats[16];
-#define LSTAT(i, v) do { if (lane_id() == 0) atomicAdd(&g_light_stats[i], (unsigned long long)(v)); } while (0)
-#define LSTAT_MAX(i, v) do { if (lane_id() == 0) atomicMax(&g_light_stats[i], (unsigned long long)(v)); } while (0)
-#define LSTAT_T0 const unsigned long long lstat_t0 = clock64()
+// dev instrumentation (make stats): one 16 x u32 record per k_light work item, written by lane 0 without atomics:
+// [0] dep [1] groups of the dependent [2] groups of this segment [3] nseg [4] pivot size [5] alive0 [6] alive at exit
+// [7] 64-group windows visited [8] groups taken by the serial path [9] batch rounds [10] sum of batch search depths
+// [11] light groups in visited windows [12..13] clock64 cycles [14] sum of visited light group sizes [15] largest
+__device__ u32* g_item_rec;
+#define LSTAT_T0 const unsigned long long lstat_t0 = clock64(); u32 ls_win = 0, ls_ser = 0, ls_bat = 0, ls_dep = 0, ls_lg = 0, ls_gs = 0, ls_gmax = 0
+#define LSTAT_WIN(lmask, gsz) do { ++ls_win; ls_lg += __popcll(lmask); ls_gs += wave_sum((u32)(gsz)); \
+    u32 m_ = (u32)(gsz); for (int o_ = 32; o_ >= 1; o_ >>= 1) { u32 t_ = __shfl_xor(m_, o_, RDF_WAVE); m_ = t_ > m_ ? t_ : m_; } \
+    ls_gmax = m_ > ls_gmax ? m_ : ls_gmax; } while (0)
+#define LSTAT_SER(k) (ls_ser += (k))
+#define LSTAT_BAT(depth) do { ++ls_bat; ls_dep += (depth); } while (0)
 #else
-#define LSTAT(i, v) do { } while (0)
-#define LSTAT_MAX(i, v) do { } while (0)
 #define LSTAT_T0 do { } while (0)
+#define LSTAT_WIN(lmask, gsz) do { } while (0)
+#define LSTAT_SER(k) do { } while (0)
+#define LSTAT_BAT(depth) do { } while (0)
 #endif
 
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
@@ -1072,9 +1109,6 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const u64 b = b0 + seg * LIGHT_SEG;
     const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
     LSTAT_T0;
-    LSTAT(0, 1);
-    LSTAT(5, __popcll(alive0));
-    LSTAT(6, nseg > 1);
     // Lanes take one group each (LIGHT_IT per lane); dependents with few groups went to k_light_packed, so
     // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
     // independent gathers per level, so the serial chain is three round trips per segment, not per 64 groups.
@@ -1105,13 +1139,9 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             // a multi-segment item drops the candidates other segments have already killed
             if (nseg > 1 && (it || s0 != b)) alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (!alive) break;
-#ifdef RDF_LIGHT_STATS
-            LSTAT(1, 1);
-            LSTAT(2, __popcll(alive));
-            LSTAT(3, __popcll(__ballot(gg[it] != NONE32)));
-#endif
             const u32 g = gg[it];
             const u64 lm = __ballot(g != NONE32);  // light groups of this window
+            LSTAT_WIN(lm, gszv[it]);
             if (__popcll(lm) <= LIGHT_SERIAL) {
                 // few light groups (the common case: most groups of a dependent are heavy and verified by the
                 // mask test): take them one at a time with the lanes over the candidates.  A group of at most
@@ -1122,6 +1152,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                 while (tg && alive) {
                     const int l = __ffsll((long long)tg) - 1;
                     tg &= tg - 1;
+                    LSTAT_SER(1);
                     const u64 gb = __shfl(gbv[it], l, RDF_WAVE);
                     const u32 gs = __shfl(gszv[it], l, RDF_WAVE);
                     const bool mine = (alive >> lane) & 1ull;
@@ -1164,6 +1195,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                     key[k] = __shfl(cand, bit[k] < 0 ? bit[0] : bit[k], RDF_WAVE);
                 }
                 bool ok[LIGHT_BATCH];
+                LSTAT_BAT(gsz ? 64 - __clzll(gsz) : 0);
                 search_batch<LIGHT_BATCH>(gm, gsz, key, ok);
 #pragma unroll
                 for (int k = 0; k < LIGHT_BATCH; ++k)
@@ -1172,16 +1204,13 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         }
     }
 #ifdef RDF_LIGHT_STATS
-    {
+    if (lane == 0 && g_item_rec) {
         const unsigned long long dt = clock64() - lstat_t0;
-        LSTAT_MAX(7, dt);
-        LSTAT(9, dt);
-        if (nseg > 1) {
-            LSTAT(10, dt);
-            LSTAT_MAX(11, dt);
-            LSTAT(12, e - b);
-            LSTAT(13, __popcll(alive0));
-        }
+        u32* r = g_item_rec + 16 * w;
+        const u32 rec[16] = {d, (u32)(e0 - b0), (u32)(e - b), (u32)nseg, (u32)(v.goff[piv + 1] - v.goff[piv]),
+                             (u32)__popcll(alive0), (u32)__popcll(alive), ls_win, ls_ser, ls_bat, ls_dep, ls_lg,
+                             (u32)dt, (u32)(dt >> 32), ls_gs, ls_gmax};
+        for (int k = 0; k < 16; ++k) r[k] = rec[k];
     }
 #endif
     const u64 oct0 = choff[d] + chunk * 8;  // first octet slot of this chunk

@@ -72,6 +72,8 @@ struct rdf_ctx {
     DevBuf ppart;           // per-block partial sums of the pivot statistics
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
+    DevBuf lsig;          // light-group signatures (SIG_W words per compact capture), computed by the pivot pass
+    bool sig_on = false;  // lsig holds this run's signatures (RDFIND_SIG=0 turns the filter off)
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
         ctiles, ctoff;
     u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
@@ -249,7 +251,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
@@ -1283,11 +1285,12 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.vpairs = nullptr;
     v.ar = c->ar_on && c->nranks == 1 ? (v.literal ? AR_S0 : AR_S2L) : AR_NONE;
     v.arref = c->arref.as<u32>();
+    v.sig = c->sig_on ? c->lsig.as<u64>() : nullptr;
     return v;
 }
 
 // local pivot statistics: pbest[d] = (size << 32 | group) of d's smallest local group, pnl[d] = local light groups
-static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
+static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     hipStream_t st = c->stream;
     const u32 C = c->C;
     HIP_TRY(c, hipEventRecord(c->ev[4], st));
@@ -1305,7 +1308,15 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
     ENSURE(c, psegoff, (C + 1ull) * 8);
     ENSURE(c, pbest, std::max<u64>(C, 1) * 8);
     ENSURE(c, pnl, std::max<u64>(C, 1) * 4);
+    static const bool sig_enabled = !getenv("RDFIND_SIG") || atoi(getenv("RDFIND_SIG")) != 0;
+    c->sig_on = sig_enabled;
+    u64* sig = nullptr;
+    if (sig_enabled) {
+        ENSURE(c, lsig, std::max<u64>(C, 1) * 8 * SIG_W);
+        sig = c->lsig.as<u64>();
+    }
     tbegin(c, RDF_T_PIVOT);
+    if (sig && C) HIP_TRY(c, hipMemsetAsync(sig, 0, (u64)C * 8 * SIG_W, st));
     if (C) {
         hipLaunchKernelGGL(k_pivot_nseg, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), C,
                            c->pseg.as<u32>());
@@ -1313,7 +1324,7 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
         HIP_TRY(c, hipMemsetAsync(c->pbest.p, 0xff, (u64)C * 8, st));
         HIP_TRY(c, hipMemsetAsync(c->pnl.p, 0, (u64)C * 4, st));
         hipLaunchKernelGGL(k_pivot_short, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->dgrp.as<u32>(),
-                           c->pbest.as<u64>(), c->pnl.as<u32>());
+                           c->pbest.as<u64>(), c->pnl.as<u32>(), sig);
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
@@ -1321,8 +1332,9 @@ static rdf_status d_pivot_local(rdf_ctx* c, const CindView& v) {
     tbegin(c, RDF_T_PIVOT);
     if (WS)
         hipLaunchKernelGGL(k_pivot_seg, dim3(vgrid(wave_blocks(WS))), dim3(RDF_BLOCK),
-                           0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>());
+                           0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>(), sig);
     tend(c, RDF_T_PIVOT);
+    v.sig = sig;  // the candidate passes of this run test the signatures
     return RDF_OK;
 }
 
@@ -1359,6 +1371,14 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, nslot * 4, st));
     ENSURE(c, item_dep, std::max<u64>(WI, 1) * 4);
     ENSURE(c, pk_dep, std::max<u64>(WP, 1) * 4);
+#ifdef RDF_LIGHT_STATS
+    u32* lrec = nullptr;
+    if (WI && getenv("RDFIND_LIGHT_DUMP")) {
+        HIP_TRY(c, hipMalloc(&lrec, WI * 64));
+        HIP_TRY(c, hipMemset(lrec, 0, WI * 64));
+        HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_item_rec), &lrec, sizeof(lrec)));
+    }
+#endif
     tbegin(c, RDF_T_LIGHT);
     if (WI)
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->itoffl.as<u64>(),
@@ -1401,16 +1421,19 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
                            c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>());
     tend(c, RDF_T_LIGHT);
 #ifdef RDF_LIGHT_STATS
-    {
-        unsigned long long h[16];
-        HIP_TRY(c, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_light_stats), sizeof(h)));
-        fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu WP=%llu E=%llu items=%llu iters=%llu checks=%llu groups=%llu logsum=%llu alive0=%llu multiseg=%llu"
-                " maxcyc=%llu cyc_few=%llu cyc_many=%llu cyc_mseg=%llu maxcyc_mseg=%llu grp_mseg=%llu alive_mseg=%llu\n",
-                (unsigned long long)WI, (unsigned long long)WL, (unsigned long long)WP, (unsigned long long)*E, h[0], h[1], h[2], h[3],
-                h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13]);
-        memset(h, 0, sizeof(h));
-        HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_light_stats), h, sizeof(h)));
+    if (lrec) {  // per-item records -> $RDFIND_LIGHT_DUMP (raw u32 x 16 per item)
+        std::vector<u32> h(WI * 16);
+        HIP_TRY(c, hipMemcpy(h.data(), lrec, WI * 64, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("RDFIND_LIGHT_DUMP"), "wb")) {
+            fwrite(h.data(), 64, WI, f);
+            fclose(f);
+        }
+        u32* z = nullptr;
+        HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_item_rec), &z, sizeof(z)));
+        HIP_TRY(c, hipFree(lrec));
     }
+    fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu WP=%llu E=%llu\n", (unsigned long long)WI, (unsigned long long)WL,
+            (unsigned long long)WP, (unsigned long long)*E);
 #endif
     return RDF_OK;
 }

@@ -27,6 +27,26 @@ class ParseError(ValueError):
     pass
 
 
+# Term separators: ASCII whitespace only, the device tokenizer's nt_space (kernels.inl).  Python's
+# str.isspace would also accept NBSP and the Unicode spaces, which the reference's byte-level line
+# records never split on.
+_SPACE_CHARS = " \t\n\v\f\r\x1c\x1d\x1e\x1f"
+_SPACE = frozenset(_SPACE_CHARS)
+
+
+def _is_space(ch: str) -> bool:
+    return ch in _SPACE
+
+
+def _strip_terminator(line: str) -> str:
+    """Lines end at '\n' only; one '\r' before it belongs to the terminator ("\r\n")."""
+    if line.endswith("\n"):
+        line = line[:-1]
+        if line.endswith("\r"):
+            line = line[:-1]
+    return line
+
+
 def _term_end(line: str, i: int, n: int) -> int:
     c = line[i]
     if c == "<":
@@ -48,7 +68,7 @@ def _term_end(line: str, i: int, n: int) -> int:
             raise ParseError(f"unterminated literal: {line!r}")
         j += 1
         if j < n and line[j] == "@":
-            while j < n and not line[j].isspace():
+            while j < n and not _is_space(line[j]):
                 j += 1
         elif j + 1 < n and line[j] == "^" and line[j + 1] == "^":
             j += 2
@@ -57,12 +77,12 @@ def _term_end(line: str, i: int, n: int) -> int:
                 if j <= 0:
                     raise ParseError(f"unterminated datatype IRI: {line!r}")
             else:
-                while j < n and not line[j].isspace():
+                while j < n and not _is_space(line[j]):
                     j += 1
         return j
     # blank node or bare token
     j = i
-    while j < n and not line[j].isspace():
+    while j < n and not _is_space(line[j]):
         j += 1
     return j
 
@@ -70,7 +90,7 @@ def _term_end(line: str, i: int, n: int) -> int:
 def parse_line(line: str, tabs: bool = False, quads: bool = False):
     """Split one N-Triples (N-Quads) line into its subject, predicate and object terms."""
     if tabs:
-        parts = line.rstrip("\n").split("\t")
+        parts = _strip_terminator(line).split("\t")
         if len(parts) < 3:
             raise ParseError(f"expected 3 tab-separated terms: {line!r}")
         return parts[0], parts[1], parts[2]
@@ -79,7 +99,7 @@ def parse_line(line: str, tabs: bool = False, quads: bool = False):
     i = 0
     need = 4 if quads else 3
     while len(terms) < 3:
-        while i < n and line[i].isspace():
+        while i < n and _is_space(line[i]):
             i += 1
         if i >= n:
             raise ParseError(f"expected {need} terms: {line!r}")
@@ -118,8 +138,8 @@ def _open(path: str):
         while path.startswith("//"):
             path = path[1:]
     if path.endswith(".gz"):
-        return io.TextIOWrapper(gzip.open(path, "rb"), encoding="utf-8")
-    return open(path, "r", encoding="utf-8")
+        return io.TextIOWrapper(gzip.open(path, "rb"), encoding="utf-8", newline="\n")
+    return open(path, "r", encoding="utf-8", newline="\n")  # no universal newlines: a lone '\r' ends no line
 
 
 def resolve_paths(paths):
@@ -154,7 +174,8 @@ def read_triples(paths, tabs: bool = False, dictionary: Dictionary | None = None
             for line in f:
                 if line.startswith("#"):
                     continue
-                if not line.strip():
+                line = _strip_terminator(line)
+                if not line.strip(_SPACE_CHARS):
                     continue
                 a, b, c = parse_line(line, tabs, quads)
                 s.append(enc(a))

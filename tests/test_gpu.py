@@ -331,6 +331,22 @@ _NT_SAMPLE = (
 )
 
 
+def _long_line_text() -> bytes:
+    """Lines of 300-2000 B literals, so most 256-line tokenizer blocks exceed the 48 KB LDS tile and parse from
+    global memory (NtGlobal), mixed with short-line blocks (LDS), and one single line > 48 KB."""
+    rng = np.random.default_rng(7)
+    lines = []
+    for i in range(3000):
+        if (i // 256) % 3 == 2:
+            lines.append(f"<s{i % 97}> <p{i % 5}> <o{i % 211}> .")
+        else:
+            lit = "".join(chr(97 + c) for c in rng.integers(0, 26, int(rng.integers(300, 2000))))
+            lines.append(f"<s{i % 97}> <p{i % 5}> \"{lit}\"@en .")
+        if i == 1500:
+            lines.append("<big> <p0> \"" + "z" * 60000 + "\" .")
+    return ("\n".join(lines) + "\n").encode()
+
+
 def _host_parse(tmp_path, data: bytes, tabs=False):
     f = tmp_path / "host.nt"
     f.write_bytes(data)
@@ -343,7 +359,7 @@ def _device_parse(ctx, data: bytes, tabs=False):
     return s, p, o, ntriples.HeapDictionary(*ctx.parsed_terms())
 
 
-@pytest.mark.parametrize("case", ["sample", "empty", "only_comments", "tabs", "golden_lubm", "golden_zipf",
+@pytest.mark.parametrize("case", ["sample", "empty", "only_comments", "tabs", "long_lines", "cr_nbsp", "golden_lubm", "golden_zipf",
                                   "synthetic_c1"])
 def test_device_parser_matches_host(ctx, tmp_path, case):
     """rdf_parse_ntriples gives the host parser's triples and dictionary bit-exactly (same ids, same terms)."""
@@ -357,6 +373,12 @@ def test_device_parser_matches_host(ctx, tmp_path, case):
         data = b"# a\n\n#b\n"
     elif case == "tabs":
         data = b"<a>\t<p>\t\"x y\"\t.\n# c\n<b>\t<p>\t<a>\n\n<a> x\t<q>\t\"z\"\r\n"
+    elif case == "long_lines":
+        data = _long_line_text()
+    elif case == "cr_nbsp":
+        # a lone '\r' ends no line; NBSP / U+3000 are term bytes, not separators (ASCII whitespace only)
+        data = ("<a> <p> \"x\ry\" .\n<b>\u00a0<c> <p> <d> .\r\n<e> <p> \"s\u3000t\" .\n"
+                "<f> <p>\r<g> <h> .\n<i> <p> <j>").encode()
     elif case.startswith("golden"):
         data = _gz.open(os.path.join(GOLDEN, f"{case.split('_')[1]}_small.nt.gz"), "rb").read()
     else:

@@ -22,10 +22,13 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, cases, q, local_slice=False):
+def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        import torch
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     from rdfind_amd import _lib, distributed
 
     out = []
@@ -49,11 +52,11 @@ def _worker(rank, world, port, cases, q, local_slice=False):
         dist.destroy_process_group()
 
 
-def _run_sharded(world, cases, local_slice=False):
+def _run_sharded(world, cases, local_slice=False, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice, backend)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in procs)
@@ -82,9 +85,9 @@ def _rowset(rows):
     return set(map(tuple, np.stack([rows["dep"], rows["ref"], rows["support"]], 1).tolist()))
 
 
-def _check(world, cases, local_slice=False):
+def _check(world, cases, local_slice=False, backend="gloo"):
     single = _single(cases)
-    res = _run_sharded(world, cases, local_slice)
+    res = _run_sharded(world, cases, local_slice, backend)
     for k, exp in enumerate(single):
         parts = [res[r][k] for r in range(world)]
         assert sum(p["n"] for p in parts) == exp["n"], k
@@ -113,6 +116,17 @@ def _random_cases(seed, count):
 @pytest.mark.parametrize("world,local_slice", [(2, False), (3, False), (2, True), (3, True)])
 def test_sharded_random_matches_single(world, local_slice):
     _check(world, _random_cases(100 + world, 24), local_slice)
+
+
+def test_sharded_rccl_backend_world1():
+    """The RCCL branch of run_protocol (exchange buffers in HBM, stream syncs around each collective): one rank
+    over the nccl backend (the box has one GPU, and RCCL refuses two ranks on one device); the 13 collectives run
+    with world size 1 and the result equals the single-GPU run."""
+    from rdfind_amd import synth
+
+    d = synth.config("c2", 0.02)
+    cases = _random_cases(7, 6) + [(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)]
+    _check(1, cases, local_slice=True, backend="nccl")
 
 
 def test_sharded_synthetic_configs_match_oracle():

@@ -27,9 +27,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     print("AB", json.dumps(out), flush=True)
     sys.exit(0)
 
-for lib in os.environ.get("RDFIND_AB_LIBS", "librdfind_hip.so").split(","):
+# a variant is "<lib>[@VAR=value[@VAR=value]]": the library plus environment switches (e.g. RDFIND_SIG=0)
+for variant in os.environ.get("RDFIND_AB_LIBS", "librdfind_hip.so").split(","):
+    lib, *envs = variant.split("@")
     env = dict(os.environ, RDFIND_HIP_LIB=os.path.join(ROOT, "rdfind_amd", lib))
+    env.update(e.split("=", 1) for e in envs)
     r = subprocess.run([sys.executable, __file__, "--child"] + sys.argv[1:], env=env, capture_output=True, text=True,
                        timeout=900)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("AB")]
-    print(lib, line[0][3:] if line else r.stderr[-2000:], flush=True)
+    print(variant, line[0][3:] if line else r.stderr[-2000:], flush=True)
