@@ -8,7 +8,8 @@ static constexpr int LH_SLOTS = 4096;     // LDS hash slots (u32 keys) for unary
 static constexpr int LB_SLOTS = 2048;     // LDS hash slots (u64 keys) for binary counting
 static constexpr int HMAX = 64;           // heavy groups tracked as bit columns (one u64 per capture)
 static constexpr uint8_t LIGHT = 0xff;
-static constexpr u32 DGRP_HEAVY = 0x80000000u;  // tag of a dependent -> group entry whose group is heavy
+static constexpr u32 DGRP_HEAVY = 0x80000000u;
+static constexpr u32 GINFO_HEAVY = 0x80000000u;  // ginfo[g] = member count | this bit for heavy groups  // tag of a dependent -> group entry whose group is heavy
 #ifndef RDF_LIGHT_SEG
 #define RDF_LIGHT_SEG 2048
 #endif
@@ -18,13 +19,14 @@ static constexpr u64 LIGHT_SEG = RDF_LIGHT_SEG;  // groups of one dependent veri
 #endif
 static constexpr int LIGHT_IT = RDF_LIGHT_IT;  // groups per lane whose metadata is loaded together
 #ifndef RDF_SIG_W
-#define RDF_SIG_W 4
+#define RDF_SIG_W 8
 #endif
 // Light-group signatures: bit h(g) of a 64*SIG_W-bit word set for every light group g of a capture.  G(d) <= G(c)
 // implies sig(d) <= sig(c), so a candidate whose signature misses a bit of the dependent's is not a ref; this kills
 // most doomed candidates before any group search (the heavy groups are exact bits of hmask already).
 static constexpr int SIG_W = RDF_SIG_W;
-static constexpr int SIG_LOG = SIG_W == 8 ? 9 : SIG_W == 4 ? 8 : SIG_W == 2 ? 7 : 6;
+static constexpr int SIG_LOG = SIG_W == 16 ? 10 : SIG_W == 8 ? 9 : SIG_W == 4 ? 8 : SIG_W == 2 ? 7 : 6;
+static_assert((1 << (SIG_LOG - 6)) == SIG_W, "SIG_W must be 1, 2, 4, 8 or 16");
 static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
 #ifndef RDF_PACK_MAXG2
 #define RDF_PACK_MAXG2 512
@@ -42,7 +44,8 @@ static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched toge
 #define RDF_LIGHT_SERIAL 4
 #endif
 static constexpr int LIGHT_SERIAL = RDF_LIGHT_SERIAL;  // windows with at most this many light groups: lanes over candidates
-static constexpr u32 LIGHT_LDS = 512;                   // groups up to this size are searched in LDS (2 KiB per wave)
+static constexpr u32 LIGHT_LDS = 512;
+                  // groups up to this size are searched in LDS (2 KiB per wave)
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
 struct __align__(16) CapInfo {
@@ -81,6 +84,8 @@ struct CindView {
     int ar;               // ArMode (--use-ars)
     const u32* arref;     // unary compact id -> the ref its association rule implies, or NONE32 [Cu]
     const u64* sig;       // light-group signature of each capture, SIG_W words (null: no signature test)
+    const u32* ginfo;     // group -> member count | GINFO_HEAVY (k_group_info)
+    const u32* piv2;      // dependent -> its smallest light group other than the pivot (NONE32: none / not computed)
 };
 
 }  // namespace rdf

@@ -730,25 +730,37 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_nseg(const u64* __restrict_
 
 // The pivot pass visits every (dependent, group) entry once and tags the entries of heavy groups in place
 // (DGRP_HEAVY): the light kernels then skip them without a per-group gather of hbit.
+// the smallest light group other than the pivot, from the pivot key and the two smallest light keys
+__device__ inline u32 second_pivot(u64 best, u64 l1, u64 l2) {
+    const u64 k = (u32)l1 == (u32)best ? l2 : l1;
+    return k == ~0ull ? NONE32 : (u32)k;
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp_tag, u64* best_out, u32* nlight_out,
-                                                           u64* sig) {
+                                                           u64* sig, u32* piv2) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = v.doff[d], e = v.doff[d + 1];
         if (e - b > PIVOT_SHORT) continue;
-        u64 best = ~0ull;
+        u64 best = ~0ull, l1 = ~0ull, l2 = ~0ull;  // smallest group; two smallest light groups
         u32 nlight = 0;
         u64 sg[SIG_W] = {};
         for (u64 j = b; j < e; ++j) {
             const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
-            const u64 key = ((v.goff[g + 1] - v.goff[g]) << 32) | g;
+            const u32 gi = v.ginfo[g];
+            const u64 key = ((u64)(gi & ~GINFO_HEAVY) << 32) | g;
             best = key < best ? key : best;
-            const bool light = v.hbit[g] == LIGHT;
+            const bool light = !(gi & GINFO_HEAVY);
             nlight += light;
-            if (light) sig_add(sg, g);
+            if (light) {
+                sig_add(sg, g);
+                l2 = key < l2 ? (key < l1 ? l1 : key) : l2;
+                l1 = key < l1 ? key : l1;
+            }
             dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
         }
         best_out[d] = best;
         nlight_out[d] = nlight;
+        if (piv2) piv2[d] = second_pivot(best, l1, l2);
         if (sig)
 #pragma unroll
             for (int k = 0; k < SIG_W; ++k) sig[d * SIG_W + k] = sg[k];
@@ -756,7 +768,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
 }
 
 __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
-                                        u64* best_out, u32* nlight_out, u64* sig) {
+                                        u64* best_out, u32* nlight_out, u64* sig, u32* piv2) {
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -764,23 +776,31 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
     const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
     const u64 b = b0 + (w - segoff[d]) * PIVOT_SEG;
     const u64 e = b + PIVOT_SEG < e0 ? b + PIVOT_SEG : e0;
-    u64 best = ~0ull;  // (size << 32 | group)
+    u64 best = ~0ull, l1 = ~0ull, l2 = ~0ull;  // (size << 32 | group): smallest; two smallest light
     u32 nlight = 0;
     u64 sg[SIG_W] = {};
     for (u64 j = b + lane; j < e; j += RDF_WAVE) {
         const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
-        const u64 sz = v.goff[g + 1] - v.goff[g];
-        const u64 key = (sz << 32) | g;
+        const u32 gi = v.ginfo[g];
+        const u64 key = ((u64)(gi & ~GINFO_HEAVY) << 32) | g;
         best = key < best ? key : best;
-        const bool light = v.hbit[g] == LIGHT;
+        const bool light = !(gi & GINFO_HEAVY);
         nlight += light;
-        if (light) sig_add(sg, g);
+        if (light) {
+            sig_add(sg, g);
+            l2 = key < l2 ? (key < l1 ? l1 : key) : l2;
+            l1 = key < l1 ? key : l1;
+        }
         dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         u64 o = __shfl_xor(best, off, RDF_WAVE);
         best = o < best ? o : best;
+        const u64 o1 = __shfl_xor(l1, off, RDF_WAVE), o2 = __shfl_xor(l2, off, RDF_WAVE);
+        const u64 hi = l1 < o1 ? o1 : l1, lo2 = l2 < o2 ? l2 : o2;
+        l1 = l1 < o1 ? l1 : o1;
+        l2 = hi < lo2 ? hi : lo2;
 #pragma unroll
         for (int k = 0; k < SIG_W; ++k) sg[k] |= __shfl_xor(sg[k], off, RDF_WAVE);
     }
@@ -790,6 +810,7 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
         if (single) {
             best_out[d] = best;
             nlight_out[d] = nlight;
+            if (piv2) piv2[d] = second_pivot(best, l1, l2);  // multi-segment dependents keep NONE32
         } else {
             atomicMin(&best_out[d], best);
             atomicAdd(&nlight_out[d], nlight);
@@ -805,9 +826,9 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(u64 nvblk, CindView v, u32* dgrp_tag,
                                                          const u64* __restrict__ segoff, u64 W, u64* best_out,
-                                                         u32* nlight_out, u64* sig) {
+                                                         u32* nlight_out, u64* sig, u32* piv2) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out, sig);
+        k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out, sig, piv2);
     }
 }
 
@@ -1000,6 +1021,42 @@ __device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& i
     return pivot_candidate(v, d, id, piv, chunk * RDF_WAVE + lane_id());
 }
 
+// per group: ginfo = size | heavy << 31 (one 4-B gather for the pivot pass instead of two offsets + the heavy byte)
+__global__ __launch_bounds__(RDF_BLOCK) void k_group_info(const u64* __restrict__ goff, const uint8_t* __restrict__ hbit,
+                                                          u64 G, u32* ginfo) {
+    for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK)
+        ginfo[g] = (u32)(goff[g + 1] - goff[g]) | (hbit[g] == LIGHT ? 0u : GINFO_HEAVY);
+}
+
+// One group (members [gb, gb+gs)) checked for every alive candidate of the wave (lanes over candidates): a group of
+// at most LIGHT_LDS members is staged into the wave's LDS slice by one coalesced load, so each search is LDS probes;
+// a larger one is searched in place (the lanes share its top levels).  Returns the candidates still alive.
+__device__ inline u64 check_group(const CindView& v, u64 gb, u32 gs, u32 cand, u64 alive, u32* buf) {
+    const int lane = lane_id();
+    const bool mine = (alive >> lane) & 1ull;
+    bool found = true;
+    if (gs <= LIGHT_LDS) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
+        __builtin_amdgcn_wave_barrier();
+        for (u32 k = lane; k < gs; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (mine) {
+            u32 lo = 0, hi = gs;
+            while (lo < hi) {
+                const u32 mid = (lo + hi) >> 1;
+                if (buf[mid] < cand) lo = mid + 1;
+                else hi = mid;
+            }
+            found = lo < gs && buf[lo] == cand;
+        }
+    } else if (mine) {
+        found = bsearch_u32(v.gcap + gb, gs, cand);
+    }
+    return alive & __ballot(found);
+}
+
 // Survivors go to per-octet slots (8 candidates of a pivot each; no shared counter: a single global append
 // counter serialises at the memory side); k_slot_compact packs the slots afterwards in slot order, which
 // is (dependent, ref) order.  Lanes [8o, 8o+8) of the wave own octet oct0 + o; octets >= nvalid belong to
@@ -1044,10 +1101,12 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     const CapInfo id = v.info[d];
     const u32 cand = pivot_candidate(v, d, id, piv, k * 8 + (g & 7));
     bool ok = cand != NONE32;
+    const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;  // the smallest light group after the pivot first (most kills)
+    if (ok && p2 != NONE32) ok = bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
     const u64 b = v.doff[d], e = v.doff[d + 1];
     for (u64 j = b; ok && j < e; ++j) {
         const u32 gr = v.dgrp[j];  // heavy entries carry DGRP_HEAVY (k_pivot_*)
-        if (gr == piv || (gr & DGRP_HEAVY)) continue;
+        if (gr == piv || gr == p2 || (gr & DGRP_HEAVY)) continue;
         ok = bsearch_u32(v.gcap + v.goff[gr], v.goff[gr + 1] - v.goff[gr], cand);
     }
     const u64 alive = __ballot(ok);
@@ -1109,6 +1168,13 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const u64 b = b0 + seg * LIGHT_SEG;
     const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
     LSTAT_T0;
+    // The dependent's smallest light group after the pivot first, lanes over candidates: it kills most doomed
+    // candidates with one (often LDS-staged) search each before the group-parallel windows below.
+    const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
+    if (p2 != NONE32 && alive) {
+        const u64 gb2 = v.goff[p2];
+        alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE]);
+    }
     // Lanes take one group each (LIGHT_IT per lane); dependents with few groups went to k_light_packed, so
     // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
     // independent gathers per level, so the serial chain is three round trips per segment, not per 64 groups.
@@ -1123,7 +1189,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         }
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it)
-            if (gg[it] == piv || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY too
+            if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it) {
             gbv[it] = 0;
@@ -1155,28 +1221,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                     LSTAT_SER(1);
                     const u64 gb = __shfl(gbv[it], l, RDF_WAVE);
                     const u32 gs = __shfl(gszv[it], l, RDF_WAVE);
-                    const bool mine = (alive >> lane) & 1ull;
-                    bool found = true;
-                    if (gs <= LIGHT_LDS) {
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
-                        __builtin_amdgcn_wave_barrier();
-                        for (u32 k = lane; k < gs; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        if (mine) {
-                            u32 lo = 0, hi = gs;
-                            while (lo < hi) {
-                                const u32 mid = (lo + hi) >> 1;
-                                if (buf[mid] < cand) lo = mid + 1;
-                                else hi = mid;
-                            }
-                            found = lo < gs && buf[lo] == cand;
-                        }
-                    } else if (mine) {
-                        found = bsearch_u32(v.gcap + gb, gs, cand);
-                    }
-                    alive &= __ballot(found);
+                    alive = check_group(v, gb, gs, cand, alive, buf);
                 }
                 continue;
             }

@@ -73,7 +73,12 @@ struct rdf_ctx {
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf lsig;          // light-group signatures (SIG_W words per compact capture), computed by the pivot pass
+    DevBuf ginfo;  // group -> size | heavy bit (k_group_info)
+    DevBuf piv2;   // dependent -> second pivot (smallest light group after the pivot)
     bool sig_on = false;  // lsig holds this run's signatures (RDFIND_SIG=0 turns the filter off)
+    bool sig_packed = false;  // the packed light path tests them too (RDFIND_SIG=1; default 2: k_light only)
+    bool piv2_on = false;     // piv2 holds this run's second pivots
+    bool piv2_packed = true;  // ... and the packed light path checks them first too (RDFIND_PIV2=2: k_light only)
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
         ctiles, ctoff;
     u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
@@ -251,7 +256,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->ginfo, &c->piv2, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
@@ -1286,6 +1291,8 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.ar = c->ar_on && c->nranks == 1 ? (v.literal ? AR_S0 : AR_S2L) : AR_NONE;
     v.arref = c->arref.as<u32>();
     v.sig = c->sig_on ? c->lsig.as<u64>() : nullptr;
+    v.ginfo = c->ginfo.as<u32>();
+    v.piv2 = c->piv2_on ? c->piv2.as<u32>() : nullptr;
     return v;
 }
 
@@ -1308,14 +1315,36 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     ENSURE(c, psegoff, (C + 1ull) * 8);
     ENSURE(c, pbest, std::max<u64>(C, 1) * 8);
     ENSURE(c, pnl, std::max<u64>(C, 1) * 4);
-    static const bool sig_enabled = !getenv("RDFIND_SIG") || atoi(getenv("RDFIND_SIG")) != 0;
+    // signature test in k_light only by default (mode 2): on the packed path (few groups per dependent) the extra
+    // line per candidate cost more than it saved (c5 at 0.1: 20.8 vs 17.6 ms light); mode 1 tests it in both
+    static const int sig_mode = getenv("RDFIND_SIG") ? atoi(getenv("RDFIND_SIG")) : 2;
+    const bool sig_enabled = sig_mode != 0;
     c->sig_on = sig_enabled;
+    c->sig_packed = sig_mode != 2;
     u64* sig = nullptr;
     if (sig_enabled) {
         ENSURE(c, lsig, std::max<u64>(C, 1) * 8 * SIG_W);
         sig = c->lsig.as<u64>();
     }
+    const u64 G = c->G;
+    ENSURE(c, ginfo, std::max<u64>(G, 1) * 4);
+    v.ginfo = c->ginfo.as<u32>();
     tbegin(c, RDF_T_PIVOT);
+    if (G)
+        hipLaunchKernelGGL(k_group_info, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(),
+                           c->hbit.as<uint8_t>(), G, c->ginfo.as<u32>());
+    tend(c, RDF_T_PIVOT);
+    static const int piv2_mode = getenv("RDFIND_PIV2") ? atoi(getenv("RDFIND_PIV2")) : 1;  // 2: k_light only
+    const bool piv2_enabled = piv2_mode != 0;
+    c->piv2_packed = piv2_mode != 2;
+    u32* piv2 = nullptr;
+    if (piv2_enabled) {
+        ENSURE(c, piv2, std::max<u64>(C, 1) * 4);
+        piv2 = c->piv2.as<u32>();
+    }
+    c->piv2_on = piv2_enabled;
+    tbegin(c, RDF_T_PIVOT);
+    if (piv2 && C) HIP_TRY(c, hipMemsetAsync(piv2, 0xff, (u64)C * 4, st));  // multi-segment dependents: none
     if (sig && C) HIP_TRY(c, hipMemsetAsync(sig, 0, (u64)C * 8 * SIG_W, st));
     if (C) {
         hipLaunchKernelGGL(k_pivot_nseg, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), C,
@@ -1324,7 +1353,7 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         HIP_TRY(c, hipMemsetAsync(c->pbest.p, 0xff, (u64)C * 8, st));
         HIP_TRY(c, hipMemsetAsync(c->pnl.p, 0, (u64)C * 4, st));
         hipLaunchKernelGGL(k_pivot_short, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->dgrp.as<u32>(),
-                           c->pbest.as<u64>(), c->pnl.as<u32>(), sig);
+                           c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2);
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
@@ -1332,9 +1361,10 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     tbegin(c, RDF_T_PIVOT);
     if (WS)
         hipLaunchKernelGGL(k_pivot_seg, dim3(vgrid(wave_blocks(WS))), dim3(RDF_BLOCK),
-                           0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>(), sig);
+                           0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2);
     tend(c, RDF_T_PIVOT);
     v.sig = sig;  // the candidate passes of this run test the signatures
+    v.piv2 = piv2;
     return RDF_OK;
 }
 
@@ -1386,8 +1416,11 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     if (WP)
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pkoff.as<u64>(),
                            c->C, c->pk_dep.as<u32>());
+    CindView vp = v;
+    if (!c->sig_packed) vp.sig = nullptr;
+    if (!c->piv2_packed) vp.piv2 = nullptr;
     if (WP)
-        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), v,
+        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
                            c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     if (WI)

@@ -9,8 +9,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["RDFIND_HIP_LIB"] = os.path.join(ROOT, "rdfind_amd", "librdfind_hip_stats.so")
-dump = os.path.join(ROOT, "gpurun_out", "light_items.bin")
-os.makedirs(os.path.dirname(dump), exist_ok=True)
+dump = os.path.join(os.environ.get("TMPDIR", "/tmp"), "light_items.bin")  # large: kept out of gpurun_out
 os.environ["RDFIND_LIGHT_DUMP"] = dump
 sys.path.insert(0, ROOT)
 from rdfind_amd import _lib, synth  # noqa: E402
