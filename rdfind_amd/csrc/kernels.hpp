@@ -45,6 +45,18 @@ static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched toge
 #endif
 static constexpr int LIGHT_SERIAL = RDF_LIGHT_SERIAL;  // windows with at most this many light groups: lanes over candidates
 static constexpr u32 LIGHT_LDS = 512;
+#ifndef RDF_LIGHT_SMALL
+#define RDF_LIGHT_SMALL 31
+#endif
+#ifndef RDF_STAGE_MIN
+#define RDF_STAGE_MIN 3
+#endif
+// windows whose light groups all have <= LIGHT_SMALL members are staged into per-lane LDS rows once at least
+// LIGHT_STAGE_MIN candidates are alive (LIGHT_STAGE_MIN > 64 turns it off)
+static constexpr u32 LIGHT_SMALL = RDF_LIGHT_SMALL;  // odd: also the row stride (conflict-free banks)
+static_assert(LIGHT_SMALL % 2 == 1, "LIGHT_SMALL is the LDS row stride and must be odd");
+static constexpr u32 LIGHT_BUF = LIGHT_LDS > 64 * LIGHT_SMALL ? LIGHT_LDS : 64 * LIGHT_SMALL;  // u32 per wave
+static constexpr int LIGHT_STAGE_MIN = RDF_STAGE_MIN;
                   // groups up to this size are searched in LDS (2 KiB per wave)
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load

@@ -1086,6 +1086,37 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_slot_compact(u64 nvblk, const u64
 }
 
 
+// one key searched in K sorted arrays at once (n[k] == 0: no array); the loads of a level are independent
+#ifndef RDF_PACK_STEP
+#define RDF_PACK_STEP 4
+#endif
+static constexpr int PACK_STEP = RDF_PACK_STEP;  // group entries per step of the packed path
+template <int K>
+__device__ inline void multi_search(const u32* const (&a)[K], const u64 (&n)[K], u32 key, bool (&found)[K]) {
+    u64 base[K], m[K];
+    bool more = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        base[k] = 0;
+        m[k] = n[k];
+        more |= m[k] > 1;
+    }
+    while (more) {
+        more = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (m[k] > 1) {
+                const u64 half = m[k] >> 1;
+                base[k] = a[k][base[k] + half] <= key ? base[k] + half : base[k];
+                m[k] -= half;
+            }
+            more |= m[k] > 1;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) found[k] = n[k] && a[k][base[k]] == key;
+}
+
 // packed light dependents (few groups): one lane per pivot candidate, 8-lane octets, candidates of many
 // dependents per wave.  Each lane walks its dependent's groups and binary-searches its candidate in every
 // light one (the same test as k_light's few-groups path, without a mostly idle wave per dependent).
@@ -1104,10 +1135,25 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;  // the smallest light group after the pivot first (most kills)
     if (ok && p2 != NONE32) ok = bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
     const u64 b = v.doff[d], e = v.doff[d + 1];
-    for (u64 j = b; ok && j < e; ++j) {
-        const u32 gr = v.dgrp[j];  // heavy entries carry DGRP_HEAVY (k_pivot_*)
-        if (gr == piv || gr == p2 || (gr & DGRP_HEAVY)) continue;
-        ok = bsearch_u32(v.gcap + v.goff[gr], v.goff[gr + 1] - v.goff[gr], cand);
+    // PACK_STEP group entries at a time: their ids, bounds and searches are independent loads (one round trip per
+    // level for all of them instead of one chain per group)
+    for (u64 j0 = b; ok && j0 < e; j0 += PACK_STEP) {
+        u32 gr[PACK_STEP];
+        const u32* ga[PACK_STEP];
+        u64 gn[PACK_STEP];
+#pragma unroll
+        for (int i = 0; i < PACK_STEP; ++i) gr[i] = j0 + i < e ? v.dgrp[j0 + i] : NONE32;  // heavy entries: DGRP_HEAVY
+#pragma unroll
+        for (int i = 0; i < PACK_STEP; ++i) {
+            const bool lt = !(gr[i] == piv || gr[i] == p2 || (gr[i] & DGRP_HEAVY));
+            const u64 gb = lt ? v.goff[gr[i]] : 0;
+            gn[i] = lt ? v.goff[gr[i] + 1] - gb : 0;
+            ga[i] = v.gcap + gb;
+        }
+        bool f[PACK_STEP];
+        multi_search<PACK_STEP>(ga, gn, cand, f);
+#pragma unroll
+        for (int i = 0; i < PACK_STEP; ++i) ok = ok && (gn[i] == 0 || f[i]);
     }
     const u64 alive = __ballot(ok);
     const int lane = lane_id(), o = lane >> 3, jj = lane & 7;
@@ -1145,13 +1191,32 @@ __device__ u32* g_item_rec;
 #define LSTAT_BAT(depth) do { } while (0)
 #endif
 
+// one batch of the group-parallel window: the next K alive candidates (taken from todo) searched in every lane's
+// group gm (g == NONE32: no group in this lane); a candidate missing from any lane's group dies
+template <int K>
+__device__ inline void light_batch(const u32* gm, u64 gsz, u32 g, u32 cand, u64& todo, u64& alive) {
+    int bit[K];
+    u32 key[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bit[k] = todo ? __ffsll((long long)todo) - 1 : -1;
+        todo &= todo - 1;
+        key[k] = __shfl(cand, bit[k] < 0 ? bit[0] : bit[k], RDF_WAVE);
+    }
+    bool ok[K];
+    search_batch<K>(gm, gsz, key, ok);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (bit[k] >= 0 && !__all(g == NONE32 || ok[k])) alive &= ~(1ull << bit[k]);
+}
+
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
 __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
                                     const u64* __restrict__ choff, u64 W, u64* dead, u64* slots, u32* counts) {
-    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_LDS];
+    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_BUF];  // a staged group, or the lanes' small-group rows
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -1227,24 +1292,60 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             }
             const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
             const u64 gsz = gszv[it];
+            if (__popcll(alive) >= LIGHT_STAGE_MIN && __all(g == NONE32 || gsz <= LIGHT_SMALL)) {
+                // every light group of the window is small: each lane copies its group into its own LDS row with
+                // <= 9 aligned 16-B loads, then the alive candidates are searched in LDS (instead of A x log2 n
+                // divergent global loads)
+                u32* row = s_light[threadIdx.x / RDF_WAVE] + lane * LIGHT_SMALL;  // odd stride: rows spread over banks
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of the rows precede the refill
+                __builtin_amdgcn_wave_barrier();
+                if (g != NONE32) {
+                    const u64 gb = gbv[it], a0 = gb & ~3ull;
+                    const int lead = (int)(gb - a0), n = (int)gsz;
+                    const int nq = (lead + n + 3) >> 2;
+                    for (int q = 0; q < nq; ++q) {
+                        const uint4 w4 = *(const uint4*)(v.gcap + a0 + 4 * q);  // gcap is padded by 16 B
+                        const u32 wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int ei = 4 * q + t - lead;
+                            if (ei >= 0 && ei < n) row[ei] = wv[t];
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                u64 todo = alive;
+                while (todo) {
+                    const int l = __ffsll((long long)todo) - 1;
+                    todo &= todo - 1;
+                    const u32 key = __shfl(cand, l, RDF_WAVE);
+                    bool found = true;
+                    if (g != NONE32) {
+                        u32 lo = 0, hi = (u32)gsz;
+                        while (lo < hi) {
+                            const u32 mid = (lo + hi) >> 1;
+                            if (row[mid] < key) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        found = lo < gsz && row[lo] == key;
+                    }
+                    if (!__all(found)) alive &= ~(1ull << l);
+                }
+                continue;
+            }
             // up to LIGHT_BATCH alive candidates are searched at once: their loads at one level of the
             // search are independent, so the serial chain is one search, not one per candidate
+            // the batch width follows the alive count: a key slot without its own candidate would repeat another
+            // slot's loads (each a divergent wave-wide load over 64 groups)
             u64 todo = alive;
             while (todo) {
-                int bit[LIGHT_BATCH];
-                u32 key[LIGHT_BATCH];
-#pragma unroll
-                for (int k = 0; k < LIGHT_BATCH; ++k) {
-                    bit[k] = todo ? __ffsll((long long)todo) - 1 : -1;
-                    todo &= todo - 1;
-                    key[k] = __shfl(cand, bit[k] < 0 ? bit[0] : bit[k], RDF_WAVE);
-                }
-                bool ok[LIGHT_BATCH];
                 LSTAT_BAT(gsz ? 64 - __clzll(gsz) : 0);
-                search_batch<LIGHT_BATCH>(gm, gsz, key, ok);
-#pragma unroll
-                for (int k = 0; k < LIGHT_BATCH; ++k)
-                    if (bit[k] >= 0 && !__all(g == NONE32 || ok[k])) alive &= ~(1ull << bit[k]);
+                const int na = __popcll(todo);
+                if (na <= 2) light_batch<2>(gm, gsz, g, cand, todo, alive);
+                else if (na <= 4) light_batch<4>(gm, gsz, g, cand, todo, alive);
+                else light_batch<LIGHT_BATCH>(gm, gsz, g, cand, todo, alive);
             }
         }
     }

@@ -1136,7 +1136,7 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     const u64 G = G32;
     c->G = G;
     ENSURE(c, goff, (G + 1) * 8);
-    ENSURE(c, gcap, std::max<u64>(Jf, 1) * 4);
+    ENSURE(c, gcap, std::max<u64>(Jf, 1) * 4 + 16);  // + 16 B: the light pass reads whole aligned quads
     ENSURE(c, gmap, (u64)V * 4);
     if (Jf) {
         hipLaunchKernelGGL(k_group_build, dim3(grid_for(Jf, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fk.as<u64>(), Jf,
