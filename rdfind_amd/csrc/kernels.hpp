@@ -57,6 +57,10 @@ static constexpr u32 LIGHT_SMALL = RDF_LIGHT_SMALL;  // odd: also the row stride
 static_assert(LIGHT_SMALL % 2 == 1, "LIGHT_SMALL is the LDS row stride and must be odd");
 static constexpr u32 LIGHT_BUF = LIGHT_LDS > 64 * LIGHT_SMALL ? LIGHT_LDS : 64 * LIGHT_SMALL;  // u32 per wave
 static constexpr int LIGHT_STAGE_MIN = RDF_STAGE_MIN;
+#ifndef RDF_STAGE_AVG
+#define RDF_STAGE_AVG 48
+#endif
+static constexpr u64 LIGHT_STAGE_AVG = RDF_STAGE_AVG;  // staging variant when the weighted mean light group is smaller
                   // groups up to this size are searched in LDS (2 KiB per wave)
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load

@@ -1022,10 +1022,21 @@ __device__ inline u32 chunk_candidate(const CindView& v, u32 d, const CapInfo& i
 }
 
 // per group: ginfo = size | heavy << 31 (one 4-B gather for the pivot pass instead of two offsets + the heavy byte)
+// part: per-block partials of (sum of light group sizes n, sum of n^2): the member-weighted mean light group size
+// picks the light kernel's variant (k_light<STAGE>)
 __global__ __launch_bounds__(RDF_BLOCK) void k_group_info(const u64* __restrict__ goff, const uint8_t* __restrict__ hbit,
-                                                          u64 G, u32* ginfo) {
-    for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK)
-        ginfo[g] = (u32)(goff[g + 1] - goff[g]) | (hbit[g] == LIGHT ? 0u : GINFO_HEAVY);
+                                                          u64 G, u32* ginfo, u64* part) {
+    u64 acc[3] = {0, 0, 0};
+    for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 n = goff[g + 1] - goff[g];
+        const bool light = hbit[g] == LIGHT;
+        ginfo[g] = (u32)n | (light ? 0u : GINFO_HEAVY);
+        if (light) {
+            acc[0] += n;
+            acc[1] += n * n;
+        }
+    }
+    block_partials3(acc, part);
 }
 
 // One group (members [gb, gb+gs)) checked for every alive candidate of the wave (lanes over candidates): a group of
@@ -1213,10 +1224,13 @@ __device__ inline void light_batch(const u32* gm, u64 gsz, u32 g, u32 cand, u64&
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
+template <bool STAGE>
 __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
                                     const u64* __restrict__ choff, u64 W, u64* dead, u64* slots, u32* counts) {
-    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][LIGHT_BUF];  // a staged group, or the lanes' small-group rows
+    // a staged group, or (STAGE) the lanes' small-group rows.  The larger buffer is only allocated by the variant
+    // that uses it: on c3 (large light groups) 31.7 KB per block cost 30 % of the kernel even with the path unused
+    __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][STAGE ? LIGHT_BUF : LIGHT_LDS];
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -1292,7 +1306,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             }
             const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
             const u64 gsz = gszv[it];
-            if (__popcll(alive) >= LIGHT_STAGE_MIN && __all(g == NONE32 || gsz <= LIGHT_SMALL)) {
+            if (STAGE && __popcll(alive) >= LIGHT_STAGE_MIN && __all(g == NONE32 || gsz <= LIGHT_SMALL)) {
                 // every light group of the window is small: each lane copies its group into its own LDS row with
                 // <= 9 aligned 16-B loads, then the alive candidates are searched in LDS (instead of A x log2 n
                 // divergent global loads)
@@ -1376,12 +1390,13 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
 #else
 #define RDF_LIGHT_ATTR
 #endif
+template <bool STAGE>
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_ATTR void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                      const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
                                                      const u64* __restrict__ choff, u64 W, u64* dead, u64* slots,
                                                      u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_light_body(vb, v, pivot, itemoff, item_dep, choff, W, dead, slots, counts);
+        k_light_body<STAGE>(vb, v, pivot, itemoff, item_dep, choff, W, dead, slots, counts);
     }
 }
 

@@ -74,6 +74,8 @@ struct rdf_ctx {
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf lsig;          // light-group signatures (SIG_W words per compact capture), computed by the pivot pass
     DevBuf ginfo;  // group -> size | heavy bit (k_group_info)
+    DevBuf gsums;  // sum of light group sizes, of their squares (k_group_info)
+    bool light_stage = false;  // k_light<true>: stage small light groups in LDS rows (chosen per run)
     DevBuf piv2;   // dependent -> second pivot (smallest light group after the pivot)
     bool sig_on = false;  // lsig holds this run's signatures (RDFIND_SIG=0 turns the filter off)
     bool sig_packed = false;  // the packed light path tests them too (RDFIND_SIG=1; default 2: k_light only)
@@ -256,7 +258,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->ginfo, &c->piv2, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->ginfo, &c->gsums, &c->piv2, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
@@ -1329,10 +1331,16 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     const u64 G = c->G;
     ENSURE(c, ginfo, std::max<u64>(G, 1) * 4);
     v.ginfo = c->ginfo.as<u32>();
+    const unsigned gi_grid = grid_for(std::max<u64>(G, 1), RDF_BLOCK, kGrid);
+    ENSURE(c, ppart, 3ull * gi_grid * 8);
+    ENSURE(c, gsums, 3 * 8);
     tbegin(c, RDF_T_PIVOT);
-    if (G)
-        hipLaunchKernelGGL(k_group_info, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(),
-                           c->hbit.as<uint8_t>(), G, c->ginfo.as<u32>());
+    HIP_TRY(c, hipMemsetAsync(c->gsums.p, 0, 3 * 8, st));
+    if (G) {
+        hipLaunchKernelGGL(k_group_info, dim3(gi_grid), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), c->hbit.as<uint8_t>(), G,
+                           c->ginfo.as<u32>(), c->ppart.as<u64>());
+        hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gi_grid, c->gsums.as<u64>());
+    }
     tend(c, RDF_T_PIVOT);
     static const int piv2_mode = getenv("RDFIND_PIV2") ? atoi(getenv("RDFIND_PIV2")) : 1;  // 2: k_light only
     const bool piv2_enabled = piv2_mode != 0;
@@ -1357,7 +1365,16 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
-    if (C) TRY(read_u64(c, c->psegoff.as<u64>() + C, &WS));
+    c->light_stage = false;
+    if (C) {
+        u64 r[3];
+        TRY(read_multi(c, {{c->psegoff.as<u64>() + C, 8}, {c->gsums.as<u64>(), 8}, {c->gsums.as<u64>() + 1, 8}}, r));
+        WS = r[0];
+        // member-weighted mean light group size sum(n^2) / sum(n): small groups -> the LDS-staging light variant
+        c->light_stage = r[2] <= (u64)LIGHT_STAGE_AVG * r[1];
+        static const char* force = getenv("RDFIND_STAGE");  // A/B and test hook: 0 / 1 forces the variant
+        if (force) c->light_stage = atoi(force) != 0;
+    }
     tbegin(c, RDF_T_PIVOT);
     if (WS)
         hipLaunchKernelGGL(k_pivot_seg, dim3(vgrid(wave_blocks(WS))), dim3(RDF_BLOCK),
@@ -1423,10 +1440,12 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
         hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
                            c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
-    if (WI)
-        hipLaunchKernelGGL(k_light, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
+    if (WI) {
+        auto kl = c->light_stage ? k_light<true> : k_light<false>;
+        hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
                            0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
                            c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+    }
     // chunks of dependents whose groups span several segments: emitted once all their segments are done
     u64 WM = 0;
     if (WI) {

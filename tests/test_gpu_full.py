@@ -110,3 +110,36 @@ def test_c3_full_sampled_direct_verification(ctx):
         jr = _capture_joins(d, rc, r1, r2)
         assert len(jd) == sup >= d.min_support
         assert np.isin(jd, jr).all()
+
+
+_VARIANT_CHILD = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from rdfind_amd import _lib, synth
+g = json.loads(sys.argv[2])
+d = synth.config(g["config"], g["scale"])
+with _lib.Context(0) as ctx:
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support, "spo", g["clean"], g["strategy"])
+    print(json.dumps({"n": ctx.cind_count(), "sum": str(ctx.checksum())}))
+"""
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("env", [{"RDFIND_STAGE": "0"}, {"RDFIND_STAGE": "1"},
+                                 {"RDFIND_SIG": "0", "RDFIND_PIV2": "0"}, {"RDFIND_SIG": "1", "RDFIND_PIV2": "2"}])
+def test_light_variants_full_size(env):
+    """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
+    paths, second pivot off / k_light only) each reproduce the c1 and c2 golden vectors.  The switches are read
+    once per process, so each combination runs in its own child process."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for key in ("c1@1.0/s1_clean", "c2@1.0/s1_clean"):
+        g = GOLD[key]
+        r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root, json.dumps(g)], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got = json.loads(r.stdout.strip().splitlines()[-1])
+        assert got["n"] == g["n_cinds"] and got["sum"] == g["checksum"], (key, env, got)
