@@ -22,7 +22,7 @@ static constexpr int FR_BITS = 14;             // rank blocks: frank_at adds bof
 static constexpr u32 FR_R = 1u << FR_BITS;
 static constexpr u32 U2_MAXB = 32768;          // K1 buckets (128 KB of LDS in the histogram passes)
 #ifndef RDF_U2_SLICE_LOG
-#define RDF_U2_SLICE_LOG 16
+#define RDF_U2_SLICE_LOG 15
 #endif
 static constexpr u64 U2_SLICE = 1ull << RDF_U2_SLICE_LOG;  // K1 records per counting block
 static constexpr int U2_CBLOCK = 1024;         // threads of a counting block
