@@ -344,6 +344,65 @@ __global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s
     }
 }
 
+// Second-level split for inputs whose hash buckets outgrow a counting slice (c3 at full size: 2^15 buckets of ~9k
+// records would all spill to the global table): one block per bucket re-partitions its records by the next `sub`
+// hash bits into S = 2^sub sub-buckets and writes their starts to bstart[b * S + j].  Counts and scatter slots come
+// from per-wave ballots over the S sub-buckets (one LDS atomic per wave and sub-bucket, never one per record: with
+// S <= 16 counters, per-record LDS atomics serialise).
+static constexpr int B2_SUB_MAX = 4;
+__device__ inline u32 b2_sub(u64 rec, int bits, int sub) {
+    return (u32)(mix64(rec & ~B2_CBITS) >> (64 - bits - sub)) & ((1u << sub) - 1);
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ rin, const u32* __restrict__ ghist, u32 NB,
+                                                        u32 G, int bits, int sub, u64* __restrict__ rout, u32* bstart) {
+    __shared__ u32 cnt[1 << B2_SUB_MAX];
+    const u32 S = 1u << sub;
+    const int lane = lane_id();
+    const u64 lt = lanemask_lt();
+    for (u32 b = blockIdx.x; b < NB; b += gridDim.x) {
+        const u64 start = ghist[(u64)b * G], end = ghist[(u64)(b + 1) * G];
+        if (threadIdx.x < S) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (u64 i0 = start + (threadIdx.x & ~(u64)(RDF_WAVE - 1)); i0 < end; i0 += RDF_BLOCK) {
+            const u64 i = i0 + lane;
+            const u32 j = i < end ? b2_sub(rin[i], bits, sub) : S;
+            for (u32 k = 0; k < S; ++k) {
+                const u64 m = __ballot(j == k);
+                if (lane == 0 && m) atomicAdd(&cnt[k], (u32)__popcll(m));
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            u32 run = 0;
+            for (u32 k = 0; k < S; ++k) {
+                const u32 c = cnt[k];
+                cnt[k] = run;
+                bstart[(u64)b * S + k] = (u32)start + run;
+                run += c;
+            }
+            if (b == NB - 1) bstart[(u64)NB * S] = (u32)end;
+        }
+        __syncthreads();
+        for (u64 i0 = start + (threadIdx.x & ~(u64)(RDF_WAVE - 1)); i0 < end; i0 += RDF_BLOCK) {
+            const u64 i = i0 + lane;
+            const u64 r = i < end ? rin[i] : 0;
+            const u32 j = i < end ? b2_sub(r, bits, sub) : S;
+            u32 pos = 0;
+            for (u32 k = 0; k < S; ++k) {
+                const u64 m = __ballot(j == k);
+                if (!m) continue;
+                const int leader = __ffsll((long long)m) - 1;
+                u32 base = 0;
+                if (lane == leader) base = atomicAdd(&cnt[k], (u32)__popcll(m));
+                base = __shfl(base, leader, RDF_WAVE);
+                if (j == k) pos = base + (u32)__popcll(m & lt);
+            }
+            if (i < end) rout[start + pos] = r;
+        }
+        __syncthreads();  // cnt is reused by the next bucket
+    }
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_b2_slices(const u32* __restrict__ ghist, u32 NB, u32 G, u32* nsl) {
     for (u32 b = blockIdx.x * RDF_BLOCK + threadIdx.x; b < NB; b += gridDim.x * RDF_BLOCK) {
         const u64 len = ghist[(u64)(b + 1) * G] - ghist[(u64)b * G];

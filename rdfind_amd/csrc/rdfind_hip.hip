@@ -73,6 +73,7 @@ struct rdf_ctx {
     DevBuf runoff, rundep;  // output run table: run r holds refs [runoff[r], runoff[r+1]) of dependent rundep[r]
     DevBuf nitl, itoffl, dead, ebin, pseg, psegoff, pbest, pnl;
     DevBuf lsig;          // light-group signatures (SIG_W words per compact capture), computed by the pivot pass
+    DevBuf brkeys2, bstart2;  // K2 records re-partitioned into sub-buckets (k_b2_split) and their starts
     DevBuf ginfo;  // group -> size | heavy bit (k_group_info)
     DevBuf gsums;  // sum of light group sizes, of their squares (k_group_info)
     bool light_stage = false;  // k_light<true>: stage small light groups in LDS rows (chosen per run)
@@ -258,7 +259,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->ginfo, &c->gsums, &c->piv2, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->brkeys2, &c->bstart2, &c->ginfo, &c->gsums, &c->piv2, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
@@ -773,11 +774,35 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
     hipLaunchKernelGGL((k_b2_part<true>), dim3(G2), dim3(B2_PBLOCK), lds, st, s, p, o, n, V, c->fbits.as<u64>(), bits,
                        c->uhist.as<u32>(), c->brkeys.as<u64>());
-    hipLaunchKernelGGL(k_b2_slices, dim3(grid_for(NB2, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(), NB2, G2,
+    // buckets that outgrow a counting slice are split by the next hash bits (RDFIND_B2_SPLIT=0: never)
+    // into sub-buckets of about 0.9 slice each (smaller ones pay the counting block's per-slice table setup for
+    // nothing); decided on the actual record count, read back only when the 3n bound says it may be needed
+    static const bool split_enabled = !getenv("RDFIND_B2_SPLIT") || atoi(getenv("RDFIND_B2_SPLIT")) != 0;
+    int sub = 0;
+    if (split_enabled && 3 * n > (u64)NB2 * B2_SLICE) {
+        u32 R = 0;
+        TRY(read_u32(c, c->uhist.as<u32>() + nh, &R));
+        while (sub < B2_SUB_MAX && (u64)R > ((u64)NB2 << sub) * (B2_SLICE * 9 / 10)) ++sub;
+    }
+    const u64* recs = c->brkeys.as<u64>();
+    const u32* bstart = c->uhist.as<u32>();
+    u32 NBc = NB2, Gc = G2;
+    if (sub) {
+        NBc = NB2 << sub;
+        Gc = 1;
+        ENSURE(c, brkeys2, maxrec * 8);
+        ENSURE(c, bstart2, ((u64)NBc + 1) * 4);
+        hipLaunchKernelGGL(k_b2_split, dim3(std::min<u32>(NB2, 4096)), dim3(RDF_BLOCK), 0, st, c->brkeys.as<u64>(),
+                           c->uhist.as<u32>(), NB2, G2, bits, sub, c->brkeys2.as<u64>(), c->bstart2.as<u32>());
+        recs = c->brkeys2.as<u64>();
+        bstart = c->bstart2.as<u32>();
+    }
+    ENSURE(c, usl, ((u64)NBc + 1) * 4);
+    hipLaunchKernelGGL(k_b2_slices, dim3(grid_for(NBc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, bstart, NBc, Gc,
                        c->usl.as<u32>());
-    HIP_TRY(c, exclusive_scan_u32(c->ws, c->usl.as<u32>(), c->usl.as<u32>(), NB2, c->usl.as<u32>() + NB2, st));
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->usl.as<u32>(), c->usl.as<u32>(), NBc, c->usl.as<u32>() + NBc, st));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 3), 0, 3 * 8, st));
-    hipLaunchKernelGGL(k_b2_count, dim3(256 * 3), dim3(RDF_BLOCK), 0, st, c->brkeys.as<u64>(), c->uhist.as<u32>(), c->usl.as<u32>(), NB2, G2, c->ms, c->bkeys.as<u64>(), c->tkeys.as<u64>(),
+    hipLaunchKernelGGL(k_b2_count, dim3(256 * 3), dim3(RDF_BLOCK), 0, st, recs, bstart, c->usl.as<u32>(), NBc, Gc, c->ms, c->bkeys.as<u64>(), c->tkeys.as<u64>(),
                        (u32*)c->pos.p, dscal(c, 3), partials ? 1 : 0);
     TRY(read_scalars(c, 6));
     *B = c->hscal[3];

@@ -22,7 +22,7 @@ for step in "$@"; do
       find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG.kernel_stats.csv \;
       head -25 gpurun_out/prof_$TAG.kernel_stats.csv ;;
     configs)  # the other BASELINE shapes on one GPU (c3 at half size: its generator runs ~2 min on the host)
-      for cfg in "c1 1.0" "c3 0.5" "c5 0.1" "c5 0.3"; do
+      for cfg in "c1 1.0" "c3 0.5" "c3 1.0" "c5 0.1" "c5 0.3"; do
         set -- $cfg
         echo "config $1 scale $2" >&2
         timeout -k 10 400 python -u bench.py --config $1 --scale $2 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest \
