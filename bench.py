@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
+RADIX_MAX_BITS = 9     # widest radix digit of the library's sorts (rdfind_amd/csrc/primitives.hip RS_MAX_BITS)
 
 # timer family -> its kernels, whose rocprofv3 PMC traffic (profiles/pmc_<config>.json, tools/pmc.sh) is summed
 FAMILY_KERNELS = {
@@ -79,7 +80,7 @@ def algorithmic_bytes(name, d, fc, gs, cs, counts):
     if name == "emit":
         return 12 * n + 8 * J                           # read triples, write (join, capture) records
     if name == "sort":
-        return 16 * counts["sort_passes_records"]       # read + write each record once per 8-bit pass
+        return 16 * counts["sort_passes_records"]       # read + write each record once per digit pass
     if name == "support":
         return 12 * J + 16 * Jf                         # read records + write fresh flags; dk + fk per kept record
     if name == "groups":
@@ -241,8 +242,9 @@ def main():
     V = d.num_terms
     capbits = int(2 * sum(fc["n_frequent_unary"]) + fc["n_frequent_binary"] - 1).bit_length()  # compact capture ids
     joinbits = max(int(V - 1).bit_length(), 1)
-    counts = {"sort_passes_records": ((capbits + joinbits + 7) // 8) * gs["n_records"],
-              "group_passes": (joinbits + 7) // 8}
+    rs = RADIX_MAX_BITS  # digits of <= 10 bits (primitives.hip RS_MAX_BITS)
+    counts = {"sort_passes_records": ((capbits + joinbits + rs - 1) // rs) * gs["n_records"],
+              "group_passes": (joinbits + rs - 1) // rs}
     fams = family_rooflines(d, fc, gs, cs, kt, counts)
     if args.scale == 1.0 and world == 1:  # HBM bytes per step from the committed PMC summary of this config
         for name, f in fams.items():

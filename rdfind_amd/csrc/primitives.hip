@@ -2,10 +2,10 @@
 //
 // The radix sort is the grouping engine that replaces Flink's sort-based groupBy on the join value
 // (ALG/programs/RDFind.scala:339-345 groupBy("joinValue") -> combineGroup -> reduceGroup): records are
-// packed as (capture << joinbits | join) and sorted on exactly the needed bits, 8 bits per pass.
-// Per pass: (1) per-tile 256-bin digit histogram in LDS, (2) device exclusive scan of the digit-major
-// histogram, (3) stable scatter where each key's in-tile rank comes from wave ballots (8 ballots give
-// the peer mask of lanes with the same digit) plus per-wave running digit counters in LDS.
+// packed as (capture << joinbits | join) and sorted on exactly the needed bits, in as few passes of <= 10-bit
+// digits as cover them (43 bits: 9+9+9+8+8).  Per pass: (1) per-tile digit histogram in LDS, (2) device exclusive
+// scan of the digit-major histogram, (3) stable scatter where each key's in-tile rank comes from wave ballots (one
+// ballot per digit bit gives the peer mask of lanes with the same digit) plus per-wave running digit counters in LDS.
 #include "primitives.hpp"
 
 namespace rdf {
@@ -188,11 +188,13 @@ static constexpr int RS_ITEMS = 16;                              // keys per lan
 static constexpr int RS_TILE = RDF_BLOCK * RS_ITEMS;             // 4096 keys per tile
 static constexpr int RS_WAVE_KEYS = RDF_WAVE * RS_ITEMS;         // 1024 keys per wave
 
-// lanes of the wave whose key is valid and has the same 8-bit digit as this lane (0 for invalid lanes)
+
+// lanes of the wave whose key is valid and has the same DB-bit digit as this lane (0 for invalid lanes)
+template <int DB>
 __device__ inline u64 digit_peers(u32 d, bool valid) {
     u64 peers = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < DB; ++b) {
         const u64 bb = __ballot((d >> b) & 1);
         peers &= ((d >> b) & 1) ? bb : ~bb;
     }
@@ -217,13 +219,16 @@ __device__ inline void load_tile_pairs(const u64* __restrict__ keys, u64 n, u64 
     }
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict__ keys, u64 n, int shift,
+// Digits of DB bits (the pass's width w <= DB is masked at run time: DB only sizes the LDS counters)
+template <int DB>
+__global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict__ keys, u64 n, int shift, int w,
                                                            u32* __restrict__ hist, u32 num_tiles) {
-    __shared__ u32 wcnt[RDF_WAVES_PER_BLOCK][256];
+    constexpr u32 NBIN = 1u << DB;
+    __shared__ u32 wcnt[RDF_WAVES_PER_BLOCK][NBIN];
     const int lane = lane_id();
     const int wave = threadIdx.x / RDF_WAVE;
-#pragma unroll
-    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) wcnt[w][threadIdx.x] = 0;
+    const u32 dmask = (1u << w) - 1u;
+    for (u32 i = threadIdx.x; i < RDF_WAVES_PER_BLOCK * NBIN; i += RDF_BLOCK) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const u64 tbase = (u64)blockIdx.x * RS_TILE;
     u64 k[RS_ITEMS];
@@ -232,29 +237,36 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
     for (int r = 0; r < RS_ITEMS; ++r) {
         const u64 idx = tbase + 2ull * ((u64)(r / 2) * RDF_BLOCK + threadIdx.x) + (r & 1);
         const bool valid = idx < n;
-        const u32 d = (u32)((k[r] >> shift) & 255);
-        const u64 peers = digit_peers(d, valid);
+        const u32 d = (u32)(k[r] >> shift) & dmask;
+        const u64 peers = digit_peers<DB>(d, valid);
         if (valid && ((peers >> lane) >> 1) == 0) wcnt[wave][d] += (u32)__popcll(peers);
     }
     __syncthreads();
-    u32 sum = 0;
+    for (u32 b = threadIdx.x; b <= dmask; b += RDF_BLOCK) {
+        u32 sum = 0;
 #pragma unroll
-    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) sum += wcnt[w][threadIdx.x];
-    hist[(u64)threadIdx.x * num_tiles + blockIdx.x] = sum;
+        for (int ww = 0; ww < RDF_WAVES_PER_BLOCK; ++ww) sum += wcnt[ww][b];
+        hist[(u64)b * num_tiles + blockIdx.x] = sum;
+    }
 }
 
+template <int DB>
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
-                                                             int shift, const u32* __restrict__ offs, u32 num_tiles) {
+                                                             int shift, int w, const u32* __restrict__ offs,
+                                                             u32 num_tiles) {
+    constexpr u32 NBIN = 1u << DB;
+    constexpr u32 PER = NBIN / RDF_BLOCK;  // digits per thread in the tile scan (1, 2 or 4)
+    static_assert(NBIN % RDF_BLOCK == 0, "digit bins must be a multiple of the block");
     __shared__ __align__(16) u64 skeys[RS_TILE];
-    __shared__ u32 wcount[RDF_WAVES_PER_BLOCK][256];
-    __shared__ u32 tstart[256];
-    __shared__ u32 gbase[256];
+    __shared__ u32 wcount[RDF_WAVES_PER_BLOCK][NBIN];
+    __shared__ u32 tstart[NBIN];
+    __shared__ u32 gbase[NBIN];
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
     const int lane = lane_id();
     const int wave = threadIdx.x / RDF_WAVE;
-#pragma unroll
-    for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) wcount[w][threadIdx.x] = 0;
-    gbase[threadIdx.x] = offs[(u64)threadIdx.x * num_tiles + blockIdx.x];
+    const u32 nbin = 1u << w, dmask = nbin - 1u;
+    for (u32 i = threadIdx.x; i < RDF_WAVES_PER_BLOCK * NBIN; i += RDF_BLOCK) (&wcount[0][0])[i] = 0;
+    for (u32 b = threadIdx.x; b < nbin; b += RDF_BLOCK) gbase[b] = offs[(u64)b * num_tiles + blockIdx.x];
     const u64 tbase = (u64)blockIdx.x * RS_TILE;
     const u64 tn = n - tbase < (u64)RS_TILE ? n - tbase : (u64)RS_TILE;
     {   // stage the tile through LDS: 16-byte global loads, then each wave reads its contiguous sub-range
@@ -276,8 +288,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn;
-        const u32 d = (u32)((k[r] >> shift) & 255);
-        const u64 peers = digit_peers(d, valid);
+        const u32 d = (u32)(k[r] >> shift) & dmask;
+        const u64 peers = digit_peers<DB>(d, valid);
         const u32 before = (u32)__popcll(peers & lt);
         const u32 old = valid ? wcount[wave][d] : 0;
         // the highest peer lane publishes the new running count (reads above precede this write)
@@ -285,22 +297,34 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
         rank[r] = old + before;
     }
     __syncthreads();
-    {   // exclusive prefix over waves per digit, then over digits for the tile
-        u32 run = 0;
+    {   // exclusive prefix over waves per digit, then over digits for the tile (PER consecutive digits a thread)
+        u32 run[PER], local = 0;
 #pragma unroll
-        for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
-            const u32 c = wcount[w][threadIdx.x];
-            wcount[w][threadIdx.x] = run;
-            run += c;
+        for (u32 q = 0; q < PER; ++q) {
+            const u32 dg = threadIdx.x * PER + q;
+            u32 acc = 0;
+#pragma unroll
+            for (int ww = 0; ww < RDF_WAVES_PER_BLOCK; ++ww) {
+                const u32 c = wcount[ww][dg];
+                wcount[ww][dg] = acc;
+                acc += c;
+            }
+            run[q] = acc;
+            local += acc;
         }
         u32 total;
-        tstart[threadIdx.x] = block_exclusive_scan<u32>(run, lds_wave, &total);
+        u32 off = block_exclusive_scan<u32>(local, lds_wave, &total);
+#pragma unroll
+        for (u32 q = 0; q < PER; ++q) {
+            tstart[threadIdx.x * PER + q] = off;
+            off += run[q];
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         if (wofs + (u32)r * RDF_WAVE + lane < tn) {
-            const u32 d = (u32)((k[r] >> shift) & 255);
+            const u32 d = (u32)(k[r] >> shift) & dmask;
             skeys[tstart[d] + wcount[wave][d] + rank[r]] = k[r];
         }
     }
@@ -310,27 +334,43 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
         const u32 p = (u32)i * RDF_BLOCK + threadIdx.x;
         if (p < tn) {
             const u64 key = skeys[p];
-            const u32 d = (u32)((key >> shift) & 255);
+            const u32 d = (u32)(key >> shift) & dmask;
             out[(u64)gbase[d] + (p - tstart[d])] = key;
         }
     }
 }
 
+template <int DB>
+static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, int shift, int w, u32* hist, u32 tiles,
+                             hipStream_t st) {
+    const u64 hn = (u64)tiles << w;
+    hipLaunchKernelGGL(k_radix_count<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, tiles);
+    hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, nullptr, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_radix_scatter<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, tiles);
+    return hipSuccess;
+}
+
+// Passes of at most RS_MAX_BITS bits, as even as possible (43 bits: 9+9+9+8+8 instead of six 8-bit passes)
 hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st) {
     if (n < 2 || hi <= lo) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
-    const u64 hn = (u64)tiles * 256;
-    u32* hist = (u32*)ws.scratch(hn * sizeof(u32), 1);
+    const int bits = hi - lo;
+    const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
+    u32* hist = (u32*)ws.scratch(((u64)tiles << RS_MAX_BITS) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
-    for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL(k_radix_count, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, hist, tiles);
-        hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, nullptr, st);
+    int shift = lo;
+    for (int p = 0; p < passes; ++p) {
+        const int w = bits / passes + (p < bits % passes ? 1 : 0);  // the wider digits first
+        hipError_t e = w <= 8 ? radix_pass<8>(ws, keys, tmp, n, shift, w, hist, tiles, st)
+                     : w == 9 ? radix_pass<9>(ws, keys, tmp, n, shift, w, hist, tiles, st)
+                              : radix_pass<10>(ws, keys, tmp, n, shift, w, hist, tiles, st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_radix_scatter, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, hist, tiles);
         u64* t = keys;
         keys = tmp;
         tmp = t;
+        shift += w;
     }
     return hipGetLastError();
 }

@@ -83,6 +83,11 @@ hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32
 hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st);
 // Stable sort on bits [lo, hi) only (8 bits per pass from lo; bits at or above the last pass's top must be
 // zero or already ordered).  Keys that arrive ordered by their low bits stay so within equal [lo, hi).
+#ifndef RDF_RS_MAX_BITS
+#define RDF_RS_MAX_BITS 9
+#endif
+static constexpr int RS_MAX_BITS = RDF_RS_MAX_BITS;  // widest radix digit (8: the old 8-bit passes)
+static_assert(RS_MAX_BITS >= 8 && RS_MAX_BITS <= 10, "digit kernels exist for 8, 9 and 10 bits");
 hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st);
 
 }  // namespace rdf

@@ -1067,7 +1067,7 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     HIP_TRY(c, radix_sort_u64(c->ws, keys, tmp, J, capbits + joinbits, st));
     tend(c, RDF_T_SORT);
     c->rec_sorted = keys;
-    c->sort_passes_records = (u64)((capbits + joinbits + 7) / 8) * J;
+    c->sort_passes_records = (u64)((capbits + joinbits + RS_MAX_BITS - 1) / RS_MAX_BITS) * J;
     // supports = distinct join values per capture: fresh (capture, join) records counted per key run
     ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
     ENSURE(c, flags, std::max<u64>(J, 1) * 4);
@@ -1533,7 +1533,7 @@ static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorte
     hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->epairs.as<u64>(), E, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
     tend(c, RDF_T_ESORT);
-    c->sort_passes_pairs = presorted ? 0 : (u64)((32 + bits_for(C ? C - 1 : 0) + 7) / 8) * E;
+    c->sort_passes_pairs = presorted ? 0 : (u64)((32 + bits_for(C ? C - 1 : 0) + RS_MAX_BITS - 1) / RS_MAX_BITS) * E;
     v.eoff = c->eoff.as<u64>();
     v.epairs = c->epairs.as<u64>();
     v.ebin = c->ebin.as<u64>();
