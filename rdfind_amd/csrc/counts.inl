@@ -353,22 +353,42 @@ static constexpr int B2_SUB_MAX = 4;
 __device__ inline u32 b2_sub(u64 rec, int bits, int sub) {
     return (u32)(mix64(rec & ~B2_CBITS) >> (64 - bits - sub)) & ((1u << sub) - 1);
 }
+static constexpr int B2_SPLIT_R = 8;  // records per lane in flight in k_b2_split
+
+// lanes of the wave with the same sub-bucket j (j < 2^sub; inactive lanes pass j = 1 << sub and get 0)
+__device__ inline u64 sub_peers(u32 j, int sub) {
+    const bool act = j < (1u << sub);
+    u64 peers = __ballot(act);
+    for (int b = 0; b < sub; ++b) {
+        const u64 bb = __ballot((j >> b) & 1);
+        peers &= ((j >> b) & 1) ? bb : ~bb;
+    }
+    return act ? peers : 0ull;
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ rin, const u32* __restrict__ ghist, u32 NB,
                                                         u32 G, int bits, int sub, u64* __restrict__ rout, u32* bstart) {
     __shared__ u32 cnt[1 << B2_SUB_MAX];
     const u32 S = 1u << sub;
     const int lane = lane_id();
     const u64 lt = lanemask_lt();
+    const u64 wave0 = (threadIdx.x / RDF_WAVE) * (u64)(RDF_WAVE * B2_SPLIT_R);
+    constexpr u64 STEP = (u64)RDF_BLOCK * B2_SPLIT_R;
     for (u32 b = blockIdx.x; b < NB; b += gridDim.x) {
         const u64 start = ghist[(u64)b * G], end = ghist[(u64)(b + 1) * G];
         if (threadIdx.x < S) cnt[threadIdx.x] = 0;
         __syncthreads();
-        for (u64 i0 = start + (threadIdx.x & ~(u64)(RDF_WAVE - 1)); i0 < end; i0 += RDF_BLOCK) {
-            const u64 i = i0 + lane;
-            const u32 j = i < end ? b2_sub(rin[i], bits, sub) : S;
-            for (u32 k = 0; k < S; ++k) {
-                const u64 m = __ballot(j == k);
-                if (lane == 0 && m) atomicAdd(&cnt[k], (u32)__popcll(m));
+        for (u64 i0 = start + wave0; i0 < end; i0 += STEP) {  // B2_SPLIT_R coalesced loads per lane in flight
+            u32 j[B2_SPLIT_R];
+#pragma unroll
+            for (int k = 0; k < B2_SPLIT_R; ++k) {
+                const u64 i = i0 + (u64)k * RDF_WAVE + lane;
+                j[k] = i < end ? b2_sub(rin[i], bits, sub) : S;
+            }
+#pragma unroll
+            for (int k = 0; k < B2_SPLIT_R; ++k) {
+                const u64 peers = sub_peers(j[k], sub);
+                if (peers && ((peers >> lane) >> 1) == 0) atomicAdd(&cnt[j[k]], (u32)__popcll(peers));  // top peer
             }
         }
         __syncthreads();
@@ -383,21 +403,24 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ 
             if (b == NB - 1) bstart[(u64)NB * S] = (u32)end;
         }
         __syncthreads();
-        for (u64 i0 = start + (threadIdx.x & ~(u64)(RDF_WAVE - 1)); i0 < end; i0 += RDF_BLOCK) {
-            const u64 i = i0 + lane;
-            const u64 r = i < end ? rin[i] : 0;
-            const u32 j = i < end ? b2_sub(r, bits, sub) : S;
-            u32 pos = 0;
-            for (u32 k = 0; k < S; ++k) {
-                const u64 m = __ballot(j == k);
-                if (!m) continue;
-                const int leader = __ffsll((long long)m) - 1;
-                u32 base = 0;
-                if (lane == leader) base = atomicAdd(&cnt[k], (u32)__popcll(m));
-                base = __shfl(base, leader, RDF_WAVE);
-                if (j == k) pos = base + (u32)__popcll(m & lt);
+        for (u64 i0 = start + wave0; i0 < end; i0 += STEP) {
+            u64 r[B2_SPLIT_R];
+#pragma unroll
+            for (int k = 0; k < B2_SPLIT_R; ++k) {
+                const u64 i = i0 + (u64)k * RDF_WAVE + lane;
+                r[k] = i < end ? rin[i] : 0;
             }
-            if (i < end) rout[start + pos] = r;
+#pragma unroll
+            for (int k = 0; k < B2_SPLIT_R; ++k) {
+                const u64 i = i0 + (u64)k * RDF_WAVE + lane;
+                const u32 jj = i < end ? b2_sub(r[k], bits, sub) : S;
+                const u64 peers = sub_peers(jj, sub);
+                const int top = peers ? 63 - __clzll((long long)peers) : lane;
+                u32 base = 0;
+                if (peers && lane == top) base = atomicAdd(&cnt[jj], (u32)__popcll(peers));
+                base = __shfl(base, top, RDF_WAVE);  // each lane reads its own group's top peer
+                if (i < end) rout[start + base + (u32)__popcll(peers & lt)] = r[k];
+            }
         }
         __syncthreads();  // cnt is reused by the next bucket
     }
