@@ -268,6 +268,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_fbits_from_counts(const u32* __re
 // ---- K2 ----------------------------------------------------------------------------------------
 
 static constexpr u64 B2_SLICE = 2560;          // K2 records per counting slice (table: next power of two >= 2x, <= B2_SLOTS)
+#ifndef RDF_B2_CR
+#define RDF_B2_CR 10
+#endif
+static constexpr int B2_CR = RDF_B2_CR;        // slice records per counting thread loaded together (10 x 256 = a slice)
 
 __device__ inline u32 b2_bucket(u64 key, int bits) { return (u32)(mix64(key) >> (64 - bits)); }
 
@@ -467,8 +471,25 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_count(const u64* __restrict__ 
             tc[i] = 0;
         }
         __syncthreads();
-        for (u64 i = s0 + threadIdx.x; i < s1; i += RDF_BLOCK) {
-            const u64 rec = rkeys[i];
+        // the slice's records (<= B2_CR per thread) are loaded up front: one round trip, not one per record
+        u64 rr[B2_CR];
+#pragma unroll
+        for (int q = 0; q < B2_CR; ++q) {
+            const u64 i = s0 + (u64)q * RDF_BLOCK + threadIdx.x;
+            rr[q] = i < s1 ? rkeys[i] : 0;
+        }
+        for (u64 i0 = s0; i0 < s1; i0 += (u64)RDF_BLOCK * B2_CR) {
+          if (i0 != s0) {  // slices longer than B2_CR x RDF_BLOCK (only with RDF_B2_CR below the default)
+#pragma unroll
+            for (int q = 0; q < B2_CR; ++q) {
+                const u64 i = i0 + (u64)q * RDF_BLOCK + threadIdx.x;
+                rr[q] = i < s1 ? rkeys[i] : 0;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < B2_CR; ++q) {
+            if (i0 + (u64)q * RDF_BLOCK + threadIdx.x >= s1) continue;
+            const u64 rec = rr[q];
             const u64 key = rec & ~B2_CBITS;
             const u32 c = b2_count_of(rec);
             u32 h = (u32)mix64(key) & (T - 1);  // low hash bits (the bucket used the high ones)
@@ -490,6 +511,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_count(const u64* __restrict__ 
                 spill_keys[at] = key;
                 spill_cnt[at] = c;
             }
+          }
         }
         __syncthreads();
         const u32 per = (T + RDF_BLOCK - 1) / RDF_BLOCK;  // consecutive slots per thread
