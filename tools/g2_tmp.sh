@@ -1,7 +1,5 @@
-# ad-hoc GPU step of the current session (dev): smoke, a quick c2 bench, and c4 at 0.05 / c3 full bench lines
+# ad-hoc GPU step of the current session (dev): c4 light switches A/B and per-item light profile
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp &&
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r02.log 2>&1 &&
-timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-ingest --no-tdisc > gpurun_out/bench_final_quick.json 2> gpurun_out/bench_final_quick.err &&
-timeout -k 10 400 python -u bench.py --config c4 --scale 0.05 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-tdisc > gpurun_out/cfg_c4_0.05.json 2> gpurun_out/cfg_c4_0.05.err &&
-timeout -k 10 400 python -u bench.py --config c3 --scale 1.0 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest --no-tdisc > gpurun_out/cfg_c3_1.0.json 2> gpurun_out/cfg_c3_1.0.err
-rc=$?; tail -2 gpurun_out/smoke_r02.log; cut -c1-200 gpurun_out/bench_final_quick.json gpurun_out/cfg_c4_0.05.json gpurun_out/cfg_c3_1.0.json; exit $rc
+RDFIND_AB_LIBS="librdfind_hip.so,librdfind_hip.so@RDFIND_STAGE=1,librdfind_hip.so@RDFIND_SIG=1,librdfind_hip.so@RDFIND_SIG=0,librdfind_hip.so@RDFIND_PIV2=0" timeout -k 10 400 python -u tools/light_ab.py c4:0.05 > gpurun_out/g26_ab.log 2>&1 &&
+timeout -k 10 300 python -u tools/light_items.py c4 0.05 > gpurun_out/g26_items_c4.log 2>&1
+rc=$?; cat gpurun_out/g26_ab.log; tail -40 gpurun_out/g26_items_c4.log; exit $rc
