@@ -12,7 +12,7 @@ For N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL over xGMI) 
 (rdfind_amd/distributed.py): each rank holds only its slice of the triples
 (synth.config_slice), the condition counts are summed over ranks, every triple travels to the ranks owning
 its join values, each rank builds the capture groups of its join-value hash shard and owns the dependents
-d % N; the twelve collectives of the protocol run inside the timed region.  `value` is the workload's
+d % N; the thirteen collectives of the protocol run inside the timed region.  `value` is the workload's
 triples divided by the max-over-ranks time per step (the default c2 workload is split over the ranks:
 strong scaling; `--config c4` draws 1B/N rows per rank).  `roofline` is computed for the dominant kernel
 family from HIP events recorded on the library's stream; `cpu_baseline` times the C restatement (oracle/,
