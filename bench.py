@@ -1,22 +1,23 @@
 """Benchmark: CIND-discovery triples/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--scale 1.0]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--scale 1.0] [--scaling weak|strong]
 
-A *step* is one pass of the hot path over one batch: rdf_run = frequent conditions -> capture groups
--> CIND extraction + --clean-implied minimality (strategy 1, the reference default), with the
-dictionary-encoded triples already resident in HBM and the CIND id-records left in HBM (the
-PCIe-inclusive rate is reported separately in DESIGN.md).  Workload: BASELINE configs[1] =
-LUBM-100-shaped synthetic triples (~13.4M), support 10, one MI355X.
+A *step* is T_disc of SURVEY.md 8(d) / BASELINE.md 2 over one batch: from dictionary-encoded triples resident
+in HBM to CIND id-records in host memory.  rdf_run = frequent conditions -> capture groups -> CIND extraction +
+--clean-implied minimality (strategy 1, the reference default), then rdf_copy_result_compact hands the
+CindSet-shaped result (explicit ref runs + the shared ref lists of the mask classes, ALG/data/CindSet.scala:9-13)
+to pinned host memory.  `value` = triples / step time.  Workload at N = 1: BASELINE configs[1] = LUBM-100-shaped
+synthetic triples (12.7M), support 10, one MI355X.  `device_resident` repeats the steps without the hand-over.
 
-For N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL over xGMI) the workload is sharded
-(rdfind_amd/distributed.py): each rank holds only its slice of the triples
-(synth.config_slice), the condition counts are summed over ranks, every triple travels to the ranks owning
-its join values, each rank builds the capture groups of its join-value hash shard and owns the dependents
-d % N; the thirteen collectives of the protocol run inside the timed region.  `value` is the workload's
-triples divided by the max-over-ranks time per step (the default c2 workload is split over the ranks:
-strong scaling; `--config c4` draws 1B/N rows per rank).  `roofline` is computed for the dominant kernel
-family from HIP events recorded on the library's stream; `cpu_baseline` times the C restatement (oracle/,
-OpenMP) on rank 0.
+N > 1: one rank per GPU under torch.distributed.run (started by this script when no launcher is used), RCCL over
+xGMI; the workload is sharded (rdfind_amd/distributed.py): each rank holds only its slice of the
+triples (synth.config_slice), the condition counts are summed over ranks, every triple travels to the ranks
+owning its join values, each rank builds the capture groups of its join-value hash shard and owns the
+dependents d % N; the protocol's collectives run inside the timed region and every rank hands over its own
+result.  Default weak scaling: N GPUs run the config at N x scale (c2: LUBM-(100 N)), so each GPU holds one
+LUBM-100-sized share; `value` = all triples / max-over-ranks step time.  `roofline` is computed for the dominant
+kernel family from HIP events recorded on the library's stream; `cpu_baseline` times the C restatement
+(oracle/, OpenMP) on rank 0.
 """
 from __future__ import annotations
 
@@ -114,61 +115,87 @@ def family_rooflines(d, fc, gs, cs, kt, counts):
     return out
 
 
-def t_disc_host(ctx, ms, reps=3):
-    """SURVEY.md 8(d) T_disc: triples resident in HBM -> CIND id-records in host memory (one step + the copy of the
-    CindSet-shaped result, rdf_copy_result_raw, into pinned host memory).  Returns (median ms, details)."""
-    import numpy as np
-    n_refs, n_runs, n_caps = ctx.result_sizes()
-    pinned = True
-    try:
-        import torch
-        refs = torch.empty(max(n_refs, 1), dtype=torch.int32, pin_memory=True)
-        refs_ptr = refs.data_ptr()
-    except Exception:  # no pinned pool: pageable numpy (slower link rate, stated in the line)
-        pinned = False
-        refs = np.empty(max(n_refs, 1), np.uint32)
-        refs_ptr = refs.ctypes.data
-    runoff = np.empty(n_runs + 1, np.uint64)
-    rundep = np.empty(max(n_runs, 1), np.uint32)
-    caps = np.empty(max(n_caps, 1), np.uint32)
-    sups = np.empty(max(n_caps, 1), np.uint32)
-    times, copy_ms = [], []
-    for _ in range(reps):
-        ctx.sync()
-        t0 = time.perf_counter()
-        ctx.run(ms)
-        ctx.sync()
-        t1 = time.perf_counter()
-        ctx.copy_result_raw(refs_ptr, runoff, rundep, caps, sups)
-        t2 = time.perf_counter()
-        times.append((t2 - t0) * 1e3)
-        copy_ms.append((t2 - t1) * 1e3)
-    med = sorted(times)[len(times) // 2]
-    cm = sorted(copy_ms)[len(copy_ms) // 2]
-    nbytes = 4 * n_refs + 12 * n_runs + 8 * n_caps
-    del refs
-    return med, {"ms": round(med, 3), "copy_ms": round(cm, 3), "bytes": nbytes,
-                 "link_gbs": round(nbytes / (cm * 1e-3) / 1e9, 1) if cm > 0 else None, "pinned": pinned}
+class CompactSink:
+    """Pinned host buffers for the compact CindSet-shaped result (rdf_copy_result_compact): the id-records the
+    metric's T_disc ends with.  Sized from the first run's layout, grown if a run needs more."""
+
+    def __init__(self):
+        self.bufs, self.cap, self.pinned, self._keep = None, {}, True, []
+
+    def ensure(self, ctx):
+        from rdfind_amd import _lib
+        L = ctx.result_layout()
+        need = {name: max(count(L), 1) for name, _, count in _lib.COMPACT_PARTS}
+        if self.bufs is not None and all(need[k] <= self.cap[k] for k in need):
+            return L
+        self.bufs, self._keep = {}, []
+        for name, dt, _ in _lib.COMPACT_PARTS:
+            n = need[name]
+            try:
+                import torch
+                t = torch.empty(n * np.dtype(dt).itemsize, dtype=torch.uint8, pin_memory=True)
+                self._keep.append(t)
+                self.bufs[name] = t.data_ptr()
+            except Exception:  # no pinned pool: pageable numpy (slower link rate, stated in the line)
+                self.pinned = False
+                a = np.empty(n, dt)
+                self._keep.append(a)
+                self.bufs[name] = a.ctypes.data
+        self.cap = need
+        return L
+
+    def copy(self, ctx):
+        L = self.ensure(ctx)
+        ctx.copy_result_compact(self.bufs)
+        return L
+
+
+def layout_bytes(L):
+    return (4 * L["n_refs"] + 12 * L["n_runs"] + 8 + 4 * L["n_list_refs"] + 8 * (L["n_lists"] + 1) +
+            8 * L["n_members"] + 8 * L["n_captures"])
+
+
+def launch_ranks(nranks, argv):
+    """--gpus N without a launcher: one rank per GPU under torch.distributed.run, started as child processes before
+    this process touches a GPU (rdfind_amd/program.py launch_ranks); returns their exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default: WORLD_SIZE or 1.  Without a "
+                    "launcher, N > 1 starts N ranks under torch.distributed.run itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2")
-    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--scale", type=float, default=1.0, help="per-GPU scale of the config (weak scaling) or the "
+                    "total scale (--scaling strong)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: every GPU holds one config-sized share (N GPUs run the config at N x scale); "
+                         "strong: the config at scale is split over the GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the N-Triples ingest leg (rank 0, N=1)")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.3)
     ap.add_argument("--cpu-full-max", type=int, default=20_000_000,
                     help="time the CPU baseline on the benchmarked workload itself up to this many triples")
-    ap.add_argument("--no-tdisc", action="store_true", help="skip the T_disc (id-records to host) leg")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
                     "exchanges, to rehearse several ranks on one GPU)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:  # self-launch before any GPU call
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -182,30 +209,46 @@ def main():
 
     from rdfind_amd import _lib, synth
 
+    total_scale = args.scale * world if args.scaling == "weak" else args.scale
     if dist is not None:  # each rank holds only its slice of the input (sharded input)
-        d, total_n = synth.config_slice(args.config, args.scale, rank, world)
+        d, total_n = synth.config_slice(args.config, total_scale, rank, world)
     else:
-        d = synth.config(args.config, args.scale)
+        d = synth.config(args.config, total_scale)
         total_n = d.n
     ms = d.min_support
     ctx = _lib.Context(local_rank)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
+    sink = CompactSink()
 
     if dist is not None:
         from rdfind_amd import distributed
 
-        def step():
+        def discover():
             distributed.run_sharded(ctx, ms, local_slice=True)
             return ctx.cinds
     else:
-        def step():
+        def discover():
             return ctx.run(ms)
+
+    def step():  # T_disc: encoded triples in HBM -> compact CIND id-records in (pinned) host memory
+        cs = discover()
+        sink.copy(ctx)
+        return cs
 
     def barrier():
         if dist is not None:
             import torch
             dist.barrier()
             torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        dev = f"cuda:{local_rank}" if args.backend == "nccl" else "cpu"
+        t = torch.tensor([x], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     for _ in range(args.warmup):
         step()
@@ -219,22 +262,27 @@ def main():
             kt_sum[k] = kt_sum.get(k, 0.0) + v
     ctx.sync()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    L = ctx.result_layout()
+    # the same steps without the hand-over (results left in HBM): the device-resident rate
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        discover()
+    ctx.sync()
+    barrier()
+    elapsed_dev = max_over_ranks(time.perf_counter() - t1)
     if dist is not None:
         import torch
         dev = f"cuda:{local_rank}" if args.backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([cs["n_cinds"]], device=dev, dtype=torch.int64)
+        tot = torch.tensor([cs["n_cinds"], layout_bytes(L)], device=dev, dtype=torch.int64)
         dist.all_reduce(tot)
-        total_cinds = int(tot.item())
+        total_cinds, total_bytes = (int(x) for x in tot.tolist())
     else:
-        total_cinds = cs["n_cinds"]
-    total_triples = float(total_n)
+        total_cinds, total_bytes = cs["n_cinds"], layout_bytes(L)
     steps = max(args.steps, 1)
     ms_per_step = elapsed * 1000.0 / steps
-    value = total_triples * steps / elapsed
+    value = float(total_n) * steps / elapsed
 
     gs, fc = ctx.groups, ctx.fc
     kt = {k: v / steps for k, v in kt_sum.items()}
@@ -246,7 +294,7 @@ def main():
     counts = {"sort_passes_records": ((capbits + joinbits + rs - 1) // rs) * gs["n_records"],
               "group_passes": (joinbits + rs - 1) // rs}
     fams = family_rooflines(d, fc, gs, cs, kt, counts)
-    if args.scale == 1.0 and world == 1:  # HBM bytes per step from the committed PMC summary of this config
+    if total_scale == 1.0 and world == 1:  # HBM bytes per step from the committed PMC summary of this config
         for name, f in fams.items():
             t = pmc_traffic(args.config, name)
             if t is not None:
@@ -258,46 +306,38 @@ def main():
         if name in fams:
             f = fams[name]
             roof = {"bound": "hbm", "kernel": name, "achieved": f["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": f["frac"], "traffic": pmc_traffic(args.config, name) if args.scale == 1.0 and world == 1 else None,
-                    "ms": f["ms"], "bytes_per_launch": f["bytes"], "dominant_kernel": dominant,
-                    "dominant_ms": round(kt[dominant], 4)}
+                    "frac": f["frac"], "traffic": f.get("traffic"), "ms": f["ms"], "bytes_per_launch": f["bytes"],
+                    "dominant_kernel": dominant, "dominant_ms": round(kt[dominant], 4)}
             break
 
     # BASELINE metric also names "% HBM roofline of count kernels": K1 (unary) and K2 (binary condition counts)
     count_roof = {k: dict(fams[k], bound="hbm") for k in ("unary", "binary") if k in fams}
-
-    tdisc = None
-    if rank == 0 and world == 1 and not args.no_tdisc:
-        tms, tdisc = t_disc_host(ctx, ms)
-        tdisc["triples_per_s"] = round(d.n / (tms * 1e-3), 1)
-        tdisc["note"] = ("SURVEY.md 8(d) T_disc: one step + copy of the CindSet-shaped id-records (4 B per CIND + run "
-                         "table) to host memory; median of 3")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import c_oracle
 
         # the same workload when the streamed C restatement finishes in ~30 s on the box's threads, else a sample
-        cpu_scale = args.scale if d.n <= args.cpu_full_max else args.cpu_sample_scale
-        sd = d if cpu_scale == args.scale else synth.config(args.config, cpu_scale)
+        cpu_scale = total_scale if d.n <= args.cpu_full_max else args.cpu_sample_scale
+        sd = d if cpu_scale == total_scale else synth.config(args.config, cpu_scale)
         t = time.perf_counter()
         r = c_oracle.stream(sd.s, sd.p, sd.o, sd.num_terms, sd.min_support, 1, True)
         ct = time.perf_counter() - t
         nt = c_oracle.threads()
-        same = cpu_scale == args.scale
+        same = cpu_scale == total_scale
         cpu = {"value": round(sd.n / ct, 1), "unit": "triples/s", "cores": nt, "kind": "port",
                "sample": f"{args.config} scale {cpu_scale} ({sd.n} triples, {r['n_cinds']} CINDs"
                          f"{', the benchmarked workload itself' if same else ''}) through oracle/c/rdfind_oracle.c "
                          f"(streamed count + checksum, same stages incl. minimality) on {nt} OpenMP threads, {ct:.1f}s"}
         if same:
-            cpu["matches_gpu"] = bool(r["n_cinds"] == cs["n_cinds"] and r["checksum"] == ctx.checksum())
+            parts = ctx.copy_result_compact()  # the hand-over the timed steps copied, expanded by the checker
+            n_c, h_c, _ = c_oracle.checksum_compact(parts, d.num_terms)
+            cpu["matches_gpu"] = bool(r["n_cinds"] == n_c == cs["n_cinds"] and r["checksum"] == h_c)
 
     ingest = None
     if rank == 0 and world == 1 and not args.no_ingest:
         # parse/encode timed separately -- the same triples as N-Triples text through
         # rdf_parse_ntriples (ids/terms are checked by tests/)
-        import numpy as np
-
         tt = d.terms.term
         strs = np.array([tt(i) + " " for i in range(d.num_terms)], dtype=object)
         text = "".join(map("".join, zip(strs[d.s], strs[d.p], strs[d.o], [".\n"] * d.n))).encode()
@@ -312,22 +352,31 @@ def main():
         assert n_parsed == d.n
         ingest = {"ms": round(pms, 3), "text_bytes": len(text), "gbs_text": round(len(text) / pms / 1e6, 1),
                   "triples_per_s": round(d.n / pms * 1e3, 1), "terms": n_terms,
-                  "wall_ms_incl_h2d": round(wms, 3), "device_resident_ms": round(pms + ms_per_step, 3),
+                  "wall_ms_incl_h2d": round(wms, 3), "t_disc_plus_ingest_ms": round(pms + ms_per_step, 3),
                   "note": "ms: rdf_parse_ntriples device time (median of 3), text already in HBM; wall_ms_incl_h2d: "
-                          "the same call timed on the host, including the text's upload from pageable memory; "
-                          "device_resident_ms = ingest + one discovery step, both device-resident"}
+                          "the same call timed on the host, including the text's upload from pageable memory"}
         del text
 
     if rank == 0:
+        per = "per GPU" if args.scaling == "weak" else "total"
+        wl = {"c2": "LUBM-shaped"}.get(args.config, args.config)
         line = {
             "metric": "CIND-discovery triples/sec", "value": round(value, 1), "unit": "triples/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": f"{args.config} ({'LUBM-100-shaped' if args.config == 'c2' else args.config}, "
-                                   f"scale {args.scale}, support {ms}, strategy 1 --use-fis --clean-implied)",
+            "higher_is_better": True, "scaling": args.scaling if world > 1 else "weak", "vs_baseline": None,
+            "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"{args.config} ({wl}, scale {args.scale} {per}: {total_n} triples over {world} GPU(s), "
+                                   f"support {ms}, strategy 1 --use-fis --clean-implied)",
                        "triples": total_n, "triples_rank0": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
                        "parallelism": f"input slices + join-hash shards x{world} (RCCL)" if world > 1 else "single"},
-            "roofline": roof, "count_kernels": count_roof, "families": fams, "t_disc_host": tdisc,
+            "step": "T_disc (SURVEY.md 8(d)): dictionary-encoded triples resident in HBM -> compact CindSet-shaped "
+                    "id-records (rdf_copy_result_compact) in pinned host memory, every rank",
+            "handover": {"bytes_all_ranks": total_bytes, "pinned": sink.pinned, "n_refs": L["n_refs"],
+                         "n_list_refs": L["n_list_refs"], "n_members": L["n_members"], "n_runs": L["n_runs"]},
+            "device_resident": {"ms_per_step": round(elapsed_dev * 1000.0 / steps, 3),
+                                "triples_per_s": round(float(total_n) * steps / elapsed_dev, 1),
+                                "note": "the same steps with the result left in HBM"},
+            "roofline": roof, "count_kernels": count_roof, "families": fams,
             "cpu_baseline": cpu, "ingest": ingest,
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],

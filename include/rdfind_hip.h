@@ -183,6 +183,30 @@ rdf_status rdf_result_sizes(rdf_ctx* ctx, uint64_t* n_refs, uint64_t* n_runs, ui
 rdf_status rdf_copy_result_raw(rdf_ctx* ctx, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* capture_ids,
                                uint32_t* supports);
 
+/* The compact result: what rdf_discover_cinds leaves in HBM, without expanding shared ref lists.  A CindSet
+ * (ALG/data/CindSet.scala:9-13: one dependent, its support, its ref conditions) per dependent, in two forms:
+ *   - explicit runs: refs[runoff[r] .. runoff[r+1]) are the refs of dependent rundep[r] (n_runs runs, n_refs refs);
+ *   - shared lists: members[i] = list << 32 | dependent; that dependent's refs are list_refs[list_off[list] ..
+ *     list_off[list+1]) except itself (n_members members of n_lists lists; dependents whose capture groups all
+ *     have the same heavy-group bitmask share one filtered list).
+ * Every id is a compact capture id: capture_ids[id] is its capture id (rdf_decode_capture) and supports[id] the
+ * dependent's support.  n_cinds = n_refs + sum over members of the list length minus the member itself.  This
+ * is the id-record hand-over the metric's T_disc ends with; the row accessors below expand it. */
+typedef struct {
+    uint64_t n_cinds;
+    uint64_t n_refs;
+    uint64_t n_runs;
+    uint64_t n_lists;
+    uint64_t n_list_refs;
+    uint64_t n_members;
+    uint64_t n_captures;
+} rdf_result_layout;
+rdf_status rdf_get_result_layout(rdf_ctx* ctx, rdf_result_layout* layout);
+/* Null pointers skip a part.  Sizes: refs n_refs, runoff n_runs + 1, rundep n_runs, list_refs n_list_refs,
+ * list_off n_lists + 1, members n_members, capture_ids and supports n_captures. */
+rdf_status rdf_copy_result_compact(rdf_ctx* ctx, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* list_refs,
+                                   uint64_t* list_off, uint64_t* members, uint32_t* capture_ids, uint32_t* supports);
+
 /* One result row in the reference's Cind shape (ALG/data/Cind.scala:12-15: depCaptureType, depConditionValue1/2,
  * refCaptureType, refConditionValue1/2, support), with term ids for the condition values; value2 = UINT32_MAX
  * stands for the reference's null (unary capture).  Seven uint32 fields, no padding. */

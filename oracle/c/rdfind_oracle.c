@@ -646,6 +646,44 @@ uint64_t orc_checksum(const orc_cind *rows, uint64_t n) {
     return acc;
 }
 
+/* Count, per-kind counts and checksum of a compact result (include/rdfind_hip.h rdf_copy_result_compact): the
+ * explicit runs plus, for every member of a shared list, the list minus the member itself.  Checker for the
+ * device's compact hand-over (the expansion the consumer would do), with external ids via capture_ids. */
+uint64_t orc_checksum_compact(const uint32_t *refs, const uint64_t *runoff, const uint32_t *rundep, uint64_t nruns,
+                              const uint32_t *list_refs, const uint64_t *list_off, const uint64_t *members,
+                              uint64_t nmem, const uint32_t *capture_ids, const uint32_t *supports, uint32_t V,
+                              uint64_t *count, uint64_t kind[4]) {
+    const uint64_t U = 6ull * V;
+    uint64_t acc = 0, cnt = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+#pragma omp parallel for reduction(+ : acc, cnt, k0, k1, k2, k3) schedule(dynamic, 64)
+    for (uint64_t r = 0; r < nruns; ++r) {
+        const uint32_t d = rundep[r], dx = capture_ids[d], sup = supports[d];
+        for (uint64_t i = runoff[r]; i < runoff[r + 1]; ++i) {
+            const uint32_t rx = capture_ids[refs[i]];
+            acc += row_hash(dx, rx, sup);
+            cnt++;
+            const int k = (dx >= U) * 2 + (rx >= U);
+            k0 += k == 0; k1 += k == 1; k2 += k == 2; k3 += k == 3;
+        }
+    }
+#pragma omp parallel for reduction(+ : acc, cnt, k0, k1, k2, k3) schedule(dynamic, 1)
+    for (uint64_t j = 0; j < nmem; ++j) {
+        const uint64_t l = members[j] >> 32;
+        const uint32_t d = (uint32_t)members[j], dx = capture_ids[d], sup = supports[d];
+        for (uint64_t i = list_off[l]; i < list_off[l + 1]; ++i) {
+            if (list_refs[i] == d) continue;
+            const uint32_t rx = capture_ids[list_refs[i]];
+            acc += row_hash(dx, rx, sup);
+            cnt++;
+            const int k = (dx >= U) * 2 + (rx >= U);
+            k0 += k == 0; k1 += k == 1; k2 += k == 2; k3 += k == 3;
+        }
+    }
+    *count = cnt;
+    kind[0] = k0; kind[1] = k1; kind[2] = k2; kind[3] = k3;
+    return acc;
+}
+
 void orc_free(void *ptr) { free(ptr); }
 
 /* threads stages 4-6 use (OMP_NUM_THREADS, else all cores) */

@@ -141,6 +141,26 @@ def checksum_rows(arr):
     return int(lib.orc_checksum(a.ctypes.data, a.shape[0])) if a.shape[0] else 0
 
 
+def checksum_compact(parts, num_terms):
+    """(count, checksum, n_kind) of a compact result (rdfind_amd._lib Context.copy_result_compact parts, sized by
+    ``parts["layout"]``): the expansion a consumer of the compact hand-over would do, counted by the checker."""
+    lib = _load()
+    lib.orc_checksum_compact.restype = ctypes.c_uint64
+    lib.orc_checksum_compact.argtypes = ([ctypes.c_void_p] * 3 + [ctypes.c_uint64] + [ctypes.c_void_p] * 3 +
+                                         [ctypes.c_uint64] + [ctypes.c_void_p] * 2 + [ctypes.c_uint32] +
+                                         [ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p])
+    L = parts["layout"]
+    arr = {k: np.ascontiguousarray(parts[k]) for k in ("refs", "runoff", "rundep", "list_refs", "list_off", "members",
+                                                        "capture_ids", "supports")}
+    cnt = ctypes.c_uint64()
+    kind = np.zeros(4, np.uint64)
+    h = lib.orc_checksum_compact(arr["refs"].ctypes.data, arr["runoff"].ctypes.data, arr["rundep"].ctypes.data,
+                                 L["n_runs"], arr["list_refs"].ctypes.data, arr["list_off"].ctypes.data,
+                                 arr["members"].ctypes.data, L["n_members"], arr["capture_ids"].ctypes.data,
+                                 arr["supports"].ctypes.data, num_terms, ctypes.byref(cnt), kind.ctypes.data)
+    return int(cnt.value), int(h), [int(x) for x in kind]
+
+
 def run_set(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):
     arr, keys, stats = run(s, p, o, num_terms, min_support, strategy, clean, projection)
     out = set()

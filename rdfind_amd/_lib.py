@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "rdf_shard_export", "rdf_shard_import", "rdf_set_dictionary", "rdf_format_size", "rdf_format_cinds",
     "rdf_distinct_triples", "rdf_copy_triples", "rdf_parse_ntriples", "rdf_copy_terms",
     "rdf_set_dictionary_parsed", "rdf_device_bytes", "rdf_copy_cinds_decoded", "rdf_result_sizes",
-    "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules",
+    "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules", "rdf_get_result_layout",
+    "rdf_copy_result_compact",
 )
 RDF_NT_TABS = 1
 
@@ -63,6 +64,18 @@ class CindStats(ctypes.Structure):
                 ("ms_heavy", ctypes.c_float), ("n_heavy_candidates", ctypes.c_uint64),
                 ("n_class_members", ctypes.c_uint64), ("n_classes", ctypes.c_uint64), ("n_class_cinds", ctypes.c_uint64),
                 ("n_light_candidates", ctypes.c_uint64), ("n_light_entries", ctypes.c_uint64)]
+
+
+class ResultLayout(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in ("n_cinds", "n_refs", "n_runs", "n_lists", "n_list_refs", "n_members",
+                                                "n_captures")]
+
+
+# rdf_copy_result_compact parts: name -> (dtype, element count from the layout)
+COMPACT_PARTS = (("refs", np.uint32, lambda L: L["n_refs"]), ("runoff", np.uint64, lambda L: L["n_runs"] + 1),
+                 ("rundep", np.uint32, lambda L: L["n_runs"]), ("list_refs", np.uint32, lambda L: L["n_list_refs"]),
+                 ("list_off", np.uint64, lambda L: L["n_lists"] + 1), ("members", np.uint64, lambda L: L["n_members"]),
+                 ("capture_ids", np.uint32, lambda L: L["n_captures"]), ("supports", np.uint32, lambda L: L["n_captures"]))
 
 
 class Exchange(ctypes.Structure):
@@ -137,6 +150,8 @@ def load():
         "rdf_copy_cinds_decoded": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_result_sizes": (i32, [P, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "rdf_copy_result_raw": (i32, [P, P, P, P, P, P]),
+        "rdf_get_result_layout": (i32, [P, ctypes.POINTER(ResultLayout)]),
+        "rdf_copy_result_compact": (i32, [P, P, P, P, P, P, P, P, P]),
         "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
         "rdf_format_cinds": (i32, [P, u64, u64, P, u64, ctypes.POINTER(u64)]),
@@ -392,6 +407,23 @@ class Context:
             return None if x is None else (x if isinstance(x, int) else x.ctypes.data)
         self._check(self.lib.rdf_copy_result_raw(self.ptr, ptr(refs_ptr), ptr(runoff), ptr(rundep), ptr(capture_ids),
                                                  ptr(supports)), "rdf_copy_result_raw")
+
+    def result_layout(self) -> dict:
+        """Sizes of the compact CindSet-shaped result (rdf_get_result_layout)."""
+        L = ResultLayout()
+        self._check(self.lib.rdf_get_result_layout(self.ptr, ctypes.byref(L)), "rdf_get_result_layout")
+        return _struct_dict(L)
+
+    def copy_result_compact(self, bufs: dict | None = None) -> dict:
+        """rdf_copy_result_compact into ``bufs`` (name -> numpy array or raw pointer, e.g. pinned memory sized from
+        :meth:`result_layout`), or into fresh numpy arrays; returns the name -> buffer dict."""
+        if bufs is None:
+            L = self.result_layout()
+            bufs = {name: np.empty(max(count(L), 1), dt) for name, dt, count in COMPACT_PARTS}
+            bufs["layout"] = L
+        ptrs = [bufs[name] if isinstance(bufs[name], int) else bufs[name].ctypes.data for name, _, _ in COMPACT_PARTS]
+        self._check(self.lib.rdf_copy_result_compact(self.ptr, *ptrs), "rdf_copy_result_compact")
+        return bufs
 
     def copy_cinds_decoded(self, offset: int = 0, count: int | None = None) -> np.ndarray:
         """Cind-shaped rows decoded on the device (rdf_copy_cinds_decoded), ROW_DTYPE."""

@@ -1931,6 +1931,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_emit(u64 nvblk, const u64* 
 }
 
 
+// first ref of each shared (class) list: class m's list is lists[lwoff[cchoff[m]], lwoff[cchoff[m + 1]])
+__global__ __launch_bounds__(RDF_BLOCK) void k_list_offsets(const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
+                                                            u32 ncls, u64* loff) {
+    for (u64 m = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; m <= ncls; m += (u64)gridDim.x * RDF_BLOCK)
+        loff[m] = lwoff[cchoff[m]];
+}
+
 // output run table (dependent runs in output order): runs [0, C) are the explicit pairs of dependent d
 // (start pos[eoff[d]]), [C, C+WH) the heavy-only binary chunks, [C+WH, C+WH+nmem) the class members
 __global__ __launch_bounds__(RDF_BLOCK) void k_output_runs(u32 C, const u64* __restrict__ eoff, const u64* __restrict__ epos,
@@ -2098,7 +2105,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_route_survivors(const u64* __rest
 // destination bounds of the dest-sorted words (dest in bits 58..63), then the destination bits cleared
 __global__ __launch_bounds__(RDF_BLOCK) void k_dest_bounds(const u64* __restrict__ words, u64 n, u32 nranks, u64* bounds) {
     for (u64 r = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; r <= nranks; r += (u64)gridDim.x * RDF_BLOCK)
-        bounds[r] = lower_bound_u64(words, n, r << 58);
+        bounds[r] = r == nranks ? n : lower_bound_u64(words, n, r << 58);  // r = 64 would wrap the shift
 }
 __global__ void k_lower_bound1(const u64* __restrict__ words, u64 n, u64 key, u64* out) { *out = lower_bound_u64(words, n, key); }
 __global__ __launch_bounds__(RDF_BLOCK) void k_clear_bits(u64* words, u64 n, u64 mask) {

@@ -85,6 +85,10 @@ struct rdf_ctx {
     DevBuf ctab, cflag, ccid, ckeys, ckeys_tmp, coff, cmask, cpiv, cnch, cchoff, ccnt, lwoff, clists, cself, cmcnt, cobase,
         ctiles, ctoff;
     u64 n_class_members = 0, n_classes = 0, n_class_out = 0;
+    // compact result: the class part (members x shared lists) is expanded into `out` only on demand
+    bool class_pending = false;
+    u64 pend_NT = 0, pend_base = 0, n_lists = 0, n_list_refs = 0, n_runs_explicit = 0;
+    DevBuf loff;  // list offsets of the shared (class) ref lists
     bool hclassed = false;  // binary heavy-only dependents emitted from class lists (single GPU, S2L semantics)
     DevBuf pedges, pedges_tmp;
     u64 ncap = 0;
@@ -266,7 +270,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref};
+            &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff};
 }
 
 extern "C" {
@@ -883,6 +887,7 @@ static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
     c->ms = min_support ? min_support : 1;  // a support of 0 admits exactly the captures that exist
     c->ar_on = false;
     c->n_rules = 0;
+    c->class_pending = false;
     for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), c->stream));
@@ -1719,7 +1724,7 @@ static rdf_status d_class_bin(rdf_ctx* c, const CindView& v, u64* WH) {
 // K7 minimality on the (owned) explicit pairs, heavy-only binary write pass, class emission -> out
 static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
     hipStream_t st = c->stream;
-    ENSURE(c, out, std::max<u64>(E + H + HC, 1) * 4);
+    ENSURE(c, out, std::max<u64>(E + H, 1) * 4);  // the class part is expanded behind it on demand (materialize)
     ENSURE(c, flags, std::max<u64>(E, 1) * 4);
     ENSURE(c, pos, (E + 1) * 8);
     tbegin(c, RDF_T_RULES);
@@ -1743,12 +1748,20 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
                            c->hbits.as<u64>(), c->hclassed ? c->clists.as<u32>() : c->gcap.as<u32>(),
                            c->hclassed ? c->sbase.as<u64>() : (const u64*)nullptr, c->hoff.as<u64>(), K, c->out.as<u32>());
     tend(c, RDF_T_HWRITE);
-    tbegin(c, RDF_T_CEMIT);
-    if (NT)
-        hipLaunchKernelGGL(k_class_emit, dim3(vgrid(NT)), dim3(RDF_BLOCK), 0, st, NT, c->coff.as<u64>(),
-                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(),
-                           (u32)c->n_classes, c->cself.as<u32>(), c->cobase.as<u64>(), K + H, c->out.as<u32>());
-    tend(c, RDF_T_CEMIT);
+    // The class part stays compact: each member's refs are its class's shared list minus itself (a CindSet whose
+    // ref list is shared, ALG/data/CindSet.scala:9-13).  rdf_copy_result_compact hands it over as is; the expanded
+    // per-dependent runs (k_class_emit) are written only when a caller asks for rows (materialize).
+    c->class_pending = NT > 0;
+    c->pend_NT = NT;
+    c->pend_base = K + H;
+    const u32 ncls = (u32)c->n_classes;
+    c->n_lists = HC ? ncls : 0;
+    c->n_list_refs = 0;
+    if (c->n_lists) {
+        ENSURE(c, loff, (ncls + 1ull) * 8);
+        hipLaunchKernelGGL(k_list_offsets, dim3(grid_for(ncls + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), ncls, c->loff.as<u64>());
+    }
     // run table: the dependent of every output ref (CindSet-shaped result, ALG/data/CindSet.scala:9-13)
     const u64 nmem = HC ? c->n_class_members : 0;
     const u64 R = (u64)c->C + WH + nmem;
@@ -1758,11 +1771,13 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
                        c->pos.as<u64>(), WH, c->choffh.as<u64>(), c->hoff.as<u64>(), K, nmem, c->ckeys.as<u64>(),
                        c->cobase.as<u64>(), H, K + H + HC, c->runoff.as<u64>(), c->rundep.as<u32>());
     c->n_runs = R;
+    c->n_runs_explicit = (u64)c->C + WH;
     c->h_runs_valid = false;
     ++c->run_id;
     HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(st));
+    if (c->n_lists) TRY(read_u64(c, c->loff.as<u64>() + ncls, &c->n_list_refs));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], c->ev[5]));
     tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS);
     c->n_out = K + H + HC;
@@ -2457,6 +2472,68 @@ rdf_status rdf_shard_import(rdf_ctx* c, const void* src, uint64_t count) {
     return RDF_OK;
 }
 
+// Expands the class part of the result (members x shared lists) into per-dependent runs behind the explicit refs:
+// needed by every row-level accessor (copy, decode, checksum, formatting), not by rdf_copy_result_compact.
+static rdf_status materialize(rdf_ctx* c) {
+    if (!c->class_pending) return RDF_OK;
+    hipStream_t st = c->stream;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, c->out.grow_keep((size_t)std::max<u64>(c->n_out, 1) * 4, st));
+    c->tn[RDF_T_CEMIT] = 0;
+    tbegin(c, RDF_T_CEMIT);
+    hipLaunchKernelGGL(k_class_emit, dim3(vgrid(c->pend_NT)), dim3(RDF_BLOCK), 0, st, c->pend_NT, c->coff.as<u64>(),
+                       c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(), c->ctoff.as<u64>(),
+                       (u32)c->n_classes, c->cself.as<u32>(), c->cobase.as<u64>(), c->pend_base, c->out.as<u32>());
+    tend(c, RDF_T_CEMIT);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    tcollect(c, RDF_T_CEMIT, RDF_T_CEMIT + 1);
+    c->out_ptr = c->out.as<u32>();
+    c->class_pending = false;
+    return RDF_OK;
+}
+
+rdf_status rdf_get_result_layout(rdf_ctx* c, rdf_result_layout* L) {
+    if (!c || !L) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    L->n_cinds = c->n_out;
+    L->n_refs = c->n_out - c->n_class_out;
+    L->n_runs = c->n_runs_explicit;
+    L->n_lists = c->n_lists;
+    L->n_list_refs = c->n_list_refs;
+    L->n_members = c->n_class_out ? c->n_class_members : 0;
+    L->n_captures = c->C;
+    return RDF_OK;
+}
+
+// The compact CindSet-shaped result (SURVEY.md 8(d) "CIND id-records in host memory"): explicit refs in runs of one
+// dependent, the shared lists and their member dependents, the capture table.  Plain async copies on the context
+// stream (pinned caller memory lets them run at the link rate); nothing is expanded.
+rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* list_refs,
+                                   uint64_t* list_off, uint64_t* members, uint32_t* capture_ids, uint32_t* supports) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const u64 nrefs = c->n_out - c->n_class_out, R = c->n_runs_explicit;
+    const u64 nmem = c->n_class_out ? c->n_class_members : 0;
+    if (refs && nrefs) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr, nrefs * 4, hipMemcpyDeviceToHost, st));
+    if (runoff) HIP_TRY(c, hipMemcpyAsync(runoff, c->runoff.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (rundep && R) HIP_TRY(c, hipMemcpyAsync(rundep, c->rundep.p, R * 4, hipMemcpyDeviceToHost, st));
+    if (c->n_lists) {
+        if (list_refs && c->n_list_refs)
+            HIP_TRY(c, hipMemcpyAsync(list_refs, c->clists.p, c->n_list_refs * 4, hipMemcpyDeviceToHost, st));
+        if (list_off) HIP_TRY(c, hipMemcpyAsync(list_off, c->loff.p, (c->n_lists + 1) * 8, hipMemcpyDeviceToHost, st));
+    } else if (list_off) {
+        list_off[0] = 0;
+    }
+    if (members && nmem) HIP_TRY(c, hipMemcpyAsync(members, c->ckeys.p, nmem * 8, hipMemcpyDeviceToHost, st));
+    if (capture_ids && c->C) HIP_TRY(c, hipMemcpyAsync(capture_ids, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
+    if (supports && c->C) HIP_TRY(c, hipMemcpyAsync(supports, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return RDF_OK;
+}
+
 rdf_status rdf_last_stats(rdf_ctx* c, rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs) {
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "no completed run");
@@ -2519,6 +2596,7 @@ rdf_status rdf_copy_cinds(rdf_ctx* c, rdf_cind* out, uint64_t cap, uint64_t* n_c
     if (!c || (cap && !out)) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(materialize(c));
     const u64 total = std::min<u64>(cap, c->n_out);
     if (total) TRY(copy_decoded(c, 0, total, out));
     if (n_copied) *n_copied = total;
@@ -2529,6 +2607,7 @@ rdf_status rdf_copy_cinds_range(rdf_ctx* c, uint64_t offset, rdf_cind* out, uint
     if (!c || (count && !out)) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(materialize(c));
     const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
     if (m) TRY(copy_decoded(c, offset, m, out));
     if (n_copied) *n_copied = m;
@@ -2552,6 +2631,7 @@ rdf_status rdf_copy_result_raw(rdf_ctx* c, uint32_t* refs, uint64_t* runoff, uin
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(materialize(c));
     hipStream_t st = c->stream;
     if (refs && c->n_out) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr, c->n_out * 4, hipMemcpyDeviceToHost, st));
     if (runoff) HIP_TRY(c, hipMemcpyAsync(runoff, c->runoff.p, (c->n_runs + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -2567,6 +2647,7 @@ rdf_status rdf_copy_cinds_decoded(rdf_ctx* c, uint64_t offset, rdf_cind_row* out
     if (!c || (count && !out)) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(materialize(c));
     const u64 m = offset >= c->n_out ? 0 : std::min<u64>(count, c->n_out - offset);
     const u64 kChunk = 1ull << 22;
     if (m) ENSURE(c, drows, std::min<u64>(m, kChunk) * sizeof(rdf_cind_row));
@@ -2587,6 +2668,7 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     if (!c || !checksum) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(materialize(c));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 7), 0, 8, c->stream));
     if (c->n_out)
         hipLaunchKernelGGL(k_checksum, dim3(grid_for(c->n_out, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
@@ -2665,6 +2747,7 @@ static rdf_status ensure_capstr(rdf_ctx* c) {
 // line offsets of result rows [offset, offset + m) -> floff, *bytes
 static rdf_status fmt_prepare(rdf_ctx* c, u64 offset, u64 m, u64* bytes) {
     hipStream_t st = c->stream;
+    TRY(materialize(c));
     TRY(ensure_capstr(c));
     ENSURE(c, flen, std::max<u64>(m, 1) * 4);
     ENSURE(c, floff, (m + 1) * 8);

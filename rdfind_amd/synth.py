@@ -5,12 +5,16 @@ Every generator returns a :class:`Dataset`: dictionary-encoded ``uint32`` column
 SURVEY.md Appendix B.3) plus a :class:`TermTable` that maps ids back to N-Triples terms.
 
 * ``zipf_rdf``  -- Zipf-distributed entity/predicate/class/literal graph (c1, c3, c4, c5 shapes).
+* ``zipf_rows`` -- the same distributions from a counter-based generator (rdfind_amd/csrc/synth_gen.c): row i
+                   depends only on (seed, i), so any row range is drawn on its own (c4 beyond scale 0.05).
 * ``lubm``      -- LUBM-schema generator (universities -> departments -> faculty, students,
                    courses, publications; ~18 predicates), the c2 shape.  The official Java UBA
                    is unavailable offline; this follows its published cardinalities.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -149,6 +153,61 @@ def zipf_rdf(name: str, n: int, n_entities: int, n_predicates: int, pred_alpha: 
             idx = np.sort(rng.choice(s.shape[0], n, replace=False))
             s, p, o = s[idx], p[idx], o[idx]
     return Dataset(name, s, p, o, terms, min_support)
+
+
+class _SynthParams(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64)] + [(k, ctypes.c_uint32) for k in (
+        "t_type", "t_pred", "t_cls", "t_ent", "t_lit", "n_pred", "n_cls", "n_ent", "n_lit")] + [
+        (k, ctypes.c_double) for k in ("pred_alpha", "subj_alpha", "class_frac", "class_alpha", "literal_frac",
+                                       "lit_alpha", "obj_alpha")]
+
+
+_SYNTH_LIB = None
+
+
+def _synth_lib():
+    global _SYNTH_LIB
+    if _SYNTH_LIB is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsynth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} not built; run __graft_entry__.build()")
+        lib = ctypes.CDLL(path)
+        lib.synth_zipf_rows.restype = None
+        lib.synth_zipf_rows.argtypes = [ctypes.POINTER(_SynthParams), ctypes.c_uint64, ctypes.c_uint64,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _SYNTH_LIB = lib
+    return _SYNTH_LIB
+
+
+def zipf_rows(name: str, n: int, row0: int, nrows: int, n_entities: int, n_predicates: int, pred_alpha: float,
+              subj_alpha: float, class_frac: float, n_classes: int, class_alpha: float, literal_frac: float,
+              n_literals: int, lit_alpha: float, obj_alpha: float, min_support: int, seed: int) -> Dataset:
+    """Rows [row0, row0 + nrows) of an n-row i.i.d. Zipf configuration (no deduplication), drawn by the
+    counter-based generator: the same term table and distributions as :func:`zipf_rdf`, and any row range is
+    generated independently of the others (sharded inputs: the ranks' slices always form the same input)."""
+    terms = TermTable()
+    q = _SynthParams(seed=seed)
+    q.t_type = terms.add(1, lambda i: RDF_TYPE)
+    q.t_pred = terms.add(n_predicates, lambda i: f"<http://ex.org/p{i}>")
+    q.t_cls = terms.add(n_classes, lambda i: f"<http://ex.org/C{i}>")
+    q.t_ent = terms.add(n_entities, lambda i: f"<http://ex.org/e{i}>")
+    q.t_lit = terms.add(n_literals, lambda i: f'"l{i}"')
+    q.n_pred, q.n_cls, q.n_ent, q.n_lit = n_predicates, n_classes, n_entities, n_literals
+    q.pred_alpha, q.subj_alpha, q.class_frac, q.class_alpha = pred_alpha, subj_alpha, class_frac, class_alpha
+    q.literal_frac, q.lit_alpha, q.obj_alpha = literal_frac, lit_alpha, obj_alpha
+    if not 0 <= row0 <= row0 + nrows <= n:
+        raise ValueError("row range outside the configuration")
+    s, p, o = (np.empty(nrows, np.uint32) for _ in range(3))
+    if nrows:
+        _synth_lib().synth_zipf_rows(ctypes.byref(q), row0, nrows, s.ctypes.data, p.ctypes.data, o.ctypes.data)
+    return Dataset(name, s, p, o, terms, min_support)
+
+
+def _c4_rows(scale: float, lo: int, hi: int) -> Dataset:
+    """c4 beyond scale 0.05: rows [lo, hi) of the counter-based Freebase-shaped configuration."""
+    n = int(1_000_000_000 * scale)
+    return zipf_rows("c4", n, lo, hi - lo, max(int(100_000_000 * scale), 100), max(int(20_000 * scale), 20), 1.2, 1.0,
+                     0.10, 2000, 1.2, 0.35, max(int(150_000_000 * scale), 100), 1.0, 1.0, 100, 4)
 
 
 # ---------------------------------------------------------------------------
@@ -362,17 +421,14 @@ def lubm(n_universities: int = 100, seed: int = 0, min_support: int = 10, max_de
 
 def config_slice(name: str, scale: float, rank: int, nranks: int) -> tuple:
     """This rank's slice of a BASELINE config for the sharded (multi-GPU) bench: (Dataset of the slice, total
-    triples).  c4 beyond scale 0.05 (1B triples at full size: no deduplication, i.i.d. rows) draws only its
-    own rows from a rank-specific seed, so no rank ever holds the whole input; the union of the slices is then
-    a function of nranks (same distribution and vocabulary).  Every other config is generated whole
-    (deterministically on every rank) and cut into contiguous row ranges."""
+    triples), the contiguous row range [n * rank / nranks, n * (rank + 1) / nranks).  c4 beyond scale 0.05 (1B
+    triples at full size: no deduplication, i.i.d. rows) draws only its own rows from the counter-based
+    generator, so no rank ever holds the whole input and the slices form the same input as config() for any
+    nranks.  Every other config is generated whole (deterministically on every rank) and cut."""
     if name == "c4" and scale > 0.05:
         n = int(1_000_000_000 * scale)
         lo, hi = n * rank // nranks, n * (rank + 1) // nranks
-        seed = int(np.random.SeedSequence([4, rank, nranks]).generate_state(1)[0])
-        d = zipf_rdf("c4", hi - lo, max(int(100_000_000 * scale), 100), max(int(20_000 * scale), 20), 1.2, 1.0,
-                     0.10, 2000, 1.2, 0.35, max(int(150_000_000 * scale), 100), 1.0, 1.0, 100, seed, dedup=False)
-        return d, n
+        return _c4_rows(scale, lo, hi), n
     d = config(name, scale)
     n = d.n
     lo, hi = n * rank // nranks, n * (rank + 1) // nranks
@@ -394,6 +450,8 @@ def config(name: str, scale: float = 1.0, seed: int | None = None) -> Dataset:
                         3 if seed is None else seed)
     if name == "c4":
         n = int(1_000_000_000 * scale)
+        if scale > 0.05:  # i.i.d. rows, counter-based (the scales that are also run sharded)
+            return _c4_rows(scale, 0, n)
         return zipf_rdf("c4", n, max(int(100_000_000 * scale), 100), max(int(20_000 * scale), 20), 1.2, 1.0,
                         0.10, 2000, 1.2, 0.35, max(int(150_000_000 * scale), 100), 1.0, 1.0, 100,
                         4 if seed is None else seed, dedup=scale <= 0.05)

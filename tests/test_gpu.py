@@ -46,6 +46,14 @@ def gpu_set(ctx, arr, nv, ms, strategy, clean, projection="spo"):
     return _lib.decoded_to_set(ctx.decoded_cinds())
 
 
+def compact_matches(ctx, nv):
+    """The compact hand-over (rdf_copy_result_compact: explicit runs + shared lists) expands to the same rows as the
+    device's own expansion: count and order-independent checksum."""
+    parts = ctx.copy_result_compact()
+    n, h, _ = C.checksum_compact(parts, nv)
+    return n == ctx.cind_count() and h == ctx.checksum()
+
+
 def test_random_parity_all_modes(ctx):
     rng = random.Random(11)
     for _ in range(150):
@@ -57,6 +65,7 @@ def test_random_parity_all_modes(ctx):
         for strategy, clean in MODES:
             assert gpu_set(ctx, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
                 (n, nv, ms, strategy, clean)
+            assert compact_matches(ctx, nv)
 
 
 def test_projection_subsets(ctx):
@@ -203,8 +212,12 @@ def test_heavy_paths_parity(monkeypatch, heavy_min):
             arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
                            dtype=np.uint32)
             for strategy, clean in MODES:
-                assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
+                g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+                g.run(ms, "spo", clean, strategy)
+                parts = g.copy_result_compact()  # before any row accessor expands the class part
+                assert _lib.decoded_to_set(g.decoded_cinds()) == expected_set(arr, nv, ms, strategy, clean), \
                     (n, nv, ms, strategy, clean, heavy_min)
+                assert C.checksum_compact(parts, nv)[:2] == (g.cind_count(), g.checksum())
         for cfg, scale in (("c5", 0.01), ("c1", 0.05)):
             d = synth.config(cfg, scale)
             exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
