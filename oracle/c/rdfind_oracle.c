@@ -195,62 +195,100 @@ static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_
     }
     free(cnt);
 
-    /* 2. binary condition counts (CreatedReducedDoubleConditionCounts.scala:45-86) */
-    u64map bmap;
-    map_init(&bmap, 3 * n + 16);
-    for (uint64_t i = 0; i < n; ++i) {
-        int fs = freq[s[i]] & 1, fp = (freq[p[i]] >> 1) & 1, fo = (freq[o[i]] >> 2) & 1;
-        if (fs + fp + fo < 2) continue;
-        if (fs && fp) (*map_slot(&bmap, (2ull << 62) | ((uint64_t)s[i] << 31) | p[i], 1))++;
-        if (fs && fo) (*map_slot(&bmap, (1ull << 62) | ((uint64_t)s[i] << 31) | o[i], 1))++;
-        if (fp && fo) (*map_slot(&bmap, (0ull << 62) | ((uint64_t)p[i] << 31) | o[i], 1))++;
+    /* 2. binary condition counts (CreatedReducedDoubleConditionCounts.scala:45-86): the keys of the triples with two
+     *    frequent values, sorted, counted per run (memory ~16 B per key; chunked passes keep any thread count's
+     *    result identical) */
+    enum { NCH = 4096 };
+    uint64_t *chunk = (uint64_t *)calloc(NCH + 1, sizeof(uint64_t));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int ch = 0; ch < NCH; ++ch) {
+        uint64_t k = 0;
+        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) {
+            int fs = freq[s[i]] & 1, fp = (freq[p[i]] >> 1) & 1, fo = (freq[o[i]] >> 2) & 1;
+            k += (fs && fp) + (fs && fo) + (fp && fo);
+        }
+        chunk[ch + 1] = k;
     }
-    st->n_binary_keys = bmap.size;
-    uint64_t nb = 0;
-    for (uint64_t h = 0; h <= bmap.mask; ++h)
-        if (bmap.keys[h] != ~0ULL && bmap.vals[h] >= ms) nb++;
+    for (int ch = 0; ch < NCH; ++ch) chunk[ch + 1] += chunk[ch];
+    const uint64_t nkeys_all = chunk[NCH];
+    uint64_t *keys = (uint64_t *)xmalloc(nkeys_all * sizeof(uint64_t));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int ch = 0; ch < NCH; ++ch) {
+        uint64_t k = chunk[ch];
+        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) {
+            int fs = freq[s[i]] & 1, fp = (freq[p[i]] >> 1) & 1, fo = (freq[o[i]] >> 2) & 1;
+            if (fs && fp) keys[k++] = (2ull << 62) | ((uint64_t)s[i] << 31) | p[i];
+            if (fs && fo) keys[k++] = (1ull << 62) | ((uint64_t)s[i] << 31) | o[i];
+            if (fp && fo) keys[k++] = (0ull << 62) | ((uint64_t)p[i] << 31) | o[i];
+        }
+    }
+    radix_sort_u64(keys, nkeys_all);
+    uint64_t nb = 0, ndist = 0;
+    for (uint64_t i = 0; i < nkeys_all;) {
+        uint64_t j = i + 1;
+        while (j < nkeys_all && keys[j] == keys[i]) ++j;
+        ndist++;
+        if (j - i >= ms) keys[nb++] = keys[i];  /* ascending: the frequent keys come out sorted */
+        i = j;
+    }
+    st->n_binary_keys = ndist;
     uint64_t *bkeys = (uint64_t *)xmalloc(nb * sizeof(uint64_t));
-    nb = 0;
-    for (uint64_t h = 0; h <= bmap.mask; ++h)
-        if (bmap.keys[h] != ~0ULL && bmap.vals[h] >= ms) bkeys[nb++] = bmap.keys[h];
-    map_free(&bmap);
-    radix_sort_u64(bkeys, nb);
+    memcpy(bkeys, keys, nb * sizeof(uint64_t));
+    free(keys);
     st->n_freq_binary = nb;
     u64map bidx;
     map_init(&bidx, nb + 16);
     for (uint64_t b = 0; b < nb; ++b) *map_slot(&bidx, bkeys[b], 1) = (uint32_t)b;
 
     /* 3. join partners (CreateJoinPartners.scala:86-147), binary captures split into their unary
-     *    components as every consumer does (CreateDependencyCandidates.scala:157-186) */
+     *    components as every consumer does (CreateDependencyCandidates.scala:157-186); counted per chunk first so
+     *    the record array has its exact size */
     const uint64_t capbits = 64 - __builtin_clzll((uint64_t)6 * V + nb + 1);
-    uint64_t cap_records = 9 * n;
-    uint64_t *rec = (uint64_t *)xmalloc(cap_records * sizeof(uint64_t));
-    uint64_t nr = 0;
-#define EMIT(join, cap) rec[nr++] = ((uint64_t)(join) << capbits) | (uint64_t)(cap)
-    for (uint64_t i = 0; i < n; ++i) {
-        uint32_t ts = s[i], tp = p[i], to = o[i];
-        int fs = freq[ts] & 1, fp = (freq[tp] >> 1) & 1, fo = (freq[to] >> 2) & 1;
-        uint32_t *b;
-        if (proj_o) {
-            if (fs) EMIT(to, 4ull * V + ts);             /* o[s] */
-            if (fp) EMIT(to, 5ull * V + tp);             /* o[p] */
-            if (fs && fp && (b = map_slot(&bidx, (2ull << 62) | ((uint64_t)ts << 31) | tp, 0)))
-                EMIT(to, 6ull * V + *b);                 /* o[s,p] */
-        }
-        if (proj_p) {
-            if (fs) EMIT(tp, 2ull * V + ts);             /* p[s] */
-            if (fo) EMIT(tp, 3ull * V + to);             /* p[o] */
-            if (fs && fo && (b = map_slot(&bidx, (1ull << 62) | ((uint64_t)ts << 31) | to, 0)))
-                EMIT(tp, 6ull * V + *b);                 /* p[s,o] */
-        }
-        if (proj_s) {
-            if (fp) EMIT(ts, 0ull * V + tp);             /* s[p] */
-            if (fo) EMIT(ts, 1ull * V + to);             /* s[o] */
-            if (fp && fo && (b = map_slot(&bidx, (0ull << 62) | ((uint64_t)tp << 31) | to, 0)))
-                EMIT(ts, 6ull * V + *b);                 /* s[p,o] */
-        }
+#define EMIT_ALL(EMIT)                                                                            \
+    {                                                                                             \
+        uint32_t ts = s[i], tp = p[i], to = o[i];                                                 \
+        int fs = freq[ts] & 1, fp = (freq[tp] >> 1) & 1, fo = (freq[to] >> 2) & 1;               \
+        uint32_t *b;                                                                              \
+        if (proj_o) {                                                                             \
+            if (fs) EMIT(to, 4ull * V + ts);             /* o[s] */                               \
+            if (fp) EMIT(to, 5ull * V + tp);             /* o[p] */                               \
+            if (fs && fp && (b = map_slot(&bidx, (2ull << 62) | ((uint64_t)ts << 31) | tp, 0)))   \
+                EMIT(to, 6ull * V + *b);                 /* o[s,p] */                             \
+        }                                                                                         \
+        if (proj_p) {                                                                             \
+            if (fs) EMIT(tp, 2ull * V + ts);             /* p[s] */                               \
+            if (fo) EMIT(tp, 3ull * V + to);             /* p[o] */                               \
+            if (fs && fo && (b = map_slot(&bidx, (1ull << 62) | ((uint64_t)ts << 31) | to, 0)))   \
+                EMIT(tp, 6ull * V + *b);                 /* p[s,o] */                             \
+        }                                                                                         \
+        if (proj_s) {                                                                             \
+            if (fp) EMIT(ts, 0ull * V + tp);             /* s[p] */                               \
+            if (fo) EMIT(ts, 1ull * V + to);             /* s[o] */                               \
+            if (fp && fo && (b = map_slot(&bidx, (0ull << 62) | ((uint64_t)tp << 31) | to, 0)))   \
+                EMIT(ts, 6ull * V + *b);                 /* s[p,o] */                             \
+        }                                                                                         \
     }
-#undef EMIT
+#define COUNT(join, cap) (void)(join), (void)(cap), k++
+#define STORE(join, cap) rec[k++] = ((uint64_t)(join) << capbits) | (uint64_t)(cap)
+    chunk[0] = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int ch = 0; ch < NCH; ++ch) {
+        uint64_t k = 0;
+        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(COUNT)
+        chunk[ch + 1] = k;
+    }
+    for (int ch = 0; ch < NCH; ++ch) chunk[ch + 1] += chunk[ch];
+    const uint64_t nr = chunk[NCH];
+    uint64_t *rec = (uint64_t *)xmalloc(nr * sizeof(uint64_t));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int ch = 0; ch < NCH; ++ch) {
+        uint64_t k = chunk[ch];
+        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(STORE)
+    }
+#undef COUNT
+#undef STORE
+#undef EMIT_ALL
+    free(chunk);
     map_free(&bidx);
     free(freq);
     st->n_records = nr;

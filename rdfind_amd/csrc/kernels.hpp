@@ -45,6 +45,10 @@ static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched toge
 #endif
 static constexpr int LIGHT_SERIAL = RDF_LIGHT_SERIAL;  // windows with at most this many light groups: lanes over candidates
 static constexpr u32 LIGHT_LDS = 512;
+// Dense light groups (at least C / RDFIND_DENSE members, default 32, and at least LIGHT_DENSE_MIN) also get an exact
+// bitmap over the compact capture space (C bits, no more bytes than the member list): a (candidate, group) test is one
+// 4-B load instead of a ~log2(n)-level divergent search.
+static constexpr u64 LIGHT_DENSE_MIN = 256;
 #ifndef RDF_LIGHT_SMALL
 #define RDF_LIGHT_SMALL 31
 #endif
@@ -102,6 +106,9 @@ struct CindView {
     const u64* sig;       // light-group signature of each capture, SIG_W words (null: no signature test)
     const u32* ginfo;     // group -> member count | GINFO_HEAVY (k_group_info)
     const u32* piv2;      // dependent -> its smallest light group other than the pivot (NONE32: none / not computed)
+    const u32* gdrow;     // group -> row of its exact member bitmap (dense light groups), NONE32 (null: no bitmaps)
+    const u32* dbits;     // dense-group bitmaps: row r at dbits + r * dwords, bit x set iff capture x is a member
+    u64 dwords;
 };
 
 }  // namespace rdf

@@ -990,6 +990,63 @@ __device__ inline u64 group_pos(const CindView& v, u32 g, u32 x) {
 }
 
 
+// exact member bitmap of a dense light group (null: g has none; search its member list)
+__device__ inline const u32* dense_row(const CindView& v, u32 g) {
+    if (!v.gdrow) return nullptr;
+    const u32 r = v.gdrow[g];
+    return r == NONE32 ? nullptr : v.dbits + (u64)r * v.dwords;
+}
+__device__ inline bool dense_has(const u32* row, u32 x) { return (row[x >> 5] >> (x & 31)) & 1u; }
+
+// dense light groups: flags (light, >= dmin members) for the row numbering scan
+__global__ __launch_bounds__(RDF_BLOCK) void k_dense_flags(const u32* __restrict__ ginfo, u64 G, u32 dmin, u32* flags) {
+    for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 gi = ginfo[g];
+        flags[g] = !(gi & GINFO_HEAVY) && gi >= dmin ? 1u : 0u;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_dense_rows(const u32* __restrict__ flags, const u32* __restrict__ pos, u64 G,
+                                                          u32* gdrow, u32* dlist) {
+    for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
+        if (flags[g]) {
+            gdrow[g] = pos[g];
+            dlist[pos[g]] = (u32)g;
+        } else {
+            gdrow[g] = NONE32;
+        }
+    }
+}
+// one block per dense row: zero it, then OR in the members (sorted, so a wave's lanes that hit the same word are
+// merged by a segmented scan and only the segment's last lane issues the atomic)
+__global__ __launch_bounds__(RDF_BLOCK) void k_dense_build(const u32* __restrict__ dlist, const u32* __restrict__ nrows,
+                                                           u64 rows_max, const u64* __restrict__ goff,
+                                                           const u32* __restrict__ gcap, u64 dwords, u32* dbits) {
+    const u64 nr = *nrows;
+    const int lane = lane_id();
+    for (u64 r = blockIdx.x; r < nr && r < rows_max; r += gridDim.x) {
+        u32* row = dbits + r * dwords;
+        for (u64 w = threadIdx.x; w < dwords; w += RDF_BLOCK) row[w] = 0;
+        __threadfence();
+        __syncthreads();
+        const u32 g = dlist[r];
+        const u64 b = goff[g], e = goff[g + 1];
+        for (u64 j0 = b; j0 < e; j0 += RDF_BLOCK) {
+            const u64 j = j0 + threadIdx.x;
+            const u32 x = j < e ? gcap[j] : NONE32;
+            const u32 w = x == NONE32 ? NONE32 : x >> 5;
+            u32 acc = x == NONE32 ? 0u : 1u << (x & 31);
+#pragma unroll
+            for (int off = 1; off < RDF_WAVE; off <<= 1) {
+                const u32 ow = __shfl_up(w, off, RDF_WAVE), ob = __shfl_up(acc, off, RDF_WAVE);
+                if (lane >= off && ow == w) acc |= ob;
+            }
+            const u32 nw = __shfl_down(w, 1, RDF_WAVE);
+            if (w != NONE32 && (lane == RDF_WAVE - 1 || nw != w)) atomicOr(&row[w], acc);
+        }
+        __syncthreads();
+    }
+}
+
 // candidate filter: the i-th member of the pivot group (or NONE)
 __device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 i) {
     if (v.vcoff) {  // sharded verify pass: the candidates are given (already filtered by the pivot holder)
@@ -1042,11 +1099,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_info(const u64* __restrict_
 // One group (members [gb, gb+gs)) checked for every alive candidate of the wave (lanes over candidates): a group of
 // at most LIGHT_LDS members is staged into the wave's LDS slice by one coalesced load, so each search is LDS probes;
 // a larger one is searched in place (the lanes share its top levels).  Returns the candidates still alive.
-__device__ inline u64 check_group(const CindView& v, u64 gb, u32 gs, u32 cand, u64 alive, u32* buf) {
+__device__ inline u64 check_group(const CindView& v, u64 gb, u32 gs, u32 cand, u64 alive, u32* buf, const u32* drow) {
     const int lane = lane_id();
     const bool mine = (alive >> lane) & 1ull;
     bool found = true;
-    if (gs <= LIGHT_LDS) {
+    if (drow) {  // dense group: one bitmap word per candidate
+        if (mine) found = dense_has(drow, cand);
+    } else if (gs <= LIGHT_LDS) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
         __builtin_amdgcn_wave_barrier();
         for (u32 k = lane; k < gs; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
@@ -1144,27 +1203,32 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     const u32 cand = pivot_candidate(v, d, id, piv, k * 8 + (g & 7));
     bool ok = cand != NONE32;
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;  // the smallest light group after the pivot first (most kills)
-    if (ok && p2 != NONE32) ok = bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
+    if (ok && p2 != NONE32) {
+        const u32* dr2 = dense_row(v, p2);
+        ok = dr2 ? dense_has(dr2, cand) : bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
+    }
     const u64 b = v.doff[d], e = v.doff[d + 1];
     // PACK_STEP group entries at a time: their ids, bounds and searches are independent loads (one round trip per
     // level for all of them instead of one chain per group)
     for (u64 j0 = b; ok && j0 < e; j0 += PACK_STEP) {
         u32 gr[PACK_STEP];
         const u32* ga[PACK_STEP];
+        const u32* dr[PACK_STEP];
         u64 gn[PACK_STEP];
 #pragma unroll
         for (int i = 0; i < PACK_STEP; ++i) gr[i] = j0 + i < e ? v.dgrp[j0 + i] : NONE32;  // heavy entries: DGRP_HEAVY
 #pragma unroll
         for (int i = 0; i < PACK_STEP; ++i) {
             const bool lt = !(gr[i] == piv || gr[i] == p2 || (gr[i] & DGRP_HEAVY));
+            dr[i] = lt ? dense_row(v, gr[i]) : nullptr;
             const u64 gb = lt ? v.goff[gr[i]] : 0;
-            gn[i] = lt ? v.goff[gr[i] + 1] - gb : 0;
+            gn[i] = lt && !dr[i] ? v.goff[gr[i] + 1] - gb : 0;  // dense groups: a bitmap word instead of a search
             ga[i] = v.gcap + gb;
         }
         bool f[PACK_STEP];
         multi_search<PACK_STEP>(ga, gn, cand, f);
 #pragma unroll
-        for (int i = 0; i < PACK_STEP; ++i) ok = ok && (gn[i] == 0 || f[i]);
+        for (int i = 0; i < PACK_STEP; ++i) ok = ok && (dr[i] ? dense_has(dr[i], cand) : (gn[i] == 0 || f[i]));
     }
     const u64 alive = __ballot(ok);
     const int lane = lane_id(), o = lane >> 3, jj = lane & 7;
@@ -1205,7 +1269,7 @@ __device__ u32* g_item_rec;
 // one batch of the group-parallel window: the next K alive candidates (taken from todo) searched in every lane's
 // group gm (g == NONE32: no group in this lane); a candidate missing from any lane's group dies
 template <int K>
-__device__ inline void light_batch(const u32* gm, u64 gsz, u32 g, u32 cand, u64& todo, u64& alive) {
+__device__ inline void light_batch(const u32* gm, u64 gsz, const u32* drow, u32 g, u32 cand, u64& todo, u64& alive) {
     int bit[K];
     u32 key[K];
 #pragma unroll
@@ -1215,7 +1279,12 @@ __device__ inline void light_batch(const u32* gm, u64 gsz, u32 g, u32 cand, u64&
         key[k] = __shfl(cand, bit[k] < 0 ? bit[0] : bit[k], RDF_WAVE);
     }
     bool ok[K];
-    search_batch<K>(gm, gsz, key, ok);
+    if (drow) {  // dense group: K independent bitmap words
+#pragma unroll
+        for (int k = 0; k < K; ++k) ok[k] = dense_has(drow, key[k]);
+    } else {
+        search_batch<K>(gm, gsz, key, ok);
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (bit[k] >= 0 && !__all(g == NONE32 || ok[k])) alive &= ~(1ull << bit[k]);
@@ -1252,7 +1321,8 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
     if (p2 != NONE32 && alive) {
         const u64 gb2 = v.goff[p2];
-        alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE]);
+        alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
+                            dense_row(v, p2));
     }
     // Lanes take one group each (LIGHT_IT per lane); dependents with few groups went to k_light_packed, so
     // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
@@ -1261,6 +1331,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         u32 gg[LIGHT_IT];
         u64 gbv[LIGHT_IT];
         u32 gszv[LIGHT_IT];
+        const u32* gdr[LIGHT_IT];
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it) {
             const u64 j = s0 + (u64)it * RDF_WAVE + lane;
@@ -1273,9 +1344,11 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         for (int it = 0; it < LIGHT_IT; ++it) {
             gbv[it] = 0;
             gszv[it] = 0;
+            gdr[it] = nullptr;
             if (gg[it] != NONE32) {
                 gbv[it] = v.goff[gg[it]];
                 gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
+                gdr[it] = dense_row(v, gg[it]);
             }
         }
 #pragma unroll
@@ -1300,7 +1373,8 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                     LSTAT_SER(1);
                     const u64 gb = __shfl(gbv[it], l, RDF_WAVE);
                     const u32 gs = __shfl(gszv[it], l, RDF_WAVE);
-                    alive = check_group(v, gb, gs, cand, alive, buf);
+                    const u32* dr = (const u32*)__shfl((unsigned long long)gdr[it], l, RDF_WAVE);
+                    alive = check_group(v, gb, gs, cand, alive, buf, dr);
                 }
                 continue;
             }
@@ -1357,9 +1431,10 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             while (todo) {
                 LSTAT_BAT(gsz ? 64 - __clzll(gsz) : 0);
                 const int na = __popcll(todo);
-                if (na <= 2) light_batch<2>(gm, gsz, g, cand, todo, alive);
-                else if (na <= 4) light_batch<4>(gm, gsz, g, cand, todo, alive);
-                else light_batch<LIGHT_BATCH>(gm, gsz, g, cand, todo, alive);
+                const u32* dr = gdr[it];
+                if (na <= 2) light_batch<2>(gm, gsz, dr, g, cand, todo, alive);
+                else if (na <= 4) light_batch<4>(gm, gsz, dr, g, cand, todo, alive);
+                else light_batch<LIGHT_BATCH>(gm, gsz, dr, g, cand, todo, alive);
             }
         }
     }
@@ -2161,6 +2236,27 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
         acc[2] += le;
     }
     block_partials3(acc, heavy_candidates);
+}
+
+// dependent segments of concatenated (dep, ref)-sorted runs with disjoint dependents: [segb[d], sege[d]) in the input
+__global__ __launch_bounds__(RDF_BLOCK) void k_seg_bounds(const u64* __restrict__ a, u64 n, u64* segb, u64* sege) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 d = a[i] >> 32;
+        if (i == 0 || (a[i - 1] >> 32) != d) segb[d] = i;
+        if (i + 1 == n || (a[i + 1] >> 32) != d) sege[d] = i + 1;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_seg_lengths(const u64* __restrict__ segb, const u64* __restrict__ sege, u32 C,
+                                                           u32* len) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
+        len[d] = (u32)(sege[d] - segb[d]);
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_seg_scatter(const u64* __restrict__ a, u64 n, const u64* __restrict__ segb,
+                                                           const u64* __restrict__ eoff, u64* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 d = a[i] >> 32;
+        out[eoff[d] + (i - segb[d])] = a[i];
+    }
 }
 
 // (dep << 32 | ref) -> (owner << 2cb | dep << cb | ref), so one radix sort groups the pairs by owner

@@ -78,6 +78,11 @@ struct rdf_ctx {
     DevBuf gsums;  // sum of light group sizes, of their squares (k_group_info)
     bool light_stage = false;  // k_light<true>: stage small light groups in LDS rows (chosen per run)
     DevBuf piv2;   // dependent -> second pivot (smallest light group after the pivot)
+    DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
+    bool dense_on = false;
+    u64 dwords = 0, n_dense = 0;
+    int dense_div = 32;                   // RDFIND_DENSE (0: no bitmaps)
+    u64 dense_min = LIGHT_DENSE_MIN;      // RDFIND_DENSE_MIN (test hook: bitmaps for small groups too)
     bool sig_on = false;  // lsig holds this run's signatures (RDFIND_SIG=0 turns the filter off)
     bool sig_packed = false;  // the packed light path tests them too (RDFIND_SIG=1; default 2: k_light only)
     bool piv2_on = false;     // piv2 holds this run's second pivots
@@ -114,6 +119,9 @@ struct rdf_ctx {
     DevBuf uhist, urecs, usl, cntg, fstage, bfreq, boff, fbits, brkeys;  // partitioned K1 / K2 (counts.inl)
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     DevBuf lmask, hrep, vpairs, vcoff, vpiv;  // holder-first light exchange (sh_phase5 / sh_phase15)
+    DevBuf ebown, segb, sege, seglen;         // this rank's binary dependents' final pairs; dependent segments
+    DevBuf ukeys, ukeys_tmp;                  // sharded: frequent unary keys (owned, then every rank's, sorted)
+    u64 sh_Eb = 0;
     u64 n_hrep = 0;
     u64 n_out = 0, n_runs = 0;
     u32* out_ptr = nullptr;
@@ -270,7 +278,8 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff};
+            &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
+            &c->ukeys_tmp};
 }
 
 extern "C" {
@@ -292,6 +301,11 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     c->allow_hclass = !(hcl && !strcmp(hcl, "0"));
     const char* hmin = getenv("RDFIND_HEAVY_MIN");
     if (hmin && atoll(hmin) > 0) c->heavy_min = (u64)atoll(hmin);
+    // dense light-group bitmaps: RDFIND_DENSE=<divisor> (groups of >= C / divisor members; 0 = off) and the test hook
+    // RDFIND_DENSE_MIN=<members> (absolute minimum, default LIGHT_DENSE_MIN)
+    if (const char* dd = getenv("RDFIND_DENSE")) c->dense_div = atoi(dd);
+    if (const char* dm = getenv("RDFIND_DENSE_MIN"))
+        if (atoll(dm) > 0) c->dense_min = (u64)atoll(dm);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -558,7 +572,7 @@ rdf_status rdf_copy_terms(rdf_ctx* c, uint64_t* offsets, uint32_t* lengths, uint
 // Stage 1: frequent conditions (FrequentConditionPlanner.constructFrequentConditionPlan)
 
 // K1 partitioned over (s, p, o, n): bucket histogram, scatter of the low key bits, per-bucket LDS counting.
-// counts_only: the dense counts land in cntg (sharded input: summed over ranks, then fc_ranks_from_counts);
+// counts_only: the dense counts land in cntg (sharded input: their nonzero entries go to the keys' owners);
 // otherwise ranks, fbits and the rank-block totals bfreq are written (fc_unary_finish makes them global).
 static rdf_status fc_unary_part(rdf_ctx* c, const u32* s, const u32* p, const u32* o, u64 n, int ubits, u64 NB,
                                 bool counts_only) {
@@ -680,52 +694,22 @@ static rdf_status fc_unary(rdf_ctx* c, u64 nfreq[3]) {
     return RDF_OK;
 }
 
-// ranks from dense, globally summed counts (sharded input)
-static rdf_status fc_ranks_from_counts(rdf_ctx* c, const u32* cnt, u64 nfreq[3]) {
-    hipStream_t st = c->stream;
-    const u32 V = c->V ? c->V : 1;
-    const u64 K = 3ull * V;
-    const int ubits = fc_ubits(K);
-    const u64 NB = (K + (1ull << ubits) - 1) >> ubits;
-    if (NB > U2_MAXB) {  // |V| beyond the bucketed range: flags + one scan over the counts (boff = 0)
-        const u64 NR = (K + FR_R - 1) / FR_R;
-        HIP_TRY(c, hipMemsetAsync(c->boff.p, 0, (NR + 2) * 4, st));
-        ENSURE(c, flags, K * 4);
-        hipLaunchKernelGGL(k_frank_flags, dim3(grid_for(K, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, K, c->ms,
-                           c->flags.as<u32>());
-        hipLaunchKernelGGL(k_fbits_from_counts, dim3(grid_for(K, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, K, c->ms,
-                           c->fbits.as<u64>());
-        HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->frank.as<u32>(), K, (u32*)dscal(c, 6), st));
-        hipLaunchKernelGGL(k_count_frequent, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, V, c->ms,
-                           dscal(c, 0));
-        TRY(read_scalars(c, 7));
-        for (int t = 0; t < 3; ++t) nfreq[t] = c->hscal[t];
-        c->U = (u32)c->hscal[6];
-        ENSURE(c, fval, std::max<u64>(c->U, 1) * 4);
-        hipLaunchKernelGGL(k_frank_final, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, cnt, V, c->ms,
-                           c->frank.as<u32>(), c->fval.as<u32>());
-        return RDF_OK;
-    }
-    if (ubits == 14)
-        hipLaunchKernelGGL(k_u2_rank_counts<14>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, c->stream, (u32)NB, K, V, c->ms, cnt,
-                           c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0));
-    else
-        hipLaunchKernelGGL(k_u2_rank_counts<15>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, c->stream, (u32)NB, K, V, c->ms, cnt,
-                           c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0));
-    return fc_unary_finish(c, nfreq);
-}
-
 // sum (key, count) pairs in one global table (2x the pairs) and append the frequent keys at bkeys + *B; the pairs
 // are either two arrays (keys, cnt) or interleaved words (cnt == nullptr).  *nkeys += distinct keys.
-static rdf_status fc_sum_pairs(rdf_ctx* c, const u64* keys, const u32* cnt, u64 m, u64* B, u64* nkeys) {
+static rdf_status fc_sum_pairs(rdf_ctx* c, const u64* keys, const u32* cnt, u64 m, u64* B, u64* nkeys,
+                               bool packed = false, DevBuf* outbuf = nullptr) {
     hipStream_t st = c->stream;
+    DevBuf& out = outbuf ? *outbuf : c->bkeys;
     const u64 tcap = next_pow2(std::max<u64>(1024, 2 * m));
     ENSURE(c, lkeys, tcap * 8);  // lkeys / lvals are rebuilt afterwards (frequent-key lookup)
     ENSURE(c, lvals, tcap * 4);
     HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, tcap * 8, st));
     HIP_TRY(c, hipMemsetAsync(c->lvals.p, 0, tcap * 4, st));
     if (m) {
-        if (cnt)
+        if (packed)
+            hipLaunchKernelGGL(k_packed_insert, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, m,
+                               c->lkeys.as<u64>(), c->lvals.as<u32>(), tcap - 1);
+        else if (cnt)
             hipLaunchKernelGGL(k_spill_insert, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, cnt, m,
                                c->lkeys.as<u64>(), c->lvals.as<u32>(), tcap - 1);
         else
@@ -740,9 +724,9 @@ static rdf_status fc_sum_pairs(rdf_ctx* c, const u64* keys, const u32* cnt, u64 
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->fpos.as<u64>(), tcap, dscal(c, 7), st));
     TRY(read_scalars(c, 8));
     const u64 nf = c->hscal[7];
-    ENSURE_KEEP(c, bkeys, (*B + nf + 1) * 8);
+    HIP_TRY(c, out.grow_keep((size_t)(*B + nf + 1) * 8, st));
     hipLaunchKernelGGL(k_bin_freq_scatter, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->lkeys.as<u64>(),
-                       c->flags.as<u32>(), c->fpos.as<u64>(), tcap, c->bkeys.as<u64>() + *B);
+                       c->flags.as<u32>(), c->fpos.as<u64>(), tcap, out.as<u64>() + *B);
     *nkeys += c->hscal[6];
     *B += nf;
     return RDF_OK;
@@ -1325,7 +1309,48 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.sig = c->sig_on ? c->lsig.as<u64>() : nullptr;
     v.ginfo = c->ginfo.as<u32>();
     v.piv2 = c->piv2_on ? c->piv2.as<u32>() : nullptr;
+    v.gdrow = c->dense_on ? c->gdrow.as<u32>() : nullptr;
+    v.dbits = c->dense_on ? c->dbits.as<u32>() : nullptr;
+    v.dwords = c->dwords;
     return v;
+}
+
+// exact member bitmaps of the dense light groups (>= C / RDFIND_DENSE members, default 32: a row of C bits is no
+// larger than the member list; 0 turns them off).  Rows are numbered in group order; no host round trip: the row
+// count stays on the device and the bitmap is sized for the most rows the member total allows.
+static rdf_status d_dense_bitmaps(rdf_ctx* c, CindView& v) {
+    hipStream_t st = c->stream;
+    const int div = c->dense_div;
+    const u64 G = c->G, C = c->C;
+    c->dense_on = false;
+    v.gdrow = nullptr;
+    v.dbits = nullptr;
+    if (div <= 0 || !G || !C) return RDF_OK;
+    const u64 dmin = std::max<u64>((C + div - 1) / div, c->dense_min);
+    const u64 rows_max = std::min<u64>(G, c->Jf / dmin);
+    if (!rows_max) return RDF_OK;
+    const u64 dwords = ((C + 31) / 32 + 31) & ~31ull;  // rows start on 128-B lines
+    tbegin(c, RDF_T_LIGHT);
+    ENSURE(c, gflag, G * 4);
+    ENSURE(c, gexcl, (G + 1) * 4);
+    ENSURE(c, gdrow, G * 4);
+    ENSURE(c, dlist, rows_max * 4);
+    ENSURE(c, dbits, rows_max * dwords * 4);
+    hipLaunchKernelGGL(k_dense_flags, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ginfo.as<u32>(), G,
+                       (u32)std::min<u64>(dmin, 0x7fffffffu), c->gflag.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), G, c->gexcl.as<u32>() + G, st));
+    hipLaunchKernelGGL(k_dense_rows, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gflag.as<u32>(),
+                       c->gexcl.as<u32>(), G, c->gdrow.as<u32>(), c->dlist.as<u32>());
+    hipLaunchKernelGGL(k_dense_build, dim3((unsigned)std::min<u64>(rows_max, 4096)), dim3(RDF_BLOCK), 0, st,
+                       c->dlist.as<u32>(), c->gexcl.as<u32>() + G, rows_max, c->goff.as<u64>(), c->gcap.as<u32>(),
+                       dwords, c->dbits.as<u32>());
+    tend(c, RDF_T_LIGHT);
+    c->dense_on = true;
+    c->dwords = dwords;
+    v.gdrow = c->gdrow.as<u32>();
+    v.dbits = c->dbits.as<u32>();
+    v.dwords = dwords;
+    return RDF_OK;
 }
 
 // local pivot statistics: pbest[d] = (size << 32 | group) of d's smallest local group, pnl[d] = local light groups
@@ -1372,6 +1397,7 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gi_grid, c->gsums.as<u64>());
     }
     tend(c, RDF_T_PIVOT);
+    TRY(d_dense_bitmaps(c, v));
     static const int piv2_mode = getenv("RDFIND_PIV2") ? atoi(getenv("RDFIND_PIV2")) : 1;  // 2: k_light only
     const bool piv2_enabled = piv2_mode != 0;
     c->piv2_packed = piv2_mode != 2;
@@ -1883,7 +1909,7 @@ static void sh_slice(rdf_ctx* c, const u32** s, const u32** p, const u32** o, u6
     *n = e - b;
 }
 
-// local dense unary counts -> all-reduce(sum)
+// local dense unary counts -> nonzero (key, count) words to the keys' owners (all-to-all)
 static rdf_status sh_phase10(rdf_ctx* c, rdf_exchange* req) {
     hipStream_t st = c->stream;
     TRY(fc_begin(c, c->sh_ms));
@@ -1904,17 +1930,66 @@ static rdf_status sh_phase10(rdf_ctx* c, rdf_exchange* req) {
             hipLaunchKernelGGL(k_unary_count, dim3(std::min<unsigned>(grid_for(n, RDF_BLOCK * 4), 1024)), dim3(RDF_BLOCK), 0,
                                st, s, p, o, n, V, c->cntg.as<u32>());
     }
+    const u32 R = c->sh_nranks;
+    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>(1024, (K + 65535) / 65536));
+    ENSURE(c, uhist, ((u64)R * G + 1) * 4);
+    ENSURE(c, xsend, std::max<u64>(std::min<u64>(K, 3 * n), 1) * 8);
+    hipLaunchKernelGGL((k_unary_route<false>), dim3(G), dim3(RDF_BLOCK), 0, st, c->cntg.as<u32>(), K, R, c->uhist.as<u32>(),
+                       (u64*)nullptr);
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), (u64)R * G, c->uhist.as<u32>() + (u64)R * G, st));
+    hipLaunchKernelGGL((k_unary_route<true>), dim3(G), dim3(RDF_BLOCK), 0, st, c->cntg.as<u32>(), K, R, c->uhist.as<u32>(),
+                       c->xsend.as<u64>());
     tend(c, RDF_T_UNARY);
+    std::vector<u32> h((u64)R * G + 1);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->uhist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U32, c->cntg.p, K, 11);
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->xsend.p, h[(u64)R * G], 16));
+    for (u32 r = 0; r < R; ++r) req->send_counts[r] = h[(u64)(r + 1) * G] - h[(u64)r * G];
+    return RDF_OK;
 }
 
-// global counts -> ranks; local binary (key, count) partials -> all-to-all to the keys' owners
+// received unary partials of this rank's keys -> summed -> frequent keys -> all-gather
+static rdf_status sh_phase16(rdf_ctx* c, rdf_exchange* req) {
+    tbegin(c, RDF_T_UNARY);
+    u64 Bu = 0, nk = 0;
+    TRY(fc_sum_pairs(c, c->xrecv.as<u64>(), nullptr, c->x_recv_count, &Bu, &nk, true, &c->ukeys));
+    tend(c, RDF_T_UNARY);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ukeys.p, Bu, 11);
+}
+
+// every owner's frequent unary keys -> global ranks; local binary (key, count) partials -> all-to-all to the keys' owners
 static rdf_status sh_phase11(rdf_ctx* c, rdf_exchange* req) {
     hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 K = 3ull * V, NR = (K + FR_R - 1) / FR_R;
+    const u64 U = c->x_recv_count;
     tbegin(c, RDF_T_UNARY);
-    TRY(fc_ranks_from_counts(c, c->xrecv.as<u32>(), c->sh_nfreq));
+    ENSURE(c, ukeys, std::max<u64>(U, 1) * 8);
+    ENSURE(c, ukeys_tmp, std::max<u64>(U, 1) * 8);
+    if (U) HIP_TRY(c, hipMemcpyAsync(c->ukeys.p, c->xrecv.p, U * 8, hipMemcpyDeviceToDevice, st));
+    {
+        u64* k = c->ukeys.as<u64>();
+        u64* t = c->ukeys_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, U, bits_for(K - 1), st));
+        if (k != c->ukeys.as<u64>()) std::swap(c->ukeys, c->ukeys_tmp);
+    }
+    HIP_TRY(c, hipMemsetAsync(c->frank.p, 0xff, K * 4, st));
+    HIP_TRY(c, hipMemsetAsync(c->fbits.p, 0, ((K + 63) / 64 + 1) * 8, st));
+    HIP_TRY(c, hipMemsetAsync(c->boff.p, 0, (NR + 2) * 4, st));  // frank holds global ranks
+    ENSURE(c, fval, std::max<u64>(U, 1) * 4);
+    if (U)
+        hipLaunchKernelGGL(k_ranks_from_keys, dim3(grid_for(U, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ukeys.as<u64>(), U,
+                           V, c->frank.as<u32>(), c->fval.as<u32>(), c->fbits.as<u64>());
+    hipLaunchKernelGGL(k_lower_bound1, dim3(1), dim3(1), 0, st, c->ukeys.as<u64>(), U, (u64)V, dscal(c, 5));
+    hipLaunchKernelGGL(k_lower_bound1, dim3(1), dim3(1), 0, st, c->ukeys.as<u64>(), U, 2ull * V, dscal(c, 6));
+    u64 lb[2];
+    TRY(read_multi(c, {{dscal(c, 5), 8}, {dscal(c, 6), 8}}, lb));
     tend(c, RDF_T_UNARY);
+    c->U = (u32)U;
+    c->sh_nfreq[0] = lb[0];
+    c->sh_nfreq[1] = lb[1] - lb[0];
+    c->sh_nfreq[2] = U - lb[1];
     const u32 *s, *p, *o;
     u64 n;
     sh_slice(c, &s, &p, &o, &n);
@@ -2258,19 +2333,60 @@ static rdf_status sh_phase6(rdf_ctx* c, rdf_exchange* req) {
     if (n)
         hipLaunchKernelGGL(k_compact_u64, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), n,
                            c->flags.as<u32>(), c->pos.as<u64>(), c->xsend.as<u64>());
+    // The minimality rules probe other dependents only through the unary components of binary dependents
+    // (R1 / R4, rule_keep -> member(comp, ref)), so only the unary dependents' pairs -- a prefix of the sorted final
+    // pairs -- go to every rank; the binary dependents' pairs stay with their owner (this rank).
+    ENSURE(c, obounds, (RDF_MAX_RANKS + 1) * 8);
+    hipLaunchKernelGGL(k_lower_bound1, dim3(1), dim3(1), 0, st, c->xsend.as<u64>(), E, (u64)c->Cu << 32,
+                       c->obounds.as<u64>());
+    u64 Eu = 0;
+    TRY(read_u64(c, c->obounds.as<u64>(), &Eu));
+    c->sh_Eb = E - Eu;
+    ENSURE(c, ebown, std::max<u64>(E - Eu, 1) * 8);
+    if (E > Eu) HIP_TRY(c, hipMemcpyAsync(c->ebown.p, c->xsend.as<u64>() + Eu, (E - Eu) * 8, hipMemcpyDeviceToDevice, st));
     tend(c, RDF_T_ESORT);
     HIP_TRY(c, hipStreamSynchronize(st));
-    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, E, 7);
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, Eu, 7);
+}
+
+// Pairs of several (dep, ref)-sorted runs whose dependents are disjoint (each rank's unary pairs, this rank's binary
+// pairs) -> one (dep, ref)-sorted array, by dependent segments (no sort): out[eoff[d] + i - head(d)] = in[i].
+static rdf_status merge_dep_runs(rdf_ctx* c, const u64* in, u64 n, u64* out) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    ENSURE(c, segb, std::max<u64>(C, 1) * 8);
+    ENSURE(c, sege, std::max<u64>(C, 1) * 8);
+    ENSURE(c, seglen, std::max<u64>(C, 1) * 4);
+    ENSURE(c, eoff, (C + 1ull) * 8);
+    if (!C) return RDF_OK;
+    HIP_TRY(c, hipMemsetAsync(c->segb.p, 0, (u64)C * 8, st));
+    HIP_TRY(c, hipMemsetAsync(c->sege.p, 0, (u64)C * 8, st));
+    if (n)
+        hipLaunchKernelGGL(k_seg_bounds, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, in, n, c->segb.as<u64>(),
+                           c->sege.as<u64>());
+    hipLaunchKernelGGL(k_seg_lengths, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->segb.as<u64>(),
+                       c->sege.as<u64>(), C, c->seglen.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->seglen.as<u32>(), c->eoff.as<u64>(), C, c->eoff.as<u64>() + C, st));
+    if (n)
+        hipLaunchKernelGGL(k_seg_scatter, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, in, n, c->segb.as<u64>(),
+                           c->eoff.as<u64>(), out);
+    return RDF_OK;
 }
 
 static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     hipStream_t st = c->stream;
-    const u64 E = c->x_recv_count;  // every rank's final explicit pairs
+    const u64 Eu = c->x_recv_count, Eb = c->sh_Eb;  // every rank's unary pairs + this rank's binary pairs
+    const u64 E = Eu + Eb;
+    ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
     ENSURE(c, epairs, std::max<u64>(E, 1) * 8);
-    HIP_TRY(c, hipMemcpyAsync(c->epairs.p, c->xrecv.p, E * 8, hipMemcpyDeviceToDevice, st));
+    if (Eu) HIP_TRY(c, hipMemcpyAsync(c->epairs_tmp.p, c->xrecv.p, Eu * 8, hipMemcpyDeviceToDevice, st));
+    if (Eb) HIP_TRY(c, hipMemcpyAsync(c->epairs_tmp.as<u64>() + Eu, c->ebown.p, Eb * 8, hipMemcpyDeviceToDevice, st));
     c->sh_E = E;
+    tbegin(c, RDF_T_ESORT);
+    TRY(merge_dep_runs(c, c->epairs_tmp.as<u64>(), E, c->epairs.as<u64>()));
+    tend(c, RDF_T_ESORT);
     CindView v = make_view(c, c->sh_flags);
-    TRY(d_explicit_index(c, v, E, false));
+    TRY(d_explicit_index(c, v, E, true));
     u64 H = 0;
     TRY(d_heavy_count(c, v, c->sh_WH, &H));
     c->sh_H = H;
@@ -2391,10 +2507,11 @@ static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
     return RDF_OK;
 }
 
-// phases: 10-14 (condition counts, routing of the triples), then 1-8; pending = a phase that follows a collective
+// phases: 10, 16, 11-14 (condition counts, routing of the triples), then 1-8 (15 between 5 and 6); pending = a
+// phase that follows a collective
 static bool sh_phase_valid(int ph, bool pending) {
     if (ph >= 1 && ph <= 8) return true;
-    if (ph >= 11 && ph <= 15) return true;
+    if (ph >= 11 && ph <= 16) return true;
     return !pending && ph == 10;
 }
 
@@ -2432,6 +2549,7 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
         case 4: r = sh_phase4(c, req); break;
         case 5: r = sh_phase5(c, req); break;
         case 15: r = sh_phase15(c, req); break;
+        case 16: r = sh_phase16(c, req); break;
         case 6: r = sh_phase6(c, req); break;
         case 7: r = sh_phase7(c, req); break;
         case 8: r = sh_phase8(c, req); break;

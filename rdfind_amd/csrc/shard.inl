@@ -1,7 +1,7 @@
 // Sharded input (SURVEY.md 8e with the input itself partitioned): every rank holds only its slice of the
 // triples.  The condition counts are combined as partial sums (FrequentConditionPlanner.scala:293-309 and
-// :381-393 groupBy(...).sum): dense unary counts by an all-reduce, binary (key, count) partials by an all-to-all
-// to the key's owner.  Then each triple travels to the ranks owning its join values
+// :381-393 groupBy(...).sum): unary and binary (key, count) partials by an all-to-all to the key's owner, which
+// sums them and contributes its frequent keys to an all-gather.  Then each triple travels to the ranks owning its join values
 // (ALG/programs/RDFind.scala:339-345 groupBy(joinValue)), so capture groups stay local to their join shard.
 // Included by kernels.inl.
 
@@ -91,17 +91,44 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pairs_insert(const u64* __restric
         global_hash_add(tkeys, tcnt, tmask, in[2 * i], (u32)in[2 * i + 1]);
 }
 
-// unary ranks of every K1 bucket from the (all-reduced) dense counts
-template <int BITS>
-__global__ __launch_bounds__(U2_CBLOCK) void k_u2_rank_counts(u32 NB, u64 K, u32 V, u32 ms, const u32* __restrict__ cnt,
-                                                              u32* frank, u32* bfreq, u32* fstage, u64* fbits, u64* nbound) {
-    constexpr u32 R = 1u << BITS;
-    __shared__ u32 lc[R];
-    const u32 bk = blockIdx.x;
-    if (bk >= NB) return;
-    const u64 base = (u64)bk << BITS;
-    const u32 lim = (u32)(K - base < R ? K - base : R);
-    for (u32 i = threadIdx.x; i < R; i += U2_CBLOCK) lc[i] = i < lim ? cnt[base + i] : 0u;
+// Sparse unary exchange: the slice's nonzero unary counts as (key << 32 | count) words (key = pos * V + value < 2^32),
+// grouped by the key's owner rank, which sums them; no rank ever moves the dense 3V counter array.
+template <bool SCATTER>
+__global__ __launch_bounds__(RDF_BLOCK) void k_unary_route(const u32* __restrict__ cnt, u64 K, u32 nranks, u32* ghist,
+                                                           u64* __restrict__ out) {
+    __shared__ u32 lh[RDF_MAX_RANKS];
+    for (u32 i = threadIdx.x; i < nranks; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
     __syncthreads();
-    u2_ranks<BITS>(lc, lim, ms, base, V, frank, bfreq, fstage, fbits, nbound);
+    const u64 per = (K + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < K ? b + per : K;
+    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
+        const u32 c = cnt[i];
+        if (!c) continue;
+        const u32 pos = atomicAdd(&lh[key_owner(i, nranks)], 1u);
+        if (SCATTER) out[pos] = (i << 32) | c;
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < nranks; i += RDF_BLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
+    }
 }
+
+// received (key << 32 | count) words -> the global summing table
+__global__ __launch_bounds__(RDF_BLOCK) void k_packed_insert(const u64* __restrict__ in, u64 m, u64* tkeys, u32* tcnt,
+                                                             u64 tmask) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK)
+        global_hash_add(tkeys, tcnt, tmask, in[i] >> 32, (u32)in[i]);
+}
+
+// every owner's frequent unary keys, sorted: global rank u of key k = its index (frank[k] = u with boff = 0),
+// fval[u] = the condition value, fbits = the frequency bitmap (zeroed before)
+__global__ __launch_bounds__(RDF_BLOCK) void k_ranks_from_keys(const u64* __restrict__ keys, u64 U, u32 V, u32* frank,
+                                                               u32* fval, u64* fbits) {
+    for (u64 u = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; u < U; u += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = keys[u];
+        frank[k] = (u32)u;
+        fval[u] = (u32)(k % V);
+        atomicOr((unsigned long long*)&fbits[k >> 6], 1ull << (k & 63));
+    }
+}
+

@@ -2,12 +2,12 @@
 
 ``ShardSim`` answers the same ``shard_begin / shard_step / shard_export / shard_import`` calls as the HIP
 ``Context`` in sharded mode, with the same sequence of collectives and message layouts
-(rdfind_amd/distributed.py, rdfind_hip.hip sh_phase10-14 and 1-8), but computes each rank's part with the
-Python oracle: dense unary counts of the rank's slice (all-reduce), binary (key, count) partials routed to
-the key's owner (all-to-all, same key hash as shard.inl key_owner), the frequent keys all-gathered, every
+(rdfind_amd/distributed.py, rdfind_hip.hip sh_phase10, 16, 11-14 and 1-8), but computes each rank's part with
+the Python oracle: unary and binary (key, count) partials of the rank's slice routed to the key's owner
+(all-to-all, same key hash as shard.inl key_owner), the frequent keys all-gathered, every
 triple routed to the owners of its join values (all-to-all, two words per copy), join lines of the join
 values this rank owns, local intersections, owner-side multiplicity check, then minimality on the gathered
-explicit set.  It treats every group as light (no bitmask columns), so the class exchange is empty.
+explicit set (every rank's unary dependents' pairs + its own binary ones).  It treats every group as light (no bitmask columns), so the class exchange is empty.
 It lets the CPU suite run the real collectives (gloo, world size 2 and 3) and check that the decomposition
 reproduces the single-process oracle result.
 """
@@ -102,19 +102,31 @@ class ShardSim:
         op, arr = self.pending
         self.recv = _view(ptr, n, arr.dtype).copy()
 
-    def _phase10(self):  # dense unary counts of the slice -> all-reduce
+    def _phase10(self):  # unary (key << 32 | count) partials of the slice -> the keys' owners
         V = self.V
-        cnt = np.zeros(3 * V, np.int32)
+        cnt = np.zeros(3 * V, np.int64)
         for s, p, o in self.slice:
             cnt[s] += 1
             cnt[V + p] += 1
             cnt[2 * V + o] += 1
-        return self._req(_lib.X_ALLREDUCE_SUM_U32, cnt, 11)
+        out = [[] for _ in range(self.R)]
+        for k in np.nonzero(cnt)[0].tolist():
+            out[key_owner(k, self.R)].append((k << 32) | int(cnt[k]))
+        send = np.array([x for o in out for x in o], np.int64)
+        return self._req(_lib.X_ALLTOALLV_U64, send, 16, [len(o) for o in out])
 
-    def _phase11(self):  # frequent unary conditions; binary partials -> owners
-        V, ms = self.V, self.ms
-        g = self.recv.astype(np.int64)
-        self.uf = {t: {v: int(g[i * V + v]) for v in range(V) if g[i * V + v] >= ms} for i, t in enumerate((R.S, R.P, R.O))}
+    def _phase16(self):  # summed partials of the owned unary keys -> frequent keys -> all-gather
+        tot = {}
+        for w in self.recv.astype(np.int64).tolist():
+            tot[w >> 32] = tot.get(w >> 32, 0) + (w & 0xFFFFFFFF)
+        return self._req(_lib.X_ALLGATHERV_U64, np.array(sorted(k for k, c in tot.items() if c >= self.ms), np.int64), 11)
+
+    def _phase11(self):  # frequent unary conditions (every owner's keys); binary partials -> owners
+        V = self.V
+        keys = sorted(int(k) for k in self.recv.tolist())
+        self.uf = {t: {} for t in (R.S, R.P, R.O)}
+        for k in keys:
+            self.uf[(R.S, R.P, R.O)[k // V]][k % V] = 1  # presence is all the join-line construction reads
         part = R.frequent_binary_conditions(self.slice, self.uf, 1)  # local counts of every key (threshold 1)
         out = [[] for _ in range(self.R)]
         for (t, v1, v2), c in sorted(part.items()):
@@ -234,14 +246,16 @@ class ShardSim:
         send = np.array([x for part in out for x in part], np.int64)
         return self._req(_lib.X_ALLTOALLV_U64, send, 6, [len(p) for p in out])
 
-    def _phase6(self):
+    def _phase6(self):  # owner check; only the unary dependents' pairs go to every rank (R1/R4 probe those)
         allr = np.concatenate([self.recv.astype(np.int64), np.array(self.reports, np.int64)])
         vals, cnt = np.unique(allr, return_counts=True)
         keep = [int(v) for v, c in zip(vals.tolist(), cnt.tolist()) if c == self.nrl[int(v) >> 32]]
-        return self._req(_lib.X_ALLGATHERV_U64, np.array(keep, np.int64), 7)
+        self.own_binary = [k for k in keep if self.freq[k >> 32].v2 is not None]
+        unary = [k for k in keep if self.freq[k >> 32].v2 is None]
+        return self._req(_lib.X_ALLGATHERV_U64, np.array(unary, np.int64), 7)
 
-    def _phase7(self):
-        self.explicit = sorted(int(x) for x in self.recv)
+    def _phase7(self):  # every rank's unary pairs + this rank's binary pairs: all the rules of owned dependents need
+        self.explicit = sorted([int(x) for x in self.recv] + self.own_binary)
         return self._req(_lib.X_ALLGATHERV_U64, np.zeros(0, np.int64), 8)
 
     def _phase8(self):

@@ -83,7 +83,7 @@ def test_sharded_protocol_matches_oracle(world, local_slice):
         else:
             expected = R.cind_set(R.rdfind(tr, ms, strategy, clean))
         parts = [set(res[r][k][1]) for r in range(world)]
-        assert all(res[r][k][0] == 13 for r in range(world))  # the library's thirteen collectives
+        assert all(res[r][k][0] == 14 for r in range(world))  # the library's fourteen collectives
         union = set().union(*parts)
         assert sum(len(p) for p in parts) == len(union)      # every dependent has one owner
         assert union == expected, (k, ms, strategy, clean)

@@ -229,6 +229,36 @@ def test_heavy_paths_parity(monkeypatch, heavy_min):
         g.close()
 
 
+def test_dense_bitmap_paths_parity(monkeypatch):
+    """Every light group verified through its exact member bitmap (RDFIND_DENSE / RDFIND_DENSE_MIN test hooks: the
+    dense-group path of the light kernels, serial, batched, packed and second-pivot checks), in every mode, and the
+    heavy columns lowered too so that bitmaps and heavy masks mix."""
+    monkeypatch.setenv("RDFIND_DENSE", "1000000")
+    monkeypatch.setenv("RDFIND_DENSE_MIN", "1")
+    for heavy_min in (64, 2):
+        monkeypatch.setenv("RDFIND_HEAVY_MIN", str(heavy_min))
+        g = _lib.Context(0)
+        try:
+            rng = random.Random(300 + heavy_min)
+            for _ in range(60):
+                n = rng.randrange(20, 400)
+                nv = rng.randrange(4, 40)
+                ms = rng.randrange(1, 4)
+                arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
+                               dtype=np.uint32)
+                for strategy, clean in MODES:
+                    assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
+                        (n, nv, ms, strategy, clean, heavy_min)
+            for cfg, scale in (("c5", 0.01), ("c1", 0.05), ("c4", 0.0003)):
+                d = synth.config(cfg, scale)
+                exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+                g.set_triples(d.s, d.p, d.o, d.num_terms)
+                g.run(d.min_support)
+                assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, heavy_min)
+        finally:
+            g.close()
+
+
 def test_large_grids_two_paths(monkeypatch):
     """c5 at scale 0.3 (8.7e9 CINDs): the heavy-only binary dependents take > 2^26 work items (a dispatch holds
     < 2^32 work-items, so the kernels loop over virtual blocks).  The classed path and the pivot-scan path

@@ -120,7 +120,7 @@ def test_sharded_random_matches_single(world, local_slice):
 
 def test_sharded_rccl_backend_world1():
     """The RCCL branch of run_protocol (exchange buffers in HBM, stream syncs around each collective): one rank
-    over the nccl backend (the box has one GPU, and RCCL refuses two ranks on one device); the 13 collectives run
+    over the nccl backend (the box has one GPU, and RCCL refuses two ranks on one device); the 14 collectives run
     with world size 1 and the result equals the single-GPU run."""
     from rdfind_amd import synth
 

@@ -12,9 +12,9 @@ for step in "$@"; do
       timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
         > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/tests_$TAG.log; exit 1; } ;;
     bench)
-      timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
+      timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
         || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
-      cat gpurun_out/bench_$TAG.json ;;
+      head -c 2500 gpurun_out/bench_$TAG.json ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 \
@@ -74,6 +74,11 @@ for step in "$@"; do
     rehearse:*)  # rehearse:<config>:<scale>:<ranks> -- sharded bench with several ranks on the one GPU (gloo)
       IFS=: read -r _ CFG SC NR <<< "$step"
       tools/shard_rehearsal.sh ${TAG}_${CFG}_$NR $CFG $SC $NR || exit 1 ;;
+    tfile:*)  # tfile:<test file>[,<test file>...] -- whole GPU test files (one pytest process)
+      FILES=$(echo "${step#tfile:}" | tr ',' ' ')
+      timeout -k 10 1000 python -u -m pytest $FILES -m gpu -x -v --timeout 600 --timeout-method thread \
+        > gpurun_out/tfile_$TAG.log 2>&1 || { echo "tfile failed"; tail -40 gpurun_out/tfile_$TAG.log; exit 1; }
+      grep -cE "PASSED" gpurun_out/tfile_$TAG.log; tail -2 gpurun_out/tfile_$TAG.log ;;
     gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
         > gpurun_out/gtest_$TAG.log 2>&1 || { echo "gtest failed"; tail -30 gpurun_out/gtest_$TAG.log; exit 1; }

@@ -28,6 +28,8 @@ CASES = {
     "c2": ("c2", 1.0, [(1, True), (0, True)]),
     "c3": ("c3", 1.0, [(1, True)]),
     "c4": ("c4", 0.05, [(1, True)]),
+    "c4_0.1": ("c4", 0.1, [(1, True)]),      # counter-based generator from here on (synth._c4_rows)
+    "c4_0.4": ("c4", 0.4, [(1, True)]),
     "c5": ("c5", 0.3, [(1, True), (0, False)]),
 }
 
