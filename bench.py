@@ -131,12 +131,11 @@ class CompactSink:
         self.bufs, self._keep = {}, []
         for name, dt, _ in _lib.COMPACT_PARTS:
             n = need[name]
-            try:
-                import torch
-                t = torch.empty(n * np.dtype(dt).itemsize, dtype=torch.uint8, pin_memory=True)
-                self._keep.append(t)
-                self.bufs[name] = t.data_ptr()
-            except Exception:  # no pinned pool: pageable numpy (slower link rate, stated in the line)
+            try:  # page-locked memory from the library (rdf_host_alloc)
+                b = _lib.PinnedBuffer(n, dt)
+                self._keep.append(b)
+                self.bufs[name] = b.ptr
+            except _lib.RdfError:  # no pinned memory: pageable numpy (slower link rate, stated in the line)
                 self.pinned = False
                 a = np.empty(n, dt)
                 self._keep.append(a)

@@ -56,7 +56,7 @@ typedef struct rdf_ctx rdf_ctx;
 
 typedef struct {
     uint32_t min_support;
-    uint32_t reserved;
+    uint32_t n_ar_suppressed;       /* --use-ars: frequent binary conditions whose captures the rules suppress */
     uint64_t n_frequent_unary[3];   /* frequent s / p / o conditions */
     uint64_t n_binary_keys;         /* distinct candidate binary conditions counted */
     uint64_t n_frequent_binary;     /* frequent binary conditions */
@@ -151,8 +151,10 @@ rdf_status rdf_frequent_conditions(rdf_ctx* ctx, uint32_t min_support, rdf_fc_st
  * rdf_build_capture_groups: the AR-implied binary conditions then produce no captures (CreateJoinPartners.scala:
  * 99-141), and rdf_discover_cinds leaves out the CINDs the reference does not produce with the rules
  * (CreateAllCindCandidates.scala:108-115 for strategy 0; SmallToLargeTraversalStrategy.scala:80-85 and the
- * candidate generation built on it for S2L).  Single-GPU only. */
+ * candidate generation built on it for S2L). */
 rdf_status rdf_association_rules(rdf_ctx* ctx, uint64_t* n_rules);
+/* Sharded mode takes RDF_USE_ASSOCIATION_RULES in rdf_shard_begin: the rules come from the summed counts of every
+ * rank's slice (one all-reduce), are identical on every rank, and rdf_copy_association_rules returns them there. */
 /* One rule (AssociationRule, ALG/data/AssociationRule.scala:9-19; confidence is always 1): condition codes
  * s = 1, p = 2, o = 4 and term ids; support = the triple count of the binary condition. */
 typedef struct {
@@ -163,6 +165,7 @@ typedef struct {
     uint32_t support;
 } rdf_assoc_rule;
 rdf_status rdf_copy_association_rules(rdf_ctx* ctx, rdf_assoc_rule* out, uint64_t cap, uint64_t* n_copied);
+rdf_status rdf_association_rule_count(rdf_ctx* ctx, uint64_t* n);
 /* projection: any combination of 's', 'p', 'o' (--projection, default "spo"). */
 rdf_status rdf_build_capture_groups(rdf_ctx* ctx, const char* projection, rdf_group_stats* stats);
 rdf_status rdf_discover_cinds(rdf_ctx* ctx, uint32_t flags, rdf_cind_stats* stats);
@@ -206,6 +209,11 @@ rdf_status rdf_get_result_layout(rdf_ctx* ctx, rdf_result_layout* layout);
  * list_off n_lists + 1, members n_members, capture_ids and supports n_captures. */
 rdf_status rdf_copy_result_compact(rdf_ctx* ctx, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* list_refs,
                                    uint64_t* list_off, uint64_t* members, uint32_t* capture_ids, uint32_t* supports);
+
+/* Page-locked host memory (hipHostMalloc) for hand-over buffers: the copies above then run at the link rate.
+ * Returns null on failure; free with rdf_host_free. */
+void* rdf_host_alloc(uint64_t bytes);
+void rdf_host_free(void* ptr);
 
 /* One result row in the reference's Cind shape (ALG/data/Cind.scala:12-15: depCaptureType, depConditionValue1/2,
  * refCaptureType, refConditionValue1/2, support), with term ids for the condition values; value2 = UINT32_MAX

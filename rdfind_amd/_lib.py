@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "rdf_distinct_triples", "rdf_copy_triples", "rdf_parse_ntriples", "rdf_copy_terms",
     "rdf_set_dictionary_parsed", "rdf_device_bytes", "rdf_copy_cinds_decoded", "rdf_result_sizes",
     "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules", "rdf_get_result_layout",
-    "rdf_copy_result_compact",
+    "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
 )
 RDF_NT_TABS = 1
 
@@ -45,7 +45,7 @@ TIMER_NAMES = ("unary", "binary", "emit", "sort", "support", "groups", "heavymas
 
 
 class FcStats(ctypes.Structure):
-    _fields_ = [("min_support", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+    _fields_ = [("min_support", ctypes.c_uint32), ("n_ar_suppressed", ctypes.c_uint32),
                 ("n_frequent_unary", ctypes.c_uint64 * 3), ("n_binary_keys", ctypes.c_uint64),
                 ("n_frequent_binary", ctypes.c_uint64)]
 
@@ -158,6 +158,9 @@ def load():
         "rdf_last_stats": (i32, [P, ctypes.POINTER(FcStats), ctypes.POINTER(GroupStats), ctypes.POINTER(CindStats)]),
         "rdf_association_rules": (i32, [P, ctypes.POINTER(u64)]),
         "rdf_copy_association_rules": (i32, [P, P, u64, ctypes.POINTER(u64)]),
+        "rdf_association_rule_count": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_host_alloc": (P, [u64]),
+        "rdf_host_free": (None, [P]),
         "rdf_shard_begin": (i32, [P, u32, u32, u32, ctypes.c_char_p, u32]),
         "rdf_shard_step": (i32, [P, ctypes.POINTER(Exchange)]),
         "rdf_shard_export": (i32, [P, P]),
@@ -169,6 +172,23 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+class PinnedBuffer:
+    """Page-locked host memory from the library (rdf_host_alloc), as a numpy array view; freed with the object."""
+
+    def __init__(self, count: int, dtype):
+        self.lib = load()
+        self.nbytes = max(int(count), 1) * np.dtype(dtype).itemsize
+        self.ptr = self.lib.rdf_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise RdfError(f"rdf_host_alloc({self.nbytes}) failed")
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr)).view(dtype)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self.lib.rdf_host_free(self.ptr)
+            self.ptr = None
 
 
 def _struct_dict(st):
@@ -298,6 +318,10 @@ class Context:
         return self.n_rules
 
     def copy_association_rules(self) -> np.ndarray:
+        """The rules of the last rdf_association_rules (or sharded run with use_ars), RULE_DTYPE rows."""
+        n = ctypes.c_uint64()
+        self._check(self.lib.rdf_association_rule_count(self.ptr, ctypes.byref(n)), "rdf_association_rule_count")
+        self.n_rules = int(n.value)
         out = np.empty(self.n_rules, dtype=RULE_DTYPE)
         got = ctypes.c_uint64()
         self._check(self.lib.rdf_copy_association_rules(self.ptr, out.ctypes.data, len(out), ctypes.byref(got)),
@@ -344,8 +368,9 @@ class Context:
     # -- sharded mode (driven by rdfind_amd.distributed.run_sharded) ---------------------------
     def shard_begin(self, rank: int, nranks: int, min_support: int, projection="spo", clean_implied=True,
                     traversal_strategy=1, local_slice=False, use_ars=False):
+        self.n_rules = 0
         """local_slice: the resident triples are this rank's slice of the input (else every rank holds all of
-        them and the library takes its row range).  use_ars: rejected (single-GPU only)."""
+        them and the library takes its row range).  use_ars: association rules from the combined counts."""
         flags = (RDF_CLEAN_IMPLIED if clean_implied else 0) | (RDF_STRATEGY_ALL_AT_ONCE if traversal_strategy == 0 else 0)
         flags |= RDF_SHARD_LOCAL_SLICE if local_slice else 0
         flags |= RDF_USE_ASSOCIATION_RULES if use_ars else 0

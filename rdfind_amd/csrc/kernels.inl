@@ -1191,11 +1191,11 @@ __device__ inline void multi_search(const u32* const (&a)[K], const u64 (&n)[K],
 // dependents per wave.  Each lane walks its dependent's groups and binary-searches its candidate in every
 // light one (the same test as k_light's few-groups path, without a mostly idle wave per dependent).
 __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                           const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep, u64 WP,
-                                           const u64* __restrict__ choff, u64* slots, u32* counts) {
+                                           const u64* __restrict__ pkoff, const u32* __restrict__ pk_dep, u64 q0, u64 WP,
+                                           const u64* __restrict__ choff, u64 ob, u64* slots, u32* counts) {
     const u64 g = (u64)vblk * RDF_BLOCK + threadIdx.x;
-    const u64 q = g >> 3;
-    if (q >= WP) return;  // whole octets only, so the octet ballots below see complete octets
+    if ((g >> 3) >= WP) return;  // whole octets only, so the octet ballots below see complete octets
+    const u64 q = q0 + (g >> 3);  // packed octets [q0, q0 + WP); output octets relative to ob (paged runs)
     const u32 d = pk_dep[q];
     const u64 k = q - pkoff[d];
     const u32 piv = pivot[d];
@@ -1233,16 +1233,17 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     const u64 alive = __ballot(ok);
     const int lane = lane_id(), o = lane >> 3, jj = lane & 7;
     const u32 om = (u32)(alive >> (o * 8)) & 0xffu;
-    const u64 oct = choff[d] + k;
+    const u64 oct = choff[d] + k - ob;
     if (jj == 0) counts[oct] = (u32)__popc(om);
     if (ok) slots[oct * 8 + __popc(om & ((1u << jj) - 1u))] = ((u64)d << 32) | cand;
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                             const u64* __restrict__ pkoff,
-                                                            const u32* __restrict__ pk_dep, u64 WP,
-                                                            const u64* __restrict__ choff, u64* slots, u32* counts) {
+                                                            const u32* __restrict__ pk_dep, u64 q0, u64 WP,
+                                                            const u64* __restrict__ choff, u64 ob, u64* slots,
+                                                            u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_light_packed_body(vb, v, pivot, pkoff, pk_dep, WP, choff, slots, counts);
+        k_light_packed_body(vb, v, pivot, pkoff, pk_dep, q0, WP, choff, ob, slots, counts);
     }
 }
 
@@ -1296,12 +1297,14 @@ __device__ inline void light_batch(const u32* gm, u64 gsz, const u32* drow, u32 
 template <bool STAGE>
 __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
-                                    const u64* __restrict__ choff, u64 W, u64* dead, u64* slots, u32* counts) {
+                                    const u64* __restrict__ choff, u64 w0, u64 W, u64 ob, u64* dead, u64* slots,
+                                    u32* counts) {
     // a staged group, or (STAGE) the lanes' small-group rows.  The larger buffer is only allocated by the variant
     // that uses it: on c3 (large light groups) 31.7 KB per block cost 30 % of the kernel even with the path unused
     __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][STAGE ? LIGHT_BUF : LIGHT_LDS];
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
+    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wl >= W) return;
+    const u64 w = w0 + wl;  // work items [w0, w0 + W); octets relative to ob (paged runs)
     const int lane = lane_id();
     const u32 d = item_dep[w];
     const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
@@ -1355,7 +1358,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         for (int it = 0; it < LIGHT_IT; ++it) {
             if (s0 + (u64)it * RDF_WAVE >= e) break;
             // a multi-segment item drops the candidates other segments have already killed
-            if (nseg > 1 && (it || s0 != b)) alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (nseg > 1 && (it || s0 != b)) alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8 - ob], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (!alive) break;
             const u32 g = gg[it];
             const u64 lm = __ballot(g != NONE32);  // light groups of this window
@@ -1448,8 +1451,8 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         for (int k = 0; k < 16; ++k) r[k] = rec[k];
     }
 #endif
-    const u64 oct0 = choff[d] + chunk * 8;  // first octet slot of this chunk
-    const u64 noct = choff[d + 1] - oct0;
+    const u64 oct0 = choff[d] + chunk * 8 - ob;  // first octet slot of this chunk
+    const u64 noct = choff[d + 1] - ob - oct0;
     const u32 nvalid = noct < 8 ? (u32)noct : 8u;
     if (nseg == 1) {
         slot_emit(oct0, nvalid, d, cand, alive, slots, counts);
@@ -1468,10 +1471,10 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
 template <bool STAGE>
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_ATTR void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                      const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
-                                                     const u64* __restrict__ choff, u64 W, u64* dead, u64* slots,
-                                                     u32* counts) {
+                                                     const u64* __restrict__ choff, u64 w0, u64 W, u64 ob, u64* dead,
+                                                     u64* slots, u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_light_body<STAGE>(vb, v, pivot, itemoff, item_dep, choff, W, dead, slots, counts);
+        k_light_body<STAGE>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
     }
 }
 
@@ -1479,26 +1482,27 @@ __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_ATTR void k_light(u64 nvblk, C
 // chunks verified by several segments: survivors = candidates minus the union of the segments' kills
 // (launched after k_light; the kernel boundary orders the kills before these reads)
 __device__ inline void k_light_mseg_emit_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                              const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep, u64 WM,
-                                              const u64* __restrict__ choff, const u64* __restrict__ dead, u64* slots,
-                                              u32* counts) {
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= WM) return;
+                                              const u64* __restrict__ mchoff, const u32* __restrict__ mch_dep, u64 m0,
+                                              u64 WM, const u64* __restrict__ choff, u64 ob, const u64* __restrict__ dead,
+                                              u64* slots, u32* counts) {
+    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wl >= WM) return;
+    const u64 w = m0 + wl;
     const u32 d = mch_dep[w];
     const u64 chunk = w - mchoff[d];
     const u32 cand = chunk_candidate(v, d, v.info[d], pivot[d], chunk);
     const u64 alive0 = __ballot(cand != NONE32);
-    const u64 oct0 = choff[d] + chunk * 8;
-    const u64 noct = choff[d + 1] - oct0;
+    const u64 oct0 = choff[d] + chunk * 8 - ob;
+    const u64 noct = choff[d + 1] - ob - oct0;
     slot_emit(oct0, noct < 8 ? (u32)noct : 8u, d, cand, alive0 & ~dead[oct0], slots, counts);
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                                const u64* __restrict__ mchoff,
-                                                               const u32* __restrict__ mch_dep, u64 WM,
-                                                               const u64* __restrict__ choff,
+                                                               const u32* __restrict__ mch_dep, u64 m0, u64 WM,
+                                                               const u64* __restrict__ choff, u64 ob,
                                                                const u64* __restrict__ dead, u64* slots, u32* counts) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_light_mseg_emit_body(vb, v, pivot, mchoff, mch_dep, WM, choff, dead, slots, counts);
+        k_light_mseg_emit_body(vb, v, pivot, mchoff, mch_dep, m0, WM, choff, ob, dead, slots, counts);
     }
 }
 
@@ -2224,11 +2228,14 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
                 lc = (u32)sz;
                 le = (u32)(v.doff[d + 1] - v.doff[d]);
             }
-            nchunk_heavy[d] = (heavy_only && d >= v.Cu && holder) ? nch : 0;
+            // unary heavy-only dependents are emitted per bitmask class, except with --use-ars (a class list is not
+            // per dependent): then they take the heavy path like the binary ones
+            const bool heavy_path = d >= v.Cu || v.ar;
+            nchunk_heavy[d] = (heavy_only && heavy_path && holder) ? nch : 0;
             nrl[d] = (u32)(gl >> 40);
             if (heavy_only) {
                 info[d].meta |= META_HEAVY_ONLY;
-                if (d >= v.Cu && holder) hc = (u32)sz;
+                if (heavy_path && holder) hc = (u32)sz;
             }
         }
         acc[0] += hc;

@@ -53,7 +53,7 @@ struct rdf_ctx {
     // --use-ars (rdf_association_rules): rules (5 u32 each), per-condition counts, unary dependent -> implied ref
     bool ar_on = false;
     u64 n_rules = 0;
-    DevBuf ar_ucnt, ar_bcnt, ar_bits, ar_rules, arref;
+    DevBuf arcnt, ar_bits, ar_rules, arref;  // arcnt: triple counts of the frequent unary | binary conditions
 
     // capture groups
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
@@ -278,7 +278,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->ar_ucnt, &c->ar_bcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
+            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
             &c->ukeys_tmp};
 }
 
@@ -911,31 +911,36 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
 // Association rules (--use-ars, FrequentConditionPlanner.findAssociationRules, ALG/plan/FrequentConditionPlanner.scala:
 // 129-193): triple counts of the frequent conditions (k_ar_count), rule bits per frequent binary key, the rules, and
 // the frequent binary keys without the AR-implied ones (CreateJoinPartners.scala:99-141 never emits those captures).
-rdf_status rdf_association_rules(rdf_ctx* c, uint64_t* n_rules) {
-    if (!c) return RDF_ERR_ARG;
-    if (c->stage != 2) return fail(c, RDF_ERR_STATE, "rdf_association_rules follows rdf_frequent_conditions");
-    if (c->ar_on) return fail(c, RDF_ERR_STATE, "association rules already applied to these frequent conditions");
-    HIP_TRY(c, hipSetDevice(c->device));
+// ar_counts: the counts of these triples into arcnt = [unary (U) | binary (B)] (sharded input: the slice's partial
+// counts, summed over the ranks before ar_apply).
+static rdf_status ar_counts(rdf_ctx* c, const u32* s, const u32* p, const u32* o, u64 n) {
     hipStream_t st = c->stream;
     const u32 V = c->V ? c->V : 1;
     const u64 B = c->B, U = c->U;
-    ENSURE(c, ar_ucnt, std::max<u64>(U, 1) * 4);
-    ENSURE(c, ar_bcnt, std::max<u64>(B, 1) * 4);
+    ENSURE(c, arcnt, (U + B + 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->arcnt.p, 0, (U + B + 1) * 4, st));
+    if (n && B)
+        hipLaunchKernelGGL(k_ar_count, dim3(grid_for(n, RDF_BLOCK * 4, kGrid)), dim3(RDF_BLOCK), 0, st, s, p, o, n, V,
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, c->arcnt.as<u32>(),
+                           c->arcnt.as<u32>() + U);
+    return RDF_OK;
+}
+
+// the rules from the (global) counts in arcnt; the frequent binary keys become the kept ones
+static rdf_status ar_apply(rdf_ctx* c) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 B = c->B, U = c->U;
+    const u32* ucnt = c->arcnt.as<u32>();
+    const u32* bcnt = c->arcnt.as<u32>() + U;
     ENSURE(c, ar_bits, std::max<u64>(B, 1) * 4);
     ENSURE(c, flags, (B + 1) * 4);
     ENSURE(c, fpos, (B + 1) * 4);
     ENSURE(c, pos, (B + 1) * 4);
     ENSURE(c, bkeys_tmp, std::max<u64>(B, 1) * 8);
-    HIP_TRY(c, hipMemsetAsync(c->ar_ucnt.p, 0, std::max<u64>(U, 1) * 4, st));
-    HIP_TRY(c, hipMemsetAsync(c->ar_bcnt.p, 0, std::max<u64>(B, 1) * 4, st));
-    if (c->n && B)
-        hipLaunchKernelGGL(k_ar_count, dim3(grid_for(c->n, RDF_BLOCK * 4, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o,
-                           c->n, V, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1,
-                           c->ar_ucnt.as<u32>(), c->ar_bcnt.as<u32>());
     if (B)
         hipLaunchKernelGGL(k_ar_flags, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, V,
-                           c->frank.as<u32>(), c->ar_ucnt.as<u32>(), c->ar_bcnt.as<u32>(), c->ar_bits.as<u32>(),
-                           c->flags.as<u32>(), (u32*)c->pos.p);
+                           c->frank.as<u32>(), ucnt, bcnt, c->ar_bits.as<u32>(), c->flags.as<u32>(), (u32*)c->pos.p);
     // rule slots (flags) and kept keys (pos) -> exclusive offsets fpos / pos (in place)
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), B, c->fpos.as<u32>() + B, st));
     HIP_TRY(c, exclusive_scan_u32(c->ws, (u32*)c->pos.p, (u32*)c->pos.p, B, (u32*)c->pos.p + B, st));
@@ -945,14 +950,34 @@ rdf_status rdf_association_rules(rdf_ctx* c, uint64_t* n_rules) {
     ENSURE(c, ar_rules, std::max<u64>(NR, 1) * 5 * 4);
     if (B)
         hipLaunchKernelGGL(k_ar_emit, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B,
-                           c->ar_bits.as<u32>(), c->ar_bcnt.as<u32>(), c->fpos.as<u32>(), (const u32*)c->pos.p,
-                           c->ar_rules.as<u32>(), c->bkeys_tmp.as<u64>());
+                           c->ar_bits.as<u32>(), bcnt, c->fpos.as<u32>(), (const u32*)c->pos.p, c->ar_rules.as<u32>(),
+                           c->bkeys_tmp.as<u64>());
     std::swap(c->bkeys, c->bkeys_tmp);
     TRY(fc_binary_index(c, Bk));  // already sorted: the radix passes keep the order
     HIP_TRY(c, hipStreamSynchronize(st));
     c->n_rules = NR;
     c->ar_on = true;
-    if (n_rules) *n_rules = NR;
+    // n_frequent_binary stays the frequent-condition count of the reference's planner; the keys whose captures the
+    // rules suppress are counted apart
+    c->fstats.n_ar_suppressed = (u32)(B - Bk);
+    return RDF_OK;
+}
+
+rdf_status rdf_association_rules(rdf_ctx* c, uint64_t* n_rules) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage != 2) return fail(c, RDF_ERR_STATE, "rdf_association_rules follows rdf_frequent_conditions");
+    if (c->ar_on) return fail(c, RDF_ERR_STATE, "association rules already applied to these frequent conditions");
+    HIP_TRY(c, hipSetDevice(c->device));
+    TRY(ar_counts(c, c->s, c->p, c->o, c->n));
+    TRY(ar_apply(c));
+    if (n_rules) *n_rules = c->n_rules;
+    return RDF_OK;
+}
+
+rdf_status rdf_association_rule_count(rdf_ctx* c, uint64_t* n) {
+    if (!c || !n) return RDF_ERR_ARG;
+    if (!c->ar_on) return fail(c, RDF_ERR_STATE, "rdf_association_rules must be called first");
+    *n = c->n_rules;
     return RDF_OK;
 }
 
@@ -1304,7 +1329,7 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.mode = (flags & RDF_CLEAN_IMPLIED) ? RULES_CLEAN : (v.literal ? RULES_NONE : RULES_S2L_RAW);
     v.vcoff = nullptr;
     v.vpairs = nullptr;
-    v.ar = c->ar_on && c->nranks == 1 ? (v.literal ? AR_S0 : AR_S2L) : AR_NONE;
+    v.ar = c->ar_on ? (v.literal ? AR_S0 : AR_S2L) : AR_NONE;
     v.arref = c->arref.as<u32>();
     v.sig = c->sig_on ? c->lsig.as<u64>() : nullptr;
     v.ginfo = c->ginfo.as<u32>();
@@ -1462,26 +1487,13 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     return RDF_OK;
 }
 
-// light dependents -> explicit raw (dep << 32 | ref) pairs in epairs, in (dep, ref) order; *E = count.
-// Output slots are octets (8 pivot candidates each): WL of them; WI k_light work items, WP packed octets.
-static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP, u64* E, const u32* pivot) {
+// owner tables of the light work (all dependents): item_dep over the k_light items, pk_dep over the packed octets,
+// the multi-segment chunks (mchoff, mch_dep); *WM = their number
+static rdf_status d_light_owners(rdf_ctx* c, u64 WI, u64 WP, u64* WM) {
     hipStream_t st = c->stream;
-    const u64 nslot = std::max<u64>(WL, 1);
-    ENSURE(c, epairs_tmp, nslot * 8 * 8);
-    ENSURE(c, dead, nslot * 8);  // kill masks of multi-segment chunks, keyed by the chunk's first octet
-    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, nslot * 8, st));
-    ENSURE(c, lslot, nslot * 4);
-    HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, nslot * 4, st));
     ENSURE(c, item_dep, std::max<u64>(WI, 1) * 4);
     ENSURE(c, pk_dep, std::max<u64>(WP, 1) * 4);
-#ifdef RDF_LIGHT_STATS
-    u32* lrec = nullptr;
-    if (WI && getenv("RDFIND_LIGHT_DUMP")) {
-        HIP_TRY(c, hipMalloc(&lrec, WI * 64));
-        HIP_TRY(c, hipMemset(lrec, 0, WI * 64));
-        HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_item_rec), &lrec, sizeof(lrec)));
-    }
-#endif
+    *WM = 0;
     tbegin(c, RDF_T_LIGHT);
     if (WI)
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->itoffl.as<u64>(),
@@ -1489,51 +1501,91 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     if (WP)
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->pkoff.as<u64>(),
                            c->C, c->pk_dep.as<u32>());
-    CindView vp = v;
-    if (!c->sig_packed) vp.sig = nullptr;
-    if (!c->piv2_packed) vp.piv2 = nullptr;
-    if (WP)
-        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
-                           pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), WP, c->choffl.as<u64>(),
-                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
-    if (WI) {
-        auto kl = c->light_stage ? k_light<true> : k_light<false>;
-        hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
-                           0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(), WI,
-                           c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
-    }
     // chunks of dependents whose groups span several segments: emitted once all their segments are done
-    u64 WM = 0;
     if (WI) {
         ENSURE(c, nmch, std::max<u64>(c->C, 1) * 4);
         ENSURE(c, mchoff, (c->C + 1ull) * 8);
         hipLaunchKernelGGL(k_mseg_chunks, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(),
                            c->nitl.as<u32>(), c->C, c->nmch.as<u32>());
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nmch.as<u32>(), c->mchoff.as<u64>(), c->C, c->mchoff.as<u64>() + c->C, st));
-        TRY(read_u64(c, c->mchoff.as<u64>() + c->C, &WM));
+        TRY(read_u64(c, c->mchoff.as<u64>() + c->C, WM));
     }
-    if (WM) {
-        ENSURE(c, mch_dep, WM * 4);
+    if (*WM) {
+        ENSURE(c, mch_dep, *WM * 4);
         hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->mchoff.as<u64>(),
                            c->C, c->mch_dep.as<u32>());
-        hipLaunchKernelGGL(k_light_mseg_emit, dim3(vgrid(wave_blocks(WM))),
-                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, pivot, c->mchoff.as<u64>(), c->mch_dep.as<u32>(), WM,
-                           c->choffl.as<u64>(), c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     }
+    tend(c, RDF_T_LIGHT);
+    return RDF_OK;
+}
+
+// Work of the light dependents [d0, d1): k_light items [i0, i1), packed octets [q0, q1), multi-segment chunks [m0, m1)
+// and output octets [o0, o1) (the scans itoffl, pkoff, mchoff, choffl at d0 and d1).
+struct LightRange {
+    u64 i0, i1, q0, q1, m0, m1, o0, o1;
+};
+
+static rdf_status light_range(rdf_ctx* c, u32 d0, u32 d1, bool mseg, LightRange* r) {
+    u64 v[8];
+    const u64* mo = mseg ? c->mchoff.as<u64>() : c->itoffl.as<u64>();  // no multi-segment items: any zero-width pair
+    TRY(read_multi(c, {{c->itoffl.as<u64>() + d0, 8}, {c->itoffl.as<u64>() + d1, 8}, {c->pkoff.as<u64>() + d0, 8},
+                       {c->pkoff.as<u64>() + d1, 8}, {mo + d0, 8}, {mo + d1, 8}, {c->choffl.as<u64>() + d0, 8},
+                       {c->choffl.as<u64>() + d1, 8}}, v));
+    *r = {v[0], v[1], v[2], v[3], mseg ? v[4] : 0, mseg ? v[5] : 0, v[6], v[7]};
+    return RDF_OK;
+}
+
+// light dependents of range r -> explicit raw (dep << 32 | ref) pairs at epairs + ebase, in (dep, ref) order;
+// *E = their count.  Output slots are octets (8 pivot candidates each), relative to r.o0.
+static rdf_status d_light_run(rdf_ctx* c, const CindView& v, const u32* pivot, const LightRange& r, u64 ebase, u64* E) {
+    hipStream_t st = c->stream;
+    const u64 WL = r.o1 - r.o0, WI = r.i1 - r.i0, WP = r.q1 - r.q0, WM = r.m1 - r.m0, ob = r.o0;
+    const u64 nslot = std::max<u64>(WL, 1);
+    ENSURE(c, epairs_tmp, nslot * 8 * 8);
+    ENSURE(c, dead, nslot * 8);  // kill masks of multi-segment chunks, keyed by the chunk's first octet
+    HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, nslot * 8, st));
+    ENSURE(c, lslot, nslot * 4);
+    HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, nslot * 4, st));
+#ifdef RDF_LIGHT_STATS
+    u32* lrec = nullptr;
+    if (WI && getenv("RDFIND_LIGHT_DUMP")) {
+        HIP_TRY(c, hipMalloc(&lrec, r.i1 * 64));
+        HIP_TRY(c, hipMemset(lrec, 0, r.i1 * 64));
+        HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_item_rec), &lrec, sizeof(lrec)));
+    }
+#endif
+    tbegin(c, RDF_T_LIGHT);
+    CindView vp = v;
+    if (!c->sig_packed) vp.sig = nullptr;
+    if (!c->piv2_packed) vp.piv2 = nullptr;
+    if (WP)
+        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
+                           pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,
+                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+    if (WI) {
+        auto kl = c->light_stage ? k_light<true> : k_light<false>;
+        hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
+                           0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
+                           r.i0, WI, ob, c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+    }
+    if (WM)
+        hipLaunchKernelGGL(k_light_mseg_emit, dim3(vgrid(wave_blocks(WM))),
+                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, pivot, c->mchoff.as<u64>(), c->mch_dep.as<u32>(), r.m0,
+                           WM, c->choffl.as<u64>(), ob, c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
     ENSURE(c, pos, (WL + 1) * 8);
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
     TRY(read_u64(c, c->pos.as<u64>() + WL, E));
-    ENSURE(c, epairs, std::max<u64>(*E, 1) * 8);
+    HIP_TRY(c, c->epairs.grow_keep((size_t)std::max<u64>(ebase + *E, 1) * 8, st));
     if (WL)
         hipLaunchKernelGGL(k_slot_compact, dim3(vgrid(thread_blocks(WL * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WL * 8),
-                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>());
+                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>() + ebase);
     tend(c, RDF_T_LIGHT);
 #ifdef RDF_LIGHT_STATS
     if (lrec) {  // per-item records -> $RDFIND_LIGHT_DUMP (raw u32 x 16 per item)
-        std::vector<u32> h(WI * 16);
-        HIP_TRY(c, hipMemcpy(h.data(), lrec, WI * 64, hipMemcpyDeviceToHost));
+        std::vector<u32> h(r.i1 * 16);
+        HIP_TRY(c, hipMemcpy(h.data(), lrec, r.i1 * 64, hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("RDFIND_LIGHT_DUMP"), "wb")) {
-            fwrite(h.data(), 64, WI, f);
+            fwrite(h.data(), 64, r.i1, f);
             fclose(f);
         }
         u32* z = nullptr;
@@ -1544,6 +1596,14 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
             (unsigned long long)WP, (unsigned long long)*E);
 #endif
     return RDF_OK;
+}
+
+// every light dependent at once: explicit raw pairs in epairs[0, *E) (WI k_light items, WL octets, WP packed octets)
+static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP, u64* E, const u32* pivot) {
+    u64 WM = 0;
+    TRY(d_light_owners(c, WI, WP, &WM));
+    const LightRange r = {0, WI, 0, WP, 0, WM, 0, WL};
+    return d_light_run(c, v, pivot, r, 0, E);
 }
 
 // sort the explicit pairs (epairs[0, E)) and index them: v.eoff / v.ebin / v.epairs
@@ -2026,17 +2086,9 @@ static rdf_status sh_phase12(rdf_ctx* c, rdf_exchange* req) {
     return x_request(c, req, RDF_X_ALLGATHERV_U64, c->bkeys.p, B, 13);
 }
 
-// every rank's frequent keys -> sorted binary ids; the local triples -> the ranks owning their join values
-static rdf_status sh_phase13(rdf_ctx* c, rdf_exchange* req) {
+// the local triples -> the ranks owning their join values (all-to-all, then phase 14)
+static rdf_status sh_route_triples(rdf_ctx* c, rdf_exchange* req) {
     hipStream_t st = c->stream;
-    const u64 B = c->x_recv_count;
-    tbegin(c, RDF_T_BINARY);
-    ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
-    if (B) HIP_TRY(c, hipMemcpyAsync(c->bkeys.p, c->xrecv.p, B * 8, hipMemcpyDeviceToDevice, st));
-    TRY(fc_binary_index(c, B));
-    tend(c, RDF_T_BINARY);
-    TRY(fc_end(c));
-    fc_stats(c, c->sh_nfreq, c->sh_nkeys, B);  // n_binary_keys: the distinct keys owned by this rank
     const u32 *s, *p, *o;
     u64 n;
     sh_slice(c, &s, &p, &o, &n);
@@ -2058,6 +2110,35 @@ static rdf_status sh_phase13(rdf_ctx* c, rdf_exchange* req) {
     TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->xsend.p, 2 * copies, 14));
     for (u32 r = 0; r < R; ++r) req->send_counts[r] = 2ull * (h[(u64)(r + 1) * G] - h[(u64)r * G]);
     return RDF_OK;
+}
+
+// every rank's frequent keys -> sorted binary ids; then (--use-ars) the slice's triple counts of the frequent
+// conditions -> all-reduce (phase 17), or the triples -> their join owners
+static rdf_status sh_phase13(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 B = c->x_recv_count;
+    tbegin(c, RDF_T_BINARY);
+    ENSURE(c, bkeys, std::max<u64>(B, 1) * 8);
+    if (B) HIP_TRY(c, hipMemcpyAsync(c->bkeys.p, c->xrecv.p, B * 8, hipMemcpyDeviceToDevice, st));
+    TRY(fc_binary_index(c, B));
+    tend(c, RDF_T_BINARY);
+    TRY(fc_end(c));
+    fc_stats(c, c->sh_nfreq, c->sh_nkeys, B);  // n_binary_keys: the distinct keys owned by this rank
+    if (!(c->sh_flags & RDF_USE_ASSOCIATION_RULES)) return sh_route_triples(c, req);
+    const u32 *s, *p, *o;
+    u64 n;
+    sh_slice(c, &s, &p, &o, &n);
+    TRY(ar_counts(c, s, p, o, n));  // FrequentConditionPlanner.findAssociationRules on the combined counts
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return x_request(c, req, RDF_X_ALLREDUCE_SUM_U32, c->arcnt.p, (u64)c->U + c->B, 17);
+}
+
+// --use-ars: the summed counts -> the rules (identical on every rank) and the kept binary keys; then the triples
+static rdf_status sh_phase17(rdf_ctx* c, rdf_exchange* req) {
+    const u64 m = (u64)c->U + c->B;
+    if (m) HIP_TRY(c, hipMemcpyAsync(c->arcnt.p, c->xrecv.p, m * 4, hipMemcpyDeviceToDevice, c->stream));
+    TRY(ar_apply(c));
+    return sh_route_triples(c, req);
 }
 
 // received triples (every triple with a join value owned here) -> join partners of this rank's shard, sort,
@@ -2094,6 +2175,7 @@ static rdf_status sh_phase14(rdf_ctx* c, rdf_exchange* req) {
 static rdf_status sh_phase1(rdf_ctx* c, rdf_exchange* req) {
     HIP_TRY(c, hipMemcpyAsync(c->support.p, c->xrecv.p, c->ncap * 4, hipMemcpyDeviceToDevice, c->stream));
     TRY(g_compact_groups(c));
+    if (c->ar_on) TRY(g_ar_refs(c));
     TRY(g_size_hist(c, c->h_hist_local));
     ENSURE(c, xsend, 256 * 8);
     std::vector<u64> w(256);
@@ -2394,7 +2476,7 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     tbegin(c, RDF_T_CLASS);
     u64 nmem_all = 0, tcapc = 0;
     u32 ncls = 0;
-    TRY(d_class_table(c, v, c->Cu, &nmem_all, &ncls, &tcapc));
+    TRY(d_class_table(c, v, v.ar ? 0u : c->Cu, &nmem_all, &ncls, &tcapc));  // --use-ars: per-dependent heavy path
     c->sh_tcapc = tcapc;
     c->n_classes = ncls;
     ENSURE(c, smask, std::max<u64>(ncls, 1) * 8);
@@ -2511,7 +2593,7 @@ static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
 // phase that follows a collective
 static bool sh_phase_valid(int ph, bool pending) {
     if (ph >= 1 && ph <= 8) return true;
-    if (ph >= 11 && ph <= 16) return true;
+    if (ph >= 11 && ph <= 17) return true;
     return !pending && ph == 10;
 }
 
@@ -2520,8 +2602,6 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     if (!c) return RDF_ERR_ARG;
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
-    if (flags & RDF_USE_ASSOCIATION_RULES)
-        return fail(c, RDF_ERR_ARG, "association rules are not supported in sharded mode (use rdf_run on one GPU)");
     c->hclassed = false;
     int proj = 0;
     TRY(parse_projection(c, projection, &proj));
@@ -2550,6 +2630,7 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
         case 5: r = sh_phase5(c, req); break;
         case 15: r = sh_phase15(c, req); break;
         case 16: r = sh_phase16(c, req); break;
+        case 17: r = sh_phase17(c, req); break;
         case 6: r = sh_phase6(c, req); break;
         case 7: r = sh_phase7(c, req); break;
         case 8: r = sh_phase8(c, req); break;
@@ -2609,6 +2690,15 @@ static rdf_status materialize(rdf_ctx* c) {
     c->out_ptr = c->out.as<u32>();
     c->class_pending = false;
     return RDF_OK;
+}
+
+// page-locked host memory for the result hand-over (the copies then run at the link rate)
+void* rdf_host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+void rdf_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 rdf_status rdf_get_result_layout(rdf_ctx* c, rdf_result_layout* L) {

@@ -3,9 +3,13 @@
 Each rank holds a slice of the triples (or all of them, and the library takes its row range).  The collectives
 the library requests one at a time (``rdf_shard_step``):
 
-  a. all-reduce(sum)  dense unary condition counts of the slices (FrequentConditionPlanner.scala:293-309)
+  a. all-to-all       unary (key, count) partials of the slices to the key's owner rank, which sums them
+                      (FrequentConditionPlanner.scala:293-309)
+  a'. all-gather      the frequent unary keys of every owner (sorted afterwards: global ranks)
   b. all-to-all       binary (key, count) partials to the key's owner rank, which sums them (:381-393)
   c. all-gather       the frequent binary keys of every owner (sorted afterwards: deterministic ids)
+  (c'. all-reduce     --use-ars only: the slices' triple counts of the frequent conditions, for the rules,
+                      FrequentConditionPlanner.scala:129-193)
   d. all-to-all       every triple to the ranks owning its join values (RDFind.scala:339-345 groupBy(joinValue)),
                       so rank r builds the capture groups of its join-value hash shard
   1. all-reduce(sum)  capture supports (distinct join values per capture)
@@ -22,7 +26,8 @@ the library requests one at a time (``rdf_shard_step``):
                       dep reported it.  Together this is the reference's combiner-side intersection
                       (AllAtOnceTraversalStrategy.scala:62-65) and the shuffle to the IntersectCindCandidates
                       reducer, with candidate generation done once per dependent instead of once per rank.
-  8. all-gather       the final explicit CIND pairs (the minimality rules R1-R4 probe other dependents)
+  8. all-gather       the final explicit CIND pairs of the unary dependents (R1 / R4 probe the components of
+                      binary dependents, which are unary); binary dependents' pairs stay with their owner
   9. all-gather       filtered ref lists of the bitmask classes pivoted on each rank
 
 Each rank then emits the CINDs of its own dependents; the union over ranks is the single-GPU result.
@@ -123,11 +128,12 @@ def run_protocol(machine, group=None, device=None):
 
 
 def run_sharded(ctx, min_support: int, projection="spo", clean_implied=True, traversal_strategy=1, group=None,
-                device=None, local_slice=False):
+                device=None, local_slice=False, use_ars=False):
     """Sharded CIND discovery on this rank's context; returns (group_stats, cind_stats) of this rank.
-    local_slice: the context's resident triples are this rank's slice of the input."""
+    local_slice: the context's resident triples are this rank's slice of the input.  use_ars: association rules from
+    the combined counts (one more all-reduce), applied as on one GPU."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy, local_slice)
+    ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy, local_slice, use_ars)
     run_protocol(ctx, group, device)
     return ctx.last_stats()

@@ -97,6 +97,12 @@ class RDFind:
     def log(self, msg):
         print(msg, file=sys.stderr)
 
+    def _term_lookup(self, ctx, dic):
+        """term id -> string: the host dictionary, or the device parser's (fetched once)."""
+        if dic is None:
+            dic = ntriples.HeapDictionary(*ctx.parsed_terms())
+        return dic.term
+
     def write_rules(self, spec, lines):
         path = _output_path(spec)
         self.log(f"Outputting assocation rules to {os.path.abspath(path)}.")
@@ -110,8 +116,6 @@ class RDFind:
             return self.launch_ranks(a.dop)
         self.rank, self.world = int(os.environ.get("RANK", "0")), world
         if world > 1:
-            if a.use_ars:
-                raise NotImplementedError("--use-ars with -dop > 1: association rules run on one GPU only")
             if a.find_only_fcs or a.do_only_join:
                 raise NotImplementedError("--find-only-fcs / --do-only-join with -dop > 1")
             import torch
@@ -152,8 +156,17 @@ class RDFind:
                     self.log(f"{n_distinct} distinct triples of {n_in}.")
             if world > 1:  # -dop: every rank parsed the same bytes (same ids) and takes its share of the work
                 from . import distributed
+                if a.ar_output:  # the rules come from the combined counts; identical on every rank, rank 0 writes
+                    distributed.run_sharded(ctx, a.support, a.projection, a.clean_implied, a.traversal_strategy,
+                                            use_ars=True)
+                    if self.rank == 0:
+                        self.write_rules(a.ar_output, format_rules(ctx.copy_association_rules(),
+                                                                   self._term_lookup(ctx, dic)))
+                    if a.use_ars:  # the run above is the result
+                        gs, cs = ctx.groups, ctx.cinds
+                        return self.write_output(ctx, dic, {"fc": ctx.fc, "groups": gs, "cinds": cs}, t1, out)
                 gs, cs = distributed.run_sharded(ctx, a.support, a.projection, a.clean_implied,
-                                                 a.traversal_strategy)
+                                                 a.traversal_strategy, use_ars=a.use_ars)
                 fc = ctx.fc
                 return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
             fc = ctx.frequent_conditions(a.support)

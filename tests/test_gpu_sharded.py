@@ -34,16 +34,22 @@ def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo"):
     out = []
     try:
         ctx = _lib.Context(0)
-        for s, p, o, nv, ms, strategy, clean in cases:
+        for case in cases:
+            s, p, o, nv, ms, strategy, clean = case[:7]
+            use_ars = len(case) > 7 and case[7]
             if local_slice:  # this rank holds only its slice (interleaved rows: slices need not be contiguous)
                 ctx.set_triples(s[rank::world], p[rank::world], o[rank::world], nv)
             else:
                 ctx.set_triples(s, p, o, nv)
-            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy, local_slice=local_slice)
+            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy, local_slice=local_slice, use_ars=use_ars)
             n = ctx.cind_count()
             rows = ctx.copy_cinds() if n <= 2_000_000 else None
-            out.append({"n": n, "checksum": ctx.checksum(), "rows": rows, "heavy": gs["n_heavy_groups"],
-                        "class_members": cs["n_class_members"]})
+            item = {"n": n, "checksum": ctx.checksum(), "rows": rows, "heavy": gs["n_heavy_groups"],
+                    "class_members": cs["n_class_members"]}
+            if use_ars:
+                item["rules"] = sorted(map(tuple, ctx.copy_association_rules().tolist()))
+                item["decoded"] = _lib.decoded_to_set(ctx.decoded_cinds())
+            out.append(item)
         ctx.close()
         q.put((rank, out))
     except Exception as e:  # report instead of hanging the parent
@@ -195,3 +201,57 @@ def test_program_dop2_reproduces_golden(tmp_path, name, mode, flags):
     assert r.returncode == 0, r.stderr[-3000:]
     assert sorted(out.read_text().splitlines()) == expected
     assert not list(tmp_path.glob("cinds.txt.part*"))
+
+
+@pytest.mark.parametrize("local_slice", [False, True])
+def test_sharded_association_rules_match_oracle(local_slice):
+    """--use-ars in sharded mode: the rules come from the slices' summed counts (one more all-reduce), are identical
+    on every rank and equal the oracle's; the union of the ranks' CINDs equals the oracle's result with the rules,
+    in all four modes (2 ranks, gloo; heavy-group columns lowered so the heavy paths carry the rules too)."""
+    import random
+
+    from oracle import rdfind_oracle as R
+    from tests.test_gpu_ars import CODE, MODES, _random_case, expected
+
+    rng = random.Random(77)
+    cases, exp = [], []
+    for i in range(32):
+        arr, nv, ms = _random_case(rng, nmax=300)
+        strategy, clean = MODES[i % 4]
+        tr = [tuple(x) for x in arr.tolist()]
+        uf = R.frequent_unary_conditions(tr, ms)
+        rules = sorted((CODE[ta], CODE[tc], va, vc, n)
+                       for ta, tc, va, vc, n in R.association_rules(uf, R.frequent_binary_conditions(tr, uf, ms)))
+        cases.append((arr[:, 0], arr[:, 1], arr[:, 2], nv, ms, strategy, clean, True))
+        exp.append((rules, expected(tr, ms, strategy, clean)))
+    res = _run_sharded(2, cases, local_slice)
+    n_rules = 0
+    for k, (rules, cinds) in enumerate(exp):
+        assert res[0][k]["rules"] == res[1][k]["rules"] == rules, k
+        assert res[0][k]["decoded"] | res[1][k]["decoded"] == cinds, k
+        assert not (res[0][k]["decoded"] & res[1][k]["decoded"]), k
+        n_rules += len(rules)
+    assert n_rules > 20
+
+
+def test_program_dop2_association_rules(tmp_path):
+    """-dop 2 --use-ars --ar-output through the driver equals the single-GPU driver: the same rules file and the
+    same CIND lines."""
+    import subprocess
+    import sys
+
+    from rdfind_amd import program
+    from tests.conftest import GOLDEN
+
+    inp = os.path.join(GOLDEN, "lubm_small.nt.gz")
+    flags = ["--use-fis", "--clean-implied", "--use-ars", "--support", "3"]
+    program.RDFind(flags + ["--output", f"file://{tmp_path}/one.txt", "--ar-output", f"file://{tmp_path}/one.ar",
+                            inp]).run()
+    env = dict(os.environ, RDFIND_DIST_BACKEND="gloo")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "rdfind_amd", "-dop", "2", *flags, "--output", f"file://{tmp_path}/two.txt",
+                        "--ar-output", f"file://{tmp_path}/two.ar", inp], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (tmp_path / "two.ar").read_text() == (tmp_path / "one.ar").read_text() != ""
+    assert sorted((tmp_path / "two.txt").read_text().splitlines()) == sorted((tmp_path / "one.txt").read_text().splitlines())
