@@ -255,3 +255,47 @@ def test_program_dop2_association_rules(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     assert (tmp_path / "two.ar").read_text() == (tmp_path / "one.ar").read_text() != ""
     assert sorted((tmp_path / "two.txt").read_text().splitlines()) == sorted((tmp_path / "one.txt").read_text().splitlines())
+
+
+def _config_worker(rank, world, port, cfg, scale, q):
+    """One rank of a sharded run on a BASELINE config: the rank draws only its own slice (synth.config_slice)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import _lib, distributed, synth
+
+    try:
+        d, _ = synth.config_slice(cfg, scale, rank, world)
+        with _lib.Context(0) as ctx:
+            ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+            del d
+            distributed.run_sharded(ctx, 100 if cfg == "c4" else 10, local_slice=True)
+            q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum()}))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_sharded_c4_at_scale_vs_golden():
+    """c4 (Freebase-shaped) at scale 0.4 -- 400M triples, support 100 -- over 2 ranks, each drawing and holding only
+    its half of the rows: the ranks' CINDs sum to the streamed oracle's golden count and checksum."""
+    import json
+
+    from tests.conftest import GOLDEN
+
+    g = json.load(open(os.path.join(GOLDEN, "full_size.json")))["c4@0.4/s1_clean"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config_worker, args=(r, 2, port, "c4", 0.4, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=840) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert not isinstance(res[r], str), res[r]
+    assert sum(res[r]["n"] for r in range(2)) == g["n_cinds"]
+    assert sum(res[r]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"])
