@@ -170,6 +170,16 @@ rdf_status rdf_association_rule_count(rdf_ctx* ctx, uint64_t* n);
 rdf_status rdf_build_capture_groups(rdf_ctx* ctx, const char* projection, rdf_group_stats* stats);
 rdf_status rdf_discover_cinds(rdf_ctx* ctx, uint32_t flags, rdf_cind_stats* stats);
 
+/* Paged discovery, for results larger than HBM (the reference streams its output to the sink, ALG/programs/RDFind.scala:
+ * 507-520): after rdf_build_capture_groups, rdf_discover_cinds_paged prepares the run with a working-memory budget per
+ * page (page_bytes; 0 = a quarter of the free HBM) and every rdf_next_page makes the next page the current result
+ * (rdf_get_result_layout, rdf_copy_result_compact, rdf_cind_checksum, the row accessors).  Page 0 holds the unary
+ * dependents, each later page a range [*first_dep, *end_dep) of binary dependents (compact capture ids); *done = 1 once
+ * the pages are exhausted (the current result is then empty).  The pages partition rdf_discover_cinds's result.
+ * Single GPU. */
+rdf_status rdf_discover_cinds_paged(rdf_ctx* ctx, uint32_t flags, uint64_t page_bytes, rdf_cind_stats* stats);
+rdf_status rdf_next_page(rdf_ctx* ctx, uint32_t* done, uint64_t* first_dep, uint64_t* end_dep);
+
 /* Whole pipeline on the current triples (the three stages above). */
 rdf_status rdf_run(rdf_ctx* ctx, uint32_t min_support, const char* projection, uint32_t flags,
                    rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs);

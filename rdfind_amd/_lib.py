@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "rdf_set_dictionary_parsed", "rdf_device_bytes", "rdf_copy_cinds_decoded", "rdf_result_sizes",
     "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules", "rdf_get_result_layout",
     "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
+    "rdf_discover_cinds_paged", "rdf_next_page",
 )
 RDF_NT_TABS = 1
 
@@ -160,6 +161,8 @@ def load():
         "rdf_copy_association_rules": (i32, [P, P, u64, ctypes.POINTER(u64)]),
         "rdf_association_rule_count": (i32, [P, ctypes.POINTER(u64)]),
         "rdf_host_alloc": (P, [u64]),
+        "rdf_discover_cinds_paged": (i32, [P, u32, u64, ctypes.POINTER(CindStats)]),
+        "rdf_next_page": (i32, [P, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "rdf_host_free": (None, [P]),
         "rdf_shard_begin": (i32, [P, u32, u32, u32, ctypes.c_char_p, u32]),
         "rdf_shard_step": (i32, [P, ctypes.POINTER(Exchange)]),
@@ -341,6 +344,31 @@ class Context:
         self._check(self.lib.rdf_discover_cinds(self.ptr, flags, ctypes.byref(st)), "rdf_discover_cinds")
         self.cinds = _struct_dict(st)
         return self.cinds
+
+    def discover_cinds_paged(self, clean_implied: bool = True, traversal_strategy: int = 1, page_bytes: int = 0):
+        """rdf_discover_cinds_paged: prepares a paged run (page_bytes of working memory per page, 0 = automatic)."""
+        flags = (RDF_CLEAN_IMPLIED if clean_implied else 0) | (RDF_STRATEGY_ALL_AT_ONCE if traversal_strategy == 0 else 0)
+        st = CindStats()
+        self._check(self.lib.rdf_discover_cinds_paged(self.ptr, flags, page_bytes, ctypes.byref(st)),
+                    "rdf_discover_cinds_paged")
+        self.cinds = _struct_dict(st)
+        return self.cinds
+
+    def next_page(self):
+        """rdf_next_page: the next page becomes the current result; returns (first_dep, end_dep), or None when done."""
+        done, d0, d1 = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.rdf_next_page(self.ptr, ctypes.byref(done), ctypes.byref(d0), ctypes.byref(d1)),
+                    "rdf_next_page")
+        return None if done.value else (int(d0.value), int(d1.value))
+
+    def pages(self, clean_implied: bool = True, traversal_strategy: int = 1, page_bytes: int = 0):
+        """Iterates a paged run: yields (first_dep, end_dep) with each page as the current result."""
+        self.discover_cinds_paged(clean_implied, traversal_strategy, page_bytes)
+        while True:
+            r = self.next_page()
+            if r is None:
+                return
+            yield r
 
     def run(self, min_support=10, projection="spo", clean_implied=True, traversal_strategy=1, use_ars=False):
         self.frequent_conditions(min_support)

@@ -720,6 +720,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_expand_owner(const u64* __restric
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
         for (u64 w = off[d]; w < off[d + 1]; ++w) owner[w] = (u32)d;
 }
+// the same for dependents [d0, d1), owner relative to off[d0]
+__global__ __launch_bounds__(RDF_BLOCK) void k_expand_owner_range(const u64* __restrict__ off, u32 d0, u32 d1, u32* owner) {
+    const u64 w0 = off[d0];
+    for (u64 d = d0 + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < d1; d += (u64)gridDim.x * RDF_BLOCK)
+        for (u64 w = off[d]; w < off[d + 1]; ++w) owner[w - w0] = (u32)d;
+}
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_nseg(const u64* __restrict__ doff, u32 C, u32* nseg) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
@@ -1538,10 +1544,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const 
 
 // R2/R3 (--clean-implied) on explicit dependents: every binary raw pair (a, X) clears the components of X
 // in a's unary refs [eoff[a], ebin[a]).  Plain stores of 0 (idempotent; k_rules_explicit has finished).
-__global__ __launch_bounds__(RDF_BLOCK) void k_rules_mark(CindView v, const u64* __restrict__ pairs, u64 E, u32 rank,
-                                                          u32 nranks, u32* keep) {
+// (pairs [e0, e0 + E) of v.epairs; keep is relative to e0, and every pair of a dependent lies in the range)
+__global__ __launch_bounds__(RDF_BLOCK) void k_rules_mark(CindView v, const u64* __restrict__ pairs, u64 e0, u64 E,
+                                                          u32 rank, u32 nranks, u32* keep) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < E; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 pr = pairs[i];
+        const u64 pr = pairs[e0 + i];
         const u32 a = (u32)(pr >> 32), x = (u32)pr;
         if (x < v.Cu || a % nranks != rank) continue;
         const u64 b = v.eoff[a], n = v.ebin[a] - b;
@@ -1550,7 +1557,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_rules_mark(CindView v, const u64*
         for (int k = 0; k < 2; ++k) {
             const u64 key = ((u64)a << 32) | bc[k];
             const u64 j = lower_bound_u64(pairs + b, n, key);
-            if (j < n && pairs[b + j] == key) keep[b + j] = 0u;
+            if (j < n && pairs[b + j] == key) keep[b + j - e0] = 0u;
         }
     }
 }
@@ -1564,24 +1571,28 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_popc_counts(const u64* __restrict
 // 64 pivot members); bits[w] holds the surviving lanes: k_heavy_eval (candidate filter + R1/R4), then
 // k_heavy_mark (R2: the components of every raw binary ref are cleared, they sit in the same pivot group),
 // then k_heavy_write streams the survivors at the scanned offsets (popcounts of bits).
+// Work items [w0, w0 + W) (a paged run takes a dependent range at a time); owner / bits / woff are indexed
+// relative to w0.
 __device__ inline void k_heavy_eval_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                         const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
-    const u32 d = owner[w];
+                                         const u64* __restrict__ choff, const u32* __restrict__ owner, u64 w0, u64 W,
+                                         u64* bits) {
+    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wl >= W) return;
+    const u64 w = w0 + wl;
+    const u32 d = owner[wl];
     const CapInfo id = v.info[d];
     const u32 piv = pivot[d];
     const u64 chunk = w - choff[d];
     const u32 cand = chunk_candidate(v, d, id, piv, chunk);
     const bool keep = cand != NONE32 && rule_keep(v, d, cand);
     const u64 kept = __ballot(keep);
-    if (lane_id() == 0) bits[w] = kept;
+    if (lane_id() == 0) bits[wl] = kept;
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_eval(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                           const u64* __restrict__ choff, const u32* __restrict__ owner,
-                                                          u64 W, u64* bits) {
+                                                          u64 w0, u64 W, u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_heavy_eval_body(vb, v, pivot, choff, owner, W, bits);
+        k_heavy_eval_body(vb, v, pivot, choff, owner, w0, W, bits);
     }
 }
 
@@ -1598,16 +1609,18 @@ __device__ inline void mark_clear(u64* bits, u64 p, bool active) {
 }
 
 __device__ inline void k_heavy_mark_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                         const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W, u64* bits) {
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
-    const u32 d = owner[w];
+                                         const u64* __restrict__ choff, const u32* __restrict__ owner, u64 w0, u64 W,
+                                         u64* bits) {
+    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wl >= W) return;
+    const u64 w = w0 + wl;
+    const u32 d = owner[wl];
     const CapInfo id = v.info[d];
     const u32 piv = pivot[d];
     const u32 x = chunk_candidate(v, d, id, piv, w - choff[d]);
     const bool bin = x != NONE32 && x >= v.Cu;
     if (!__ballot(bin)) return;
-    const u64 base = choff[d] * RDF_WAVE;  // bit index of pivot position 0
+    const u64 base = (choff[d] - w0) * RDF_WAVE;  // bit index of pivot position 0 (all of d's chunks are in range)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const u32 t = bin ? v.bcomp[2ull * (x - v.Cu) + k] : NONE32;
@@ -1619,9 +1632,9 @@ __device__ inline void k_heavy_mark_body(u64 vblk, CindView v, const u32* __rest
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                           const u64* __restrict__ choff, const u32* __restrict__ owner,
-                                                          u64 W, u64* bits) {
+                                                          u64 w0, u64 W, u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_heavy_mark_body(vb, v, pivot, choff, owner, W, bits);
+        k_heavy_mark_body(vb, v, pivot, choff, owner, w0, W, bits);
     }
 }
 
@@ -1629,26 +1642,27 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mark(u64 nvblk, CindView v,
 // survivors of a heavy work item -> output run of its dependent; src[sbase[d] + i] is candidate i of d
 // (classed binary dependents: their class list; otherwise sbase = null and the pivot group is the source)
 __device__ inline void k_heavy_write_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
-                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 W,
+                                          const u64* __restrict__ choff, const u32* __restrict__ owner, u64 w0, u64 W,
                                           const u64* __restrict__ bits, const u32* __restrict__ src,
                                           const u64* __restrict__ sbase, const u64* __restrict__ woff, u64 out_base,
                                           u32* out) {
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
-    const u64 kept = bits[w];
+    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wl >= W) return;
+    const u64 w = w0 + wl;
+    const u64 kept = bits[wl];
     const int lane = lane_id();
     if (!((kept >> lane) & 1ull)) return;
-    const u32 d = owner[w];
+    const u32 d = owner[wl];
     const u64 base = sbase ? sbase[d] : v.goff[pivot[d]];
-    out[out_base + woff[w] + __popcll(kept & lanemask_lt())] = src[base + (w - choff[d]) * RDF_WAVE + lane];
+    out[out_base + woff[wl] + __popcll(kept & lanemask_lt())] = src[base + (w - choff[d]) * RDF_WAVE + lane];
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(u64 nvblk, CindView v, const u32* __restrict__ pivot,
                                                            const u64* __restrict__ choff, const u32* __restrict__ owner,
-                                                           u64 W, const u64* __restrict__ bits,
+                                                           u64 w0, u64 W, const u64* __restrict__ bits,
                                                            const u32* __restrict__ src, const u64* __restrict__ sbase,
                                                            const u64* __restrict__ woff, u64 out_base, u32* out) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_heavy_write_body(vb, v, pivot, choff, owner, W, bits, src, sbase, woff, out_base, out);
+        k_heavy_write_body(vb, v, pivot, choff, owner, w0, W, bits, src, sbase, woff, out_base, out);
     }
 }
 
@@ -1749,29 +1763,30 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_bin_chunks(CindView v, cons
 // R2 is already in L'(m): D's binary raw refs are the binary members of L(m), the class marks cleared their
 // components.  Survivor bits per chunk, as k_heavy_eval.
 __device__ inline void k_class_bin_eval_body(u64 vblk, CindView v, const u64* __restrict__ choff,
-                                             const u32* __restrict__ owner, u64 W, const u64* __restrict__ sbase,
+                                             const u32* __restrict__ owner, u64 w0, u64 W, const u64* __restrict__ sbase,
                                              const u32* __restrict__ dcls, const u64* __restrict__ cchoff,
                                              const u64* __restrict__ lwoff, const u32* __restrict__ lists, u64* bits) {
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= W) return;
-    const u32 d = owner[w];
+    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wl >= W) return;
+    const u64 w = w0 + wl;
+    const u32 d = owner[wl];
     const u32 m = dcls[d - v.Cu];
     const u64 i = sbase[d] + (w - choff[d]) * RDF_WAVE + lane_id();
     bool keep = i < lwoff[cchoff[m + 1]];
     const u32 r = keep ? lists[i] : 0u;
     keep = keep && r != d && !is_trivial(v, d, r) && rule_keep(v, d, r);
     const u64 kept = __ballot(keep);
-    if (lane_id() == 0) bits[w] = kept;
+    if (lane_id() == 0) bits[wl] = kept;
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_bin_eval(u64 nvblk, CindView v, const u64* __restrict__ choff,
-                                                              const u32* __restrict__ owner, u64 W,
+                                                              const u32* __restrict__ owner, u64 w0, u64 W,
                                                               const u64* __restrict__ sbase,
                                                               const u32* __restrict__ dcls,
                                                               const u64* __restrict__ cchoff,
                                                               const u64* __restrict__ lwoff,
                                                               const u32* __restrict__ lists, u64* bits) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_class_bin_eval_body(vb, v, choff, owner, W, sbase, dcls, cchoff, lwoff, lists, bits);
+        k_class_bin_eval_body(vb, v, choff, owner, w0, W, sbase, dcls, cchoff, lwoff, lists, bits);
     }
 }
 
@@ -2037,6 +2052,34 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_output_runs(u32 C, const u64* __r
             rundep[i] = find_dep(choffh, C, w);
         } else {
             const u64 j = i - C - WH;
+            runoff[i] = K + H + cobase[j];
+            rundep[i] = (u32)ckeys[j];
+        }
+    }
+}
+
+// run table of one page of a paged run: explicit runs of dependents [d0, d1) (their pairs start at e0 of the explicit
+// array; epos = the page's compaction offsets), heavy work items [h0, h0 + WH), then the class members (page 0)
+__global__ __launch_bounds__(RDF_BLOCK) void k_output_runs_range(u32 C, u32 d0, u32 d1, const u64* __restrict__ eoff, u64 e0,
+                                                                 const u64* __restrict__ epos, u64 h0, u64 WH,
+                                                                 const u64* __restrict__ choffh, const u64* __restrict__ hoff,
+                                                                 u64 K, u64 nmem, const u64* __restrict__ ckeys,
+                                                                 const u64* __restrict__ cobase, u64 H, u64 n_out,
+                                                                 u64* runoff, u32* rundep) {
+    const u64 nd = d1 - d0, R = nd + WH + nmem;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= R; i += (u64)gridDim.x * RDF_BLOCK) {
+        if (i == R) {
+            runoff[i] = n_out;
+        } else if (i < nd) {
+            const u32 d = (u32)(d0 + i);
+            runoff[i] = epos[eoff[d] - e0];
+            rundep[i] = d;
+        } else if (i < nd + WH) {
+            const u64 w = i - nd;
+            runoff[i] = K + hoff[w];
+            rundep[i] = find_dep(choffh, C, h0 + w);
+        } else {
+            const u64 j = i - nd - WH;
             runoff[i] = K + H + cobase[j];
             rundep[i] = (u32)ckeys[j];
         }

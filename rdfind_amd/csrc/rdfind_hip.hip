@@ -94,6 +94,11 @@ struct rdf_ctx {
     bool class_pending = false;
     u64 pend_NT = 0, pend_base = 0, n_lists = 0, n_list_refs = 0, n_runs_explicit = 0;
     DevBuf loff;  // list offsets of the shared (class) ref lists
+    // paged discovery (rdf_discover_cinds_paged / rdf_next_page): dependents in ranges, one page at a time
+    bool paged = false, pg_unary_done = false;
+    u32 pg_flags = 0, pg_next = 0;
+    u64 pg_budget = 0, pg_Eu = 0, pg_HC = 0, pg_NT = 0, pg_WM = 0, pg_pages = 0;
+    std::vector<u64> h_choffl, h_choffh;
     bool hclassed = false;  // binary heavy-only dependents emitted from class lists (single GPU, S2L semantics)
     DevBuf pedges, pedges_tmp;
     u64 ncap = 0;
@@ -872,6 +877,7 @@ static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
     c->ar_on = false;
     c->n_rules = 0;
     c->class_pending = false;
+    c->paged = false;
     for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), c->stream));
@@ -1646,14 +1652,14 @@ static rdf_status d_heavy_count(rdf_ctx* c, const CindView& v, u64 WH, u64* H) {
         const u64 nvb = wave_blocks(WH);
         const dim3 grid(vgrid(nvb));
         if (c->hclassed)
-            hipLaunchKernelGGL(k_class_bin_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+            hipLaunchKernelGGL(k_class_bin_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->choffh.as<u64>(), c->hown.as<u32>(), 0ull, WH,
                                c->sbase.as<u64>(), c->dcls.as<u32>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(),
                                c->clists.as<u32>(), c->hbits.as<u64>());
         else
             hipLaunchKernelGGL(k_heavy_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(),
-                               c->hown.as<u32>(), WH, c->hbits.as<u64>());
+                               c->hown.as<u32>(), 0ull, WH, c->hbits.as<u64>());
         if (v.mode == RULES_CLEAN && !c->hclassed)
-            hipLaunchKernelGGL(k_heavy_mark, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+            hipLaunchKernelGGL(k_heavy_mark, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), 0ull, WH,
                                c->hbits.as<u64>());
         hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WH, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->hbits.as<u64>(),
                            WH, c->hcounts.as<u32>());
@@ -1819,7 +1825,7 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
                            c->epairs.as<u64>(), E, c->rank, c->nranks, c->flags.as<u32>());
     if (E && v.mode == RULES_CLEAN)
         hipLaunchKernelGGL(k_rules_mark, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->epairs.as<u64>(),
-                           E, c->rank, c->nranks, c->flags.as<u32>());
+                           0ull, E, c->rank, c->nranks, c->flags.as<u32>());
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), E, c->pos.as<u64>() + E, st));
     if (E)
         hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E,
@@ -1830,7 +1836,7 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     tbegin(c, RDF_T_HWRITE);
     if (WH)
         hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(WH))),
-                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WH), v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), WH,
+                           dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WH), v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), 0ull, WH,
                            c->hbits.as<u64>(), c->hclassed ? c->clists.as<u32>() : c->gcap.as<u32>(),
                            c->hclassed ? c->sbase.as<u64>() : (const u64*)nullptr, c->hoff.as<u64>(), K, c->out.as<u32>());
     tend(c, RDF_T_HWRITE);
@@ -1920,6 +1926,238 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     TRY(d_heavy_count(c, v, WH, &H));
     TRY(d_emit(c, v, E, WH, H, HC, NT));
     if (stats) *stats = c->cstats;
+    return RDF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Paged discovery: the result of a dependent range at a time, in bounded HBM (the reference streams its output to
+// the sink, ALG/programs/RDFind.scala:507-520).  The minimality rules probe other dependents only through the unary
+// components of binary dependents (R1 / R4), so the unary dependents' explicit pairs are computed first and stay
+// resident; every later page takes a range of binary dependents: its light pass, its explicit index on top of the
+// unary pairs, its rules, its heavy-only dependents.  Page 0 holds the unary dependents (explicit runs, the shared
+// class lists, heavy-path ones), pages 1.. the binary ones.  Each page is the context's current result (compact
+// hand-over, checksum, row accessors); the pages partition the result of rdf_discover_cinds.
+
+// result of dependents [d0, d1): explicit pairs epairs[e0, e1) (their rules), heavy-only work items [h0, h1), and on
+// page 0 the class part (pending expansion)
+static rdf_status d_page_emit(rdf_ctx* c, const CindView& v, u32 d0, u32 d1, u64 e0, u64 e1, u64 h0, u64 h1, u64 HC,
+                              u64 NT) {
+    hipStream_t st = c->stream;
+    const u64 E = e1 - e0, WHr = h1 - h0, nd = d1 - d0;
+    // heavy-only dependents of the range: survivor bits, counts, offsets
+    ENSURE(c, hcounts, std::max<u64>(WHr, 1) * 4);
+    ENSURE(c, hoff, (WHr + 1) * 8);
+    ENSURE(c, hbits, std::max<u64>(WHr, 1) * 8);
+    ENSURE(c, hown, std::max<u64>(WHr, 1) * 4);
+    tbegin(c, RDF_T_HCOUNT);
+    if (WHr) {
+        hipLaunchKernelGGL(k_expand_owner_range, dim3(grid_for(nd, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->choffh.as<u64>(), d0, d1, c->hown.as<u32>());
+        const u64 nvb = wave_blocks(WHr);
+        const dim3 grid(vgrid(nvb));
+        if (c->hclassed)
+            hipLaunchKernelGGL(k_class_bin_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->choffh.as<u64>(), c->hown.as<u32>(),
+                               h0, WHr, c->sbase.as<u64>(), c->dcls.as<u32>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(),
+                               c->clists.as<u32>(), c->hbits.as<u64>());
+        else
+            hipLaunchKernelGGL(k_heavy_eval, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(),
+                               c->hown.as<u32>(), h0, WHr, c->hbits.as<u64>());
+        if (v.mode == RULES_CLEAN && !c->hclassed)
+            hipLaunchKernelGGL(k_heavy_mark, grid, dim3(RDF_BLOCK), 0, st, nvb, v, c->pivot.as<u32>(), c->choffh.as<u64>(),
+                               c->hown.as<u32>(), h0, WHr, c->hbits.as<u64>());
+        hipLaunchKernelGGL(k_popc_counts, dim3(grid_for(WHr, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->hbits.as<u64>(),
+                           WHr, c->hcounts.as<u32>());
+    }
+    tend(c, RDF_T_HCOUNT);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->hcounts.as<u32>(), c->hoff.as<u64>(), WHr, c->hoff.as<u64>() + WHr, st));
+    // minimality on the range's explicit pairs
+    ENSURE(c, flags, std::max<u64>(E, 1) * 4);
+    ENSURE(c, pos, (E + 1) * 8);
+    tbegin(c, RDF_T_RULES);
+    if (E)
+        hipLaunchKernelGGL(k_rules_explicit, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                           c->epairs.as<u64>() + e0, E, 0u, 1u, c->flags.as<u32>());
+    if (E && v.mode == RULES_CLEAN)
+        hipLaunchKernelGGL(k_rules_mark, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->epairs.as<u64>(),
+                           e0, E, 0u, 1u, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), E, c->pos.as<u64>() + E, st));
+    tend(c, RDF_T_RULES);
+    u64 kh[2];
+    TRY(read_multi(c, {{c->pos.as<u64>() + E, 8}, {c->hoff.as<u64>() + WHr, 8}}, kh));
+    const u64 K = kh[0], H = kh[1];
+    ENSURE(c, out, std::max<u64>(K + H, 1) * 4);
+    if (E)
+        hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->epairs.as<u64>() + e0, E, c->flags.as<u32>(), c->pos.as<u64>(), c->out.as<u32>());
+    tbegin(c, RDF_T_HWRITE);
+    if (WHr)
+        hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(WHr))), dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WHr), v,
+                           c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), h0, WHr, c->hbits.as<u64>(),
+                           c->hclassed ? c->clists.as<u32>() : c->gcap.as<u32>(),
+                           c->hclassed ? c->sbase.as<u64>() : (const u64*)nullptr, c->hoff.as<u64>(), K, c->out.as<u32>());
+    tend(c, RDF_T_HWRITE);
+    c->class_pending = NT > 0;
+    c->pend_NT = NT;
+    c->pend_base = K + H;
+    const u32 ncls = (u32)c->n_classes;
+    c->n_lists = HC ? ncls : 0;
+    c->n_list_refs = 0;
+    if (c->n_lists) {
+        ENSURE(c, loff, (ncls + 1ull) * 8);
+        hipLaunchKernelGGL(k_list_offsets, dim3(grid_for(ncls + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->cchoff.as<u64>(), c->lwoff.as<u64>(), ncls, c->loff.as<u64>());
+    }
+    const u64 nmem = HC ? c->n_class_members : 0;
+    const u64 R = nd + WHr + nmem;
+    ENSURE(c, runoff, (R + 1) * 8);
+    ENSURE(c, rundep, std::max<u64>(R, 1) * 4);
+    hipLaunchKernelGGL(k_output_runs_range, dim3(grid_for(R + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->C, d0, d1,
+                       v.eoff, e0, c->pos.as<u64>(), h0, WHr, c->choffh.as<u64>(), c->hoff.as<u64>(), K, nmem,
+                       c->ckeys.as<u64>(), c->cobase.as<u64>(), H, K + H + HC, c->runoff.as<u64>(), c->rundep.as<u32>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    if (c->n_lists) TRY(read_u64(c, c->loff.as<u64>() + ncls, &c->n_list_refs));
+    c->n_runs = R;
+    c->n_runs_explicit = nd + WHr;
+    c->h_runs_valid = false;
+    ++c->run_id;
+    c->n_out = K + H + HC;
+    c->n_class_out = HC;
+    c->out_ptr = c->out.as<u32>();
+    c->cstats.n_cinds = c->n_out;
+    c->stage = 4;
+    return RDF_OK;
+}
+
+// greedy dependent range from d0 whose light octets and heavy work items fit the page budget (at least one dependent)
+static u32 page_end(const rdf_ctx* c, u32 d0, u32 dmax) {
+    const u64 per_oct = 8 * 8 + 8 + 12 + 8 * 4 + 8 + 4;   // slots, kill mask, counts, pairs, flags / positions, refs
+    const u64 per_chunk = 8 + 4 + 8 + 4 + RDF_WAVE * 4;  // bits, counts, offsets, owner, refs
+    u32 d1 = d0 + 1;
+    while (d1 < dmax) {
+        const u64 oct = c->h_choffl[d1 + 1] - c->h_choffl[d0], ch = c->h_choffh[d1 + 1] - c->h_choffh[d0];
+        if (oct * per_oct + ch * per_chunk > c->pg_budget) break;
+        ++d1;
+    }
+    return d1;
+}
+
+rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_bytes, rdf_cind_stats* stats) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
+    if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    if (!page_bytes) {  // a quarter of the free HBM
+        size_t fr = 0, tot = 0;
+        HIP_TRY(c, hipMemGetInfo(&fr, &tot));
+        page_bytes = std::max<u64>(fr / 4, 1ull << 26);
+    }
+    CindView v = make_view(c, flags);
+    TRY(d_pivot_local(c, v));
+    tbegin(c, RDF_T_PIVOT);
+    if (c->C) {
+        const unsigned gp = grid_for(c->C, RDF_BLOCK, kGrid);
+        ENSURE(c, ppart, 3ull * gp * 8);
+        hipLaunchKernelGGL(k_pivot_final, dim3(gp), dim3(RDF_BLOCK), 0, st, v, c->pbest.as<u64>(),
+                           c->pnl.as<u32>(), c->pivot.as<u32>(), c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>(),
+                           c->nchh.as<u32>(), c->info.as<CapInfo>(), c->ppart.as<u64>());
+        hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gp, dscal(c, 2));
+    }
+    tend(c, RDF_T_PIVOT);
+    u64 WL = 0, WH = 0, WI = 0, WP = 0, WM = 0, HC = 0, NT = 0;
+    TRY(d_chunks(c, &WL, &WH, &WI, &WP));
+    TRY(d_light_owners(c, WI, WP, &WM));
+    c->pg_budget = page_bytes;
+    c->pg_WM = WM;
+    c->h_choffl.resize(c->C + 1ull);
+    HIP_TRY(c, hipMemcpy(c->h_choffl.data(), c->choffl.p, (c->C + 1ull) * 8, hipMemcpyDeviceToHost));
+    c->h_choffh.assign(c->C + 1ull, 0);  // no heavy work while the unary light pass is batched
+    // the unary dependents' explicit pairs, in budgeted batches, resident for the rest of the run
+    u64 Eu = 0;
+    for (u32 d0 = 0; d0 < c->Cu;) {
+        const u32 d1 = page_end(c, d0, c->Cu);
+        LightRange r;
+        TRY(light_range(c, d0, d1, WM > 0, &r));
+        u64 E = 0;
+        TRY(d_light_run(c, v, c->pivot.as<u32>(), r, Eu, &E));
+        Eu += E;
+        d0 = d1;
+    }
+    c->n_explicit_raw = Eu;
+    c->n_light_chunks = WL;
+    TRY(d_explicit_index(c, v, Eu, true));
+    c->hclassed = !v.literal && c->allow_hclass && !v.ar;
+    TRY(d_classes_single(c, v, &HC, &NT));
+    if (c->hclassed) TRY(d_class_bin(c, v, &WH));
+    HIP_TRY(c, hipMemcpy(c->h_choffh.data(), c->choffh.p, (c->C + 1ull) * 8, hipMemcpyDeviceToHost));
+    c->pg_Eu = Eu;
+    c->pg_HC = HC;
+    c->pg_NT = NT;
+    c->pg_flags = flags;
+    c->pg_next = 0;
+    c->pg_pages = 0;
+    c->pg_unary_done = false;
+    c->paged = true;
+    HIP_TRY(c, hipEventRecord(c->ev[5], st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], c->ev[5]));
+    tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS);
+    rdf_cind_stats& cs = c->cstats;
+    memset(&cs, 0, sizeof(cs));
+    cs.n_light_chunks = WL;
+    cs.n_heavy_chunks = WH;
+    cs.n_class_members = c->n_class_members;
+    cs.n_classes = c->n_classes;
+    cs.n_class_cinds = HC;
+    cs.n_light_candidates = c->light_candidates;
+    cs.n_light_entries = c->light_entries;
+    cs.n_heavy_candidates = c->heavy_candidates;
+    if (stats) *stats = cs;
+    c->stage = 3;  // no current result until rdf_next_page
+    return RDF_OK;
+}
+
+rdf_status rdf_next_page(rdf_ctx* c, uint32_t* done, uint64_t* first_dep, uint64_t* end_dep) {
+    if (!c || !done) return RDF_ERR_ARG;
+    if (!c->paged) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds_paged must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    CindView v = make_view(c, c->pg_flags);
+    v.eoff = c->eoff.as<u64>();
+    v.epairs = c->epairs.as<u64>();
+    v.ebin = c->ebin.as<u64>();
+    u32 d0 = 0, d1 = 0;
+    *done = 0;
+    if (!c->pg_unary_done) {  // page 0: the unary dependents
+        d1 = c->Cu;
+        TRY(d_page_emit(c, v, 0, c->Cu, 0, c->pg_Eu, c->h_choffh[0], c->h_choffh[c->Cu], c->pg_HC, c->pg_NT));
+        c->pg_unary_done = true;
+        c->pg_next = c->Cu;
+    } else if (c->pg_next < c->C) {  // a range of binary dependents on top of the resident unary pairs
+        d0 = c->pg_next;
+        d1 = page_end(c, d0, c->C);
+        LightRange r;
+        TRY(light_range(c, d0, d1, c->pg_WM > 0, &r));
+        u64 Eb = 0;
+        TRY(d_light_run(c, v, c->pivot.as<u32>(), r, c->pg_Eu, &Eb));
+        c->n_explicit_raw += Eb;
+        TRY(d_explicit_index(c, v, c->pg_Eu + Eb, true));
+        TRY(d_page_emit(c, v, d0, d1, c->pg_Eu, c->pg_Eu + Eb, c->h_choffh[d0], c->h_choffh[d1], 0, 0));
+        c->pg_next = d1;
+    } else {
+        *done = 1;
+        c->n_out = c->n_class_out = c->n_runs = c->n_runs_explicit = c->n_lists = c->n_list_refs = 0;
+        c->class_pending = false;
+        HIP_TRY(c, c->runoff.ensure(8));
+        HIP_TRY(c, hipMemsetAsync(c->runoff.p, 0, 8, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->stage = 4;
+        return RDF_OK;
+    }
+    ++c->pg_pages;
+    c->cstats.n_explicit_raw = c->n_explicit_raw;
+    if (first_dep) *first_dep = d0;
+    if (end_dep) *end_dep = d1;
     return RDF_OK;
 }
 

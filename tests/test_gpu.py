@@ -259,6 +259,53 @@ def test_dense_bitmap_paths_parity(monkeypatch):
             g.close()
 
 
+def _paged(g, ms, strategy, clean, page_bytes):
+    """Every page of a paged run: (union of decoded rows, total count, sum of page checksums, pages, compact ok)."""
+    g.frequent_conditions(ms)
+    g.build_capture_groups("spo")
+    rows, n, h, pages, compact_ok = set(), 0, 0, 0, True
+    for _ in g.pages(clean, strategy, page_bytes):
+        parts = g.copy_result_compact()
+        cnt = g.cind_count()
+        page_rows = _lib.decoded_to_set(g.decoded_cinds())
+        assert not (rows & page_rows)  # pages are disjoint
+        rows |= page_rows
+        n += cnt
+        h = (h + g.checksum()) % (1 << 64)
+        compact_ok &= C.checksum_compact(parts, g.num_terms)[:2] == (cnt, g.checksum())
+        pages += 1
+    return rows, n, h, pages, compact_ok
+
+
+@pytest.mark.parametrize("heavy_min", [64, 2])
+def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
+    """rdf_discover_cinds_paged with a one-byte page budget (every binary dependent is its own page) partitions the
+    unpaged result, in every mode, with and without bitmask columns and classes."""
+    monkeypatch.setenv("RDFIND_HEAVY_MIN", str(heavy_min))
+    g = _lib.Context(0)
+    try:
+        rng = random.Random(500 + heavy_min)
+        for _ in range(30):
+            n = rng.randrange(20, 400)
+            nv = rng.randrange(4, 40)
+            ms = rng.randrange(1, 4)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            for strategy, clean in MODES:
+                exp = expected_set(arr, nv, ms, strategy, clean)
+                g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+                rows, cnt, _, pages, ok = _paged(g, ms, strategy, clean, 1)
+                assert rows == exp and cnt == len(exp) and ok, (n, nv, ms, strategy, clean, heavy_min)
+        for cfg, scale in (("c5", 0.01), ("c1", 0.05)):
+            d = synth.config(cfg, scale)
+            exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+            g.set_triples(d.s, d.p, d.o, d.num_terms)
+            rows, cnt, _, pages, ok = _paged(g, d.min_support, 1, True, 1 << 16)
+            assert rows == exp and ok and pages > 2, (cfg, heavy_min, pages)
+    finally:
+        g.close()
+
+
 def test_large_grids_two_paths(monkeypatch):
     """c5 at scale 0.3 (8.7e9 CINDs): the heavy-only binary dependents take > 2^26 work items (a dispatch holds
     < 2^32 work-items, so the kernels loop over virtual blocks).  The classed path and the pivot-scan path

@@ -149,3 +149,31 @@ def test_light_variants_full_size(env):
         assert r.returncode == 0, r.stderr[-2000:]
         got = json.loads(r.stdout.strip().splitlines()[-1])
         assert got["n"] == g["n_cinds"] and got["sum"] == g["checksum"], (key, env, got)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("key,page_bytes", [("c5@0.3/s1_clean", 4 << 30), ("c5@1.0/s1_clean", 0)])
+def test_paged_full_size_vs_oracle(ctx, key, page_bytes):
+    """Paged discovery (bounded HBM per page) at the pair-explosion config: the pages' counts and checksums (device
+    expansion, and the compact hand-over expanded by the checker) sum to the streamed oracle's golden vector.  c5 at
+    scale 1.0 is the BASELINE size; its result does not fit in HBM at once."""
+    from oracle import c_oracle as C
+
+    if key not in GOLD:
+        pytest.skip(f"{key} golden vector not generated")
+    g = GOLD[key]
+    d = dataset(g["config"], g["scale"])
+    assert str(fingerprint(d)) == g["fingerprint"], "synthetic generator drifted from the golden input"
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.frequent_conditions(d.min_support)
+    ctx.build_capture_groups("spo")
+    n = h = hc = pages = 0
+    for _ in ctx.pages(g["clean"], g["strategy"], page_bytes):
+        cnt, hh, _ = C.checksum_compact(ctx.copy_result_compact(), d.num_terms)
+        assert cnt == ctx.cind_count()
+        n += cnt
+        hc = (hc + hh) % (1 << 64)
+        h = (h + ctx.checksum()) % (1 << 64)
+        pages += 1
+    assert pages >= 2
+    assert n == g["n_cinds"] and h == int(g["checksum"]) and hc == h

@@ -11,7 +11,7 @@ from tests.conftest import ROOT
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "rdfind_hip.h")).read()
-    return sorted(set(re.findall(r"^(?:rdf_status|void|const char\s*\*)\s*(rdf_[a-z_0-9]+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:rdf_status|void\s*\*|void|const char\s*\*)\s*(rdf_[a-z_0-9]+)\s*\(", src, re.M)))
 
 
 def test_library_exports_header_symbols():

@@ -31,6 +31,7 @@ CASES = {
     "c4_0.1": ("c4", 0.1, [(1, True)]),      # counter-based generator from here on (synth._c4_rows)
     "c4_0.4": ("c4", 0.4, [(1, True)]),
     "c5": ("c5", 0.3, [(1, True), (0, False)]),
+    "c5_1.0": ("c5", 1.0, [(1, True)]),      # the BASELINE size (paged discovery on the GPU)
 }
 
 
