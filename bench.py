@@ -154,6 +154,11 @@ def layout_bytes(L):
             8 * L["n_members"] + 8 * L["n_captures"])
 
 
+def ctx_pages(ctx):
+    """Pages of the last paged run (rdf_next_page calls that produced a page)."""
+    return getattr(ctx, "_pages", None)
+
+
 def launch_ranks(nranks, argv):
     """--gpus N without a launcher: one rank per GPU under torch.distributed.run, started as child processes before
     this process touches a GPU (rdfind_amd/program.py launch_ranks); returns their exit status."""
@@ -186,6 +191,10 @@ def main():
                     help="time the CPU baseline on the benchmarked workload itself up to this many triples")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
                     "exchanges, to rehearse several ranks on one GPU)")
+    ap.add_argument("--page-bytes", type=int, default=None,
+                    help="paged discovery (rdf_discover_cinds_paged) with this working memory per page, 0 = a quarter "
+                         "of the free HBM; every page is handed over in turn.  Default: unpaged, except c5 beyond "
+                         "scale 0.3, whose result does not fit in HBM")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -219,20 +228,35 @@ def main():
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
     sink = CompactSink()
 
+    paged = dist is None and (args.page_bytes is not None or (args.config == "c5" and total_scale > 0.3))
     if dist is not None:
         from rdfind_amd import distributed
 
-        def discover():
+        def discover(hand_over):
             distributed.run_sharded(ctx, ms, local_slice=True)
+            if hand_over:
+                sink.copy(ctx)
             return ctx.cinds
+    elif paged:  # pages of bounded HBM, each handed over before the next (the reference streams to its sink)
+        def discover(hand_over):
+            ctx.frequent_conditions(ms)
+            ctx.build_capture_groups("spo")
+            n = 0
+            for _ in ctx.pages(True, 1, args.page_bytes or 0):
+                n += ctx.cind_count()
+                if hand_over:
+                    sink.copy(ctx)
+            _, cs = ctx.last_stats()
+            return dict(cs, n_cinds=n, pages=ctx_pages(ctx))
     else:
-        def discover():
-            return ctx.run(ms)
+        def discover(hand_over):
+            cs = ctx.run(ms)
+            if hand_over:
+                sink.copy(ctx)
+            return cs
 
     def step():  # T_disc: encoded triples in HBM -> compact CIND id-records in (pinned) host memory
-        cs = discover()
-        sink.copy(ctx)
-        return cs
+        return discover(True)
 
     def barrier():
         if dist is not None:
@@ -267,7 +291,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        discover()
+        discover(False)
     ctx.sync()
     barrier()
     elapsed_dev = max_over_ranks(time.perf_counter() - t1)
@@ -328,7 +352,7 @@ def main():
                "sample": f"{args.config} scale {cpu_scale} ({sd.n} triples, {r['n_cinds']} CINDs"
                          f"{', the benchmarked workload itself' if same else ''}) through oracle/c/rdfind_oracle.c "
                          f"(streamed count + checksum, same stages incl. minimality) on {nt} OpenMP threads, {ct:.1f}s"}
-        if same:
+        if same and not paged:
             parts = ctx.copy_result_compact()  # the hand-over the timed steps copied, expanded by the checker
             n_c, h_c, _ = c_oracle.checksum_compact(parts, d.num_terms)
             cpu["matches_gpu"] = bool(r["n_cinds"] == n_c == cs["n_cinds"] and r["checksum"] == h_c)
@@ -369,7 +393,8 @@ def main():
                        "triples": total_n, "triples_rank0": d.n, "cinds": total_cinds, "cinds_rank0": cs["n_cinds"],
                        "parallelism": f"input slices + join-hash shards x{world} (RCCL)" if world > 1 else "single"},
             "step": "T_disc (SURVEY.md 8(d)): dictionary-encoded triples resident in HBM -> compact CindSet-shaped "
-                    "id-records (rdf_copy_result_compact) in pinned host memory, every rank",
+                    "id-records (rdf_copy_result_compact) in pinned host memory, every rank" +
+                    (" (paged: every page handed over in turn)" if paged else ""),
             "handover": {"bytes_all_ranks": total_bytes, "pinned": sink.pinned, "n_refs": L["n_refs"],
                          "n_list_refs": L["n_list_refs"], "n_members": L["n_members"], "n_runs": L["n_runs"]},
             "device_resident": {"ms_per_step": round(elapsed_dev * 1000.0 / steps, 3),

@@ -364,10 +364,12 @@ class Context:
     def pages(self, clean_implied: bool = True, traversal_strategy: int = 1, page_bytes: int = 0):
         """Iterates a paged run: yields (first_dep, end_dep) with each page as the current result."""
         self.discover_cinds_paged(clean_implied, traversal_strategy, page_bytes)
+        self._pages = 0
         while True:
             r = self.next_page()
             if r is None:
                 return
+            self._pages += 1
             yield r
 
     def run(self, min_support=10, projection="spo", clean_implied=True, traversal_strategy=1, use_ars=False):

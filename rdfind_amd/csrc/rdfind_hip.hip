@@ -155,8 +155,8 @@ static void tend(rdf_ctx* c, int id) {
     if (c->tn[id] < rdf_ctx::kTSeg) (void)hipEventRecord(c->tev[2 * (id * rdf_ctx::kTSeg + c->tn[id]) + 1], c->stream);
     c->tn[id]++;
 }
-// call after a stream sync: fold the recorded segments of timers [lo, hi) into tms
-static void tcollect(rdf_ctx* c, int lo, int hi) {
+// call after a stream sync: fold the recorded segments of timers [lo, hi) into tms (add: onto the previous value)
+static void tcollect(rdf_ctx* c, int lo, int hi, bool add = false) {
     for (int i = lo; i < hi; ++i) {
         float total = 0;
         for (int k = 0; k < std::min(c->tn[i], rdf_ctx::kTSeg); ++k) {
@@ -164,7 +164,7 @@ static void tcollect(rdf_ctx* c, int lo, int hi) {
             const int e = 2 * (i * rdf_ctx::kTSeg + k);
             if (hipEventElapsedTime(&ms, c->tev[e], c->tev[e + 1]) == hipSuccess) total += ms;
         }
-        c->tms[i] = total;
+        c->tms[i] = add ? c->tms[i] + total : total;
         c->tn[i] = 0;
     }
 }
@@ -2155,6 +2155,7 @@ rdf_status rdf_next_page(rdf_ctx* c, uint32_t* done, uint64_t* first_dep, uint64
         return RDF_OK;
     }
     ++c->pg_pages;
+    tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS, true);  // kernel-family times add up over the pages
     c->cstats.n_explicit_raw = c->n_explicit_raw;
     if (first_dep) *first_dep = d0;
     if (end_dep) *end_dep = d1;

@@ -53,7 +53,8 @@ def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo"):
         ctx.close()
         q.put((rank, out))
     except Exception as e:  # report instead of hanging the parent
-        q.put((rank, repr(e)))
+        import traceback
+        q.put((rank, repr(e) + "\n" + traceback.format_exc()[-1500:]))
     finally:
         dist.destroy_process_group()
 
@@ -65,11 +66,17 @@ def _run_sharded(world, cases, local_slice=False, backend="gloo"):
     procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice, backend)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=600) for _ in procs)
-    for p in procs:
-        p.join(timeout=120)
-    for r in range(world):
-        assert not isinstance(res[r], str), res[r]
+    res = {}
+    try:
+        for _ in procs:
+            r, item = q.get(timeout=600)
+            assert not isinstance(item, str), f"rank {r}: {item}"  # a failed rank: stop its peers (below), report
+            res[r] = item
+    finally:
+        for p in procs:
+            p.join(timeout=5 if len(res) < world else 120)
+            if p.is_alive():
+                p.terminate()
     return res
 
 
@@ -292,10 +299,16 @@ def test_sharded_c4_at_scale_vs_golden():
     procs = [ctx.Process(target=_config_worker, args=(r, 2, port, "c4", 0.4, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=840) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-    for r in range(2):
-        assert not isinstance(res[r], str), res[r]
+    res = {}
+    try:
+        for _ in procs:
+            r, item = q.get(timeout=840)
+            assert not isinstance(item, str), f"rank {r}: {item}"
+            res[r] = item
+    finally:
+        for p in procs:
+            p.join(timeout=5 if len(res) < 2 else 60)
+            if p.is_alive():
+                p.terminate()
     assert sum(res[r]["n"] for r in range(2)) == g["n_cinds"]
     assert sum(res[r]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"])

@@ -74,10 +74,14 @@ for step in "$@"; do
     rehearse:*)  # rehearse:<config>:<scale>:<ranks> -- sharded bench with several ranks on the one GPU (gloo)
       IFS=: read -r _ CFG SC NR <<< "$step"
       tools/shard_rehearsal.sh ${TAG}_${CFG}_$NR $CFG $SC $NR || exit 1 ;;
-    tfile:*)  # tfile:<test file>[,<test file>...] -- whole GPU test files (one pytest process)
-      FILES=$(echo "${step#tfile:}" | tr ',' ' ')
-      timeout -k 10 1000 python -u -m pytest $FILES -m gpu -x -v --timeout 600 --timeout-method thread \
-        > gpurun_out/tfile_$TAG.log 2>&1 || { echo "tfile failed"; tail -40 gpurun_out/tfile_$TAG.log; exit 1; }
+    tfile:*)  # tfile:<test file>[,<test file>...][@-k expr] -- GPU test files (one pytest process), with a heartbeat
+      SPEC=${step#tfile:}; FILES=$(echo "${SPEC%%@*}" | tr ',' ' '); KEXPR=""
+      [[ "$SPEC" == *@* ]] && KEXPR="${SPEC#*@}"
+      timeout -k 10 1000 python -u -m pytest $FILES -m gpu -x -v --timeout 600 --timeout-method thread ${KEXPR:+-k "$KEXPR"} \
+        > gpurun_out/tfile_$TAG.log 2>&1 &
+      PID=$!
+      while kill -0 $PID 2>/dev/null; do sleep 30; echo "[hb $(date +%T)] $(grep -cE 'PASSED' gpurun_out/tfile_$TAG.log) passed"; done
+      wait $PID || { echo "tfile failed"; tail -60 gpurun_out/tfile_$TAG.log; exit 1; }
       grep -cE "PASSED" gpurun_out/tfile_$TAG.log; tail -2 gpurun_out/tfile_$TAG.log ;;
     gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
