@@ -321,6 +321,24 @@ rdf_status rdf_shard_step(rdf_ctx* ctx, rdf_exchange* x);
 rdf_status rdf_shard_export(rdf_ctx* ctx, void* dst);
 rdf_status rdf_shard_import(rdf_ctx* ctx, const void* src, uint64_t count);
 
+/*
+ * Sharded ingest (-dop N; the reference splits its input per task, FLK/persistence/MultiFileTextInputFormat.java:49-100,
+ * and parses in parallel, ALG/programs/RDFind.scala:196-237): rdf_shard_parse_begin parses this rank's part of the
+ * input (whole lines) into a local dictionary, then the same rdf_shard_step / export / import loop as above runs
+ * the dictionary exchange: every local term goes to the rank owning its hash, which deduplicates the terms it
+ * receives (byte-verified) and assigns global ids (owner base + first-arrival rank), and the ids come back.  At
+ * RDF_X_DONE the resident triples are this rank's slice in the global id space (rdf_num_terms = all distinct terms),
+ * ready for rdf_shard_begin with RDF_SHARD_LOCAL_SLICE.  After that run, rdf_shard_dictionary_begin + the loop give
+ * every rank the formatting dictionary of the terms its output lines can name (the values of the frequent
+ * conditions, gathered from their owners); rdf_dictionary_terms reads terms of it back.
+ */
+rdf_status rdf_shard_parse_begin(rdf_ctx* ctx, uint32_t rank, uint32_t nranks, const char* text, uint64_t nbytes,
+                                 uint32_t flags, uint64_t* n_triples);
+rdf_status rdf_shard_dictionary_begin(rdf_ctx* ctx);
+rdf_status rdf_num_terms(rdf_ctx* ctx, uint32_t* n);
+/* offsets[n + 1]: term ids[i] is out[offsets[i], offsets[i+1]); RDF_ERR_ARG (offsets filled) if cap is too small. */
+rdf_status rdf_dictionary_terms(rdf_ctx* ctx, const uint32_t* ids, uint64_t n, char* out, uint64_t cap, uint64_t* offsets);
+
 /* Device time (ms) of the last call of each stage: [0] fc, [1] groups, [2] cinds. */
 rdf_status rdf_stage_times(rdf_ctx* ctx, float* ms3);
 /* Device time (ms) of each kernel family (RDF_T_*) in the last calls; count <= RDF_NUM_TIMERS. */

@@ -32,7 +32,8 @@ EXPORTED_SYMBOLS = (
     "rdf_set_dictionary_parsed", "rdf_device_bytes", "rdf_copy_cinds_decoded", "rdf_result_sizes",
     "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules", "rdf_get_result_layout",
     "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
-    "rdf_discover_cinds_paged", "rdf_next_page",
+    "rdf_discover_cinds_paged", "rdf_next_page", "rdf_shard_parse_begin", "rdf_shard_dictionary_begin", "rdf_num_terms",
+    "rdf_dictionary_terms",
 )
 RDF_NT_TABS = 1
 
@@ -161,6 +162,10 @@ def load():
         "rdf_copy_association_rules": (i32, [P, P, u64, ctypes.POINTER(u64)]),
         "rdf_association_rule_count": (i32, [P, ctypes.POINTER(u64)]),
         "rdf_host_alloc": (P, [u64]),
+        "rdf_shard_parse_begin": (i32, [P, u32, u32, ctypes.c_char_p, u64, u32, ctypes.POINTER(u64)]),
+        "rdf_shard_dictionary_begin": (i32, [P]),
+        "rdf_num_terms": (i32, [P, ctypes.POINTER(u32)]),
+        "rdf_dictionary_terms": (i32, [P, P, u64, P, u64, P]),
         "rdf_discover_cinds_paged": (i32, [P, u32, u64, ctypes.POINTER(CindStats)]),
         "rdf_next_page": (i32, [P, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "rdf_host_free": (None, [P]),
@@ -407,6 +412,41 @@ class Context:
         self._nranks = nranks
         self._check(self.lib.rdf_shard_begin(self.ptr, rank, nranks, min_support, projection.encode(), flags),
                     "rdf_shard_begin")
+
+    def shard_parse_begin(self, rank: int, nranks: int, data: bytes, tabs: bool = False) -> int:
+        """Sharded ingest of this rank's part of the input (rdf_shard_parse_begin); drive it with
+        distributed.run_protocol.  Returns the rank's triples."""
+        n = ctypes.c_uint64()
+        self._nranks = nranks
+        self._parsed = data
+        self._check(self.lib.rdf_shard_parse_begin(self.ptr, rank, nranks, data, len(data), RDF_NT_TABS if tabs else 0,
+                                                   ctypes.byref(n)), "rdf_shard_parse_begin")
+        return int(n.value)
+
+    def shard_dictionary_begin(self):
+        """The formatting dictionary by owner lookup after a sharded run (rdf_shard_dictionary_begin)."""
+        self._check(self.lib.rdf_shard_dictionary_begin(self.ptr), "rdf_shard_dictionary_begin")
+
+    def num_terms_now(self) -> int:
+        v = ctypes.c_uint32()
+        self._check(self.lib.rdf_num_terms(self.ptr, ctypes.byref(v)), "rdf_num_terms")
+        self.num_terms = int(v.value)
+        return self.num_terms
+
+    def dictionary_terms(self, ids) -> list:
+        """Terms of the formatting dictionary (rdf_dictionary_terms), as str."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        off = np.zeros(ids.shape[0] + 1, np.uint64)
+        cap = 1 << 20
+        while True:
+            out = ctypes.create_string_buffer(cap)
+            rc = self.lib.rdf_dictionary_terms(self.ptr, ids.ctypes.data, ids.shape[0], out, cap, off.ctypes.data)
+            if rc == 0:
+                raw = out.raw
+                return [raw[int(off[i]):int(off[i + 1])].decode("utf-8") for i in range(ids.shape[0])]
+            if int(off[-1]) <= cap:
+                self._check(rc, "rdf_dictionary_terms")
+            cap = int(off[-1])
 
     def shard_step(self) -> ExchangeRequest:
         x = Exchange()

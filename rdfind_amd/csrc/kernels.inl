@@ -2908,6 +2908,165 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_nt_assign(const u64* __restrict__
 
 namespace rdf {
 
+// ---- sharded ingest: a global dictionary from every rank's local one (term owner = hash of the term bytes) ----
+
+// per local term: hash of its bytes, owner rank, sort key (owner << 32 | term), payload words (8 B each)
+__global__ __launch_bounds__(RDF_BLOCK) void k_term_route_keys(const unsigned char* __restrict__ text,
+                                                               const u64* __restrict__ toff, const u32* __restrict__ tlen,
+                                                               u64 V, u32 nranks, u64* hv, u64* keys) {
+    for (u64 t = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; t < V; t += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 h = nt_hash(text, toff[t], tlen[t]);
+        hv[t] = h;
+        keys[t] = ((h >> 40) % nranks) << 32 | t;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_term_words(const u64* __restrict__ keys, u64 V, const u32* __restrict__ tlen,
+                                                          u32* words) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < V; i += (u64)gridDim.x * RDF_BLOCK)
+        words[i] = (tlen[(u32)keys[i]] + 7) / 8;
+}
+// headers (hash, src << 58 | len << 32 | local id) and the payload words, in owner-sorted order
+__global__ __launch_bounds__(RDF_BLOCK) void k_term_pack(const unsigned char* __restrict__ text, const u64* __restrict__ keys,
+                                                         u64 V, const u64* __restrict__ toff, const u32* __restrict__ tlen,
+                                                         const u64* __restrict__ hv, const u64* __restrict__ woff, u32 src,
+                                                         u64* hdr, u64* payload) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < V; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 t = (u32)keys[i];
+        const u32 n = tlen[t];
+        hdr[2 * i] = hv[t];
+        hdr[2 * i + 1] = ((u64)src << 58) | ((u64)n << 32) | t;
+        const u64 a = toff[t], w0 = woff[i];
+        for (u32 w = 0; w < (n + 7) / 8; ++w) {
+            u64 x = 0;
+            for (u32 k = 0; k < 8 && 8 * w + k < n; ++k) x |= (u64)text[a + 8 * w + k] << (8 * k);
+            payload[w0 + w] = x;
+        }
+    }
+}
+// owner side: the received records as "occurrences" of the dictionary kernels (text = payload bytes)
+__global__ __launch_bounds__(RDF_BLOCK) void k_term_records(const u64* __restrict__ hdr, u64 m, u32* words, u32* tlen,
+                                                            u64* hv, u32* src_hist) {
+    __shared__ u32 lh[RDF_MAX_RANKS];
+    for (u32 i = threadIdx.x; i < RDF_MAX_RANKS; i += RDF_BLOCK) lh[i] = 0;
+    __syncthreads();
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 w = hdr[2 * i + 1];
+        const u32 n = (u32)((w >> 32) & ((1u << 26) - 1));
+        tlen[i] = n;
+        words[i] = (n + 7) / 8;
+        hv[i] = hdr[2 * i];
+        atomicAdd(&lh[w >> 58], 1u);
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < RDF_MAX_RANKS; i += RDF_BLOCK)
+        if (lh[i]) atomicAdd(&src_hist[i], lh[i]);
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_needed_words(const u32* __restrict__ flags, const u32* __restrict__ len,
+                                                            u32 n, u32* words) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        words[i] = flags[i] ? (len[i] + 7) / 8 : 0u;
+}
+__global__ void k_gather_u64_at(const u64* __restrict__ a, const u64* __restrict__ idx, u32 n, u64* out) {
+    for (u32 i = threadIdx.x; i < n; i += blockDim.x) out[i] = a[idx[i]];
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_words_to_bytes(const u64* __restrict__ woff, u64 m, u64* tstart) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK) tstart[i] = 8 * woff[i];
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_fill_u32(u32* a, u64 n, u32 v) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) a[i] = v;
+}
+// owner's global ids: reply word (sender's local id << 32 | global id) per record (records arrive grouped by sender)
+// and the owner's term table (first occurrence's byte offset and length in the payload)
+__global__ __launch_bounds__(RDF_BLOCK) void k_term_reply(const u64* __restrict__ hdr, u64 m, const u32* __restrict__ rep,
+                                                          const u32* __restrict__ first, const u32* __restrict__ fid, u32 base,
+                                                          const u64* __restrict__ tstart, const u32* __restrict__ tlen,
+                                                          u64* reply, u64* own_off, u32* own_len) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 id = fid[rep[i]];
+        reply[i] = ((u64)(u32)hdr[2 * i + 1] << 32) | (base + id);
+        if (first[i]) {
+            own_off[id] = tstart[i];
+            own_len[id] = tlen[i];
+        }
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_term_gmap(const u64* __restrict__ reply, u64 m, u32* gmapv) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK)
+        gmapv[reply[i] >> 32] = (u32)reply[i];
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_remap3(u32* s, u32* p, u32* o, u64 n, const u32* __restrict__ gmapv) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        s[i] = gmapv[s[i]];
+        p[i] = gmapv[p[i]];
+        o[i] = gmapv[o[i]];
+    }
+}
+
+// formatting dictionary by owner lookup: the terms every rank's output may name are the values of the frequent
+// conditions (unary fval, binary keys); each owner marks its own among them
+__global__ __launch_bounds__(RDF_BLOCK) void k_mark_needed(const u32* __restrict__ fval, u64 U, const u64* __restrict__ bkeys,
+                                                           u64 B, u32 base, u32 nown, u32* flags) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < U + B; i += (u64)gridDim.x * RDF_BLOCK) {
+        u32 v[2] = {NONE32, NONE32};
+        if (i < U) {
+            v[0] = fval[i];
+        } else {
+            const u64 k = bkeys[i - U];
+            v[0] = bin_key_v1(k);
+            v[1] = bin_key_v2(k);
+        }
+        for (int j = 0; j < 2; ++j)
+            if (v[j] != NONE32 && v[j] >= base && v[j] - base < nown) flags[v[j] - base] = 1u;
+    }
+}
+// the owner's needed terms: header (global id << 32 | len) at pos[i], payload words at woff[i]
+__global__ __launch_bounds__(RDF_BLOCK) void k_dict_pack(const u32* __restrict__ flags, const u32* __restrict__ pos, u32 nown,
+                                                         u32 base, const u64* __restrict__ own_off,
+                                                         const u32* __restrict__ own_len,
+                                                         const unsigned char* __restrict__ text, const u64* __restrict__ woff,
+                                                         u64* hdr, u64* payload) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < nown; i += (u64)gridDim.x * RDF_BLOCK) {
+        if (!flags[i]) continue;
+        const u32 j = pos[i], n = own_len[i];
+        hdr[j] = ((u64)(base + i) << 32) | n;
+        const u64 a = own_off[i], w0 = woff[i];
+        for (u32 w = 0; w < (n + 7) / 8; ++w) {
+            u64 x = 0;
+            for (u32 k = 0; k < 8 && 8 * w + k < n; ++k) x |= (u64)text[a + 8 * w + k] << (8 * k);
+            payload[w0 + w] = x;
+        }
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_dict_lengths(const u64* __restrict__ hdr, u64 m, u32* len, u32* words) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK) {
+        len[hdr[i] >> 32] = (u32)hdr[i];
+        words[i] = ((u32)hdr[i] + 7) / 8;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_dict_fill(const u64* __restrict__ hdr, u64 m, const u64* __restrict__ woff,
+                                                         const u64* __restrict__ payload, const u64* __restrict__ dtoff,
+                                                         char* heap) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 g = (u32)(hdr[i] >> 32), n = (u32)hdr[i];
+        const unsigned char* src = (const unsigned char*)(payload + woff[i]);
+        for (u32 k = 0; k < n; ++k) heap[dtoff[g] + k] = (char)src[k];
+    }
+}
+// terms of the given ids from the formatting dictionary: lengths, then bytes at the scanned offsets
+__global__ __launch_bounds__(RDF_BLOCK) void k_dict_term_len(const u32* __restrict__ ids, u64 n, const u64* __restrict__ dtoff,
+                                                             u32* len) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
+        len[i] = (u32)(dtoff[ids[i] + 1] - dtoff[ids[i]]);
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_dict_term_copy(const u32* __restrict__ ids, u64 n, const u64* __restrict__ dtoff,
+                                                              const char* __restrict__ heap, const u64* __restrict__ off,
+                                                              char* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 a = dtoff[ids[i]], m = dtoff[ids[i] + 1] - a;
+        for (u64 k = 0; k < m; ++k) out[off[i] + k] = heap[a + k];
+    }
+}
+
 // parsed dictionary -> the formatter's contiguous term heap (term i at heap[off[i], off[i+1]))
 __global__ __launch_bounds__(RDF_BLOCK) void k_nt_dict_gather(const unsigned char* __restrict__ text,
                                                               const u64* __restrict__ term_off,

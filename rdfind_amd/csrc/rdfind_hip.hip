@@ -126,6 +126,14 @@ struct rdf_ctx {
     DevBuf lmask, hrep, vpairs, vcoff, vpiv;  // holder-first light exchange (sh_phase5 / sh_phase15)
     DevBuf ebown, segb, sege, seglen;         // this rank's binary dependents' final pairs; dependent segments
     DevBuf ukeys, ukeys_tmp;                  // sharded: frequent unary keys (owned, then every rank's, sorted)
+    // sharded ingest (rdf_shard_parse_begin): local terms routed to their owners, the owner's dictionary, global ids
+    DevBuf ithv, ikeys, ikeys_tmp, iwords, iwoff, ihdr, ipay, ibnd, iwb, rhdr, rlen, rwords, rwoff, rts, rhv, rvalid, rtab,
+        rslot, rrep, rfirst, rfid, rhist, rreply, own_text, own_off, own_len, gmapv;
+    DevBuf dneed, dnpos, dwn, dwo, dhdr, dlen, dlwords, dwoff, tids, tlenv, toffv, tout;  // dictionary by owner lookup
+    bool ingest_sharded = false;              // the resident ids are global ids of a sharded ingest
+    u32 own_n = 0, own_base = 0;
+    u64 ing_Vl = 0, ing_m = 0;
+    std::vector<u64> ing_pay_counts, ing_src_counts;
     u64 sh_Eb = 0;
     u64 n_hrep = 0;
     u64 n_out = 0, n_runs = 0;
@@ -284,7 +292,10 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
             &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
-            &c->ukeys_tmp};
+            &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
+            &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
+            &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
+            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout};
 }
 
 extern "C" {
@@ -384,6 +395,7 @@ rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, con
     c->V = num_terms;
     c->stage = 1;
     c->parsed_dict = false;
+    c->ingest_sharded = false;
     return RDF_OK;
 }
 
@@ -399,6 +411,7 @@ rdf_status rdf_set_triples_device(rdf_ctx* c, const uint32_t* s, const uint32_t*
     c->V = num_terms;
     c->stage = 1;
     c->parsed_dict = false;
+    c->ingest_sharded = false;
     return RDF_OK;
 }
 
@@ -553,6 +566,7 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
     c->stage = 1;
     c->n_terms_parsed = V;
     c->parsed_dict = true;
+    c->ingest_sharded = false;
     if (n_triples) *n_triples = n;
     if (num_terms) *num_terms = (u32)V;
     return RDF_OK;
@@ -2828,12 +2842,261 @@ static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
     return RDF_OK;
 }
 
+// ---- sharded ingest (SURVEY.md 8f row 1 at -dop N; FLK/persistence/MultiFileTextInputFormat.java:49-100 splits the
+// input per task): every rank parses its own byte range into a local dictionary; each local term goes to the
+// rank owning its hash, which deduplicates the terms it receives (byte-verified) and assigns global ids; the ids go
+// back and the rank's triples are rewritten.  Global id = the owner's base (an exclusive scan of the owners' term
+// counts) + the term's rank among the owner's distinct terms in arrival order: deterministic for any thread count.
+
+// local terms -> owners: headers (hash, src << 58 | len << 32 | local id) to the owners (all-to-all)
+static rdf_status sh_phase20(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 V = c->ing_Vl;
+    const u32 R = c->sh_nranks;
+    const unsigned char* text = (const unsigned char*)c->ntext.p;
+    ENSURE(c, ithv, std::max<u64>(V, 1) * 8);
+    ENSURE(c, ikeys, std::max<u64>(V, 1) * 8);
+    ENSURE(c, ikeys_tmp, std::max<u64>(V, 1) * 8);
+    ENSURE(c, iwords, std::max<u64>(V, 1) * 4);
+    ENSURE(c, iwoff, (V + 1) * 8);
+    ENSURE(c, ibnd, (RDF_MAX_RANKS + 1) * 8);
+    ENSURE(c, iwb, (RDF_MAX_RANKS + 1) * 8);
+    if (V)
+        hipLaunchKernelGGL(k_term_route_keys, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, text,
+                           c->nterm_off.as<u64>(), c->nterm_len.as<u32>(), V, R, c->ithv.as<u64>(), c->ikeys.as<u64>());
+    {
+        u64* k = c->ikeys.as<u64>();
+        u64* t = c->ikeys_tmp.as<u64>();
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, V, 32 + bits_for(R), st));
+        if (k != c->ikeys.as<u64>()) std::swap(c->ikeys, c->ikeys_tmp);
+    }
+    if (V)
+        hipLaunchKernelGGL(k_term_words, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ikeys.as<u64>(), V,
+                           c->nterm_len.as<u32>(), c->iwords.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->iwords.as<u32>(), c->iwoff.as<u64>(), V, c->iwoff.as<u64>() + V, st));
+    hipLaunchKernelGGL(k_owner_bounds, dim3(1), dim3(RDF_BLOCK), 0, st, c->ikeys.as<u64>(), V, 16, R, c->ibnd.as<u64>());
+    hipLaunchKernelGGL(k_gather_u64_at, dim3(1), dim3(RDF_BLOCK), 0, st, c->iwoff.as<u64>(), c->ibnd.as<u64>(), R + 1,
+                       c->iwb.as<u64>());
+    std::vector<u64> bnd(R + 1), wb(R + 1);
+    HIP_TRY(c, hipMemcpyAsync(bnd.data(), c->ibnd.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(wb.data(), c->iwb.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    const u64 W = wb[R];
+    ENSURE(c, ihdr, std::max<u64>(2 * V, 1) * 8);
+    ENSURE(c, ipay, std::max<u64>(W, 1) * 8);
+    if (V)
+        hipLaunchKernelGGL(k_term_pack, dim3(grid_for(V, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, text, c->ikeys.as<u64>(), V,
+                           c->nterm_off.as<u64>(), c->nterm_len.as<u32>(), c->ithv.as<u64>(), c->iwoff.as<u64>(), c->sh_rank,
+                           c->ihdr.as<u64>(), c->ipay.as<u64>());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->ing_pay_counts.assign(R, 0);
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->ihdr.p, 2 * V, 21));
+    for (u32 r = 0; r < R; ++r) {
+        req->send_counts[r] = 2 * (bnd[r + 1] - bnd[r]);
+        c->ing_pay_counts[r] = wb[r + 1] - wb[r];
+    }
+    return RDF_OK;
+}
+
+// received headers -> kept; the payload words follow (all-to-all, same grouping)
+static rdf_status sh_phase21(rdf_ctx* c, rdf_exchange* req) {
+    const u64 n = c->x_recv_count;
+    ENSURE(c, rhdr, std::max<u64>(n, 1) * 8);
+    if (n) HIP_TRY(c, hipMemcpyAsync(c->rhdr.p, c->xrecv.p, n * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->ing_m = n / 2;
+    u64 W = 0;
+    for (u64 w : c->ing_pay_counts) W += w;
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->ipay.p, W, 22));
+    for (u32 r = 0; r < c->sh_nranks; ++r) req->send_counts[r] = c->ing_pay_counts[r];
+    return RDF_OK;
+}
+
+// owner: the received terms deduplicated (hash table of the parser, byte-verified), ids by first arrival; the count of
+// distinct owned terms -> all-gather
+static rdf_status sh_phase22(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 m = c->ing_m, W = c->x_recv_count;
+    if (m >= 0xffffffffull) return fail(c, RDF_ERR_LIMIT, "sharded ingest: too many terms at one owner");
+    ENSURE(c, own_text, W * 8 + 16);
+    if (W) HIP_TRY(c, hipMemcpyAsync(c->own_text.p, c->xrecv.p, W * 8, hipMemcpyDeviceToDevice, st));
+    ENSURE(c, rlen, std::max<u64>(m, 1) * 4);
+    ENSURE(c, rwords, std::max<u64>(m, 1) * 4);
+    ENSURE(c, rwoff, (m + 1) * 8);
+    ENSURE(c, rts, std::max<u64>(m, 1) * 8);
+    ENSURE(c, rhv, std::max<u64>(m, 1) * 8);
+    ENSURE(c, rhist, RDF_MAX_RANKS * 4);
+    const u64 nv = (m + 2) / 3;
+    ENSURE(c, rvalid, std::max<u64>(nv, 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->rhist.p, 0, RDF_MAX_RANKS * 4, st));
+    if (m)
+        hipLaunchKernelGGL(k_term_records, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->rhdr.as<u64>(), m,
+                           c->rwords.as<u32>(), c->rlen.as<u32>(), c->rhv.as<u64>(), c->rhist.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->rwords.as<u32>(), c->rwoff.as<u64>(), m, c->rwoff.as<u64>() + m, st));
+    if (m) {
+        hipLaunchKernelGGL(k_words_to_bytes, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->rwoff.as<u64>(), m,
+                           c->rts.as<u64>());
+        hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(nv, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->rvalid.as<u32>(), nv, 1u);
+    }
+    const u64 T = next_pow2(2 * std::max<u64>(m, 1));
+    ENSURE(c, rtab, T * 8);
+    ENSURE(c, rslot, std::max<u64>(m, 1) * 4);
+    ENSURE(c, rrep, std::max<u64>(m, 1) * 4);
+    ENSURE(c, rfirst, std::max<u64>(m, 1) * 4);
+    ENSURE(c, rfid, (m + 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->rtab.p, 0xff, T * 8, st));
+    const unsigned g = grid_for(std::max<u64>(m, 1), RDF_BLOCK, kGrid);
+    if (m) {
+        hipLaunchKernelGGL(k_nt_dict_insert, dim3(g), dim3(RDF_BLOCK), 0, st, (const unsigned char*)c->own_text.p,
+                           c->rts.as<u64>(), c->rlen.as<u32>(), c->rvalid.as<u32>(), m, c->rhv.as<u64>(), c->rtab.as<u64>(),
+                           T - 1, c->rslot.as<u32>());
+        hipLaunchKernelGGL(k_nt_dict_rep, dim3(g), dim3(RDF_BLOCK), 0, st, c->rvalid.as<u32>(), m, c->rslot.as<u32>(),
+                           c->rtab.as<u64>(), c->rrep.as<u32>(), c->rfirst.as<u32>());
+    }
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->rfirst.as<u32>(), c->rfid.as<u32>(), m, c->rfid.as<u32>() + m, st));
+    u32 nown = 0;
+    TRY(read_u32(c, c->rfid.as<u32>() + m, &nown));
+    c->own_n = nown;
+    c->ing_src_counts.assign(RDF_MAX_RANKS, 0);
+    std::vector<u32> hh(RDF_MAX_RANKS);
+    HIP_TRY(c, hipMemcpy(hh.data(), c->rhist.p, RDF_MAX_RANKS * 4, hipMemcpyDeviceToHost));
+    for (int r = 0; r < RDF_MAX_RANKS; ++r) c->ing_src_counts[r] = hh[r];
+    ENSURE(c, xsend, 8);
+    c->hscal[14] = nown;
+    HIP_TRY(c, hipMemcpy(c->xsend.p, c->hscal + 14, 8, hipMemcpyHostToDevice));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, 1, 23);
+}
+
+// owners' term counts -> bases; each received term's global id back to its sender (all-to-all)
+static rdf_status sh_phase23(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u32 R = c->sh_nranks;
+    if (c->x_recv_count != R) return fail(c, RDF_ERR_ARG, "term-count all-gather: wrong element count");
+    std::vector<u64> cnt(R);
+    HIP_TRY(c, hipMemcpy(cnt.data(), c->xrecv.p, R * 8, hipMemcpyDeviceToHost));
+    u64 base = 0, tot = 0;
+    for (u32 r = 0; r < R; ++r) {
+        if (r < c->sh_rank) base += cnt[r];
+        tot += cnt[r];
+    }
+    if (tot >= (1ull << 30)) return fail(c, RDF_ERR_LIMIT, "num_terms must be < 2^30");
+    c->own_base = (u32)base;
+    const u64 m = c->ing_m;
+    ENSURE(c, rreply, std::max<u64>(m, 1) * 8);
+    ENSURE(c, own_off, std::max<u64>(c->own_n, 1) * 8);
+    ENSURE(c, own_len, std::max<u64>(c->own_n, 1) * 4);
+    if (m)
+        hipLaunchKernelGGL(k_term_reply, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->rhdr.as<u64>(), m,
+                           c->rrep.as<u32>(), c->rfirst.as<u32>(), c->rfid.as<u32>(), (u32)base, c->rts.as<u64>(),
+                           c->rlen.as<u32>(), c->rreply.as<u64>(), c->own_off.as<u64>(), c->own_len.as<u32>());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->V = (u32)tot;
+    TRY(x_request(c, req, RDF_X_ALLTOALLV_U64, c->rreply.p, m, 24));
+    for (u32 r = 0; r < R; ++r) req->send_counts[r] = c->ing_src_counts[r];
+    return RDF_OK;
+}
+
+// every local term's global id -> the rank's triples rewritten in the global id space
+static rdf_status sh_phase24(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 m = c->x_recv_count, Vl = c->ing_Vl;
+    if (m != Vl) return fail(c, RDF_ERR_ARG, "sharded ingest: a local term got no global id");
+    ENSURE(c, gmapv, std::max<u64>(Vl, 1) * 4);
+    if (m)
+        hipLaunchKernelGGL(k_term_gmap, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->xrecv.as<u64>(), m,
+                           c->gmapv.as<u32>());
+    if (c->n)
+        hipLaunchKernelGGL(k_remap3, dim3(grid_for(c->n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ts.as<u32>(),
+                           c->tp.as<u32>(), c->to.as<u32>(), c->n, c->gmapv.as<u32>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->parsed_dict = false;
+    c->ingest_sharded = true;
+    c->stage = 1;
+    memset(req, 0, sizeof(*req));
+    req->op = RDF_X_DONE;
+    c->sh_phase = 9;
+    return RDF_OK;
+}
+
+// ---- formatting dictionary by owner lookup: the values of the frequent conditions (the only terms an output line
+// can name) from their owners to every rank (two all-gathers: headers, then the bytes)
+static rdf_status sh_phase30(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u32 nown = c->own_n;
+    ENSURE(c, dneed, std::max<u64>(nown, 1) * 4);
+    ENSURE(c, dnpos, (nown + 1ull) * 4);
+    ENSURE(c, dwn, std::max<u64>(nown, 1) * 4);
+    ENSURE(c, dwo, (nown + 1ull) * 8);
+    HIP_TRY(c, hipMemsetAsync(c->dneed.p, 0, std::max<u64>(nown, 1) * 4, st));
+    if ((u64)c->U + c->B)
+        hipLaunchKernelGGL(k_mark_needed, dim3(grid_for((u64)c->U + c->B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->fval.as<u32>(), (u64)c->U, c->bkeys.as<u64>(), c->B, c->own_base, nown, c->dneed.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->dneed.as<u32>(), c->dnpos.as<u32>(), nown, c->dnpos.as<u32>() + nown, st));
+    if (nown)
+        hipLaunchKernelGGL(k_needed_words, dim3(grid_for(nown, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->dneed.as<u32>(),
+                           c->own_len.as<u32>(), nown, c->dwn.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->dwn.as<u32>(), c->dwo.as<u64>(), nown, c->dwo.as<u64>() + nown, st));
+    u64 v[2];
+    TRY(read_multi(c, {{c->dnpos.as<u32>() + nown, 4}, {c->dwo.as<u64>() + nown, 8}}, v));
+    const u64 nneed = v[0], W = v[1];
+    ENSURE(c, ihdr, std::max<u64>(nneed, 1) * 8);
+    ENSURE(c, ipay, std::max<u64>(W, 1) * 8);
+    if (nown)
+        hipLaunchKernelGGL(k_dict_pack, dim3(grid_for(nown, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->dneed.as<u32>(),
+                           c->dnpos.as<u32>(), nown, c->own_base, c->own_off.as<u64>(), c->own_len.as<u32>(),
+                           (const unsigned char*)c->own_text.p, c->dwo.as<u64>(), c->ihdr.as<u64>(), c->ipay.as<u64>());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->ing_pay_counts.assign(1, W);
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ihdr.p, nneed, 31);
+}
+
+static rdf_status sh_phase31(rdf_ctx* c, rdf_exchange* req) {
+    const u64 M = c->x_recv_count;
+    ENSURE(c, dhdr, std::max<u64>(M, 1) * 8);
+    if (M) HIP_TRY(c, hipMemcpyAsync(c->dhdr.p, c->xrecv.p, M * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->ing_m = M;
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ipay.p, c->ing_pay_counts[0], 32);
+}
+
+static rdf_status sh_phase32(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
+    const u64 M = c->ing_m, V = c->V;
+    ENSURE(c, dlen, std::max<u64>(V, 1) * 4);
+    ENSURE(c, dlwords, std::max<u64>(M, 1) * 4);
+    ENSURE(c, dwoff, (M + 1) * 8);
+    ENSURE(c, dtoff, (V + 1) * 8);
+    HIP_TRY(c, hipMemsetAsync(c->dlen.p, 0, std::max<u64>(V, 1) * 4, st));
+    if (M)
+        hipLaunchKernelGGL(k_dict_lengths, dim3(grid_for(M, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->dhdr.as<u64>(), M,
+                           c->dlen.as<u32>(), c->dlwords.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->dlwords.as<u32>(), c->dwoff.as<u64>(), M, c->dwoff.as<u64>() + M, st));
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->dlen.as<u32>(), c->dtoff.as<u64>(), V, c->dtoff.as<u64>() + V, st));
+    u64 heap = 0;
+    TRY(read_u64(c, c->dtoff.as<u64>() + V, &heap));
+    ENSURE(c, dheap, std::max<u64>(heap, 1));
+    if (M)
+        hipLaunchKernelGGL(k_dict_fill, dim3(grid_for(M, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->dhdr.as<u64>(), M,
+                           c->dwoff.as<u64>(), c->xrecv.as<u64>(), c->dtoff.as<u64>(), c->dheap.as<char>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->dict_terms = V;
+    c->capstr_run = ~0ull;
+    memset(req, 0, sizeof(*req));
+    req->op = RDF_X_DONE;
+    c->sh_phase = 9;
+    return RDF_OK;
+}
+
 // phases: 10, 16, 11-14 (condition counts, routing of the triples), then 1-8 (15 between 5 and 6); pending = a
 // phase that follows a collective
 static bool sh_phase_valid(int ph, bool pending) {
     if (ph >= 1 && ph <= 8) return true;
     if (ph >= 11 && ph <= 17) return true;
-    return !pending && ph == 10;
+    if (ph >= 21 && ph <= 24) return true;
+    if (ph >= 31 && ph <= 32) return true;
+    return !pending && (ph == 10 || ph == 20 || ph == 30);
 }
 
 rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t min_support, const char* projection,
@@ -2855,6 +3118,66 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     return RDF_OK;
 }
 
+rdf_status rdf_shard_parse_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, const char* text, uint64_t nbytes,
+                                 uint32_t flags, uint64_t* n_triples) {
+    if (!c) return RDF_ERR_ARG;
+    if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
+    uint64_t n = 0;
+    u32 Vl = 0;
+    TRY(rdf_parse_ntriples(c, text, nbytes, flags, &n, &Vl, nullptr));
+    c->ing_Vl = Vl;
+    c->ingest_sharded = false;
+    c->sh_rank = rank;
+    c->sh_nranks = nranks;
+    c->sh_phase = 20;
+    c->x_imported = true;
+    c->stage = 0;  // no usable triples until the global ids arrive
+    if (n_triples) *n_triples = n;
+    return RDF_OK;
+}
+
+rdf_status rdf_shard_dictionary_begin(rdf_ctx* c) {
+    if (!c) return RDF_ERR_ARG;
+    if (!c->ingest_sharded) return fail(c, RDF_ERR_STATE, "the triples do not come from rdf_shard_parse_begin");
+    if (c->stage < 2) return fail(c, RDF_ERR_STATE, "a (sharded) run must come first: the frequent conditions name the terms");
+    c->sh_phase = 30;
+    c->x_imported = true;
+    return RDF_OK;
+}
+
+rdf_status rdf_num_terms(rdf_ctx* c, uint32_t* n) {
+    if (!c || !n) return RDF_ERR_ARG;
+    *n = c->V;
+    return RDF_OK;
+}
+
+// terms of ids[0, n) from the formatting dictionary: offsets[n + 1] and their bytes (cap bytes; RDF_ERR_ARG if short)
+rdf_status rdf_dictionary_terms(rdf_ctx* c, const uint32_t* ids, uint64_t n, char* out, uint64_t cap, uint64_t* offsets) {
+    if (!c || (n && (!ids || !offsets))) return RDF_ERR_ARG;
+    if (c->dict_terms < c->V) return fail(c, RDF_ERR_STATE, "no formatting dictionary covers the term ids");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    ENSURE(c, tids, std::max<u64>(n, 1) * 4);
+    ENSURE(c, tlenv, std::max<u64>(n, 1) * 4);
+    ENSURE(c, toffv, (n + 1) * 8);
+    if (n) HIP_TRY(c, hipMemcpyAsync(c->tids.p, ids, n * 4, hipMemcpyHostToDevice, st));
+    if (n)
+        hipLaunchKernelGGL(k_dict_term_len, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->tids.as<u32>(), n,
+                           c->dtoff.as<u64>(), c->tlenv.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->tlenv.as<u32>(), c->toffv.as<u64>(), n, c->toffv.as<u64>() + n, st));
+    HIP_TRY(c, hipMemcpyAsync(offsets, c->toffv.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    const u64 total = offsets[n];
+    if (total > cap) return fail(c, RDF_ERR_ARG, "term buffer too small (see offsets[n])");
+    ENSURE(c, tout, std::max<u64>(total, 1));
+    if (n)
+        hipLaunchKernelGGL(k_dict_term_copy, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->tids.as<u32>(), n,
+                           c->dtoff.as<u64>(), c->dheap.as<char>(), c->toffv.as<u64>(), c->tout.as<char>());
+    if (total) HIP_TRY(c, hipMemcpyAsync(out, c->tout.p, total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return RDF_OK;
+}
+
 rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
     if (!c || !req) return RDF_ERR_ARG;
     if (!sh_phase_valid(c->sh_phase, false)) return fail(c, RDF_ERR_STATE, "rdf_shard_begin must be called first");
@@ -2870,6 +3193,14 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
         case 15: r = sh_phase15(c, req); break;
         case 16: r = sh_phase16(c, req); break;
         case 17: r = sh_phase17(c, req); break;
+        case 20: r = sh_phase20(c, req); break;
+        case 21: r = sh_phase21(c, req); break;
+        case 22: r = sh_phase22(c, req); break;
+        case 23: r = sh_phase23(c, req); break;
+        case 24: r = sh_phase24(c, req); break;
+        case 30: r = sh_phase30(c, req); break;
+        case 31: r = sh_phase31(c, req); break;
+        case 32: r = sh_phase32(c, req); break;
         case 6: r = sh_phase6(c, req); break;
         case 7: r = sh_phase7(c, req); break;
         case 8: r = sh_phase8(c, req); break;

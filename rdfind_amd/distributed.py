@@ -141,3 +141,20 @@ def run_sharded(ctx, min_support: int, projection="spo", clean_implied=True, tra
     ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy, local_slice, use_ars)
     run_protocol(ctx, group, device)
     return ctx.last_stats()
+
+
+def run_ingest(ctx, data: bytes, tabs=False, group=None, device=None) -> int:
+    """Sharded ingest (rdf_shard_parse_begin): this rank parses ``data`` (its part of the input), the dictionary
+    exchange assigns global term ids, and the rank's triples become its slice in that id space.  Returns the rank's
+    triple count; ``ctx.num_terms`` is the global dictionary size."""
+    n = ctx.shard_parse_begin(dist.get_rank(group), dist.get_world_size(group), data, tabs)
+    run_protocol(ctx, group, device)
+    ctx.num_terms_now()
+    return n
+
+
+def run_dictionary(ctx, group=None, device=None):
+    """After a sharded run on sharded-ingest triples: the formatting dictionary of every term an output line can name,
+    gathered from the terms' owners (rdf_shard_dictionary_begin)."""
+    ctx.shard_dictionary_begin()
+    run_protocol(ctx, group, device)

@@ -283,6 +283,75 @@ def read_bytes(paths) -> bytes:
     return b"".join(parts)
 
 
+def _plain_path(path):
+    if path.startswith("file:"):
+        path = path[5:]
+        while path.startswith("//"):
+            path = path[1:]
+    return path
+
+
+def read_byte_range(paths, rank: int, nranks: int) -> bytes:
+    """This rank's part of the input for the sharded ingest: the bytes of the whole lines that start in
+    [T * rank / nranks, T * (rank + 1) / nranks) of the concatenated input of T bytes (read_bytes' stream: a line
+    break after a file without one).  A line belongs to the rank its first byte falls to, so the parts partition the
+    lines (the reference's input splits, FLK/persistence/MultiFileTextInputFormat.java:49-100).  Plain files are
+    read by seeking to the range; a .gz file cannot be split and is decompressed whole, keeping only the range."""
+    files = []  # (path, size of its stream part, gz)
+    for path in paths:
+        path = _plain_path(path)
+        if path.endswith(".gz"):
+            with gzip.open(path, "rb") as f:
+                data = f.read()
+            if data and not data.endswith(b"\n"):
+                data += b"\n"
+            files.append((path, len(data), data))
+        else:
+            size = os.path.getsize(path)
+            with open(path, "rb") as f:
+                if size:
+                    f.seek(size - 1)
+                    last = f.read(1)
+                else:
+                    last = b"\n"
+            files.append((path, size + (0 if last == b"\n" else 1), None))
+    total = sum(sz for _, sz, _ in files)
+    lo, hi = total * rank // nranks, total * (rank + 1) // nranks
+
+    def read(a, b):  # stream bytes [a, b)
+        out, base = [], 0
+        for path, sz, data in files:
+            s0, s1 = max(a, base), min(b, base + sz)
+            if s0 < s1:
+                if data is not None:
+                    out.append(data[s0 - base:s1 - base])
+                else:
+                    with open(path, "rb") as f:
+                        f.seek(s0 - base)
+                        chunk = f.read(s1 - s0)
+                    if len(chunk) < s1 - s0:  # the virtual line break after a file without one
+                        chunk += b"\n"
+                    out.append(chunk)
+            base += sz
+        return b"".join(out)
+
+    def line_start_at_or_after(x):  # first line start >= x (a line starts at 0 or right after a "\n")
+        if x <= 0:
+            return 0
+        pos = x - 1
+        step = 1 << 16
+        while pos < total:
+            chunk = read(pos, min(pos + step, total))
+            k = chunk.find(b"\n")
+            if k >= 0:
+                return pos + k + 1
+            pos += len(chunk)
+        return total
+
+    b0, b1 = line_start_at_or_after(lo), line_start_at_or_after(hi)
+    return read(b0, b1) if b0 < b1 else b""
+
+
 class HeapDictionary:
     """Term id -> string over a (heap, offsets) pair, e.g. the device dictionary of rdf_parse_ntriples."""
 

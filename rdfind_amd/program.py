@@ -131,6 +131,8 @@ class RDFind:
         paths = ntriples.resolve_paths(a.inputs)
         if not paths:
             raise ValueError("no input files")
+        if world > 1 and not (a.host_parser or a.prefixes or a.distinct_triples or a.only_read):
+            return self.run_sharded_ingest(paths, device, t0, out)
         with _lib.Context(device) as ctx:
             if a.host_parser:  # host tokenizer + dictionary (rdfind_amd/ntriples.py)
                 s, p, o, dic = ntriples.read_triples(paths, tabs=a.tabs)
@@ -191,7 +193,40 @@ class RDFind:
             cs = ctx.discover_cinds(clean_implied=a.clean_implied, traversal_strategy=a.traversal_strategy)
             return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
 
-    def write_output(self, ctx, dic, stats, t1, out):
+    def run_sharded_ingest(self, paths, device, t0, out):
+        """-dop N with the input split over the ranks: each rank parses only its part of the bytes, the global
+        dictionary is built by the terms' owner ranks (distributed.run_ingest), the rank keeps only its triples
+        (RDF_SHARD_LOCAL_SLICE), and the formatter gets the terms it needs from their owners (run_dictionary).
+        --prefixes, --distinct-triples and --host-parser keep the replicated parse (a shared host dictionary)."""
+        from . import distributed
+        a = self.args
+        with _lib.Context(device) as ctx:
+            data = ntriples.read_byte_range(paths, self.rank, self.world)
+            self.bytes_parsed = len(data)
+            n_in = distributed.run_ingest(ctx, data, a.tabs)
+            del data
+            ctx._parsed = None
+            if a.debug_level >= 1:
+                self.log(f"rank {self.rank}: {n_in} triples of {self.bytes_parsed} bytes, {ctx.num_terms} terms in all.")
+            self.timings["read"] = time.time() - t0
+            t1 = time.time()
+            if a.ar_output:  # rules from the combined counts; their terms by owner lookup; rank 0 writes them
+                distributed.run_sharded(ctx, a.support, a.projection, a.clean_implied, a.traversal_strategy,
+                                        local_slice=True, use_ars=True)
+                distributed.run_dictionary(ctx)
+                if self.rank == 0:
+                    rules = ctx.copy_association_rules()
+                    ids = np.unique(np.concatenate([rules["antecedent"], rules["consequent"]])) if len(rules) else []
+                    names = dict(zip((int(i) for i in ids), ctx.dictionary_terms(ids))) if len(ids) else {}
+                    self.write_rules(a.ar_output, format_rules(rules, names.__getitem__))
+            if not (a.ar_output and a.use_ars):
+                distributed.run_sharded(ctx, a.support, a.projection, a.clean_implied, a.traversal_strategy,
+                                        local_slice=True, use_ars=a.use_ars)
+                distributed.run_dictionary(ctx)
+            return self.write_output(ctx, None, {"fc": ctx.fc, "groups": ctx.groups, "cinds": ctx.cinds}, t1, out,
+                                     dictionary_ready=True)
+
+    def write_output(self, ctx, dic, stats, t1, out, dictionary_ready=False):
         """Cind.toString lines formatted on the GPU (rdf_format_cinds) in chunks of rows, to --output and/or the
         returned list.  With -dop > 1 every rank writes its own CINDs to a part file and rank 0 concatenates them
         into the one output file (the reference writes file:// outputs with parallelism 1, RDFind.scala:507-520)."""
@@ -202,7 +237,9 @@ class RDFind:
         self.stats = stats
         t2 = time.time()
         n = ctx.cind_count()
-        if dic is None:
+        if dictionary_ready:
+            pass  # the sharded ingest's dictionary by owner lookup (distributed.run_dictionary)
+        elif dic is None:
             ctx.set_dictionary_parsed()  # device dictionary straight into the formatter
         else:
             ctx.set_dictionary(dic.terms)

@@ -203,11 +203,18 @@ def test_program_dop2_reproduces_golden(tmp_path, name, mode, flags):
     env = dict(os.environ, RDFIND_DIST_BACKEND="gloo")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "rdfind_amd", "-dop", "2", *flags, "--support", str(ms), "--output",
-                        f"file://{out}", os.path.join(GOLDEN, f"{name}.nt.gz")], cwd=root, env=env,
+                        f"file://{out}", "--debug-level", "1", os.path.join(GOLDEN, f"{name}.nt.gz")], cwd=root, env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     assert sorted(out.read_text().splitlines()) == expected
     assert not list(tmp_path.glob("cinds.txt.part*"))
+    # sharded ingest: each rank parsed its own part of the bytes, about half (the parts partition the input)
+    import gzip
+    import re
+    total = len(gzip.open(os.path.join(GOLDEN, f"{name}.nt.gz")).read())
+    got = {int(m.group(1)): int(m.group(3)) for m in re.finditer(r"rank (\d+): (\d+) triples of (\d+) bytes", r.stderr)}
+    assert sorted(got) == [0, 1] and sum(got.values()) in (total, total + 1), (got, total)
+    assert all(abs(b - total / 2) < total / 4 for b in got.values()), got
 
 
 @pytest.mark.parametrize("local_slice", [False, True])

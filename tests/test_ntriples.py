@@ -96,3 +96,21 @@ def test_prefixes_and_distinct_flags_accepted():
     from rdfind_amd import program
     prog = program.RDFind(["--use-fis", "--prefixes", "a.nt,b.nt", "--prefixes", "c.nt", "--distinct-triples", "x.nt"])
     assert prog.args.prefixes == ["a.nt,b.nt", "c.nt"] and prog.args.distinct_triples
+
+
+def test_read_byte_range_partitions_lines(tmp_path):
+    """The sharded ingest's byte ranges (read_byte_range): the ranks' parts are whole lines and concatenate to the
+    input stream (plain files seeked, .gz files decompressed, a line break after a file without one)."""
+    import gzip
+
+    a, b, c = tmp_path / "a.nt", tmp_path / "b.nt.gz", tmp_path / "c.nt"
+    a.write_bytes(b"".join(b"<s%d> <p> <o%d> .\n" % (i, i) for i in range(100)))
+    with gzip.open(b, "wb") as f:
+        f.write(b"".join(b'<x%d> <p> "l%d" .\n' % (i, i) for i in range(57)) + b"<last> <p> <o> .")
+    c.write_bytes(b"<c1> <p> <o> .\n<c2> <p> <o> .")
+    paths = [str(a), str(b), str(c)]
+    full = ntriples.read_bytes(paths)
+    for nranks in (1, 2, 3, 5, 8, 64):
+        parts = [ntriples.read_byte_range(paths, r, nranks) for r in range(nranks)]
+        assert b"".join(parts) == full, nranks
+        assert all(not p or p.endswith(b"\n") for p in parts)
