@@ -1677,6 +1677,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_write(u64 nvblk, CindView v
 // and each dependent's output is L'(m) minus itself: a streaming copy bound by the HBM write rate.
 
 // masks of the heavy-only dependents [0, cmax): cmax = Cu (unary only) or C (binary ones classed too)
+// slot of mask m in the class table (bounded probe: a mask that is not there gives ~0 instead of a spinning wave)
+__device__ inline u64 class_slot(const u64* __restrict__ tkeys, u64 tmask, u64 m) {
+    u64 h = mix64(m) & tmask;
+    for (u64 probe = 0; probe <= tmask; ++probe, h = (h + 1) & tmask) {
+        const u64 k = tkeys[h];
+        if (k == m) return h;
+        if (k == 0) return ~0ull;
+    }
+    return ~0ull;
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_insert(CindView v, u32 cmax, u64* tkeys, u64 tmask, u64* nmembers) {
     u32 cnt = 0;
     const u64 n_round = ((u64)cmax + RDF_WAVE - 1) / RDF_WAVE * RDF_WAVE;
@@ -1713,11 +1724,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_keys(CindView v, const u64*
         u32 want = 0;
         u64 key = 0;
         if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY) && (u32)d % nranks == rank) {
-            const u64 m = v.info[d].hmask;
-            u64 h = mix64(m) & tmask;
-            while (tkeys[h] != m) h = (h + 1) & tmask;
-            key = ((u64)cid[h] << 32) | d;
-            want = 1;
+            const u64 h = class_slot(tkeys, tmask, v.info[d].hmask);
+            if (h != ~0ull) {
+                key = ((u64)cid[h] << 32) | d;
+                want = 1;
+            }
         }
         u64 pos = wave_append(counter, want);
         if (want) out[pos] = key;
@@ -1731,13 +1742,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_of(CindView v, const u64* _
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         u32 m = NONE32;
         if (v.info[d].meta & META_HEAVY_ONLY) {
-            const u64 mk = v.info[d].hmask;
-            u64 h = mix64(mk) & tmask;
-            while (tkeys[h] != mk) h = (h + 1) & tmask;
-            m = cid[h];
-            // any member represents its class (same groups, same pivot): a plain store once the slot is seen
-            // taken is skipped (thousands of members per class would otherwise serialise on one address)
-            if (crep[m] == NONE32) crep[m] = (u32)d;
+            const u64 h = class_slot(tkeys, tmask, v.info[d].hmask);
+            if (h != ~0ull) {
+                m = cid[h];
+                // any member represents its class (same groups, same pivot): a plain store once the slot is seen
+                // taken is skipped (thousands of members per class would otherwise serialise on one address)
+                if (crep[m] == NONE32) crep[m] = (u32)d;
+            }
         }
         if (d >= v.Cu) dcls[d - v.Cu] = m;
     }
@@ -2358,10 +2369,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_compact_u64(const u64* __restrict
 __global__ __launch_bounds__(RDF_BLOCK) void k_class_rank(const u64* __restrict__ tkeys, u64 tmask,
                                                           const u64* __restrict__ smask, u32 ncls, u32* cid) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < ncls; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 m = smask[i];
-        u64 h = mix64(m) & tmask;
-        while (tkeys[h] != m) h = (h + 1) & tmask;
-        cid[h] = (u32)i;
+        const u64 h = class_slot(tkeys, tmask, smask[i]);
+        if (h != ~0ull) cid[h] = (u32)i;
     }
 }
 
@@ -2381,9 +2390,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_pivot_shard(CindView v, con
                                                                  u32* cnch) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.Cu; d += (u64)gridDim.x * RDF_BLOCK) {
         if (!(v.info[d].meta & META_HEAVY_ONLY) || (u32)gbest[d] != rank) continue;
-        const u64 m = v.info[d].hmask;
-        u64 h = mix64(m) & tmask;
-        while (tkeys[h] != m) h = (h + 1) & tmask;
+        const u64 h = class_slot(tkeys, tmask, v.info[d].hmask);
+        if (h == ~0ull) continue;
         const u32 c = cid[h];
         const u32 g = pivot[d];  // members of a class have the same groups, hence the same pivot
         cpiv[c] = g;

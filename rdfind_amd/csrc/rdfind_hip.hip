@@ -2751,7 +2751,7 @@ static rdf_status sh_phase7(rdf_ctx* c, rdf_exchange* req) {
     ENSURE(c, ckeys, std::max<u64>(nmem_all, 1) * 8);
     ENSURE(c, ckeys_tmp, std::max<u64>(nmem_all, 1) * 8);
     HIP_TRY(c, hipMemsetAsync(dscal(c, 4), 0, 8, st));
-    if (c->Cu)
+    if (c->Cu && ncls)  // (--use-ars: no classes, every heavy-only dependent takes the heavy path)
         hipLaunchKernelGGL(k_class_keys, dim3(grid_for(c->Cu, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->ctab.as<u64>(),
                            c->ccid.as<u32>(), tcapc - 1, c->rank, c->nranks, c->ckeys.as<u64>(), dscal(c, 4));
     u64 nmem = 0;

@@ -45,6 +45,9 @@ for step in "$@"; do
       python3 tools/trace_step.py gpurun_out/qprof_$TAG/run_kernel_trace.csv | awk '$2 > 40 || /total/' ;;
     pmc)
       tools/pmc.sh $TAG || exit 1 ;;
+    pmc:*)  # pmc:<config>:<scale> -- the PMC passes on another BASELINE shape
+      IFS=: read -r _ CFG SC <<< "$step"
+      tools/pmc.sh ${TAG}_$CFG --config $CFG --scale $SC || exit 1 ;;
     lstats)
       timeout -k 10 300 python -u tools/light_stats.py c2 1.0 > gpurun_out/lstats_$TAG.log 2>&1 \
         || { echo "lstats failed"; tail -30 gpurun_out/lstats_$TAG.log; exit 1; }
