@@ -133,4 +133,5 @@ def test_ars_state_and_errors(ctx):
     tr = [tuple(x) for x in arr.tolist()]
     assert _lib.decoded_to_set(ctx.decoded_cinds()) == R.cind_set(R.rdfind(tr, 1, 1, True))
     with pytest.raises(_lib.RdfError):
-        ctx.shard_begin(0, 1, 1, use_ars=True)
+        ctx.shard_begin(2, 2, 1, use_ars=True)  # rank outside [0, nranks)
+    ctx.shard_begin(0, 1, 1, use_ars=True)  # sharded rules are supported
