@@ -2144,6 +2144,41 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_checksum(const u32* __restrict__ 
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, RDF_WAVE);
     if (lane_id() == 0 && acc) atomicAdd(sum, acc);
 }
+
+// checksum of the class part straight from the compact form (members x shared lists, self excluded), so a
+// checksum never needs the expanded rows: same tiles as k_class_emit, list segment staged in LDS once per tile
+__global__ __launch_bounds__(RDF_BLOCK) void k_class_checksum(u64 nvblk, const u64* __restrict__ coff,
+                                                              const u64* __restrict__ cchoff, const u64* __restrict__ lwoff,
+                                                              const u32* __restrict__ lists, const u64* __restrict__ toff,
+                                                              u32 ncls, const u64* __restrict__ ckeys,
+                                                              const u32* __restrict__ fcap, const u32* __restrict__ csup,
+                                                              u64* sum) {
+    __shared__ u32 sl[CLS_LS];
+    __shared__ u32 s_m;
+    u64 acc = 0;
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_m = find_dep(toff, ncls, vb);
+        __syncthreads();
+        const u32 m = s_m;
+        const u64 lb = lwoff[cchoff[m]], len = lwoff[cchoff[m + 1]] - lb;
+        const u64 nseg = (len + CLS_LS - 1) / CLS_LS;
+        const u64 t = vb - toff[m];
+        const u64 dt = t / nseg, seg = t % nseg;
+        const u64 k0 = coff[m] + dt * CLS_DT, k1 = k0 + CLS_DT < coff[m + 1] ? k0 + CLS_DT : coff[m + 1];
+        const u64 p0 = seg * CLS_LS, p1 = p0 + CLS_LS < len ? p0 + CLS_LS : len;
+        for (u64 i = threadIdx.x; i < p1 - p0; i += RDF_BLOCK) sl[i] = fcap[lists[lb + p0 + i]];
+        __syncthreads();
+        for (u64 k = k0; k < k1; ++k) {
+            const u32 d = (u32)ckeys[k], de = fcap[d], sup = csup[d];
+            for (u64 i = threadIdx.x; i < p1 - p0; i += RDF_BLOCK)
+                if (sl[i] != de) acc += row_hash(de, sl[i], sup);  // fcap is injective: the self entry only
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, RDF_WAVE);
+    if (lane_id() == 0 && acc) atomicAdd(sum, acc);
+}
 // Cind-shaped rows (ALG/data/Cind.scala:12-15) of output elements [first, first + n): capture code and condition
 // values of dependent and referenced capture (value2 = NONE for unary captures) plus the support.
 __device__ inline void decode_capture(u32 ext, u32 V, const u64* __restrict__ bkeys, u32* code, u32* v1, u32* v2) {

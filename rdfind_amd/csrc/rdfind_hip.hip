@@ -3446,12 +3446,19 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     if (!c || !checksum) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
-    TRY(materialize(c));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 7), 0, 8, c->stream));
-    if (c->n_out)
-        hipLaunchKernelGGL(k_checksum, dim3(grid_for(c->n_out, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
-                           c->out_ptr, c->n_out, c->runoff.as<u64>(), c->rundep.as<u32>(), c->n_runs, c->fext.as<u32>(),
+    // a pending class part is summed from the compact form (no expansion: 4 B per row of HBM it would need)
+    const u64 nrows = c->class_pending ? c->n_out - c->n_class_out : c->n_out;
+    if (nrows)
+        hipLaunchKernelGGL(k_checksum, dim3(grid_for(nrows, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
+                           c->out_ptr, nrows, c->runoff.as<u64>(), c->rundep.as<u32>(), c->n_runs, c->fext.as<u32>(),
                            c->csup.as<u32>(), dscal(c, 7));
+    if (c->class_pending && c->pend_NT)
+        hipLaunchKernelGGL(k_class_checksum, dim3(vgrid(c->pend_NT)), dim3(RDF_BLOCK), 0, c->stream, c->pend_NT,
+                           c->coff.as<u64>(), c->cchoff.as<u64>(), c->lwoff.as<u64>(), c->clists.as<u32>(),
+                           c->ctoff.as<u64>(), (u32)c->n_classes, c->ckeys.as<u64>(), c->fext.as<u32>(),
+                           c->csup.as<u32>(), dscal(c, 7));
+    HIP_TRY(c, hipGetLastError());
     u64 v = 0;
     rdf_status rs = read_u64(c, dscal(c, 7), &v);
     *checksum = v;
