@@ -191,6 +191,8 @@ def main():
                     help="time the CPU baseline on the benchmarked workload itself up to this many triples")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
                     "exchanges, to rehearse several ranks on one GPU)")
+    ap.add_argument("--no-resident", action="store_true", help="skip the device-resident repeat of the steps")
+    ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
     ap.add_argument("--page-bytes", type=int, default=None,
                     help="paged discovery (rdf_discover_cinds_paged) with this working memory per page, 0 = a quarter "
                          "of the free HBM; every page is handed over in turn.  Default: unpaged, except c5 beyond "
@@ -242,10 +244,12 @@ def main():
             ctx.frequent_conditions(ms)
             ctx.build_capture_groups("spo")
             n = 0
-            for _ in ctx.pages(True, 1, args.page_bytes or 0):
+            for i, _ in enumerate(ctx.pages(True, 1, args.page_bytes or 0)):
                 n += ctx.cind_count()
                 if hand_over:
                     sink.copy(ctx)
+                if args.page_log:
+                    print(f"page {i}: {n} CINDs so far", file=sys.stderr, flush=True)
             _, cs = ctx.last_stats()
             return dict(cs, n_cinds=n, pages=ctx_pages(ctx))
     else:
@@ -288,13 +292,15 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0)
     L = ctx.result_layout()
     # the same steps without the hand-over (results left in HBM): the device-resident rate
-    barrier()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        discover(False)
-    ctx.sync()
-    barrier()
-    elapsed_dev = max_over_ranks(time.perf_counter() - t1)
+    elapsed_dev = None
+    if not args.no_resident:
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            discover(False)
+        ctx.sync()
+        barrier()
+        elapsed_dev = max_over_ranks(time.perf_counter() - t1)
     if dist is not None:
         import torch
         dev = f"cuda:{local_rank}" if args.backend == "nccl" else "cpu"
@@ -397,7 +403,8 @@ def main():
                     (" (paged: every page handed over in turn)" if paged else ""),
             "handover": {"bytes_all_ranks": total_bytes, "pinned": sink.pinned, "n_refs": L["n_refs"],
                          "n_list_refs": L["n_list_refs"], "n_members": L["n_members"], "n_runs": L["n_runs"]},
-            "device_resident": {"ms_per_step": round(elapsed_dev * 1000.0 / steps, 3),
+            "device_resident": None if elapsed_dev is None else
+                               {"ms_per_step": round(elapsed_dev * 1000.0 / steps, 3),
                                 "triples_per_s": round(float(total_n) * steps / elapsed_dev, 1),
                                 "note": "the same steps with the result left in HBM"},
             "roofline": roof, "count_kernels": count_roof, "families": fams,

@@ -75,6 +75,11 @@ __device__ inline u32 bucket_slot(u32* lh, u32 bk, bool active) {
 
 // ---- K1 ----------------------------------------------------------------------------------------
 
+#ifndef RDF_PART_U
+#define RDF_PART_U 4
+#endif
+static constexpr int PART_U = RDF_PART_U;  // triples per thread whose loads are in flight together (partition passes)
+
 template <bool SCATTER>
 __global__ __launch_bounds__(RDF_BLOCK) void k_u2_part(const u32* __restrict__ s, const u32* __restrict__ p,
                                                        const u32* __restrict__ o, u64 n, u32 V, u32 NB, int bits,
@@ -85,14 +90,26 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_u2_part(const u32* __restrict__ s
     const u64 per = (n + gridDim.x - 1) / gridDim.x;
     const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
     const u64 lmask = (1ull << bits) - 1;
-    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
-        const u64 i = i0 + threadIdx.x;
-        const bool act = i < e;
-        const u64 key[3] = {act ? (u64)s[i] : 0, act ? (u64)V + p[i] : 0, act ? 2ull * V + o[i] : 0};
+    // PART_U rows per thread loaded before any is used: the chunk is read with PART_U x 3 loads in flight per lane
+    // instead of one round trip per 256 rows (the slot reservations below are LDS work)
+    for (u64 i0 = b; i0 < e; i0 += (u64)RDF_BLOCK * PART_U) {
+        u32 ts[PART_U], tp[PART_U], to[PART_U];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const u32 pos = bucket_slot(lh, (u32)(key[t] >> bits), act);
-            if (SCATTER && act) recs[pos] = (uint16_t)(key[t] & lmask);
+        for (int u = 0; u < PART_U; ++u) {
+            const u64 i = i0 + (u64)u * RDF_BLOCK + threadIdx.x;
+            ts[u] = i < e ? s[i] : 0u;
+            tp[u] = i < e ? p[i] : 0u;
+            to[u] = i < e ? o[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            const bool act = i0 + (u64)u * RDF_BLOCK + threadIdx.x < e;
+            const u64 key[3] = {(u64)ts[u], (u64)V + tp[u], 2ull * V + to[u]};
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const u32 pos = bucket_slot(lh, (u32)(key[t] >> bits), act);
+                if (SCATTER && act) recs[pos] = (uint16_t)(key[t] & lmask);
+            }
         }
     }
     if (!SCATTER) {
@@ -300,18 +317,7 @@ __device__ inline u32 wave_runs4(u64 key, bool active) {
 
 // the binary keys of one triple window with runs of equal keys in adjacent lanes merged (the same merge in both
 // passes, so the histogram pass and the scatter pass agree; a record counts <= 4 occurrences)
-__device__ inline void b2_keys(const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o, u64 i,
-                               bool act, u32 V, const u64* __restrict__ fbits, u64 (&key)[3], u32 (&cnt)[3]) {
-    u32 ts = 0, tp = 0, to = 0;
-    bool fs = false, fp = false, fo = false;
-    if (act) {
-        ts = s[i];
-        tp = p[i];
-        to = o[i];
-        fs = fbit(fbits, ts);
-        fp = fbit(fbits, (u64)V + tp);
-        fo = fbit(fbits, 2ull * V + to);
-    }
+__device__ inline void b2_keys(u32 ts, u32 tp, u32 to, bool fs, bool fp, bool fo, u64 (&key)[3], u32 (&cnt)[3]) {
     key[0] = bin_key(2, ts, tp);  // o[s,p] (35)
     key[1] = bin_key(1, ts, to);  // p[s,o] (21)
     key[2] = bin_key(0, tp, to);  // s[p,o] (14)
@@ -330,16 +336,35 @@ __global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s
     __syncthreads();
     const u64 per = (n + gridDim.x - 1) / gridDim.x;
     const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
-    for (u64 i0 = b; i0 < e; i0 += B2_PBLOCK) {
-        const u64 i = i0 + threadIdx.x;
-        u64 key[3];
-        u32 cnt[3];
-        b2_keys(s, p, o, i, i < e, V, fbits, key, cnt);
+    // PART_U rows per thread: their triple loads, then their frequency-bit loads, each batch in flight together
+    for (u64 i0 = b; i0 < e; i0 += (u64)B2_PBLOCK * PART_U) {
+        u32 ts[PART_U], tp[PART_U], to[PART_U];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const bool a = cnt[t] != 0;
-            const u32 pos = bucket_slot(lh, a ? b2_bucket(key[t], bits) : 0u, a);
-            if (SCATTER && a) rkeys[pos] = b2_pack(key[t], cnt[t]);
+        for (int u = 0; u < PART_U; ++u) {
+            const u64 i = i0 + (u64)u * B2_PBLOCK + threadIdx.x;
+            ts[u] = i < e ? s[i] : 0u;
+            tp[u] = i < e ? p[i] : 0u;
+            to[u] = i < e ? o[i] : 0u;
+        }
+        bool fs[PART_U], fp[PART_U], fo[PART_U];
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            const bool act = i0 + (u64)u * B2_PBLOCK + threadIdx.x < e;
+            fs[u] = act && fbit(fbits, ts[u]);
+            fp[u] = act && fbit(fbits, (u64)V + tp[u]);
+            fo[u] = act && fbit(fbits, 2ull * V + to[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            u64 key[3];
+            u32 cnt[3];
+            b2_keys(ts[u], tp[u], to[u], fs[u], fp[u], fo[u], key, cnt);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const bool a = cnt[t] != 0;
+                const u32 pos = bucket_slot(lh, a ? b2_bucket(key[t], bits) : 0u, a);
+                if (SCATTER && a) rkeys[pos] = b2_pack(key[t], cnt[t]);
+            }
         }
     }
     if (!SCATTER) {

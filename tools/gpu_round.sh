@@ -86,6 +86,14 @@ for step in "$@"; do
       while kill -0 $PID 2>/dev/null; do sleep 30; echo "[hb $(date +%T)] $(grep -cE 'PASSED' gpurun_out/tfile_$TAG.log) passed"; done
       wait $PID || { echo "tfile failed"; tail -60 gpurun_out/tfile_$TAG.log; exit 1; }
       grep -cE "PASSED" gpurun_out/tfile_$TAG.log; tail -2 gpurun_out/tfile_$TAG.log ;;
+    benchcfg:*)  # benchcfg:<config>:<scale>:<steps> -- one BASELINE shape on one GPU, with a heartbeat (long steps)
+      IFS=: read -r _ CFG SC NS <<< "$step"
+      timeout -k 10 1000 python -u bench.py --config $CFG --scale $SC --steps $NS --warmup 0 --no-cpu-baseline --no-ingest --no-resident --page-log \
+        > gpurun_out/bcfg_${TAG}_$CFG.json 2> gpurun_out/bcfg_${TAG}_$CFG.err &
+      PID=$!
+      while kill -0 $PID 2>/dev/null; do sleep 30; echo "[hb $(date +%T)] $(tail -c 200 gpurun_out/bcfg_${TAG}_$CFG.err | tr '\n' ' ')"; done
+      wait $PID || { echo "benchcfg $CFG failed"; tail -30 gpurun_out/bcfg_${TAG}_$CFG.err; exit 1; }
+      cat gpurun_out/bcfg_${TAG}_$CFG.json ;;
     gtest:*)  # gtest:<pytest -k expression> -- a subset of the GPU tests
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#gtest:}" \
         > gpurun_out/gtest_$TAG.log 2>&1 || { echo "gtest failed"; tail -30 gpurun_out/gtest_$TAG.log; exit 1; }
