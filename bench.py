@@ -414,7 +414,8 @@ def main():
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],
                      "explicit_raw": cs["n_explicit_raw"], "heavy_chunks": cs["n_heavy_chunks"],
                      "heavy_candidates": cs["n_heavy_candidates"], "class_members": cs["n_class_members"],
-                     "classes": cs["n_classes"], "class_cinds": cs["n_class_cinds"]},
+                     "classes": cs["n_classes"], "class_cinds": cs["n_class_cinds"],
+                     **({"exchange_rank0": getattr(ctx, "x_stats", None)} if world > 1 else {})},
         }
         print(json.dumps(line), flush=True)
     ctx.close()

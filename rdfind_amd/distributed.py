@@ -112,9 +112,12 @@ def run_protocol(machine, group=None, device=None):
     takes the result.  Returns the number of collectives performed."""
     device = device or exchange_device(group)
     n = 0
+    sent = received = 0
     while True:
         req = machine.shard_step()
         if req.op == _lib.X_DONE:
+            # this rank's exchange volume (elements x element size), kept on the machine for the bench's work counters
+            machine.x_stats = {"collectives": n, "bytes_sent": sent, "bytes_received": received}
             return n
         send = torch.empty(req.count, dtype=_dtype(req.op), device=device)
         machine.shard_export(send.data_ptr())
@@ -127,6 +130,8 @@ def run_protocol(machine, group=None, device=None):
         recv = exchange(req, send, group).contiguous()
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
+        sent += send.numel() * send.element_size()
+        received += recv.numel() * recv.element_size()
         machine.shard_import(recv.data_ptr(), recv.numel())
         n += 1
 
