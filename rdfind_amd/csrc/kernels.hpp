@@ -49,14 +49,6 @@ static constexpr u32 LIGHT_LDS = 512;
 // bitmap over the compact capture space (C bits, no more bytes than the member list): a (candidate, group) test is one
 // 4-B load instead of a ~log2(n)-level divergent search.
 static constexpr u64 LIGHT_DENSE_MIN = 256;
-// Capture rows, the transpose: the captures with the most local groups (at least G / RDFIND_CROW_DIV, default 256,
-// within a byte budget, largest first) get a bitmap over the group space.  The candidates that survive many light
-// groups are such large captures (a true ref's support is at least its dependent's); with the lanes over a
-// dependent's ascending groups, testing one candidate is one bit load per lane into a few lines of its row instead
-// of a goff gather plus a divergent search per lane.
-static constexpr u64 CROW_DIV = 256;
-static constexpr u64 CROW_MIN = 64;          // never a row for a capture with fewer groups
-static constexpr u64 CROW_BUDGET = 1ull << 29;  // bytes of rows (RDFIND_CROW_MB overrides)
 #ifndef RDF_LIGHT_SMALL
 #define RDF_LIGHT_SMALL 31
 #endif
@@ -117,9 +109,6 @@ struct CindView {
     const u32* gdrow;     // group -> row of its exact member bitmap (dense light groups), NONE32 (null: no bitmaps)
     const u32* dbits;     // dense-group bitmaps: row r at dbits + r * dwords, bit x set iff capture x is a member
     u64 dwords;
-    const u32* crow;      // capture -> row of its group bitmap (the largest captures), NONE32 (null: no capture rows)
-    const u32* cbits;     // capture group bitmaps: row r at cbits + r * cwords, bit g set iff the capture is in group g
-    u64 cwords;
 };
 
 }  // namespace rdf

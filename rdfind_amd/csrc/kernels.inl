@@ -1053,77 +1053,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_dense_build(const u32* __restrict
     }
 }
 
-// capture rows (CindView::crow): bit g of a large capture's row is set iff the capture is in group g
-__device__ inline const u32* cap_row(const CindView& v, u32 x) {
-    if (!v.crow || x == NONE32) return nullptr;
-    const u32 r = v.crow[x];
-    return r == NONE32 ? nullptr : v.cbits + (u64)r * v.cwords;
-}
-__device__ inline bool crow_has(const u32* row, u32 g) { return (row[g >> 5] >> (g & 31)) & 1u; }
-
-// log2 histogram of the captures' local group counts, merged per block in LDS
-__global__ __launch_bounds__(RDF_BLOCK) void k_crow_hist(const u64* __restrict__ doff, u32 C, u32* hist) {
-    __shared__ u32 lh[64];
-    for (u32 i = threadIdx.x; i < 64; i += RDF_BLOCK) lh[i] = 0;
-    __syncthreads();
-    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 n = doff[d + 1] - doff[d];
-        if (n) atomicAdd(&lh[63 - __clzll(n)], 1u);
-    }
-    __syncthreads();
-    for (u32 i = threadIdx.x; i < 64; i += RDF_BLOCK)
-        if (lh[i]) atomicAdd(&hist[i], lh[i]);
-}
-// row threshold: max(2^b, nmin) for the smallest b whose captures (>= 2^b groups) number at most rows_max
-__global__ void k_crow_thresh(const u32* __restrict__ hist, u64 nmin, u64 rows_max, u64* thr) {
-    if (threadIdx.x || blockIdx.x) return;
-    u64 cum = 0;
-    int best = -1;
-    for (int b = 63; b >= 0; --b) {
-        cum += hist[b];
-        if (cum > rows_max) break;
-        best = b;
-    }
-    const u64 t = best < 0 ? ~0ull : 1ull << best;
-    *thr = t > nmin ? t : nmin;
-}
-__global__ __launch_bounds__(RDF_BLOCK) void k_crow_flags(const u64* __restrict__ doff, u32 C, const u64* __restrict__ thr,
-                                                          u32* flags) {
-    const u64 t = *thr;
-    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
-        flags[d] = doff[d + 1] - doff[d] >= t ? 1u : 0u;
-}
-// one block per row: zero it, then OR in the capture's groups (ascending: lanes hitting one word merged by a segmented
-// scan, one atomic per word run)
-__global__ __launch_bounds__(RDF_BLOCK) void k_crow_build(const u32* __restrict__ clist, const u32* __restrict__ nrows,
-                                                          u64 rows_max, const u64* __restrict__ doff,
-                                                          const u32* __restrict__ dgrp, u64 cwords, u32* cbits) {
-    const u64 nr = *nrows;
-    const int lane = lane_id();
-    for (u64 r = blockIdx.x; r < nr && r < rows_max; r += gridDim.x) {
-        u32* row = cbits + r * cwords;
-        for (u64 w = threadIdx.x; w < cwords; w += RDF_BLOCK) row[w] = 0;
-        __threadfence();
-        __syncthreads();
-        const u32 x = clist[r];
-        const u64 b = doff[x], e = doff[x + 1];
-        for (u64 j0 = b; j0 < e; j0 += RDF_BLOCK) {
-            const u64 j = j0 + threadIdx.x;
-            const u32 g = j < e ? dgrp[j] & ~DGRP_HEAVY : NONE32;
-            const u32 w = g == NONE32 ? NONE32 : g >> 5;
-            u32 acc = g == NONE32 ? 0u : 1u << (g & 31);
-#pragma unroll
-            for (int off = 1; off < RDF_WAVE; off <<= 1) {
-                const u32 ow = __shfl_up(w, off, RDF_WAVE), ob = __shfl_up(acc, off, RDF_WAVE);
-                if (lane >= off && ow == w) acc |= ob;
-            }
-            const u32 nw = __shfl_down(w, 1, RDF_WAVE);
-            if (w != NONE32 && (lane == RDF_WAVE - 1 || nw != w)) atomicOr(&row[w], acc);
-        }
-        __syncthreads();
-    }
-}
-
 // candidate filter: the i-th member of the pivot group (or NONE)
 __device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 i) {
     if (v.vcoff) {  // sharded verify pass: the candidates are given (already filtered by the pivot holder)
@@ -1176,36 +1105,30 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_info(const u64* __restrict_
 // One group (members [gb, gb+gs)) checked for every alive candidate of the wave (lanes over candidates): a group of
 // at most LIGHT_LDS members is staged into the wave's LDS slice by one coalesced load, so each search is LDS probes;
 // a larger one is searched in place (the lanes share its top levels).  Returns the candidates still alive.
-__device__ inline u64 check_group(const CindView& v, u32 g, u64 gb, u32 gs, u32 cand, u64 alive, u32* buf, const u32* drow,
-                                  const u32* myrow) {
+__device__ inline u64 check_group(const CindView& v, u64 gb, u32 gs, u32 cand, u64 alive, u32* buf, const u32* drow) {
     const int lane = lane_id();
     const bool mine = (alive >> lane) & 1ull;
     bool found = true;
-    if (mine && myrow) found = crow_has(myrow, g);  // a candidate with a capture row: one bit of its own row
-    const u64 rest = alive & ~__ballot(myrow != nullptr);  // the candidates that need the group's members
-    if (rest) {
-        const bool m2 = (rest >> lane) & 1ull;
-        if (drow) {  // dense group: one bitmap word per candidate
-            if (m2) found = dense_has(drow, cand);
-        } else if (gs <= LIGHT_LDS) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
-            __builtin_amdgcn_wave_barrier();
-            for (u32 k = lane; k < gs; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (m2) {
-                u32 lo = 0, hi = gs;
-                while (lo < hi) {
-                    const u32 mid = (lo + hi) >> 1;
-                    if (buf[mid] < cand) lo = mid + 1;
-                    else hi = mid;
-                }
-                found = lo < gs && buf[lo] == cand;
+    if (drow) {  // dense group: one bitmap word per candidate
+        if (mine) found = dense_has(drow, cand);
+    } else if (gs <= LIGHT_LDS) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
+        __builtin_amdgcn_wave_barrier();
+        for (u32 k = lane; k < gs; k += RDF_WAVE) buf[k] = v.gcap[gb + k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (mine) {
+            u32 lo = 0, hi = gs;
+            while (lo < hi) {
+                const u32 mid = (lo + hi) >> 1;
+                if (buf[mid] < cand) lo = mid + 1;
+                else hi = mid;
             }
-        } else if (m2) {
-            found = bsearch_u32(v.gcap + gb, gs, cand);
+            found = lo < gs && buf[lo] == cand;
         }
+    } else if (mine) {
+        found = bsearch_u32(v.gcap + gb, gs, cand);
     }
     return alive & __ballot(found);
 }
@@ -1286,29 +1209,14 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     const u32 cand = pivot_candidate(v, d, id, piv, k * 8 + (g & 7));
     bool ok = cand != NONE32;
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;  // the smallest light group after the pivot first (most kills)
-#ifndef RDF_CROW_PACKED
-#define RDF_CROW_PACKED 1
-#endif
-    const u32* myrow = RDF_CROW_PACKED ? cap_row(v, cand) : nullptr;
     if (ok && p2 != NONE32) {
-        const u32* dr2 = myrow ? nullptr : dense_row(v, p2);
-        ok = myrow ? crow_has(myrow, p2)
-                   : dr2 ? dense_has(dr2, cand) : bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
+        const u32* dr2 = dense_row(v, p2);
+        ok = dr2 ? dense_has(dr2, cand) : bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
     }
     const u64 b = v.doff[d], e = v.doff[d + 1];
-    if (myrow) {  // a candidate with a capture row: one bit per light group, no member lists
-        for (u64 j0 = b; ok && j0 < e; j0 += PACK_STEP) {
-            u32 gr[PACK_STEP];
-#pragma unroll
-            for (int i = 0; i < PACK_STEP; ++i) gr[i] = j0 + i < e ? v.dgrp[j0 + i] : NONE32;
-#pragma unroll
-            for (int i = 0; i < PACK_STEP; ++i)
-                ok = ok && (gr[i] == piv || gr[i] == p2 || (gr[i] & DGRP_HEAVY) || crow_has(myrow, gr[i]));
-        }
-    }
     // PACK_STEP group entries at a time: their ids, bounds and searches are independent loads (one round trip per
     // level for all of them instead of one chain per group)
-    for (u64 j0 = b; ok && !myrow && j0 < e; j0 += PACK_STEP) {
+    for (u64 j0 = b; ok && j0 < e; j0 += PACK_STEP) {
         u32 gr[PACK_STEP];
         const u32* ga[PACK_STEP];
         const u32* dr[PACK_STEP];
@@ -1365,25 +1273,6 @@ __device__ u32* g_item_rec;
 #define LSTAT_BAT(depth) do { } while (0)
 #endif
 
-// the next K row candidates (taken from todo): every lane tests its group g (NONE32: none) in each candidate's row
-template <int K>
-__device__ inline void row_batch(u32 g, const u32* myrow, u64& todo, u64& alive) {
-    int bit[K];
-    const u32* rp[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        bit[k] = todo ? __ffsll((long long)todo) - 1 : -1;
-        todo &= todo - 1;
-        rp[k] = (const u32*)__shfl((unsigned long long)myrow, bit[k] < 0 ? bit[0] : bit[k], RDF_WAVE);
-    }
-    bool ok[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) ok[k] = g == NONE32 || crow_has(rp[k], g);
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        if (bit[k] >= 0 && !__all(ok[k])) alive &= ~(1ull << bit[k]);
-}
-
 // one batch of the group-parallel window: the next K alive candidates (taken from todo) searched in every lane's
 // group gm (g == NONE32: no group in this lane); a candidate missing from any lane's group dies
 template <int K>
@@ -1433,8 +1322,6 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const u32 cand = chunk_candidate(v, d, id, piv, chunk);
     const u64 alive0 = __ballot(cand != NONE32);
     u64 alive = alive0;
-    const u32* myrow = cap_row(v, cand);  // large candidates: their group rows replace the member searches
-    const u64 hasrow = __ballot(myrow != nullptr);
     const u64 b = b0 + seg * LIGHT_SEG;
     const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
     LSTAT_T0;
@@ -1443,8 +1330,8 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
     if (p2 != NONE32 && alive) {
         const u64 gb2 = v.goff[p2];
-        alive = check_group(v, p2, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
-                            dense_row(v, p2), nullptr);
+        alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
+                            dense_row(v, p2));
     }
     // Lanes take one group each (LIGHT_IT per lane); dependents with few groups went to k_light_packed, so
     // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
@@ -1496,8 +1383,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                     const u64 gb = __shfl(gbv[it], l, RDF_WAVE);
                     const u32 gs = __shfl(gszv[it], l, RDF_WAVE);
                     const u32* dr = (const u32*)__shfl((unsigned long long)gdr[it], l, RDF_WAVE);
-                    const u32 gl = __shfl(g, l, RDF_WAVE);
-                    alive = check_group(v, gl, gb, gs, cand, alive, buf, dr, nullptr);
+                    alive = check_group(v, gb, gs, cand, alive, buf, dr);
                 }
                 continue;
             }
@@ -1550,15 +1436,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             // search are independent, so the serial chain is one search, not one per candidate
             // the batch width follows the alive count: a key slot without its own candidate would repeat another
             // slot's loads (each a divergent wave-wide load over 64 groups)
-            // candidates with a capture row: one bit per lane in the candidate's row instead of a search per lane
-            u64 rt = alive & hasrow;
-            while (rt) {
-                const int na = __popcll(rt);
-                if (na <= 2) row_batch<2>(g, myrow, rt, alive);
-                else if (na <= 4) row_batch<4>(g, myrow, rt, alive);
-                else row_batch<LIGHT_BATCH>(g, myrow, rt, alive);
-            }
-            u64 todo = alive & ~hasrow;
+            u64 todo = alive;
             while (todo) {
                 LSTAT_BAT(gsz ? 64 - __clzll(gsz) : 0);
                 const int na = __popcll(todo);

@@ -83,12 +83,6 @@ struct rdf_ctx {
     u64 dwords = 0, n_dense = 0;
     int dense_div = 32;                   // RDFIND_DENSE (0: no bitmaps)
     u64 dense_min = LIGHT_DENSE_MIN;      // RDFIND_DENSE_MIN (test hook: bitmaps for small groups too)
-    DevBuf crmap, crlist, crbits, crhist, crthr;  // capture rows: capture -> row, row -> capture, the rows, selection
-    bool crow_on = false;
-    u64 crwords = 0;
-    u64 crow_div = CROW_DIV;       // RDFIND_CROW_DIV (0: no capture rows)
-    u64 crow_min = CROW_MIN;       // RDFIND_CROW_MIN (test hook: rows for small captures too)
-    u64 crow_budget = CROW_BUDGET; // RDFIND_CROW_MB
     bool sig_on = false;  // lsig holds this run's signatures (RDFIND_SIG=0 turns the filter off)
     bool sig_packed = false;  // the packed light path tests them too (RDFIND_SIG=1; default 2: k_light only)
     bool piv2_on = false;     // piv2 holds this run's second pivots
@@ -297,7 +291,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->crmap, &c->crlist, &c->crbits, &c->crhist, &c->crthr, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
+            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
@@ -328,13 +322,6 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (const char* dd = getenv("RDFIND_DENSE")) c->dense_div = atoi(dd);
     if (const char* dm = getenv("RDFIND_DENSE_MIN"))
         if (atoll(dm) > 0) c->dense_min = (u64)atoll(dm);
-    // capture rows: RDFIND_CROW_DIV=<divisor> (captures of >= G / divisor local groups; 0 = off), the test hook
-    // RDFIND_CROW_MIN=<groups> (absolute minimum) and RDFIND_CROW_MB=<row budget in MiB>
-    if (const char* cd = getenv("RDFIND_CROW_DIV")) c->crow_div = (u64)atoll(cd);
-    if (const char* cm = getenv("RDFIND_CROW_MIN"))
-        if (atoll(cm) > 0) c->crow_min = (u64)atoll(cm);
-    if (const char* cb = getenv("RDFIND_CROW_MB"))
-        if (atoll(cb) > 0) c->crow_budget = (u64)atoll(cb) << 20;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -405,7 +392,7 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next) {
     for (DevBuf* b : ctx_buffers(c))
         if (!kept(b)) b->release();
     c->ws.release();
-    c->crow_on = c->dense_on = false;
+    c->dense_on = false;
     c->class_pending = false;
     c->h_runs_valid = false;
     c->h_bkeys_valid = false;
@@ -1397,9 +1384,6 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.gdrow = c->dense_on ? c->gdrow.as<u32>() : nullptr;
     v.dbits = c->dense_on ? c->dbits.as<u32>() : nullptr;
     v.dwords = c->dwords;
-    v.crow = c->crow_on ? c->crmap.as<u32>() : nullptr;
-    v.cbits = c->crow_on ? c->crbits.as<u32>() : nullptr;
-    v.cwords = c->crwords;
     return v;
 }
 
@@ -1438,50 +1422,6 @@ static rdf_status d_dense_bitmaps(rdf_ctx* c, CindView& v) {
     v.gdrow = c->gdrow.as<u32>();
     v.dbits = c->dbits.as<u32>();
     v.dwords = dwords;
-    return RDF_OK;
-}
-
-// group bitmaps of the largest captures (>= G / RDFIND_CROW_DIV local groups, default 256, and >= CROW_MIN; largest
-// first within the byte budget: the threshold is the smallest power of two whose captures fit, found on the device
-// from a log2 histogram, so there is no host round trip).  Built from the dependent -> group lists (heavy tags masked).
-static rdf_status d_capture_rows(rdf_ctx* c, CindView& v) {
-    hipStream_t st = c->stream;
-    const u64 G = c->G, C = c->C;
-    c->crow_on = false;
-    v.crow = nullptr;
-    v.cbits = nullptr;
-    if (!c->crow_div || !G || !C) return RDF_OK;
-    const u64 cwords = ((G + 31) / 32 + 31) & ~31ull;  // rows start on 128-B lines
-    const u64 rows_max = std::min<u64>(C, c->crow_budget / (cwords * 4));
-    const u64 nmin = std::max<u64>((G + c->crow_div - 1) / c->crow_div, c->crow_min);
-    if (!rows_max || c->Jf / nmin == 0) return RDF_OK;
-    const u64 rows_cap = std::min<u64>(rows_max, c->Jf / nmin);  // captures of >= nmin entries are at most Jf / nmin
-    tbegin(c, RDF_T_LIGHT);
-    ENSURE(c, crhist, 64 * 4);
-    ENSURE(c, crthr, 8);
-    ENSURE(c, gflag, C * 4);
-    ENSURE(c, gexcl, (C + 1) * 4);
-    ENSURE(c, crmap, C * 4);
-    ENSURE(c, crlist, rows_cap * 4);
-    ENSURE(c, crbits, rows_cap * cwords * 4);
-    HIP_TRY(c, hipMemsetAsync(c->crhist.p, 0, 64 * 4, st));
-    hipLaunchKernelGGL(k_crow_hist, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), (u32)C,
-                       c->crhist.as<u32>());
-    hipLaunchKernelGGL(k_crow_thresh, dim3(1), dim3(64), 0, st, c->crhist.as<u32>(), nmin, rows_cap, c->crthr.as<u64>());
-    hipLaunchKernelGGL(k_crow_flags, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), (u32)C,
-                       c->crthr.as<u64>(), c->gflag.as<u32>());
-    HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), C, c->gexcl.as<u32>() + C, st));
-    hipLaunchKernelGGL(k_dense_rows, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gflag.as<u32>(),
-                       c->gexcl.as<u32>(), C, c->crmap.as<u32>(), c->crlist.as<u32>());
-    hipLaunchKernelGGL(k_crow_build, dim3((unsigned)std::min<u64>(rows_cap, 4096)), dim3(RDF_BLOCK), 0, st,
-                       c->crlist.as<u32>(), c->gexcl.as<u32>() + C, rows_cap, c->doff.as<u64>(), c->dgrp.as<u32>(), cwords,
-                       c->crbits.as<u32>());
-    tend(c, RDF_T_LIGHT);
-    c->crow_on = true;
-    c->crwords = cwords;
-    v.crow = c->crmap.as<u32>();
-    v.cbits = c->crbits.as<u32>();
-    v.cwords = cwords;
     return RDF_OK;
 }
 
@@ -1530,7 +1470,6 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     }
     tend(c, RDF_T_PIVOT);
     TRY(d_dense_bitmaps(c, v));
-    TRY(d_capture_rows(c, v));
     static const int piv2_mode = getenv("RDFIND_PIV2") ? atoi(getenv("RDFIND_PIV2")) : 1;  // 2: k_light only
     const bool piv2_enabled = piv2_mode != 0;
     c->piv2_packed = piv2_mode != 2;

@@ -259,44 +259,6 @@ def test_dense_bitmap_paths_parity(monkeypatch):
             g.close()
 
 
-@pytest.mark.parametrize("dense", [False, True])
-def test_capture_row_paths_parity(monkeypatch, dense):
-    """Every capture with a group gets a capture row (RDFIND_CROW_DIV / RDFIND_CROW_MIN test hooks), so the row paths
-    of the light kernels (row batches, the serial and second-pivot checks with rows, the packed walk) carry the
-    verification, mixed with candidates without rows under a small budget, with and without the dense-group bitmaps,
-    in every mode and with the heavy columns lowered."""
-    monkeypatch.setenv("RDFIND_CROW_DIV", "1000000")
-    monkeypatch.setenv("RDFIND_CROW_MIN", "1")
-    if dense:
-        monkeypatch.setenv("RDFIND_DENSE", "1000000")
-        monkeypatch.setenv("RDFIND_DENSE_MIN", "1")
-    for heavy_min, budget_mb in ((64, None), (2, None), (64, "1")):
-        monkeypatch.setenv("RDFIND_HEAVY_MIN", str(heavy_min))
-        if budget_mb:
-            monkeypatch.setenv("RDFIND_CROW_MB", budget_mb)
-        g = _lib.Context(0)
-        try:
-            rng = random.Random(500 + heavy_min + 7 * dense)
-            for _ in range(40):
-                n = rng.randrange(20, 400)
-                nv = rng.randrange(4, 40)
-                ms = rng.randrange(1, 4)
-                arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
-                               dtype=np.uint32)
-                for strategy, clean in MODES:
-                    assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
-                        (n, nv, ms, strategy, clean, heavy_min, budget_mb)
-            for cfg, scale in (("c5", 0.01), ("c1", 0.05), ("c4", 0.0003), ("c2", 0.01)):
-                d = synth.config(cfg, scale)
-                exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
-                g.set_triples(d.s, d.p, d.o, d.num_terms)
-                g.run(d.min_support)
-                assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, heavy_min, budget_mb)
-        finally:
-            g.close()
-            monkeypatch.delenv("RDFIND_CROW_MB", raising=False)
-
-
 def _paged(g, ms, strategy, clean, page_bytes):
     """Every page of a paged run: (union of decoded rows, total count, sum of page checksums, pages, compact ok)."""
     g.frequent_conditions(ms)
