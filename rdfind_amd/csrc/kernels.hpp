@@ -49,6 +49,10 @@ static constexpr u32 LIGHT_LDS = 512;
 // bitmap over the compact capture space (C bits, no more bytes than the member list): a (candidate, group) test is one
 // 4-B load instead of a ~log2(n)-level divergent search.
 static constexpr u64 LIGHT_DENSE_MIN = 256;
+#ifndef RDF_DENSE_SER
+#define RDF_DENSE_SER 8
+#endif
+static constexpr int LIGHT_DENSE_SER = RDF_DENSE_SER;  // alive candidates from which dense groups go lanes-over-candidates
 #ifndef RDF_LIGHT_SMALL
 #define RDF_LIGHT_SMALL 31
 #endif
@@ -66,6 +70,12 @@ static constexpr int LIGHT_STAGE_MIN = RDF_STAGE_MIN;
 #endif
 static constexpr u64 LIGHT_STAGE_AVG = RDF_STAGE_AVG;  // staging variant when the weighted mean light group is smaller
                   // groups up to this size are searched in LDS (2 KiB per wave)
+
+static constexpr u32 PRE_TAG = 0x80000000u;  // light pass A: an unverified survivor (ref bit 31; compact ids < 2^31)
+#ifndef RDF_PRE_MAX
+#define RDF_PRE_MAX 64
+#endif
+static constexpr int LIGHT_PRE_MAX = RDF_PRE_MAX;  // pass A defers chunks with at most this many candidates left (64: all)
 
 // per frequent capture (compact id) metadata, 16 bytes, one dwordx4 load
 struct __align__(16) CapInfo {
@@ -109,6 +119,8 @@ struct CindView {
     const u32* gdrow;     // group -> row of its exact member bitmap (dense light groups), NONE32 (null: no bitmaps)
     const u32* dbits;     // dense-group bitmaps: row r at dbits + r * dwords, bit x set iff capture x is a member
     u64 dwords;
+    int prefilter;        // light pass A: dependents of several chunks only filtered (survivors tagged PRE_TAG)
+    int p2done;           // light pass B: the given candidates already passed the second pivot
 };
 
 }  // namespace rdf

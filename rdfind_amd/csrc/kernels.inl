@@ -1209,7 +1209,7 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
     const u32 cand = pivot_candidate(v, d, id, piv, k * 8 + (g & 7));
     bool ok = cand != NONE32;
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;  // the smallest light group after the pivot first (most kills)
-    if (ok && p2 != NONE32) {
+    if (ok && p2 != NONE32 && !v.p2done) {
         const u32* dr2 = dense_row(v, p2);
         ok = dr2 ? dense_has(dr2, cand) : bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
     }
@@ -1328,10 +1328,22 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // The dependent's smallest light group after the pivot first, lanes over candidates: it kills most doomed
     // candidates with one (often LDS-staged) search each before the group-parallel windows below.
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
-    if (p2 != NONE32 && alive) {
+    // pass A (prefilter): a chunk of a dependent of several chunks with few candidates left after the filters and the
+    // second pivot is not verified here; its survivors go out tagged (item seg 0) and pass B verifies them compacted
+    const bool multi = v.prefilter && itemoff[d + 1] - itemoff[d] > nseg;
+    if (p2 != NONE32 && alive && !v.p2done) {
         const u64 gb2 = v.goff[p2];
         alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
                             dense_row(v, p2));
+    }
+    if (multi && __popcll(alive) <= LIGHT_PRE_MAX) {  // every segment item of the chunk reaches the same decision
+        if (seg == 0) {
+            const u64 oct0 = choff[d] + chunk * 8 - ob;
+            const u64 noct = choff[d + 1] - ob - oct0;
+            slot_emit(oct0, noct < 8 ? (u32)noct : 8u, d, cand | PRE_TAG, alive, slots, counts);
+            if (nseg > 1 && lane == 0) dead[oct0] = ~0ull;  // k_light_mseg_emit leaves the chunk alone
+        }
+        return;
     }
     // Lanes take one group each (LIGHT_IT per lane); dependents with few groups went to k_light_packed, so
     // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
@@ -1366,9 +1378,33 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             // a multi-segment item drops the candidates other segments have already killed
             if (nseg > 1 && (it || s0 != b)) alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8 - ob], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (!alive) break;
-            const u32 g = gg[it];
-            const u64 lm = __ballot(g != NONE32);  // light groups of this window
+            u32 g = gg[it];
+            u64 lm = __ballot(g != NONE32);  // light groups of this window
             LSTAT_WIN(lm, gszv[it]);
+            const u64 dm = __ballot(gdr[it] != nullptr);  // ... of which dense (member bitmaps)
+            if (dm && __popcll(alive) >= LIGHT_DENSE_SER) {
+                // many candidates alive: the dense groups one at a time with the lanes over the candidates.  The
+                // candidates are ascending pivot members, so a group's 64 tests hit a few lines of its bitmap row
+                // (lanes over groups would touch 64 rows per candidate).  Four groups' loads in flight.
+                u64 t = dm;
+                while (t && alive) {
+                    const u32* dr[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int l = t ? __ffsll((long long)t) - 1 : -1;
+                        t &= t - 1;
+                        dr[k] = l < 0 ? nullptr : (const u32*)__shfl((unsigned long long)gdr[it], l, RDF_WAVE);
+                    }
+                    const bool mine = (alive >> lane) & 1ull;
+                    bool f = true;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) f = f && (!mine || !dr[k] || dense_has(dr[k], cand));
+                    alive &= __ballot(f);
+                }
+                if (gdr[it]) g = NONE32;  // what is left: the sparse light groups of the window
+                lm = __ballot(g != NONE32);
+                if (!lm || !alive) continue;
+            }
             if (__popcll(lm) <= LIGHT_SERIAL) {
                 // few light groups (the common case: most groups of a dependent are heavy and verified by the
                 // mask test): take them one at a time with the lanes over the candidates.  A group of at most
@@ -1440,7 +1476,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             while (todo) {
                 LSTAT_BAT(gsz ? 64 - __clzll(gsz) : 0);
                 const int na = __popcll(todo);
-                const u32* dr = gdr[it];
+                const u32* dr = g == NONE32 ? nullptr : gdr[it];
                 if (na <= 2) light_batch<2>(gm, gsz, dr, g, cand, todo, alive);
                 else if (na <= 4) light_batch<4>(gm, gsz, dr, g, cand, todo, alive);
                 else light_batch<LIGHT_BATCH>(gm, gsz, dr, g, cand, todo, alive);
@@ -1500,6 +1536,7 @@ __device__ inline void k_light_mseg_emit_body(u64 vblk, CindView v, const u32* _
     const u64 alive0 = __ballot(cand != NONE32);
     const u64 oct0 = choff[d] + chunk * 8 - ob;
     const u64 noct = choff[d + 1] - ob - oct0;
+    if (v.prefilter && dead[oct0] == ~0ull) return;  // pass A: a tagged chunk, emitted by its first segment item
     slot_emit(oct0, noct < 8 ? (u32)noct : 8u, d, cand, alive0 & ~dead[oct0], slots, counts);
 }
 __global__ __launch_bounds__(RDF_BLOCK) void k_light_mseg_emit(u64 nvblk, CindView v, const u32* __restrict__ pivot,
@@ -1529,6 +1566,36 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restric
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d <= C; d += (u64)gridDim.x * RDF_BLOCK) {
         eoff[d] = lower_bound_u64(pairs, E, d << 32);
         if (d < C) ebin[d] = lower_bound_u64(pairs, E, (d << 32) | Cu);
+    }
+}
+
+// two light passes: the octets whose slots hold tagged survivors (flags = their counts, else 0), their survivors
+// gathered in octet order (tag cleared), and pass B's verdicts applied back: a tagged slot stays iff pass B kept its
+// pair (bpairs sorted, boff = its lower bounds per dependent)
+__global__ __launch_bounds__(RDF_BLOCK) void k_tag_octets(const u64* __restrict__ slots, const u32* __restrict__ counts,
+                                                          u64 W, u32* flags) {
+    for (u64 o = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; o < W; o += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 n = counts[o];
+        flags[o] = n && ((u32)slots[o * 8] & PRE_TAG) ? n : 0u;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_tag_gather(const u64* __restrict__ slots, const u32* __restrict__ flags,
+                                                          const u64* __restrict__ pos, u64 W, u64* out) {
+    for (u64 o = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; o < W; o += (u64)gridDim.x * RDF_BLOCK)
+        for (u32 j = 0; j < flags[o]; ++j) out[pos[o] + j] = slots[o * 8 + j] & ~(u64)PRE_TAG;
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_tag_fix(u64* slots, u32* counts, const u32* __restrict__ flags, u64 W,
+                                                       const u64* __restrict__ bpairs, const u64* __restrict__ boff) {
+    for (u64 o = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; o < W; o += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 n = flags[o];
+        if (!n) continue;
+        u32 k = 0;
+        for (u32 j = 0; j < n; ++j) {
+            const u64 x = slots[o * 8 + j] & ~(u64)PRE_TAG;
+            const u64 d = x >> 32;
+            if (bsearch_u64(bpairs + boff[d], boff[d + 1] - boff[d], x)) slots[o * 8 + k++] = x;
+        }
+        counts[o] = k;
     }
 }
 

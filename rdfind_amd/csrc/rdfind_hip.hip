@@ -102,7 +102,7 @@ struct rdf_ctx {
     bool hclassed = false;  // binary heavy-only dependents emitted from class lists (single GPU, S2L semantics)
     DevBuf pedges, pedges_tmp;
     u64 ncap = 0;
-    u64 n_explicit_raw = 0, n_light_chunks = 0;
+    u64 n_explicit_raw = 0, n_light_chunks = 0, n_light_survivors = 0;
     rdf_fc_stats fstats = {};
     rdf_group_stats gstats = {};
     rdf_cind_stats cstats = {};
@@ -125,6 +125,7 @@ struct rdf_ctx {
     DevBuf xsend, xrecv, gbest, nrl, smask, smask_tmp, cpairs, cpairs_tmp, obounds;
     DevBuf lmask, hrep, vpairs, vcoff, vpiv;  // holder-first light exchange (sh_phase5 / sh_phase15)
     DevBuf ebown, segb, sege, seglen;         // this rank's binary dependents' final pairs; dependent segments
+    DevBuf bslots, bcounts;                   // light pass B's output slots (pass A's stay in epairs_tmp / lslot)
     DevBuf ukeys, ukeys_tmp;                  // sharded: frequent unary keys (owned, then every rank's, sorted)
     // sharded ingest (rdf_shard_parse_begin): local terms routed to their owners, the owner's dictionary, global ids
     DevBuf ithv, ikeys, ikeys_tmp, iwords, iwoff, ihdr, ipay, ibnd, iwb, rhdr, rlen, rwords, rwoff, rts, rhv, rvalid, rtab,
@@ -291,7 +292,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->segb, &c->sege, &c->seglen, &c->ukeys,
+            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->bslots, &c->bcounts, &c->segb, &c->sege, &c->seglen, &c->ukeys,
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
@@ -1384,6 +1385,8 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.gdrow = c->dense_on ? c->gdrow.as<u32>() : nullptr;
     v.dbits = c->dense_on ? c->dbits.as<u32>() : nullptr;
     v.dwords = c->dwords;
+    v.prefilter = 0;
+    v.p2done = 0;
     return v;
 }
 
@@ -1582,17 +1585,17 @@ static rdf_status light_range(rdf_ctx* c, u32 d0, u32 d1, bool mseg, LightRange*
     return RDF_OK;
 }
 
-// light dependents of range r -> explicit raw (dep << 32 | ref) pairs at epairs + ebase, in (dep, ref) order;
-// *E = their count.  Output slots are octets (8 pivot candidates each), relative to r.o0.
-static rdf_status d_light_run(rdf_ctx* c, const CindView& v, const u32* pivot, const LightRange& r, u64 ebase, u64* E) {
+// light kernels of dependent range r: survivor slots (8 per output octet, relative to r.o0) and per-octet counts
+static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivot, const LightRange& r, DevBuf& slots,
+                                  DevBuf& counts) {
     hipStream_t st = c->stream;
     const u64 WL = r.o1 - r.o0, WI = r.i1 - r.i0, WP = r.q1 - r.q0, WM = r.m1 - r.m0, ob = r.o0;
     const u64 nslot = std::max<u64>(WL, 1);
-    ENSURE(c, epairs_tmp, nslot * 8 * 8);
+    HIP_TRY(c, slots.ensure(nslot * 8 * 8));
     ENSURE(c, dead, nslot * 8);  // kill masks of multi-segment chunks, keyed by the chunk's first octet
     HIP_TRY(c, hipMemsetAsync(c->dead.p, 0, nslot * 8, st));
-    ENSURE(c, lslot, nslot * 4);
-    HIP_TRY(c, hipMemsetAsync(c->lslot.p, 0, nslot * 4, st));
+    HIP_TRY(c, counts.ensure(nslot * 4));
+    HIP_TRY(c, hipMemsetAsync(counts.p, 0, nslot * 4, st));
 #ifdef RDF_LIGHT_STATS
     u32* lrec = nullptr;
     if (WI && getenv("RDFIND_LIGHT_DUMP")) {
@@ -1608,24 +1611,17 @@ static rdf_status d_light_run(rdf_ctx* c, const CindView& v, const u32* pivot, c
     if (WP)
         hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,
-                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+                           slots.as<u64>(), counts.as<u32>());
     if (WI) {
         auto kl = c->light_stage ? k_light<true> : k_light<false>;
         hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
                            0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
-                           r.i0, WI, ob, c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
+                           r.i0, WI, ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>());
     }
     if (WM)
         hipLaunchKernelGGL(k_light_mseg_emit, dim3(vgrid(wave_blocks(WM))),
                            dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, pivot, c->mchoff.as<u64>(), c->mch_dep.as<u32>(), r.m0,
-                           WM, c->choffl.as<u64>(), ob, c->dead.as<u64>(), c->epairs_tmp.as<u64>(), c->lslot.as<u32>());
-    ENSURE(c, pos, (WL + 1) * 8);
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
-    TRY(read_u64(c, c->pos.as<u64>() + WL, E));
-    HIP_TRY(c, c->epairs.grow_keep((size_t)std::max<u64>(ebase + *E, 1) * 8, st));
-    if (WL)
-        hipLaunchKernelGGL(k_slot_compact, dim3(vgrid(thread_blocks(WL * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WL * 8),
-                           c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->pos.as<u64>(), WL, c->epairs.as<u64>() + ebase);
+                           WM, c->choffl.as<u64>(), ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>());
     tend(c, RDF_T_LIGHT);
 #ifdef RDF_LIGHT_STATS
     if (lrec) {  // per-item records -> $RDFIND_LIGHT_DUMP (raw u32 x 16 per item)
@@ -1639,10 +1635,35 @@ static rdf_status d_light_run(rdf_ctx* c, const CindView& v, const u32* pivot, c
         HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_item_rec), &z, sizeof(z)));
         HIP_TRY(c, hipFree(lrec));
     }
-    fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu WP=%llu E=%llu\n", (unsigned long long)WI, (unsigned long long)WL,
-            (unsigned long long)WP, (unsigned long long)*E);
+    fprintf(stderr, "LIGHT_STATS WI=%llu WL=%llu WP=%llu\n", (unsigned long long)WI, (unsigned long long)WL,
+            (unsigned long long)WP);
 #endif
     return RDF_OK;
+}
+
+// the WL octets' survivor slots, in octet (= (dep, ref)) order, -> out[ebase, ebase + *E)
+static rdf_status d_light_compact(rdf_ctx* c, u64 WL, const DevBuf& slots, const DevBuf& counts, DevBuf& out, u64 ebase,
+                                  u64* E) {
+    hipStream_t st = c->stream;
+    tbegin(c, RDF_T_LIGHT);
+    ENSURE(c, pos, (WL + 1) * 8);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, counts.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
+    tend(c, RDF_T_LIGHT);
+    TRY(read_u64(c, c->pos.as<u64>() + WL, E));
+    HIP_TRY(c, out.grow_keep((size_t)std::max<u64>(ebase + *E, 1) * 8, st));
+    tbegin(c, RDF_T_LIGHT);
+    if (WL)
+        hipLaunchKernelGGL(k_slot_compact, dim3(vgrid(thread_blocks(WL * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WL * 8),
+                           slots.as<u64>(), counts.as<u32>(), c->pos.as<u64>(), WL, out.as<u64>() + ebase);
+    tend(c, RDF_T_LIGHT);
+    return RDF_OK;
+}
+
+// light dependents of range r -> explicit raw (dep << 32 | ref) pairs at epairs + ebase, in (dep, ref) order;
+// *E = their count.  Output slots are octets (8 pivot candidates each), relative to r.o0.
+static rdf_status d_light_run(rdf_ctx* c, const CindView& v, const u32* pivot, const LightRange& r, u64 ebase, u64* E) {
+    TRY(d_light_kernels(c, v, pivot, r, c->epairs_tmp, c->lslot));
+    return d_light_compact(c, r.o1 - r.o0, c->epairs_tmp, c->lslot, c->epairs, ebase, E);
 }
 
 // every light dependent at once: explicit raw pairs in epairs[0, *E) (WI k_light items, WL octets, WP packed octets)
@@ -1651,6 +1672,70 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     TRY(d_light_owners(c, WI, WP, &WM));
     const LightRange r = {0, WI, 0, WP, 0, WM, 0, WL};
     return d_light_run(c, v, pivot, r, 0, E);
+}
+
+// Two light passes (single GPU).  A k_light work item verifies 64 pivot candidates of one dependent against a segment of
+// its groups, so every chunk of a dependent re-reads the same groups, although the cheap filters (support, heavy mask,
+// signature, second pivot) often leave few candidates per chunk.  Pass A verifies the packed dependents and those of one
+// chunk as before; the chunks of the other dependents (at most LIGHT_PRE_MAX candidates left, by default all) only
+// filter, and their survivors stay in their output slots tagged (PRE_TAG).  Pass B verifies the tagged survivors 64 to a
+// chunk, as the sharded verify pass does (candidates given by vcoff / vpairs; the pivot group is still skipped, the
+// second pivot not checked again); a fix-up drops the tagged slots pass B killed, and one compaction writes the
+// (dep, ref)-ordered result, so pass A's verified pairs are never moved.  RDFIND_LIGHT2=0 keeps the single pass.
+static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP, u64* E, const u32* pivot) {
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    CindView va = v;
+    va.prefilter = 1;
+    u64 WM = 0;
+    TRY(d_light_owners(c, WI, WP, &WM));
+    TRY(d_light_kernels(c, va, pivot, {0, WI, 0, WP, 0, WM, 0, WL}, c->epairs_tmp, c->lslot));
+    // the tagged octets' survivors -> vpairs (octet order keeps (dep, ref) order)
+    tbegin(c, RDF_T_LIGHT);
+    ENSURE(c, flags, std::max<u64>(WL, 1) * 4);
+    ENSURE(c, vcoff, (std::max<u64>(WL, C) + 1ull) * 8);  // tagged octet offsets first, then pass B's dependent offsets
+    if (WL)
+        hipLaunchKernelGGL(k_tag_octets, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
+                           c->lslot.as<u32>(), WL, c->flags.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->vcoff.as<u64>(), WL, c->vcoff.as<u64>() + WL, st));
+    tend(c, RDF_T_LIGHT);
+    u64 T = 0;
+    TRY(read_u64(c, c->vcoff.as<u64>() + WL, &T));
+    c->n_light_survivors = T;
+    if (T) {
+        tbegin(c, RDF_T_LIGHT);
+        ENSURE(c, vpairs, T * 8);
+        hipLaunchKernelGGL(k_tag_gather, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
+                           c->flags.as<u32>(), c->vcoff.as<u64>(), WL, c->vpairs.as<u64>());
+        ENSURE(c, ebin, std::max<u64>(C, 1) * 8);
+        hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->vpairs.as<u64>(), T, C, c->Cu, c->vcoff.as<u64>(), c->ebin.as<u64>());
+        CindView vb = v;
+        vb.vcoff = c->vcoff.as<u64>();
+        vb.vpairs = c->vpairs.as<u64>();
+        vb.p2done = 1;
+        if (C)
+            hipLaunchKernelGGL(k_verify_plan, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, vb, c->pnl.as<u32>(),
+                               c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>());
+        tend(c, RDF_T_LIGHT);
+        const u64 hc = c->heavy_candidates, lc = c->light_candidates, le = c->light_entries;
+        u64 WL2 = 0, WH2 = 0, WI2 = 0, WP2 = 0, WM2 = 0, EB = 0;
+        TRY(d_chunks(c, &WL2, &WH2, &WI2, &WP2));
+        c->heavy_candidates = hc;
+        c->light_candidates = lc;
+        c->light_entries = le;
+        TRY(d_light_owners(c, WI2, WP2, &WM2));
+        TRY(d_light_kernels(c, vb, pivot, {0, WI2, 0, WP2, 0, WM2, 0, WL2}, c->bslots, c->bcounts));
+        TRY(d_light_compact(c, WL2, c->bslots, c->bcounts, c->cpairs, 0, &EB));
+        // pass B's verdicts back into pass A's tagged slots
+        tbegin(c, RDF_T_LIGHT);
+        hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->cpairs.as<u64>(), EB, C, c->Cu, c->vcoff.as<u64>(), c->ebin.as<u64>());
+        hipLaunchKernelGGL(k_tag_fix, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
+                           c->lslot.as<u32>(), c->flags.as<u32>(), WL, c->cpairs.as<u64>(), c->vcoff.as<u64>());
+        tend(c, RDF_T_LIGHT);
+    }
+    return d_light_compact(c, WL, c->epairs_tmp, c->lslot, c->epairs, 0, E);
 }
 
 // sort the explicit pairs (epairs[0, E)) and index them: v.eoff / v.ebin / v.epairs
@@ -1956,7 +2041,10 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     tend(c, RDF_T_PIVOT);
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0, H = 0, HC = 0, NT = 0;
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
-    TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
+    static const bool two_pass = !getenv("RDFIND_LIGHT2") || atoi(getenv("RDFIND_LIGHT2")) != 0;
+    c->n_light_survivors = 0;
+    if (two_pass && WI) TRY(d_light_two_pass(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
+    else TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));

@@ -132,11 +132,11 @@ with _lib.Context(0) as ctx:
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("env", [{"RDFIND_STAGE": "0"}, {"RDFIND_STAGE": "1"},
                                  {"RDFIND_SIG": "0", "RDFIND_PIV2": "0"}, {"RDFIND_SIG": "1", "RDFIND_PIV2": "2"},
-                                 {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}])
+                                 {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}, {"RDFIND_LIGHT2": "0"}])
 def test_light_variants_full_size(env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
-    paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members) each reproduce
-    the c1 and c2 golden vectors.  The switches are read
+    paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, one light pass
+    instead of the filter and verify passes) each reproduce the c1 and c2 golden vectors.  The switches are read
     once per process, so each combination runs in its own child process."""
     import subprocess
     import sys
