@@ -117,7 +117,12 @@ def family_rooflines(d, fc, gs, cs, kt, counts):
 
 class CompactSink:
     """Pinned host buffers for the compact CindSet-shaped result (rdf_copy_result_compact): the id-records the
-    metric's T_disc ends with.  Sized from the first run's layout, grown if a run needs more."""
+    metric's T_disc ends with.  Sized from the first run's layout, grown if a run needs more.  A result
+    with more explicit refs than STREAM_REFS (the pages of c5 at full size: up to 10^10 refs each) streams them through
+    one bounded pinned staging buffer (rdf_copy_result_refs), as a sink consuming its input would; page-locking tens of
+    GB per page cost more than the copies."""
+
+    STREAM_REFS = 1 << 28  # 1 GiB of u32 refs
 
     def __init__(self):
         self.bufs, self.cap, self.pinned, self._keep = None, {}, True, []
@@ -125,27 +130,40 @@ class CompactSink:
     def ensure(self, ctx):
         from rdfind_amd import _lib
         L = ctx.result_layout()
-        need = {name: max(count(L), 1) for name, _, count in _lib.COMPACT_PARTS}
-        if self.bufs is not None and all(need[k] <= self.cap[k] for k in need):
-            return L
-        self.bufs, self._keep = {}, []
-        for name, dt, _ in _lib.COMPACT_PARTS:
-            n = need[name]
+        if self.bufs is None:
+            self.bufs, self._keep = {}, {}
+        for name, dt, count in _lib.COMPACT_PARTS:  # only a part that outgrew its buffer is re-allocated
+            need = max(count(L), 1)
+            if name == "refs":
+                need = min(need, self.STREAM_REFS)
+            if name in self.cap and need <= self.cap[name]:
+                continue
+            if name in self.cap:  # grow with headroom: page-locking is slow
+                need = max(need, self.cap[name] + self.cap[name] // 2)
+                if name == "refs":
+                    need = min(need, self.STREAM_REFS)
+            self._keep.pop(name, None)
             try:  # page-locked memory from the library (rdf_host_alloc)
-                b = _lib.PinnedBuffer(n, dt)
-                self._keep.append(b)
+                b = _lib.PinnedBuffer(need, dt)
+                self._keep[name] = b
                 self.bufs[name] = b.ptr
             except _lib.RdfError:  # no pinned memory: pageable numpy (slower link rate, stated in the line)
                 self.pinned = False
-                a = np.empty(n, dt)
-                self._keep.append(a)
+                a = np.empty(need, dt)
+                self._keep[name] = a
                 self.bufs[name] = a.ctypes.data
-        self.cap = need
+            self.cap[name] = need
         return L
 
     def copy(self, ctx):
         L = self.ensure(ctx)
-        ctx.copy_result_compact(self.bufs)
+        if L["n_refs"] <= self.cap["refs"]:
+            ctx.copy_result_compact(self.bufs)
+            return L
+        ctx.copy_result_compact(dict(self.bufs, refs=0))  # everything but the refs, which stream in chunks
+        off = 0
+        while off < L["n_refs"]:
+            off += ctx.copy_result_refs(off, self.cap["refs"], self.bufs["refs"])
         return L
 
 
@@ -244,12 +262,19 @@ def main():
             ctx.frequent_conditions(ms)
             ctx.build_capture_groups("spo")
             n = 0
+            t_page = time.perf_counter()
             for i, _ in enumerate(ctx.pages(True, 1, args.page_bytes or 0)):
                 n += ctx.cind_count()
+                t_copy = time.perf_counter()
                 if hand_over:
                     sink.copy(ctx)
                 if args.page_log:
-                    print(f"page {i}: {n} CINDs so far", file=sys.stderr, flush=True)
+                    _, pcs = ctx.last_stats()
+                    t_end = time.perf_counter()
+                    print(f"page {i}: {n} CINDs so far, explicit raw {pcs['n_explicit_raw']}, "
+                          f"HBM held {ctx.device_bytes() / 2**30:.1f} GiB, page {t_copy - t_page:.2f} s, "
+                          f"hand-over {t_end - t_copy:.2f} s", file=sys.stderr, flush=True)
+                    t_page = time.perf_counter()
             _, cs = ctx.last_stats()
             return dict(cs, n_cinds=n, pages=ctx_pages(ctx))
     else:

@@ -220,6 +220,11 @@ rdf_status rdf_get_result_layout(rdf_ctx* ctx, rdf_result_layout* layout);
 rdf_status rdf_copy_result_compact(rdf_ctx* ctx, uint32_t* refs, uint64_t* runoff, uint32_t* rundep, uint32_t* list_refs,
                                    uint64_t* list_off, uint64_t* members, uint32_t* capture_ids, uint32_t* supports);
 
+/* refs[offset, offset + count) of the compact result (the explicit ref part, n_refs in all) -> refs; *n_copied = the
+ * refs copied (fewer at the end).  A streaming sink hands a large page over through one bounded staging buffer
+ * (the reference's sink consumes its output as it comes, ALG/programs/RDFind.scala:507-520). */
+rdf_status rdf_copy_result_refs(rdf_ctx* ctx, uint64_t offset, uint64_t count, uint32_t* refs, uint64_t* n_copied);
+
 /* Page-locked host memory (hipHostMalloc) for hand-over buffers: the copies above then run at the link rate.
  * Returns null on failure; free with rdf_host_free. */
 void* rdf_host_alloc(uint64_t bytes);

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules", "rdf_get_result_layout",
     "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
     "rdf_discover_cinds_paged", "rdf_next_page", "rdf_shard_parse_begin", "rdf_shard_dictionary_begin", "rdf_num_terms",
-    "rdf_dictionary_terms",
+    "rdf_dictionary_terms", "rdf_copy_result_refs",
 )
 RDF_NT_TABS = 1
 
@@ -154,6 +154,7 @@ def load():
         "rdf_copy_result_raw": (i32, [P, P, P, P, P, P]),
         "rdf_get_result_layout": (i32, [P, ctypes.POINTER(ResultLayout)]),
         "rdf_copy_result_compact": (i32, [P, P, P, P, P, P, P, P, P]),
+        "rdf_copy_result_refs": (i32, [P, u64, u64, P, ctypes.POINTER(u64)]),
         "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
         "rdf_format_cinds": (i32, [P, u64, u64, P, u64, ctypes.POINTER(u64)]),
@@ -519,6 +520,14 @@ class Context:
         ptrs = [bufs[name] if isinstance(bufs[name], int) else bufs[name].ctypes.data for name, _, _ in COMPACT_PARTS]
         self._check(self.lib.rdf_copy_result_compact(self.ptr, *ptrs), "rdf_copy_result_compact")
         return bufs
+
+    def copy_result_refs(self, offset: int, count: int, ptr) -> int:
+        """rdf_copy_result_refs: refs[offset, offset + count) of the compact result into ``ptr`` (numpy array or raw
+        pointer); returns the refs copied."""
+        copied = ctypes.c_uint64()
+        p = ptr if isinstance(ptr, int) else ptr.ctypes.data
+        self._check(self.lib.rdf_copy_result_refs(self.ptr, offset, count, p, ctypes.byref(copied)), "rdf_copy_result_refs")
+        return copied.value
 
     def copy_cinds_decoded(self, offset: int = 0, count: int | None = None) -> np.ndarray:
         """Cind-shaped rows decoded on the device (rdf_copy_cinds_decoded), ROW_DTYPE."""

@@ -98,7 +98,7 @@ struct rdf_ctx {
     bool paged = false, pg_unary_done = false;
     u32 pg_flags = 0, pg_next = 0;
     u64 pg_budget = 0, pg_Eu = 0, pg_HC = 0, pg_NT = 0, pg_WM = 0, pg_pages = 0;
-    std::vector<u64> h_choffl, h_choffh;
+    std::vector<u64> h_choffl, h_choffh, h_eoffu;
     bool hclassed = false;  // binary heavy-only dependents emitted from class lists (single GPU, S2L semantics)
     DevBuf pedges, pedges_tmp;
     u64 ncap = 0;
@@ -1650,7 +1650,9 @@ static rdf_status d_light_compact(rdf_ctx* c, u64 WL, const DevBuf& slots, const
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, counts.as<u32>(), c->pos.as<u64>(), WL, c->pos.as<u64>() + WL, st));
     tend(c, RDF_T_LIGHT);
     TRY(read_u64(c, c->pos.as<u64>() + WL, E));
-    HIP_TRY(c, out.grow_keep((size_t)std::max<u64>(ebase + *E, 1) * 8, st));
+    size_t need = (size_t)std::max<u64>(ebase + *E, 1) * 8;
+    if (ebase && need > out.cap) need = std::max<size_t>(need, out.cap + out.cap / 4);  // appends (paged): grow by >= 1/4
+    HIP_TRY(c, out.grow_keep(need, st));
     tbegin(c, RDF_T_LIGHT);
     if (WL)
         hipLaunchKernelGGL(k_slot_compact, dim3(vgrid(thread_blocks(WL * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WL * 8),
@@ -1743,7 +1745,7 @@ static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL
 static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorted) {
     hipStream_t st = c->stream;
     const u32 C = c->C;
-    ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
+    if (!presorted) ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
     tbegin(c, RDF_T_ESORT);
     if (!presorted) {
         u64* k = c->epairs.as<u64>();
@@ -2159,13 +2161,26 @@ static rdf_status d_page_emit(rdf_ctx* c, const CindView& v, u32 d0, u32 d1, u64
 }
 
 // greedy dependent range from d0 whose light octets and heavy work items fit the page budget (at least one dependent)
+static constexpr u64 PAGE_PER_OCT = 8 * 8 + 8 + 12 + 8 * 4 + 8 + 4;  // slots, kill mask, counts, pairs, flags / positions, refs
+static constexpr u64 PAGE_PER_CHUNK = 8 + 4 + 8 + 4 + RDF_WAVE * 4;   // bits, counts, offsets, owner, refs
 static u32 page_end(const rdf_ctx* c, u32 d0, u32 dmax) {
-    const u64 per_oct = 8 * 8 + 8 + 12 + 8 * 4 + 8 + 4;   // slots, kill mask, counts, pairs, flags / positions, refs
-    const u64 per_chunk = 8 + 4 + 8 + 4 + RDF_WAVE * 4;  // bits, counts, offsets, owner, refs
     u32 d1 = d0 + 1;
     while (d1 < dmax) {
         const u64 oct = c->h_choffl[d1 + 1] - c->h_choffl[d0], ch = c->h_choffh[d1 + 1] - c->h_choffh[d0];
-        if (oct * per_oct + ch * per_chunk > c->pg_budget) break;
+        if (oct * PAGE_PER_OCT + ch * PAGE_PER_CHUNK > c->pg_budget) break;
+        ++d1;
+    }
+    return d1;
+}
+// the same for the unary dependents' output pages, whose explicit pairs are resident: the emission's per-pair scratch
+// (rule flags, positions, output refs) and the heavy work items of the range must fit the budget
+static u32 unary_page_end(const rdf_ctx* c, u32 d0) {
+    const u64 per_pair = 4 + 8 + 4;
+    if (d0 >= c->Cu) return c->Cu;
+    u32 d1 = d0 + 1;
+    while (d1 < c->Cu) {
+        const u64 np = c->h_eoffu[d1 + 1] - c->h_eoffu[d0], ch = c->h_choffh[d1 + 1] - c->h_choffh[d0];
+        if (np * per_pair + ch * PAGE_PER_CHUNK > c->pg_budget) break;
         ++d1;
     }
     return d1;
@@ -2177,10 +2192,10 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    if (!page_bytes) {  // a quarter of the free HBM
+    if (!page_bytes) {  // an eighth of the free HBM, at most 32 GB: the resident unary pairs need the rest
         size_t fr = 0, tot = 0;
         HIP_TRY(c, hipMemGetInfo(&fr, &tot));
-        page_bytes = std::max<u64>(fr / 4, 1ull << 26);
+        page_bytes = std::max<u64>(std::min<u64>(fr / 8, 32ull << 30), 1ull << 26);
     }
     CindView v = make_view(c, flags);
     TRY(d_pivot_local(c, v));
@@ -2215,7 +2230,13 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     }
     c->n_explicit_raw = Eu;
     c->n_light_chunks = WL;
+    // room behind the resident unary pairs for the largest binary page (<= 8 pairs per light octet of the budget), so
+    // the pages append without re-copying the resident pairs
+    HIP_TRY(c, c->epairs.grow_keep((size_t)(Eu + c->pg_budget / PAGE_PER_OCT * 8 + 1) * 8, st));
     TRY(d_explicit_index(c, v, Eu, true));
+    c->h_eoffu.resize(c->Cu + 1ull);  // on the context stream: hipMemcpy would not wait for k_pair_offsets there
+    HIP_TRY(c, hipMemcpyAsync(c->h_eoffu.data(), c->eoff.p, (c->Cu + 1ull) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
     c->hclassed = !v.literal && c->allow_hclass && !v.ar;
     TRY(d_classes_single(c, v, &HC, &NT));
     if (c->hclassed) TRY(d_class_bin(c, v, &WH));
@@ -2257,11 +2278,14 @@ rdf_status rdf_next_page(rdf_ctx* c, uint32_t* done, uint64_t* first_dep, uint64
     v.ebin = c->ebin.as<u64>();
     u32 d0 = 0, d1 = 0;
     *done = 0;
-    if (!c->pg_unary_done) {  // page 0: the unary dependents
-        d1 = c->Cu;
-        TRY(d_page_emit(c, v, 0, c->Cu, 0, c->pg_Eu, c->h_choffh[0], c->h_choffh[c->Cu], c->pg_HC, c->pg_NT));
-        c->pg_unary_done = true;
-        c->pg_next = c->Cu;
+    if (!c->pg_unary_done) {  // the unary dependents (their pairs resident), in ranges; the first holds the class part
+        d0 = c->pg_next;
+        d1 = unary_page_end(c, d0);
+        const bool first = d0 == 0;
+        TRY(d_page_emit(c, v, d0, d1, c->h_eoffu[d0], c->h_eoffu[d1], c->h_choffh[d0], c->h_choffh[d1],
+                        first ? c->pg_HC : 0, first ? c->pg_NT : 0));
+        c->pg_unary_done = d1 >= c->Cu;
+        c->pg_next = d1;
     } else if (c->pg_next < c->C) {  // a range of binary dependents on top of the resident unary pairs
         d0 = c->pg_next;
         d1 = page_end(c, d0, c->C);
@@ -3424,6 +3448,18 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     if (capture_ids && c->C) HIP_TRY(c, hipMemcpyAsync(capture_ids, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
     if (supports && c->C) HIP_TRY(c, hipMemcpyAsync(supports, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
+    return RDF_OK;
+}
+
+rdf_status rdf_copy_result_refs(rdf_ctx* c, uint64_t offset, uint64_t count, uint32_t* refs, uint64_t* n_copied) {
+    if (!c || (count && !refs)) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 nrefs = c->n_out - c->n_class_out;
+    const u64 n = offset < nrefs ? std::min<u64>(count, nrefs - offset) : 0;
+    if (n) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr + offset, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (n_copied) *n_copied = n;
     return RDF_OK;
 }
 

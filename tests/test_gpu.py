@@ -516,6 +516,27 @@ def test_program_host_parser_reproduces_golden(tmp_path, name):
     assert sorted(out.read_text().splitlines()) == expected
 
 
+def test_copy_result_refs_ranges(ctx):
+    """rdf_copy_result_refs (the streaming hand-over of the explicit refs) returns the refs part of the compact result
+    chunk by chunk, with a short last chunk and nothing past the end."""
+    d = synth.config("c1", 0.05)
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    ctx.run(d.min_support)
+    whole = ctx.copy_result_compact()
+    nrefs = ctx.result_layout()["n_refs"]
+    assert nrefs > 1000
+    for chunk in (1, 97, 1 << 12, nrefs, nrefs + 5):
+        buf = np.empty(chunk, np.uint32)
+        got, off = [], 0
+        while off < nrefs:
+            k = ctx.copy_result_refs(off, chunk, buf)
+            assert 0 < k <= chunk
+            got.append(buf[:k].copy())
+            off += k
+        np.testing.assert_array_equal(np.concatenate(got), whole["refs"][:nrefs])
+        assert ctx.copy_result_refs(nrefs, chunk, buf) == 0
+
+
 def test_copy_cinds_decoded_matches_host_decode(ctx):
     """rdf_copy_cinds_decoded (Cind-shaped rows decoded on the device) equals the host decode of rdf_copy_cinds,
     for the whole result and for ranges, in every mode."""

@@ -40,8 +40,12 @@ def fingerprint(d):
     return fp(d)
 
 
+# golden entries whose result exceeds one GPU's HBM at once: checked page by page (test_paged_full_size_vs_oracle)
+PAGED_ONLY = {"c5@1.0/s1_clean"}
+
+
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("key", sorted(GOLD))
+@pytest.mark.parametrize("key", sorted(set(GOLD) - PAGED_ONLY))
 def test_full_size_vs_oracle(ctx, key):
     g = GOLD[key]
     d = dataset(g["config"], g["scale"])
