@@ -205,7 +205,7 @@ def test_heavy_paths_parity(monkeypatch, heavy_min):
     g = _lib.Context(0)
     try:
         rng = random.Random(100 + heavy_min)
-        for _ in range(60):
+        for _ in range(30):
             n = rng.randrange(20, 400)
             nv = rng.randrange(4, 40)
             ms = rng.randrange(1, 4)
@@ -240,7 +240,7 @@ def test_dense_bitmap_paths_parity(monkeypatch):
         g = _lib.Context(0)
         try:
             rng = random.Random(300 + heavy_min)
-            for _ in range(60):
+            for _ in range(30):
                 n = rng.randrange(20, 400)
                 nv = rng.randrange(4, 40)
                 ms = rng.randrange(1, 4)
@@ -285,7 +285,7 @@ def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
     g = _lib.Context(0)
     try:
         rng = random.Random(500 + heavy_min)
-        for _ in range(30):
+        for _ in range(16):
             n = rng.randrange(20, 400)
             nv = rng.randrange(4, 40)
             ms = rng.randrange(1, 4)

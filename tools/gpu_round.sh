@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+      timeout -k 10 1150 python -u -m pytest tests -m gpu -x -v --durations=40 --timeout 600 --timeout-method thread \
         > gpurun_out/tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/tests_$TAG.log; exit 1; } ;;
     bench)
       timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
