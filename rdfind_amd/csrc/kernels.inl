@@ -1559,6 +1559,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_mseg_chunks(const u64* __restrict
     }
 }
 
+// the k_light items of dependents with several candidate chunks (what the two light passes compact), as per-block
+// partials [0] = such items, [1] = all items, [2] = unused
+__global__ __launch_bounds__(RDF_BLOCK) void k_multi_items(const u64* __restrict__ doff, const u32* __restrict__ nitem, u32 C,
+                                                           u64* part) {
+    u64 acc[3] = {0, 0, 0};
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 nseg = (doff[d + 1] - doff[d] + LIGHT_SEG - 1) / LIGHT_SEG;
+        acc[0] += nitem[d] > nseg ? nitem[d] : 0u;
+        acc[1] += nitem[d];
+    }
+    block_partials3(acc, part);
+}
+
 // explicit CSR offsets: eoff[d] = first pair with dep >= d
 // ebin[d] = first explicit pair of d with a binary ref (ref >= Cu)
 __global__ __launch_bounds__(RDF_BLOCK) void k_pair_offsets(const u64* __restrict__ pairs, u64 E, u32 C, u32 Cu, u64* eoff,

@@ -102,7 +102,7 @@ struct rdf_ctx {
     bool hclassed = false;  // binary heavy-only dependents emitted from class lists (single GPU, S2L semantics)
     DevBuf pedges, pedges_tmp;
     u64 ncap = 0;
-    u64 n_explicit_raw = 0, n_light_chunks = 0, n_light_survivors = 0;
+    u64 n_explicit_raw = 0, n_light_chunks = 0, n_light_survivors = 0, n_multi_items = 0;
     rdf_fc_stats fstats = {};
     rdf_group_stats gstats = {};
     rdf_cind_stats cstats = {};
@@ -1524,9 +1524,11 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->npk.as<u32>(), c->pkoff.as<u64>(), C, c->pkoff.as<u64>() + C, st));
-    u64 v[7];
+    u64 v[8];  // [7]: k_multi_items' sum when rdf_discover_cinds launched it (else stale, unused)
     TRY(read_multi(c, {{c->choffl.as<u64>() + C, 8}, {c->pkoff.as<u64>() + C, 8}, {c->choffh.as<u64>() + C, 8},
-                       {dscal(c, 2), 8}, {c->itoffl.as<u64>() + C, 8}, {dscal(c, 3), 8}, {dscal(c, 4), 8}}, v));
+                       {dscal(c, 2), 8}, {c->itoffl.as<u64>() + C, 8}, {dscal(c, 3), 8}, {dscal(c, 4), 8},
+                       {dscal(c, 5), 8}}, v));
+    c->n_multi_items = v[7];
     *WL = v[0];
     *WP = v[1];
     *WH = v[2];
@@ -1674,6 +1676,29 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     TRY(d_light_owners(c, WI, WP, &WM));
     const LightRange r = {0, WI, 0, WP, 0, WM, 0, WL};
     return d_light_run(c, v, pivot, r, 0, E);
+}
+
+// The two light passes pay ~5 host round trips and a dozen launches more than one pass (~0.3 ms); they are taken
+// when the multi-chunk dependents hold at least LIGHT2_MIN_ITEMS k_light items, the work whose repeated group reads
+// the second pass removes.  Measured (profiles/r03_light_two_pass_items.log), multi-chunk items -> light ms one / two
+// passes: c4 at 0.05 1.21M -> 15.2 / 3.3; c3 at 0.5 441k -> 11.5 / 7.5; c5 at 0.1 91k -> 18.2 / 17.0; c1 45k ->
+// 0.99 / 0.95; c2 123 (of 256k items) -> nothing to gain.  RDFIND_LIGHT2=0 / 1 forces one pass / two passes.
+static constexpr u64 LIGHT2_MIN_ITEMS = 1ull << 15;
+// the multi-chunk dependents' k_light items -> dscal(c, 5), read back by d_chunks (c->n_multi_items)
+static rdf_status d_multi_items(rdf_ctx* c) {
+    hipStream_t st = c->stream;
+    const unsigned gp = grid_for(std::max<u32>(c->C, 1), RDF_BLOCK, kGrid);
+    ENSURE(c, ppart, 3ull * gp * 8);
+    hipLaunchKernelGGL(k_multi_items, dim3(gp), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), c->nitl.as<u32>(), c->C,
+                       c->ppart.as<u64>());
+    hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gp, dscal(c, 5));
+    return RDF_OK;
+}
+static bool use_two_pass(const rdf_ctx* c, u64 WI) {
+    static const char* force = getenv("RDFIND_LIGHT2");
+    if (!WI) return false;
+    if (force) return atoi(force) != 0;
+    return c->n_multi_items >= LIGHT2_MIN_ITEMS;
 }
 
 // Two light passes (single GPU).  A k_light work item verifies 64 pivot candidates of one dependent against a segment of
@@ -2042,11 +2067,16 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     }
     tend(c, RDF_T_PIVOT);
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0, H = 0, HC = 0, NT = 0;
+    TRY(d_multi_items(c));
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
-    static const bool two_pass = !getenv("RDFIND_LIGHT2") || atoi(getenv("RDFIND_LIGHT2")) != 0;
     c->n_light_survivors = 0;
-    if (two_pass && WI) TRY(d_light_two_pass(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
+    const bool two = use_two_pass(c, WI);
+    if (two) TRY(d_light_two_pass(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     else TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
+    if (getenv("RDFIND_LIGHT2_LOG"))
+        fprintf(stderr, "LIGHT2 two=%d items=%llu multi_chunk_items=%llu survivors=%llu explicit=%llu\n", (int)two,
+                (unsigned long long)WI, (unsigned long long)c->n_multi_items, (unsigned long long)c->n_light_survivors,
+                (unsigned long long)E);
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));
