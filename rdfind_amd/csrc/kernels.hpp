@@ -71,6 +71,8 @@ static constexpr int LIGHT_STAGE_MIN = RDF_STAGE_MIN;
 static constexpr u64 LIGHT_STAGE_AVG = RDF_STAGE_AVG;  // staging variant when the weighted mean light group is smaller
                   // groups up to this size are searched in LDS (2 KiB per wave)
 
+static constexpr int EMIT_DEDUP_SLOTS = 4096;  // K3 write pass: LDS hash of one iteration's <= 9 x 256 records
+static constexpr u64 EMIT_PAD = ~0ull;         // K3 padding of removed duplicates (no record has all bits set)
 static constexpr u32 PRE_TAG = 0x80000000u;  // light pass A: an unverified survivor (ref bit 31; compact ids < 2^31)
 #ifndef RDF_PRE_MAX
 #define RDF_PRE_MAX 64

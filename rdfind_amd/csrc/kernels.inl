@@ -426,23 +426,75 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                             const u32* __restrict__ lvals, u64 lmask, int proj,
                                                             int joinbits, u32 rank, u32 nranks, u64* block_counts,
-                                                            const u64* __restrict__ block_offsets, u64* out) {
+                                                            const u64* __restrict__ block_offsets, u64* out, int recbits) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
     __shared__ u64 stage[WRITE ? RDF_BLOCK * 9 : 1];  // the iteration's records, written out contiguously
+    __shared__ u64 htab[WRITE ? EMIT_DEDUP_SLOTS : 1];  // the iteration's distinct records (write pass)
     const u64 b = (u64)blockIdx.x * per;
     const u64 e = b + per < n ? b + per : n;
     u64 run = WRITE ? block_offsets[blockIdx.x] : 0;
+#ifndef RDF_EMIT_DEDUP
+#define RDF_EMIT_DEDUP 1
+#endif
+    const bool dedup = WRITE && RDF_EMIT_DEDUP && recbits <= 48;
+    u32 tag = 0;
+    if (dedup) {
+        for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;  // tag 0: empty
+    }
     for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
         u32 c = 0;
         if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, rank, nranks, rec);
         u32 total;
-        const u32 off = block_exclusive_scan_u32(c, lds_wave, &total);
-        if (WRITE) {
-            for (u32 k = 0; k < c; ++k) stage[off + k] = rec[k];
+        if (!WRITE) {
+            block_exclusive_scan_u32(c, lds_wave, &total);
+        } else {
+            // Records repeated within the iteration's 256 triples (the same subject's predicate, the same
+            // (predicate, object) pair: ~23 % of c2's records) are written once; the count pass's region stays
+            // as it is and its tail is padded with EMIT_PAD, which the record sort's first pass drops.  The LDS table
+            // slots carry the iteration's tag in bits 48.. (records have <= 48 bits here), so it is never cleared.
+            u32 keep = (1u << c) - 1u;
+            if (dedup) {
+                ++tag;
+                if (tag == (1u << 15)) {  // tags wrap: clear the table once
+                    for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;
+                    tag = 1;
+                }
+                __syncthreads();
+                keep = 0;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    if ((u32)k >= c) break;
+                    const u64 want = rec[k] | ((u64)tag << 48);
+                    u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
+                    u64 cur = htab[h];
+                    while (true) {
+                        if ((u32)(cur >> 48) != tag) {  // a slot of an earlier iteration: free
+                            const u64 prev = atomicCAS((unsigned long long*)&htab[h], (unsigned long long)cur,
+                                                       (unsigned long long)want);
+                            if (prev == cur) {  // the first copy of the record: kept
+                                keep |= 1u << k;
+                                break;
+                            }
+                            cur = prev;
+                            continue;
+                        }
+                        if (cur == want) break;  // a copy is kept by another record
+                        h = (h + 1) & (EMIT_DEDUP_SLOTS - 1);
+                        cur = htab[h];
+                    }
+                }
+            }
+            u32 kept;
+            const u32 koff = block_exclusive_scan_u32((u32)__popc(keep), lds_wave, &kept);
+            block_exclusive_scan_u32(c, lds_wave, &total);
+            u32 q = koff;
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+                if ((keep >> k) & 1u) stage[q++] = rec[k];
             __syncthreads();
-            for (u32 k = threadIdx.x; k < total; k += RDF_BLOCK) out[run + k] = stage[k];
+            for (u32 k = threadIdx.x; k < total; k += RDF_BLOCK) out[run + k] = k < kept ? stage[k] : EMIT_PAD;
             __syncthreads();
         }
         run += total;

@@ -220,9 +220,11 @@ __device__ inline void load_tile_pairs(const u64* __restrict__ keys, u64 n, u64 
 }
 
 // Digits of DB bits (the pass's width w <= DB is masked at run time: DB only sizes the LDS counters)
+// drop: keys equal to ~0 (padding) are left out of the histogram and of the scattered output (first pass of a sort
+// whose input carries padding; the output then holds only the other keys)
 template <int DB>
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict__ keys, u64 n, int shift, int w,
-                                                           u32* __restrict__ hist, u32 num_tiles) {
+                                                           u32* __restrict__ hist, u32 num_tiles, int drop) {
     constexpr u32 NBIN = 1u << DB;
     __shared__ u32 wcnt[RDF_WAVES_PER_BLOCK][NBIN];
     const int lane = lane_id();
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         const u64 idx = tbase + 2ull * ((u64)(r / 2) * RDF_BLOCK + threadIdx.x) + (r & 1);
-        const bool valid = idx < n;
+        const bool valid = idx < n && !(drop && k[r] == ~0ull);
         const u32 d = (u32)(k[r] >> shift) & dmask;
         const u64 peers = digit_peers<DB>(d, valid);
         if (valid && ((peers >> lane) >> 1) == 0) wcnt[wave][d] += (u32)__popcll(peers);
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
 template <int DB>
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
                                                              int shift, int w, const u32* __restrict__ offs,
-                                                             u32 num_tiles) {
+                                                             u32 num_tiles, int drop) {
     constexpr u32 NBIN = 1u << DB;
     constexpr u32 PER = NBIN / RDF_BLOCK;  // digits per thread in the tile scan (1, 2 or 4)
     static_assert(NBIN % RDF_BLOCK == 0, "digit bins must be a multiple of the block");
@@ -262,6 +264,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     __shared__ u32 tstart[NBIN];
     __shared__ u32 gbase[NBIN];
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
+    __shared__ u32 s_tvalid;
     const int lane = lane_id();
     const int wave = threadIdx.x / RDF_WAVE;
     const u32 nbin = 1u << w, dmask = nbin - 1u;
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     for (int r = 0; r < RS_ITEMS; ++r) k[r] = skeys[wofs + (u32)r * RDF_WAVE + lane];
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn;
+        const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == ~0ull);
         const u32 d = (u32)(k[r] >> shift) & dmask;
         const u64 peers = digit_peers<DB>(d, valid);
         const u32 before = (u32)__popcll(peers & lt);
@@ -319,20 +322,22 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
             tstart[threadIdx.x * PER + q] = off;
             off += run[q];
         }
+        if (threadIdx.x == 0) s_tvalid = total;  // the tile's kept keys (all of them unless padding is dropped)
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        if (wofs + (u32)r * RDF_WAVE + lane < tn) {
+        if (wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == ~0ull)) {
             const u32 d = (u32)(k[r] >> shift) & dmask;
             skeys[tstart[d] + wcount[wave][d] + rank[r]] = k[r];
         }
     }
     __syncthreads();
+    const u32 tv = s_tvalid;
 #pragma unroll
     for (int i = 0; i < RS_ITEMS; ++i) {
         const u32 p = (u32)i * RDF_BLOCK + threadIdx.x;
-        if (p < tn) {
+        if (p < tv) {
             const u64 key = skeys[p];
             const u32 d = (u32)(key >> shift) & dmask;
             out[(u64)gbase[d] + (p - tstart[d])] = key;
@@ -342,13 +347,39 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
 
 template <int DB>
 static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, int shift, int w, u32* hist, u32 tiles,
-                             hipStream_t st) {
+                             hipStream_t st, u32* d_kept = nullptr) {
     const u64 hn = (u64)tiles << w;
-    hipLaunchKernelGGL(k_radix_count<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, tiles);
-    hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, nullptr, st);
+    const int drop = d_kept ? 1 : 0;
+    hipLaunchKernelGGL(k_radix_count<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, tiles, drop);
+    hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, d_kept, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_radix_scatter<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, tiles);
+    hipLaunchKernelGGL(k_radix_scatter<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, tiles, drop);
     return hipSuccess;
+}
+
+// Sort of keys some of which are padding (~0): the first pass drops them, *n_out (host) = the other keys, which the
+// remaining passes sort.  One host read-back between the first and the second pass.
+hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u32* d_kept, u64* n_out,
+                               hipStream_t st) {
+    *n_out = 0;
+    if (n == 0 || bits <= 0) return hipSuccess;
+    if (n >= (1ull << 32)) return hipErrorInvalidValue;
+    const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
+    const int w0 = bits / passes + (0 < bits % passes ? 1 : 0);
+    const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
+    u32* hist = (u32*)ws.scratch(((u64)tiles << RS_MAX_BITS) * sizeof(u32), 1);
+    if (!hist) return hipErrorOutOfMemory;
+    hipError_t e = w0 <= 8 ? radix_pass<8>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept)
+                 : w0 == 9 ? radix_pass<9>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept)
+                           : radix_pass<10>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept);
+    if (e != hipSuccess) return e;
+    u32 kept = 0;
+    e = hipMemcpyAsync(&kept, d_kept, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    std::swap(keys, tmp);
+    *n_out = kept;
+    return radix_sort_u64_bits(ws, keys, tmp, kept, w0, bits, st);
 }
 
 // Passes of at most RS_MAX_BITS bits, as even as possible (43 bits: 9+9+9+8+8 instead of six 8-bit passes)

@@ -58,7 +58,7 @@ struct rdf_ctx {
     // capture groups
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
     DevBuf hist, heavy_list, hbit, bcomp, bkeyc, pcnt, poff, pcur, plist;
-    u64 J = 0, Jf = 0, G = 0;
+    u64 J = 0, Jf = 0, G = 0, J_emit = 0;  // J: distinct-within-iteration records sorted; J_emit: records emitted
     u32 C = 0, Cu = 0, nheavy = 0;
     u64 heavy_threshold = 0;
     int capbits = 0, joinbits = 0;
@@ -1113,23 +1113,25 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     if (n) {
         hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
                            c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, c->rank,
-                           c->nranks, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr);
+                           c->nranks, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
         HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
         hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
                            c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, c->rank,
-                           c->nranks, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>());
+                           c->nranks, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
     }
     tend(c, RDF_T_EMIT);
     TRY(read_scalars(c, 1));
-    const u64 J = c->hscal[0];
-    c->J = J;
+    const u64 Je = c->hscal[0];  // emitted record slots (repeats within an emission iteration are padding)
+    c->J_emit = Je;
     u64* keys = c->rec.as<u64>();
     u64* tmp = c->rec_tmp.as<u64>();
+    u64 J = 0;
     tbegin(c, RDF_T_SORT);
-    HIP_TRY(c, radix_sort_u64(c->ws, keys, tmp, J, capbits + joinbits, st));
+    HIP_TRY(c, radix_sort_u64_drop(c->ws, keys, tmp, Je, capbits + joinbits, (u32*)dscal(c, 1), &J, st));
     tend(c, RDF_T_SORT);
+    c->J = J;
     c->rec_sorted = keys;
-    c->sort_passes_records = (u64)((capbits + joinbits + RS_MAX_BITS - 1) / RS_MAX_BITS) * J;
+    c->sort_passes_records = Je + (u64)((capbits + joinbits + RS_MAX_BITS - 1) / RS_MAX_BITS - 1) * J;
     // supports = distinct join values per capture: fresh (capture, join) records counted per key run
     ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
     ENSURE(c, flags, std::max<u64>(J, 1) * 4);
@@ -1316,7 +1318,7 @@ static rdf_status g_heavy_binary(rdf_ctx* c, u64 thr, u32 base) {
 static void fill_group_stats(rdf_ctx* c) {
     rdf_group_stats& s = c->gstats;
     memset(&s, 0, sizeof(s));
-    s.n_records = c->J;
+    s.n_records = c->J_emit;
     s.n_frequent_records = c->Jf;
     s.n_groups = c->G;
     s.n_captures = c->C;

@@ -30,7 +30,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
                 kt = ctx.kernel_times()
                 best = kt if best is None or kt["light"] < best["light"] else best
             out[spec] = {"light": round(best["light"], 3), "pivot": round(best["pivot"], 3),
-                         "binary": round(best["binary"], 3), "unary": round(best["unary"], 3), "sort": round(best["sort"], 3), "groups": round(best["groups"], 3),
+                         "binary": round(best["binary"], 3), "unary": round(best["unary"], 3), "sort": round(best["sort"], 3), "groups": round(best["groups"], 3), "emit": round(best["emit"], 3), "support": round(best["support"], 3),
                          "total": round(sum(best.values()), 3), "n": ctx.cind_count(), "sum": ctx.checksum()}
     print("AB", json.dumps(out), flush=True)
     sys.exit(0)
