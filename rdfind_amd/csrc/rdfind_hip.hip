@@ -148,7 +148,8 @@ struct rdf_ctx {
     hipEvent_t ev[8] = {};
     float stage_ms[3] = {0, 0, 0};
     // per kernel-family device timers (events on the context stream)
-    static constexpr int kTSeg = 6;  // segments per timer (a kernel family may run in several places)
+    static constexpr int kTSeg = 32;  // segments per timer (a kernel family may run in several places: the two light
+                                      // passes record ~14 light segments)
     hipEvent_t tev[2 * RDF_NUM_TIMERS * kTSeg] = {};
     int tn[RDF_NUM_TIMERS] = {};
     float tms[RDF_NUM_TIMERS] = {};
@@ -1680,12 +1681,12 @@ static rdf_status d_light(rdf_ctx* c, const CindView& v, u64 WI, u64 WL, u64 WP,
     return d_light_run(c, v, pivot, r, 0, E);
 }
 
-// The two light passes pay ~5 host round trips and a dozen launches more than one pass (~0.3 ms); they are taken
-// when the multi-chunk dependents hold at least LIGHT2_MIN_ITEMS k_light items, the work whose repeated group reads
-// the second pass removes.  Measured (profiles/r03_light_two_pass_items.log), multi-chunk items -> light ms one / two
-// passes: c4 at 0.05 1.21M -> 15.2 / 3.3; c3 at 0.5 441k -> 11.5 / 7.5; c5 at 0.1 91k -> 18.2 / 17.0; c1 45k ->
-// 0.99 / 0.95; c2 123 (of 256k items) -> nothing to gain.  RDFIND_LIGHT2=0 / 1 forces one pass / two passes.
-static constexpr u64 LIGHT2_MIN_ITEMS = 1ull << 15;
+// The two light passes pay ~5 host round trips and a dozen launches more than one pass; they are taken when the
+// multi-chunk dependents hold at least LIGHT2_MIN_ITEMS k_light items, the work whose repeated group reads the second
+// pass removes.  Measured by the device-resident step (profiles/r03_light_two_pass_steps.log), multi-chunk items ->
+// ms one / two passes: c4 at 0.05 1.21M -> 40.4 / 39.3; c3 at 0.5 441k -> 42.7 / 42.8; c5 at 0.1 91k -> 60.2 / 62.7;
+// c1 45k -> 3.37 / 3.73; c2 123 (of 256k items) -> nothing to gain.  RDFIND_LIGHT2=0 / 1 forces one / two passes.
+static constexpr u64 LIGHT2_MIN_ITEMS = 1ull << 20;
 // the multi-chunk dependents' k_light items -> dscal(c, 5), read back by d_chunks (c->n_multi_items)
 static rdf_status d_multi_items(rdf_ctx* c) {
     hipStream_t st = c->stream;

@@ -136,11 +136,11 @@ with _lib.Context(0) as ctx:
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("env", [{"RDFIND_STAGE": "0"}, {"RDFIND_STAGE": "1"},
                                  {"RDFIND_SIG": "0", "RDFIND_PIV2": "0"}, {"RDFIND_SIG": "1", "RDFIND_PIV2": "2"},
-                                 {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}, {"RDFIND_LIGHT2": "0"}])
+                                 {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}, {"RDFIND_LIGHT2": "1"}])
 def test_light_variants_full_size(env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
-    paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, one light pass
-    instead of the filter and verify passes) each reproduce the c1 and c2 golden vectors.  The switches are read
+    paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
+    verify passes forced instead of one light pass) each reproduce the c1 and c2 golden vectors.  The switches are read
     once per process, so each combination runs in its own child process."""
     import subprocess
     import sys
@@ -181,3 +181,45 @@ def test_paged_full_size_vs_oracle(ctx, key, page_bytes):
         pages += 1
     assert pages >= 2
     assert n == g["n_cinds"] and h == int(g["checksum"]) and hc == h
+
+
+_TWO_PASS_CHILD = r"""
+import json, random, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from rdfind_amd import _lib
+from oracle import c_oracle as C
+rng = random.Random(int(sys.argv[2]))
+bad = []
+with _lib.Context(0) as g:
+    for it in range(40):
+        n = rng.randrange(50, 600)
+        nv = rng.randrange(4, 40)
+        ms = rng.randrange(1, 3)
+        arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
+                       dtype=np.uint32)
+        for strategy, clean in ((1, True), (0, True), (0, False)):
+            exp, _ = C.run_set(arr[:, 0], arr[:, 1], arr[:, 2], nv, ms, strategy, clean)
+            g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+            g.run(ms, "spo", clean, strategy)
+            if _lib.decoded_to_set(g.decoded_cinds()) != exp:
+                bad.append((it, n, nv, ms, strategy, clean))
+print(json.dumps({"bad": bad}))
+"""
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("heavy_min", ["64", "2"])
+def test_two_light_passes_random(heavy_min):
+    """The filter + verify light passes forced on random inputs (RDFIND_LIGHT2=1; LIGHT_PRE_MAX defers every chunk of
+    a multi-chunk dependent) against the C oracle in three modes, with and without lowered heavy columns.  In its own
+    process: the switch is read once per process."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RDFIND_LIGHT2="1", RDFIND_HEAVY_MIN=heavy_min)
+    r = subprocess.run([sys.executable, "-c", _TWO_PASS_CHILD, root, "71" + heavy_min], env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["bad"] == []
