@@ -83,7 +83,8 @@ def algorithmic_bytes(name, d, fc, gs, cs, counts):
     if name == "sort":
         return 16 * counts["sort_passes_records"]       # read + write each record once per digit pass
     if name == "support":
-        return 12 * J + 16 * Jf                         # read records + write fresh flags; dk + fk per kept record
+        Js = gs.get("n_sorted_records", J)              # the sorted records (an emission iteration's repeats dropped)
+        return 12 * Js + 16 * Jf                        # read records + write fresh flags; dk + fk per kept record
     if name == "groups":
         return 16 * Jf * counts["group_passes"] + 32 * Jf   # fk sort passes; flags/build/gcap/dgrp gathers
     if name == "pivot":
@@ -352,7 +353,8 @@ def main():
     capbits = int(2 * sum(fc["n_frequent_unary"]) + fc["n_frequent_binary"] - 1).bit_length()  # compact capture ids
     joinbits = max(int(V - 1).bit_length(), 1)
     rs = RADIX_MAX_BITS  # digits of <= 10 bits (primitives.hip RS_MAX_BITS)
-    counts = {"sort_passes_records": ((capbits + joinbits + rs - 1) // rs) * gs["n_records"],
+    # the first pass reads every emitted record slot, the others only the records it kept (repeats dropped)
+    counts = {"sort_passes_records": gs["n_records"] + ((capbits + joinbits + rs - 1) // rs - 1) * gs["n_sorted_records"],
               "group_passes": (joinbits + rs - 1) // rs}
     fams = family_rooflines(d, fc, gs, cs, kt, counts)
     if total_scale == 1.0 and world == 1:  # HBM bytes per step from the committed PMC summary of this config

@@ -70,6 +70,8 @@ typedef struct {
     uint64_t n_unary_captures;
     uint64_t n_heavy_groups;        /* groups tracked as bitmask columns */
     uint64_t heavy_threshold;       /* minimum size of a heavy group */
+    uint64_t n_sorted_records;      /* records the join-partner sort keeps after its first pass (an emission iteration's
+                                       repeats dropped) */
 } rdf_group_stats;
 
 typedef struct {

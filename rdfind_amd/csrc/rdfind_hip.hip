@@ -1320,6 +1320,7 @@ static void fill_group_stats(rdf_ctx* c) {
     rdf_group_stats& s = c->gstats;
     memset(&s, 0, sizeof(s));
     s.n_records = c->J_emit;
+    s.n_sorted_records = c->J;
     s.n_frequent_records = c->Jf;
     s.n_groups = c->G;
     s.n_captures = c->C;
