@@ -382,38 +382,42 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
 // contiguous, so its support is a run length (no atomics) and its join list is the dependent -> groups CSR.
 
 // records of triple i (at most 9); returns the count
+// rep (optional): bit k set for the records that repeat across triples of one subject or one (predicate, object) pair
+// (p[s], s[p], o[p], p[o]: the same predicate twice for a subject, the same typed object for many subjects); the others
+// (o[s], s[o] and the binary captures) practically never repeat within an emission iteration
 __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
                                      u32 V, u32 twoU, const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                      const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, u32 rank, u32 nranks,
-                                     u64 (&rec)[9]) {
-    u32 c = 0;
+                                     u64 (&rec)[9], u32* rep = nullptr) {
+    u32 c = 0, rp_mask = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
     const u32 rs = frank[ts], rp = frank[(u64)V + tp], ro = frank[2ull * V + to];  // global condition ranks (or NONE)
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
     if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
         if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
-        if (fp) rec[c++] = ((2ull * rp + 1) << joinbits) | to;
+        if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp + 1) << joinbits) | to; }
         if (fs && fp) {
             u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
         }
     }
     if ((proj & 2) && shard_of(tp, nranks) == rank) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
-        if (fs) rec[c++] = ((2ull * rs) << joinbits) | tp;
-        if (fo) rec[c++] = ((2ull * ro + 1) << joinbits) | tp;
+        if (fs) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
+        if (fo) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
         if (fs && fo) {
             u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
         }
     }
     if ((proj & 1) && shard_of(ts, nranks) == rank) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
-        if (fp) rec[c++] = ((2ull * rp) << joinbits) | ts;
+        if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
         if (fo) rec[c++] = ((2ull * ro) << joinbits) | ts;
         if (fp && fo) {
             u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | ts;
         }
     }
+    if (rep) *rep = rp_mask;
     return c;
 }
 
@@ -444,14 +448,15 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
     for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
-        u32 c = 0;
-        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, rank, nranks, rec);
+        u32 c = 0, rep = 0;
+        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, rank, nranks, rec, &rep);
         u32 total;
         if (!WRITE) {
             block_exclusive_scan_u32(c, lds_wave, &total);
         } else {
             // Records repeated within the iteration's 256 triples (the same subject's predicate, the same
-            // (predicate, object) pair: ~23 % of c2's records) are written once; the count pass's region stays
+            // (predicate, object) pair: ~23 % of c2's records; only the kinds flagged by triple_records are looked up)
+            // are written once; the count pass's region stays
             // as it is and its tail is padded with EMIT_PAD, which the record sort's first pass drops.  The LDS table
             // slots carry the iteration's tag in bits 48.. (records have <= 48 bits here), so it is never cleared.
             u32 keep = (1u << c) - 1u;
@@ -462,10 +467,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                     tag = 1;
                 }
                 __syncthreads();
-                keep = 0;
-#pragma unroll
+                keep = ((1u << c) - 1u) & ~rep;  // only the repeating kinds go through the table
                 for (int k = 0; k < 9; ++k) {
                     if ((u32)k >= c) break;
+                    if (!((rep >> k) & 1u)) continue;
                     const u64 want = rec[k] | ((u64)tag << 48);
                     u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
                     u64 cur = htab[h];
