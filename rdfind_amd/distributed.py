@@ -50,15 +50,23 @@ def _dtype(op):
 
 
 def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
-    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order (one broadcast per rank
-    into its exact slice of the result: no padding to the largest contribution)."""
+    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order.  Balanced contributions
+    (padding to the largest adds <= 50 %) go through one all-gather of padded slices; skewed ones through one
+    broadcast per rank into its exact slice of the result (no padding)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n, group=group)
     counts = [int(c.item()) for c in counts]
-    out = send.new_empty(sum(counts))
+    mx, tot = max(counts), sum(counts)
+    if mx and 2 * world * mx <= 3 * tot:
+        pad = send.new_zeros(mx)
+        pad[: send.numel()].copy_(send)
+        parts = [send.new_empty(mx) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        return torch.cat([p[:c] for p, c in zip(parts, counts)])
+    out = send.new_empty(tot)
     off = 0
     for r, c in enumerate(counts):
         if c:

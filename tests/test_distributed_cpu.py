@@ -90,7 +90,8 @@ def test_sharded_protocol_matches_oracle(world, local_slice):
 
 
 def test_exchange_helpers_gloo():
-    """allgatherv / alltoallv with ragged and empty contributions."""
+    """allgatherv (padded all-gather for balanced contributions, broadcasts for skewed ones) / alltoallv with ragged
+    and empty contributions."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -103,6 +104,7 @@ def test_exchange_helpers_gloo():
         assert p.exitcode == 0
     assert got[0]["ag"] == [0, 1, 2, 10] and got[1]["ag"] == [0, 1, 2, 10]
     assert got[0]["empty"] == [] and got[1]["empty"] == []
+    assert got[0]["skew"] == list(range(10)) + [77] and got[1]["skew"] == got[0]["skew"]
     # rank 0 sends [100] to 0 and [101, 102] to 1; rank 1 sends [] to 0 and [200] to 1
     assert got[0]["a2a"] == [100] and got[1]["a2a"] == [101, 102, 200]
 
@@ -119,10 +121,12 @@ def _helpers_worker(rank, world, port, q):
         send = torch.tensor([0, 1, 2] if rank == 0 else [10], dtype=torch.int64)
         ag = distributed.allgatherv(send).tolist()
         empty = distributed.allgatherv(torch.zeros(0, dtype=torch.int64)).tolist()
+        skew = distributed.allgatherv(torch.arange(10, dtype=torch.int64) if rank == 0 else  # broadcasts (skewed)
+                                      torch.tensor([77], dtype=torch.int64)).tolist()
         if rank == 0:
             a2a = distributed.alltoallv(torch.tensor([100, 101, 102], dtype=torch.int64), [1, 2]).tolist()
         else:
             a2a = distributed.alltoallv(torch.tensor([200], dtype=torch.int64), [0, 1]).tolist()
-        q.put((rank, {"ag": ag, "empty": empty, "a2a": a2a}))
+        q.put((rank, {"ag": ag, "empty": empty, "skew": skew, "a2a": a2a}))
     finally:
         dist.destroy_process_group()
