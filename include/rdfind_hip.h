@@ -72,6 +72,8 @@ typedef struct {
     uint64_t heavy_threshold;       /* minimum size of a heavy group */
     uint64_t n_sorted_records;      /* records the join-partner sort keeps after its first pass (an emission iteration's
                                        repeats dropped) */
+    uint64_t n_join_ranges;         /* join-value ranges the groups were built in (1; more for inputs of >= 2^32/9
+                                       triples, whose records exceed one sort: Flink's spilling groupBy, RDFind.scala:339-345) */
 } rdf_group_stats;
 
 typedef struct {

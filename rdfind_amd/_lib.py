@@ -56,7 +56,8 @@ class GroupStats(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint64), ("n_frequent_records", ctypes.c_uint64),
                 ("n_groups", ctypes.c_uint64), ("n_captures", ctypes.c_uint64),
                 ("n_unary_captures", ctypes.c_uint64), ("n_heavy_groups", ctypes.c_uint64),
-                ("heavy_threshold", ctypes.c_uint64), ("n_sorted_records", ctypes.c_uint64)]
+                ("heavy_threshold", ctypes.c_uint64), ("n_sorted_records", ctypes.c_uint64),
+                ("n_join_ranges", ctypes.c_uint64)]
 
 
 class CindStats(ctypes.Structure):

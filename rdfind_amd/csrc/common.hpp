@@ -42,6 +42,16 @@ __host__ __device__ inline u32 shard_of(u32 join, u32 nranks) {
     return nranks <= 1 ? 0u : (u32)((((u64)join * 0x9E3779B97F4A7C15ull) >> 32) % nranks);
 }
 
+// join values whose capture records a K3 emission writes: this rank's shard (hash) and, when the capture groups are
+// built in join-value ranges (one GPU, inputs whose records exceed one pass), the range [lo, hi)
+struct JoinSel {
+    u32 rank, nranks, lo, hi;
+    __host__ __device__ inline bool take(u32 join) const {
+        return shard_of(join, nranks) == rank && join >= lo && join < hi;
+    }
+};
+static constexpr u32 JOIN_ALL_HI = 0xffffffffu;
+
 __device__ inline u32 hash32(u32 x) {
     x ^= x >> 16;
     x *= 0x7feb352dU;

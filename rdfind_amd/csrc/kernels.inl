@@ -387,13 +387,13 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
 // (o[s], s[o] and the binary captures) practically never repeat within an emission iteration
 __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
                                      u32 V, u32 twoU, const u32* __restrict__ frank, const u64* __restrict__ lkeys,
-                                     const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, u32 rank, u32 nranks,
+                                     const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, JoinSel js,
                                      u64 (&rec)[9], u32* rep = nullptr) {
     u32 c = 0, rp_mask = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
     const u32 rs = frank[ts], rp = frank[(u64)V + tp], ro = frank[2ull * V + to];  // global condition ranks (or NONE)
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
-    if ((proj & 4) && shard_of(to, nranks) == rank) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
+    if ((proj & 4) && js.take(to)) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
         if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp + 1) << joinbits) | to; }
         if (fs && fp) {
@@ -401,7 +401,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
         }
     }
-    if ((proj & 2) && shard_of(tp, nranks) == rank) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
+    if ((proj & 2) && js.take(tp)) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
         if (fs) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
         if (fo) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
         if (fs && fo) {
@@ -409,7 +409,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
         }
     }
-    if ((proj & 1) && shard_of(ts, nranks) == rank) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
+    if ((proj & 1) && js.take(ts)) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
         if (fo) rec[c++] = ((2ull * ro) << joinbits) | ts;
         if (fp && fo) {
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
                                                             const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                             const u32* __restrict__ lvals, u64 lmask, int proj,
-                                                            int joinbits, u32 rank, u32 nranks, u64* block_counts,
+                                                            int joinbits, JoinSel js, u64* block_counts,
                                                             const u64* __restrict__ block_offsets, u64* out, int recbits) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
     __shared__ u64 stage[WRITE ? RDF_BLOCK * 9 : 1];  // the iteration's records, written out contiguously
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
         u32 c = 0, rep = 0;
-        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, rank, nranks, rec, &rep);
+        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, &rep);
         u32 total;
         if (!WRITE) {
             block_exclusive_scan_u32(c, lds_wave, &total);
@@ -621,6 +621,77 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_info_support_u32(const CapInfo* _
 __global__ __launch_bounds__(RDF_BLOCK) void k_key_offsets(const u64* __restrict__ keys, u64 n, u32 C, u64* off) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d <= C; d += (u64)gridDim.x * RDF_BLOCK)
         off[d] = lower_bound_u64(keys, n, d << 32);
+}
+
+// ---- capture groups built in join-value ranges (one GPU, more records than one sort pass holds) -----------------
+// Records of join value j all lie in one range, so a range's groups are whole; ranges ascend, so group ids, the
+// members of each group and every dependent's group list come out exactly as the one-pass build makes them.
+
+// records per join bucket (join >> jshift, JH_BUCKETS buckets): the K3 count pass's per-triple record counts split by
+// their join value (o, p or s of the triple), LDS-privatised
+static constexpr u32 JH_BUCKETS = 1u << 14;
+__global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_hist(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                              const u32* __restrict__ o, u64 n, u32 V, u32 twoU,
+                                                              const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                                              const u32* __restrict__ lvals, u64 lmask, int proj,
+                                                              int joinbits, int jshift, u64* hist) {
+    __shared__ u32 lh[JH_BUCKETS];
+    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lh[k] = 0;
+    __syncthreads();
+    const JoinSel all = {0u, 1u, 0u, JOIN_ALL_HI};
+    const u64 jmask = (1ull << joinbits) - 1;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        u64 rec[9];
+        const u32 c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, all, rec);
+        // a triple's records are grouped by join value (o, then p, then s): one LDS atomic per run
+        u32 k = 0;
+        while (k < c) {
+            const u64 j = rec[k] & jmask;
+            u32 r = 1;
+            while (k + r < c && (rec[k + r] & jmask) == j) ++r;
+            atomicAdd(&lh[(u32)(j >> jshift)], r);
+            k += r;
+        }
+    }
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK)
+        if (lh[k]) atomicAdd(&hist[k], (u64)lh[k]);
+}
+
+// a range's groups: goff[gbase + g] = rbase + first member, gcap[rbase + i], gmap[join] = gbase + g
+__global__ __launch_bounds__(RDF_BLOCK) void k_group_build_at(const u64* __restrict__ fk, u64 n, const u32* __restrict__ gflag,
+                                                              const u32* __restrict__ gexcl, u64 rbase, u32 gbase, u64* goff,
+                                                              u32* gcap, u32* gmap) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = fk[i];
+        gcap[rbase + i] = (u32)(k & 0xffffffffu);
+        if (gflag[i]) {
+            const u32 g = gbase + gexcl[i];
+            goff[g] = rbase + i;
+            gmap[k >> 32] = g;
+        }
+    }
+}
+
+// a range's dependent -> group entries: dk (compact capture << 32 | join, (capture, join) order) with this range's
+// per-dependent offsets offp; dependent d's entries go behind the dcur[d] entries of earlier ranges
+__global__ __launch_bounds__(RDF_BLOCK) void k_dgrp_range(const u64* __restrict__ dk, u64 n, const u64* __restrict__ offp,
+                                                          const u64* __restrict__ doff, const u32* __restrict__ dcur,
+                                                          const u32* __restrict__ gmap, u32* dgrp) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = dk[i];
+        const u32 d = (u32)(k >> 32);
+        dgrp[doff[d] + dcur[d] + (i - offp[d])] = gmap[(u32)k];
+    }
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_dcur_add(const u64* __restrict__ offp, u32 C, u32* dcur) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK)
+        dcur[d] += (u32)(offp[d + 1] - offp[d]);
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_add_u32(u32* a, const u32* __restrict__ b, u64 n) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) a[i] += b[i];
 }
 
 

@@ -58,6 +58,9 @@ struct rdf_ctx {
     // capture groups
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
     DevBuf hist, heavy_list, hbit, bcomp, bkeyc, pcnt, poff, pcur, plist;
+    DevBuf jhist, rsup, offp;  // capture groups built in join-value ranges (g_build_ranges)
+    u64 group_range_records = 0;  // RDFIND_GROUP_RANGE test hook: records per join range (0: automatic)
+    u64 n_group_ranges = 1;
     u64 J = 0, Jf = 0, G = 0, J_emit = 0;  // J: distinct-within-iteration records sorted; J_emit: records emitted
     u32 C = 0, Cu = 0, nheavy = 0;
     u64 heavy_threshold = 0;
@@ -282,7 +285,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
                       &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
                       &c->gcap, &c->gmap, &c->csup,
-                      &c->doff, &c->dcur, &c->dgrp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
+                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
@@ -322,6 +325,10 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     // dense light-group bitmaps: RDFIND_DENSE=<divisor> (groups of >= C / divisor members; 0 = off) and the test hook
     // RDFIND_DENSE_MIN=<members> (absolute minimum, default LIGHT_DENSE_MIN)
     if (const char* dd = getenv("RDFIND_DENSE")) c->dense_div = atoi(dd);
+    // test hook: RDFIND_GROUP_RANGE=<records> builds the capture groups in join-value ranges of at most that many
+    // K3 records (the path inputs of >= 2^32 / 9 triples take), so small parity inputs run it
+    if (const char* gr = getenv("RDFIND_GROUP_RANGE"))
+        if (atoll(gr) > 0) c->group_range_records = (u64)atoll(gr);
     if (const char* dm = getenv("RDFIND_DENSE_MIN"))
         if (atoll(dm) > 0) c->dense_min = (u64)atoll(dm);
     hipError_t e = hipSetDevice(device);
@@ -369,9 +376,11 @@ rdf_status rdf_device_bytes(rdf_ctx* c, uint64_t* bytes) {
     return RDF_OK;
 }
 
+// Per-context input limits: term ids < 2^30 (binary keys, K2's count bits); 3n K1/K2 records addressed by u32 offsets.
+// Inputs of >= 2^32 / 9 triples build their capture groups in join-value ranges (g_build_ranges).
 static rdf_status check_terms(rdf_ctx* c, u64 n, u32 num_terms) {
     if (num_terms >= (1u << 30)) return fail(c, RDF_ERR_LIMIT, "num_terms must be < 2^30");
-    if (n >= (1ull << 32) / 9) return fail(c, RDF_ERR_LIMIT, "n must be < 2^32/9 triples per GPU (shard larger inputs)");
+    if (n >= (1ull << 32) / 3) return fail(c, RDF_ERR_LIMIT, "n must be < 2^32/3 triples per GPU (shard larger inputs)");
     return RDF_OK;
 }
 
@@ -391,6 +400,7 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next) {
         if (!kept(b)) held += b->cap;
     if (held <= std::max<u64>(4ull << 30, n_next << 10)) return;
     (void)hipStreamSynchronize(c->stream);
+    c->paged = false;
     for (DevBuf* b : ctx_buffers(c))
         if (!kept(b)) b->release();
     c->ws.release();
@@ -423,6 +433,7 @@ rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, con
     c->n = n;
     c->V = num_terms;
     c->stage = 1;
+    c->paged = false;  // a paged run's state belongs to the previous input
     c->parsed_dict = false;
     c->ingest_sharded = false;
     return RDF_OK;
@@ -439,6 +450,7 @@ rdf_status rdf_set_triples_device(rdf_ctx* c, const uint32_t* s, const uint32_t*
     c->n = n;
     c->V = num_terms;
     c->stage = 1;
+    c->paged = false;  // a paged run's state belongs to the previous input
     c->parsed_dict = false;
     c->ingest_sharded = false;
     return RDF_OK;
@@ -489,6 +501,7 @@ rdf_status rdf_distinct_triples(rdf_ctx* c, uint64_t* n_distinct, float* ms) {
     if (ms) HIP_TRY(c, hipEventElapsedTime(ms, c->ev[6], c->ev[7]));
     c->n = kept;
     c->stage = 1;
+    c->paged = false;  // a paged run's state belongs to the previous input
     if (n_distinct) *n_distinct = kept;
     return RDF_OK;
 }
@@ -593,6 +606,7 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
     c->n = n;
     c->V = (u32)V;
     c->stage = 1;
+    c->paged = false;  // a paged run's state belongs to the previous input
     c->n_terms_parsed = V;
     c->parsed_dict = true;
     c->ingest_sharded = false;
@@ -1089,10 +1103,8 @@ static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj
 }
 
 
-// K3 emission of this rank's join shard, K4 sort by (join, capture), K5 local supports -> c->support[ncap]
-static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
-    hipStream_t st = c->stream;
-    const u64 n = c->n;
+// record key layout of this run's K3 records: capture << joinbits | join
+static rdf_status g_record_bits(rdf_ctx* c) {
     const u32 V = c->V ? c->V : 1;
     const u64 ncap = 2ull * c->U + c->B;  // compact candidate captures (k_frank_final)
     const int capbits = bits_for(ncap ? ncap - 1 : 0);
@@ -1102,39 +1114,49 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     c->capbits = capbits;
     c->joinbits = joinbits;
     c->ncap = ncap;
-    HIP_TRY(c, hipEventRecord(c->ev[2], st));
+    return RDF_OK;
+}
+
+// K3 emission of the selected join values (record buffers of cap_rec slots), K4 sort by (capture, join), K5 run
+// bounds (cstart), fresh-record scan (fpos) and the records' supports -> sup[ncap].  The sorted records are left in
+// c->rec_sorted; *Jout = their number.  Adds to c->J_emit and c->sort_passes_records.
+static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u32* sup, u64* Jout) {
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const u32 V = c->V ? c->V : 1;
+    const u64 ncap = c->ncap;
+    const int capbits = c->capbits, joinbits = c->joinbits;
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
-    const u64 cap_rec = std::max<u64>(9 * n, 1);
-    ENSURE(c, rec, cap_rec * 8);
-    ENSURE(c, rec_tmp, cap_rec * 8);
+    ENSURE(c, rec, std::max<u64>(cap_rec, 1) * 8);
+    ENSURE(c, rec_tmp, std::max<u64>(cap_rec, 1) * 8);
     tbegin(c, RDF_T_EMIT);
     const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
     const u64 per = n ? (n + eg - 1) / eg : 0;
     ENSURE(c, eblk, (eg + 1ull) * 8);
     if (n) {
         hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, c->rank,
-                           c->nranks, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
+                           c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
         HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
         hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, c->rank,
-                           c->nranks, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
+                           (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
     }
     tend(c, RDF_T_EMIT);
     TRY(read_scalars(c, 1));
     const u64 Je = c->hscal[0];  // emitted record slots (repeats within an emission iteration are padding)
-    c->J_emit = Je;
+    if (Je > cap_rec) return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
+    c->J_emit += Je;
     u64* keys = c->rec.as<u64>();
     u64* tmp = c->rec_tmp.as<u64>();
     u64 J = 0;
     tbegin(c, RDF_T_SORT);
     HIP_TRY(c, radix_sort_u64_drop(c->ws, keys, tmp, Je, capbits + joinbits, (u32*)dscal(c, 1), &J, st));
     tend(c, RDF_T_SORT);
-    c->J = J;
+    *Jout = J;
     c->rec_sorted = keys;
-    c->sort_passes_records = Je + (u64)((capbits + joinbits + RS_MAX_BITS - 1) / RS_MAX_BITS - 1) * J;
+    c->sort_passes_records += Je + (u64)((capbits + joinbits + RS_MAX_BITS - 1) / RS_MAX_BITS - 1) * J;
     // supports = distinct join values per capture: fresh (capture, join) records counted per key run
-    ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
     ENSURE(c, flags, std::max<u64>(J, 1) * 4);
     ENSURE(c, fpos, (J + 1) * 4);
     ENSURE(c, cstart, (ncap + 1) * 4);
@@ -1144,20 +1166,30 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), J, c->fpos.as<u32>() + J, st));
     if (ncap)
         hipLaunchKernelGGL(k_run_support, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cstart.as<u32>(),
-                           ncap, c->fpos.as<u32>(), c->support.as<u32>());
+                           ncap, c->fpos.as<u32>(), sup);
     tend(c, RDF_T_SUPPORT);
     return RDF_OK;
 }
 
-// frequent-capture compaction (c->support = global supports), capture groups, dependent -> groups CSR
-static rdf_status g_compact_groups(rdf_ctx* c) {
+// K3 emission of this rank's join shard, K4 sort by (capture, join), K5 local supports -> c->support[ncap]
+static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
+    TRY(g_record_bits(c));
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    c->J_emit = 0;
+    c->sort_passes_records = 0;
+    ENSURE(c, support, std::max<u64>(c->ncap, 1) * 4);
+    u64 J = 0;
+    TRY(g_emit_range(c, proj, JoinSel{c->rank, c->nranks, 0u, JOIN_ALL_HI}, 9 * c->n, c->support.as<u32>(), &J));
+    c->J = J;
+    return RDF_OK;
+}
+
+// frequent-capture compaction (c->support = global supports): C, Cu, fidx, fcap, info, fext
+static rdf_status g_compact_captures(rdf_ctx* c) {
     hipStream_t st = c->stream;
     const u32 V = c->V ? c->V : 1;
-    const u64 ncap = c->ncap, J = c->J;
-    const int joinbits = c->joinbits;
-    u64* keys = c->rec_sorted;
-    tbegin(c, RDF_T_SUPPORT);
-    ENSURE(c, flags, std::max(J, ncap) * 4);
+    const u64 ncap = c->ncap;
+    ENSURE(c, flags, std::max<u64>(ncap, 1) * 4);
     ENSURE(c, fidx, (ncap + 1) * 4);
     hipLaunchKernelGGL(k_support_flags, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
@@ -1179,6 +1211,20 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     if (C)
         hipLaunchKernelGGL(k_external_ids, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fcap.as<u32>(), C,
                            2u * c->U, V, c->fval.as<u32>(), c->Us, c->Up, c->fext.as<u32>());
+    return RDF_OK;
+}
+
+// frequent-capture compaction (c->support = global supports), capture groups, dependent -> groups CSR
+static rdf_status g_compact_groups(rdf_ctx* c) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 ncap = c->ncap, J = c->J;
+    const int joinbits = c->joinbits;
+    u64* keys = c->rec_sorted;
+    tbegin(c, RDF_T_SUPPORT);
+    ENSURE(c, flags, std::max(J, ncap) * 4);
+    TRY(g_compact_captures(c));
+    const u32 C = c->C;
     // distinct records of frequent captures -> dk = (compact capture << 32 | join) in (capture, join) order,
     // written to the record buffer that does not hold the sorted keys
     ENSURE(c, skip, (ncap + 1) * 4);
@@ -1240,6 +1286,179 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(c->goff.as<u64>() + G, c->hscal + 14, 8, hipMemcpyHostToDevice, st));
     tend(c, RDF_T_GROUPS);
     return RDF_OK;
+}
+
+// Capture groups of one GPU in ranges of join values, for inputs whose K3 records exceed what one sort holds (the u32
+// record offsets of K4/K5: n >= 2^32 / 9 triples; c4 at full size emits ~5.8·10^9 records) or the memory of one pass.
+// The reference has no such ceiling: Flink's sort-based groupBy("joinValue") spills (ALG/programs/RDFind.scala:339-345).
+//  1. records per join bucket (k_emit_join_hist) -> consecutive bucket ranges of at most max_range records each;
+//  2. per range: K3-K5 (g_emit_range), its supports summed into c->support (a join value's records are all in one
+//     range, so the ranges' distinct (capture, join) counts add up);
+//  3. capture compaction; doff = scan of the frequent supports (a frequent capture keeps one record per join value);
+//  4. per range again: K3-K5, the kept records -> that range's groups appended at (G0, Jf0) and its dependent ->
+//     group entries placed behind the earlier ranges' (dcur).  Ranges ascend in join value and groups are numbered in
+//     join order, so goff / gcap / gmap / dgrp are exactly the one-pass build's.
+static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const u32 V = c->V ? c->V : 1;
+    TRY(g_record_bits(c));
+    const u64 ncap = c->ncap;
+    const int joinbits = c->joinbits;
+    HIP_TRY(c, hipEventRecord(c->ev[2], st));
+    c->J_emit = 0;
+    c->sort_passes_records = 0;
+    // the frequent-condition stage's record scratch is not needed again this run (up to 84 GB at 10^9 triples)
+    c->brkeys.release();
+    c->brkeys2.release();
+    c->tkeys.release();
+    c->urecs.release();
+    // 1. ranges
+    const int jshift = joinbits > 14 ? joinbits - 14 : 0;
+    ENSURE(c, jhist, JH_BUCKETS * 8);
+    HIP_TRY(c, hipMemsetAsync(c->jhist.p, 0, JH_BUCKETS * 8, st));
+    tbegin(c, RDF_T_EMIT);
+    if (n)
+        hipLaunchKernelGGL(k_emit_join_hist, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V,
+                           2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits,
+                           jshift, c->jhist.as<u64>());
+    tend(c, RDF_T_EMIT);
+    std::vector<u64> h(JH_BUCKETS);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->jhist.p, JH_BUCKETS * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    struct Range { u32 lo, hi; u64 recs; };
+    std::vector<Range> ranges;
+    u64 acc = 0, cap_rec = 1;
+    u32 lo = 0;
+    for (u32 b = 0; b < JH_BUCKETS; ++b) {
+        if (acc && acc + h[b] > max_range) {
+            ranges.push_back({lo, b << jshift, acc});
+            lo = b << jshift;
+            acc = 0;
+        }
+        acc += h[b];
+    }
+    ranges.push_back({lo, JOIN_ALL_HI, acc});
+    for (const Range& r : ranges) cap_rec = std::max(cap_rec, r.recs);
+    if (cap_rec >= (1ull << 32) - 1)
+        return fail(c, RDF_ERR_LIMIT, "one join bucket holds >= 2^32 capture records");
+    c->n_group_ranges = ranges.size();
+    // 2. supports
+    ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
+    ENSURE(c, rsup, std::max<u64>(ncap, 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->support.p, 0, std::max<u64>(ncap, 1) * 4, st));
+    u64 Jtot = 0;
+    for (const Range& r : ranges) {
+        u64 J = 0;
+        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J));
+        Jtot += J;
+        if (ncap)
+            hipLaunchKernelGGL(k_add_u32, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->support.as<u32>(),
+                               c->rsup.as<u32>(), ncap);
+    }
+    const u64 J_emit = c->J_emit;
+    // 3. compaction; each frequent capture's dependent -> group list has support entries
+    tbegin(c, RDF_T_SUPPORT);
+    TRY(g_compact_captures(c));
+    const u32 C = c->C;
+    ENSURE(c, csup, std::max<u64>(C, 1) * 4);
+    ENSURE(c, doff, (C + 1ull) * 8);
+    if (C)
+        hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->info.as<CapInfo>(), C, c->csup.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->csup.as<u32>(), c->doff.as<u64>(), C, c->doff.as<u64>() + C, st));
+    tend(c, RDF_T_SUPPORT);
+    u64 Jf = 0;
+    TRY(read_u64(c, c->doff.as<u64>() + C, &Jf));
+    c->Jf = Jf;
+    const u64 Gmax = std::min<u64>(V, Jf);
+    ENSURE(c, goff, (Gmax + 1) * 8);
+    ENSURE(c, gcap, std::max<u64>(Jf, 1) * 4 + 16);  // + 16 B: the light pass reads whole aligned quads
+    ENSURE(c, gmap, (u64)V * 4);
+    ENSURE(c, dgrp, std::max<u64>(Jf, 1) * 4);
+    ENSURE(c, dcur, std::max<u64>(C, 1) * 4);
+    ENSURE(c, offp, (C + 1ull) * 8);
+    ENSURE(c, skip, (ncap + 1) * 4);
+    HIP_TRY(c, hipMemsetAsync(c->dcur.p, 0, std::max<u64>(C, 1) * 4, st));
+    // 4. groups, range by range
+    u64 Jf0 = 0, G0 = 0;
+    for (const Range& r : ranges) {
+        u64 J = 0;
+        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J));
+        u64* keys = c->rec_sorted;
+        tbegin(c, RDF_T_SUPPORT);
+        ENSURE(c, flags, std::max<u64>(std::max<u64>(J, ncap), 1) * 4);
+        if (ncap)
+            hipLaunchKernelGGL(k_skip_counts, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cstart.as<u32>(),
+                               c->fpos.as<u32>(), c->support.as<u32>(), ncap, c->ms, c->flags.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->skip.as<u32>(), ncap, c->skip.as<u32>() + ncap, st));
+        u64 fs[2];
+        TRY(read_multi(c, {{c->fpos.as<u32>() + J, 4}, {c->skip.as<u32>() + ncap, 4}}, fs));
+        const u64 Jr = fs[0] - fs[1];  // this range's kept records
+        u64* dk = keys == c->rec.as<u64>() ? c->rec_tmp.as<u64>() : c->rec.as<u64>();
+        ENSURE(c, fk, std::max<u64>(Jr, 1) * 8);
+        ENSURE(c, fk_tmp, std::max<u64>(Jr, 1) * 8);
+        if (J)
+            hipLaunchKernelGGL(k_keep_scatter, dim3(grid_for(J, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, joinbits,
+                               c->fpos.as<u32>(), c->skip.as<u32>(), c->support.as<u32>(), c->ms, c->fidx.as<u32>(), dk,
+                               c->fk.as<u64>());
+        tend(c, RDF_T_SUPPORT);
+        tbegin(c, RDF_T_GROUPS);
+        if (Jr) {
+            u64* tk = c->fk.as<u64>();
+            u64* tt = c->fk_tmp.as<u64>();
+            HIP_TRY(c, radix_sort_u64_bits(c->ws, tk, tt, Jr, 32, 32 + joinbits, st));
+            if (tk != c->fk.as<u64>()) std::swap(c->fk, c->fk_tmp);
+        }
+        ENSURE(c, gflag, std::max<u64>(Jr, 1) * 4);
+        ENSURE(c, gexcl, (Jr + 1) * 4);
+        if (Jr)
+            hipLaunchKernelGGL(k_group_flags, dim3(grid_for(Jr, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fk.as<u64>(), Jr,
+                               c->gflag.as<u32>());
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), Jr, c->gexcl.as<u32>() + Jr, st));
+        u32 Gr = 0;
+        TRY(read_u32(c, c->gexcl.as<u32>() + Jr, &Gr));
+        if (G0 + Gr > Gmax || Jf0 + Jr > Jf) return fail(c, RDF_ERR_LIMIT, "join ranges disagree on the kept records");
+        if (Jr) {
+            hipLaunchKernelGGL(k_group_build_at, dim3(grid_for(Jr, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->fk.as<u64>(), Jr,
+                               c->gflag.as<u32>(), c->gexcl.as<u32>(), Jf0, (u32)G0, c->goff.as<u64>(), c->gcap.as<u32>(),
+                               c->gmap.as<u32>());
+            hipLaunchKernelGGL(k_key_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, dk, Jr, C,
+                               c->offp.as<u64>());
+            hipLaunchKernelGGL(k_dgrp_range, dim3(grid_for(Jr, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, dk, Jr,
+                               c->offp.as<u64>(), c->doff.as<u64>(), c->dcur.as<u32>(), c->gmap.as<u32>(), c->dgrp.as<u32>());
+            if (C)
+                hipLaunchKernelGGL(k_dcur_add, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->offp.as<u64>(), C,
+                                   c->dcur.as<u32>());
+        }
+        tend(c, RDF_T_GROUPS);
+        Jf0 += Jr;
+        G0 += Gr;
+    }
+    if (Jf0 != Jf) return fail(c, RDF_ERR_LIMIT, "join ranges disagree on the kept records");
+    c->G = G0;
+    c->J = Jtot;
+    c->J_emit = J_emit;  // every range was emitted twice: the first pass's count
+    c->hscal[14] = Jf;
+    HIP_TRY(c, hipMemcpyAsync(c->goff.as<u64>() + G0, c->hscal + 14, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    // the range scratch is sized by the largest range; the discovery stage needs the room
+    for (DevBuf* b : {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->gflag, &c->gexcl, &c->fpos, &c->flags}) b->release();
+    c->rec_sorted = nullptr;
+    return RDF_OK;
+}
+
+// records per join range of the automatic g_build_ranges: the range scratch (two record buffers, fresh flags + scan,
+// kept keys and their sort buffer, group flags + scan: <= 48 B per record) in the free HBM left after the stage's
+// global arrays (gcap + dgrp, <= 8 B per record overall), at most 2^31 (u32 scans inside a range)
+static u64 auto_range_records(rdf_ctx* c) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1ull << 30;
+    const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap;  // released by g_build_ranges
+    const u64 avail = (u64)free_b + held;
+    const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30);  // ~4.5 records per triple kept
+    const u64 r = avail > global ? (avail - global) / 48 : 0;
+    return std::max<u64>(std::min<u64>(r, 1ull << 31), 1ull << 24);
 }
 
 // local group-size histogram (quarter-octave buckets) -> h_hist (host)
@@ -1327,6 +1546,7 @@ static void fill_group_stats(rdf_ctx* c) {
     s.n_unary_captures = c->Cu;
     s.n_heavy_groups = c->nheavy;
     s.heavy_threshold = c->heavy_threshold;
+    s.n_join_ranges = c->n_group_ranges;
 }
 
 static rdf_status g_finish(rdf_ctx* c, rdf_group_stats* stats) {
@@ -1348,8 +1568,14 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     TRY(parse_projection(c, projection, &proj));
     c->rank = 0;
     c->nranks = 1;
-    TRY(g_emit_sort_support(c, proj));
-    TRY(g_compact_groups(c));
+    c->paged = false;
+    c->n_group_ranges = 1;
+    if (c->group_range_records || 9 * c->n >= (1ull << 32)) {
+        TRY(g_build_ranges(c, proj, c->group_range_records ? c->group_range_records : auto_range_records(c)));
+    } else {
+        TRY(g_emit_sort_support(c, proj));
+        TRY(g_compact_groups(c));
+    }
     if (c->ar_on) TRY(g_ar_refs(c));
     u32 h_hist[256];
     TRY(g_size_hist(c, h_hist));
@@ -2057,6 +2283,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
+    c->paged = false;
     hipStream_t st = c->stream;
     CindView v = make_view(c, flags);
     TRY(d_pivot_local(c, v));
@@ -2304,7 +2531,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
 
 rdf_status rdf_next_page(rdf_ctx* c, uint32_t* done, uint64_t* first_dep, uint64_t* end_dep) {
     if (!c || !done) return RDF_ERR_ARG;
-    if (!c->paged) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds_paged must be called first");
+    if (!c->paged || c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds_paged must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
     CindView v = make_view(c, c->pg_flags);
     v.eoff = c->eoff.as<u64>();
@@ -3186,6 +3413,7 @@ static rdf_status sh_phase24(rdf_ctx* c, rdf_exchange* req) {
     c->parsed_dict = false;
     c->ingest_sharded = true;
     c->stage = 1;
+    c->paged = false;  // a paged run's state belongs to the previous input
     memset(req, 0, sizeof(*req));
     req->op = RDF_X_DONE;
     c->sh_phase = 9;
@@ -3288,6 +3516,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     c->sh_phase = 10;
     c->x_imported = true;
     c->stage = std::min(c->stage, 1);
+    c->paged = false;
     return RDF_OK;
 }
 
@@ -3305,6 +3534,7 @@ rdf_status rdf_shard_parse_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, con
     c->sh_phase = 20;
     c->x_imported = true;
     c->stage = 0;  // no usable triples until the global ids arrive
+    c->paged = false;
     if (n_triples) *n_triples = n;
     return RDF_OK;
 }

@@ -306,6 +306,67 @@ def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
         g.close()
 
 
+@pytest.mark.parametrize("range_records", [1, 7, 300])
+def test_join_range_groups_parity(monkeypatch, range_records):
+    """Capture groups built in join-value ranges (the path of inputs with >= 2^32/9 triples; RDFIND_GROUP_RANGE forces
+    ranges of at most that many K3 records, a single join value's records may exceed it): every mode gives the oracle's
+    set, and the stage statistics equal the one-pass build's."""
+    ref = _lib.Context(0)
+    monkeypatch.setenv("RDFIND_GROUP_RANGE", str(range_records))
+    g = _lib.Context(0)
+    try:
+        rng = random.Random(900 + range_records)
+        for _ in range(25):
+            n = rng.randrange(1, 400)
+            nv = rng.randrange(2, 60)
+            ms = rng.randrange(1, 4)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            for strategy, clean in MODES:
+                assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
+                    (n, nv, ms, strategy, clean, range_records)
+                assert compact_matches(g, nv)
+            gpu_set(ref, arr, nv, ms, 1, True)
+            keys = ("n_records", "n_sorted_records", "n_frequent_records", "n_groups", "n_captures", "n_heavy_groups")
+            assert {k: g.groups[k] for k in keys} == {k: ref.groups[k] for k in keys}
+            assert (g.cind_count(), g.checksum()) == (ref.cind_count(), ref.checksum())
+            if range_records == 1 and n > 50:
+                assert g.groups["n_join_ranges"] > 1
+        for cfg, scale in (("c1", 0.05), ("c5", 0.01), ("c4", 0.0003)):
+            d = synth.config(cfg, scale)
+            exp, st = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+            g.set_triples(d.s, d.p, d.o, d.num_terms)
+            g.run(d.min_support)
+            assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, range_records)
+            assert g.groups["n_records"] == st["n_records"] and g.groups["n_captures"] == st["n_freq_captures"]
+            assert g.groups["n_join_ranges"] > 1
+    finally:
+        g.close()
+        ref.close()
+
+
+def test_next_page_needs_a_current_paged_run(ctx):
+    """rdf_next_page fails with RDF_ERR_STATE (never runs on stale page state) once new triples, new capture groups or
+    an unpaged discovery replaced the paged run."""
+    rng = random.Random(4)
+    arr = np.array([(rng.randrange(30), rng.randrange(6), rng.randrange(30)) for _ in range(300)], dtype=np.uint32)
+    for breaker in ("set_triples", "groups", "unpaged"):
+        ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], 30)
+        ctx.frequent_conditions(2)
+        ctx.build_capture_groups("spo")
+        ctx.discover_cinds_paged(True, 1, 1)
+        assert ctx.next_page() is not None
+        if breaker == "set_triples":
+            ctx.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], 30)
+        elif breaker == "groups":
+            ctx.frequent_conditions(2)
+            ctx.build_capture_groups("spo")
+        else:
+            ctx.discover_cinds(True, 1)
+        with pytest.raises(_lib.RdfError):
+            ctx.next_page()
+
+
 def test_large_grids_two_paths(monkeypatch):
     """c5 at scale 0.3 (8.7e9 CINDs): the heavy-only binary dependents take > 2^26 work items (a dispatch holds
     < 2^32 work-items, so the kernels loop over virtual blocks).  The classed path and the pivot-scan path

@@ -120,6 +120,74 @@ def test_c3_full_sampled_direct_verification(ctx):
         assert np.isin(jd, jr).all()
 
 
+@pytest.mark.timeout(600)
+def test_join_ranges_full_size_vs_oracle(monkeypatch):
+    """c4 at 0.1 (10^8 triples, 5.6·10^8 records) with its capture groups built in join-value ranges of <= 10^8 records
+    (RDFIND_GROUP_RANGE; the automatic path of inputs >= 2^32/9 triples) gives the golden vector."""
+    g = GOLD["c4@0.1/s1_clean"]
+    d = dataset(g["config"], g["scale"])
+    monkeypatch.setenv("RDFIND_GROUP_RANGE", str(100_000_000))
+    with _lib.Context(0) as c:
+        c.set_triples(d.s, d.p, d.o, d.num_terms)
+        c.run(d.min_support, "spo", g["clean"], g["strategy"])
+        assert c.groups["n_join_ranges"] >= 5
+        assert c.groups["n_records"] == g["n_records"] and c.groups["n_captures"] == g["n_freq_captures"]
+        assert (c.cind_count(), c.checksum()) == (g["n_cinds"], int(g["checksum"]))
+
+
+def _sample_verify(ctx, d, k, seed):
+    """k sampled CINDs of the current result hold on the triples themselves: every join value of the dependent is one
+    of the referenced capture's, and the support is the dependent's number of distinct join values."""
+    n = ctx.cind_count()
+    rng = np.random.default_rng(seed)
+    offs = rng.choice(n, size=min(k, n), replace=False)
+    sample = np.concatenate([ctx.copy_cinds_range(int(o), 1) for o in offs])
+    dec = _lib.decode_rows(sample, d.num_terms, ctx.binary_keys())
+    for dc, d1, d2, rc, r1, r2, sup in dec.tolist():
+        jd = _capture_joins(d, dc, d1, d2)
+        jr = _capture_joins(d, rc, r1, r2)
+        assert len(jd) == sup >= d.min_support
+        assert np.isin(jd, jr).all()
+
+
+@pytest.mark.timeout(1100)
+def test_c4_full_size_one_gpu(ctx, monkeypatch):
+    """c4 at its BASELINE size (Freebase-shaped, 10^9 triples, support 100) on one MI355X.  Its ~5.8·10^9 capture
+    records exceed one sort's u32 offsets, so the capture groups are built in join-value ranges (the reference's
+    sort-based groupBy spills instead, ALG/programs/RDFind.scala:339-345).  Checked: the same result (count, checksum,
+    stage counts) from two different range splits, run to run determinism, the compact hand-over expanded by the
+    checker, sampled CINDs verified on the triples, and the streamed oracle's golden vector when it has been made."""
+    from oracle import c_oracle as C
+
+    d = dataset("c4", 1.0)
+    assert d.n == 1_000_000_000
+    results = []
+    monkeypatch.setenv("RDFIND_GROUP_RANGE", str(600_000_000))  # ~10 ranges
+    with _lib.Context(0) as c:
+        c.set_triples(d.s, d.p, d.o, d.num_terms)
+        c.run(d.min_support)
+        forced = c.groups["n_join_ranges"]
+        assert forced >= 8
+        results.append((c.cind_count(), c.checksum(), c.groups["n_records"], c.groups["n_groups"]))
+    monkeypatch.delenv("RDFIND_GROUP_RANGE")
+    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+    for _ in range(2):
+        ctx.run(d.min_support)
+        assert 1 < ctx.groups["n_join_ranges"] < forced
+        results.append((ctx.cind_count(), ctx.checksum(), ctx.groups["n_records"], ctx.groups["n_groups"]))
+    assert results[0] == results[1] == results[2]
+    n, h, _ = C.checksum_compact(ctx.copy_result_compact(), d.num_terms)
+    assert (n, h) == results[0][:2] and n > 0
+    assert ctx.groups["n_records"] > 2 ** 32  # more records than one pass addresses
+    _sample_verify(ctx, d, 10, 4)
+    g = GOLD.get("c4@1.0/s1_clean")
+    if g is not None:
+        assert str(fingerprint(d)) == g["fingerprint"]
+        assert ctx.fc["n_frequent_unary"] == g["n_freq_unary"] and ctx.fc["n_frequent_binary"] == g["n_freq_binary"]
+        assert ctx.groups["n_records"] == g["n_records"] and ctx.groups["n_captures"] == g["n_freq_captures"]
+        assert (n, h) == (g["n_cinds"], int(g["checksum"]))
+
+
 _VARIANT_CHILD = r"""
 import json, sys
 sys.path.insert(0, sys.argv[1])
