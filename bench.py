@@ -13,7 +13,7 @@ N > 1: one rank per GPU under torch.distributed.run (started by this script when
 xGMI; the workload is sharded (rdfind_amd/distributed.py): each rank holds only its slice of the
 triples (synth.config_slice), the condition counts are summed over ranks, every triple travels to the ranks
 owning its join values, each rank builds the capture groups of its join-value hash shard and owns the
-dependents d % N; the protocol's collectives run inside the timed region and every rank hands over its own
+dependents by hash (dep_owner); the protocol's collectives run inside the timed region and every rank hands over its own
 result.  Default weak scaling: N GPUs run the config at N x scale (c2: LUBM-(100 N)), so each GPU holds one
 LUBM-100-sized share; `value` = all triples / max-over-ranks step time.  `roofline` is computed for the dominant
 kernel family from HIP events recorded on the library's stream; `cpu_baseline` times the C restatement
@@ -49,6 +49,9 @@ FAMILY_KERNELS = {
     "rules": ["k_rules_explicit", "k_rules_mark", "k_compact_refs"],
     "cemit": ["k_class_emit"],
 }
+# CPU baseline sample per config: the streamed C restatement runs ~10-30 s on the box's threads at these scales
+# (c1/c2: the whole workload; c5 grows super-linearly with its pair explosion)
+CPU_SAMPLE_SCALE = {"c1": 1.0, "c2": 1.0, "c3": 0.1, "c4": 0.02, "c5": 0.05}
 PMC_STEP_KERNEL = "k_pivot_final"  # launched once per discovery step: the number of steps in the PMC run
 
 
@@ -205,7 +208,8 @@ def main():
                          "strong: the config at scale is split over the GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the N-Triples ingest leg (rank 0, N=1)")
-    ap.add_argument("--cpu-sample-scale", type=float, default=0.3)
+    ap.add_argument("--cpu-sample-scale", type=float, default=None,
+                    help="scale of the config the CPU baseline runs (default: CPU_SAMPLE_SCALE, ~10-30 s of CPU work)")
     ap.add_argument("--cpu-full-max", type=int, default=20_000_000,
                     help="time the CPU baseline on the benchmarked workload itself up to this many triples")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
@@ -213,9 +217,9 @@ def main():
     ap.add_argument("--no-resident", action="store_true", help="skip the device-resident repeat of the steps")
     ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
     ap.add_argument("--page-bytes", type=int, default=None,
-                    help="paged discovery (rdf_discover_cinds_paged) with this working memory per page, 0 = a quarter "
-                         "of the free HBM; every page is handed over in turn.  Default: unpaged, except c5 beyond "
-                         "scale 0.3, whose result does not fit in HBM")
+                    help="paged discovery (rdf_discover_cinds_paged) with this working memory per page, 0 = "
+                         "automatic; every page is handed over in turn.  Default: unpaged, or automatic pages when the "
+                         "unpaged run exceeds HBM (RDF_ERR_OOM; c5 beyond scale 0.3)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -249,7 +253,16 @@ def main():
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
     sink = CompactSink()
 
-    paged = dist is None and (args.page_bytes is not None or (args.config == "c5" and total_scale > 0.3))
+    paged = dist is None and args.page_bytes is not None
+    if dist is None and not paged:  # a result larger than HBM: the unpaged run fails with RDF_ERR_OOM -> pages
+        try:
+            ctx.run(ms)
+        except _lib.RdfError as e:
+            if e.status != _lib.RDF_ERR_OOM:
+                raise
+            print("bench.py: the unpaged result exceeds HBM; paged discovery", file=sys.stderr, flush=True)
+            ctx.release_scratch()
+            paged = True
     if dist is not None:
         from rdfind_amd import distributed
 
@@ -381,7 +394,9 @@ def main():
         from oracle import c_oracle
 
         # the same workload when the streamed C restatement finishes in ~30 s on the box's threads, else a sample
-        cpu_scale = total_scale if d.n <= args.cpu_full_max else args.cpu_sample_scale
+        cpu_scale = args.cpu_sample_scale or min(total_scale, CPU_SAMPLE_SCALE.get(args.config, 0.3))
+        if d.n <= args.cpu_full_max and args.config in ("c1", "c2"):
+            cpu_scale = total_scale  # the benchmarked workload itself
         sd = d if cpu_scale == total_scale else synth.config(args.config, cpu_scale)
         t = time.perf_counter()
         r = c_oracle.stream(sd.s, sd.p, sd.o, sd.num_terms, sd.min_support, 1, True)

@@ -286,10 +286,10 @@ rdf_status rdf_last_stats(rdf_ctx* ctx, rdf_fc_stats* fc, rdf_group_stats* gs, r
  * Sharded multi-GPU mode (the reference's --dop parallelism over Flink task slots).
  * With RDF_SHARD_LOCAL_SLICE the resident triples are this rank's slice of the input (any partition of the
  * triples over the ranks, one dictionary); without it every rank holds all triples and takes rows
- * [n * rank / nranks, n * (rank + 1) / nranks).  Condition counts are summed over ranks (unary: all-reduce of
- * dense counts; binary: (key, count) partials all-to-all'd to the key's owner, frequent keys all-gathered), then
+ * [n * rank / nranks, n * (rank + 1) / nranks).  Condition counts are summed over ranks (unary and binary: the
+ * slice's nonzero (key, count) partials all-to-all'd to the key's owner, frequent keys all-gathered), then
  * each triple travels to the ranks owning its join values (hash(join) % nranks), so rank r builds the capture
- * groups of its join values and owns the dependents d with d % nranks == r.  The library stops at every
+ * groups of its join values and owns the dependents d with dep_owner(d) == r (a hash).  The library stops at every
  * collective and describes it in an rdf_exchange; the caller performs it (torch.distributed over RCCL,
  * see rdfind_amd/distributed.py) and hands the result back:
  *
@@ -356,6 +356,10 @@ rdf_status rdf_kernel_times(rdf_ctx* ctx, float* ms, int count);
 rdf_status rdf_sync(rdf_ctx* ctx);
 /* Device memory (bytes) the context holds right now (its HBM buffers and scratch). */
 rdf_status rdf_device_bytes(rdf_ctx* ctx, uint64_t* bytes);
+/* Releases every per-run device buffer, keeping only the resident triples and the formatting dictionary (e.g. after
+ * rdf_discover_cinds failed with RDF_ERR_OOM, before a paged run).  The context is back at the "triples set" stage:
+ * rdf_frequent_conditions comes next. */
+rdf_status rdf_release_scratch(rdf_ctx* ctx);
 
 #ifdef __cplusplus
 }

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_result_raw", "rdf_association_rules", "rdf_copy_association_rules", "rdf_get_result_layout",
     "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
     "rdf_discover_cinds_paged", "rdf_next_page", "rdf_shard_parse_begin", "rdf_shard_dictionary_begin", "rdf_num_terms",
-    "rdf_dictionary_terms", "rdf_copy_result_refs",
+    "rdf_dictionary_terms", "rdf_copy_result_refs", "rdf_release_scratch",
 )
 RDF_NT_TABS = 1
 
@@ -108,8 +108,15 @@ ROW_DTYPE = np.dtype([("dep_capture_type", "<u4"), ("dep_value1", "<u4"), ("dep_
 _lib = None
 
 
+RDF_ERR_OOM = -3  # device memory exhausted (include/rdfind_hip.h)
+
+
 class RdfError(RuntimeError):
-    pass
+    """A failed library call; ``status`` is its rdf_status (e.g. RDF_ERR_OOM), None for load failures."""
+
+    def __init__(self, msg, status=None):
+        super().__init__(msg)
+        self.status = status
 
 
 def load():
@@ -148,6 +155,7 @@ def load():
         "rdf_kernel_times": (i32, [P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
         "rdf_sync": (i32, [P]),
         "rdf_device_bytes": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_release_scratch": (i32, [P]),
         "rdf_copy_cinds_range": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
         "rdf_cind_checksum": (i32, [P, ctypes.POINTER(u64)]),
         "rdf_copy_cinds_decoded": (i32, [P, u64, P, u64, ctypes.POINTER(u64)]),
@@ -241,7 +249,7 @@ class Context:
     def _check(self, rc, what):
         if rc != 0:
             msg = self.lib.rdf_last_error(self.ptr)
-            raise RdfError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+            raise RdfError(f"{what} failed ({rc}): {msg.decode() if msg else ''}", rc)
 
     # -- stages ------------------------------------------------------------------------------
     def set_triples(self, s, p, o, num_terms: int):
@@ -394,6 +402,10 @@ class Context:
         v = ctypes.c_uint64()
         self._check(self.lib.rdf_device_bytes(self.ptr, ctypes.byref(v)), "rdf_device_bytes")
         return int(v.value)
+
+    def release_scratch(self):
+        """rdf_release_scratch: frees every per-run buffer (triples and dictionary stay); frequent_conditions next."""
+        self._check(self.lib.rdf_release_scratch(self.ptr), "rdf_release_scratch")
 
     def last_stats(self):
         fc, gs, cs = FcStats(), GroupStats(), CindStats()

@@ -42,6 +42,13 @@ __host__ __device__ inline u32 shard_of(u32 join, u32 nranks) {
     return nranks <= 1 ? 0u : (u32)((((u64)join * 0x9E3779B97F4A7C15ull) >> 32) % nranks);
 }
 
+// owner rank of a dependent (compact capture id): it finalises the dependent's refs in sharded mode.  Hashed, not
+// d % N: compact ids are 2 rank(cond) + (t >= 3), so id parity follows the projection and d % 2 gave one rank 64 % of
+// the CINDs at two ranks
+__host__ __device__ inline u32 dep_owner(u32 d, u32 nranks) {
+    return nranks <= 1 ? 0u : (u32)((mix64(d) >> 32) % nranks);
+}
+
 // join values whose capture records a K3 emission writes: this rank's shard (hash) and, when the capture groups are
 // built in join-value ranges (one GPU, inputs whose records exceed one pass), the range [lo, hi)
 struct JoinSel {

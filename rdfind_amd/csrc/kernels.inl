@@ -1746,7 +1746,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_rules_explicit(CindView v, const 
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < E; i += (u64)gridDim.x * RDF_BLOCK) {
         const u64 pr = pairs[i];
         const u32 d = (u32)(pr >> 32);
-        keep[i] = (d % nranks == rank && rule_keep(v, d, (u32)pr)) ? 1u : 0u;
+        keep[i] = (dep_owner(d, nranks) == rank && rule_keep(v, d, (u32)pr)) ? 1u : 0u;
     }
 }
 
@@ -1758,7 +1758,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_rules_mark(CindView v, const u64*
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < E; i += (u64)gridDim.x * RDF_BLOCK) {
         const u64 pr = pairs[e0 + i];
         const u32 a = (u32)(pr >> 32), x = (u32)pr;
-        if (x < v.Cu || a % nranks != rank) continue;
+        if (x < v.Cu || dep_owner(a, nranks) != rank) continue;
         const u64 b = v.eoff[a], n = v.ebin[a] - b;
         const u32* bc = v.bcomp + 2ull * (x - v.Cu);
 #pragma unroll
@@ -1931,7 +1931,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_keys(CindView v, const u64*
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < n_round; d += (u64)gridDim.x * RDF_BLOCK) {
         u32 want = 0;
         u64 key = 0;
-        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY) && (u32)d % nranks == rank) {
+        if (d < v.Cu && (v.info[d].meta & META_HEAVY_ONLY) && dep_owner((u32)d, nranks) == rank) {
             const u64 h = class_slot(tkeys, tmask, v.info[d].hmask);
             if (h != ~0ull) {
                 key = ((u64)cid[h] << 32) | d;
@@ -2433,7 +2433,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_decode_rows(const u32* __restrict
 // Sharded mode: capture groups partitioned by join-value hash over R ranks.  Global
 // quantities (supports, group-size histogram, heavy masks, pivot sizes, light-group counts) are combined
 // by the caller's collectives; light dependents' local survivors are routed to the dependent's owner
-// (dep % R), which keeps a ref iff every rank holding a light group of the dependent reported it.
+// (dep_owner), which keeps a ref iff every rank holding a light group of the dependent reported it.
 
 // MIN-allreduce keys of the local pivot: (size << 32 | rank), INT64_MAX where the rank has no group
 __global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __restrict__ best, u32 C, u32 rank, u64* out) {
@@ -2470,7 +2470,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_route_survivors(const u64* __rest
             continue;
         }
         u64 o = pos[i];
-        out[o++] = ((u64)(d % nranks) << 58) | pr;
+        out[o++] = ((u64)dep_owner((u32)d, nranks) << 58) | pr;
         for (u64 m = others; m; m &= m - 1) {
             const u64 r = (u64)(__ffsll((long long)m) - 1);
             out[o++] = (r << 58) | (1ull << (32 + cb)) | pr;
@@ -2568,7 +2568,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_owner_pack(u64* pairs, u64 n, u32
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         const u64 pr = pairs[i];
         const u64 d = pr >> 32, r = pr & 0xffffffffull;
-        pairs[i] = ((d % nranks) << (2 * cb)) | (d << cb) | r;
+        pairs[i] = ((u64)dep_owner((u32)d, nranks) << (2 * cb)) | (d << cb) | r;
     }
 }
 

@@ -388,7 +388,7 @@ static rdf_status check_terms(rdf_ctx* c, u64 n, u32 num_terms) {
 // what the context holds beyond the input and the uploaded dictionary exceeds max(4 GB, 1 KB per new triple), it is
 // released first: a test sequence c4 at 0.4 (400M triples) -> c5 at 0.3 (3M triples, 10^10 CINDs) must not carry
 // the first run's buffers into the second run's growth.
-static void release_run_buffers(rdf_ctx* c, u64 n_next) {
+static void release_run_buffers(rdf_ctx* c, u64 n_next, bool always = false) {
     const DevBuf* keep[] = {&c->scal, &c->ts, &c->tp, &c->to, &c->dheap, &c->dtoff, &c->own_text, &c->own_off, &c->own_len};
     auto kept = [&](const DevBuf* b) {
         for (const DevBuf* k : keep)
@@ -398,7 +398,7 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next) {
     u64 held = c->ws.bytes();
     for (DevBuf* b : ctx_buffers(c))
         if (!kept(b)) held += b->cap;
-    if (held <= std::max<u64>(4ull << 30, n_next << 10)) return;
+    if (!always && held <= std::max<u64>(4ull << 30, n_next << 10)) return;
     (void)hipStreamSynchronize(c->stream);
     c->paged = false;
     for (DevBuf* b : ctx_buffers(c))
@@ -409,6 +409,15 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next) {
     c->h_runs_valid = false;
     c->h_bkeys_valid = false;
     c->capstr_run = ~0ull;
+}
+
+rdf_status rdf_release_scratch(rdf_ctx* c) {
+    if (!c) return RDF_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    release_run_buffers(c, 0, true);
+    c->paged = false;
+    c->stage = std::min(c->stage, 1);
+    return RDF_OK;
 }
 
 rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, const uint32_t* o, uint64_t n,
@@ -2953,7 +2962,7 @@ static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
     return RDF_OK;
 }
 
-// (dep << 32 | ref) pairs epairs[0, E) -> grouped by owner rank (dep % R) for an all-to-all to next_phase
+// (dep << 32 | ref) pairs epairs[0, E) -> grouped by owner rank (dep_owner) for an all-to-all to next_phase
 static rdf_status sh_to_owners(rdf_ctx* c, rdf_exchange* req, u64 E, int next_phase) {
     hipStream_t st = c->stream;
     const u32 C = c->C, R = c->nranks;

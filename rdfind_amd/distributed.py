@@ -20,7 +20,7 @@ the library requests one at a time (``rdf_shard_step``):
                       rank mask
   6. all-to-all       holder-first light exchange: only the rank holding d's globally smallest group (the pivot
                       holder) draws candidates from it and checks its own light groups; each survivor (dep, ref)
-                      goes to the owner (dep % R) as the holder's report and to every other rank with a light
+                      goes to the owner (dep_owner(dep), a hash mod R) as the holder's report and to every other rank with a light
                       group of dep for verification
   7. all-to-all       the verified survivors -> the owner, which keeps a ref iff every rank with a light group of
                       dep reported it.  Together this is the reference's combiner-side intersection
@@ -50,22 +50,29 @@ def _dtype(op):
 
 
 def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
-    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order.  Balanced contributions
-    (padding to the largest adds <= 50 %) go through one all-gather of padded slices; skewed ones through one
-    broadcast per rank into its exact slice of the result (no padding)."""
+    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order.  One all-gather of the counts,
+    then, unless the contributions are very skewed, one all-gather of padded slices into a single preallocated tensor
+    (world x the largest slice), compacted by one copy.  When padding would exceed 4x the payload and 64 MiB, one
+    broadcast per rank into its exact slice of the result instead (no padding)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
+    counts_t = torch.empty(world, dtype=torch.int64, device=send.device)
+    dist.all_gather_into_tensor(counts_t, n, group=group)
+    counts = [int(c) for c in counts_t.tolist()]
     mx, tot = max(counts), sum(counts)
-    if mx and 2 * world * mx <= 3 * tot:
-        pad = send.new_zeros(mx)
-        pad[: send.numel()].copy_(send)
-        parts = [send.new_empty(mx) for _ in range(world)]
-        dist.all_gather(parts, pad, group=group)
-        return torch.cat([p[:c] for p, c in zip(parts, counts)])
+    if not tot:
+        return send.new_empty(0)
+    pad_bytes = (world * mx - tot) * send.element_size()
+    if world * mx <= 4 * tot or pad_bytes <= (64 << 20):
+        pad = send.new_zeros(mx) if send.numel() < mx else send
+        if send.numel() < mx:
+            pad[: send.numel()].copy_(send)
+        gathered = send.new_empty(world * mx)
+        dist.all_gather_into_tensor(gathered, pad, group=group)
+        if mx * world == tot:
+            return gathered
+        return torch.cat([gathered[r * mx: r * mx + c] for r, c in enumerate(counts) if c])
     out = send.new_empty(tot)
     off = 0
     for r, c in enumerate(counts):
@@ -133,8 +140,8 @@ def run_protocol(machine, group=None, device=None):
             machine.shard_import(send.data_ptr(), 0)  # an all-reduce has the same count on every rank: all skip it
             n += 1
             continue
-        if device.type == "cuda":
-            torch.cuda.current_stream(device).synchronize()
+        # shard_export returns once the library's stream has written `send`, so the collective (on torch's stream)
+        # may start at once; the library reads `recv` on its own stream, so torch's stream must have finished it
         recv = exchange(req, send, group).contiguous()
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
@@ -152,7 +159,13 @@ def run_sharded(ctx, min_support: int, projection="spo", clean_implied=True, tra
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     ctx.shard_begin(rank, world, min_support, projection, clean_implied, traversal_strategy, local_slice, use_ars)
-    run_protocol(ctx, group, device)
+    try:
+        run_protocol(ctx, group, device)
+    except _lib.RdfError as e:
+        if e.status == _lib.RDF_ERR_OOM:  # sharded runs are not paged (one GPU pages, rdf_discover_cinds_paged)
+            raise _lib.RdfError(f"rank {rank} of {world}: its share of the result exceeds the device memory; sharded "
+                                f"discovery is not paged, use more ranks ({e})", e.status) from e
+        raise
     return ctx.last_stats()
 
 

@@ -61,6 +61,10 @@ def build_parser():
     ap.add_argument("--only-read", action="store_true")
     ap.add_argument("--create-join-histogram", action="store_true")
     ap.add_argument("-dop", "--gpus", dest="dop", type=int, default=-1, help="degree of parallelism (GPUs)")
+    ap.add_argument("--page-bytes", type=int, default=None,
+                    help="build-specific: discover the CINDs in pages of this much device working memory (0: "
+                         "automatic), each page written before the next.  Without it a result larger than the device "
+                         "memory switches to pages by itself")
     ap.add_argument("--device", type=int, default=0)
     for flag, typ in _RESULT_NEUTRAL.items():
         if typ is None:
@@ -190,8 +194,24 @@ class RDFind:
             gs = ctx.build_capture_groups(a.projection)
             if a.do_only_join:
                 return []
-            cs = ctx.discover_cinds(clean_implied=a.clean_implied, traversal_strategy=a.traversal_strategy)
-            return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
+            page_bytes = a.page_bytes
+            if page_bytes is None:
+                try:
+                    cs = ctx.discover_cinds(clean_implied=a.clean_implied, traversal_strategy=a.traversal_strategy)
+                    return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
+                except _lib.RdfError as e:
+                    if e.status != _lib.RDF_ERR_OOM:
+                        raise
+                # the result does not fit in HBM at once: the reference streams it to its sink at any size
+                # (RDFind.scala:507-520); here the discovery goes page by page, each page written before the next
+                self.log("The CIND result exceeds the device memory; discovering it in pages.")
+                ctx.release_scratch()
+                fc = ctx.frequent_conditions(a.support)
+                if a.use_ars:
+                    ctx.association_rules()
+                gs = ctx.build_capture_groups(a.projection)
+                page_bytes = 0
+            return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": None}, t1, out, page_bytes=page_bytes)
 
     def run_sharded_ingest(self, paths, device, t0, out):
         """-dop N with the input split over the ranks: each rank parses only its part of the bytes, the global
@@ -226,39 +246,51 @@ class RDFind:
             return self.write_output(ctx, None, {"fc": ctx.fc, "groups": ctx.groups, "cinds": ctx.cinds}, t1, out,
                                      dictionary_ready=True)
 
-    def write_output(self, ctx, dic, stats, t1, out, dictionary_ready=False):
+    def write_output(self, ctx, dic, stats, t1, out, dictionary_ready=False, page_bytes=None):
         """Cind.toString lines formatted on the GPU (rdf_format_cinds) in chunks of rows, to --output and/or the
         returned list.  With -dop > 1 every rank writes its own CINDs to a part file and rank 0 concatenates them
-        into the one output file (the reference writes file:// outputs with parallelism 1, RDFind.scala:507-520)."""
+        into the one output file (the reference writes file:// outputs with parallelism 1, RDFind.scala:507-520).
+        page_bytes (not None): the discovery runs now, page by page (rdf_discover_cinds_paged), and every page is
+        formatted and written before the next one is computed."""
         a = self.args
         ctx.sync()
         self.timings["discover"] = time.time() - t1
-        self.timings["device_ms"] = ctx.stage_times()
         self.stats = stats
         t2 = time.time()
-        n = ctx.cind_count()
         if dictionary_ready:
             pass  # the sharded ingest's dictionary by owner lookup (distributed.run_dictionary)
         elif dic is None:
             ctx.set_dictionary_parsed()  # device dictionary straight into the formatter
         else:
             ctx.set_dictionary(dic.terms)
-        keep_lines = n <= KEEP_LINES_MAX or a.collect_result or a.debug_level >= 3
-        lines = [] if keep_lines else None
+        keep_all = a.collect_result or a.debug_level >= 3
+        lines = []
         f = None
         path = _output_path(a.output) if a.output else None
         if path:
             f = open(path if self.world == 1 else f"{path}.part{self.rank}", "wb")
+        n = 0
         try:
-            for off in range(0, n, FORMAT_CHUNK):
-                text = ctx.format_array(off, FORMAT_CHUNK)
-                if f is not None:
-                    f.write(memoryview(text))
-                if keep_lines:
-                    lines.extend(text.tobytes().decode("utf-8").splitlines())
+            if page_bytes is None:
+                n = ctx.cind_count()
+                lines = lines if n <= KEEP_LINES_MAX or keep_all else None
+                self._format_result(ctx, n, f, lines)
+            else:
+                pages = 0
+                for _ in ctx.pages(a.clean_implied, a.traversal_strategy, page_bytes):
+                    m = ctx.cind_count()
+                    n += m
+                    pages += 1
+                    if lines is not None and n > KEEP_LINES_MAX and not keep_all:
+                        lines = None
+                    self._format_result(ctx, m, f, lines)
+                self.stats["pages"] = pages
+                if a.debug_level >= 1:
+                    self.log(f"{pages} pages.")
         finally:
             if f is not None:
                 f.close()
+        self.timings["device_ms"] = ctx.stage_times()
         if self.world > 1:
             n, lines = self.merge_ranks(n, lines, path)
             if self.rank != 0:
@@ -273,7 +305,20 @@ class RDFind:
                 print(ln, file=out)
         if not a.output and not a.collect_result:
             print(f"Detected {n} CINDs.", file=out)
+        self.n_cinds = n
         return lines
+
+    @staticmethod
+    def _format_result(ctx, n, f, lines):
+        """The current result's n rows as text lines: written to f and/or appended to lines (neither: nothing to do)."""
+        if f is None and lines is None:
+            return
+        for off in range(0, n, FORMAT_CHUNK):
+            text = ctx.format_array(off, FORMAT_CHUNK)
+            if f is not None:
+                f.write(memoryview(text))
+            if lines is not None:
+                lines.extend(text.tobytes().decode("utf-8").splitlines())
 
     def merge_ranks(self, n, lines, path):
         """-dop > 1: total count (all-reduce), the part files concatenated by rank 0, the lines gathered on rank 0."""

@@ -46,6 +46,11 @@ def key_owner(key: int, nranks: int) -> int:
     return (mix64(key) & 0xFFFFFFFF) % nranks
 
 
+def dep_owner(d: int, nranks: int) -> int:
+    """common.hpp dep_owner: the rank that finalises a dependent's refs."""
+    return 0 if nranks <= 1 else (mix64(d) >> 32) % nranks
+
+
 # binary condition type (S|P, S|O, P|O) <-> the library's key type bt (o[s,p] 2, p[s,o] 1, s[p,o] 0)
 _BT = {3: 2, 5: 1, 6: 0}
 _BT_INV = {v: k for k, v in _BT.items()}
@@ -227,7 +232,7 @@ class ShardSim:
             refs = set.intersection(*(set(g) for g in gs))
             for r in sorted(refs):
                 if r != d and not self._excluded(d, r):
-                    out[d % self.R].append((0, d, r))
+                    out[dep_owner(d, self.R)].append((0, d, r))
                     for q in range(self.R):
                         if q != self.rank and (lmask[d] >> q) & 1:
                             out[q].append((1, d, r))
@@ -242,7 +247,7 @@ class ShardSim:
             if w >> 63:
                 d, r = (w >> 32) & 0x7FFFFFFF, w & 0xFFFFFFFF
                 if all(r in g for g in self.dep_groups[d]):
-                    out[d % self.R].append((d << 32) | r)
+                    out[dep_owner(d, self.R)].append((d << 32) | r)
         send = np.array([x for part in out for x in part], np.int64)
         return self._req(_lib.X_ALLTOALLV_U64, send, 6, [len(p) for p in out])
 
@@ -269,7 +274,7 @@ class ShardSim:
             v = R.remove_implied(*R.split_by_arity(v))
         elif self.strategy == 1:
             v = R.s2l_exact_raw(v)
-        owned = {self.freq[d].key() for d in range(len(self.freq)) if d % self.R == self.rank}
+        owned = {self.freq[d].key() for d in range(len(self.freq)) if dep_owner(d, self.R) == self.rank}
         self.result = [c for c in v if R.Cond(c.dv1, c.dv2, c.dt).key() in owned]
         self.phase = 9
         return _lib.ExchangeRequest(_lib.X_DONE, 8, 0)
