@@ -14,6 +14,7 @@ import pytest
 
 from oracle import c_oracle as C, rdfind_oracle as R
 from rdfind_amd import _lib, ntriples, program, synth
+from tests import kats
 from tests.conftest import GOLDEN
 from tests.test_oracle import KAT_PEOPLE, KAT_PEOPLE_CLEAN, KAT_PEOPLE_RAW, read_golden
 
@@ -100,6 +101,38 @@ def test_kat_people(ctx):
         ctx.run(2, "spo", clean, 0)
         lines = sorted(program.format_rows(ctx.decoded_cinds(), dic.term))
         assert lines == (expected if expected is not None else KAT_PEOPLE_RAW)
+
+
+@pytest.mark.parametrize("kat", kats.RULE_KATS, ids=lambda k: k["name"])
+def test_rule_kats(ctx, tmp_path, kat):
+    """The hand-derived R1-R4 / 1/2, 2/1, 2/2 KATs (tests/kats.py) on the GPU in all four modes, with the heavy-group
+    paths both off and forced (every group a bit column), and through the driver from N-Triples text."""
+    arr, dic = kats.encode(kat)
+    ms, proj = kat["support"], kat["projection"]
+    want = {(1, True): "clean", (0, True): "clean", (0, False): "s0_raw", (1, False): "s2l_raw"}
+    for g in (ctx, None):
+        own = g is None
+        if own:
+            os.environ["RDFIND_HEAVY_MIN"] = "1"
+            try:
+                g = _lib.Context(0)
+            finally:
+                del os.environ["RDFIND_HEAVY_MIN"]
+        try:
+            for (strategy, clean), mode in want.items():
+                g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], dic.size)
+                g.run(ms, proj, clean, strategy)
+                got = kats.lines_of(_lib.decoded_to_set(g.decoded_cinds()), dic.term)
+                assert got == kats.expected(kat, mode), (kat["name"], strategy, clean, own)
+        finally:
+            if own:
+                g.close()
+    nt = tmp_path / "kat.nt"
+    ntriples.write_ntriples(str(nt), (f"{a} {b} {c} ." for a, b, c in kat["triples"]))
+    out = tmp_path / "out.txt"
+    program.RDFind(["--use-fis", "--clean-implied", "--support", str(ms), "--projection", proj,
+                    "--output", f"file://{out}", str(nt)]).run()
+    assert sorted(out.read_text().splitlines()) == kats.expected(kat, "clean")
 
 
 @pytest.mark.parametrize("name", ["zipf_small", "lubm_small", "skew_small"])

@@ -11,6 +11,7 @@ from hypothesis import given, settings, strategies as st
 
 from oracle import rdfind_oracle as R
 from rdfind_amd import ntriples
+from tests import kats
 from tests.conftest import GOLDEN
 
 # hand-derived: see DESIGN.md "known-answer test" for the derivation
@@ -126,3 +127,30 @@ def test_python_oracle_reproduces_golden(name, mode, strategy, clean):
     ms, expected = read_golden(name, mode)
     got = R.format_cinds(R.rdfind(golden_triples(name), ms, strategy, clean, full_prune=True))
     assert got == expected
+
+
+@pytest.mark.parametrize("kat", kats.RULE_KATS, ids=lambda k: k["name"])
+def test_rule_kats_python_oracle(kat):
+    """Hand-derived KATs (tests/kats.py) for R1-R4 and the 1/2, 2/1, 2/2 paths: the valid set V, both strategies'
+    clean output, S2L's raw output and strategy 0's raw output."""
+    tr, ms, proj = kat["triples"], kat["support"], kat["projection"]
+    uf = R.frequent_unary_conditions(tr, ms)
+    v = R.all_at_once(R.join_lines(tr, uf, R.frequent_binary_conditions(tr, uf, ms), proj), ms, False,
+                      literal_implies=False)
+    assert R.format_cinds(v) == sorted(kat["v"])
+    for strategy in (0, 1):
+        assert R.format_cinds(R.rdfind(tr, ms, strategy, True, projection=proj)) == kats.expected(kat, "clean")
+    assert R.format_cinds(R.rdfind(tr, ms, 1, False, projection=proj, full_prune=True)) == kats.expected(kat, "s2l_raw")
+    # the candidate Bloom filters' false positives and the 2/2 prune's order do not change S2L's clean output
+    for seed in range(3):
+        assert R.format_cinds(R.rdfind(tr, ms, 1, True, projection=proj, bloom_fpp=0.5, prune_seed=seed)) == \
+            kats.expected(kat, "clean")
+    assert R.format_cinds(R.rdfind(tr, ms, 0, False, projection=proj)) == kats.expected(kat, "s0_raw")
+
+
+def test_rule_kats_cover_every_rule_and_path():
+    """Every rule removes at least one hand-derived line, and every CIND kind survives in some clean result."""
+    removed = {rule for k in kats.RULE_KATS for rule in k["v"].values() if rule}
+    assert removed == {"R1", "R2", "R3", "R4"}
+    kinds = [set(i for i, part in enumerate(kats.split(kats.expected(k, "clean"))) if part) for k in kats.RULE_KATS]
+    assert set().union(*kinds) == {0, 1, 2, 3}  # 1/1, 1/2, 2/1, 2/2 all present in some clean output

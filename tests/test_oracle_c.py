@@ -6,6 +6,7 @@ import pytest
 
 from oracle import c_oracle as C, rdfind_oracle as R
 from rdfind_amd import ntriples
+from tests import kats
 from tests.test_oracle import golden_triples, read_golden
 import os
 from tests.conftest import GOLDEN
@@ -59,3 +60,16 @@ def test_c_oracle_reproduces_golden(name, mode, strategy, clean):
     got, _ = C.run_set(s, p, o, dic.size, ms, strategy, clean)
     lines = R.format_cinds([R.Cind(*x) for x in got], dic.term)
     assert lines == expected
+
+
+@pytest.mark.parametrize("kat", kats.RULE_KATS, ids=lambda k: k["name"])
+def test_rule_kats_c_oracle(kat):
+    """The hand-derived KATs (tests/kats.py) through the C restatement: clean in both strategies, strategy 0 raw, and
+    strategy 1 raw (the C oracle's raw strategy-1 mode is the valid set V)."""
+    arr, dic = kats.encode(kat)
+    ms, proj = kat["support"], kat["projection"]
+    run = lambda strategy, clean: kats.lines_of(C.run_set(arr[:, 0], arr[:, 1], arr[:, 2], dic.size, ms, strategy,
+                                                          clean, proj)[0], dic.term)
+    assert run(1, True) == run(0, True) == kats.expected(kat, "clean")
+    assert run(0, False) == kats.expected(kat, "s0_raw")
+    assert run(1, False) == sorted(kat["v"])
