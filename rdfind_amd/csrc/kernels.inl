@@ -243,18 +243,26 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_binary_emit_count(const u32* __re
     block_counter_add(total, c);
 }
 
+// u32 count that saturates at 2^32 - 1 instead of wrapping (a condition summed over the ranks' slices can reach 2^32
+// occurrences; saturation keeps every `count >= min_support` test right).  Any add that wraps sets the maximum, which
+// no later add can lower: the final value is exact below 2^32 and 2^32 - 1 otherwise.
+__device__ inline void sat_add_u32(u32* p, u32 c) {
+    const u32 old = atomicAdd(p, c);
+    if (old + c < old) atomicMax(p, 0xffffffffu);
+}
+
 __device__ inline void global_hash_add(u64* tkeys, u32* tcnt, u64 mask, u64 key, u32 c) {
     u64 h = mix64(key) & mask;
     for (;;) {
         u64 k = tkeys[h];
         if (k == key) {
-            atomicAdd(&tcnt[h], c);
+            sat_add_u32(&tcnt[h], c);
             return;
         }
         if (k == EMPTY64) {
             u64 prev = atomicCAS(&tkeys[h], EMPTY64, key);
             if (prev == EMPTY64 || prev == key) {
-                atomicAdd(&tcnt[h], c);
+                sat_add_u32(&tcnt[h], c);
                 return;
             }
         }

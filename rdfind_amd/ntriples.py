@@ -291,21 +291,47 @@ def _plain_path(path):
     return path
 
 
+_GZ_STEP = 1 << 22
+
+
+def _gz_size(path):
+    """(decompressed size, last byte) of a .gz file, streamed."""
+    n, last = 0, b""
+    with gzip.open(path, "rb") as f:
+        while chunk := f.read(_GZ_STEP):
+            n += len(chunk)
+            last = chunk[-1:]
+    return n, last
+
+
+def _gz_slice(path, a, b):
+    """Decompressed bytes [a, b) of a .gz file, streamed: the bytes before a are discarded as they come."""
+    out, pos = [], 0
+    with gzip.open(path, "rb") as f:
+        while pos < b:
+            chunk = f.read(_GZ_STEP)
+            if not chunk:
+                break
+            lo, hi = max(a - pos, 0), min(b - pos, len(chunk))
+            if lo < hi:
+                out.append(chunk[lo:hi])
+            pos += len(chunk)
+    return b"".join(out)
+
+
 def read_byte_range(paths, rank: int, nranks: int) -> bytes:
     """This rank's part of the input for the sharded ingest: the bytes of the whole lines that start in
     [T * rank / nranks, T * (rank + 1) / nranks) of the concatenated input of T bytes (read_bytes' stream: a line
     break after a file without one).  A line belongs to the rank its first byte falls to, so the parts partition the
     lines (the reference's input splits, FLK/persistence/MultiFileTextInputFormat.java:49-100).  Plain files are
-    read by seeking to the range; a .gz file cannot be split and is decompressed whole, keeping only the range."""
+    read by seeking to the range; a .gz file cannot be split, so it is stream-decompressed (once for its size, then up
+    to the end of the range) and only the range is kept: no rank holds a whole compressed input."""
     files = []  # (path, size of its stream part, gz)
     for path in paths:
         path = _plain_path(path)
         if path.endswith(".gz"):
-            with gzip.open(path, "rb") as f:
-                data = f.read()
-            if data and not data.endswith(b"\n"):
-                data += b"\n"
-            files.append((path, len(data), data))
+            size, last = _gz_size(path)
+            files.append((path, size + (0 if last in (b"", b"\n") else 1), True))
         else:
             size = os.path.getsize(path)
             with open(path, "rb") as f:
@@ -323,8 +349,11 @@ def read_byte_range(paths, rank: int, nranks: int) -> bytes:
         for path, sz, data in files:
             s0, s1 = max(a, base), min(b, base + sz)
             if s0 < s1:
-                if data is not None:
-                    out.append(data[s0 - base:s1 - base])
+                if data:
+                    chunk = _gz_slice(path, s0 - base, s1 - base)
+                    if len(chunk) < s1 - s0:  # the virtual line break after a file without one
+                        chunk += b"\n"
+                    out.append(chunk)
                 else:
                     with open(path, "rb") as f:
                         f.seek(s0 - base)
