@@ -2497,6 +2497,232 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_clear_bits(u64* words, u64 n, u64
 }
 
 // verify pass plan: candidates = the verify pairs of d, groups = all local light groups of d (no pivot skipped)
+// ---- light pass B, group-major (IntersectCindCandidates.scala:40-43: a ref survives iff it is in every group of the
+// dependent).  Pass B's candidate-major verification searches every surviving candidate in every light group of its
+// dependent: (survivors x groups x log2 n) divergent loads.  For a dependent with many survivors that are mostly true
+// refs (c4: 1,570 survivors of a 2,229-member pivot through ~800 light groups of ~8k members) one coalesced sweep of each
+// light group's members, marking the candidates it holds (an LDS hash of the dependent's survivors), reads ~Σ n_g words
+// instead.  k_gm_select picks, per dependent, the cheaper of the two by their estimated lines read; k_light_gm verifies
+// the chosen ones, one block per (dependent, chunk of <= GM_CAND survivors, segment of GM_SEG group entries), and flags
+// the survivors some light group lacks (gdead, one byte per survivor of vpairs).
+static constexpr u32 GM_CAND = 4096;   // survivors per block (LDS: hash keys 32 KB + indices 16 KB + bitmaps)
+static constexpr u32 GM_HASH = 8192;   // LDS hash slots (load <= 1/2)
+static constexpr u64 GM_SEG = 256;     // group entries of the dependent per block (64 per wave)
+static constexpr u32 GM_MIN_SURV = 16; // fewer survivors: candidate-major always
+
+__device__ inline u32 gm_hash(u32 x) { return hash32(x) & (GM_HASH - 1); }
+
+// per dependent with pass-B survivors: light groups, their members, the survivors -> gm (1: group-major), its k_light_gm
+// items, and the candidate-major plan of the group-major dependents cleared (one wave per dependent)
+__device__ inline void k_gm_select_body(u64 vblk, CindView v, const u32* __restrict__ pivot, int mode, u32* gm,
+                                        u32* gmitems, u32* nchunk_light, u32* nitem_light, u32* npacked) {
+    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (w >= v.C) return;
+    const u32 d = (u32)w;
+    const int lane = lane_id();
+    const u64 S = v.vcoff[d + 1] - v.vcoff[d];
+    const u64 b = v.doff[d], e = v.doff[d + 1];
+    bool pick = false;
+    if (mode && S >= (mode == 2 ? 1u : GM_MIN_SURV) && e > b) {
+        const u32 piv = pivot[d], p2 = v.piv2 ? v.piv2[d] : NONE32;
+        u64 m = 0, sum = 0, lg = 0;
+        for (u64 j = b + lane; j < e; j += RDF_WAVE) {
+            const u32 g = v.dgrp[j];
+            if ((g & DGRP_HEAVY) || g == piv || g == p2) continue;
+            const u32 n = v.ginfo[g] & ~GINFO_HEAVY;
+            ++m;
+            sum += n;
+            lg += n > 1 ? 32 - __clz(n - 1) : 1;  // search levels
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            m += __shfl_xor(m, off, RDF_WAVE);
+            sum += __shfl_xor(sum, off, RDF_WAVE);
+            lg += __shfl_xor(lg, off, RDF_WAVE);
+        }
+        // lines read: candidate-major ~ one 64-B sector per search level per (survivor, group); group-major ~ the
+        // members (16 per sector) + two 64-lane bound probes per group
+        const u64 cm = S * lg, gmc = sum / 16 + 2 * RDF_WAVE * m;
+        pick = m && (mode == 2 || gmc < cm);
+    }
+    if (lane == 0) {
+        gm[d] = pick ? 1u : 0u;
+        gmitems[d] = pick ? (u32)(((S + GM_CAND - 1) / GM_CAND) * ((e - b + GM_SEG - 1) / GM_SEG)) : 0u;
+        if (pick) nchunk_light[d] = nitem_light[d] = npacked[d] = 0;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_gm_select(u64 nvblk, CindView v, const u32* __restrict__ pivot, int mode,
+                                                         u32* gm, u32* gmitems, u32* nchunk_light, u32* nitem_light,
+                                                         u32* npacked) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
+        k_gm_select_body(vb, v, pivot, mode, gm, gmitems, nchunk_light, nitem_light, npacked);
+}
+
+// lower_bound(lo_key) and upper_bound(hi_key) in the sorted a[0, n) by 64-ary probes: per level every lane loads one of
+// 64 splitters of the remaining interval (both bounds from one pair of ballots), so ~8k members take three levels instead
+// of thirteen dependent steps of a binary search; the last interval of <= 64 members is read whole
+__device__ inline u64 gm_pos(u64 b, u64 len, int l) { return b + (len * (u64)(l + 1)) / 65; }
+__device__ inline void gm_bounds(const u32* __restrict__ a, u64 n, u32 lo_key, u32 hi_key, u64* lo, u64* hi) {
+    const int lane = lane_id();
+    u64 b0 = 0, e0 = n, b1 = 0, e1 = n;  // the bound lies in [b, e]
+    bool done0 = false, done1 = false;
+    while (!(done0 && done1)) {
+        const u64 l0 = e0 - b0, l1 = e1 - b1;
+        bool t0 = false, t1 = false;
+        if (!done0) t0 = l0 <= RDF_WAVE ? ((u64)lane < l0 && a[b0 + lane] < lo_key) : a[gm_pos(b0, l0, lane)] < lo_key;
+        if (!done1) t1 = l1 <= RDF_WAVE ? ((u64)lane < l1 && a[b1 + lane] <= hi_key) : a[gm_pos(b1, l1, lane)] <= hi_key;
+        const int k0 = __popcll(__ballot(t0)), k1 = __popcll(__ballot(t1));  // splitters below the key (a prefix)
+        if (!done0) {
+            if (l0 <= RDF_WAVE) {
+                b0 += k0;
+                done0 = true;
+            } else {
+                const u64 nb = k0 ? gm_pos(b0, l0, k0 - 1) + 1 : b0;
+                e0 = k0 < RDF_WAVE ? gm_pos(b0, l0, k0) : e0;
+                b0 = nb;
+            }
+        }
+        if (!done1) {
+            if (l1 <= RDF_WAVE) {
+                b1 += k1;
+                done1 = true;
+            } else {
+                const u64 nb = k1 ? gm_pos(b1, l1, k1 - 1) + 1 : b1;
+                e1 = k1 < RDF_WAVE ? gm_pos(b1, l1, k1) : e1;
+                b1 = nb;
+            }
+        }
+    }
+    *lo = b0;
+    *hi = b1 > b0 ? b1 : b0;
+}
+
+__device__ inline void k_light_gm_body(u64 vblk, CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
+                                       const u32* __restrict__ item_dep, u64 W, uint8_t* gdead, u32* s_key,
+                                       uint16_t* s_idx, u32* s_alive, u32* s_found) {
+    if (vblk >= W) return;
+    const u32 d = item_dep[vblk];
+    const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
+    const u64 nseg = (e0 - b0 + GM_SEG - 1) / GM_SEG;
+    const u64 item = vblk - itemoff[d];
+    const u64 q = item / nseg, seg = item % nseg;
+    const u64 c0 = v.vcoff[d] + q * GM_CAND;
+    const u64 c1 = c0 + GM_CAND < v.vcoff[d + 1] ? c0 + GM_CAND : v.vcoff[d + 1];
+    const u32 S = (u32)(c1 - c0);
+    const u32 NW = (S + 31) / 32;
+    const int lane = lane_id(), wv = threadIdx.x / RDF_WAVE;
+    u32* found = s_found + wv * (GM_CAND / 32);
+    for (u32 k = threadIdx.x; k < GM_HASH; k += RDF_BLOCK) s_key[k] = EMPTY32;
+    for (u32 k = threadIdx.x; k < GM_CAND / 32; k += RDF_BLOCK) s_alive[k] = k < NW ? (k + 1 < NW || !(S & 31) ? ~0u : (1u << (S & 31)) - 1u) : 0u;
+    for (u32 k = threadIdx.x; k < RDF_WAVES_PER_BLOCK * (GM_CAND / 32); k += RDF_BLOCK) s_found[k] = 0;
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < S; k += RDF_BLOCK) {
+        const u32 x = (u32)v.vpairs[c0 + k];
+        u32 h = gm_hash(x);
+        while (atomicCAS(&s_key[h], EMPTY32, x) != EMPTY32) h = (h + 1) & (GM_HASH - 1);
+        s_idx[h] = (uint16_t)k;
+    }
+    __syncthreads();
+    const u32 cmin = (u32)v.vpairs[c0], cmax = (u32)v.vpairs[c1 - 1];  // the survivors ascend
+    const u32 piv = pivot[d], p2 = v.piv2 ? v.piv2[d] : NONE32;
+    const u64 jb = b0 + seg * GM_SEG, je = jb + GM_SEG < e0 ? jb + GM_SEG : e0;
+    for (u64 j = jb + wv; j < je; j += RDF_WAVES_PER_BLOCK) {
+        const u32 g = v.dgrp[j];
+        if ((g & DGRP_HEAVY) || g == piv || g == p2) continue;
+        // anything left to verify?  (other waves clear bits concurrently: a stale word only costs a sweep)
+        bool any = false;
+        for (u32 k = lane; k < NW; k += RDF_WAVE) any |= s_alive[k] != 0;
+        if (!__any(any)) break;
+        const u32* dr = dense_row(v, g);
+        if (dr) {  // dense group: one bitmap word per alive candidate (lanes over candidates)
+            for (u32 k = lane; k < S; k += RDF_WAVE) {
+                const u32 bit = 1u << (k & 31);
+                if ((s_alive[k >> 5] & bit) && !dense_has(dr, (u32)v.vpairs[c0 + k])) atomicAnd(&s_alive[k >> 5], ~bit);
+            }
+            continue;
+        }
+        const u64 gb = v.goff[g], n = v.goff[g + 1] - gb;
+        u64 lo, hi;
+        gm_bounds(v.gcap + gb, n, cmin, cmax, &lo, &hi);
+        // sweep the members in [cmin, cmax]: 4 coalesced loads in flight per lane, each member looked up in the hash
+        for (u64 i0 = gb + lo; i0 < gb + hi; i0 += 4 * RDF_WAVE) {
+            u32 x[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const u64 i = i0 + (u64)t * RDF_WAVE + lane;
+                x[t] = i < gb + hi ? v.gcap[i] : EMPTY32;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (x[t] == EMPTY32) continue;
+                u32 h = gm_hash(x[t]);
+                for (;;) {
+                    const u32 k = s_key[h];
+                    if (k == x[t]) {
+                        const u32 idx = s_idx[h];
+                        atomicOr(&found[idx >> 5], 1u << (idx & 31));
+                        break;
+                    }
+                    if (k == EMPTY32) break;
+                    h = (h + 1) & (GM_HASH - 1);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (u32 k = lane; k < NW; k += RDF_WAVE) {
+            const u32 f = found[k];
+            if (~f & s_alive[k]) atomicAnd(&s_alive[k], f);
+            found[k] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < S; k += RDF_BLOCK)
+        if (!((s_alive[k >> 5] >> (k & 31)) & 1u)) gdead[c0 + k] = 1;  // several segments may write the same 1
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_gm(u64 nvblk, CindView v, const u32* __restrict__ pivot,
+                                                        const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
+                                                        u64 W, uint8_t* gdead) {
+    __shared__ u32 s_key[GM_HASH];
+    __shared__ uint16_t s_idx[GM_HASH];
+    __shared__ u32 s_alive[GM_CAND / 32];
+    __shared__ u32 s_found[RDF_WAVES_PER_BLOCK * (GM_CAND / 32)];
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
+        k_light_gm_body(vb, v, pivot, itemoff, item_dep, W, gdead, s_key, s_idx, s_alive, s_found);
+        __syncthreads();  // the block's LDS is reused by its next item
+    }
+}
+
+// pass A's tagged slots after pass B: candidate-major dependents keep the pairs pass B verified (bpairs / boff), group-
+// major ones the survivors k_light_gm did not flag (vpairs / voff / gdead)
+__global__ __launch_bounds__(RDF_BLOCK) void k_tag_fix_gm(u64* slots, u32* counts, const u32* __restrict__ flags, u64 W,
+                                                          const u64* __restrict__ bpairs, const u64* __restrict__ boff,
+                                                          const u32* __restrict__ gm, const u64* __restrict__ vpairs,
+                                                          const u64* __restrict__ voff, const uint8_t* __restrict__ gdead) {
+    for (u64 o = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; o < W; o += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 n = flags[o];
+        if (!n) continue;
+        u32 k = 0;
+        for (u32 j = 0; j < n; ++j) {
+            const u64 x = slots[o * 8 + j] & ~(u64)PRE_TAG;
+            const u64 d = x >> 32;
+            bool keep;
+            if (gm[d]) {
+                const u64 p = lower_bound_u64(vpairs + voff[d], voff[d + 1] - voff[d], x);
+                keep = !gdead[voff[d] + p];
+            } else {
+                keep = bsearch_u64(bpairs + boff[d], boff[d + 1] - boff[d], x);
+            }
+            if (keep) slots[o * 8 + k++] = x;
+        }
+        counts[o] = k;
+    }
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_verify_plan(CindView v, const u32* __restrict__ nlight_in, u32* nchunk_light,
                                                            u32* nitem_light, u32* npacked) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {

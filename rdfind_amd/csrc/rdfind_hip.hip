@@ -129,6 +129,8 @@ struct rdf_ctx {
     DevBuf lmask, hrep, vpairs, vcoff, vpiv;  // holder-first light exchange (sh_phase5 / sh_phase15)
     DevBuf ebown, segb, sege, seglen;         // this rank's binary dependents' final pairs; dependent segments
     DevBuf bslots, bcounts;                   // light pass B's output slots (pass A's stay in epairs_tmp / lslot)
+    DevBuf gmflag, gmitems, gmioff, gmdep, gdead, voff2;  // light pass B, group-major (k_gm_select / k_light_gm)
+    u64 n_gm_deps = 0, n_gm_items = 0;
     DevBuf ukeys, ukeys_tmp;                  // sharded: frequent unary keys (owned, then every rank's, sorted)
     // sharded ingest (rdf_shard_parse_begin): local terms routed to their owners, the owner's dictionary, global ids
     DevBuf ithv, ikeys, ikeys_tmp, iwords, iwoff, ihdr, ipay, ibnd, iwb, rhdr, rlen, rwords, rwoff, rts, rhv, rvalid, rtab,
@@ -296,7 +298,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->bslots, &c->bcounts, &c->segb, &c->sege, &c->seglen, &c->ukeys,
+            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->bslots, &c->bcounts, &c->gmflag, &c->gmitems, &c->gmioff, &c->gmdep, &c->gdead, &c->voff2, &c->segb, &c->sege, &c->seglen, &c->ukeys,
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
@@ -1984,6 +1986,39 @@ static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL
             hipLaunchKernelGGL(k_verify_plan, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, vb, c->pnl.as<u32>(),
                                c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>());
         tend(c, RDF_T_LIGHT);
+        // dependents with many survivors: group-major sweeps of their light groups instead (k_gm_select picks them and
+        // clears their candidate-major plan); RDFIND_LIGHT_GM=0 keeps every dependent candidate-major, 2 none
+        static const int gm_mode = getenv("RDFIND_LIGHT_GM") ? atoi(getenv("RDFIND_LIGHT_GM")) : 1;
+        u64 WG = 0;
+        c->n_gm_items = 0;
+        if (gm_mode && C) {
+            tbegin(c, RDF_T_LIGHT);
+            ENSURE(c, gmflag, (u64)C * 4);
+            ENSURE(c, gmitems, (u64)C * 4);
+            ENSURE(c, gmioff, (C + 1ull) * 8);
+            ENSURE(c, voff2, (C + 1ull) * 8);
+            HIP_TRY(c, hipMemcpyAsync(c->voff2.p, c->vcoff.p, (C + 1ull) * 8, hipMemcpyDeviceToDevice, st));
+            vb.vcoff = c->voff2.as<u64>();  // the survivors' offsets (vcoff is rewritten for pass B's pairs below)
+            hipLaunchKernelGGL(k_gm_select, dim3(vgrid(wave_blocks(C))), dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(C), vb,
+                               pivot, gm_mode, c->gmflag.as<u32>(), c->gmitems.as<u32>(), c->nchl.as<u32>(),
+                               c->nitl.as<u32>(), c->npk.as<u32>());
+            HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->gmitems.as<u32>(), c->gmioff.as<u64>(), C, c->gmioff.as<u64>() + C, st));
+            tend(c, RDF_T_LIGHT);
+            TRY(read_u64(c, c->gmioff.as<u64>() + C, &WG));
+            c->n_gm_items = WG;
+            if (WG) {
+                tbegin(c, RDF_T_LIGHT);
+                ENSURE(c, gmdep, WG * 4);
+                ENSURE(c, gdead, T);
+                HIP_TRY(c, hipMemsetAsync(c->gdead.p, 0, T, st));
+                hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                                   c->gmioff.as<u64>(), C, c->gmdep.as<u32>());
+                hipLaunchKernelGGL(k_light_gm, dim3(vgrid(WG)), dim3(RDF_BLOCK), 0, st, WG, vb, pivot, c->gmioff.as<u64>(),
+                                   c->gmdep.as<u32>(), WG, c->gdead.as<uint8_t>());
+                tend(c, RDF_T_LIGHT);
+            }
+            vb.vcoff = c->vcoff.as<u64>();
+        }
         const u64 hc = c->heavy_candidates, lc = c->light_candidates, le = c->light_entries;
         u64 WL2 = 0, WH2 = 0, WI2 = 0, WP2 = 0, WM2 = 0, EB = 0;
         TRY(d_chunks(c, &WL2, &WH2, &WI2, &WP2));
@@ -1997,8 +2032,14 @@ static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL
         tbegin(c, RDF_T_LIGHT);
         hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->cpairs.as<u64>(), EB, C, c->Cu, c->vcoff.as<u64>(), c->ebin.as<u64>());
-        hipLaunchKernelGGL(k_tag_fix, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
-                           c->lslot.as<u32>(), c->flags.as<u32>(), WL, c->cpairs.as<u64>(), c->vcoff.as<u64>());
+        if (WG)
+            hipLaunchKernelGGL(k_tag_fix_gm, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                               c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->flags.as<u32>(), WL, c->cpairs.as<u64>(),
+                               c->vcoff.as<u64>(), c->gmflag.as<u32>(), c->vpairs.as<u64>(), c->voff2.as<u64>(),
+                               c->gdead.as<uint8_t>());
+        else
+            hipLaunchKernelGGL(k_tag_fix, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
+                               c->lslot.as<u32>(), c->flags.as<u32>(), WL, c->cpairs.as<u64>(), c->vcoff.as<u64>());
         tend(c, RDF_T_LIGHT);
     }
     return d_light_compact(c, WL, c->epairs_tmp, c->lslot, c->epairs, 0, E);
@@ -2314,9 +2355,9 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (two) TRY(d_light_two_pass(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     else TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     if (getenv("RDFIND_LIGHT2_LOG"))
-        fprintf(stderr, "LIGHT2 two=%d items=%llu multi_chunk_items=%llu survivors=%llu explicit=%llu\n", (int)two,
-                (unsigned long long)WI, (unsigned long long)c->n_multi_items, (unsigned long long)c->n_light_survivors,
-                (unsigned long long)E);
+        fprintf(stderr, "LIGHT2 two=%d items=%llu multi_chunk_items=%llu survivors=%llu gm_items=%llu explicit=%llu\n",
+                (int)two, (unsigned long long)WI, (unsigned long long)c->n_multi_items,
+                (unsigned long long)c->n_light_survivors, (unsigned long long)c->n_gm_items, (unsigned long long)E);
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));

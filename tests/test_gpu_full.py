@@ -204,7 +204,9 @@ with _lib.Context(0) as ctx:
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("env", [{"RDFIND_STAGE": "0"}, {"RDFIND_STAGE": "1"},
                                  {"RDFIND_SIG": "0", "RDFIND_PIV2": "0"}, {"RDFIND_SIG": "1", "RDFIND_PIV2": "2"},
-                                 {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}, {"RDFIND_LIGHT2": "1"}])
+                                 {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}, {"RDFIND_LIGHT2": "1"},
+                                 {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "2"}, {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "0"},
+                                 {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "2", "RDFIND_DENSE": "0"}])
 def test_light_variants_full_size(env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
     paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
@@ -277,16 +279,17 @@ print(json.dumps({"bad": bad}))
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("heavy_min", ["64", "2"])
-def test_two_light_passes_random(heavy_min):
+@pytest.mark.parametrize("heavy_min,gm", [("64", "1"), ("2", "1"), ("64", "2"), ("2", "2")])
+def test_two_light_passes_random(heavy_min, gm):
     """The filter + verify light passes forced on random inputs (RDFIND_LIGHT2=1; LIGHT_PRE_MAX defers every chunk of
-    a multi-chunk dependent) against the C oracle in three modes, with and without lowered heavy columns.  In its own
+    a multi-chunk dependent) against the C oracle in three modes, with and without lowered heavy columns, pass B
+    choosing group-major per dependent (RDFIND_LIGHT_GM=1) or group-major for every dependent (2).  In its own
     process: the switch is read once per process."""
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RDFIND_LIGHT2="1", RDFIND_HEAVY_MIN=heavy_min)
+    env = dict(os.environ, RDFIND_LIGHT2="1", RDFIND_HEAVY_MIN=heavy_min, RDFIND_LIGHT_GM=gm)
     r = subprocess.run([sys.executable, "-c", _TWO_PASS_CHILD, root, "71" + heavy_min], env=env, capture_output=True,
                        text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
