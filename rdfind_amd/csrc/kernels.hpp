@@ -71,6 +71,15 @@ static constexpr int LIGHT_STAGE_MIN = RDF_STAGE_MIN;
 static constexpr u64 LIGHT_STAGE_AVG = RDF_STAGE_AVG;  // staging variant when the weighted mean light group is smaller
                   // groups up to this size are searched in LDS (2 KiB per wave)
 
+#ifndef RDF_SWEEP_F
+#define RDF_SWEEP_F 64
+#endif
+#ifndef RDF_SWEEP_MIN
+#define RDF_SWEEP_MIN 16
+#endif
+static constexpr int LIGHT_SWEEP_F = RDF_SWEEP_F;      // default of CindView::sweep_f (RDFIND_SWEEP_F)
+static constexpr int LIGHT_SWEEP_MIN = RDF_SWEEP_MIN;  // alive candidates from which a window may be swept
+
 static constexpr int EMIT_DEDUP_SLOTS = 4096;  // K3 write pass: LDS hash of one iteration's <= 9 x 256 records
 static constexpr u64 EMIT_PAD = ~0ull;         // K3 padding of removed duplicates (no record has all bits set)
 static constexpr u32 PRE_TAG = 0x80000000u;  // light pass A: an unverified survivor (ref bit 31; compact ids < 2^31)
@@ -123,6 +132,8 @@ struct CindView {
     u64 dwords;
     int prefilter;        // light pass A: dependents of several chunks only filtered (survivors tagged PRE_TAG)
     int p2done;           // light pass B: the given candidates already passed the second pivot
+    int sweep_f;          // k_light range sweep: a window's groups are swept when their members in the alive candidates'
+                          // value range number <= sweep_f per (alive candidate, light group) pair (0: never)
 };
 
 }  // namespace rdf

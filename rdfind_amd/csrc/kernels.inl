@@ -1433,6 +1433,113 @@ __device__ inline void light_batch(const u32* gm, u64 gsz, const u32* drow, u32 
         if (bit[k] >= 0 && !__all(g == NONE32 || ok[k])) alive &= ~(1ull << bit[k]);
 }
 
+// Range sweep of a window (lanes over its groups, many candidates alive).  A candidate-major batch searches every alive
+// candidate in every lane's group: per (candidate, group) a ~log2(n)-level chain of divergent loads.  The alive
+// candidates of a chunk are consecutive pivot members, so they span a narrow slice of the capture-id space: each lane
+// bounds its group's members to [min, max] of the alive candidates (two searches in flight), and when those members are
+// few per (candidate, group) pair, the wave reads them all instead -- coalesced, SWEEP_U loads in flight per lane, the
+// window's ranges concatenated so every lane stays busy -- and marks the candidates each group holds.  Returns false
+// (nothing done) when the slices are too large for that to pay; the caller then batches as before.
+// LDS per wave (the light pass's 2 KB slice): member starts (u64) and range prefix (u32) per lane, the lanes' candidates,
+// the per-group found masks (u64).
+#ifndef RDF_SWEEP_U
+#define RDF_SWEEP_U 8
+#endif
+static constexpr int SWEEP_U = RDF_SWEEP_U;
+__device__ inline bool light_sweep(const CindView& v, const u32* gm, u64 gsz, u32 g, u32 cand, u64& alive, u32* buf) {
+    const int lane = lane_id();
+    const bool mine = (alive >> lane) & 1ull;
+    u32 cmn = mine ? cand : 0xffffffffu, cmx = mine ? cand : 0u;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const u32 a = __shfl_xor(cmn, off, RDF_WAVE), b = __shfl_xor(cmx, off, RDF_WAVE);
+        cmn = a < cmn ? a : cmn;
+        cmx = b > cmx ? b : cmx;
+    }
+    u64 lo = 0, hi = 0;
+    if (g != NONE32 && gsz) {  // lower_bound(cmn), upper_bound(cmx): two independent chains
+        u64 b0 = 0, n0 = gsz, b1 = 0, n1 = gsz;
+        while (n0 > 0 || n1 > 0) {
+            if (n0 > 0) {
+                const u64 h = n0 >> 1;
+                if (gm[b0 + h] < cmn) { b0 += h + 1; n0 -= h + 1; } else n0 = h;
+            }
+            if (n1 > 0) {
+                const u64 h = n1 >> 1;
+                if (gm[b1 + h] <= cmx) { b1 += h + 1; n1 -= h + 1; } else n1 = h;
+            }
+        }
+        lo = b0;
+        hi = b1 > b0 ? b1 : b0;
+    }
+    const u32 r = (u32)(hi - lo);
+    const u32 incl = wave_inclusive_scan(r);
+    const u32 R = __shfl(incl, RDF_WAVE - 1, RDF_WAVE);
+    const u32 nl = (u32)__popcll(__ballot(g != NONE32));
+    if ((u64)R > (u64)v.sweep_f * (u64)__popcll(alive) * nl) return false;
+    u64* s_start = (u64*)buf;                 // [64] first member of each lane's slice (global index into gcap)
+    u32* s_pre = buf + 2 * RDF_WAVE;          // [65] exclusive prefix of the slice lengths
+    u32* s_cand = s_pre + RDF_WAVE + 1;       // [64] the lanes' candidates (ascending)
+    u64* s_found = (u64*)(buf + 4 * RDF_WAVE + 2);  // [64] candidates found in lane l's group (8-B aligned: 258 words)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // earlier reads of buf precede the refill
+    __builtin_amdgcn_wave_barrier();
+    s_start[lane] = (u64)(gm - v.gcap) + lo;
+    s_pre[lane] = incl - r;
+    if (lane == 0) s_pre[RDF_WAVE] = R;
+    // the lanes' candidates, ascending: a lane without an alive candidate repeats the nearest alive one below it, so a
+    // lower bound lands on the alive lane (pivot members ascend by lane; filtered lanes hold NONE32)
+    u32 cv = mine ? cand : 0u;
+#pragma unroll
+    for (int off = 1; off < RDF_WAVE; off <<= 1) {
+        const u32 t = __shfl_up(cv, off, RDF_WAVE);
+        if (lane >= off) cv = t > cv ? t : cv;
+    }
+    s_cand[lane] = cv;
+    s_found[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (u32 base = 0; base < R; base += SWEEP_U * RDF_WAVE) {
+        u32 x[SWEEP_U];
+        int owner[SWEEP_U];
+#pragma unroll
+        for (int u = 0; u < SWEEP_U; ++u) {
+            const u32 f = base + (u32)u * RDF_WAVE + (u32)lane;
+            owner[u] = -1;
+            x[u] = 0;
+            if (f < R) {
+                int a = 0, b = RDF_WAVE - 1;  // last lane whose slice starts at or before f
+                while (a < b) {
+                    const int m = (a + b + 1) >> 1;
+                    if (s_pre[m] <= f) a = m;
+                    else b = m - 1;
+                }
+                owner[u] = a;
+                x[u] = v.gcap[s_start[a] + (f - s_pre[a])];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SWEEP_U; ++u) {
+            if (owner[u] < 0) continue;
+            int a = 0, b = RDF_WAVE;  // lower_bound of the member among the 64 candidates
+            while (a < b) {
+                const int m = (a + b) >> 1;
+                if (s_cand[m] < x[u]) a = m + 1;
+                else b = m;
+            }
+            if (a < RDF_WAVE && s_cand[a] == x[u]) atomicOr((unsigned long long*)&s_found[owner[u]], 1ull << a);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    u64 keep = g != NONE32 ? s_found[lane] : ~0ull;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) keep &= __shfl_xor(keep, off, RDF_WAVE);
+    alive &= keep;
+    return true;
+}
+
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
@@ -1561,6 +1668,9 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             }
             const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
             const u64 gsz = gszv[it];
+            if (v.sweep_f && __popcll(alive) >= LIGHT_SWEEP_MIN && !__any(gdr[it] != nullptr && g != NONE32) &&
+                light_sweep(v, gm, gsz, g, cand, alive, s_light[threadIdx.x / RDF_WAVE]))
+                continue;
             if (STAGE && __popcll(alive) >= LIGHT_STAGE_MIN && __all(g == NONE32 || gsz <= LIGHT_SMALL)) {
                 // every light group of the window is small: each lane copies its group into its own LDS row with
                 // <= 9 aligned 16-B loads, then the alive candidates are searched in LDS (instead of A x log2 n

@@ -1628,6 +1628,8 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.dwords = c->dwords;
     v.prefilter = 0;
     v.p2done = 0;
+    static const int sweep_f = getenv("RDFIND_SWEEP_F") ? atoi(getenv("RDFIND_SWEEP_F")) : LIGHT_SWEEP_F;
+    v.sweep_f = sweep_f;
     return v;
 }
 

@@ -360,6 +360,7 @@ def test_join_range_groups_parity(monkeypatch, range_records):
                     (n, nv, ms, strategy, clean, range_records)
                 assert compact_matches(g, nv)
             gpu_set(ref, arr, nv, ms, 1, True)
+            gpu_set(g, arr, nv, ms, 1, True)
             keys = ("n_records", "n_sorted_records", "n_frequent_records", "n_groups", "n_captures", "n_heavy_groups")
             assert {k: g.groups[k] for k in keys} == {k: ref.groups[k] for k in keys}
             assert (g.cind_count(), g.checksum()) == (ref.cind_count(), ref.checksum())
