@@ -80,7 +80,11 @@ static constexpr u64 LIGHT_STAGE_AVG = RDF_STAGE_AVG;  // staging variant when t
 static constexpr int LIGHT_SWEEP_F = RDF_SWEEP_F;      // default of CindView::sweep_f (RDFIND_SWEEP_F)
 static constexpr int LIGHT_SWEEP_MIN = RDF_SWEEP_MIN;  // alive candidates from which a window may be swept
 
-static constexpr int EMIT_DEDUP_SLOTS = 4096;  // K3 write pass: LDS hash of one iteration's <= 9 x 256 records
+#ifndef RDF_EMIT_DEDUP_SLOTS
+#define RDF_EMIT_DEDUP_SLOTS 4096
+#endif
+static constexpr int EMIT_DEDUP_SLOTS = RDF_EMIT_DEDUP_SLOTS;  // K3 write pass: LDS hash of one iteration's repeating
+                                                               // records (<= 4 x 256)
 static constexpr u64 EMIT_PAD = ~0ull;         // K3 padding of removed duplicates (no record has all bits set)
 static constexpr u32 PRE_TAG = 0x80000000u;  // light pass A: an unverified survivor (ref bit 31; compact ids < 2^31)
 #ifndef RDF_PRE_MAX

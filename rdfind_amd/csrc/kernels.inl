@@ -352,6 +352,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_bin_freq_scatter(const u64* __res
 }
 
 // lookup table of frequent binary keys -> index b (keys sorted, so b is deterministic)
+// binary keys (bt << 62 | v1 << 31 | v2) <-> (bt << 2jb | v1 << jb | v2), values < 2^jb: the dense form keeps the
+// order and needs 2 + 2jb radix bits instead of 64
+__global__ __launch_bounds__(RDF_BLOCK) void k_bkey_repack(u64* __restrict__ keys, u64 B, int jb, int unpack) {
+    const u64 m = (1ull << jb) - 1;
+    for (u64 b = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; b < B; b += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = keys[b];
+        keys[b] = unpack ? bin_key(k >> (2 * jb), (k >> jb) & m, k & m)
+                         : ((u64)bin_key_type(k) << (2 * jb)) | ((u64)bin_key_v1(k) << jb) | bin_key_v2(k);
+    }
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_bin_lookup_build(const u64* __restrict__ bkeys, u64 B, u64* lkeys, u32* lvals,
                                                                 u64 mask) {
     for (u64 b = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; b < B; b += (u64)gridDim.x * RDF_BLOCK) {

@@ -916,8 +916,13 @@ static rdf_status fc_binary_index(rdf_ctx* c, u64 B) {
     {
         u64* k = c->bkeys.as<u64>();
         u64* t = c->bkeys_tmp.as<u64>();
-        HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, 64, st));
+        const int jb = c->V ? bits_for(c->V - 1) : 31;
+        const bool dense = B && jb < 31;
+        const dim3 g(grid_for(B, RDF_BLOCK, kGrid));
+        if (dense) hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, k, B, jb, 0);
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, dense ? 2 + 2 * jb : 64, st));
         if (k != c->bkeys.as<u64>()) std::swap(c->bkeys, c->bkeys_tmp);
+        if (dense) hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, jb, 1);
     }
     c->lcap = next_pow2(2 * B + 16);
     ENSURE(c, lkeys, c->lcap * 8);
