@@ -44,6 +44,7 @@ typedef struct {
     uint64_t n_freq_captures;   /* captures with support >= ms */
     uint64_t n_raw_cinds;       /* |V| before minimality */
     uint64_t n_cinds;
+    uint64_t n_join_ranges;     /* join-value ranges stages 3-4 ran in */
 } orc_stats;
 
 /* ---------------------------------------------------------------- utils */
@@ -163,19 +164,43 @@ typedef struct {
     uint64_t nb;          /* frequent binary conditions (sorted keys) */
     uint64_t *bkeys;
     uint64_t ncap, ng;    /* capture id space 6V + nb; groups */
-    uint32_t *support;    /* [ncap + 1] distinct join values per capture */
+    uint32_t *fidx;       /* [ncap] index of a frequent capture (support >= ms) among them, ~0 otherwise */
+    uint64_t C;           /* frequent captures */
+    uint32_t *csup;       /* [C] their supports (distinct join values) */
+    uint64_t *cdoff;      /* [C + 1] their groups in dgrp */
     uint64_t *goff;       /* [ng + 1] */
     uint32_t *gcap;       /* group members, ascending capture ids */
-    uint64_t *doff;       /* [ncap + 1] groups of each frequent capture */
     uint32_t *dgrp;
 } orc_csr;
 
+#define ORC_NONE 0xffffffffu
+
 static void csr_free(orc_csr *c) {
-    free(c->support); free(c->goff); free(c->gcap); free(c->doff); free(c->dgrp);
+    free(c->fidx); free(c->csup); free(c->cdoff); free(c->goff); free(c->gcap); free(c->dgrp);
 }
+
+/* support[ncap] -> fidx / csup / cdoff (the frequent captures in id order); returns C */
+static uint64_t compact_captures(orc_csr *c, const uint32_t *support, uint64_t ncap, uint32_t ms) {
+    c->fidx = (uint32_t *)xmalloc(ncap * sizeof(uint32_t));
+    uint64_t C = 0;
+    for (uint64_t a = 0; a < ncap; ++a) c->fidx[a] = support[a] >= ms ? (uint32_t)C++ : ORC_NONE;
+    c->C = C;
+    c->csup = (uint32_t *)xmalloc(C * sizeof(uint32_t));
+    c->cdoff = (uint64_t *)xmalloc((C + 1) * sizeof(uint64_t));
+    uint64_t acc = 0;
+    for (uint64_t a = 0; a < ncap; ++a)
+        if (c->fidx[a] != ORC_NONE) { c->csup[c->fidx[a]] = support[a]; c->cdoff[c->fidx[a]] = acc; acc += support[a]; }
+    c->cdoff[C] = acc;
+    return C;
+}
+
+static uint64_t g_range_records = 0;  /* orc_set_range_records: join-range size of stages 3-4 (0: one pass) */
+
+void orc_set_range_records(uint64_t r) { g_range_records = r; }
 
 static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n, uint32_t V, uint32_t ms,
                 const char *projection, orc_csr *c, orc_stats *st) {
+    const uint64_t range_records = g_range_records;
     memset(st, 0, sizeof(*st));
     memset(c, 0, sizeof(*c));
     if (V >= (1u << 31)) return -1;
@@ -196,54 +221,71 @@ static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_
     free(cnt);
 
     /* 2. binary condition counts (CreatedReducedDoubleConditionCounts.scala:45-86): the keys of the triples with two
-     *    frequent values, sorted, counted per run (memory ~16 B per key; chunked passes keep any thread count's
-     *    result identical) */
+     *    frequent values, one binary type (key bits 62-63) at a time, sorted and counted per run; the types ascend in
+     *    the key's top bits, so the frequent keys of the three passes concatenate sorted (memory ~16 B per key of one
+     *    type; chunked passes keep any thread count's result identical) */
     enum { NCH = 4096 };
     uint64_t *chunk = (uint64_t *)calloc(NCH + 1, sizeof(uint64_t));
+    uint64_t *bkeys = NULL, nb = 0, ndist = 0;
+    for (int bt = 0; bt < 3; ++bt) {
+        /* bt 0: s[p,o] (p, o frequent); 1: p[s,o] (s, o); 2: o[s,p] (s, p) */
+#define BKEY_OF(i, OK, KEY)                                                                       \
+        int fs = freq[s[i]] & 1, fp = (freq[p[i]] >> 1) & 1, fo = (freq[o[i]] >> 2) & 1;           \
+        const int OK = bt == 0 ? (fp && fo) : bt == 1 ? (fs && fo) : (fs && fp);                     \
+        const uint64_t KEY = bt == 0 ? (((uint64_t)p[i] << 31) | o[i])                             \
+                           : bt == 1 ? ((1ull << 62) | ((uint64_t)s[i] << 31) | o[i])                \
+                                     : ((2ull << 62) | ((uint64_t)s[i] << 31) | p[i]);
+        chunk[0] = 0;
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int ch = 0; ch < NCH; ++ch) {
-        uint64_t k = 0;
-        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) {
-            int fs = freq[s[i]] & 1, fp = (freq[p[i]] >> 1) & 1, fo = (freq[o[i]] >> 2) & 1;
-            k += (fs && fp) + (fs && fo) + (fp && fo);
+        for (int ch = 0; ch < NCH; ++ch) {
+            uint64_t k = 0;
+            for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) {
+                BKEY_OF(i, ok, key)
+                (void)key;
+                k += ok;
+            }
+            chunk[ch + 1] = k;
         }
-        chunk[ch + 1] = k;
-    }
-    for (int ch = 0; ch < NCH; ++ch) chunk[ch + 1] += chunk[ch];
-    const uint64_t nkeys_all = chunk[NCH];
-    uint64_t *keys = (uint64_t *)xmalloc(nkeys_all * sizeof(uint64_t));
+        for (int ch = 0; ch < NCH; ++ch) chunk[ch + 1] += chunk[ch];
+        const uint64_t nk = chunk[NCH];
+        uint64_t *keys = (uint64_t *)xmalloc(nk * sizeof(uint64_t));
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int ch = 0; ch < NCH; ++ch) {
-        uint64_t k = chunk[ch];
-        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) {
-            int fs = freq[s[i]] & 1, fp = (freq[p[i]] >> 1) & 1, fo = (freq[o[i]] >> 2) & 1;
-            if (fs && fp) keys[k++] = (2ull << 62) | ((uint64_t)s[i] << 31) | p[i];
-            if (fs && fo) keys[k++] = (1ull << 62) | ((uint64_t)s[i] << 31) | o[i];
-            if (fp && fo) keys[k++] = (0ull << 62) | ((uint64_t)p[i] << 31) | o[i];
+        for (int ch = 0; ch < NCH; ++ch) {
+            uint64_t k = chunk[ch];
+            for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) {
+                BKEY_OF(i, ok, key)
+                if (ok) keys[k++] = key;
+            }
         }
-    }
-    radix_sort_u64(keys, nkeys_all);
-    uint64_t nb = 0, ndist = 0;
-    for (uint64_t i = 0; i < nkeys_all;) {
-        uint64_t j = i + 1;
-        while (j < nkeys_all && keys[j] == keys[i]) ++j;
-        ndist++;
-        if (j - i >= ms) keys[nb++] = keys[i];  /* ascending: the frequent keys come out sorted */
-        i = j;
+#undef BKEY_OF
+        radix_sort_u64(keys, nk);
+        uint64_t nf = 0;
+        for (uint64_t i = 0; i < nk;) {
+            uint64_t j = i + 1;
+            while (j < nk && keys[j] == keys[i]) ++j;
+            ndist++;
+            if (j - i >= ms) keys[nf++] = keys[i];  /* ascending: the frequent keys come out sorted */
+            i = j;
+        }
+        bkeys = (uint64_t *)realloc(bkeys, (nb + nf + 1) * sizeof(uint64_t));
+        memcpy(bkeys + nb, keys, nf * sizeof(uint64_t));
+        nb += nf;
+        free(keys);
     }
     st->n_binary_keys = ndist;
-    uint64_t *bkeys = (uint64_t *)xmalloc(nb * sizeof(uint64_t));
-    memcpy(bkeys, keys, nb * sizeof(uint64_t));
-    free(keys);
     st->n_freq_binary = nb;
     u64map bidx;
     map_init(&bidx, nb + 16);
     for (uint64_t b = 0; b < nb; ++b) *map_slot(&bidx, bkeys[b], 1) = (uint32_t)b;
 
     /* 3. join partners (CreateJoinPartners.scala:86-147), binary captures split into their unary
-     *    components as every consumer does (CreateDependencyCandidates.scala:157-186); counted per chunk first so
-     *    the record array has its exact size */
+     *    components as every consumer does (CreateDependencyCandidates.scala:157-186), as records
+     *    join << capbits | capture.  Inputs whose records exceed range_records (0: no limit) are processed in ranges
+     *    of join values (the reference's sort-based groupBy("joinValue") spills instead, RDFind.scala:339-345): a
+     *    join value's records all fall in one range, so each range's groups are whole. */
     const uint64_t capbits = 64 - __builtin_clzll((uint64_t)6 * V + nb + 1);
+    const uint64_t ncap = 6ull * V + nb;
+    const uint64_t capmask = (1ull << capbits) - 1;
 #define EMIT_ALL(EMIT)                                                                            \
     {                                                                                             \
         uint32_t ts = s[i], tp = p[i], to = o[i];                                                 \
@@ -268,73 +310,125 @@ static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_
                 EMIT(ts, 6ull * V + *b);                 /* s[p,o] */                             \
         }                                                                                         \
     }
-#define COUNT(join, cap) (void)(join), (void)(cap), k++
-#define STORE(join, cap) rec[k++] = ((uint64_t)(join) << capbits) | (uint64_t)(cap)
-    chunk[0] = 0;
-#pragma omp parallel for schedule(dynamic, 1)
-    for (int ch = 0; ch < NCH; ++ch) {
-        uint64_t k = 0;
-        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(COUNT)
-        chunk[ch + 1] = k;
+#define IN_RANGE(join) ((uint64_t)(join) >= jlo && (uint64_t)(join) < jhi)
+#define COUNT(join, cap) if (IN_RANGE(join)) { (void)(cap); k++; }
+#define STORE(join, cap) if (IN_RANGE(join)) rec[k++] = ((uint64_t)(join) << capbits) | (uint64_t)(cap)
+#define HIST(join, cap) { (void)(cap); h[(uint64_t)(join) >> jshift]++; }
+    /* join ranges: records per join bucket (2^16 buckets), consecutive buckets up to range_records records each */
+    enum { NJB = 1 << 16 };
+    const int joinbits = V > 1 ? 64 - __builtin_clzll((uint64_t)V - 1) : 1;
+    const int jshift = joinbits > 16 ? joinbits - 16 : 0;
+    uint64_t *rlo = (uint64_t *)xmalloc((NJB + 2) * sizeof(uint64_t)), nrange = 0;
+    if (range_records) {
+        const int nt = omp_get_max_threads();
+        uint64_t *hist = (uint64_t *)calloc((size_t)nt * NJB, sizeof(uint64_t));
+#pragma omp parallel
+        {
+            uint64_t *h = hist + (size_t)omp_get_thread_num() * NJB;
+#pragma omp for schedule(dynamic, 1)
+            for (int ch = 0; ch < NCH; ++ch)
+                for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(HIST)
+        }
+        uint64_t acc = 0;
+        rlo[nrange++] = 0;
+        for (uint64_t bk = 0; bk < NJB; ++bk) {
+            uint64_t hb = 0;
+            for (int t = 0; t < nt; ++t) hb += hist[(size_t)t * NJB + bk];
+            if (acc && acc + hb > range_records) { rlo[nrange++] = bk << jshift; acc = 0; }
+            acc += hb;
+        }
+        free(hist);
+    } else {
+        rlo[nrange++] = 0;
     }
-    for (int ch = 0; ch < NCH; ++ch) chunk[ch + 1] += chunk[ch];
-    const uint64_t nr = chunk[NCH];
-    uint64_t *rec = (uint64_t *)xmalloc(nr * sizeof(uint64_t));
-#pragma omp parallel for schedule(dynamic, 1)
-    for (int ch = 0; ch < NCH; ++ch) {
-        uint64_t k = chunk[ch];
-        for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(STORE)
+    rlo[nrange] = ~0ull;
+    st->n_join_ranges = nrange;
+
+    /* records of join values [jlo, jhi), sorted and made distinct (UnionJoinCandidates / UnionCombinedJoinCandidates) */
+    uint64_t *rec = NULL, nu = 0;
+#define RANGE_RECORDS(r)                                                                          \
+    {                                                                                             \
+        const uint64_t jlo = rlo[r], jhi = rlo[(r) + 1];                                          \
+        chunk[0] = 0;                                                                             \
+        _Pragma("omp parallel for schedule(dynamic, 1)")                                          \
+        for (int ch = 0; ch < NCH; ++ch) {                                                        \
+            uint64_t k = 0;                                                                       \
+            for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(COUNT)          \
+            chunk[ch + 1] = k;                                                                    \
+        }                                                                                         \
+        for (int ch = 0; ch < NCH; ++ch) chunk[ch + 1] += chunk[ch];                             \
+        const uint64_t nr = chunk[NCH];                                                           \
+        free(rec);                                                                                \
+        rec = (uint64_t *)xmalloc(nr * sizeof(uint64_t));                                         \
+        _Pragma("omp parallel for schedule(dynamic, 1)")                                          \
+        for (int ch = 0; ch < NCH; ++ch) {                                                        \
+            uint64_t k = chunk[ch];                                                               \
+            for (uint64_t i = n * ch / NCH; i < n * (ch + 1) / NCH; ++i) EMIT_ALL(STORE)          \
+        }                                                                                         \
+        radix_sort_u64(rec, nr);                                                                  \
+        nu = 0;                                                                                   \
+        for (uint64_t i = 0; i < nr; ++i)                                                         \
+            if (nu == 0 || rec[nu - 1] != rec[i]) rec[nu++] = rec[i];                             \
+        rec_count = nr;                                                                           \
     }
+    /* 4a. supports = distinct join values per capture (BulkMergeDependencies.scala:78), summed over the ranges */
+    uint32_t *support = (uint32_t *)calloc(ncap + 1, sizeof(uint32_t));
+    for (uint64_t r = 0; r < nrange; ++r) {
+        uint64_t rec_count = 0;
+        RANGE_RECORDS(r)
+        st->n_records += rec_count;
+        st->n_unique += nu;
+        for (uint64_t i = 0; i < nu; ++i) support[rec[i] & capmask]++;
+        if (nrange > 1) { free(rec); rec = NULL; }
+    }
+    const uint64_t C = compact_captures(c, support, ncap, ms);
+    free(support);
+    st->n_freq_captures = C;
+    /* 4b. groups (join values with a frequent member; a ref is in every group of its dependent, so its support is at
+     *     least the dependent's: infrequent captures are no refs), members ascending; dependent -> groups, ascending */
+    const uint64_t Jf = c->cdoff[C];
+    const uint64_t gmax = Jf < V ? Jf : V;
+    uint64_t *goff = (uint64_t *)xmalloc((gmax + 1) * sizeof(uint64_t));
+    uint32_t *gcap = (uint32_t *)xmalloc((Jf ? Jf : 1) * sizeof(uint32_t));
+    uint32_t *dgrp = (uint32_t *)xmalloc((Jf ? Jf : 1) * sizeof(uint32_t));
+    uint64_t *cur = (uint64_t *)xmalloc((C + 1) * sizeof(uint64_t));
+    memcpy(cur, c->cdoff, (C + 1) * sizeof(uint64_t));
+    uint64_t ng = 0, gpos = 0;
+    for (uint64_t r = 0; r < nrange; ++r) {
+        if (nrange > 1) {
+            uint64_t rec_count = 0;
+            RANGE_RECORDS(r)
+            (void)rec_count;
+        }
+        for (uint64_t i = 0; i < nu;) {
+            uint64_t j = i;
+            const uint64_t gstart = gpos;
+            for (; j < nu && (rec[j] >> capbits) == (rec[i] >> capbits); ++j) {
+                const uint32_t cap = (uint32_t)(rec[j] & capmask), f = c->fidx[cap];
+                if (f == ORC_NONE) continue;
+                gcap[gpos++] = cap;
+                dgrp[cur[f]++] = (uint32_t)ng;
+            }
+            if (gpos > gstart) goff[ng++] = gstart;
+            i = j;
+        }
+    }
+    goff[ng] = gpos;
+    free(rec);
+    free(cur);
+    free(rlo);
+#undef RANGE_RECORDS
+#undef IN_RANGE
+#undef HIST
 #undef COUNT
 #undef STORE
 #undef EMIT_ALL
     free(chunk);
     map_free(&bidx);
     free(freq);
-    st->n_records = nr;
-
-    /* 4. capture groups: sort + unique (UnionJoinCandidates / UnionCombinedJoinCandidates) */
-    radix_sort_u64(rec, nr);
-    uint64_t nu = 0;
-    for (uint64_t i = 0; i < nr; ++i)
-        if (nu == 0 || rec[nu - 1] != rec[i]) rec[nu++] = rec[i];
-    st->n_unique = nu;
-    const uint64_t capmask = (1ull << capbits) - 1;
-    const uint64_t ncap = 6ull * V + nb;
-    uint32_t *support = (uint32_t *)calloc(ncap + 1, sizeof(uint32_t));
-    uint64_t ng = 0;
-    for (uint64_t i = 0; i < nu; ++i) {
-        support[rec[i] & capmask]++;
-        if (i == 0 || (rec[i] >> capbits) != (rec[i - 1] >> capbits)) ng++;
-    }
     st->n_groups = ng;
-    uint64_t *goff = (uint64_t *)xmalloc((ng + 1) * sizeof(uint64_t));
-    uint32_t *gcap = (uint32_t *)xmalloc(nu * sizeof(uint32_t));
-    ng = 0;
-    for (uint64_t i = 0; i < nu; ++i) {
-        if (i == 0 || (rec[i] >> capbits) != (rec[i - 1] >> capbits)) goff[ng++] = i;
-        gcap[i] = (uint32_t)(rec[i] & capmask);
-    }
-    goff[ng] = nu;
-    free(rec);
-
-    /* transposed: capture -> groups (only captures with support >= ms can be dependents) */
-    uint64_t *doff = (uint64_t *)xmalloc((ncap + 1) * sizeof(uint64_t));
-    uint64_t acc = 0;
-    for (uint64_t cc = 0; cc < ncap; ++cc) {
-        doff[cc] = acc;
-        if (support[cc] >= ms) { acc += support[cc]; st->n_freq_captures++; }
-    }
-    doff[ncap] = acc;
-    uint32_t *dgrp = (uint32_t *)xmalloc(acc * sizeof(uint32_t));
-    uint64_t *cur = (uint64_t *)xmalloc((ncap + 1) * sizeof(uint64_t));
-    memcpy(cur, doff, (ncap + 1) * sizeof(uint64_t));
-    for (uint64_t g = 0; g < ng; ++g)
-        for (uint64_t i = goff[g]; i < goff[g + 1]; ++i)
-            if (support[gcap[i]] >= ms) dgrp[cur[gcap[i]]++] = (uint32_t)g;
-    free(cur);
-    c->nb = nb; c->bkeys = bkeys; c->ncap = ncap; c->ng = ng; c->support = support;
-    c->goff = goff; c->gcap = gcap; c->doff = doff; c->dgrp = dgrp;
+    c->nb = nb; c->bkeys = bkeys; c->ncap = ncap; c->ng = ng;
+    c->goff = goff; c->gcap = gcap; c->dgrp = dgrp;
     return 0;
 }
 
@@ -379,7 +473,8 @@ static uint64_t raw_refs(const orc_csr *c, uint64_t a, int strategy, refbuf *b) 
         dv2 = (uint32_t)(key & 0x7fffffff);
         comps_of(c, a, &triv1, &triv2);
     }
-    const uint64_t j0 = c->doff[a], j1 = c->doff[a + 1];
+    const uint32_t fa = c->fidx[a];
+    const uint64_t j0 = c->cdoff[fa], j1 = c->cdoff[fa + 1];
     if (j0 == j1) return 0;
     uint64_t jp = j0;  /* pivot: smallest group */
     for (uint64_t j = j0 + 1; j < j1; ++j) {
@@ -447,7 +542,6 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
     orc_csr c;
     if (prep(s, p, o, n, V, ms, projection, &c, st)) return -1;
     const uint64_t ncap = c.ncap;
-    const uint32_t *support = c.support;
     const uint64_t *bkeys = c.bkeys;
 
     /* 5. per dependent: raw ref set.  Dependents are split into chunks processed by OpenMP threads; each
@@ -464,13 +558,13 @@ int orc_run(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t n,
             orc_cind *cind = (orc_cind *)xmalloc(ccap * sizeof(orc_cind));
             const uint64_t a0 = ncap * ch / nchunk, a1 = ncap * (ch + 1) / nchunk;
             for (uint64_t a = a0; a < a1; ++a) {
-                if (support[a] < ms) continue;
+                if (c.fidx[a] == ORC_NONE) continue;
                 const uint64_t nref = raw_refs(&c, a, strategy, &rb);
                 for (uint64_t i = 0; i < nref; ++i) {
                     if (nc == ccap) { ccap *= 2; cind = (orc_cind *)realloc(cind, ccap * sizeof(orc_cind)); }
                     cind[nc].dep = (uint32_t)a;
                     cind[nc].ref = rb.refs[i];
-                    cind[nc].support = support[a];
+                    cind[nc].support = c.csup[c.fidx[a]];
                     nc++;
                 }
             }
@@ -599,11 +693,11 @@ int orc_stream(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_t
         for (uint64_t ch = 0; ch < nchunk; ++ch) {
             const uint64_t a0 = ncap * ch / nchunk, a1 = ncap * (ch + 1) / nchunk;
             for (uint64_t a = a0; a < a1; ++a) {
-                if (c.support[a] < ms) continue;
+                if (c.fidx[a] == ORC_NONE) continue;
                 const uint64_t nref = raw_refs(&c, a, strategy, &rb);
                 if (!nref) continue;
                 t_raw += nref;
-                const uint32_t sup = c.support[a];
+                const uint32_t sup = c.csup[c.fidx[a]];
                 /* first binary ref (refs are sorted: unary ids < 6V first) */
                 uint64_t nb0 = 0;
                 while (nb0 < nref && rb.refs[nb0] < U) nb0++;

@@ -27,7 +27,7 @@ class OrcStats(ctypes.Structure):
                 ("n_freq_binary", ctypes.c_uint64), ("n_records", ctypes.c_uint64),
                 ("n_unique", ctypes.c_uint64), ("n_groups", ctypes.c_uint64),
                 ("n_freq_captures", ctypes.c_uint64), ("n_raw_cinds", ctypes.c_uint64),
-                ("n_cinds", ctypes.c_uint64)]
+                ("n_cinds", ctypes.c_uint64), ("n_join_ranges", ctypes.c_uint64)]
 
 
 class OrcStream(ctypes.Structure):
@@ -69,6 +69,7 @@ def _load():
         lib.orc_stream.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                             ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                                             ctypes.POINTER(OrcStream), ctypes.POINTER(OrcStats)]
+        lib.orc_set_range_records.argtypes = [ctypes.c_uint64]
         lib.orc_checksum.restype = ctypes.c_uint64
         lib.orc_checksum.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         _lib = lib
@@ -114,6 +115,12 @@ def run(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo
     lib.orc_free(bk)
     stats = {f: (list(getattr(st, f)) if f == "n_freq_unary" else getattr(st, f)) for f, _ in OrcStats._fields_}
     return arr, keys, stats
+
+
+def set_range_records(n):
+    """Stages 3-4 (capture records and groups) in join-value ranges of at most n records each (0: one pass): the
+    memory of inputs whose records do not fit at once (c4 at 10^9 triples emits ~5.8·10^9)."""
+    _load().orc_set_range_records(int(n))
 
 
 def stream(s, p, o, num_terms, min_support, strategy=1, clean=True, projection="spo"):

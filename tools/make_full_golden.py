@@ -30,6 +30,7 @@ CASES = {
     "c4": ("c4", 0.05, [(1, True)]),
     "c4_0.1": ("c4", 0.1, [(1, True)]),      # counter-based generator from here on (synth._c4_rows)
     "c4_0.4": ("c4", 0.4, [(1, True)]),
+    "c4_1.0": ("c4", 1.0, [(1, True)]),      # the BASELINE size: the oracle's stages 3-4 in join-value ranges
     "c5": ("c5", 0.3, [(1, True), (0, False)]),
     "c5_1.0": ("c5", 1.0, [(1, True)]),      # the BASELINE size (paged discovery on the GPU)
 }
@@ -46,10 +47,15 @@ def fingerprint(d):
         return int(x.sum(dtype=np.uint64))
 
 
+# oracle stages 3-4 in join-value ranges of at most this many records (memory: ~16 B per record of a range)
+RANGE_RECORDS = {"c4_1.0": 200_000_000}
+
+
 def main(names):
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
     for name in names:
         cfg, scale, modes = CASES[name]
+        C.set_range_records(RANGE_RECORDS.get(name, 0))
         t = time.time()
         d = synth.config(cfg, scale)
         gen_s = time.time() - t
