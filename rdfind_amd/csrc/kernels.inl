@@ -1448,7 +1448,7 @@ __device__ inline void light_batch(const u32* gm, u64 gsz, const u32* drow, u32 
 // candidate in every lane's group: per (candidate, group) a ~log2(n)-level chain of divergent loads.  The alive
 // candidates of a chunk are consecutive pivot members, so they span a narrow slice of the capture-id space: each lane
 // bounds its group's members to [min, max] of the alive candidates (two searches in flight), and when those members are
-// few per (candidate, group) pair, the wave reads them all instead -- coalesced, SWEEP_U loads in flight per lane, the
+// few against the searches they replace, the wave reads them all instead -- coalesced, SWEEP_U loads in flight per lane, the
 // window's ranges concatenated so every lane stays busy -- and marks the candidates each group holds.  Returns false
 // (nothing done) when the slices are too large for that to pay; the caller then batches as before.
 // LDS per wave (the light pass's 2 KB slice): member starts (u64) and range prefix (u32) per lane, the lanes' candidates,
@@ -1486,8 +1486,15 @@ __device__ inline bool light_sweep(const CindView& v, const u32* gm, u64 gsz, u3
     const u32 r = (u32)(hi - lo);
     const u32 incl = wave_inclusive_scan(r);
     const u32 R = __shfl(incl, RDF_WAVE - 1, RDF_WAVE);
+    // cost model: a batch round searches 8 alive candidates in every lane's group, ~L = log2(mean group size) levels of
+    // divergent loads; the sweep reads R members, SWEEP_U x 64 per round plus LDS lookups.  Sweep when
+    // R <= sweep_f x alive x L (measured: sweep_f 16 beat 64 and 256 on c4, whose wide slices made 64 ~2x slower)
+    u32 lv = g != NONE32 && gsz > 1 ? 64 - __clzll(gsz - 1) : 0;
     const u32 nl = (u32)__popcll(__ballot(g != NONE32));
-    if ((u64)R > (u64)v.sweep_f * (u64)__popcll(alive) * nl) return false;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) lv += __shfl_xor(lv, off, RDF_WAVE);
+    const u64 L = nl ? (lv + nl - 1) / nl : 1;
+    if ((u64)R > (u64)v.sweep_f * (u64)__popcll(alive) * L) return false;
     u64* s_start = (u64*)buf;                 // [64] first member of each lane's slice (global index into gcap)
     u32* s_pre = buf + 2 * RDF_WAVE;          // [65] exclusive prefix of the slice lengths
     u32* s_cand = s_pre + RDF_WAVE + 1;       // [64] the lanes' candidates (ascending)
