@@ -1687,8 +1687,10 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
             const u64 gsz = gszv[it];
             if (v.sweep_f && __popcll(alive) >= LIGHT_SWEEP_MIN && !__any(gdr[it] != nullptr && g != NONE32) &&
-                light_sweep(v, gm, gsz, g, cand, alive, s_light[threadIdx.x / RDF_WAVE]))
+                light_sweep(v, gm, gsz, g, cand, alive, s_light[threadIdx.x / RDF_WAVE])) {
+                LSTAT_SER(1u << 16);  // stats records: swept windows in the serial counter's high half
                 continue;
+            }
             if (STAGE && __popcll(alive) >= LIGHT_STAGE_MIN && __all(g == NONE32 || gsz <= LIGHT_SMALL)) {
                 // every light group of the window is small: each lane copies its group into its own LDS row with
                 // <= 9 aligned 16-B loads, then the alive candidates are searched in LDS (instead of A x log2 n

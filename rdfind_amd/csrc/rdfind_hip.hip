@@ -1942,11 +1942,14 @@ static rdf_status d_multi_items(rdf_ctx* c) {
     hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gp, dscal(c, 5));
     return RDF_OK;
 }
+// With the window range sweeps (light_sweep) one pass is faster on every measured shape (light ms, one / two passes:
+// c4 at 0.4 181.8 / 197.9, c4 at 0.05 11.2 / 12.5, c3 at 0.5 10.6 / 10.9, c5 at 0.1 17.9 / 20.4, c2 2.60 / 2.92), so the
+// two passes only run on request (RDFIND_LIGHT2=1, which the parity tests use) or with the sweeps off.
 static bool use_two_pass(const rdf_ctx* c, u64 WI) {
     static const char* force = getenv("RDFIND_LIGHT2");
     if (!WI) return false;
     if (force) return atoi(force) != 0;
-    return c->n_multi_items >= LIGHT2_MIN_ITEMS;
+    return LIGHT_SWEEP_F == 0 && c->n_multi_items >= LIGHT2_MIN_ITEMS;
 }
 
 // Two light passes (single GPU).  A k_light work item verifies 64 pivot candidates of one dependent against a segment of

@@ -27,6 +27,8 @@ names = ["dep", "ng", "segg", "nseg", "piv", "alive0", "alive1", "win", "ser", "
          "gsum", "gmax"]
 col = {n: r[:, i] for i, n in enumerate(names)}
 cyc = col["cyc_lo"] + (col["cyc_hi"] << 32)
+col["sweep"] = col["ser"] >> 16  # windows verified by a range sweep (kernels.inl light_sweep)
+col["ser"] = col["ser"] & 0xFFFF
 tot = cyc.sum()
 print(f"items {len(r)}  total cycles {tot:.3e}  mean {cyc.mean():.0f}  max {cyc.max()}")
 
@@ -45,18 +47,20 @@ for lo, hi in [(0, 1), (1, 2), (2, 5), (5, 17), (17, 65), (65, 1 << 30)]:
 for lo, hi in [(0, 1), (1, 4), (4, 16), (16, 64), (64, 256), (256, 1 << 30)]:
     share((col["bat"] >= lo) & (col["bat"] < hi), f"batch rounds in [{lo},{hi})")
 s = lambda k: col[k].sum()
-print(f"sums: windows {s('win')}  serial groups {s('ser')}  batches {s('bat')}  depth {s('depth')}  light groups {s('lg')}"
+for lo, hi in [(0, 1), (1, 4), (4, 16), (16, 1 << 30)]:
+    share((col["sweep"] >= lo) & (col["sweep"] < hi), f"swept windows in [{lo},{hi})")
+print(f"sums: windows {s('win')}  swept {s('sweep')}  serial groups {s('ser')}  batches {s('bat')}  depth {s('depth')}  light groups {s('lg')}"
       f"  light group members {s('gsum')}  alive0 {s('alive0')}  alive1 {s('alive1')}")
 print(f"mean depth per batch {s('depth') / max(s('bat'), 1):.2f}; "
       f"members per light group {s('gsum') / max(s('lg'), 1):.1f}; batches per window {s('bat') / max(s('win'), 1):.2f}")
 # a linear model of the cycles: which counter explains them
-X = np.stack([np.ones(len(r)), col["win"], col["ser"], col["bat"], col["depth"]], 1).astype(np.float64)
+X = np.stack([np.ones(len(r)), col["win"], col["ser"], col["bat"], col["depth"], col["sweep"]], 1).astype(np.float64)
 coef, *_ = np.linalg.lstsq(X, cyc.astype(np.float64), rcond=None)
-print("cycles ~ " + " + ".join(f"{c:.0f}*{n}" for c, n in zip(coef, ["1", "win", "ser", "bat", "depth"])))
+print("cycles ~ " + " + ".join(f"{c:.0f}*{n}" for c, n in zip(coef, ["1", "win", "ser", "bat", "depth", "sweep"])))
 top = np.argsort(-cyc)[:12]
 print("slowest items:")
 for i in top:
-    print("  " + " ".join(f"{n}={col[n][i]}" for n in names if not n.startswith("cyc")) + f" cyc={cyc[i]}")
+    print("  " + " ".join(f"{n}={col[n][i]}" for n in names if not n.startswith("cyc")) + f" sweep={col['sweep'][i]} cyc={cyc[i]}")
 # per-dependent totals
 deps, inv = np.unique(col["dep"], return_inverse=True)
 dc = np.bincount(inv, weights=cyc.astype(np.float64))
