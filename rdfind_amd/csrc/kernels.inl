@@ -1407,7 +1407,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_packed(u64 nvblk, CindView 
 // [7] 64-group windows visited [8] groups taken by the serial path [9] batch rounds [10] sum of batch search depths
 // [11] light groups in visited windows [12..13] clock64 cycles [14] sum of visited light group sizes [15] largest
 __device__ u32* g_item_rec;
-#define LSTAT_T0 const unsigned long long lstat_t0 = clock64(); u32 ls_win = 0, ls_ser = 0, ls_bat = 0, ls_dep = 0, ls_lg = 0, ls_gs = 0, ls_gmax = 0
+#define LSTAT_T0 const unsigned long long lstat_t0 = clock64(); u32 ls_win = 0, ls_ser = 0, ls_bat = 0, ls_dep = 0, ls_lg = 0, ls_gs = 0, ls_gmax = 0; \
+    unsigned long long ls_ph[6] = {0, 0, 0, 0, 0, 0}, ls_tic = 0
+// phase timers (cycles): [0] second pivot, [1] window metadata loads, [2] dense groups, [3] serial groups, [4] sweeps,
+// [5] batches
+#define LSTAT_TIC() (ls_tic = clock64())
+#define LSTAT_TOC(k) (ls_ph[k] += clock64() - ls_tic)
 #define LSTAT_WIN(lmask, gsz) do { ++ls_win; ls_lg += __popcll(lmask); ls_gs += wave_sum((u32)(gsz)); \
     u32 m_ = (u32)(gsz); for (int o_ = 32; o_ >= 1; o_ >>= 1) { u32 t_ = __shfl_xor(m_, o_, RDF_WAVE); m_ = t_ > m_ ? t_ : m_; } \
     ls_gmax = m_ > ls_gmax ? m_ : ls_gmax; } while (0)
@@ -1415,6 +1420,8 @@ __device__ u32* g_item_rec;
 #define LSTAT_BAT(depth) do { ++ls_bat; ls_dep += (depth); } while (0)
 #else
 #define LSTAT_T0 do { } while (0)
+#define LSTAT_TIC() do { } while (0)
+#define LSTAT_TOC(k) do { } while (0)
 #define LSTAT_WIN(lmask, gsz) do { } while (0)
 #define LSTAT_SER(k) do { } while (0)
 #define LSTAT_BAT(depth) do { } while (0)
@@ -1592,11 +1599,13 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // pass A (prefilter): a chunk of a dependent of several chunks with few candidates left after the filters and the
     // second pivot is not verified here; its survivors go out tagged (item seg 0) and pass B verifies them compacted
     const bool multi = v.prefilter && itemoff[d + 1] - itemoff[d] > nseg;
+    LSTAT_TIC();
     if (p2 != NONE32 && alive && !v.p2done) {
         const u64 gb2 = v.goff[p2];
         alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
                             dense_row(v, p2));
     }
+    LSTAT_TOC(0);
     if (multi && __popcll(alive) <= LIGHT_PRE_MAX) {  // every segment item of the chunk reaches the same decision
         if (seg == 0) {
             const u64 oct0 = choff[d] + chunk * 8 - ob;
@@ -1610,6 +1619,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // here groups outnumber candidates.  The segment's group metadata is loaded up front, LIGHT_IT
     // independent gathers per level, so the serial chain is three round trips per segment, not per 64 groups.
     for (u64 s0 = b; s0 < e && alive; s0 += (u64)LIGHT_IT * RDF_WAVE) {
+        LSTAT_TIC();
         u32 gg[LIGHT_IT];
         u64 gbv[LIGHT_IT];
         u32 gszv[LIGHT_IT];
@@ -1633,6 +1643,10 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                 gdr[it] = dense_row(v, gg[it]);
             }
         }
+#ifdef RDF_LIGHT_STATS
+        { u32 x = gszv[0] + (u32)gbv[0]; asm volatile("" : : "v"(x)); }  // stats: the metadata loads have arrived
+#endif
+        LSTAT_TOC(1);
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it) {
             if (s0 + (u64)it * RDF_WAVE >= e) break;
@@ -1643,6 +1657,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             u64 lm = __ballot(g != NONE32);  // light groups of this window
             LSTAT_WIN(lm, gszv[it]);
             const u64 dm = __ballot(gdr[it] != nullptr);  // ... of which dense (member bitmaps)
+            LSTAT_TIC();
             if (dm && __popcll(alive) >= LIGHT_DENSE_SER) {
                 // many candidates alive: the dense groups one at a time with the lanes over the candidates.  The
                 // candidates are ascending pivot members, so a group's 64 tests hit a few lines of its bitmap row
@@ -1664,6 +1679,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                 }
                 if (gdr[it]) g = NONE32;  // what is left: the sparse light groups of the window
                 lm = __ballot(g != NONE32);
+                LSTAT_TOC(2);
                 if (!lm || !alive) continue;
             }
             if (__popcll(lm) <= LIGHT_SERIAL) {
@@ -1671,6 +1687,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                 // mask test): take them one at a time with the lanes over the candidates.  A group of at most
                 // LIGHT_LDS captures is staged into the wave's LDS slice by one coalesced load, so each
                 // candidate's search is one global round trip plus LDS probes.
+                LSTAT_TIC();
                 u32* buf = s_light[threadIdx.x / RDF_WAVE];
                 u64 tg = lm;
                 while (tg && alive) {
@@ -1682,15 +1699,20 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                     const u32* dr = (const u32*)__shfl((unsigned long long)gdr[it], l, RDF_WAVE);
                     alive = check_group(v, gb, gs, cand, alive, buf, dr);
                 }
+                LSTAT_TOC(3);
                 continue;
             }
             const u32* gm = g != NONE32 ? v.gcap + gbv[it] : nullptr;
             const u64 gsz = gszv[it];
+            LSTAT_TIC();
             if (v.sweep_f && __popcll(alive) >= LIGHT_SWEEP_MIN && !__any(gdr[it] != nullptr && g != NONE32) &&
                 light_sweep(v, gm, gsz, g, cand, alive, s_light[threadIdx.x / RDF_WAVE])) {
                 LSTAT_SER(1u << 16);  // stats records: swept windows in the serial counter's high half
+                LSTAT_TOC(4);
                 continue;
             }
+            LSTAT_TOC(4);
+            LSTAT_TIC();
             if (STAGE && __popcll(alive) >= LIGHT_STAGE_MIN && __all(g == NONE32 || gsz <= LIGHT_SMALL)) {
                 // every light group of the window is small: each lane copies its group into its own LDS row with
                 // <= 9 aligned 16-B loads, then the alive candidates are searched in LDS (instead of A x log2 n
@@ -1747,16 +1769,19 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
                 else if (na <= 4) light_batch<4>(gm, gsz, dr, g, cand, todo, alive);
                 else light_batch<LIGHT_BATCH>(gm, gsz, dr, g, cand, todo, alive);
             }
+            LSTAT_TOC(5);
         }
     }
 #ifdef RDF_LIGHT_STATS
     if (lane == 0 && g_item_rec) {
         const unsigned long long dt = clock64() - lstat_t0;
-        u32* r = g_item_rec + 16 * w;
+        u32* r = g_item_rec + 24 * w;
         const u32 rec[16] = {d, (u32)(e0 - b0), (u32)(e - b), (u32)nseg, (u32)(v.goff[piv + 1] - v.goff[piv]),
                              (u32)__popcll(alive0), (u32)__popcll(alive), ls_win, ls_ser, ls_bat, ls_dep, ls_lg,
                              (u32)dt, (u32)(dt >> 32), ls_gs, ls_gmax};
         for (int k = 0; k < 16; ++k) r[k] = rec[k];
+        for (int k = 0; k < 6; ++k) r[16 + k] = (u32)(ls_ph[k] >> 8);  // phase cycles / 256
+        r[22] = r[23] = 0;
     }
 #endif
     const u64 oct0 = choff[d] + chunk * 8 - ob;  // first octet slot of this chunk

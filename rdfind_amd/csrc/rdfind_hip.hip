@@ -1849,8 +1849,8 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
 #ifdef RDF_LIGHT_STATS
     u32* lrec = nullptr;
     if (WI && getenv("RDFIND_LIGHT_DUMP")) {
-        HIP_TRY(c, hipMalloc(&lrec, r.i1 * 64));
-        HIP_TRY(c, hipMemset(lrec, 0, r.i1 * 64));
+        HIP_TRY(c, hipMalloc(&lrec, r.i1 * 96));
+        HIP_TRY(c, hipMemset(lrec, 0, r.i1 * 96));
         HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_item_rec), &lrec, sizeof(lrec)));
     }
 #endif
@@ -1874,11 +1874,11 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
                            WM, c->choffl.as<u64>(), ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>());
     tend(c, RDF_T_LIGHT);
 #ifdef RDF_LIGHT_STATS
-    if (lrec) {  // per-item records -> $RDFIND_LIGHT_DUMP (raw u32 x 16 per item)
-        std::vector<u32> h(r.i1 * 16);
-        HIP_TRY(c, hipMemcpy(h.data(), lrec, r.i1 * 64, hipMemcpyDeviceToHost));
+    if (lrec) {  // per-item records -> $RDFIND_LIGHT_DUMP (raw u32 x 24 per item)
+        std::vector<u32> h(r.i1 * 24);
+        HIP_TRY(c, hipMemcpy(h.data(), lrec, r.i1 * 96, hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("RDFIND_LIGHT_DUMP"), "wb")) {
-            fwrite(h.data(), 64, r.i1, f);
+            fwrite(h.data(), 96, r.i1, f);
             fclose(f);
         }
         u32* z = nullptr;

@@ -167,7 +167,7 @@ def test_c4_full_size_one_gpu(ctx, monkeypatch):
         c.set_triples(d.s, d.p, d.o, d.num_terms)
         c.run(d.min_support)
         forced = c.groups["n_join_ranges"]
-        assert forced >= 8
+        assert forced >= 4
         results.append((c.cind_count(), c.checksum(), c.groups["n_records"], c.groups["n_groups"]))
     monkeypatch.delenv("RDFIND_GROUP_RANGE")
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)

@@ -22,10 +22,12 @@ with _lib.Context(0) as ctx:
     cs = ctx.run(d.min_support)
     print(cfg, scale, ctx.groups, cs, ctx.kernel_times(), flush=True)
 
-r = np.fromfile(dump, dtype=np.uint32).reshape(-1, 16).astype(np.int64)
+r = np.fromfile(dump, dtype=np.uint32).reshape(-1, 24).astype(np.int64)
 names = ["dep", "ng", "segg", "nseg", "piv", "alive0", "alive1", "win", "ser", "bat", "depth", "lg", "cyc_lo", "cyc_hi",
-         "gsum", "gmax"]
+         "gsum", "gmax", "t_p2", "t_meta", "t_dense", "t_serial", "t_sweep", "t_batch"]
 col = {n: r[:, i] for i, n in enumerate(names)}
+for n in names[16:]:
+    col[n] = col[n] * 256  # phase cycles are recorded / 256
 cyc = col["cyc_lo"] + (col["cyc_hi"] << 32)
 col["sweep"] = col["ser"] >> 16  # windows verified by a range sweep (kernels.inl light_sweep)
 col["ser"] = col["ser"] & 0xFFFF
@@ -57,6 +59,7 @@ print(f"mean depth per batch {s('depth') / max(s('bat'), 1):.2f}; "
 X = np.stack([np.ones(len(r)), col["win"], col["ser"], col["bat"], col["depth"], col["sweep"]], 1).astype(np.float64)
 coef, *_ = np.linalg.lstsq(X, cyc.astype(np.float64), rcond=None)
 print("cycles ~ " + " + ".join(f"{c:.0f}*{n}" for c, n in zip(coef, ["1", "win", "ser", "bat", "depth", "sweep"])))
+print("phase cycles: " + ", ".join(f"{n[2:]} {col[n].sum() / tot:5.1%}" for n in names[16:]) + "  (of the item cycles)")
 top = np.argsort(-cyc)[:12]
 print("slowest items:")
 for i in top:
