@@ -435,6 +435,19 @@ def main():
                           "the same call timed on the host, including the text's upload from pageable memory"}
         del text
 
+    # per-rank work and time (N > 1): the balance of the sharded ownership, max / mean over ranks per quantity
+    ranks = None
+    if dist is not None:
+        mine = {"triples": d.n, "records": gs["n_records"], "groups": gs["n_groups"],
+                "light_chunks": cs["n_light_chunks"], "explicit_raw": cs["n_explicit_raw"], "cinds": cs["n_cinds"],
+                "light_ms": round(kt.get("light", 0.0), 4), "kernel_ms": round(sum(kt.values()), 4),
+                **{k: v for k, v in (getattr(ctx, "x_stats", None) or {}).items() if k in ("bytes_sent", "bytes_received")}}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        ranks = {"per_rank": allr,
+                 "max_over_mean": {k: round(max(r[k] for r in allr) / max(sum(r[k] for r in allr) / world, 1e-12), 3)
+                                   for k in mine if all(isinstance(r.get(k), (int, float)) for r in allr)}}
+
     if rank == 0:
         per = "per GPU" if args.scaling == "weak" else "total"
         wl = {"c2": "LUBM-shaped"}.get(args.config, args.config)
@@ -457,7 +470,7 @@ def main():
                                 "triples_per_s": round(float(total_n) * steps / elapsed_dev, 1),
                                 "note": "the same steps with the result left in HBM"},
             "roofline": roof, "count_kernels": count_roof, "families": fams,
-            "cpu_baseline": cpu, "ingest": ingest,
+            "cpu_baseline": cpu, "ingest": ingest, **({"ranks": ranks} if ranks else {}),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],

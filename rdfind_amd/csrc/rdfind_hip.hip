@@ -5,6 +5,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <string>
+#include <chrono>
 #include <vector>
 #include <utility>
 #include <initializer_list>
@@ -217,6 +218,22 @@ static u64 next_pow2(u64 x) {
     while (p < x) p <<= 1;
     return p;
 }
+
+// RDFIND_SYNC_TRACE=1: every host wait on the stream prints "SYNC <line> <t_us> <wait_us>" to stderr (dev tool: where
+// the host round trips of a step are, tools/sync_trace.py)
+static hipError_t traced_sync(hipStream_t s, int line) {
+    static const bool on = getenv("RDFIND_SYNC_TRACE") != nullptr;
+    if (!on) return hipStreamSynchronize(s);
+    using clk = std::chrono::steady_clock;
+    static const clk::time_point t00 = clk::now();
+    const clk::time_point t0 = clk::now();
+    const hipError_t e = hipStreamSynchronize(s);
+    const clk::time_point t1 = clk::now();
+    fprintf(stderr, "SYNC %d %.1f %.1f\n", line, std::chrono::duration<double, std::micro>(t0 - t00).count(),
+            std::chrono::duration<double, std::micro>(t1 - t0).count());
+    return e;
+}
+#define hipStreamSynchronize(s) traced_sync((s), __LINE__)
 
 static rdf_status read_scalars(rdf_ctx* c, int count) {
     HIP_TRY(c, hipMemcpyAsync(c->hscal, c->scal.p, count * sizeof(u64), hipMemcpyDeviceToHost, c->stream));

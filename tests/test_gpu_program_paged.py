@@ -65,3 +65,26 @@ def test_program_result_beyond_hbm_switches_to_pages(tmp_path):
     prog, out = run_program(["--use-fis", "--clean-implied", "--support", "2", "--debug-level", "1", str(nt)])
     assert prog.stats["pages"] >= 2
     assert f"Detected {g['n_cinds']} CINDs." in out
+
+
+@pytest.mark.timeout(900)
+def test_program_pages_written_lines_vs_oracle(tmp_path):
+    """c5 (support 2, the pair-explosion shape) at 3·10^4 triples: 2.7·10^6 CINDs written through the driver in pages
+    of a 4 MiB budget are exactly the C oracle's rows formatted as Cind.toString lines.  (At the BASELINE sizes the
+    written text would be 0.5 TB (c5 at 0.3) or more; those runs are checked by count and checksum instead:
+    test_program_result_beyond_hbm_switches_to_pages and tests/test_gpu.py::test_paged_full_size_vs_oracle.)"""
+    from oracle import c_oracle
+    from tests.kats import lines_of
+
+    d = synth.config("c5", 0.003)
+    nt = tmp_path / "c5.nt"
+    write_text(d, nt)
+    out = tmp_path / "cinds.txt"
+    prog, _ = run_program(["--use-fis", "--clean-implied", "--support", str(d.min_support), "--page-bytes",
+                           str(4 << 20), "--output", f"file://{out}", str(nt)])
+    assert prog.stats["pages"] >= 4
+    got = out.read_text(encoding="utf-8").splitlines()
+    rows, _ = c_oracle.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+    want = lines_of(rows, d.terms.term)
+    assert len(got) == len(want) == 2698238
+    assert sorted(got) == want
