@@ -732,8 +732,33 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_size_hist(const u64* __rest
     if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restrict__ goff, u64 G, u64 threshold, u32 base,
+// heavy threshold on the device (single GPU: no host round trip between the histogram and the selection): the
+// smallest size bucket such that the groups in it and above number at most HMAX, its smallest size, at least min_size;
+// 0 = no heavy groups.  The same rule as the host's heavy_threshold (rdfind_hip.hip), which sharded runs use on the
+// all-gathered histogram.
+__global__ void k_heavy_threshold(const u32* __restrict__ hist, u64 min_size, u64* thr) {
+    u64 cum = 0;
+    int best = -1;
+    for (int b = 255; b >= 0; --b) {
+        cum += hist[b];
+        if (cum > (u64)HMAX) break;
+        if (hist[b]) best = b;
+    }
+    u64 t = 0;
+    if (best >= 0) {
+        t = 0;
+        for (u64 sz = 1; sz < 64 && !t; ++sz)
+            if (size_bucket(sz) == best) t = sz;
+        if (!t) t = (u64)(4 + best % 4) << (best / 4 - 2);
+        t = t > min_size ? t : min_size;
+    }
+    *thr = t;
+}
+
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restrict__ goff, u64 G, u64 threshold_h,
+                                                            const u64* __restrict__ threshold_d, u32 base,
                                                             u32* nheavy, u32* heavy_list, uint8_t* hbit) {
+    const u64 threshold = threshold_d ? *threshold_d : threshold_h;
     for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
         u64 sz = goff[g + 1] - goff[g];
         uint8_t b = LIGHT;
@@ -748,9 +773,13 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_select(const u64* __restric
     }
 }
 
+// one block row per heavy column; with nheavy (device count) the grid has HMAX - base rows and the rows beyond the
+// count exit
 __global__ __launch_bounds__(RDF_BLOCK) void k_heavy_mask(const u64* __restrict__ goff, const u32* __restrict__ gcap,
-                                                          const u32* __restrict__ heavy_list, u32 base, CapInfo* info) {
+                                                          const u32* __restrict__ heavy_list, u32 base, CapInfo* info,
+                                                          const u32* __restrict__ nheavy) {
     const u32 h = blockIdx.y;
+    if (nheavy && h >= *nheavy) return;
     const u32 g = heavy_list[h];
     const u64 b = goff[g], e = goff[g + 1];
     for (u64 i = b + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < e; i += (u64)gridDim.x * RDF_BLOCK)
@@ -2599,10 +2628,18 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_decode_rows(const u32* __restrict
 // (dep_owner), which keeps a ref iff every rank holding a light group of the dependent reported it.
 
 // MIN-allreduce keys of the local pivot: (size << 32 | rank), INT64_MAX where the rank has no group
+// (smallest local group size, tie-break, rank) of each dependent for the MIN all-reduce that elects the pivot holder.
+// Ties between ranks (common: many dependents have equal smallest groups on several ranks) go to a pseudo-random rank
+// per dependent, not to the lowest rank, so the holders' work (light candidates, verify traffic) spreads evenly.
+__device__ __host__ inline u64 holder_key(u64 size, u32 d, u32 rank) {
+    return (size << 32) | ((mix64(((u64)d << 8) | rank) >> 40) << 8) | rank;
+}
+__device__ __host__ inline u32 holder_rank(u64 key) { return (u32)(key & 0xffu); }
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __restrict__ best, u32 C, u32 rank, u64* out) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = best[d];
-        out[d] = b == ~0ull ? 0x7fffffffffffffffull : ((b >> 32) << 32) | rank;
+        out[d] = b == ~0ull ? 0x7fffffffffffffffull : holder_key(b >> 32, (u32)d, rank);
     }
 }
 
@@ -2904,7 +2941,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_final_shard(CindView v, con
             const u32 nlight = nlight_in[d];
             const u64 gl = glight[d];
             const bool heavy_only = (gl & ((1ull << 40) - 1)) == 0;
-            const bool holder = (u32)gbest[d] == rank && best != ~0ull;
+            const bool holder = holder_rank(gbest[d]) == rank && best != ~0ull;
             const u64 sz = best == ~0ull ? 0 : best >> 32;
             const u32 nch = (u32)((sz + RDF_WAVE - 1) / RDF_WAVE);
             pivot[d] = (u32)(best & 0xffffffffu);
@@ -3021,7 +3058,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_class_pivot_shard(CindView v, con
                                                                  const u64* __restrict__ gbest, u32 rank, u32* cpiv,
                                                                  u32* cnch) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.Cu; d += (u64)gridDim.x * RDF_BLOCK) {
-        if (!(v.info[d].meta & META_HEAVY_ONLY) || (u32)gbest[d] != rank) continue;
+        if (!(v.info[d].meta & META_HEAVY_ONLY) || holder_rank(gbest[d]) != rank) continue;
         const u64 h = class_slot(tkeys, tmask, v.info[d].hmask);
         if (h == ~0ull) continue;
         const u32 c = cid[h];

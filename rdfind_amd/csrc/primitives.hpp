@@ -21,6 +21,7 @@ struct DevBuf {
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) {
             p = nullptr;
+            (void)hipGetLastError();  // the failure is returned here; later hipGetLastError checks must not see it again
             return e;
         }
         cap = want;
@@ -37,7 +38,10 @@ struct DevBuf {
         void* q = nullptr;
         size_t want = bytes < 256 ? 256 : bytes;
         hipError_t e = hipMalloc(&q, want);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return e;
+        }
         if (p && cap) {
             e = hipMemcpyAsync(q, p, cap, hipMemcpyDeviceToDevice, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);

@@ -27,6 +27,8 @@ struct rdf_ctx {
     // device scalars + pinned host mirror
     DevBuf scal;
     u64* hscal = nullptr;
+    u64* hread = nullptr;   // pinned, device-mapped: k_gather_scalars writes the read-back scalars here directly
+    u64* hread_d = nullptr; // its device address
 
     // triples
     DevBuf ts, tp, to;
@@ -153,6 +155,10 @@ struct rdf_ctx {
 
     hipEvent_t ev[8] = {};
     float stage_ms[3] = {0, 0, 0};
+    // stage timings whose end events are recorded but not yet read (read at the run's final wait, or on demand):
+    // the stage boundaries do not drain the stream
+    bool pend_fc = false, pend_groups = false;
+    bool pend_heavy = false;  // heavy threshold / count of the last group build still on the device (hist + 256, + 258)
     // per kernel-family device timers (events on the context stream)
     static constexpr int kTSeg = 32;  // segments per timer (a kernel family may run in several places: the two light
                                       // passes record ~14 light segments)
@@ -219,46 +225,34 @@ static u64 next_pow2(u64 x) {
     return p;
 }
 
-// RDFIND_SYNC_TRACE=1: every host wait on the stream prints "SYNC <line> <t_us> <wait_us>" to stderr (dev tool: where
-// the host round trips of a step are, tools/sync_trace.py)
-static hipError_t traced_sync(hipStream_t s, int line) {
-    static const bool on = getenv("RDFIND_SYNC_TRACE") != nullptr;
-    if (!on) return hipStreamSynchronize(s);
+// Host waits on the stream.  Each read-back of a device size drains the stream: the GPU idles from the end of the
+// read until the host has launched the next kernel (~25-40 us per read on c2, tools/gaps.py), so the reads are one
+// kernel that stores the scalars straight into pinned host memory (no separate copy).  RDFIND_SPIN=1 polls the stream
+// instead of blocking in hipStreamSynchronize (measured: no gain on c2, 10.27 vs 10.23 ms, profiles/r04_sync_trace_*).
+// RDFIND_SYNC_TRACE=1: every wait prints "SYNC <line> <t_us> <wait_us>" to stderr (tools/sync_trace.py).
+static hipError_t stream_wait(hipStream_t s, int line) {
+    static const bool trace = getenv("RDFIND_SYNC_TRACE") != nullptr;
+    static const bool spin = getenv("RDFIND_SPIN") && atoi(getenv("RDFIND_SPIN")) != 0;
     using clk = std::chrono::steady_clock;
     static const clk::time_point t00 = clk::now();
-    const clk::time_point t0 = clk::now();
-    const hipError_t e = hipStreamSynchronize(s);
-    const clk::time_point t1 = clk::now();
-    fprintf(stderr, "SYNC %d %.1f %.1f\n", line, std::chrono::duration<double, std::micro>(t0 - t00).count(),
-            std::chrono::duration<double, std::micro>(t1 - t0).count());
+    const clk::time_point t0 = trace ? clk::now() : clk::time_point();
+    hipError_t e;
+    if (spin) {
+        while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+        }
+    } else {
+        e = hipStreamSynchronize(s);
+    }
+    if (trace) {
+        const clk::time_point t1 = clk::now();
+        fprintf(stderr, "SYNC %d %.1f %.1f\n", line, std::chrono::duration<double, std::micro>(t0 - t00).count(),
+                std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
     return e;
 }
-#define hipStreamSynchronize(s) traced_sync((s), __LINE__)
+#define hipStreamSynchronize(s) stream_wait((s), __LINE__)
 
-static rdf_status read_scalars(rdf_ctx* c, int count) {
-    HIP_TRY(c, hipMemcpyAsync(c->hscal, c->scal.p, count * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return RDF_OK;
-}
-
-static rdf_status read_u64(rdf_ctx* c, const void* dptr, u64* out) {
-    HIP_TRY(c, hipMemcpyAsync(c->hscal + 15, dptr, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    *out = c->hscal[15];
-    return RDF_OK;
-}
-
-static rdf_status read_u32(rdf_ctx* c, const void* dptr, u32* out) {
-    HIP_TRY(c, hipMemcpyAsync(c->hscal + 15, dptr, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    *out = (u32)(c->hscal[15] & 0xffffffffu);
-    return RDF_OK;
-}
-
-static u64* dscal(rdf_ctx* c, int i) { return c->scal.as<u64>() + i; }
-
-// Several device scalars with ONE host round trip: a one-thread kernel gathers them into scal[8..15],
-// one copy brings them back (each separate read is a stream drain plus a copy, ~20-40 us).
+// Several device scalars with ONE host round trip: a one-thread kernel gathers them into the mapped host buffer.
 struct ScalarGather {
     const void* p[8];
     int bytes[8];
@@ -269,6 +263,47 @@ __global__ void k_gather_scalars(ScalarGather g, u64* dst) {
     for (int i = 0; i < g.n; ++i) dst[i] = g.bytes[i] == 8 ? *(const u64*)g.p[i] : (u64) * (const u32*)g.p[i];
 }
 
+static u64* dscal(rdf_ctx* c, int i) { return c->scal.as<u64>() + i; }
+
+static rdf_status gather_read(rdf_ctx* c, const ScalarGather& g, u64* out) {
+    hipLaunchKernelGGL(k_gather_scalars, dim3(1), dim3(1), 0, c->stream, g, c->hread_d);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const volatile u64* h = c->hread;
+    for (int i = 0; i < g.n; ++i) out[i] = h[i];
+    return RDF_OK;
+}
+
+// scal[0, count) -> hscal[0, count)
+static rdf_status read_scalars(rdf_ctx* c, int count) {
+    ScalarGather g = {};
+    for (int i = 0; i < count; ++i) {
+        g.p[i] = dscal(c, i);
+        g.bytes[i] = 8;
+    }
+    g.n = count;
+    return gather_read(c, g, c->hscal);
+}
+
+static rdf_status read_u64(rdf_ctx* c, const void* dptr, u64* out) {
+    ScalarGather g = {};
+    g.p[0] = dptr;
+    g.bytes[0] = 8;
+    g.n = 1;
+    return gather_read(c, g, out);
+}
+
+static rdf_status read_u32(rdf_ctx* c, const void* dptr, u32* out) {
+    ScalarGather g = {};
+    g.p[0] = dptr;
+    g.bytes[0] = 4;
+    g.n = 1;
+    u64 v = 0;
+    TRY(gather_read(c, g, &v));
+    *out = (u32)v;
+    return RDF_OK;
+}
+
 static rdf_status read_multi(rdf_ctx* c, std::initializer_list<std::pair<const void*, int>> refs, u64* out) {
     ScalarGather g = {};
     for (const auto& r : refs) {
@@ -276,11 +311,7 @@ static rdf_status read_multi(rdf_ctx* c, std::initializer_list<std::pair<const v
         g.bytes[g.n] = r.second;
         ++g.n;
     }
-    hipLaunchKernelGGL(k_gather_scalars, dim3(1), dim3(1), 0, c->stream, g, dscal(c, 8));
-    HIP_TRY(c, hipMemcpyAsync(c->hscal + 8, dscal(c, 8), g.n * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < g.n; ++i) out[i] = c->hscal[8 + i];
-    return RDF_OK;
+    return gather_read(c, g, out);
 }
 
 static rdf_status load_bkeys(rdf_ctx* c) {
@@ -354,6 +385,8 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->hread, 16 * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->hread_d, c->hread, 0);
     for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
     for (int i = 0; i < 2 * RDF_NUM_TIMERS * rdf_ctx::kTSeg && e == hipSuccess; ++i) e = hipEventCreate(&c->tev[i]);
     if (e != hipSuccess) {
@@ -371,6 +404,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     for (DevBuf* b : ctx_buffers(c)) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
+    if (c->hread) (void)hipHostFree(c->hread);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->tev)
@@ -434,6 +468,7 @@ rdf_status rdf_release_scratch(rdf_ctx* c) {
     if (!c) return RDF_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     release_run_buffers(c, 0, true);
+    (void)hipGetLastError();  // an out-of-memory failure before this call is not the next call's error
     c->paged = false;
     c->stage = std::min(c->stage, 1);
     return RDF_OK;
@@ -969,6 +1004,7 @@ static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
     c->class_pending = false;
     c->paged = false;
     for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
+    c->pend_fc = c->pend_groups = c->pend_heavy = false;
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), c->stream));
     return RDF_OK;
@@ -976,11 +1012,23 @@ static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
 
 static rdf_status fc_end(rdf_ctx* c) {
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]));
-    tcollect(c, RDF_T_UNARY, RDF_T_BINARY + 1);
+    c->pend_fc = true;
     c->stage = 2;
     return RDF_OK;
+}
+
+// read the pending stage timings (waits for their end events; free after the run's final stream wait)
+static void settle_timings(rdf_ctx* c) {
+    if (c->pend_fc && hipEventSynchronize(c->ev[1]) == hipSuccess) {
+        (void)hipEventElapsedTime(&c->stage_ms[0], c->ev[0], c->ev[1]);
+        tcollect(c, RDF_T_UNARY, RDF_T_BINARY + 1);
+    }
+    c->pend_fc = false;
+    if (c->pend_groups && hipEventSynchronize(c->ev[3]) == hipSuccess) {
+        (void)hipEventElapsedTime(&c->stage_ms[1], c->ev[2], c->ev[3]);
+        tcollect(c, RDF_T_EMIT, RDF_T_HEAVYMASK + 1);
+    }
+    c->pend_groups = false;
 }
 
 rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stats* stats) {
@@ -1494,7 +1542,8 @@ static u64 auto_range_records(rdf_ctx* c) {
     return std::max<u64>(std::min<u64>(r, 1ull << 31), 1ull << 24);
 }
 
-// local group-size histogram (quarter-octave buckets) -> h_hist (host)
+// local group-size histogram (quarter-octave buckets) -> h_hist (host; nullptr: left on the device for
+// k_heavy_threshold)
 static rdf_status g_size_hist(rdf_ctx* c, u32* h_hist) {
     hipStream_t st = c->stream;
     tbegin(c, RDF_T_HEAVYMASK);
@@ -1504,6 +1553,7 @@ static rdf_status g_size_hist(rdf_ctx* c, u32* h_hist) {
         hipLaunchKernelGGL(k_group_size_hist, dim3(grid_for(c->G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->goff.as<u64>(), c->G, c->hist.as<u32>());
     tend(c, RDF_T_HEAVYMASK);
+    if (!h_hist) return RDF_OK;
     HIP_TRY(c, hipMemcpyAsync(h_hist, c->hist.p, 256 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
     return RDF_OK;
@@ -1523,8 +1573,10 @@ static u64 heavy_count(const u32* hist, u64 thr) {
     return n;
 }
 
-// heavy groups -> bitmask columns base.. (this rank's), binary components and parents CSR
-static rdf_status g_heavy_binary(rdf_ctx* c, u64 thr, u32 base) {
+// heavy groups -> bitmask columns base.. (this rank's), binary components and parents CSR.  dev_thr: the threshold
+// comes from the device histogram (k_heavy_threshold) and the heavy count stays on the device until the run's stats
+// are read (settle_group_stats); otherwise thr is the host's (sharded: from the all-gathered histogram).
+static rdf_status g_heavy_binary(rdf_ctx* c, u64 thr, u32 base, bool dev_thr = false) {
     hipStream_t st = c->stream;
     const u64 G = c->G;
     const u32 C = c->C, Cu = c->Cu;
@@ -1534,17 +1586,27 @@ static rdf_status g_heavy_binary(rdf_ctx* c, u64 thr, u32 base) {
     ENSURE(c, heavy_list, HMAX * 4);
     ENSURE(c, hbit, std::max<u64>(G, 1));
     u32* d_nheavy = c->hist.as<u32>() + 256;
+    u64* d_thr = reinterpret_cast<u64*>(c->hist.as<u32>() + 258);
     HIP_TRY(c, hipMemsetAsync(d_nheavy, 0, 4, st));
+    if (dev_thr) hipLaunchKernelGGL(k_heavy_threshold, dim3(1), dim3(1), 0, st, c->hist.as<u32>(), c->heavy_min, d_thr);
     if (G)
         hipLaunchKernelGGL(k_heavy_select, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), G,
-                           thr, base, d_nheavy, c->heavy_list.as<u32>(), c->hbit.as<uint8_t>());
-    u32 nh = 0;
-    TRY(read_u32(c, d_nheavy, &nh));
-    nh = base >= (u32)HMAX ? 0 : std::min<u32>(nh, HMAX - base);
-    c->nheavy = nh;
-    if (nh)
-        hipLaunchKernelGGL(k_heavy_mask, dim3(64, nh), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), c->gcap.as<u32>(),
-                           c->heavy_list.as<u32>(), base, c->info.as<CapInfo>());
+                           thr, dev_thr ? d_thr : nullptr, base, d_nheavy, c->heavy_list.as<u32>(), c->hbit.as<uint8_t>());
+    if (dev_thr) {
+        // k_heavy_select numbers at most HMAX - base columns (base = 0 here)
+        c->pend_heavy = true;
+        if (G)
+            hipLaunchKernelGGL(k_heavy_mask, dim3(64, HMAX), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), c->gcap.as<u32>(),
+                               c->heavy_list.as<u32>(), 0u, c->info.as<CapInfo>(), (const u32*)d_nheavy);
+    } else {
+        u32 nh = 0;
+        TRY(read_u32(c, d_nheavy, &nh));
+        nh = base >= (u32)HMAX ? 0 : std::min<u32>(nh, HMAX - base);
+        c->nheavy = nh;
+        if (nh)
+            hipLaunchKernelGGL(k_heavy_mask, dim3(64, nh), dim3(RDF_BLOCK), 0, st, c->goff.as<u64>(), c->gcap.as<u32>(),
+                               c->heavy_list.as<u32>(), base, c->info.as<CapInfo>(), (const u32*)nullptr);
+    }
     const u32 Cb = C - Cu;
     ENSURE(c, bcomp, std::max<u64>(2ull * Cb, 1) * 4);
     ENSURE(c, bkeyc, std::max<u64>(Cb, 1) * 8);
@@ -1582,13 +1644,27 @@ static void fill_group_stats(rdf_ctx* c) {
     s.n_join_ranges = c->n_group_ranges;
 }
 
+// the heavy threshold and count of a device-threshold build -> gstats (one host read; at the run's end for rdf_run)
+static rdf_status settle_group_stats(rdf_ctx* c) {
+    if (c->pend_heavy) {
+        u64 v[2];
+        TRY(read_multi(c, {{c->hist.as<u32>() + 258, 8}, {c->hist.as<u32>() + 256, 4}}, v));
+        c->heavy_threshold = v[0];
+        c->nheavy = (u32)std::min<u64>(v[1], HMAX);
+        c->pend_heavy = false;
+        fill_group_stats(c);
+    }
+    return RDF_OK;
+}
+
 static rdf_status g_finish(rdf_ctx* c, rdf_group_stats* stats) {
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[1], c->ev[2], c->ev[3]));
-    tcollect(c, RDF_T_EMIT, RDF_T_HEAVYMASK + 1);
+    c->pend_groups = true;
     fill_group_stats(c);
-    if (stats) *stats = c->gstats;
+    if (stats) {
+        TRY(settle_group_stats(c));
+        *stats = c->gstats;
+    }
     c->stage = 3;
     return RDF_OK;
 }
@@ -1610,9 +1686,8 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
         TRY(g_compact_groups(c));
     }
     if (c->ar_on) TRY(g_ar_refs(c));
-    u32 h_hist[256];
-    TRY(g_size_hist(c, h_hist));
-    TRY(g_heavy_binary(c, heavy_threshold(c, h_hist), 0));
+    TRY(g_size_hist(c, nullptr));
+    TRY(g_heavy_binary(c, 0, 0, true));
     return g_finish(c, stats);
 }
 
@@ -2333,6 +2408,7 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
     HIP_TRY(c, hipStreamSynchronize(st));
     if (c->n_lists) TRY(read_u64(c, c->loff.as<u64>() + ncls, &c->n_list_refs));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], c->ev[5]));
+    settle_timings(c);
     tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS);
     c->n_out = K + H + HC;
     c->n_class_out = HC;
@@ -2592,6 +2668,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     HIP_TRY(c, hipEventRecord(c->ev[5], st));
     HIP_TRY(c, hipStreamSynchronize(st));
     HIP_TRY(c, hipEventElapsedTime(&c->stage_ms[2], c->ev[4], c->ev[5]));
+    settle_timings(c);
     tcollect(c, RDF_T_PIVOT, RDF_NUM_TIMERS);
     rdf_cind_stats& cs = c->cstats;
     memset(&cs, 0, sizeof(cs));
@@ -2663,9 +2740,13 @@ rdf_status rdf_run(rdf_ctx* c, uint32_t min_support, const char* projection, uin
         r = rdf_association_rules(c, nullptr);
         if (r) return r;
     }
-    r = rdf_build_capture_groups(c, projection, gs);
+    r = rdf_build_capture_groups(c, projection, nullptr);  // its stats are read after the discovery (no extra wait)
     if (r) return r;
-    return rdf_discover_cinds(c, flags, cs);
+    r = rdf_discover_cinds(c, flags, cs);
+    if (r) return r;
+    TRY(settle_group_stats(c));
+    if (gs) *gs = c->gstats;
+    return RDF_OK;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3810,7 +3891,10 @@ rdf_status rdf_last_stats(rdf_ctx* c, rdf_fc_stats* fc, rdf_group_stats* gs, rdf
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "no completed run");
     if (fc) *fc = c->fstats;
-    if (gs) *gs = c->gstats;
+    if (gs) {
+        TRY(settle_group_stats(c));
+        *gs = c->gstats;
+    }
     if (cs) *cs = c->cstats;
     return RDF_OK;
 }
@@ -4103,12 +4187,14 @@ rdf_status rdf_copy_binary_keys(rdf_ctx* c, uint64_t* out, uint64_t cap) {
 
 rdf_status rdf_kernel_times(rdf_ctx* c, float* ms, int count) {
     if (!c || !ms || count < 0) return RDF_ERR_ARG;
+    settle_timings(c);
     for (int i = 0; i < count; ++i) ms[i] = i < RDF_NUM_TIMERS ? c->tms[i] : 0.f;
     return RDF_OK;
 }
 
 rdf_status rdf_stage_times(rdf_ctx* c, float* ms3) {
     if (!c || !ms3) return RDF_ERR_ARG;
+    settle_timings(c);
     for (int i = 0; i < 3; ++i) ms3[i] = c->stage_ms[i];
     return RDF_OK;
 }

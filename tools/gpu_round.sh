@@ -21,14 +21,17 @@ for step in "$@"; do
         || { echo "prof failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
       find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_$TAG.kernel_stats.csv \;
       head -25 gpurun_out/prof_$TAG.kernel_stats.csv ;;
-    configs)  # the other BASELINE shapes on one GPU (c3 at half size: its generator runs ~2 min on the host)
-      for cfg in "c1 1.0" "c3 0.5" "c3 1.0" "c5 0.1" "c5 0.3"; do
-        set -- $cfg
-        echo "config $1 scale $2" >&2
-        timeout -k 10 400 python -u bench.py --config $1 --scale $2 --steps 3 --warmup 1 --no-cpu-baseline --no-ingest \
-          > gpurun_out/cfg_${TAG}_$1.json 2> gpurun_out/cfg_${TAG}_$1.err \
-          || { echo "config $1 failed"; tail -20 gpurun_out/cfg_${TAG}_$1.err; exit 1; }
-        cat gpurun_out/cfg_${TAG}_$1.json
+    configs|configs:*)  # the other BASELINE shapes on one GPU, each with its CPU baseline (a bounded sample where the
+      # full run is too long; bench.py CPU_SAMPLE_SCALE).  configs:<cfg>@<scale>,... picks them
+      LIST="c1@1.0 c3@0.5 c3@1.0 c4@0.05 c4@0.4 c5@0.1 c5@0.3"
+      [ "$step" != configs ] && LIST=$(echo "${step#configs:}" | tr ',' ' ')
+      for cs in $LIST; do
+        CFG=${cs%@*}; SC=${cs#*@}
+        echo "config $CFG scale $SC" >&2
+        timeout -k 10 500 python -u bench.py --config $CFG --scale $SC --steps 3 --warmup 1 --no-ingest \
+          > gpurun_out/cfg_${TAG}_${CFG}_$SC.json 2> gpurun_out/cfg_${TAG}_${CFG}_$SC.err \
+          || { echo "config $CFG $SC failed"; tail -20 gpurun_out/cfg_${TAG}_${CFG}_$SC.err; exit 1; }
+        head -c 600 gpurun_out/cfg_${TAG}_${CFG}_$SC.json; echo
       done ;;
     cprof:*)  # cprof:<config>:<scale> -- kernel stats of one step of another BASELINE shape
       IFS=: read -r _ CFG SC <<< "$step"
