@@ -45,7 +45,7 @@ FAMILY_KERNELS = {
                 "k_keep_scatter"],
     "groups": ["k_key_offsets", "k_group_flags", "k_group_build", "k_dgrp"],
     "pivot": ["k_group_info", "k_pivot_nseg", "k_pivot_short", "k_pivot_seg", "k_pivot_final"],
-    "light": ["k_light", "k_light_packed", "k_light_mseg_emit", "k_mseg_chunks", "k_slot_compact"],
+    "light": ["k_light", "k_light_stage", "k_light_plain", "k_light_packed", "k_light_mseg_emit", "k_mseg_chunks", "k_slot_compact"],
     "rules": ["k_rules_explicit", "k_rules_mark", "k_compact_refs"],
     "cemit": ["k_class_emit"],
 }

@@ -451,79 +451,88 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
                                                             int joinbits, JoinSel js, u64* block_counts,
                                                             const u64* __restrict__ block_offsets, u64* out, int recbits) {
     __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
-    __shared__ u64 stage[WRITE ? RDF_BLOCK * 9 : 1];  // the iteration's records, written out contiguously
     __shared__ u64 htab[WRITE ? EMIT_DEDUP_SLOTS : 1];  // the iteration's distinct records (write pass)
     const u64 b = (u64)blockIdx.x * per;
     const u64 e = b + per < n ? b + per : n;
-    u64 run = WRITE ? block_offsets[blockIdx.x] : 0;
+    if (!WRITE) {  // the block's record count: per-thread sums, one block reduction at the end
+        u32 mine = 0;
+        for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
+            u64 rec[9];
+            mine += triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec);
+        }
+        u32 total;
+        block_exclusive_scan_u32(mine, lds_wave, &total);
+        if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+        return;
+    }
+    u64 run = block_offsets[blockIdx.x];
 #ifndef RDF_EMIT_DEDUP
 #define RDF_EMIT_DEDUP 1
 #endif
-    const bool dedup = WRITE && RDF_EMIT_DEDUP && recbits <= 48;
+    const bool dedup = RDF_EMIT_DEDUP && recbits <= 48;
     u32 tag = 0;
     if (dedup) {
         for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;  // tag 0: empty
+        __syncthreads();
     }
     for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
         u32 c = 0, rep = 0;
         if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, &rep);
-        u32 total;
-        if (!WRITE) {
-            block_exclusive_scan_u32(c, lds_wave, &total);
-        } else {
-            // Records repeated within the iteration's 256 triples (the same subject's predicate, the same
-            // (predicate, object) pair: ~23 % of c2's records; only the kinds flagged by triple_records are looked up)
-            // are written once; the count pass's region stays
-            // as it is and its tail is padded with EMIT_PAD, which the record sort's first pass drops.  The LDS table
-            // slots carry the iteration's tag in bits 48.. (records have <= 48 bits here), so it is never cleared.
-            u32 keep = (1u << c) - 1u;
-            if (dedup) {
-                ++tag;
-                if (tag == (1u << 15)) {  // tags wrap: clear the table once
-                    for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;
-                    tag = 1;
-                }
+        // Records repeated within the iteration's 256 triples (the same subject's predicate, the same (predicate,
+        // object) pair: ~23 % of c2's records; only the kinds flagged by triple_records are looked up) are written
+        // once; the count pass's region stays as it is and its tail is padded with EMIT_PAD, which the record sort's
+        // first pass drops.  The LDS table slots carry the iteration's tag in bits 48.. (records have <= 48 bits
+        // here), so it is cleared only when the tag wraps; the previous iteration's insertions finished before its
+        // scan's barriers.
+        u32 keep = (1u << c) - 1u;
+        if (dedup) {
+            ++tag;
+            if (tag == (1u << 15)) {  // tags wrap: clear the table once
                 __syncthreads();
-                keep = ((1u << c) - 1u) & ~rep;  // only the repeating kinds go through the table
-                for (int k = 0; k < 9; ++k) {
-                    if ((u32)k >= c) break;
-                    if (!((rep >> k) & 1u)) continue;
-                    const u64 want = rec[k] | ((u64)tag << 48);
-                    u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
-                    u64 cur = htab[h];
-                    while (true) {
-                        if ((u32)(cur >> 48) != tag) {  // a slot of an earlier iteration: free
-                            const u64 prev = atomicCAS((unsigned long long*)&htab[h], (unsigned long long)cur,
-                                                       (unsigned long long)want);
-                            if (prev == cur) {  // the first copy of the record: kept
-                                keep |= 1u << k;
-                                break;
-                            }
-                            cur = prev;
-                            continue;
+                for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;
+                __syncthreads();
+                tag = 1;
+            }
+            keep = ((1u << c) - 1u) & ~rep;  // only the repeating kinds go through the table
+            for (int k = 0; k < 9; ++k) {
+                if ((u32)k >= c) break;
+                if (!((rep >> k) & 1u)) continue;
+                const u64 want = rec[k] | ((u64)tag << 48);
+                u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
+                u64 cur = htab[h];
+                while (true) {
+                    if ((u32)(cur >> 48) != tag) {  // a slot of an earlier iteration: free
+                        const u64 prev = atomicCAS((unsigned long long*)&htab[h], (unsigned long long)cur,
+                                                   (unsigned long long)want);
+                        if (prev == cur) {  // the first copy of the record: kept
+                            keep |= 1u << k;
+                            break;
                         }
-                        if (cur == want) break;  // a copy is kept by another record
-                        h = (h + 1) & (EMIT_DEDUP_SLOTS - 1);
-                        cur = htab[h];
+                        cur = prev;
+                        continue;
                     }
+                    if (cur == want) break;  // a copy is kept by another record
+                    h = (h + 1) & (EMIT_DEDUP_SLOTS - 1);
+                    cur = htab[h];
                 }
             }
-            u32 kept;
-            const u32 koff = block_exclusive_scan_u32((u32)__popc(keep), lds_wave, &kept);
-            block_exclusive_scan_u32(c, lds_wave, &total);
-            u32 q = koff;
-#pragma unroll
-            for (int k = 0; k < 9; ++k)
-                if ((keep >> k) & 1u) stage[q++] = rec[k];
-            __syncthreads();
-            for (u32 k = threadIdx.x; k < total; k += RDF_BLOCK) out[run + k] = k < kept ? stage[k] : EMIT_PAD;
-            __syncthreads();
         }
+        // one scan of (kept, emitted) packed in 16-bit halves (each <= 9 x 256): this thread's kept records go to the
+        // front of the iteration's region, its dropped ones become padding behind all kept records
+        const u32 nk = (u32)__popc(keep);
+        u32 tot;
+        const u32 off = block_exclusive_scan_u32(nk | (c << 16), lds_wave, &tot);
+        const u32 kept = tot & 0xffffu, total = tot >> 16;
+        u64 q = run + (off & 0xffffu);
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            if ((keep >> k) & 1u) out[q++] = rec[k];
+        u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
+        for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
         run += total;
     }
-    if (!WRITE && threadIdx.x == 0) block_counts[blockIdx.x] = run;
 }
 
 // ================================================================================================
@@ -1825,19 +1834,30 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // counter: an agent-scope release fence writes back the whole L2 of the XCD, per work item.
     if (lane == 0 && (alive0 & ~alive)) atomicOr(&dead[oct0], alive0 & ~alive);
 }
-#ifdef RDF_LIGHT_WAVES
-#define RDF_LIGHT_ATTR __attribute__((amdgpu_waves_per_eu(RDF_LIGHT_WAVES)))
+// Occupancy per variant (waves per SIMD; the register budget follows): the staging variant (small groups, c2) is
+// fastest unconstrained (151 VGPRs, 3 waves); the plain variant (large groups, c4) at RDF_LIGHT_PLAIN_WAVES
+// (profiles/r04_light_ab_occupancy.log)
+#ifdef RDF_LIGHT_STAGE_WAVES
+#define RDF_LIGHT_STAGE_ATTR __attribute__((amdgpu_waves_per_eu(RDF_LIGHT_STAGE_WAVES)))
 #else
-#define RDF_LIGHT_ATTR
+#define RDF_LIGHT_STAGE_ATTR
 #endif
-template <bool STAGE>
-__global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_ATTR void k_light(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
-                                                     const u64* __restrict__ choff, u64 w0, u64 W, u64 ob, u64* dead,
-                                                     u64* slots, u32* counts) {
-    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_light_body<STAGE>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
-    }
+#ifdef RDF_LIGHT_PLAIN_WAVES
+#define RDF_LIGHT_PLAIN_ATTR __attribute__((amdgpu_waves_per_eu(RDF_LIGHT_PLAIN_WAVES)))
+#else
+#define RDF_LIGHT_PLAIN_ATTR
+#endif
+#define RDF_LIGHT_ARGS                                                                                                     \
+    u64 nvblk, CindView v, const u32 *__restrict__ pivot, const u64 *__restrict__ itemoff,                               \
+        const u32 *__restrict__ item_dep, const u64 *__restrict__ choff, u64 w0, u64 W, u64 ob, u64 *dead, u64 *slots,  \
+        u32 *counts
+__global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_STAGE_ATTR void k_light_stage(RDF_LIGHT_ARGS) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
+        k_light_body<true>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
+}
+__global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_PLAIN_ATTR void k_light_plain(RDF_LIGHT_ARGS) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
+        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
 }
 
 
@@ -2627,19 +2647,27 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_decode_rows(const u32* __restrict
 // by the caller's collectives; light dependents' local survivors are routed to the dependent's owner
 // (dep_owner), which keeps a ref iff every rank holding a light group of the dependent reported it.
 
-// MIN-allreduce keys of the local pivot: (size << 32 | rank), INT64_MAX where the rank has no group
+// MIN-allreduce keys of the local pivot, INT64_MAX where the rank has no group:
 // (smallest local group size, tie-break, rank) of each dependent for the MIN all-reduce that elects the pivot holder.
-// Ties between ranks (common: many dependents have equal smallest groups on several ranks) go to a pseudo-random rank
-// per dependent, not to the lowest rank, so the holders' work (light candidates, verify traffic) spreads evenly.
-__device__ __host__ inline u64 holder_key(u64 size, u32 d, u32 rank) {
-    return (size << 32) | ((mix64(((u64)d << 8) | rank) >> 40) << 8) | rank;
+// Ties between ranks (common: many dependents have equal smallest groups on several ranks) go to a pseudo-random rank,
+// not to the lowest rank, so the holders' work (light candidates, verify traffic) spreads evenly.  The tie-break is
+// salted by the heavy-group mask when there is one: the members of a mask class have the same groups and must elect
+// the same holder (k_class_pivot_shard builds each class's list on its members' holder).
+#ifndef RDF_HOLDER_TIEBREAK
+#define RDF_HOLDER_TIEBREAK 1
+#endif
+__device__ __host__ inline u64 holder_key(u64 size, u64 hmask, u32 d, u32 rank) {
+    const u64 salt = hmask ? hmask : ((u64)d | (1ull << 63));
+    const u64 tie = RDF_HOLDER_TIEBREAK ? mix64(salt ^ ((u64)(rank + 1) * 0x9E3779B97F4A7C15ull)) >> 40 : 0ull;
+    return (size << 32) | (tie << 8) | rank;
 }
 __device__ __host__ inline u32 holder_rank(u64 key) { return (u32)(key & 0xffu); }
 
-__global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __restrict__ best, u32 C, u32 rank, u64* out) {
+__global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __restrict__ best, const CapInfo* __restrict__ info,
+                                                               u32 C, u32 rank, u64* out) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = best[d];
-        out[d] = b == ~0ull ? 0x7fffffffffffffffull : holder_key(b >> 32, (u32)d, rank);
+        out[d] = b == ~0ull ? 0x7fffffffffffffffull : holder_key(b >> 32, info[d].hmask, (u32)d, rank);
     }
 }
 

@@ -1955,7 +1955,7 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,
                            slots.as<u64>(), counts.as<u32>());
     if (WI) {
-        auto kl = c->light_stage ? k_light<true> : k_light<false>;
+        auto kl = c->light_stage ? k_light_stage : k_light_plain;
         hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
                            0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
                            r.i0, WI, ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>());
@@ -3032,7 +3032,7 @@ static rdf_status sh_phase3(rdf_ctx* c, rdf_exchange* req) {
     ENSURE(c, xsend, std::max<u64>(c->C, 1) * 8);
     if (c->C)
         hipLaunchKernelGGL(k_shard_best_keys, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
-                           c->pbest.as<u64>(), c->C, c->rank, c->xsend.as<u64>());
+                           c->pbest.as<u64>(), c->info.as<CapInfo>(), c->C, c->rank, c->xsend.as<u64>());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return x_request(c, req, RDF_X_ALLREDUCE_MIN_U64, c->xsend.p, c->C, 4);
 }

@@ -177,13 +177,14 @@ def test_sharded_bench_size_properties():
 
 
 def test_shard_slice_limit_is_per_rank():
-    """The 2^32/9-triples-per-context limit applies to a rank's own slice and join shard, not to the input: a
-    sharded input of more triples than one context accepts is taken slice by slice (the size check only)."""
+    """The per-context input limit (2^32/3 triples: K1/K2 address their 3n records with u32 offsets; larger inputs
+    than 2^32/9 build their groups in join ranges) applies to a rank's own slice, not to the input: a sharded input
+    of more triples than one context accepts is taken slice by slice (the size check only)."""
     from rdfind_amd import _lib
 
     with _lib.Context(0) as ctx:
-        n_total = (1 << 32) // 9 + 1000  # above the single-context limit
-        with pytest.raises(_lib.RdfError, match="2\\^32/9"):
+        n_total = (1 << 32) // 3 + 1000  # above the single-context limit
+        with pytest.raises(_lib.RdfError, match="2\\^32/3"):
             ctx.set_triples_device(1 << 20, 1 << 20, 1 << 20, n_total, 1000)  # size check precedes any access
         ctx.set_triples_device(1 << 20, 1 << 20, 1 << 20, n_total // 8, 1000)  # one rank of 8: accepted
 
