@@ -68,6 +68,13 @@ static constexpr int LIGHT_STAGE_MIN = RDF_STAGE_MIN;
 #ifndef RDF_STAGE_AVG
 #define RDF_STAGE_AVG 48
 #endif
+// k_light_plain_hi (6 waves per SIMD) when the member-weighted mean light group has >= LIGHT_HIOCC_AVG members AND
+// the light work has >= LIGHT_HIOCC_OCT output octets per capture (long, latency-bound items: many candidates per
+// dependent searched in large groups).  Measured (profiles/r04_light_ab_hiocc.log): c4 at 0.05 (2,674 / 59) light
+// 11.2 -> 10.5 ms, c4 at 0.4 (13,560 / 55) 182 -> 160 ms; c3 at 0.5 (4,719 / 9.7) 10.6 -> 11.5 and c1 (412 / 68)
+// 0.96 -> 1.10 lose, c5 at 0.1 (1,291 / 232) is flat, so both conditions must hold.
+static constexpr u64 LIGHT_HIOCC_AVG = 2048;
+static constexpr u64 LIGHT_HIOCC_OCT = 32;
 static constexpr u64 LIGHT_STAGE_AVG = RDF_STAGE_AVG;  // staging variant when the weighted mean light group is smaller
                   // groups up to this size are searched in LDS (2 KiB per wave)
 

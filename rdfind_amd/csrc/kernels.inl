@@ -1859,6 +1859,12 @@ __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_PLAIN_ATTR void k_light_plain(
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
         k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
 }
+// the plain variant at 6 waves per SIMD (84 VGPRs, some spills): inputs whose light groups are very large (c4: the
+// searches and sweeps are latency-bound, more waves hide more of it), chosen by LIGHT_HIOCC_AVG
+__global__ __launch_bounds__(RDF_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_light_plain_hi(RDF_LIGHT_ARGS) {
+    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
+        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
+}
 
 
 // chunks verified by several segments: survivors = candidates minus the union of the segments' kills

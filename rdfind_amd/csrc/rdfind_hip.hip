@@ -82,7 +82,9 @@ struct rdf_ctx {
     DevBuf brkeys2, bstart2;  // K2 records re-partitioned into sub-buckets (k_b2_split) and their starts
     DevBuf ginfo;  // group -> size | heavy bit (k_group_info)
     DevBuf gsums;  // sum of light group sizes, of their squares (k_group_info)
-    bool light_stage = false;  // k_light<true>: stage small light groups in LDS rows (chosen per run)
+    bool light_stage = false;  // k_light_stage: stage small light groups in LDS rows (chosen per run)
+    bool light_hiocc = false;  // k_light_plain_hi: the plain variant at 6 waves per SIMD (LIGHT_HIOCC_*)
+    u64 light_wmean = 0;       // member-weighted mean light group size of the run (k_group_info sums)
     DevBuf piv2;   // dependent -> second pivot (smallest light group after the pivot)
     DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
     bool dense_on = false;
@@ -1843,6 +1845,7 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         WS = r[0];
         // member-weighted mean light group size sum(n^2) / sum(n): small groups -> the LDS-staging light variant
         c->light_stage = r[2] <= (u64)LIGHT_STAGE_AVG * r[1];
+        c->light_wmean = r[1] ? r[2] / r[1] : 0;
         static const char* force = getenv("RDFIND_STAGE");  // A/B and test hook: 0 / 1 forces the variant
         if (force) c->light_stage = atoi(force) != 0;
     }
@@ -1870,6 +1873,12 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
                        {dscal(c, 5), 8}}, v));
     c->n_multi_items = v[7];
     *WL = v[0];
+    c->light_hiocc = !c->light_stage && c->light_wmean >= LIGHT_HIOCC_AVG && v[0] >= LIGHT_HIOCC_OCT * (u64)C;
+    static const char* hi = getenv("RDFIND_LIGHT_HIOCC");  // A/B and test hook: 0 / 1 forces the occupancy
+    if (hi) c->light_hiocc = !c->light_stage && atoi(hi) != 0;
+    if (getenv("RDFIND_DEBUG_LIGHT"))
+        fprintf(stderr, "LIGHT weighted mean light group %llu, octets per capture %.1f (stage %d, hiocc %d)\n",
+                (unsigned long long)c->light_wmean, C ? (double)v[0] / C : 0.0, (int)c->light_stage, (int)c->light_hiocc);
     *WP = v[1];
     *WH = v[2];
     c->heavy_candidates = v[3];
@@ -1955,7 +1964,7 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,
                            slots.as<u64>(), counts.as<u32>());
     if (WI) {
-        auto kl = c->light_stage ? k_light_stage : k_light_plain;
+        auto kl = c->light_stage ? k_light_stage : c->light_hiocc ? k_light_plain_hi : k_light_plain;
         hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
                            0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
                            r.i0, WI, ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>());
@@ -3069,7 +3078,7 @@ static rdf_status sh_phase5(rdf_ctx* c, rdf_exchange* req) {
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
     c->sh_WH = WH;
     TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
-    c->n_explicit_raw = E;
+    c->n_explicit_raw = E;  // the holder's survivors until the owners have the verified pairs (sh_phase6)
     c->n_light_chunks = WL;
     // holder-first exchange: every survivor to d's owner (report) and to the other ranks holding light groups of d
     // (verify), grouped by destination
@@ -3224,6 +3233,7 @@ static rdf_status sh_phase6(rdf_ctx* c, rdf_exchange* req) {
     HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->flags.as<u32>(), c->pos.as<u64>(), n, c->pos.as<u64>() + n, st));
     u64 E = 0;
     TRY(read_u64(c, c->pos.as<u64>() + n, &E));
+    c->n_explicit_raw = E;  // the verified raw pairs this rank owns (the ranks' sum is the single-GPU count)
     ENSURE(c, xsend, std::max<u64>(E, 1) * 8);
     if (n)
         hipLaunchKernelGGL(k_compact_u64, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), n,
