@@ -936,7 +936,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
         u32 nlight = 0;
         u64 sg[SIG_W] = {};
         for (u64 j = b; j < e; ++j) {
-            const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
+            const u32 raw = v.dgrp[j], g = raw & ~DGRP_HEAVY;
             const u32 gi = v.ginfo[g];
             const u64 key = ((u64)(gi & ~GINFO_HEAVY) << 32) | g;
             best = key < best ? key : best;
@@ -947,7 +947,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
                 l2 = key < l2 ? (key < l1 ? l1 : key) : l2;
                 l1 = key < l1 ? key : l1;
             }
-            dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
+            const u32 tagged = light ? g : (g | DGRP_HEAVY);
+            if (tagged != raw) dgrp_tag[j] = tagged;  // in place: light entries stay as they are (no rewrite)
         }
         best_out[d] = best;
         nlight_out[d] = nlight;
@@ -971,7 +972,7 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
     u32 nlight = 0;
     u64 sg[SIG_W] = {};
     for (u64 j = b + lane; j < e; j += RDF_WAVE) {
-        const u32 g = v.dgrp[j] & ~DGRP_HEAVY;
+        const u32 raw = v.dgrp[j], g = raw & ~DGRP_HEAVY;
         const u32 gi = v.ginfo[g];
         const u64 key = ((u64)(gi & ~GINFO_HEAVY) << 32) | g;
         best = key < best ? key : best;
@@ -982,7 +983,8 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
             l2 = key < l2 ? (key < l1 ? l1 : key) : l2;
             l1 = key < l1 ? key : l1;
         }
-        dgrp_tag[j] = light ? g : (g | DGRP_HEAVY);
+        const u32 tagged = light ? g : (g | DGRP_HEAVY);
+        if (tagged != raw) dgrp_tag[j] = tagged;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
