@@ -473,6 +473,7 @@ def main():
             "cpu_baseline": cpu, "ingest": ingest, **({"ranks": ranks} if ranks else {}),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
+                     "join_ranges": gs.get("n_join_ranges", 1),
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],
                      "explicit_raw": cs["n_explicit_raw"], "heavy_chunks": cs["n_heavy_chunks"],
                      "heavy_candidates": cs["n_heavy_candidates"], "class_members": cs["n_class_members"],

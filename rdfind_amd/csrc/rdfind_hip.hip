@@ -160,7 +160,8 @@ struct rdf_ctx {
     // stage timings whose end events are recorded but not yet read (read at the run's final wait, or on demand):
     // the stage boundaries do not drain the stream
     bool pend_fc = false, pend_groups = false;
-    bool pend_heavy = false;  // heavy threshold / count of the last group build still on the device (hist + 256, + 258)
+    bool pend_heavy = false;
+    bool spare_fc = false, spare_groups = false;  // reclaim_spare may release these stages' scratch  // heavy threshold / count of the last group build still on the device (hist + 256, + 258)
     // per kernel-family device timers (events on the context stream)
     static constexpr int kTSeg = 32;  // segments per timer (a kernel family may run in several places: the two light
                                       // passes record ~14 light segments)
@@ -212,7 +213,34 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
         if (_r != RDF_OK) return _r; \
     } while (0)
 
-#define ENSURE(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.ensure((size_t)(bytes)))
+// Spare buffers: the frequent-condition stage's record scratch after that stage, and the group build's record and
+// sort buffers after it (up to ~120 GB at 10^9 triples).  They stay allocated across runs (re-allocating tens of GB
+// every step cost seconds: c4 at 10^9 triples spent 4.3 of 6.4 s per step outside its kernels) and are released
+// only when an allocation of a later stage would otherwise fail.
+static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
+    DevBuf* fc_scratch[] = {&c->brkeys, &c->brkeys2, &c->tkeys, &c->urecs};
+    DevBuf* grp_scratch[] = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp};
+    bool any = false;
+    for (int k = 0; k < 2; ++k) {
+        if (!(k == 0 ? c->spare_fc : c->spare_groups)) continue;
+        for (DevBuf* b : (k == 0 ? fc_scratch : grp_scratch)) {
+            if (b == keep || !b->p) continue;
+            if (!any) (void)hipStreamSynchronize(c->stream);  // queued kernels may still read them
+            b->release();
+            any = true;
+        }
+    }
+    (void)hipGetLastError();
+    return any;
+}
+static rdf_status ensure_buf(rdf_ctx* c, DevBuf* b, size_t bytes, const char* what) {
+    hipError_t e = b->ensure(bytes);
+    if (e == hipErrorOutOfMemory && reclaim_spare(c, b)) e = b->ensure(bytes);
+    if (e != hipSuccess)
+        return fail(c, e == hipErrorOutOfMemory ? RDF_ERR_OOM : RDF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return RDF_OK;
+}
+#define ENSURE(ctx, buf, bytes) TRY(ensure_buf(ctx, &(ctx)->buf, (size_t)(bytes), "allocating " #buf))
 #define ENSURE_KEEP(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.grow_keep((size_t)(bytes), (ctx)->stream))
 
 static int bits_for(u64 maxval) {  // bits needed to represent values in [0, maxval]
@@ -1007,6 +1035,7 @@ static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
     c->paged = false;
     for (int i = 0; i < RDF_NUM_TIMERS; ++i) c->tn[i] = 0;  // a failed run may have left segments behind
     c->pend_fc = c->pend_groups = c->pend_heavy = false;
+    c->spare_fc = false;  // this stage's scratch is in use again
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), c->stream));
     return RDF_OK;
@@ -1015,6 +1044,7 @@ static rdf_status fc_begin(rdf_ctx* c, uint32_t min_support) {
 static rdf_status fc_end(rdf_ctx* c) {
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     c->pend_fc = true;
+    c->spare_fc = true;
     c->stage = 2;
     return RDF_OK;
 }
@@ -1188,6 +1218,7 @@ static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj
 
 // record key layout of this run's K3 records: capture << joinbits | join
 static rdf_status g_record_bits(rdf_ctx* c) {
+    c->spare_groups = false;  // a group build starts: its record buffers are in use
     const u32 V = c->V ? c->V : 1;
     const u64 ncap = 2ull * c->U + c->B;  // compact candidate captures (k_frank_final)
     const int capbits = bits_for(ncap ? ncap - 1 : 0);
@@ -1391,11 +1422,8 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     HIP_TRY(c, hipEventRecord(c->ev[2], st));
     c->J_emit = 0;
     c->sort_passes_records = 0;
-    // the frequent-condition stage's record scratch is not needed again this run (up to 84 GB at 10^9 triples)
-    c->brkeys.release();
-    c->brkeys2.release();
-    c->tkeys.release();
-    c->urecs.release();
+    // the frequent-condition stage's record scratch (up to 84 GB at 10^9 triples) is spare from here on: reclaimed
+    // by the range buffers' allocation if they need the room
     // 1. ranges
     const int jshift = joinbits > 14 ? joinbits - 14 : 0;
     ENSURE(c, jhist, JH_BUCKETS * 8);
@@ -1525,8 +1553,7 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     c->hscal[14] = Jf;
     HIP_TRY(c, hipMemcpyAsync(c->goff.as<u64>() + G0, c->hscal + 14, 8, hipMemcpyHostToDevice, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    // the range scratch is sized by the largest range; the discovery stage needs the room
-    for (DevBuf* b : {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->gflag, &c->gexcl, &c->fpos, &c->flags}) b->release();
+    // the range scratch is sized by the largest range: spare for the discovery stage (g_finish marks it)
     c->rec_sorted = nullptr;
     return RDF_OK;
 }
@@ -1661,6 +1688,8 @@ static rdf_status settle_group_stats(rdf_ctx* c) {
 
 static rdf_status g_finish(rdf_ctx* c, rdf_group_stats* stats) {
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    c->spare_groups = true;  // the records and their sort buffers are not read after the group build
+    c->rec_sorted = nullptr;
     c->pend_groups = true;
     fill_group_stats(c);
     if (stats) {
