@@ -1608,6 +1608,9 @@ __device__ inline bool light_sweep(const CindView& v, const u32* gm, u64 gsz, u3
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
+#ifndef RDF_LIGHT_PREFETCH
+#define RDF_LIGHT_PREFETCH 0
+#endif
 template <bool STAGE>
 __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
@@ -1627,15 +1630,39 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const u64 chunk = item / nseg, seg = item % nseg;
     const u32 piv = pivot[d];
     const CapInfo id = v.info[d];
+    const u64 b = b0 + seg * LIGHT_SEG;
+    const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
+    // The dependent's smallest light group after the pivot is checked first (below).  It and the first window's group
+    // metadata do not depend on the candidates, so with RDF_LIGHT_PREFETCH their loads are issued before the
+    // candidate filter's and overlap its round trips (a 1-window item's serial chain: 5 round trips instead of 7).
+    const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
+    u32 gg[LIGHT_IT];
+    u64 gbv[LIGHT_IT];
+    u32 gszv[LIGHT_IT];
+    const u32* gdr[LIGHT_IT];
+#if RDF_LIGHT_PREFETCH
+    const bool pf = true;
+#pragma unroll
+    for (int it = 0; it < LIGHT_IT; ++it) {
+        const u64 j = b + (u64)it * RDF_WAVE + lane;
+        gg[it] = j < e ? v.dgrp[j] : NONE32;
+        if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY
+        gbv[it] = 0;
+        gszv[it] = 0;
+        gdr[it] = nullptr;
+        if (gg[it] != NONE32) {
+            gbv[it] = v.goff[gg[it]];
+            gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
+            gdr[it] = dense_row(v, gg[it]);
+        }
+    }
+#else
+    const bool pf = false;
+#endif
     const u32 cand = chunk_candidate(v, d, id, piv, chunk);
     const u64 alive0 = __ballot(cand != NONE32);
     u64 alive = alive0;
-    const u64 b = b0 + seg * LIGHT_SEG;
-    const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
     LSTAT_T0;
-    // The dependent's smallest light group after the pivot first, lanes over candidates: it kills most doomed
-    // candidates with one (often LDS-staged) search each before the group-parallel windows below.
-    const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
     // pass A (prefilter): a chunk of a dependent of several chunks with few candidates left after the filters and the
     // second pivot is not verified here; its survivors go out tagged (item seg 0) and pass B verifies them compacted
     const bool multi = v.prefilter && itemoff[d + 1] - itemoff[d] > nseg;
@@ -1660,27 +1687,25 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // independent gathers per level, so the serial chain is three round trips per segment, not per 64 groups.
     for (u64 s0 = b; s0 < e && alive; s0 += (u64)LIGHT_IT * RDF_WAVE) {
         LSTAT_TIC();
-        u32 gg[LIGHT_IT];
-        u64 gbv[LIGHT_IT];
-        u32 gszv[LIGHT_IT];
-        const u32* gdr[LIGHT_IT];
+        if (!pf || s0 != b) {  // the first window's metadata was prefetched
 #pragma unroll
-        for (int it = 0; it < LIGHT_IT; ++it) {
-            const u64 j = s0 + (u64)it * RDF_WAVE + lane;
-            gg[it] = j < e ? v.dgrp[j] : NONE32;
-        }
+            for (int it = 0; it < LIGHT_IT; ++it) {
+                const u64 j = s0 + (u64)it * RDF_WAVE + lane;
+                gg[it] = j < e ? v.dgrp[j] : NONE32;
+            }
 #pragma unroll
-        for (int it = 0; it < LIGHT_IT; ++it)
-            if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY
+            for (int it = 0; it < LIGHT_IT; ++it)
+                if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY
 #pragma unroll
-        for (int it = 0; it < LIGHT_IT; ++it) {
-            gbv[it] = 0;
-            gszv[it] = 0;
-            gdr[it] = nullptr;
-            if (gg[it] != NONE32) {
-                gbv[it] = v.goff[gg[it]];
-                gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
-                gdr[it] = dense_row(v, gg[it]);
+            for (int it = 0; it < LIGHT_IT; ++it) {
+                gbv[it] = 0;
+                gszv[it] = 0;
+                gdr[it] = nullptr;
+                if (gg[it] != NONE32) {
+                    gbv[it] = v.goff[gg[it]];
+                    gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
+                    gdr[it] = dense_row(v, gg[it]);
+                }
             }
         }
 #ifdef RDF_LIGHT_STATS
