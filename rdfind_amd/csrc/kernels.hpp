@@ -27,6 +27,17 @@ static constexpr int LIGHT_IT = RDF_LIGHT_IT;  // groups per lane whose metadata
 static constexpr int SIG_W = RDF_SIG_W;
 static constexpr int SIG_LOG = SIG_W == 16 ? 10 : SIG_W == 8 ? 9 : SIG_W == 4 ? 8 : SIG_W == 2 ? 7 : 6;
 static_assert((1 << (SIG_LOG - 6)) == SIG_W, "SIG_W must be 1, 2, 4, 8 or 16");
+// Light groups checked one at a time (lanes over candidates) after the second pivot and before the windows: the
+// pivot pass stores PIV_EXTRA of them per dependent (the next smallest), the plain light variant checks v.npx of them.
+// One on the plain variant's inputs, all four on the high-occupancy ones (large groups, long items: c4), whose pivot
+// pass keeps them; measured in profiles/r04_light_ab_pivots.log (c4 at 0.4 light 157.5 -> 121.3 ms with one, 98.9 with
+// four; c3 full 29.7 -> 27.2 with one but 31.5 with four; c2, which runs the staging variant, none)
+static constexpr int PIV_EXTRA = 4;
+static constexpr int PIV_EXTRA_PLAIN = 1;
+// the pivot pass keeps PIV_EXTRA (else PIV_EXTRA_PLAIN) from this weighted mean light group up on inputs with at
+// least PIVX_GPC groups per capture (the light variant's choice comes later; these predict it: c4 45-51, c3 15)
+static constexpr u64 PIVX_WMEAN = 2048;
+static constexpr u64 PIVX_GPC = 32;
 static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many groups take the packed light path
 #ifndef RDF_PACK_MAXG2
 #define RDF_PACK_MAXG2 512
@@ -138,6 +149,8 @@ struct CindView {
     const u64* sig;       // light-group signature of each capture, SIG_W words (null: no signature test)
     const u32* ginfo;     // group -> member count | GINFO_HEAVY (k_group_info)
     const u32* piv2;      // dependent -> its smallest light group other than the pivot (NONE32: none / not computed)
+    const u32* pivx;      // ... the next smallest, [d * PIV_EXTRA + k] (k_light plain only; NONE32: none)
+    int npx;              // how many of them k_light checks (<= PIV_EXTRA)
     const u32* gdrow;     // group -> row of its exact member bitmap (dense light groups), NONE32 (null: no bitmaps)
     const u32* dbits;     // dense-group bitmaps: row r at dbits + r * dwords, bit x set iff capture x is a member
     u64 dwords;

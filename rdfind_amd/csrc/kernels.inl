@@ -926,13 +926,42 @@ __device__ inline u32 second_pivot(u64 best, u64 l1, u64 l2) {
     const u64 k = (u32)l1 == (u32)best ? l2 : l1;
     return k == ~0ull ? NONE32 : (u32)k;
 }
+// the NP smallest light keys l[0..NP) of a dependent (ascending; distinct: one entry per group).  NP = EX + 2: the
+// pivot may be l[0], then the second pivot, then EX extra pivots
+template <int NP>
+__device__ inline void smallest_k(u64 (&l)[NP], u64 key) {
+    if (key >= l[NP - 1]) return;
+    l[NP - 1] = key;
+#pragma unroll
+    for (int i = NP - 1; i > 0; --i)
+        if (l[i] < l[i - 1]) {
+            const u64 t = l[i - 1];
+            l[i - 1] = l[i];
+            l[i] = t;
+        }
+}
+// the light groups after the second pivot: pivx[d * PIV_EXTRA + k] (NONE32 where there is none / k >= EX)
+template <int NP>
+__device__ inline void extra_pivots(u64 best, const u64 (&l)[NP], u32* pivx, u64 d) {
+    const int s = (u32)l[0] == (u32)best ? 2 : 1;  // skip the pivot (if light) and the second pivot
+#pragma unroll
+    for (int k = 0; k < PIV_EXTRA; ++k) {
+        const u64 x = s + k < NP ? l[s + k] : ~0ull;
+        pivx[d * PIV_EXTRA + k] = x == ~0ull ? NONE32 : (u32)x;
+    }
+}
 
+template <int EX>
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp_tag, u64* best_out, u32* nlight_out,
-                                                           u64* sig, u32* piv2) {
+                                                           u64* sig, u32* piv2, u32* pivx) {
+    constexpr int NPIV = EX + 2;
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = v.doff[d], e = v.doff[d + 1];
         if (e - b > PIVOT_SHORT) continue;
-        u64 best = ~0ull, l1 = ~0ull, l2 = ~0ull;  // smallest group; two smallest light groups
+        u64 best = ~0ull;  // smallest group; the NPIV smallest light groups
+        u64 l[NPIV];
+#pragma unroll
+        for (int k = 0; k < NPIV; ++k) l[k] = ~0ull;
         u32 nlight = 0;
         u64 sg[SIG_W] = {};
         for (u64 j = b; j < e; ++j) {
@@ -944,23 +973,25 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
             nlight += light;
             if (light) {
                 sig_add(sg, g);
-                l2 = key < l2 ? (key < l1 ? l1 : key) : l2;
-                l1 = key < l1 ? key : l1;
+                smallest_k(l, key);
             }
             const u32 tagged = light ? g : (g | DGRP_HEAVY);
             if (tagged != raw) dgrp_tag[j] = tagged;  // in place: light entries stay as they are (no rewrite)
         }
         best_out[d] = best;
         nlight_out[d] = nlight;
-        if (piv2) piv2[d] = second_pivot(best, l1, l2);
+        if (piv2) piv2[d] = second_pivot(best, l[0], l[1]);
+        if (pivx) extra_pivots(best, l, pivx, d);
         if (sig)
 #pragma unroll
             for (int k = 0; k < SIG_W; ++k) sig[d * SIG_W + k] = sg[k];
     }
 }
 
+template <int EX>
 __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, const u64* __restrict__ segoff, u64 W,
-                                        u64* best_out, u32* nlight_out, u64* sig, u32* piv2) {
+                                        u64* best_out, u32* nlight_out, u64* sig, u32* piv2, u32* pivx) {
+    constexpr int NPIV = EX + 2;
     const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
     if (w >= W) return;
     const int lane = lane_id();
@@ -968,7 +999,10 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
     const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
     const u64 b = b0 + (w - segoff[d]) * PIVOT_SEG;
     const u64 e = b + PIVOT_SEG < e0 ? b + PIVOT_SEG : e0;
-    u64 best = ~0ull, l1 = ~0ull, l2 = ~0ull;  // (size << 32 | group): smallest; two smallest light
+    u64 best = ~0ull;  // (size << 32 | group): smallest; the NPIV smallest light
+    u64 l[NPIV];
+#pragma unroll
+    for (int k = 0; k < NPIV; ++k) l[k] = ~0ull;
     u32 nlight = 0;
     u64 sg[SIG_W] = {};
     for (u64 j = b + lane; j < e; j += RDF_WAVE) {
@@ -980,8 +1014,7 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
         nlight += light;
         if (light) {
             sig_add(sg, g);
-            l2 = key < l2 ? (key < l1 ? l1 : key) : l2;
-            l1 = key < l1 ? key : l1;
+            smallest_k(l, key);
         }
         const u32 tagged = light ? g : (g | DGRP_HEAVY);
         if (tagged != raw) dgrp_tag[j] = tagged;
@@ -990,10 +1023,11 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
     for (int off = 32; off >= 1; off >>= 1) {
         u64 o = __shfl_xor(best, off, RDF_WAVE);
         best = o < best ? o : best;
-        const u64 o1 = __shfl_xor(l1, off, RDF_WAVE), o2 = __shfl_xor(l2, off, RDF_WAVE);
-        const u64 hi = l1 < o1 ? o1 : l1, lo2 = l2 < o2 ? l2 : o2;
-        l1 = l1 < o1 ? l1 : o1;
-        l2 = hi < lo2 ? hi : lo2;
+        u64 ol[NPIV];
+#pragma unroll
+        for (int k = 0; k < NPIV; ++k) ol[k] = __shfl_xor(l[k], off, RDF_WAVE);
+#pragma unroll
+        for (int k = 0; k < NPIV; ++k) smallest_k(l, ol[k]);  // the lanes' keys are distinct (one entry per group)
 #pragma unroll
         for (int k = 0; k < SIG_W; ++k) sg[k] |= __shfl_xor(sg[k], off, RDF_WAVE);
     }
@@ -1003,7 +1037,8 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
         if (single) {
             best_out[d] = best;
             nlight_out[d] = nlight;
-            if (piv2) piv2[d] = second_pivot(best, l1, l2);  // multi-segment dependents keep NONE32
+            if (piv2) piv2[d] = second_pivot(best, l[0], l[1]);  // multi-segment dependents keep NONE32
+            if (pivx) extra_pivots(best, l, pivx, d);
         } else {
             atomicMin(&best_out[d], best);
             atomicAdd(&nlight_out[d], nlight);
@@ -1017,11 +1052,12 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
         else if (x) atomicOr((unsigned long long*)&sig[(u64)d * SIG_W + lane], (unsigned long long)x);
     }
 }
+template <int EX>
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_seg(u64 nvblk, CindView v, u32* dgrp_tag,
                                                          const u64* __restrict__ segoff, u64 W, u64* best_out,
-                                                         u32* nlight_out, u64* sig, u32* piv2) {
+                                                         u32* nlight_out, u64* sig, u32* piv2, u32* pivx) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_pivot_seg_body(vb, v, dgrp_tag, segoff, W, best_out, nlight_out, sig, piv2);
+        k_pivot_seg_body<EX>(vb, v, dgrp_tag, segoff, W, best_out, nlight_out, sig, piv2, pivx);
     }
 }
 
@@ -1608,9 +1644,6 @@ __device__ inline bool light_sweep(const CindView& v, const u32* gm, u64 gsz, u3
 // light dependents: a work item is (dependent, chunk of 64 pivot candidates, segment of LIGHT_SEG of the
 // dependent's groups).  Single-segment dependents emit their explicit (dep << 32 | ref) pairs directly;
 // multi-segment ones publish the candidates they kill with atomicOr, and the last segment to finish emits.
-#ifndef RDF_LIGHT_PREFETCH
-#define RDF_LIGHT_PREFETCH 0
-#endif
 template <bool STAGE>
 __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
@@ -1632,33 +1665,18 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     const CapInfo id = v.info[d];
     const u64 b = b0 + seg * LIGHT_SEG;
     const u64 e = b + LIGHT_SEG < e0 ? b + LIGHT_SEG : e0;
-    // The dependent's smallest light group after the pivot is checked first (below).  It and the first window's group
-    // metadata do not depend on the candidates, so with RDF_LIGHT_PREFETCH their loads are issued before the
-    // candidate filter's and overlap its round trips (a 1-window item's serial chain: 5 round trips instead of 7).
+    // The dependent's smallest light groups after the pivot first, lanes over candidates: they kill most doomed
+    // candidates with one (often LDS-staged) search each before the group-parallel windows below.  (Issuing the first
+    // window's metadata loads before the candidate filter's was measured: c2 -0.8 %, c4 +19 %: the items whose
+    // candidates all fail the filter paid for loads they never use.)
     const u32 p2 = v.piv2 ? v.piv2[d] : NONE32;
+    // the extra pivots (plain variant only: the staging variant's inputs, c2, lose with them); read in a rolled loop
+    // below, not held in registers (four unrolled checks cost the plain variant an occupancy step: 130 VGPRs)
+    const u32* pxs = !STAGE && v.pivx && v.npx ? v.pivx + (u64)d * PIV_EXTRA : nullptr;
     u32 gg[LIGHT_IT];
     u64 gbv[LIGHT_IT];
     u32 gszv[LIGHT_IT];
     const u32* gdr[LIGHT_IT];
-#if RDF_LIGHT_PREFETCH
-    const bool pf = true;
-#pragma unroll
-    for (int it = 0; it < LIGHT_IT; ++it) {
-        const u64 j = b + (u64)it * RDF_WAVE + lane;
-        gg[it] = j < e ? v.dgrp[j] : NONE32;
-        if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY
-        gbv[it] = 0;
-        gszv[it] = 0;
-        gdr[it] = nullptr;
-        if (gg[it] != NONE32) {
-            gbv[it] = v.goff[gg[it]];
-            gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
-            gdr[it] = dense_row(v, gg[it]);
-        }
-    }
-#else
-    const bool pf = false;
-#endif
     const u32 cand = chunk_candidate(v, d, id, piv, chunk);
     const u64 alive0 = __ballot(cand != NONE32);
     u64 alive = alive0;
@@ -1671,6 +1689,18 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         const u64 gb2 = v.goff[p2];
         alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
                             dense_row(v, p2));
+    }
+    // the next smallest light groups too: the candidates that survive the second pivot mostly die in the first
+    // window's searches (c3: half of the light cycles), one targeted check each (lanes over candidates) before it
+    if (pxs && !v.p2done) {
+#pragma unroll 1
+        for (int k = 0; k < v.npx && alive; ++k) {
+            const u32 pk = pxs[k];
+            if (pk == NONE32) break;  // ascending: no more light groups
+            const u64 gb3 = v.goff[pk];
+            alive = check_group(v, gb3, (u32)(v.goff[pk + 1] - gb3), cand, alive, s_light[threadIdx.x / RDF_WAVE],
+                                dense_row(v, pk));
+        }
     }
     LSTAT_TOC(0);
     if (multi && __popcll(alive) <= LIGHT_PRE_MAX) {  // every segment item of the chunk reaches the same decision
@@ -1687,25 +1717,24 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // independent gathers per level, so the serial chain is three round trips per segment, not per 64 groups.
     for (u64 s0 = b; s0 < e && alive; s0 += (u64)LIGHT_IT * RDF_WAVE) {
         LSTAT_TIC();
-        if (!pf || s0 != b) {  // the first window's metadata was prefetched
 #pragma unroll
-            for (int it = 0; it < LIGHT_IT; ++it) {
-                const u64 j = s0 + (u64)it * RDF_WAVE + lane;
-                gg[it] = j < e ? v.dgrp[j] : NONE32;
-            }
+        for (int it = 0; it < LIGHT_IT; ++it) {
+            const u64 j = s0 + (u64)it * RDF_WAVE + lane;
+            gg[it] = j < e ? v.dgrp[j] : NONE32;
+        }
 #pragma unroll
-            for (int it = 0; it < LIGHT_IT; ++it)
-                if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY)) gg[it] = NONE32;  // NONE32 carries DGRP_HEAVY
+        for (int it = 0; it < LIGHT_IT; ++it)
+            if (gg[it] == piv || gg[it] == p2 || (gg[it] & DGRP_HEAVY))  // the extra pivots stay (their re-check is
+                gg[it] = NONE32;  // one group of a window); NONE32 carries DGRP_HEAVY
 #pragma unroll
-            for (int it = 0; it < LIGHT_IT; ++it) {
-                gbv[it] = 0;
-                gszv[it] = 0;
-                gdr[it] = nullptr;
-                if (gg[it] != NONE32) {
-                    gbv[it] = v.goff[gg[it]];
-                    gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
-                    gdr[it] = dense_row(v, gg[it]);
-                }
+        for (int it = 0; it < LIGHT_IT; ++it) {
+            gbv[it] = 0;
+            gszv[it] = 0;
+            gdr[it] = nullptr;
+            if (gg[it] != NONE32) {
+                gbv[it] = v.goff[gg[it]];
+                gszv[it] = (u32)(v.goff[gg[it] + 1] - gbv[it]);
+                gdr[it] = dense_row(v, gg[it]);
             }
         }
 #ifdef RDF_LIGHT_STATS

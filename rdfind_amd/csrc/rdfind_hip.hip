@@ -86,6 +86,10 @@ struct rdf_ctx {
     bool light_hiocc = false;  // k_light_plain_hi: the plain variant at 6 waves per SIMD (LIGHT_HIOCC_*)
     u64 light_wmean = 0;       // member-weighted mean light group size of the run (k_group_info sums)
     DevBuf piv2;   // dependent -> second pivot (smallest light group after the pivot)
+    DevBuf pivx;   // dependent -> the next PIV_EXTRA light groups after the second pivot (k_light plain only)
+    bool pivx_on = false;
+    int pivx_kept = 0;  // extra pivots the pivot pass computed this run (PIV_EXTRA_PLAIN or PIV_EXTRA)
+    int light_npx = 0;  // ... and how many k_light checks
     DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
@@ -369,7 +373,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->brkeys2, &c->bstart2, &c->ginfo, &c->gsums, &c->piv2, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->brkeys2, &c->bstart2, &c->ginfo, &c->gsums, &c->piv2, &c->pivx, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
@@ -1751,6 +1755,8 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.sig = c->sig_on ? c->lsig.as<u64>() : nullptr;
     v.ginfo = c->ginfo.as<u32>();
     v.piv2 = c->piv2_on ? c->piv2.as<u32>() : nullptr;
+    v.pivx = c->pivx_on ? c->pivx.as<u32>() : nullptr;
+    v.npx = 0;  // set per k_light launch (d_light_kernels)
     v.gdrow = c->dense_on ? c->gdrow.as<u32>() : nullptr;
     v.dbits = c->dense_on ? c->dbits.as<u32>() : nullptr;
     v.dwords = c->dwords;
@@ -1853,8 +1859,16 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         piv2 = c->piv2.as<u32>();
     }
     c->piv2_on = piv2_enabled;
+    static const bool pivx_enabled = piv2_enabled && (!getenv("RDFIND_PIVX") || atoi(getenv("RDFIND_PIVX")) != 0);
+    u32* pivx = nullptr;
+    if (pivx_enabled) {
+        ENSURE(c, pivx, std::max<u64>(C, 1) * 4 * PIV_EXTRA);
+        pivx = c->pivx.as<u32>();
+    }
+    c->pivx_on = pivx_enabled;
     tbegin(c, RDF_T_PIVOT);
     if (piv2 && C) HIP_TRY(c, hipMemsetAsync(piv2, 0xff, (u64)C * 4, st));  // multi-segment dependents: none
+    if (pivx && C) HIP_TRY(c, hipMemsetAsync(pivx, 0xff, (u64)C * 4 * PIV_EXTRA, st));
     if (sig && C) HIP_TRY(c, hipMemsetAsync(sig, 0, (u64)C * 8 * SIG_W, st));
     if (C) {
         hipLaunchKernelGGL(k_pivot_nseg, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->doff.as<u64>(), C,
@@ -1862,12 +1876,11 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->pseg.as<u32>(), c->psegoff.as<u64>(), C, c->psegoff.as<u64>() + C, st));
         HIP_TRY(c, hipMemsetAsync(c->pbest.p, 0xff, (u64)C * 8, st));
         HIP_TRY(c, hipMemsetAsync(c->pnl.p, 0, (u64)C * 4, st));
-        hipLaunchKernelGGL(k_pivot_short, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->dgrp.as<u32>(),
-                           c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2);
     }
     tend(c, RDF_T_PIVOT);
     u64 WS = 0;
     c->light_stage = false;
+    c->light_wmean = 0;
     if (C) {
         u64 r[3];
         TRY(read_multi(c, {{c->psegoff.as<u64>() + C, 8}, {c->gsums.as<u64>(), 8}, {c->gsums.as<u64>() + 1, 8}}, r));
@@ -1878,13 +1891,33 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         static const char* force = getenv("RDFIND_STAGE");  // A/B and test hook: 0 / 1 forces the variant
         if (force) c->light_stage = atoi(force) != 0;
     }
+    // extra pivots: all PIV_EXTRA where the high-occupancy light variant may run (large groups), one elsewhere
+    c->pivx_kept = !pivx ? 0
+                   : (!c->light_stage && c->light_wmean >= PIVX_WMEAN && G >= PIVX_GPC * (u64)C) ? PIV_EXTRA
+                                                                                                 : PIV_EXTRA_PLAIN;
     tbegin(c, RDF_T_PIVOT);
-    if (WS)
-        hipLaunchKernelGGL(k_pivot_seg, dim3(vgrid(wave_blocks(WS))), dim3(RDF_BLOCK),
-                           0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2);
+    if (C) {
+        if (c->pivx_kept == PIV_EXTRA)
+            hipLaunchKernelGGL(k_pivot_short<PIV_EXTRA>, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                               c->dgrp.as<u32>(), c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2, pivx);
+        else
+            hipLaunchKernelGGL(k_pivot_short<PIV_EXTRA_PLAIN>, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v,
+                               c->dgrp.as<u32>(), c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2, pivx);
+    }
+    if (WS) {
+        const dim3 g(vgrid(wave_blocks(WS)));
+        if (c->pivx_kept == PIV_EXTRA)
+            hipLaunchKernelGGL(k_pivot_seg<PIV_EXTRA>, g, dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WS), v, c->dgrp.as<u32>(),
+                               c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2, pivx);
+        else
+            hipLaunchKernelGGL(k_pivot_seg<PIV_EXTRA_PLAIN>, g, dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WS), v,
+                               c->dgrp.as<u32>(), c->psegoff.as<u64>(), WS, c->pbest.as<u64>(), c->pnl.as<u32>(), sig, piv2,
+                               pivx);
+    }
     tend(c, RDF_T_PIVOT);
     v.sig = sig;  // the candidate passes of this run test the signatures
     v.piv2 = piv2;
+    v.pivx = pivx;
     return RDF_OK;
 }
 
@@ -1905,9 +1938,13 @@ static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     c->light_hiocc = !c->light_stage && c->light_wmean >= LIGHT_HIOCC_AVG && v[0] >= LIGHT_HIOCC_OCT * (u64)C;
     static const char* hi = getenv("RDFIND_LIGHT_HIOCC");  // A/B and test hook: 0 / 1 forces the occupancy
     if (hi) c->light_hiocc = !c->light_stage && atoi(hi) != 0;
+    c->light_npx = std::min(c->pivx_kept, c->light_hiocc ? PIV_EXTRA : PIV_EXTRA_PLAIN);
+    static const char* npx = getenv("RDFIND_PIVX_N");  // A/B and test hook: how many extra pivots k_light checks
+    if (npx) c->light_npx = std::min(c->pivx_kept, atoi(npx));
     if (getenv("RDFIND_DEBUG_LIGHT"))
-        fprintf(stderr, "LIGHT weighted mean light group %llu, octets per capture %.1f (stage %d, hiocc %d)\n",
-                (unsigned long long)c->light_wmean, C ? (double)v[0] / C : 0.0, (int)c->light_stage, (int)c->light_hiocc);
+        fprintf(stderr, "LIGHT weighted mean light group %llu, octets per capture %.1f (stage %d, hiocc %d, extra pivots %d of %d)\n",
+                (unsigned long long)c->light_wmean, C ? (double)v[0] / C : 0.0, (int)c->light_stage, (int)c->light_hiocc,
+                c->light_npx, c->pivx_kept);
     *WP = v[1];
     *WH = v[2];
     c->heavy_candidates = v[3];
@@ -1988,14 +2025,17 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
     CindView vp = v;
     if (!c->sig_packed) vp.sig = nullptr;
     if (!c->piv2_packed) vp.piv2 = nullptr;
+    vp.pivx = nullptr;  // the packed path's dependents have few light groups: the second pivot does it there
     if (WP)
         hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,
                            slots.as<u64>(), counts.as<u32>());
     if (WI) {
         auto kl = c->light_stage ? k_light_stage : c->light_hiocc ? k_light_plain_hi : k_light_plain;
+        CindView vl = v;
+        vl.npx = c->light_npx;
         hipLaunchKernelGGL(kl, dim3(vgrid(wave_blocks(WI))), dim3(RDF_BLOCK),
-                           0, st, (u64)wave_blocks(WI), v, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
+                           0, st, (u64)wave_blocks(WI), vl, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
                            r.i0, WI, ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>());
     }
     if (WM)

@@ -209,20 +209,22 @@ with _lib.Context(0) as ctx:
                                  {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "2", "RDFIND_DENSE": "0"},
                                  {"RDFIND_SWEEP_F": "0"}, {"RDFIND_SWEEP_F": "1000000000"},
                                  {"RDFIND_SWEEP_F": "1000000000", "RDFIND_LIGHT2": "1", "RDFIND_DENSE": "0"},
-                                 {"RDFIND_LIGHT_HIOCC": "1"}, {"RDFIND_LIGHT_HIOCC": "0"}])
+                                 {"RDFIND_LIGHT_HIOCC": "1"}, {"RDFIND_LIGHT_HIOCC": "0"}, {"RDFIND_PIVX": "0"},
+                                 {"RDFIND_PIVX_N": "2"}])
 def test_light_variants_full_size(env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
     paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
     verify passes forced instead of one light pass, pass B group-major for every dependent or none, window range sweeps
-    never / whenever many candidates are alive, the plain variant at 6 waves per SIMD forced on / off) each reproduce
-    the c1 and c2 golden vectors (and c4 at 0.1 for the sweep, group-major and occupancy switches).  The switches are read
+    never / whenever many candidates are alive, the plain variant at 6 waves per SIMD forced on / off, no extra pivots /
+    two) each reproduce the c1 and c2 golden vectors (and c4 at 0.1 for the sweep, group-major, occupancy and pivot
+    switches).  The switches are read
     once per process, so each combination runs in its own child process."""
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     keys = ["c1@1.0/s1_clean", "c2@1.0/s1_clean"]
-    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC"} & set(env):  # the c4 shape runs these paths
+    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N"} & set(env):  # c4 runs these
         keys.append("c4@0.1/s1_clean")
     for key in keys:
         g = GOLD[key]
