@@ -165,7 +165,9 @@ struct rdf_ctx {
     // the stage boundaries do not drain the stream
     bool pend_fc = false, pend_groups = false;
     bool pend_heavy = false;
-    bool spare_fc = false, spare_groups = false;  // reclaim_spare may release these stages' scratch  // heavy threshold / count of the last group build still on the device (hist + 256, + 258)
+    bool spare_fc = false, spare_groups = false;  // reclaim_spare may release these stages' scratch
+    DevBuf ecache;                   // join ranges: each range's scanned K3 block offsets from its first emission
+    std::vector<u64> ecache_je;      // ... and its record-slot count  // heavy threshold / count of the last group build still on the device (hist + 256, + 258)
     // per kernel-family device timers (events on the context stream)
     static constexpr int kTSeg = 32;  // segments per timer (a kernel family may run in several places: the two light
                                       // passes record ~14 light segments)
@@ -373,7 +375,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
-                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->brkeys2, &c->bstart2, &c->ginfo, &c->gsums, &c->piv2, &c->pivx, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
+                      &c->pseg, &c->psegoff, &c->pbest, &c->pnl, &c->lsig, &c->brkeys2, &c->bstart2, &c->ginfo, &c->gsums, &c->piv2, &c->pivx, &c->ecache, &c->ctab, &c->cflag, &c->ccid, &c->ckeys,
                       &c->ckeys_tmp, &c->coff, &c->cmask, &c->cpiv, &c->cnch, &c->cchoff, &c->ccnt, &c->lwoff,
                       &c->clists, &c->cself, &c->cmcnt, &c->cobase, &c->ctiles, &c->ctoff, &c->pedges, &c->pedges_tmp,
                       &c->item_dep, &c->eblk, &c->lslot, &c->npk, &c->pkoff, &c->pk_dep, &c->nmch, &c->mchoff, &c->mch_dep, &c->uhist, &c->urecs, &c->usl, &c->cntg, &c->fstage, &c->bfreq, &c->boff,
@@ -1238,7 +1240,10 @@ static rdf_status g_record_bits(rdf_ctx* c) {
 // K3 emission of the selected join values (record buffers of cap_rec slots), K4 sort by (capture, join), K5 run
 // bounds (cstart), fresh-record scan (fpos) and the records' supports -> sup[ncap].  The sorted records are left in
 // c->rec_sorted; *Jout = their number.  Adds to c->J_emit and c->sort_passes_records.
-static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u32* sup, u64* Jout) {
+// Join ranges (g_build_ranges) emit every range twice with the same selection: the first emission (cache = +1 + k,
+// range k) keeps the scanned per-block offsets and the slot count, the second (cache = -1 - k) reuses them instead of
+// re-running the count pass and its scan and read-back.  cache = 0: no reuse.
+static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u32* sup, u64* Jout, int cache = 0) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
@@ -1251,18 +1256,38 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
     const u64 per = n ? (n + eg - 1) / eg : 0;
     ENSURE(c, eblk, (eg + 1ull) * 8);
+    const int slot = cache > 0 ? cache - 1 : cache < 0 ? -cache - 1 : -1;
+    const bool reuse = cache < 0 && slot < (int)c->ecache_je.size();
+    if (cache > 0) {
+        if ((int)c->ecache_je.size() <= slot) c->ecache_je.resize(slot + 1);
+        HIP_TRY(c, c->ecache.grow_keep((size_t)(slot + 1) * (eg + 1ull) * 8, st));
+    }
     if (n) {
-        hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
-                           c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
-        HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
+        if (reuse) {
+            HIP_TRY(c, hipMemcpyAsync(c->eblk.p, c->ecache.as<u64>() + (u64)slot * (eg + 1ull), eg * 8ull,
+                                      hipMemcpyDeviceToDevice, st));
+        } else {
+            hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
+                               c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
+            HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
+            if (cache > 0)
+                HIP_TRY(c, hipMemcpyAsync(c->ecache.as<u64>() + (u64)slot * (eg + 1ull), c->eblk.p, eg * 8ull,
+                                          hipMemcpyDeviceToDevice, st));
+        }
         hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
                            c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
                            (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
     }
     tend(c, RDF_T_EMIT);
-    TRY(read_scalars(c, 1));
-    const u64 Je = c->hscal[0];  // emitted record slots (repeats within an emission iteration are padding)
+    u64 Je = 0;  // emitted record slots (repeats within an emission iteration are padding)
+    if (reuse) {
+        Je = c->ecache_je[slot];
+    } else {
+        TRY(read_scalars(c, 1));
+        Je = c->hscal[0];
+        if (cache > 0) c->ecache_je[slot] = Je;
+    }
     if (Je > cap_rec) return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
     c->J_emit += Je;
     u64* keys = c->rec.as<u64>();
@@ -1463,9 +1488,11 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     ENSURE(c, rsup, std::max<u64>(ncap, 1) * 4);
     HIP_TRY(c, hipMemsetAsync(c->support.p, 0, std::max<u64>(ncap, 1) * 4, st));
     u64 Jtot = 0;
-    for (const Range& r : ranges) {
+    c->ecache_je.clear();
+    for (size_t k = 0; k < ranges.size(); ++k) {
+        const Range& r = ranges[k];
         u64 J = 0;
-        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J));
+        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
         Jtot += J;
         if (ncap)
             hipLaunchKernelGGL(k_add_u32, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->support.as<u32>(),
@@ -1497,9 +1524,10 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     HIP_TRY(c, hipMemsetAsync(c->dcur.p, 0, std::max<u64>(C, 1) * 4, st));
     // 4. groups, range by range
     u64 Jf0 = 0, G0 = 0;
-    for (const Range& r : ranges) {
+    for (size_t k = 0; k < ranges.size(); ++k) {
+        const Range& r = ranges[k];
         u64 J = 0;
-        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J));
+        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
         u64* keys = c->rec_sorted;
         tbegin(c, RDF_T_SUPPORT);
         ENSURE(c, flags, std::max<u64>(std::max<u64>(J, ncap), 1) * 4);
