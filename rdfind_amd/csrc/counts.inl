@@ -395,16 +395,9 @@ __device__ inline u64 sub_peers(u32 j, int sub) {
     return act ? peers : 0ull;
 }
 
-#ifndef RDF_B2_SPLIT_STAGE
-#define RDF_B2_SPLIT_STAGE 0
-#endif
-// RDF_B2_SPLIT_STAGE > 0: a bucket of at most that many records is read from HBM once, staged in LDS for both of its
-// passes; larger ones are read twice
-static constexpr u32 B2_SPLIT_STAGE = RDF_B2_SPLIT_STAGE;
 __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ rin, const u32* __restrict__ ghist, u32 NB,
                                                         u32 G, int bits, int sub, u64* __restrict__ rout, u32* bstart) {
     __shared__ u32 cnt[1 << B2_SUB_MAX];
-    __shared__ u64 stage[B2_SPLIT_STAGE ? B2_SPLIT_STAGE : 1];
     const u32 S = 1u << sub;
     const int lane = lane_id();
     const u64 lt = lanemask_lt();
@@ -412,9 +405,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ 
     constexpr u64 STEP = (u64)RDF_BLOCK * B2_SPLIT_R;
     for (u32 b = blockIdx.x; b < NB; b += gridDim.x) {
         const u64 start = ghist[(u64)b * G], end = ghist[(u64)(b + 1) * G];
-        const bool staged = B2_SPLIT_STAGE && end - start <= B2_SPLIT_STAGE;
-        if (staged)
-            for (u64 i = start + threadIdx.x; i < end; i += RDF_BLOCK) stage[i - start] = rin[i];
         if (threadIdx.x < S) cnt[threadIdx.x] = 0;
         __syncthreads();
         for (u64 i0 = start + wave0; i0 < end; i0 += STEP) {  // B2_SPLIT_R coalesced loads per lane in flight
@@ -422,7 +412,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ 
 #pragma unroll
             for (int k = 0; k < B2_SPLIT_R; ++k) {
                 const u64 i = i0 + (u64)k * RDF_WAVE + lane;
-                j[k] = i < end ? b2_sub(staged ? stage[i - start] : rin[i], bits, sub) : S;
+                j[k] = i < end ? b2_sub(rin[i], bits, sub) : S;
             }
 #pragma unroll
             for (int k = 0; k < B2_SPLIT_R; ++k) {
@@ -447,7 +437,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ 
 #pragma unroll
             for (int k = 0; k < B2_SPLIT_R; ++k) {
                 const u64 i = i0 + (u64)k * RDF_WAVE + lane;
-                r[k] = i < end ? (staged ? stage[i - start] : rin[i]) : 0;
+                r[k] = i < end ? rin[i] : 0;
             }
 #pragma unroll
             for (int k = 0; k < B2_SPLIT_R; ++k) {
