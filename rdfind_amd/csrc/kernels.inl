@@ -1436,6 +1436,11 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
         const u32* dr2 = dense_row(v, p2);
         ok = dr2 ? dense_has(dr2, cand) : bsearch_u32(v.gcap + v.goff[p2], v.goff[p2 + 1] - v.goff[p2], cand);
     }
+    const u32 p3 = v.pivx && v.npx ? v.pivx[(u64)d * PIV_EXTRA] : NONE32;  // ... then the next one
+    if (ok && p3 != NONE32 && !v.p2done) {
+        const u32* dr3 = dense_row(v, p3);
+        ok = dr3 ? dense_has(dr3, cand) : bsearch_u32(v.gcap + v.goff[p3], v.goff[p3 + 1] - v.goff[p3], cand);
+    }
     const u64 b = v.doff[d], e = v.doff[d + 1];
     // PACK_STEP group entries at a time: their ids, bounds and searches are independent loads (one round trip per
     // level for all of them instead of one chain per group)
@@ -1448,7 +1453,7 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
         for (int i = 0; i < PACK_STEP; ++i) gr[i] = j0 + i < e ? v.dgrp[j0 + i] : NONE32;  // heavy entries: DGRP_HEAVY
 #pragma unroll
         for (int i = 0; i < PACK_STEP; ++i) {
-            const bool lt = !(gr[i] == piv || gr[i] == p2 || (gr[i] & DGRP_HEAVY));
+            const bool lt = !(gr[i] == piv || gr[i] == p2 || gr[i] == p3 || (gr[i] & DGRP_HEAVY));
             dr[i] = lt ? dense_row(v, gr[i]) : nullptr;
             const u64 gb = lt ? v.goff[gr[i]] : 0;
             gn[i] = lt && !dr[i] ? v.goff[gr[i] + 1] - gb : 0;  // dense groups: a bitmap word instead of a search

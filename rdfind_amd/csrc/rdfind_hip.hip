@@ -2053,7 +2053,12 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
     CindView vp = v;
     if (!c->sig_packed) vp.sig = nullptr;
     if (!c->piv2_packed) vp.piv2 = nullptr;
-    vp.pivx = nullptr;  // the packed path's dependents have few light groups: the second pivot does it there
+    // the packed path checks the first extra pivot after the second one on large-group inputs (c3 full: packed + plain
+    // light 27.5 -> 26.8 ms; c2, c5 lose 1-2 %: profiles/r04_light_ab_pivx_packed.log).  RDFIND_PIVX_PACKED=0/1 forces
+    static const char* pxp = getenv("RDFIND_PIVX_PACKED");
+    const bool pivx_packed = pxp ? atoi(pxp) != 0 : !c->light_stage && c->light_wmean >= PIVX_WMEAN;
+    vp.npx = pivx_packed && c->pivx_kept ? 1 : 0;
+    if (!vp.npx) vp.pivx = nullptr;
     if (WP)
         hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
                            pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,

@@ -121,6 +121,18 @@ def exchange_device(group=None) -> torch.device:
     return torch.device("cpu")
 
 
+def _send_buffer(machine, n, dtype, device):
+    """The rank's send buffer for one collective: a view of a persistent buffer per (dtype, device), grown by half
+    again when a collective needs more (the 14 collectives of a run reuse it instead of allocating each time)."""
+    bufs = machine.__dict__.setdefault("_x_send", {})
+    key = (dtype, device.type, device.index)
+    b = bufs.get(key)
+    if b is None or b.numel() < n:
+        b = torch.empty(max(n, 1, b.numel() + b.numel() // 2 if b is not None else 0), dtype=dtype, device=device)
+        bufs[key] = b
+    return b[:n]
+
+
 def run_protocol(machine, group=None, device=None):
     """Drive a shard machine to completion.  ``machine.shard_step()`` returns an ExchangeRequest;
     ``machine.shard_export(ptr)`` fills ``count`` elements at ``ptr``; ``machine.shard_import(ptr, n)``
@@ -134,7 +146,7 @@ def run_protocol(machine, group=None, device=None):
             # this rank's exchange volume (elements x element size), kept on the machine for the bench's work counters
             machine.x_stats = {"collectives": n, "bytes_sent": sent, "bytes_received": received}
             return n
-        send = torch.empty(req.count, dtype=_dtype(req.op), device=device)
+        send = _send_buffer(machine, req.count, _dtype(req.op), device)
         machine.shard_export(send.data_ptr())
         if req.count == 0 and req.op in (_lib.X_ALLREDUCE_SUM_U32, _lib.X_ALLREDUCE_SUM_U64, _lib.X_ALLREDUCE_MIN_U64):
             machine.shard_import(send.data_ptr(), 0)  # an all-reduce has the same count on every rank: all skip it

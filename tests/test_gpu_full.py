@@ -210,7 +210,7 @@ with _lib.Context(0) as ctx:
                                  {"RDFIND_SWEEP_F": "0"}, {"RDFIND_SWEEP_F": "1000000000"},
                                  {"RDFIND_SWEEP_F": "1000000000", "RDFIND_LIGHT2": "1", "RDFIND_DENSE": "0"},
                                  {"RDFIND_LIGHT_HIOCC": "1"}, {"RDFIND_LIGHT_HIOCC": "0"}, {"RDFIND_PIVX": "0"},
-                                 {"RDFIND_PIVX_N": "2"}])
+                                 {"RDFIND_PIVX_N": "2"}, {"RDFIND_PIVX_PACKED": "1"}])
 def test_light_variants_full_size(env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
     paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
@@ -224,7 +224,8 @@ def test_light_variants_full_size(env):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     keys = ["c1@1.0/s1_clean", "c2@1.0/s1_clean"]
-    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N"} & set(env):  # c4 runs these
+    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N",
+            "RDFIND_PIVX_PACKED"} & set(env):  # c4 runs these
         keys.append("c4@0.1/s1_clean")
     for key in keys:
         g = GOLD[key]
