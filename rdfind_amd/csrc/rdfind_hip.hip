@@ -21,7 +21,6 @@ using namespace rdf;
 struct rdf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t xstream = nullptr;  // a second stream for the hand-over copies (two copy engines over the host link)
     std::string err;
     Workspace ws;
 
@@ -446,7 +445,6 @@ void rdf_ctx_destroy(rdf_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->tev)
         if (e) (void)hipEventDestroy(e);
-    if (c->xstream) (void)hipStreamDestroy(c->xstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -3970,17 +3968,9 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    // the result is complete (rdf_discover_cinds ended with a stream wait), so the parts go out on two streams at once:
-    // the first half of the refs on the context stream, the rest of the parts on the second
-    if (!c->xstream) HIP_TRY(c, hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-    hipStream_t st2 = c->xstream;
     const u64 nrefs = c->n_out - c->n_class_out, R = c->n_runs_explicit;
     const u64 nmem = c->n_class_out ? c->n_class_members : 0;
-    const u64 half = nrefs / 2;
-    if (refs && half) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr, half * 4, hipMemcpyDeviceToHost, st));
-    if (refs && nrefs > half)
-        HIP_TRY(c, hipMemcpyAsync(refs + half, c->out_ptr + half, (nrefs - half) * 4, hipMemcpyDeviceToHost, st2));
-    st = st2;  // the remaining parts
+    if (refs && nrefs) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr, nrefs * 4, hipMemcpyDeviceToHost, st));
     if (runoff) HIP_TRY(c, hipMemcpyAsync(runoff, c->runoff.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
     if (rundep && R) HIP_TRY(c, hipMemcpyAsync(rundep, c->rundep.p, R * 4, hipMemcpyDeviceToHost, st));
     if (c->n_lists) {
@@ -3993,8 +3983,7 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     if (members && nmem) HIP_TRY(c, hipMemcpyAsync(members, c->ckeys.p, nmem * 8, hipMemcpyDeviceToHost, st));
     if (capture_ids && c->C) HIP_TRY(c, hipMemcpyAsync(capture_ids, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
     if (supports && c->C) HIP_TRY(c, hipMemcpyAsync(supports, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st2));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipStreamSynchronize(st));
     return RDF_OK;
 }
 
