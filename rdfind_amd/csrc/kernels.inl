@@ -1228,16 +1228,22 @@ __device__ inline const u32* dense_row(const CindView& v, u32 g) {
 __device__ inline bool dense_has(const u32* row, u32 x) { return (row[x >> 5] >> (x & 31)) & 1u; }
 
 // dense light groups: flags (light, >= dmin members) for the row numbering scan
-__global__ __launch_bounds__(RDF_BLOCK) void k_dense_flags(const u32* __restrict__ ginfo, u64 G, u32 dmin, u32* flags) {
+// dmin = dmin_stage where the light pass will take the staging variant (member-weighted mean light group <=
+// LIGHT_STAGE_AVG, from gsums = (sum n, sum n^2) of k_group_info: the same test the host makes after its read-back),
+// else dmin_other
+__global__ __launch_bounds__(RDF_BLOCK) void k_dense_flags(const u32* __restrict__ ginfo, u64 G, const u64* __restrict__ gsums,
+                                                           u32 dmin_stage, u32 dmin_other, u32* flags) {
+    const u32 dmin = gsums[1] <= (u64)LIGHT_STAGE_AVG * gsums[0] ? dmin_stage : dmin_other;
     for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
         const u32 gi = ginfo[g];
         flags[g] = !(gi & GINFO_HEAVY) && gi >= dmin ? 1u : 0u;
     }
 }
+// rows >= cap (past the bitmap budget) stay member lists
 __global__ __launch_bounds__(RDF_BLOCK) void k_dense_rows(const u32* __restrict__ flags, const u32* __restrict__ pos, u64 G,
-                                                          u32* gdrow, u32* dlist) {
+                                                          u32 cap, u32* gdrow, u32* dlist) {
     for (u64 g = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; g < G; g += (u64)gridDim.x * RDF_BLOCK) {
-        if (flags[g]) {
+        if (flags[g] && pos[g] < cap) {
             gdrow[g] = pos[g];
             dlist[pos[g]] = (u32)g;
         } else {

@@ -93,7 +93,8 @@ struct rdf_ctx {
     DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
-    int dense_div = 32;                   // RDFIND_DENSE (0: no bitmaps)
+    int dense_div = -1;                   // RDFIND_DENSE (0: no bitmaps; -1: by input, d_dense_flags)
+    bool dense_flagged = false;           // d_dense_flags numbered rows this run (d_dense_build fills them)
     u64 dense_min = LIGHT_DENSE_MIN;      // RDFIND_DENSE_MIN (test hook: bitmaps for small groups too)
     bool sig_on = false;  // lsig holds this run's signatures (RDFIND_SIG=0 turns the filter off)
     bool sig_packed = false;  // the packed light path tests them too (RDFIND_SIG=1; default 2: k_light only)
@@ -1795,34 +1796,63 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     return v;
 }
 
-// exact member bitmaps of the dense light groups (>= C / RDFIND_DENSE members, default 32: a row of C bits is no
-// larger than the member list; 0 turns them off).  Rows are numbered in group order; no host round trip: the row
-// count stays on the device and the bitmap is sized for the most rows the member total allows.
-static rdf_status d_dense_bitmaps(rdf_ctx* c, CindView& v) {
+// exact member bitmaps of the dense light groups: light groups of >= C / div members get a row of C bits.  div
+// (RDFIND_DENSE) defaults to DENSE_DIV_STAGE where the staging light variant runs (small groups, c2), else to
+// DENSE_DIV_MANY for inputs with many groups per capture (G >= PIVX_GPC * C: c4, whose windows lose the range sweep to
+// dense groups) and DENSE_DIV_FEW otherwise (c3: searches of ~5k-member groups become one bitmap word),
+// profiles/r04_dense_ab.log, profiles/r04_xcd_dense_ab.log; 0 turns them off.  Two steps around the pivot pass's one read-back:
+// d_dense_flags numbers the rows on the device, d_dense_build (after the read, which carries the row count) sizes the
+// bitmap for the rows that exist, capped at DENSE_BYTES (rows past the cap stay member lists), and fills it.
+static rdf_status d_dense_flags(rdf_ctx* c) {
     hipStream_t st = c->stream;
-    const int div = c->dense_div;
     const u64 G = c->G, C = c->C;
     c->dense_on = false;
-    v.gdrow = nullptr;
-    v.dbits = nullptr;
-    if (div <= 0 || !G || !C) return RDF_OK;
-    const u64 dmin = std::max<u64>((C + div - 1) / div, c->dense_min);
-    const u64 rows_max = std::min<u64>(G, c->Jf / dmin);
-    if (!rows_max) return RDF_OK;
-    const u64 dwords = ((C + 31) / 32 + 31) & ~31ull;  // rows start on 128-B lines
+    c->dense_flagged = false;
+    // RDFIND_DENSE=<div> sets one divisor for every input (0: no bitmaps)
+    const int div_stage = c->dense_div >= 0 ? c->dense_div : DENSE_DIV_STAGE;
+    const int div_other = c->dense_div >= 0 ? c->dense_div : (G >= PIVX_GPC * C ? DENSE_DIV_MANY : DENSE_DIV_FEW);
+    if (div_stage <= 0 || !G || !C) return RDF_OK;
+    auto dmin_of = [&](int div) {
+        return (u32)std::min<u64>(std::max<u64>((C + div - 1) / div, c->dense_min), 0x7fffffffu);
+    };
     tbegin(c, RDF_T_LIGHT);
     ENSURE(c, gflag, G * 4);
     ENSURE(c, gexcl, (G + 1) * 4);
     ENSURE(c, gdrow, G * 4);
-    ENSURE(c, dlist, rows_max * 4);
-    ENSURE(c, dbits, rows_max * dwords * 4);
     hipLaunchKernelGGL(k_dense_flags, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ginfo.as<u32>(), G,
-                       (u32)std::min<u64>(dmin, 0x7fffffffu), c->gflag.as<u32>());
+                       c->gsums.as<u64>(), dmin_of(div_stage), dmin_of(div_other), c->gflag.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), G, c->gexcl.as<u32>() + G, st));
+    tend(c, RDF_T_LIGHT);
+    c->dense_flagged = true;
+    return RDF_OK;
+}
+
+static rdf_status d_dense_build(rdf_ctx* c, CindView& v, u64 nrows) {
+    hipStream_t st = c->stream;
+    v.gdrow = nullptr;
+    v.dbits = nullptr;
+    if (!c->dense_flagged || !nrows) return RDF_OK;
+    const u64 G = c->G, C = c->C;
+    const u64 dwords = ((C + 31) / 32 + 31) & ~31ull;  // rows start on 128-B lines
+    const u64 budget = getenv("RDFIND_DENSE_BYTES") ? (u64)atoll(getenv("RDFIND_DENSE_BYTES")) : DENSE_BYTES;
+    const u64 rows = std::min<u64>(nrows, budget / (dwords * 4));
+    if (getenv("RDFIND_DEBUG_LIGHT"))
+        fprintf(stderr, "dense: C %llu G %llu rows %llu of %llu, %.1f MB\n", (unsigned long long)C, (unsigned long long)G,
+                (unsigned long long)rows, (unsigned long long)nrows, rows * dwords * 4 / 1e6);
+    if (!rows) return RDF_OK;
+    ENSURE(c, dlist, rows * 4);
+    // the bitmaps only speed the light pass up: without the memory for them the member lists serve
+    const rdf_status sb = ensure_buf(c, &c->dbits, rows * dwords * 4, "allocating dbits");
+    if (sb == RDF_ERR_OOM) {
+        c->err.clear();
+        return RDF_OK;
+    }
+    TRY(sb);
+    tbegin(c, RDF_T_LIGHT);
     hipLaunchKernelGGL(k_dense_rows, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gflag.as<u32>(),
-                       c->gexcl.as<u32>(), G, c->gdrow.as<u32>(), c->dlist.as<u32>());
-    hipLaunchKernelGGL(k_dense_build, dim3((unsigned)std::min<u64>(rows_max, 4096)), dim3(RDF_BLOCK), 0, st,
-                       c->dlist.as<u32>(), c->gexcl.as<u32>() + G, rows_max, c->goff.as<u64>(), c->gcap.as<u32>(),
+                       c->gexcl.as<u32>(), G, (u32)rows, c->gdrow.as<u32>(), c->dlist.as<u32>());
+    hipLaunchKernelGGL(k_dense_build, dim3((unsigned)std::min<u64>(rows, 4096)), dim3(RDF_BLOCK), 0, st,
+                       c->dlist.as<u32>(), c->gexcl.as<u32>() + G, rows, c->goff.as<u64>(), c->gcap.as<u32>(),
                        dwords, c->dbits.as<u32>());
     tend(c, RDF_T_LIGHT);
     c->dense_on = true;
@@ -1877,7 +1907,7 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
         hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gi_grid, c->gsums.as<u64>());
     }
     tend(c, RDF_T_PIVOT);
-    TRY(d_dense_bitmaps(c, v));
+    TRY(d_dense_flags(c));
     static const int piv2_mode = getenv("RDFIND_PIV2") ? atoi(getenv("RDFIND_PIV2")) : 1;  // 2: k_light only
     const bool piv2_enabled = piv2_mode != 0;
     c->piv2_packed = piv2_mode != 2;
@@ -1910,8 +1940,13 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
     c->light_stage = false;
     c->light_wmean = 0;
     if (C) {
-        u64 r[3];
-        TRY(read_multi(c, {{c->psegoff.as<u64>() + C, 8}, {c->gsums.as<u64>(), 8}, {c->gsums.as<u64>() + 1, 8}}, r));
+        u64 r[4] = {0, 0, 0, 0};
+        if (c->dense_flagged)
+            TRY(read_multi(c, {{c->psegoff.as<u64>() + C, 8}, {c->gsums.as<u64>(), 8}, {c->gsums.as<u64>() + 1, 8},
+                               {c->gexcl.as<u32>() + c->G, 4}}, r));
+        else
+            TRY(read_multi(c, {{c->psegoff.as<u64>() + C, 8}, {c->gsums.as<u64>(), 8}, {c->gsums.as<u64>() + 1, 8}}, r));
+        TRY(d_dense_build(c, v, r[3]));
         WS = r[0];
         // member-weighted mean light group size sum(n^2) / sum(n): small groups -> the LDS-staging light variant
         c->light_stage = r[2] <= (u64)LIGHT_STAGE_AVG * r[1];

@@ -262,12 +262,16 @@ def test_heavy_paths_parity(monkeypatch, heavy_min):
         g.close()
 
 
-def test_dense_bitmap_paths_parity(monkeypatch):
+@pytest.mark.parametrize("budget", [None, "384"])
+def test_dense_bitmap_paths_parity(monkeypatch, budget):
     """Every light group verified through its exact member bitmap (RDFIND_DENSE / RDFIND_DENSE_MIN test hooks: the
     dense-group path of the light kernels, serial, batched, packed and second-pivot checks), in every mode, and the
-    heavy columns lowered too so that bitmaps and heavy masks mix."""
+    heavy columns lowered too so that bitmaps and heavy masks mix.  With a bitmap budget of 3 rows (RDFIND_DENSE_BYTES)
+    the first groups get bitmaps and the rest keep their member lists, mixed within one dependent."""
     monkeypatch.setenv("RDFIND_DENSE", "1000000")
     monkeypatch.setenv("RDFIND_DENSE_MIN", "1")
+    if budget:
+        monkeypatch.setenv("RDFIND_DENSE_BYTES", budget)
     for heavy_min in (64, 2):
         monkeypatch.setenv("RDFIND_HEAVY_MIN", str(heavy_min))
         g = _lib.Context(0)

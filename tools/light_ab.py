@@ -44,3 +44,6 @@ for variant in os.environ.get("RDFIND_AB_LIBS", "librdfind_hip.so").split(","):
                        timeout=900)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("AB")]
     print(variant, line[0][3:] if line else r.stderr[-2000:], flush=True)
+    for ln in r.stderr.splitlines():  # library decisions printed under RDFIND_DEBUG_LIGHT
+        if ln.startswith(("dense:", "LIGHT weighted")):
+            print("  ", ln, flush=True)
