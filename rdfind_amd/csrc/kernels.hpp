@@ -56,17 +56,17 @@ static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched toge
 #endif
 static constexpr int LIGHT_SERIAL = RDF_LIGHT_SERIAL;  // windows with at most this many light groups: lanes over candidates
 static constexpr u32 LIGHT_LDS = 512;
-// Dense light groups (at least C / div members and at least LIGHT_DENSE_MIN) also get an exact bitmap over the compact
-// capture space (C bits): a (candidate, group) test is one 4-B load instead of a ~log2(n)-level divergent search.  div
-// by input (d_dense_flags): DENSE_DIV_STAGE for the staging light variant (c2), DENSE_DIV_MANY where groups outnumber
-// captures 32-fold (c4: dense groups cost windows their range sweep), DENSE_DIV_FEW elsewhere (a row then holds up to
-// 32x the bytes of its member list); at most DENSE_BYTES of rows.  Measured light ms, divisor 32 / 128 / 1024: c3
-// 26.8 / 21.8 / 17.7, c4 at 0.05 10.8 / 7.7 / 12.0, c5 at 0.1 18.2 / 15.3 / 15.1, c2 2.60 / 2.61 / 2.63
-// (profiles/r04_dense_ab.log).
+// Dense light groups also get an exact bitmap over the compact capture space (C bits): a (candidate, group) test is one
+// 4-B load instead of a ~log2(n)-level divergent search.  Threshold (d_dense_flags): C / DENSE_DIV_STAGE members for the
+// staging light variant (c2: a row no larger than its member list), else min(C / 32, DENSE_MIN_ABS) members (a row up
+// to C / (4 DENSE_MIN_ABS) times its list); at least LIGHT_DENSE_MIN; at most DENSE_BYTES of rows and half the free
+// HBM.  Measured light ms at thresholds of C / 32 | C / 128 | C / 512 | C / 1024 members: c3 26.8 | 21.8 | 18.1 | 17.7
+// (C / 1024 = 1,452), c4 at 0.4 101 | 80.3 | 64.1 (C / 512 = 2,036) | -, c4 at 0.05 10.8 | 7.7 (1,293) | - | 12.0 (256),
+// c5 at 0.1 18.2 | 15.3 | 15.1 | 15.1 (profiles/r04_dense_ab.log, r04_dense_div_ab.log): ~2k members is near the best
+// everywhere.
 static constexpr u64 LIGHT_DENSE_MIN = 256;
 static constexpr int DENSE_DIV_STAGE = 32;
-static constexpr int DENSE_DIV_MANY = 128;
-static constexpr int DENSE_DIV_FEW = 1024;
+static constexpr u64 DENSE_MIN_ABS = 2048;
 static constexpr u64 DENSE_BYTES = 8ull << 30;
 #ifndef RDF_DENSE_SER
 #define RDF_DENSE_SER 8

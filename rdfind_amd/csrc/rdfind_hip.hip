@@ -1796,31 +1796,27 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     return v;
 }
 
-// exact member bitmaps of the dense light groups: light groups of >= C / div members get a row of C bits.  div
-// (RDFIND_DENSE) defaults to DENSE_DIV_STAGE where the staging light variant runs (small groups, c2), else to
-// DENSE_DIV_MANY for inputs with many groups per capture (G >= PIVX_GPC * C: c4, whose windows lose the range sweep to
-// dense groups) and DENSE_DIV_FEW otherwise (c3: searches of ~5k-member groups become one bitmap word),
-// profiles/r04_dense_ab.log, profiles/r04_xcd_dense_ab.log; 0 turns them off.  Two steps around the pivot pass's one read-back:
-// d_dense_flags numbers the rows on the device, d_dense_build (after the read, which carries the row count) sizes the
-// bitmap for the rows that exist, capped at DENSE_BYTES (rows past the cap stay member lists), and fills it.
+// exact member bitmaps of the dense light groups (a row of C bits each; thresholds in kernels.hpp, DENSE_MIN_ABS;
+// RDFIND_DENSE=<div> sets C / div for every input, 0 turns them off).  Two steps around the pivot pass's one
+// read-back: d_dense_flags numbers the rows on the device, d_dense_build (after the read, which carries the row count)
+// sizes the bitmap for the rows that exist, capped at DENSE_BYTES and half the free HBM (rows past the cap stay member
+// lists), and fills it.
 static rdf_status d_dense_flags(rdf_ctx* c) {
     hipStream_t st = c->stream;
     const u64 G = c->G, C = c->C;
     c->dense_on = false;
     c->dense_flagged = false;
-    // RDFIND_DENSE=<div> sets one divisor for every input (0: no bitmaps)
-    const int div_stage = c->dense_div >= 0 ? c->dense_div : DENSE_DIV_STAGE;
-    const int div_other = c->dense_div >= 0 ? c->dense_div : (G >= PIVX_GPC * C ? DENSE_DIV_MANY : DENSE_DIV_FEW);
-    if (div_stage <= 0 || !G || !C) return RDF_OK;
-    auto dmin_of = [&](int div) {
-        return (u32)std::min<u64>(std::max<u64>((C + div - 1) / div, c->dense_min), 0x7fffffffu);
-    };
+    const int div = c->dense_div >= 0 ? c->dense_div : DENSE_DIV_STAGE;  // RDFIND_DENSE: one divisor for every input
+    if (div <= 0 || !G || !C) return RDF_OK;
+    auto clampd = [&](u64 m) { return (u32)std::min<u64>(std::max<u64>(m, c->dense_min), 0x7fffffffu); };
+    const u32 dmin_stage = clampd((C + div - 1) / div);
+    const u32 dmin_other = c->dense_div >= 0 ? dmin_stage : clampd(std::min<u64>((C + 31) / 32, DENSE_MIN_ABS));
     tbegin(c, RDF_T_LIGHT);
     ENSURE(c, gflag, G * 4);
     ENSURE(c, gexcl, (G + 1) * 4);
     ENSURE(c, gdrow, G * 4);
     hipLaunchKernelGGL(k_dense_flags, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->ginfo.as<u32>(), G,
-                       c->gsums.as<u64>(), dmin_of(div_stage), dmin_of(div_other), c->gflag.as<u32>());
+                       c->gsums.as<u64>(), dmin_stage, dmin_other, c->gflag.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->gflag.as<u32>(), c->gexcl.as<u32>(), G, c->gexcl.as<u32>() + G, st));
     tend(c, RDF_T_LIGHT);
     c->dense_flagged = true;
@@ -1834,20 +1830,19 @@ static rdf_status d_dense_build(rdf_ctx* c, CindView& v, u64 nrows) {
     if (!c->dense_flagged || !nrows) return RDF_OK;
     const u64 G = c->G, C = c->C;
     const u64 dwords = ((C + 31) / 32 + 31) & ~31ull;  // rows start on 128-B lines
-    const u64 budget = getenv("RDFIND_DENSE_BYTES") ? (u64)atoll(getenv("RDFIND_DENSE_BYTES")) : DENSE_BYTES;
+    u64 budget = getenv("RDFIND_DENSE_BYTES") ? (u64)atoll(getenv("RDFIND_DENSE_BYTES")) : DENSE_BYTES;
+    size_t hfree = 0, htotal = 0;
+    if (hipMemGetInfo(&hfree, &htotal) == hipSuccess) budget = std::min<u64>(budget, std::max<u64>(c->dbits.cap, hfree / 2));
+    (void)hipGetLastError();
     const u64 rows = std::min<u64>(nrows, budget / (dwords * 4));
     if (getenv("RDFIND_DEBUG_LIGHT"))
         fprintf(stderr, "dense: C %llu G %llu rows %llu of %llu, %.1f MB\n", (unsigned long long)C, (unsigned long long)G,
                 (unsigned long long)rows, (unsigned long long)nrows, rows * dwords * 4 / 1e6);
     if (!rows) return RDF_OK;
     ENSURE(c, dlist, rows * 4);
-    // the bitmaps only speed the light pass up: without the memory for them the member lists serve
-    const rdf_status sb = ensure_buf(c, &c->dbits, rows * dwords * 4, "allocating dbits");
-    if (sb == RDF_ERR_OOM) {
-        c->err.clear();
-        return RDF_OK;
-    }
-    TRY(sb);
+    // the bitmaps only speed the light pass up: without the memory for them the member lists serve (no reclaim of the
+    // spare scratch for them either: the next run would allocate that again)
+    if (c->dbits.ensure(rows * dwords * 4) != hipSuccess) return RDF_OK;
     tbegin(c, RDF_T_LIGHT);
     hipLaunchKernelGGL(k_dense_rows, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gflag.as<u32>(),
                        c->gexcl.as<u32>(), G, (u32)rows, c->gdrow.as<u32>(), c->dlist.as<u32>());
