@@ -194,6 +194,87 @@ def launch_ranks(nranks, argv):
     return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
 
 
+def per_rank_balance(dist, world, mine):
+    """Every rank's work counters (all-gathered) and max / mean over ranks per numeric quantity."""
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return {"per_rank": allr,
+            "max_over_mean": {k: round(max(r[k] for r in allr) / max(sum(r[k] for r in allr) / world, 1e-12), 3)
+                              for k in mine if all(isinstance(r.get(k), (int, float)) for r in allr)}}
+
+
+# the one-GPU c4 step this leg is compared with: round 4, profiles/r04_bcfg_c4_1.0_dense_abs.json
+C4_ONE_GPU_MS = 1616.0
+
+
+def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):
+    """BASELINE configs[3] (c4 at 10^9 triples, support 100) split over the N ranks -- strong scaling, the north-star
+    scaling config.  Each rank draws and holds only its 1/N of the rows (synth.config_slice); a rank whose join shard
+    holds >= 2^32/9 triples builds its groups in join ranges (N = 1, 2, 4).  Same step as the main leg: T_disc with every
+    rank's compact result handed to pinned host memory."""
+    from rdfind_amd import _lib, synth
+
+    scale = args.c4_scale
+    if dist is not None:
+        d, total_n = synth.config_slice("c4", scale, rank, world)
+    else:
+        d = synth.config("c4", scale)
+        total_n = d.n
+    ms = d.min_support
+    n_local = d.n
+    sink = CompactSink()
+    with _lib.Context(local_rank) as ctx:
+        ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+        del d
+        if dist is not None:
+            from rdfind_amd import distributed
+
+            def step():
+                distributed.run_sharded(ctx, ms, local_slice=True)
+                sink.copy(ctx)
+                return ctx.cinds
+        else:
+            def step():
+                cs = ctx.run(ms)
+                sink.copy(ctx)
+                return cs
+        for _ in range(args.c4_warmup):
+            step()
+        ctx.sync()
+        barrier()
+        kt_sum = {}
+        t0 = time.perf_counter()
+        for _ in range(args.c4_steps):
+            cs = step()
+            for k, v in ctx.kernel_times().items():
+                kt_sum[k] = kt_sum.get(k, 0.0) + v
+        ctx.sync()
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        steps = max(args.c4_steps, 1)
+        gs = ctx.groups
+        kt = {k: v / steps for k, v in kt_sum.items()}
+        mine = {"triples": n_local, "records": gs["n_records"], "join_ranges": gs.get("n_join_ranges", 1),
+                "groups": gs["n_groups"], "light_chunks": cs["n_light_chunks"], "explicit_raw": cs["n_explicit_raw"],
+                "cinds": cs["n_cinds"], "light_ms": round(kt.get("light", 0.0), 3),
+                "kernel_ms": round(sum(kt.values()), 3), "hbm_held_gib": round(ctx.device_bytes() / 2**30, 1),
+                **{k: v for k, v in (getattr(ctx, "x_stats", None) or {}).items() if k in ("bytes_sent", "bytes_received")}}
+    total_cinds = cs["n_cinds"]
+    bal = None
+    if dist is not None:
+        bal = per_rank_balance(dist, world, mine)
+        total_cinds = sum(r["cinds"] for r in bal["per_rank"])
+    ms_step = elapsed * 1000.0 / steps
+    return {"workload": f"c4 (Freebase-shaped) scale {scale}: {total_n} triples split over {world} GPU(s), support {ms}, "
+                        "strategy 1 --use-fis --clean-implied",
+            "scaling": "strong", "n_gpus": world, "steps": args.c4_steps, "warmup": args.c4_warmup,
+            "ms_per_step": round(ms_step, 3), "triples_per_s": round(total_n * steps / elapsed, 1), "cinds": total_cinds,
+            "one_gpu_ms_ref": C4_ONE_GPU_MS if scale == 1.0 else None,
+            "speedup_vs_one_gpu_ref": round(C4_ONE_GPU_MS / ms_step, 3) if scale == 1.0 else None,
+            "kernel_ms_rank0": {k: round(v, 3) for k, v in kt.items()}, "rank0": mine,
+            **({"ranks": bal} if bal else {})}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default: WORLD_SIZE or 1.  Without a "
@@ -216,6 +297,13 @@ def main():
                     "exchanges, to rehearse several ranks on one GPU)")
     ap.add_argument("--no-resident", action="store_true", help="skip the device-resident repeat of the steps")
     ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
+    ap.add_argument("--c4-strong", choices=("auto", "on", "off"), default="auto",
+                    help="also time BASELINE configs[3] (c4, Freebase-shaped, 10^9 triples, support 100) split over the "
+                         "N GPUs (strong scaling; the north-star scaling config) and report it as `c4_strong` (auto: "
+                         "when N > 1 with the default c2 workload and the nccl backend)")
+    ap.add_argument("--c4-scale", type=float, default=1.0, help="scale of the c4_strong leg (1.0 = 10^9 triples)")
+    ap.add_argument("--c4-steps", type=int, default=2)
+    ap.add_argument("--c4-warmup", type=int, default=1)
     ap.add_argument("--page-bytes", type=int, default=None,
                     help="paged discovery (rdf_discover_cinds_paged) with this working memory per page, 0 = "
                          "automatic; every page is handed over in turn.  Default: unpaged, or automatic pages when the "
@@ -442,11 +530,17 @@ def main():
                 "light_chunks": cs["n_light_chunks"], "explicit_raw": cs["n_explicit_raw"], "cinds": cs["n_cinds"],
                 "light_ms": round(kt.get("light", 0.0), 4), "kernel_ms": round(sum(kt.values()), 4),
                 **{k: v for k, v in (getattr(ctx, "x_stats", None) or {}).items() if k in ("bytes_sent", "bytes_received")}}
-        allr = [None] * world
-        dist.all_gather_object(allr, mine)
-        ranks = {"per_rank": allr,
-                 "max_over_mean": {k: round(max(r[k] for r in allr) / max(sum(r[k] for r in allr) / world, 1e-12), 3)
-                                   for k in mine if all(isinstance(r.get(k), (int, float)) for r in allr)}}
+        ranks = per_rank_balance(dist, world, mine)
+
+    ctx.close()
+    c4 = None
+    want_c4 = args.c4_strong == "on" or (args.c4_strong == "auto" and args.config == "c2"
+                                         and (world == 1 or args.backend == "nccl"))
+    if want_c4:
+        try:
+            c4 = c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks)
+        except Exception as e:  # reported in the line; the main leg's measurement stands
+            c4 = {"error": f"{type(e).__name__}: {e}"[:500]}
 
     if rank == 0:
         per = "per GPU" if args.scaling == "weak" else "total"
@@ -471,6 +565,7 @@ def main():
                                 "note": "the same steps with the result left in HBM"},
             "roofline": roof, "count_kernels": count_roof, "families": fams,
             "cpu_baseline": cpu, "ingest": ingest, **({"ranks": ranks} if ranks else {}),
+            **({"c4_strong": c4} if c4 else {}),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
                      "join_ranges": gs.get("n_join_ranges", 1),
@@ -481,7 +576,6 @@ def main():
                      **({"exchange_rank0": getattr(ctx, "x_stats", None)} if world > 1 else {})},
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

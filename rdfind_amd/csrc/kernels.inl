@@ -662,11 +662,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_hist(const u32* __restr
                                                               const u32* __restrict__ o, u64 n, u32 V, u32 twoU,
                                                               const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                               const u32* __restrict__ lvals, u64 lmask, int proj,
-                                                              int joinbits, int jshift, u64* hist) {
+                                                              int joinbits, JoinSel own, int jshift, u64* hist) {
     __shared__ u32 lh[JH_BUCKETS];
     for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lh[k] = 0;
     __syncthreads();
-    const JoinSel all = {0u, 1u, 0u, JOIN_ALL_HI};
+    const JoinSel all = {own.rank, own.nranks, 0u, JOIN_ALL_HI};  // this rank's join values (sharded), every range
     const u64 jmask = (1ull << joinbits) - 1;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         u64 rec[9];
@@ -720,6 +720,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_dcur_add(const u64* __restrict__ 
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_add_u32(u32* a, const u32* __restrict__ b, u64 n) {
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) a[i] += b[i];
+}
+
+// out[i] = v[idx[i]] (a frequent capture's local support, sharded join ranges)
+__global__ __launch_bounds__(RDF_BLOCK) void k_gather_u32(const u32* __restrict__ v, const u32* __restrict__ idx, u64 n,
+                                                          u32* out) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) out[i] = v[idx[i]];
 }
 
 
@@ -2729,18 +2735,28 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_decode_rows(const u32* __restrict
 #ifndef RDF_HOLDER_TIEBREAK
 #define RDF_HOLDER_TIEBREAK 1
 #endif
-__device__ __host__ inline u64 holder_key(u64 size, u64 hmask, u32 d, u32 rank) {
+// Load-aware election (qbits > 0): the size enters as a log-scale bucket with qbits mantissa bits (2^qbits buckets per
+// octave), so ranks whose smallest groups are within ~2^(1/2^qbits) of each other tie and the hash spreads them.  A rank
+// whose groups are all a little smaller (it holds fewer records) then no longer wins every dependent; the holder's
+// pivot grows by at most that factor.  Members of one mask class still agree (same groups on every rank).
+__device__ __host__ inline u64 size_bucket_q(u64 size, int qbits) {
+    if (!qbits || !size) return size;
+    const int lz = 63 - __builtin_clzll(size);
+    const u64 m = lz >= qbits ? (size >> (lz - qbits)) : (size << (qbits - lz));
+    return ((u64)lz << qbits) | (m & ((1ull << qbits) - 1));
+}
+__device__ __host__ inline u64 holder_key(u64 size, u64 hmask, u32 d, u32 rank, int qbits) {
     const u64 salt = hmask ? hmask : ((u64)d | (1ull << 63));
     const u64 tie = RDF_HOLDER_TIEBREAK ? mix64(salt ^ ((u64)(rank + 1) * 0x9E3779B97F4A7C15ull)) >> 40 : 0ull;
-    return (size << 32) | (tie << 8) | rank;
+    return (size_bucket_q(size, qbits) << 32) | (tie << 8) | rank;
 }
 __device__ __host__ inline u32 holder_rank(u64 key) { return (u32)(key & 0xffu); }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_shard_best_keys(const u64* __restrict__ best, const CapInfo* __restrict__ info,
-                                                               u32 C, u32 rank, u64* out) {
+                                                               u32 C, u32 rank, int qbits, u64* out) {
     for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < C; d += (u64)gridDim.x * RDF_BLOCK) {
         const u64 b = best[d];
-        out[d] = b == ~0ull ? 0x7fffffffffffffffull : holder_key(b >> 32, info[d].hmask, (u32)d, rank);
+        out[d] = b == ~0ull ? 0x7fffffffffffffffull : holder_key(b >> 32, info[d].hmask, (u32)d, rank, qbits);
     }
 }
 

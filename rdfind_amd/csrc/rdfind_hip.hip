@@ -62,6 +62,14 @@ struct rdf_ctx {
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
     DevBuf hist, heavy_list, hbit, bcomp, bkeyc, pcnt, poff, pcur, plist;
     DevBuf jhist, rsup, offp;  // capture groups built in join-value ranges (g_build_ranges)
+    DevBuf lsup;               // sharded join ranges: this rank's supports (the all-reduce replaces c->support)
+    struct JoinRange { u32 lo, hi; u64 recs; };
+    std::vector<JoinRange> jranges;  // the current build's join ranges (pass 1 -> pass 2)
+    u64 jr_cap_rec = 1;              // records of the largest range (the range scratch's size)
+    bool sh_ranged = false;          // the sharded build of this run goes in join ranges (sh_phase14 -> sh_phase1)
+    u64 sh_m = 0;                    // sharded: triples received for this rank's join shard (wts / wtp / wto)
+    std::string test_fail_launch;    // RDFIND_TEST_FAIL_LAUNCH: a kernel launched with an invalid configuration (test hook)
+    int holder_qbits = 2;            // RDFIND_HOLDER_Q: pivot-holder election on log-size buckets (holder_key; 0: exact)
     u64 group_range_records = 0;  // RDFIND_GROUP_RANGE test hook: records per join range (0: automatic)
     u64 n_group_ranges = 1;
     u64 J = 0, Jf = 0, G = 0, J_emit = 0;  // J: distinct-within-iteration records sorted; J_emit: records emitted
@@ -289,6 +297,15 @@ static hipError_t stream_wait(hipStream_t s, int line) {
 }
 #define hipStreamSynchronize(s) stream_wait((s), __LINE__)
 
+// Host <-> device copies of a context's buffers are ordered on the context's stream and wait for it.  The context
+// stream is non-blocking, so the null stream a plain hipMemcpy runs on would not wait for kernels still queued there
+// (e.g. rdf_copy_binary_keys right after rdf_frequent_conditions, whose key sort may still be running).
+static hipError_t ctx_copy_(hipStream_t s, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, int line) {
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+    return e != hipSuccess ? e : stream_wait(s, line);
+}
+#define ctx_copy(c, dst, src, bytes, kind) ctx_copy_((c)->stream, (dst), (src), (bytes), (kind), __LINE__)
+
 // Several device scalars with ONE host round trip: a one-thread kernel gathers them into the mapped host buffer.
 struct ScalarGather {
     const void* p[8];
@@ -354,7 +371,7 @@ static rdf_status read_multi(rdf_ctx* c, std::initializer_list<std::pair<const v
 static rdf_status load_bkeys(rdf_ctx* c) {
     if (c->h_bkeys_valid) return RDF_OK;
     c->h_bkeys.resize(c->B);
-    if (c->B) HIP_TRY(c, hipMemcpy(c->h_bkeys.data(), c->bkeys.p, c->B * 8, hipMemcpyDeviceToHost));
+    if (c->B) HIP_TRY(c, ctx_copy(c, c->h_bkeys.data(), c->bkeys.p, c->B * 8, hipMemcpyDeviceToHost));
     c->h_bkeys_valid = true;
     return RDF_OK;
 }
@@ -372,7 +389,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
                       &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
                       &c->gcap, &c->gmap, &c->csup,
-                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
+                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->lsup, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
@@ -418,6 +435,8 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
         if (atoll(gr) > 0) c->group_range_records = (u64)atoll(gr);
     if (const char* dm = getenv("RDFIND_DENSE_MIN"))
         if (atoll(dm) > 0) c->dense_min = (u64)atoll(dm);
+    if (const char* hq = getenv("RDFIND_HOLDER_Q")) c->holder_qbits = std::max(0, std::min(atoi(hq), 8));
+    if (const char* tf = getenv("RDFIND_TEST_FAIL_LAUNCH")) c->test_fail_launch = tf;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -927,13 +946,18 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
     // buckets that outgrow a counting slice are split by the next hash bits (RDFIND_B2_SPLIT=0: never)
     // into sub-buckets of about 0.9 slice each (smaller ones pay the counting block's per-slice table setup for
     // nothing); decided on the actual record count, read back only when the 3n bound says it may be needed
-    static const bool split_enabled = !getenv("RDFIND_B2_SPLIT") || atoi(getenv("RDFIND_B2_SPLIT")) != 0;
+    // (RDFIND_B2_SPLIT=2: at least one split bit whatever the size, a test hook for the split path on small inputs)
+    static const int split_mode = getenv("RDFIND_B2_SPLIT") ? atoi(getenv("RDFIND_B2_SPLIT")) : 1;
+    // a failed launch would leave uhist stale for the scan and the split below: caught here, not as a fault in a
+    // consumer of garbage offsets
+    HIP_TRY(c, hipGetLastError());
     int sub = 0;
-    if (split_enabled && 3 * n > (u64)NB2 * B2_SLICE) {
+    if (split_mode && 3 * n > (u64)NB2 * B2_SLICE) {
         u32 R = 0;
         TRY(read_u32(c, c->uhist.as<u32>() + nh, &R));
         while (sub < B2_SUB_MAX && (u64)R > ((u64)NB2 << sub) * (B2_SLICE * 9 / 10)) ++sub;
     }
+    if (split_mode == 2 && n) sub = std::max(sub, 1);
     const u64* recs = c->brkeys.as<u64>();
     const u32* bstart = c->uhist.as<u32>();
     u32 NBc = NB2, Gc = G2;
@@ -942,8 +966,14 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
         Gc = 1;
         ENSURE(c, brkeys2, maxrec * 8);
         ENSURE(c, bstart2, ((u64)NBc + 1) * 4);
-        hipLaunchKernelGGL(k_b2_split, dim3(std::min<u32>(NB2, 4096)), dim3(RDF_BLOCK), 0, st, c->brkeys.as<u64>(),
+        // RDFIND_TEST_FAIL_LAUNCH=k_b2_split (test hook): launched with an invalid block size, so the launch fails
+        const unsigned sblock = c->test_fail_launch == "k_b2_split" ? 4 * 1024 : RDF_BLOCK;
+        hipLaunchKernelGGL(k_b2_split, dim3(std::min<u32>(NB2, 4096)), dim3(sblock), 0, st, c->brkeys.as<u64>(),
                            c->uhist.as<u32>(), NB2, G2, bits, sub, c->brkeys2.as<u64>(), c->bstart2.as<u32>());
+        // bstart2 (the sub-bucket starts) is consumed as record offsets by k_b2_slices and k_b2_count: a launch that
+        // did not run must stop here (the round-4 aperture violation in rdf_frequent_conditions was a count kernel
+        // reading offsets no kernel had written)
+        HIP_TRY(c, hipGetLastError());
         recs = c->brkeys2.as<u64>();
         bstart = c->bstart2.as<u32>();
     }
@@ -1169,7 +1199,7 @@ rdf_status rdf_copy_association_rules(rdf_ctx* c, rdf_assoc_rule* out, uint64_t 
     if (!c || (!out && cap)) return RDF_ERR_ARG;
     if (!c->ar_on) return fail(c, RDF_ERR_STATE, "rdf_association_rules must be called first");
     const u64 m = std::min<u64>(cap, c->n_rules);
-    if (m) HIP_TRY(c, hipMemcpy(out, c->ar_rules.p, m * sizeof(rdf_assoc_rule), hipMemcpyDeviceToHost));
+    if (m) HIP_TRY(c, ctx_copy(c, out, c->ar_rules.p, m * sizeof(rdf_assoc_rule), hipMemcpyDeviceToHost));
     if (n_copied) *n_copied = m;
     return RDF_OK;
 }
@@ -1432,17 +1462,22 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
     return RDF_OK;
 }
 
-// Capture groups of one GPU in ranges of join values, for inputs whose K3 records exceed what one sort holds (the u32
-// record offsets of K4/K5: n >= 2^32 / 9 triples; c4 at full size emits ~5.8·10^9 records) or the memory of one pass.
-// The reference has no such ceiling: Flink's sort-based groupBy("joinValue") spills (ALG/programs/RDFind.scala:339-345).
+// Capture groups in ranges of join values, for inputs whose K3 records exceed what one sort holds (the u32 record
+// offsets of K4/K5: n >= 2^32 / 9 triples; c4 at full size emits ~5.8·10^9 records) or the memory of one pass.  The
+// reference has no such ceiling: Flink's sort-based groupBy("joinValue") spills (ALG/programs/RDFind.scala:339-345).
+// Pass 1 (g_ranges_supports):
 //  1. records per join bucket (k_emit_join_hist) -> consecutive bucket ranges of at most max_range records each;
 //  2. per range: K3-K5 (g_emit_range), its supports summed into c->support (a join value's records are all in one
-//     range, so the ranges' distinct (capture, join) counts add up);
-//  3. capture compaction; doff = scan of the frequent supports (a frequent capture keeps one record per join value);
+//     range, so the ranges' distinct (capture, join) counts add up).
+// Pass 2 (g_ranges_groups):
+//  3. capture compaction; doff = scan of the frequent captures' record counts (a frequent capture keeps one record per
+//     join value: its support on one GPU, its local support `lsup` on a rank of a sharded run);
 //  4. per range again: K3-K5, the kept records -> that range's groups appended at (G0, Jf0) and its dependent ->
 //     group entries placed behind the earlier ranges' (dcur).  Ranges ascend in join value and groups are numbered in
 //     join order, so goff / gcap / gmap / dgrp are exactly the one-pass build's.
-static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
+// One GPU runs the passes back to back (g_build_ranges).  A rank of a sharded run (own = its join shard) runs pass 1
+// on the triples it received, all-reduces the supports, and runs pass 2 (sh_phase14 -> sh_phase1).
+static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel own) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
@@ -1462,13 +1497,13 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     if (n)
         hipLaunchKernelGGL(k_emit_join_hist, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V,
                            2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits,
-                           jshift, c->jhist.as<u64>());
+                           own, jshift, c->jhist.as<u64>());
     tend(c, RDF_T_EMIT);
     std::vector<u64> h(JH_BUCKETS);
     HIP_TRY(c, hipMemcpyAsync(h.data(), c->jhist.p, JH_BUCKETS * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
-    struct Range { u32 lo, hi; u64 recs; };
-    std::vector<Range> ranges;
+    std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
+    ranges.clear();
     u64 acc = 0, cap_rec = 1;
     u32 lo = 0;
     for (u32 b = 0; b < JH_BUCKETS; ++b) {
@@ -1480,9 +1515,10 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
         acc += h[b];
     }
     ranges.push_back({lo, JOIN_ALL_HI, acc});
-    for (const Range& r : ranges) cap_rec = std::max(cap_rec, r.recs);
+    for (const rdf_ctx::JoinRange& r : ranges) cap_rec = std::max(cap_rec, r.recs);
     if (cap_rec >= (1ull << 32) - 1)
         return fail(c, RDF_ERR_LIMIT, "one join bucket holds >= 2^32 capture records");
+    c->jr_cap_rec = cap_rec;
     c->n_group_ranges = ranges.size();
     // 2. supports
     ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
@@ -1491,25 +1527,46 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     u64 Jtot = 0;
     c->ecache_je.clear();
     for (size_t k = 0; k < ranges.size(); ++k) {
-        const Range& r = ranges[k];
+        const rdf_ctx::JoinRange& r = ranges[k];
         u64 J = 0;
-        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
+        TRY(g_emit_range(c, proj, JoinSel{own.rank, own.nranks, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
         Jtot += J;
         if (ncap)
             hipLaunchKernelGGL(k_add_u32, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->support.as<u32>(),
                                c->rsup.as<u32>(), ncap);
     }
-    const u64 J_emit = c->J_emit;
-    // 3. compaction; each frequent capture's dependent -> group list has support entries
+    c->J = Jtot;
+    return RDF_OK;
+}
+
+// pass 2 (above): c->support holds the global supports; local_sup (sharded: this rank's supports from pass 1) gives
+// each frequent capture's record count here, nullptr = its global support (one GPU)
+static rdf_status g_ranges_groups(rdf_ctx* c, int proj, JoinSel own, const u32* local_sup) {
+    hipStream_t st = c->stream;
+    const u32 V = c->V ? c->V : 1;
+    const u64 ncap = c->ncap;
+    const int joinbits = c->joinbits;
+    const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
+    const u64 cap_rec = c->jr_cap_rec;
+    const u64 J_emit = c->J_emit, Jtot = c->J;
+    // 3. compaction; each frequent capture's dependent -> group list has one entry per (local) join value
     tbegin(c, RDF_T_SUPPORT);
     TRY(g_compact_captures(c));
     const u32 C = c->C;
     ENSURE(c, csup, std::max<u64>(C, 1) * 4);
     ENSURE(c, doff, (C + 1ull) * 8);
+    ENSURE(c, dcur, std::max<u64>(C, 1) * 4);
     if (C)
         hipLaunchKernelGGL(k_info_support_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->info.as<CapInfo>(), C, c->csup.as<u32>());
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->csup.as<u32>(), c->doff.as<u64>(), C, c->doff.as<u64>() + C, st));
+    const u32* nrec = c->csup.as<u32>();
+    if (local_sup) {  // records per frequent capture on this rank: its local support (dcur is scratch until zeroed)
+        if (C)
+            hipLaunchKernelGGL(k_gather_u32, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, local_sup,
+                               c->fcap.as<u32>(), (u64)C, c->dcur.as<u32>());
+        nrec = c->dcur.as<u32>();
+    }
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, nrec, c->doff.as<u64>(), C, c->doff.as<u64>() + C, st));
     tend(c, RDF_T_SUPPORT);
     u64 Jf = 0;
     TRY(read_u64(c, c->doff.as<u64>() + C, &Jf));
@@ -1519,16 +1576,15 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     ENSURE(c, gcap, std::max<u64>(Jf, 1) * 4 + 16);  // + 16 B: the light pass reads whole aligned quads
     ENSURE(c, gmap, (u64)V * 4);
     ENSURE(c, dgrp, std::max<u64>(Jf, 1) * 4);
-    ENSURE(c, dcur, std::max<u64>(C, 1) * 4);
     ENSURE(c, offp, (C + 1ull) * 8);
     ENSURE(c, skip, (ncap + 1) * 4);
     HIP_TRY(c, hipMemsetAsync(c->dcur.p, 0, std::max<u64>(C, 1) * 4, st));
     // 4. groups, range by range
     u64 Jf0 = 0, G0 = 0;
     for (size_t k = 0; k < ranges.size(); ++k) {
-        const Range& r = ranges[k];
+        const rdf_ctx::JoinRange& r = ranges[k];
         u64 J = 0;
-        TRY(g_emit_range(c, proj, JoinSel{0u, 1u, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
+        TRY(g_emit_range(c, proj, JoinSel{own.rank, own.nranks, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
         u64* keys = c->rec_sorted;
         tbegin(c, RDF_T_SUPPORT);
         ENSURE(c, flags, std::max<u64>(std::max<u64>(J, ncap), 1) * 4);
@@ -1589,6 +1645,12 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
     // the range scratch is sized by the largest range: spare for the discovery stage (g_finish marks it)
     c->rec_sorted = nullptr;
     return RDF_OK;
+}
+
+static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
+    const JoinSel all = {0u, 1u, 0u, JOIN_ALL_HI};
+    TRY(g_ranges_supports(c, proj, max_range, all));
+    return g_ranges_groups(c, proj, all, nullptr);
 }
 
 // records per join range of the automatic g_build_ranges: the range scratch (two record buffers, fresh flags + scan,
@@ -2109,7 +2171,7 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
 #ifdef RDF_LIGHT_STATS
     if (lrec) {  // per-item records -> $RDFIND_LIGHT_DUMP (raw u32 x 24 per item)
         std::vector<u32> h(r.i1 * 24);
-        HIP_TRY(c, hipMemcpy(h.data(), lrec, r.i1 * 96, hipMemcpyDeviceToHost));
+        HIP_TRY(c, ctx_copy(c, h.data(), lrec, r.i1 * 96, hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("RDFIND_LIGHT_DUMP"), "wb")) {
             fwrite(h.data(), 96, r.i1, f);
             fclose(f);
@@ -2772,7 +2834,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     c->pg_budget = page_bytes;
     c->pg_WM = WM;
     c->h_choffl.resize(c->C + 1ull);
-    HIP_TRY(c, hipMemcpy(c->h_choffl.data(), c->choffl.p, (c->C + 1ull) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, ctx_copy(c, c->h_choffl.data(), c->choffl.p, (c->C + 1ull) * 8, hipMemcpyDeviceToHost));
     c->h_choffh.assign(c->C + 1ull, 0);  // no heavy work while the unary light pass is batched
     // the unary dependents' explicit pairs, in budgeted batches, resident for the rest of the run
     u64 Eu = 0;
@@ -2797,7 +2859,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     c->hclassed = !v.literal && c->allow_hclass && !v.ar;
     TRY(d_classes_single(c, v, &HC, &NT));
     if (c->hclassed) TRY(d_class_bin(c, v, &WH));
-    HIP_TRY(c, hipMemcpy(c->h_choffh.data(), c->choffh.p, (c->C + 1ull) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, ctx_copy(c, c->h_choffh.data(), c->choffh.p, (c->C + 1ull) * 8, hipMemcpyDeviceToHost));
     c->pg_Eu = Eu;
     c->pg_HC = HC;
     c->pg_NT = NT;
@@ -3095,6 +3157,26 @@ static rdf_status sh_phase17(rdf_ctx* c, rdf_exchange* req) {
     return sh_route_triples(c, req);
 }
 
+// the triples this rank received for its join shard (wts/wtp/wto, sh_m of them) stand in for the resident input while
+// in scope; the resident slice is restored on every exit path (it is the input of the next run)
+struct ReceivedTriples {
+    rdf_ctx* c;
+    const u32 *s0, *p0, *o0;
+    u64 n0;
+    explicit ReceivedTriples(rdf_ctx* ctx) : c(ctx), s0(ctx->s), p0(ctx->p), o0(ctx->o), n0(ctx->n) {
+        c->s = c->wts.as<u32>();
+        c->p = c->wtp.as<u32>();
+        c->o = c->wto.as<u32>();
+        c->n = c->sh_m;
+    }
+    ~ReceivedTriples() {
+        c->s = s0;
+        c->p = p0;
+        c->o = o0;
+        c->n = n0;
+    }
+};
+
 // received triples (every triple with a join value owned here) -> join partners of this rank's shard, sort,
 // local supports -> all-reduce(sum) (then phases 1-8)
 static rdf_status sh_phase14(rdf_ctx* c, rdf_exchange* req) {
@@ -3106,35 +3188,43 @@ static rdf_status sh_phase14(rdf_ctx* c, rdf_exchange* req) {
     if (m)
         hipLaunchKernelGGL(k_unpack_triples, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->xrecv.as<u64>(), m,
                            c->wts.as<u32>(), c->wtp.as<u32>(), c->wto.as<u32>());
-    if (m >= (1ull << 32) / 9) return fail(c, RDF_ERR_LIMIT, "join shard holds >= 2^32/9 triples (use more ranks)");
-    // K3 reads the received triples; the resident input stays this rank's slice for the next run
-    const u32 *s0 = c->s, *p0 = c->p, *o0 = c->o;
-    const u64 n0 = c->n;
-    c->s = c->wts.as<u32>();
-    c->p = c->wtp.as<u32>();
-    c->o = c->wto.as<u32>();
-    c->n = m;
     c->rank = c->sh_rank;
     c->nranks = c->sh_nranks;
-    const rdf_status r = g_emit_sort_support(c, c->sh_proj);
-    c->s = s0;
-    c->p = p0;
-    c->o = o0;
-    c->n = n0;
-    TRY(r);
+    c->sh_m = m;
+    // a join shard whose K3 records exceed one sort's u32 offsets (>= 2^32/9 received triples, e.g. c4 at 10^9 triples
+    // over 2 or 4 ranks) builds its groups in join ranges, as one GPU does: pass 1 here, pass 2 after the all-reduce
+    c->sh_ranged = c->group_range_records || 9 * m >= (1ull << 32);
+    c->n_group_ranges = 1;
+    {
+        ReceivedTriples rt(c);  // K3 reads the received triples; the resident input stays this rank's slice
+        if (c->sh_ranged) {
+            TRY(g_ranges_supports(c, c->sh_proj, c->group_range_records ? c->group_range_records : auto_range_records(c),
+                                  JoinSel{c->rank, c->nranks, 0u, JOIN_ALL_HI}));
+            // this rank's supports, kept for pass 2 (the all-reduce brings the global ones)
+            ENSURE(c, lsup, std::max<u64>(c->ncap, 1) * 4);
+            HIP_TRY(c, hipMemcpyAsync(c->lsup.p, c->support.p, std::max<u64>(c->ncap, 1) * 4, hipMemcpyDeviceToDevice, st));
+        } else {
+            TRY(g_emit_sort_support(c, c->sh_proj));
+        }
+    }
     HIP_TRY(c, hipStreamSynchronize(st));
     return x_request(c, req, RDF_X_ALLREDUCE_SUM_U32, c->support.p, c->ncap, 1);
 }
 
 static rdf_status sh_phase1(rdf_ctx* c, rdf_exchange* req) {
     HIP_TRY(c, hipMemcpyAsync(c->support.p, c->xrecv.p, c->ncap * 4, hipMemcpyDeviceToDevice, c->stream));
-    TRY(g_compact_groups(c));
+    if (c->sh_ranged) {  // pass 2 of the join-range build, on the received triples again
+        ReceivedTriples rt(c);
+        TRY(g_ranges_groups(c, c->sh_proj, JoinSel{c->rank, c->nranks, 0u, JOIN_ALL_HI}, c->lsup.as<u32>()));
+    } else {
+        TRY(g_compact_groups(c));
+    }
     if (c->ar_on) TRY(g_ar_refs(c));
     TRY(g_size_hist(c, c->h_hist_local));
     ENSURE(c, xsend, 256 * 8);
     std::vector<u64> w(256);
     for (int i = 0; i < 256; ++i) w[i] = c->h_hist_local[i];
-    HIP_TRY(c, hipMemcpy(c->xsend.p, w.data(), 256 * 8, hipMemcpyHostToDevice));
+    HIP_TRY(c, ctx_copy(c, c->xsend.p, w.data(), 256 * 8, hipMemcpyHostToDevice));
     return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, 256, 2);
 }
 
@@ -3142,7 +3232,7 @@ static rdf_status sh_phase2(rdf_ctx* c, rdf_exchange* req) {
     const u32 R = c->nranks;
     if (c->x_recv_count != 256ull * R) return fail(c, RDF_ERR_ARG, "histogram all-gather: wrong element count");
     std::vector<u64> all(256ull * R);
-    HIP_TRY(c, hipMemcpy(all.data(), c->xrecv.p, all.size() * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, ctx_copy(c, all.data(), c->xrecv.p, all.size() * 8, hipMemcpyDeviceToHost));
     u32 gh[256] = {};
     for (u32 r = 0; r < R; ++r)
         for (int b = 0; b < 256; ++b) gh[b] += (u32)all[256ull * r + b];
@@ -3173,7 +3263,7 @@ static rdf_status sh_phase3(rdf_ctx* c, rdf_exchange* req) {
     ENSURE(c, xsend, std::max<u64>(c->C, 1) * 8);
     if (c->C)
         hipLaunchKernelGGL(k_shard_best_keys, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, c->stream,
-                           c->pbest.as<u64>(), c->info.as<CapInfo>(), c->C, c->rank, c->xsend.as<u64>());
+                           c->pbest.as<u64>(), c->info.as<CapInfo>(), c->C, c->rank, c->holder_qbits, c->xsend.as<u64>());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return x_request(c, req, RDF_X_ALLREDUCE_MIN_U64, c->xsend.p, c->C, 4);
 }
@@ -3661,11 +3751,11 @@ static rdf_status sh_phase22(rdf_ctx* c, rdf_exchange* req) {
     c->own_n = nown;
     c->ing_src_counts.assign(RDF_MAX_RANKS, 0);
     std::vector<u32> hh(RDF_MAX_RANKS);
-    HIP_TRY(c, hipMemcpy(hh.data(), c->rhist.p, RDF_MAX_RANKS * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, ctx_copy(c, hh.data(), c->rhist.p, RDF_MAX_RANKS * 4, hipMemcpyDeviceToHost));
     for (int r = 0; r < RDF_MAX_RANKS; ++r) c->ing_src_counts[r] = hh[r];
     ENSURE(c, xsend, 8);
     c->hscal[14] = nown;
-    HIP_TRY(c, hipMemcpy(c->xsend.p, c->hscal + 14, 8, hipMemcpyHostToDevice));
+    HIP_TRY(c, ctx_copy(c, c->xsend.p, c->hscal + 14, 8, hipMemcpyHostToDevice));
     return x_request(c, req, RDF_X_ALLGATHERV_U64, c->xsend.p, 1, 23);
 }
 
@@ -3675,7 +3765,7 @@ static rdf_status sh_phase23(rdf_ctx* c, rdf_exchange* req) {
     const u32 R = c->sh_nranks;
     if (c->x_recv_count != R) return fail(c, RDF_ERR_ARG, "term-count all-gather: wrong element count");
     std::vector<u64> cnt(R);
-    HIP_TRY(c, hipMemcpy(cnt.data(), c->xrecv.p, R * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, ctx_copy(c, cnt.data(), c->xrecv.p, R * 8, hipMemcpyDeviceToHost));
     u64 base = 0, tot = 0;
     for (u32 r = 0; r < R; ++r) {
         if (r < c->sh_rank) base += cnt[r];
@@ -4054,14 +4144,14 @@ static rdf_status load_runs(rdf_ctx* c) {
     if (c->h_runs_valid) return RDF_OK;
     c->h_runoff.resize(c->n_runs + 1);
     c->h_rundep.resize(c->n_runs);
-    HIP_TRY(c, hipMemcpy(c->h_runoff.data(), c->runoff.p, (c->n_runs + 1) * 8, hipMemcpyDeviceToHost));
-    if (c->n_runs) HIP_TRY(c, hipMemcpy(c->h_rundep.data(), c->rundep.p, c->n_runs * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, ctx_copy(c, c->h_runoff.data(), c->runoff.p, (c->n_runs + 1) * 8, hipMemcpyDeviceToHost));
+    if (c->n_runs) HIP_TRY(c, ctx_copy(c, c->h_rundep.data(), c->rundep.p, c->n_runs * 4, hipMemcpyDeviceToHost));
     const u32 C = c->C;
     c->h_fcap.resize(C);
     c->h_csup.resize(C);
     if (C) {
-        HIP_TRY(c, hipMemcpy(c->h_fcap.data(), c->fext.p, (u64)C * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(c, hipMemcpy(c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, ctx_copy(c, c->h_fcap.data(), c->fext.p, (u64)C * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, ctx_copy(c, c->h_csup.data(), c->csup.p, (u64)C * 4, hipMemcpyDeviceToHost));
     }
     c->h_runs_valid = true;
     return RDF_OK;
@@ -4077,7 +4167,7 @@ static rdf_status copy_decoded(rdf_ctx* c, u64 offset, u64 m, rdf_cind* out) {
     r = r ? r - 1 : 0;
     for (u64 b = 0; b < m; b += chunk) {
         const u64 k = std::min(chunk, m - b);
-        HIP_TRY(c, hipMemcpy(buf.data(), c->out_ptr + offset + b, k * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, ctx_copy(c, buf.data(), c->out_ptr + offset + b, k * 4, hipMemcpyDeviceToHost));
         for (u64 i = 0; i < k; ++i) {
             const u64 e = offset + b + i;
             while (c->h_runoff[r + 1] <= e) ++r;
@@ -4195,8 +4285,8 @@ rdf_status rdf_set_dictionary(rdf_ctx* c, const char* heap, uint64_t heap_bytes,
     HIP_TRY(c, hipSetDevice(c->device));
     ENSURE(c, dheap, std::max<u64>(heap_bytes, 1));
     ENSURE(c, dtoff, (n_terms + 1) * 8);
-    if (heap_bytes) HIP_TRY(c, hipMemcpy(c->dheap.p, heap, heap_bytes, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(c->dtoff.p, offsets, (n_terms + 1) * 8, hipMemcpyHostToDevice));
+    if (heap_bytes) HIP_TRY(c, ctx_copy(c, c->dheap.p, heap, heap_bytes, hipMemcpyHostToDevice));
+    HIP_TRY(c, ctx_copy(c, c->dtoff.p, offsets, (n_terms + 1) * 8, hipMemcpyHostToDevice));
     c->dict_terms = n_terms;
     c->capstr_run = ~0ull;
     return RDF_OK;

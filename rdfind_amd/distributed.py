@@ -49,11 +49,35 @@ def _dtype(op):
     return _DTYPES.get(op, torch.int64)
 
 
+_COMPACT_CHUNK_BYTES = 64 << 20  # staging chunk of allgatherv's in-place compaction
+
+
+def _compact_in_place(buf: torch.Tensor, counts, mx: int) -> int:
+    """Move slice r of ``buf`` (at r * mx, counts[r] elements) to the running offset sum(counts[:r]), in place and in
+    rank order.  Destinations never pass their sources, so copying each slice front to back in chunks staged through
+    one bounded scratch tensor never overwrites data not yet moved.  Returns the total count."""
+    chunk = max(_COMPACT_CHUNK_BYTES // buf.element_size(), 1)
+    scratch = None
+    off = 0
+    for r, c in enumerate(counts):
+        src = r * mx
+        if c and src != off:
+            if scratch is None:
+                scratch = buf.new_empty(min(chunk, max(counts)))
+            for k in range(0, c, chunk):
+                m = min(chunk, c - k)
+                scratch[:m].copy_(buf[src + k: src + k + m])
+                buf[off + k: off + k + m].copy_(scratch[:m])
+        off += c
+    return off
+
+
 def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
     """Variable-length all-gather: concatenation of every rank's ``send`` in rank order.  One all-gather of the counts,
     then, unless the contributions are very skewed, one all-gather of padded slices into a single preallocated tensor
-    (world x the largest slice), compacted by one copy.  When padding would exceed 4x the payload and 64 MiB, one
-    broadcast per rank into its exact slice of the result instead (no padding)."""
+    (world x the largest slice) that is compacted in place, so the peak is that tensor (+ one padded copy of this
+    rank's slice and a 64 MiB staging chunk), not a second result-sized copy.  When padding would exceed 4x the payload
+    and 64 MiB, one broadcast per rank into its exact slice of the result instead (no padding)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
@@ -65,14 +89,14 @@ def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
         return send.new_empty(0)
     pad_bytes = (world * mx - tot) * send.element_size()
     if world * mx <= 4 * tot or pad_bytes <= (64 << 20):
-        pad = send.new_zeros(mx) if send.numel() < mx else send
+        pad = send
         if send.numel() < mx:
+            pad = send.new_zeros(mx)
             pad[: send.numel()].copy_(send)
         gathered = send.new_empty(world * mx)
         dist.all_gather_into_tensor(gathered, pad, group=group)
-        if mx * world == tot:
-            return gathered
-        return torch.cat([gathered[r * mx: r * mx + c] for r, c in enumerate(counts) if c])
+        del pad
+        return gathered[: _compact_in_place(gathered, counts, mx)]
     out = send.new_empty(tot)
     off = 0
     for r, c in enumerate(counts):

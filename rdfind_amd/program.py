@@ -196,12 +196,14 @@ class RDFind:
                 return []
             page_bytes = a.page_bytes
             if page_bytes is None:
-                try:
+                cs = None
+                try:  # only the discovery falls back to pages: an OOM while writing is an error of the writer
                     cs = ctx.discover_cinds(clean_implied=a.clean_implied, traversal_strategy=a.traversal_strategy)
-                    return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
                 except _lib.RdfError as e:
                     if e.status != _lib.RDF_ERR_OOM:
                         raise
+                if cs is not None:
+                    return self.write_output(ctx, dic, {"fc": fc, "groups": gs, "cinds": cs}, t1, out)
                 # the result does not fit in HBM at once: the reference streams it to its sink at any size
                 # (RDFind.scala:507-520); here the discovery goes page by page, each page written before the next
                 self.log("The CIND result exceeds the device memory; discovering it in pages.")

@@ -130,3 +130,65 @@ def _helpers_worker(rank, world, port, q):
         q.put((rank, {"ag": ag, "empty": empty, "skew": skew, "a2a": a2a}))
     finally:
         dist.destroy_process_group()
+
+
+def test_allgatherv_compaction_in_place():
+    """allgatherv's in-place compaction of the padded all-gather (no second result-sized copy): random ragged counts,
+    gaps of one element between a slice's source and destination, and chunks much smaller than a slice."""
+    import torch
+
+    from rdfind_amd import distributed
+
+    rng = random.Random(5)
+    old = distributed._COMPACT_CHUNK_BYTES
+    try:
+        for it in range(300):
+            distributed._COMPACT_CHUNK_BYTES = 8 * rng.choice([1, 2, 3, 7, 1000])
+            world = rng.randrange(1, 9)
+            counts = [rng.choice([0, rng.randrange(1, 20), 19]) for _ in range(world)]
+            mx = max(counts + [1])
+            buf = torch.full((world * mx,), -1, dtype=torch.int64)
+            want = []
+            for r, c in enumerate(counts):
+                vals = torch.arange(c, dtype=torch.int64) + 1000 * r
+                buf[r * mx: r * mx + c] = vals
+                want += vals.tolist()
+            tot = distributed._compact_in_place(buf, counts, mx)
+            assert tot == sum(counts) and buf[:tot].tolist() == want, (counts, it)
+    finally:
+        distributed._COMPACT_CHUNK_BYTES = old
+
+
+def _skew_worker(rank, world, port, q):
+    import torch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import distributed
+
+    try:
+        distributed._COMPACT_CHUNK_BYTES = 16  # 2 elements: many chunks per slice
+        sizes = [6, 7, 0, 5][:world]
+        send = torch.arange(sizes[rank], dtype=torch.int64) + 100 * rank
+        q.put((rank, distributed.allgatherv(send).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_allgatherv_skewed_contributions_gloo(world):
+    """Ragged contributions (one rank empty) through the padded all-gather and its in-place compaction, over gloo."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_skew_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sizes = [6, 7, 0, 5][:world]
+    want = [100 * r + i for r in range(world) for i in range(sizes[r])]
+    assert all(got[r] == want for r in range(world))

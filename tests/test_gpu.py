@@ -16,6 +16,7 @@ from oracle import c_oracle as C, rdfind_oracle as R
 from rdfind_amd import _lib, ntriples, program, synth
 from tests import kats
 from tests.conftest import GOLDEN
+from tests.parity import assert_rows_equal, assert_stream_matches, dataset, oracle_stream
 from tests.test_oracle import KAT_PEOPLE, KAT_PEOPLE_CLEAN, KAT_PEOPLE_RAW, read_golden
 
 pytestmark = pytest.mark.gpu
@@ -150,16 +151,17 @@ def test_program_reproduces_golden(tmp_path, name, mode, flags):
 
 @pytest.mark.parametrize("cfg,scale", [("c1", 0.3), ("c2", 0.05), ("c3", 0.002), ("c4", 0.0003), ("c5", 0.01)])
 def test_synthetic_configs_vs_oracle(ctx, cfg, scale):
-    d = synth.config(cfg, scale)
-    exp, st = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+    """Scaled BASELINE shapes: every result row equals the materializing C oracle's, and the intermediate stage
+    counts agree with the restatement too."""
+    d = dataset(cfg, scale)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)
     ctx.run(d.min_support)
-    # intermediate stages agree with the restatement too
+    st = assert_rows_equal(ctx, d, 1, True)
     assert ctx.fc["n_frequent_unary"] == st["n_freq_unary"]
     assert ctx.fc["n_frequent_binary"] == st["n_freq_binary"]
     assert ctx.groups["n_records"] == st["n_records"]
     assert ctx.groups["n_captures"] == st["n_freq_captures"]
-    assert _lib.decoded_to_set(ctx.decoded_cinds()) == exp
+    assert_stream_matches(ctx, cfg, scale)
 
 
 def test_global_count_paths(ctx, monkeypatch):
@@ -178,7 +180,7 @@ def test_global_count_paths(ctx, monkeypatch):
             for strategy, clean in ((1, True), (0, False)):
                 assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean)
         for cfg, scale in (("c1", 0.2), ("c5", 0.01)):
-            d = synth.config(cfg, scale)
+            d = dataset(cfg, scale)
             stats = []
             for c in (g, ctx):
                 c.set_triples(d.s, d.p, d.o, d.num_terms)
@@ -203,7 +205,7 @@ def _capture_joins(d, code, v1, v2):
 
 def test_bench_size_properties(ctx):
     """c2 at full size (the bench workload): determinism, rule monotonicity, sampled verification."""
-    d = synth.config("c2", 1.0)
+    d = dataset("c2", 1.0)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)
     ctx.run(d.min_support, "spo", True, 1)
     n_clean = ctx.cind_count()
@@ -252,11 +254,10 @@ def test_heavy_paths_parity(monkeypatch, heavy_min):
                     (n, nv, ms, strategy, clean, heavy_min)
                 assert C.checksum_compact(parts, nv)[:2] == (g.cind_count(), g.checksum())
         for cfg, scale in (("c5", 0.01), ("c1", 0.05)):
-            d = synth.config(cfg, scale)
-            exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+            d = dataset(cfg, scale)
             g.set_triples(d.s, d.p, d.o, d.num_terms)
-            cs = g.run(d.min_support)
-            assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, heavy_min)
+            g.run(d.min_support)
+            assert_stream_matches(g, cfg, scale, what=heavy_min)
             assert g.groups["n_heavy_groups"] > 0
     finally:
         g.close()
@@ -287,26 +288,28 @@ def test_dense_bitmap_paths_parity(monkeypatch, budget):
                     assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
                         (n, nv, ms, strategy, clean, heavy_min)
             for cfg, scale in (("c5", 0.01), ("c1", 0.05), ("c4", 0.0003)):
-                d = synth.config(cfg, scale)
-                exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+                d = dataset(cfg, scale)
                 g.set_triples(d.s, d.p, d.o, d.num_terms)
                 g.run(d.min_support)
-                assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, heavy_min)
+                assert_stream_matches(g, cfg, scale, what=heavy_min)
         finally:
             g.close()
 
 
-def _paged(g, ms, strategy, clean, page_bytes):
-    """Every page of a paged run: (union of decoded rows, total count, sum of page checksums, pages, compact ok)."""
+def _paged(g, ms, strategy, clean, page_bytes, keep_rows=True):
+    """Every page of a paged run: (union of decoded rows, total count, sum of page checksums, pages, compact ok).
+    Without keep_rows only the counts and checksums are summed (disjointness then follows from count + checksum
+    equal to the oracle's)."""
     g.frequent_conditions(ms)
     g.build_capture_groups("spo")
     rows, n, h, pages, compact_ok = set(), 0, 0, 0, True
     for _ in g.pages(clean, strategy, page_bytes):
         parts = g.copy_result_compact()
         cnt = g.cind_count()
-        page_rows = _lib.decoded_to_set(g.decoded_cinds())
-        assert not (rows & page_rows)  # pages are disjoint
-        rows |= page_rows
+        if keep_rows:
+            page_rows = _lib.decoded_to_set(g.decoded_cinds())
+            assert not (rows & page_rows)  # pages are disjoint
+            rows |= page_rows
         n += cnt
         h = (h + g.checksum()) % (1 << 64)
         compact_ok &= C.checksum_compact(parts, g.num_terms)[:2] == (cnt, g.checksum())
@@ -334,11 +337,11 @@ def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
                 rows, cnt, _, pages, ok = _paged(g, ms, strategy, clean, 1)
                 assert rows == exp and cnt == len(exp) and ok, (n, nv, ms, strategy, clean, heavy_min)
         for cfg, scale in (("c5", 0.01), ("c1", 0.05)):
-            d = synth.config(cfg, scale)
-            exp, _ = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+            d = dataset(cfg, scale)
+            exp = oracle_stream(cfg, scale)
             g.set_triples(d.s, d.p, d.o, d.num_terms)
-            rows, cnt, _, pages, ok = _paged(g, d.min_support, 1, True, 1 << 16)
-            assert rows == exp and ok and pages > 2, (cfg, heavy_min, pages)
+            _, cnt, h, pages, ok = _paged(g, d.min_support, 1, True, 1 << 16, keep_rows=False)
+            assert (cnt, h) == (exp["n_cinds"], exp["checksum"]) and ok and pages > 2, (cfg, heavy_min, pages)
     finally:
         g.close()
 
@@ -371,16 +374,111 @@ def test_join_range_groups_parity(monkeypatch, range_records):
             if range_records == 1 and n > 50:
                 assert g.groups["n_join_ranges"] > 1
         for cfg, scale in (("c1", 0.05), ("c5", 0.01), ("c4", 0.0003)):
-            d = synth.config(cfg, scale)
-            exp, st = C.run_set(d.s, d.p, d.o, d.num_terms, d.min_support, 1, True)
+            d = dataset(cfg, scale)
             g.set_triples(d.s, d.p, d.o, d.num_terms)
             g.run(d.min_support)
-            assert _lib.decoded_to_set(g.decoded_cinds()) == exp, (cfg, range_records)
+            st = assert_stream_matches(g, cfg, scale, what=range_records)["stats"]
             assert g.groups["n_records"] == st["n_records"] and g.groups["n_captures"] == st["n_freq_captures"]
             assert g.groups["n_join_ranges"] > 1
     finally:
         g.close()
         ref.close()
+
+
+def test_binary_keys_right_after_frequent_conditions(ctx):
+    """rdf_copy_binary_keys straight after rdf_frequent_conditions (whose key sort may still be queued on the context
+    stream) returns the sorted keys, the same as after a whole discovery."""
+    for cfg, scale in (("c2", 0.05), ("c1", 0.3)):
+        d = dataset(cfg, scale)
+        ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+        ctx.frequent_conditions(d.min_support)
+        early = ctx.binary_keys()
+        ctx.run(d.min_support)
+        late = ctx.binary_keys()
+        assert early.shape[0] > 1000
+        np.testing.assert_array_equal(early, late)
+        assert (early[1:] > early[:-1]).all()  # sorted, unpacked keys
+
+
+def test_k2_split_forced_small_inputs(monkeypatch):
+    """The K2 sub-bucket split (k_b2_split, which large inputs take: c3 / c4) forced on small inputs (RDFIND_B2_SPLIT=2,
+    read once per process: a child process) gives the oracle's sets in every mode and c1/c5 samples' checksums."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = r"""
+import json, random, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from rdfind_amd import _lib
+from tests.test_gpu import MODES, expected_set
+from tests.parity import dataset, oracle_stream
+bad = []
+rng = random.Random(61)
+with _lib.Context(0) as g:
+    for it in range(20):
+        n = rng.randrange(20, 400); nv = rng.randrange(4, 40); ms = rng.randrange(1, 4)
+        arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)], dtype=np.uint32)
+        for strategy, clean in MODES:
+            g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+            g.run(ms, "spo", clean, strategy)
+            if _lib.decoded_to_set(g.decoded_cinds()) != expected_set(arr, nv, ms, strategy, clean):
+                bad.append((it, strategy, clean))
+    for cfg, scale in (("c1", 0.05), ("c5", 0.01)):
+        d = dataset(cfg, scale)
+        g.set_triples(d.s, d.p, d.o, d.num_terms)
+        g.run(d.min_support)
+        e = oracle_stream(cfg, scale)
+        if (g.cind_count(), g.checksum()) != (e["n_cinds"], e["checksum"]):
+            bad.append(cfg)
+print(json.dumps({"bad": bad}))
+"""
+    r = subprocess.run([sys.executable, "-c", child, root], env=dict(os.environ, RDFIND_B2_SPLIT="2"), capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["bad"] == []
+
+
+def test_failed_split_launch_is_an_error_not_a_fault():
+    """A k_b2_split launch that does not run (RDFIND_TEST_FAIL_LAUNCH=k_b2_split: an invalid block size; the split forced
+    by RDFIND_B2_SPLIT=2) makes rdf_frequent_conditions fail with RDF_ERR_HIP before any kernel consumes the sub-bucket
+    offsets it would have written -- the round-4 aperture violation was a count kernel reading such offsets (DESIGN.md
+    section 10).  A context without the hook then runs normally in the same process.  Own process: both switches are
+    read once per process or per context."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+from rdfind_amd import _lib
+from tests.parity import dataset, oracle_stream
+d = dataset("c1", 0.05)
+out = {}
+with _lib.Context(0) as g:
+    g.set_triples(d.s, d.p, d.o, d.num_terms)
+    try:
+        g.frequent_conditions(d.min_support)
+        out["failed"] = None
+    except _lib.RdfError as e:
+        out["failed"], out["msg"] = e.status, str(e)
+del os.environ["RDFIND_TEST_FAIL_LAUNCH"]
+with _lib.Context(0) as h:
+    h.set_triples(d.s, d.p, d.o, d.num_terms)
+    h.run(d.min_support)
+    out["ok"] = (h.cind_count(), h.checksum()) == (oracle_stream("c1", 0.05)["n_cinds"], oracle_stream("c1", 0.05)["checksum"])
+print(json.dumps(out))
+"""
+    env = dict(os.environ, RDFIND_TEST_FAIL_LAUNCH="k_b2_split", RDFIND_B2_SPLIT="2")
+    r = subprocess.run([sys.executable, "-c", child, root], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["failed"] == -2 and "hipGetLastError" in got["msg"], got  # RDF_ERR_HIP
+    assert got["ok"], got
 
 
 def test_next_page_needs_a_current_paged_run(ctx):
@@ -409,7 +507,7 @@ def test_large_grids_two_paths(monkeypatch):
     """c5 at scale 0.3 (8.7e9 CINDs): the heavy-only binary dependents take > 2^26 work items (a dispatch holds
     < 2^32 work-items, so the kernels loop over virtual blocks).  The classed path and the pivot-scan path
     (RDFIND_HCLASS=0) compute them independently and must agree on the count and the set checksum."""
-    d = synth.config("c5", 0.3)
+    d = dataset("c5", 0.3)
     got = []
     for flag in ("1", "0"):
         monkeypatch.setenv("RDFIND_HCLASS", flag)
@@ -450,7 +548,7 @@ def test_device_formatting_matches_host(ctx):
             a, b = total // 3, 2 * total // 3
             parts = ctx.format_cinds(0, a) + ctx.format_cinds(a, b - a) + ctx.format_cinds(b, total)
             assert parts == text
-    d = synth.config("c2", 0.05)
+    d = dataset("c2", 0.05)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)
     ctx.run(d.min_support)
     terms = ["<http://www.Department%d.University%d.edu/t%d>" % (i % 15, i % 7, i) for i in range(d.num_terms)]
@@ -618,7 +716,7 @@ def test_program_host_parser_reproduces_golden(tmp_path, name):
 def test_copy_result_refs_ranges(ctx):
     """rdf_copy_result_refs (the streaming hand-over of the explicit refs) returns the refs part of the compact result
     chunk by chunk, with a short last chunk and nothing past the end."""
-    d = synth.config("c1", 0.05)
+    d = dataset("c1", 0.05)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)
     ctx.run(d.min_support)
     whole = ctx.copy_result_compact()
@@ -658,7 +756,7 @@ def test_copy_cinds_decoded_matches_host_decode(ctx):
         if host.shape[0] > 5:
             part = ctx.copy_cinds_decoded(2, 3)
             np.testing.assert_array_equal(part, dev[2:5])
-    d = synth.config("c2", 0.05)
+    d = dataset("c2", 0.05)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)
     ctx.run(d.min_support)
     n = ctx.cind_count()

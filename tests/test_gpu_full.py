@@ -11,21 +11,13 @@ import os
 import numpy as np
 import pytest
 
-from rdfind_amd import _lib, synth
+from rdfind_amd import _lib
 from tests.conftest import GOLDEN
+from tests.parity import dataset, dataset_npz
 
 pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(GOLDEN, "full_size.json")))
-_DATA = {}
-
-
-def dataset(cfg, scale):
-    key = (cfg, scale)
-    if key not in _DATA:
-        _DATA.clear()  # one full-size input at a time
-        _DATA[key] = synth.config(cfg, scale)
-    return _DATA[key]
 
 
 @pytest.fixture(scope="module")
@@ -40,12 +32,14 @@ def fingerprint(d):
     return fp(d)
 
 
-# golden entries whose result exceeds one GPU's HBM at once: checked page by page (test_paged_full_size_vs_oracle)
+# golden entries whose result exceeds one GPU's HBM at once: checked page by page (test_paged_full_size_vs_oracle);
+# c4 at 10^9 triples has its own test (test_c4_full_size_one_gpu), which checks the same golden entry
 PAGED_ONLY = {"c5@1.0/s1_clean"}
+OWN_TEST = {"c4@1.0/s1_clean"}
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("key", sorted(set(GOLD) - PAGED_ONLY))
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("key", sorted(set(GOLD) - PAGED_ONLY - OWN_TEST))
 def test_full_size_vs_oracle(ctx, key):
     g = GOLD[key]
     d = dataset(g["config"], g["scale"])
@@ -150,54 +144,45 @@ def _sample_verify(ctx, d, k, seed):
         assert np.isin(jd, jr).all()
 
 
-@pytest.mark.timeout(1100)
-def test_c4_full_size_one_gpu(ctx, monkeypatch):
+@pytest.mark.timeout(300)
+def test_c4_full_size_one_gpu(ctx):
     """c4 at its BASELINE size (Freebase-shaped, 10^9 triples, support 100) on one MI355X.  Its ~5.8·10^9 capture
     records exceed one sort's u32 offsets, so the capture groups are built in join-value ranges (the reference's
-    sort-based groupBy spills instead, ALG/programs/RDFind.scala:339-345).  Checked: the same result (count, checksum,
-    stage counts) from two different range splits, run to run determinism, the compact hand-over expanded by the
-    checker, sampled CINDs verified on the triples, and the streamed oracle's golden vector when it has been made."""
+    sort-based groupBy spills instead, ALG/programs/RDFind.scala:339-345).  One run, checked against the streamed
+    oracle's golden vector (stage counts, count, checksum), through the compact hand-over expanded by the checker, and
+    by sampled CINDs verified on the triples.  Other range splits are parity-tested at c4 at 0.1
+    (test_join_ranges_full_size_vs_oracle) and on random inputs (test_gpu.py::test_join_range_groups_parity)."""
     from oracle import c_oracle as C
 
+    g = GOLD["c4@1.0/s1_clean"]
     d = dataset("c4", 1.0)
-    assert d.n == 1_000_000_000
-    results = []
-    monkeypatch.setenv("RDFIND_GROUP_RANGE", str(600_000_000))  # ~10 ranges
-    with _lib.Context(0) as c:
-        c.set_triples(d.s, d.p, d.o, d.num_terms)
-        c.run(d.min_support)
-        forced = c.groups["n_join_ranges"]
-        assert forced >= 4
-        results.append((c.cind_count(), c.checksum(), c.groups["n_records"], c.groups["n_groups"]))
-    monkeypatch.delenv("RDFIND_GROUP_RANGE")
+    assert d.n == 1_000_000_000 == g["n_triples"]
+    assert str(fingerprint(d)) == g["fingerprint"]
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)
-    for _ in range(2):
-        ctx.run(d.min_support)
-        assert 1 < ctx.groups["n_join_ranges"] < forced
-        results.append((ctx.cind_count(), ctx.checksum(), ctx.groups["n_records"], ctx.groups["n_groups"]))
-    assert results[0] == results[1] == results[2]
-    n, h, _ = C.checksum_compact(ctx.copy_result_compact(), d.num_terms)
-    assert (n, h) == results[0][:2] and n > 0
+    ctx.run(d.min_support)
+    assert ctx.groups["n_join_ranges"] > 1
     assert ctx.groups["n_records"] > 2 ** 32  # more records than one pass addresses
+    assert ctx.fc["n_frequent_unary"] == g["n_freq_unary"] and ctx.fc["n_frequent_binary"] == g["n_freq_binary"]
+    assert ctx.groups["n_records"] == g["n_records"] and ctx.groups["n_captures"] == g["n_freq_captures"]
+    assert (ctx.cind_count(), ctx.checksum()) == (g["n_cinds"], int(g["checksum"]))
+    n, h, kind = C.checksum_compact(ctx.copy_result_compact(), d.num_terms)
+    assert (n, h, kind) == (g["n_cinds"], int(g["checksum"]), g["n_kind"])
     _sample_verify(ctx, d, 10, 4)
-    g = GOLD.get("c4@1.0/s1_clean")
-    if g is not None:
-        assert str(fingerprint(d)) == g["fingerprint"]
-        assert ctx.fc["n_frequent_unary"] == g["n_freq_unary"] and ctx.fc["n_frequent_binary"] == g["n_freq_binary"]
-        assert ctx.groups["n_records"] == g["n_records"] and ctx.groups["n_captures"] == g["n_freq_captures"]
-        assert (n, h) == (g["n_cinds"], int(g["checksum"]))
 
 
 _VARIANT_CHILD = r"""
 import json, sys
 sys.path.insert(0, sys.argv[1])
-from rdfind_amd import _lib, synth
-g = json.loads(sys.argv[2])
-d = synth.config(g["config"], g["scale"])
+from rdfind_amd import _lib
+from tests.parity import load_npz
+out = []
 with _lib.Context(0) as ctx:
-    ctx.set_triples(d.s, d.p, d.o, d.num_terms)
-    ctx.run(d.min_support, "spo", g["clean"], g["strategy"])
-    print(json.dumps({"n": ctx.cind_count(), "sum": str(ctx.checksum())}))
+    for g, path in json.loads(sys.argv[2]):
+        s, p, o, nv, ms = load_npz(path)
+        ctx.set_triples(s, p, o, nv)
+        ctx.run(ms, "spo", g["clean"], g["strategy"])
+        out.append({"n": ctx.cind_count(), "sum": str(ctx.checksum())})
+print(json.dumps(out))
 """
 
 
@@ -227,16 +212,16 @@ def test_light_variants_full_size(env):
     if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N",
             "RDFIND_PIVX_PACKED"} & set(env):  # c4 runs these
         keys.append("c4@0.1/s1_clean")
-    for key in keys:
+    jobs = [(GOLD[key], dataset_npz(GOLD[key]["config"], GOLD[key]["scale"])) for key in keys]
+    r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root, json.dumps(jobs)], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for key, got in zip(keys, json.loads(r.stdout.strip().splitlines()[-1])):
         g = GOLD[key]
-        r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root, json.dumps(g)], env=dict(os.environ, **env),
-                           capture_output=True, text=True, timeout=240)
-        assert r.returncode == 0, r.stderr[-2000:]
-        got = json.loads(r.stdout.strip().splitlines()[-1])
         assert got["n"] == g["n_cinds"] and got["sum"] == g["checksum"], (key, env, got)
 
 
-@pytest.mark.timeout(900)
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("key,page_bytes", [("c5@0.3/s1_clean", 4 << 30), ("c5@1.0/s1_clean", 0)])
 def test_paged_full_size_vs_oracle(ctx, key, page_bytes):
     """Paged discovery (bounded HBM per page) at the pair-explosion config: the pages' counts and checksums (device

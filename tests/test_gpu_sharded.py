@@ -22,7 +22,8 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo"):
+def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo", env=None):
+    os.environ.update(env or {})  # library switches (read when a context is created)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     if backend == "nccl":
@@ -45,7 +46,7 @@ def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo"):
             n = ctx.cind_count()
             rows = ctx.copy_cinds() if n <= 2_000_000 else None
             item = {"n": n, "checksum": ctx.checksum(), "rows": rows, "heavy": gs["n_heavy_groups"],
-                    "class_members": cs["n_class_members"]}
+                    "class_members": cs["n_class_members"], "ranges": gs["n_join_ranges"]}
             if use_ars:
                 item["rules"] = sorted(map(tuple, ctx.copy_association_rules().tolist()))
                 item["decoded"] = _lib.decoded_to_set(ctx.decoded_cinds())
@@ -59,11 +60,11 @@ def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo"):
         dist.destroy_process_group()
 
 
-def _run_sharded(world, cases, local_slice=False, backend="gloo"):
+def _run_sharded(world, cases, local_slice=False, backend="gloo", env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice, backend)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, local_slice, backend, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -98,9 +99,9 @@ def _rowset(rows):
     return set(map(tuple, np.stack([rows["dep"], rows["ref"], rows["support"]], 1).tolist()))
 
 
-def _check(world, cases, local_slice=False, backend="gloo"):
+def _check(world, cases, local_slice=False, backend="gloo", env=None):
     single = _single(cases)
-    res = _run_sharded(world, cases, local_slice, backend)
+    res = _run_sharded(world, cases, local_slice, backend, env)
     for k, exp in enumerate(single):
         parts = [res[r][k] for r in range(world)]
         assert sum(p["n"] for p in parts) == exp["n"], k
@@ -272,8 +273,9 @@ def test_program_dop2_association_rules(tmp_path):
     assert sorted((tmp_path / "two.txt").read_text().splitlines()) == sorted((tmp_path / "one.txt").read_text().splitlines())
 
 
-def _config_worker(rank, world, port, cfg, scale, q):
+def _config_worker(rank, world, port, cfg, scale, q, env=None):
     """One rank of a sharded run on a BASELINE config: the rank draws only its own slice (synth.config_slice)."""
+    os.environ.update(env or {})
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -284,39 +286,68 @@ def _config_worker(rank, world, port, cfg, scale, q):
         with _lib.Context(0) as ctx:
             ctx.set_triples(d.s, d.p, d.o, d.num_terms)
             del d
-            distributed.run_sharded(ctx, 100 if cfg == "c4" else 10, local_slice=True)
-            q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum()}))
+            gs, _ = distributed.run_sharded(ctx, 100 if cfg == "c4" else 10, local_slice=True)
+            q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum(), "ranges": gs["n_join_ranges"]}))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(900)
-def test_sharded_c4_at_scale_vs_golden():
-    """c4 (Freebase-shaped) at scale 0.4 -- 400M triples, support 100 -- over 2 ranks, each drawing and holding only
-    its half of the rows: the ranks' CINDs sum to the streamed oracle's golden count and checksum."""
-    import json
-
-    from tests.conftest import GOLDEN
-
-    g = json.load(open(os.path.join(GOLDEN, "full_size.json")))["c4@0.4/s1_clean"]
+def _run_config(world, cfg, scale, env=None, timeout=840):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_config_worker, args=(r, 2, port, "c4", 0.4, q)) for r in range(2)]
+    procs = [ctx.Process(target=_config_worker, args=(r, world, port, cfg, scale, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     try:
         for _ in procs:
-            r, item = q.get(timeout=840)
+            r, item = q.get(timeout=timeout)
             assert not isinstance(item, str), f"rank {r}: {item}"
             res[r] = item
     finally:
         for p in procs:
-            p.join(timeout=5 if len(res) < 2 else 60)
+            p.join(timeout=5 if len(res) < world else 60)
             if p.is_alive():
                 p.terminate()
+    return res
+
+
+def _golden(key):
+    import json
+
+    from tests.conftest import GOLDEN
+    return json.load(open(os.path.join(GOLDEN, "full_size.json")))[key]
+
+
+@pytest.mark.timeout(300)
+def test_sharded_c4_at_scale_vs_golden():
+    """c4 (Freebase-shaped) at scale 0.4 -- 400M triples, support 100 -- over 2 ranks, each drawing and holding only
+    its half of the rows: the ranks' CINDs sum to the streamed oracle's golden count and checksum."""
+    g = _golden("c4@0.4/s1_clean")
+    res = _run_config(2, "c4", 0.4)
     assert sum(res[r]["n"] for r in range(2)) == g["n_cinds"]
     assert sum(res[r]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"])
+
+
+@pytest.mark.timeout(300)
+def test_sharded_c4_join_ranges_vs_golden():
+    """A rank's join shard built in join-value ranges (sh_phase14 -> sh_phase1: the path of shards of >= 2^32/9
+    received triples, e.g. c4 at 10^9 triples over 2 or 4 ranks; RDFIND_GROUP_RANGE forces it here): c4 at 0.1 over 2
+    ranks, each rank's ~2.8·10^8 records in ranges of <= 6·10^7, sums to the golden count and checksum."""
+    g = _golden("c4@0.1/s1_clean")
+    res = _run_config(2, "c4", 0.1, env={"RDFIND_GROUP_RANGE": str(60_000_000)})
+    assert all(res[r]["ranges"] >= 4 for r in range(2)), res
+    assert sum(res[r]["n"] for r in range(2)) == g["n_cinds"]
+    assert sum(res[r]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"])
+
+
+@pytest.mark.parametrize("range_records", [7, 300])
+def test_sharded_join_ranges_random(range_records):
+    """Random inputs in all four modes over 2 ranks, each rank's join shard in ranges of at most range_records K3
+    records (a single join value's records may exceed it): the union equals the single-GPU result."""
+    res = _check(2, _random_cases(400 + range_records, 24), local_slice=True,
+                 env={"RDFIND_GROUP_RANGE": str(range_records)})
+    assert any(res[r][k]["ranges"] > 1 for r in range(2) for k in range(24))
