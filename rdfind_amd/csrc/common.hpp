@@ -49,12 +49,30 @@ __host__ __device__ inline u32 dep_owner(u32 d, u32 nranks) {
     return nranks <= 1 ? 0u : (u32)((mix64(d) >> 32) % nranks);
 }
 
-// join values whose capture records a K3 emission writes: this rank's shard (hash) and, when the capture groups are
-// built in join-value ranges (one GPU, inputs whose records exceed one pass), the range [lo, hi)
+// Hot join values (sharded): a small open-addressing table of (join << 32 | owner rank) entries, load <= 1/2, probed
+// linearly from mix64(join) & mask.  The values whose occurrences are a visible share of a rank's load get owners
+// from a balanced (largest-first) assignment instead of the hash (sh_phase18); every other value keeps shard_of.
+__host__ __device__ inline u32 hot_slot(u32 join, u32 mask) { return (u32)(mix64(join) & mask); }
+__device__ inline u32 join_owner(u32 join, u32 nranks, const u64* __restrict__ hot, u32 hmask) {
+    if (nranks <= 1) return 0u;
+    if (hot) {
+        for (u32 h = hot_slot(join, hmask);; h = (h + 1) & hmask) {
+            const u64 e = hot[h];
+            if (e == EMPTY64) break;
+            if ((u32)(e >> 32) == join) return (u32)e;
+        }
+    }
+    return shard_of(join, nranks);
+}
+
+// join values whose capture records a K3 emission writes: this rank's shard (hash, or the hot table's owner) and, when
+// the capture groups are built in join-value ranges (inputs whose records exceed one pass), the range [lo, hi)
 struct JoinSel {
     u32 rank, nranks, lo, hi;
-    __host__ __device__ inline bool take(u32 join) const {
-        return shard_of(join, nranks) == rank && join >= lo && join < hi;
+    const u64* hot = nullptr;  // sharded: the hot join values' owners (nullptr: hash only)
+    u32 hmask = 0;
+    __device__ inline bool take(u32 join) const {
+        return join >= lo && join < hi && join_owner(join, nranks, hot, hmask) == rank;
     }
 };
 static constexpr u32 JOIN_ALL_HI = 0xffffffffu;

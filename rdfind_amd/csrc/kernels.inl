@@ -410,9 +410,13 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
                                      u64 (&rec)[9], u32* rep = nullptr) {
     u32 c = 0, rp_mask = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
-    const u32 rs = frank[ts], rp = frank[(u64)V + tp], ro = frank[2ull * V + to];  // global condition ranks (or NONE)
+    // the join values this selection takes; only the condition ranks their records need are loaded (a join range
+    // takes a fraction of the join values: the random frank loads, not the coalesced triple reads, bound its emission)
+    const bool jo = (proj & 4) && js.take(to), jp = (proj & 2) && js.take(tp), js_ = (proj & 1) && js.take(ts);
+    const u32 rs = jo || jp ? frank[ts] : NONE32, rp = jo || js_ ? frank[(u64)V + tp] : NONE32,
+              ro = jp || js_ ? frank[2ull * V + to] : NONE32;  // global condition ranks (or NONE)
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
-    if ((proj & 4) && js.take(to)) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
+    if (jo) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
         if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp + 1) << joinbits) | to; }
         if (fs && fp) {
@@ -420,7 +424,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
         }
     }
-    if ((proj & 2) && js.take(tp)) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
+    if (jp) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
         if (fs) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
         if (fo) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
         if (fs && fo) {
@@ -428,7 +432,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
         }
     }
-    if ((proj & 1) && js.take(ts)) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
+    if (js_) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
         if (fo) rec[c++] = ((2ull * ro) << joinbits) | ts;
         if (fp && fo) {
@@ -439,6 +443,144 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
     if (rep) *rep = rp_mask;
     return c;
 }
+
+// One join range's (triple, attribute) entries: the triples whose subject (entries [0, m_s)), predicate ([m_s, m_sp))
+// or object ([m_sp, m)) is a join value of the range, ascending triple index per attribute.  The records of entry e are
+// those triple_records makes for that attribute (at most 3), in the same order; the join value needs no selection test.
+__device__ inline u32 entry_records(u64 e, const u32* __restrict__ ent, u64 m_s, u64 m_sp, const u32* __restrict__ s,
+                                    const u32* __restrict__ p, const u32* __restrict__ o, u32 V, u32 twoU,
+                                    const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                    const u32* __restrict__ lvals, u64 lmask, int joinbits, u64 (&rec)[9], u32* rep) {
+    const u64 i = ent[e];
+    const u32 ts = s[i], tp = p[i], to = o[i];
+    u32 c = 0, rp_mask = 0;
+    if (e >= m_sp) {  // o[s] (t4), o[p] (t5), o[s,p]
+        const u32 rs = frank[ts], rp = frank[(u64)V + tp];
+        if (rs != NONE32) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
+        if (rp != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp + 1) << joinbits) | to; }
+        if (rs != NONE32 && rp != NONE32) {
+            const u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
+            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
+        }
+    } else if (e >= m_s) {  // p[s] (t2), p[o] (t3), p[s,o]
+        const u32 rs = frank[ts], ro = frank[2ull * V + to];
+        if (rs != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
+        if (ro != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
+        if (rs != NONE32 && ro != NONE32) {
+            const u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
+            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
+        }
+    } else {  // s[p] (t0), s[o] (t1), s[p,o]
+        const u32 rp = frank[(u64)V + tp], ro = frank[2ull * V + to];
+        if (rp != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
+        if (ro != NONE32) rec[c++] = ((2ull * ro) << joinbits) | ts;
+        if (rp != NONE32 && ro != NONE32) {
+            const u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
+            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | ts;
+        }
+    }
+    if (rep) *rep = rp_mask;
+    return c;
+}
+
+// k_emit_records' two passes over a join range's entries (ENTRIES; the triple form below is k_emit_records itself,
+// kept as its own kernel: folded into this body it compiled to 45 instead of 75 VGPRs and c2's emission went from
+// 0.79 to 1.01 ms)
+template <bool WRITE, bool ENTRIES>
+__device__ inline void emit_records_body(const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
+                                         const u32* __restrict__ ent, u64 m_s, u64 m_sp, u64 n, u64 per, u32 V, u32 twoU,
+                                         const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                         const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, JoinSel js,
+                                         u64* __restrict__ block_counts, const u64* __restrict__ block_offsets,
+                                         u64* __restrict__ out, int recbits) {
+    __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
+    __shared__ u64 htab[WRITE ? EMIT_DEDUP_SLOTS : 1];  // the iteration's distinct records (write pass)
+    const u64 b = (u64)blockIdx.x * per;
+    const u64 e = b + per < n ? b + per : n;
+#define RDF_UNIT_RECORDS(i, rec, rep)                                                                                  \
+    (ENTRIES ? entry_records(i, ent, m_s, m_sp, s, p, o, V, twoU, frank, lkeys, lvals, lmask, joinbits, rec, rep)        \
+             : triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, rep))
+    if (!WRITE) {  // the block's record count: per-thread sums, one block reduction at the end
+        u32 mine = 0;
+        for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
+            u64 rec[9];
+            mine += RDF_UNIT_RECORDS(i, rec, nullptr);
+        }
+        u32 total;
+        block_exclusive_scan_u32(mine, lds_wave, &total);
+        if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+        return;
+    }
+    u64 run = block_offsets[blockIdx.x];
+#ifndef RDF_EMIT_DEDUP
+#define RDF_EMIT_DEDUP 1
+#endif
+    const bool dedup = RDF_EMIT_DEDUP && recbits <= 48;
+    u32 tag = 0;
+    if (dedup) {
+        for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;  // tag 0: empty
+        __syncthreads();
+    }
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        u64 rec[9];
+        u32 c = 0, rep = 0;
+        if (i < e) c = RDF_UNIT_RECORDS(i, rec, &rep);
+        // Records repeated within the iteration's 256 units (the same subject's predicate, the same (predicate,
+        // object) pair: ~23 % of c2's records; only the kinds flagged by the source are looked up) are written
+        // once; the count pass's region stays as it is and its tail is padded with EMIT_PAD, which the record sort's
+        // first pass drops.  The LDS table slots carry the iteration's tag in bits 48.. (records have <= 48 bits
+        // here), so it is cleared only when the tag wraps; the previous iteration's insertions finished before its
+        // scan's barriers.
+        u32 keep = (1u << c) - 1u;
+        if (dedup) {
+            ++tag;
+            if (tag == (1u << 15)) {  // tags wrap: clear the table once
+                __syncthreads();
+                for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;
+                __syncthreads();
+                tag = 1;
+            }
+            keep = ((1u << c) - 1u) & ~rep;  // only the repeating kinds go through the table
+            for (int k = 0; k < 9; ++k) {
+                if ((u32)k >= c) break;
+                if (!((rep >> k) & 1u)) continue;
+                const u64 want = rec[k] | ((u64)tag << 48);
+                u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
+                u64 cur = htab[h];
+                while (true) {
+                    if ((u32)(cur >> 48) != tag) {  // a slot of an earlier iteration: free
+                        const u64 prev = atomicCAS((unsigned long long*)&htab[h], (unsigned long long)cur,
+                                                   (unsigned long long)want);
+                        if (prev == cur) {  // the first copy of the record: kept
+                            keep |= 1u << k;
+                            break;
+                        }
+                        cur = prev;
+                        continue;
+                    }
+                    if (cur == want) break;  // a copy is kept by another record
+                    h = (h + 1) & (EMIT_DEDUP_SLOTS - 1);
+                    cur = htab[h];
+                }
+            }
+        }
+        // one scan of (kept, emitted) packed in 16-bit halves (each <= 9 x 256): this thread's kept records go to the
+        // front of the iteration's region, its dropped ones become padding behind all kept records
+        const u32 nk = (u32)__popc(keep);
+        u32 tot;
+        const u32 off = block_exclusive_scan_u32(nk | (c << 16), lds_wave, &tot);
+        const u32 kept = tot & 0xffffu, total = tot >> 16;
+        u64 q = run + (off & 0xffffu);
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            if ((keep >> k) & 1u) out[q++] = rec[k];
+        u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
+        for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
+        run += total;
+    }
+}
+#undef RDF_UNIT_RECORDS
 
 // two passes over contiguous per-block chunks of triples: COUNT writes each block's record count, the
 // write pass places records at the scanned block offset + block-local prefix (no shared counter, and the
@@ -532,6 +674,57 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
         for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
         run += total;
+    }
+}
+
+// K3 over one join range's entry lists (m entries, entry_records)
+template <bool WRITE>
+__global__ __launch_bounds__(RDF_BLOCK) void k_emit_entries(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                            const u32* __restrict__ o, const u32* __restrict__ ent, u64 m,
+                                                            u64 m_s, u64 m_sp, u64 per, u32 V, u32 twoU,
+                                                            const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                                            const u32* __restrict__ lvals, u64 lmask, int joinbits,
+                                                            u64* block_counts, const u64* __restrict__ block_offsets,
+                                                            u64* out, int recbits) {
+    const JoinSel all{0u, 1u, 0u, JOIN_ALL_HI};
+    emit_records_body<WRITE, true>(s, p, o, ent, m_s, m_sp, m, per, V, twoU, frank, lkeys, lvals, lmask, 7, joinbits, all,
+                                   block_counts, block_offsets, out, recbits);
+}
+
+// (triple, attribute) entries of the join ranges: bin = range * 3 + attribute (0 s, 1 p, 2 o) of each projected join
+// value this rank takes, its range from the bucket -> range map (join >> jshift, JH_BUCKETS buckets).  Pass 1 counts
+// per (bin, block) -> ghist[bin * G + block]; pass 2 writes the triple indices at the scanned offsets (LDS cursors).
+// Each block takes one contiguous chunk of triples, so the entries of a bin ascend by block.
+static constexpr u32 JH_BUCKETS = 1u << 14;  // join buckets of the join-range build (join >> jshift)
+static constexpr u32 RE_MAX_BINS = 3 * 1024;
+template <bool SCATTER>
+__global__ __launch_bounds__(RDF_BLOCK) void k_range_entries(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                             const u32* __restrict__ o, u64 n, int proj, JoinSel own,
+                                                             int jshift, const uint16_t* __restrict__ bmap, u32 nbins,
+                                                             u32* ghist, u32* __restrict__ out) {
+    __shared__ uint16_t lmap[JH_BUCKETS];
+    __shared__ u32 lh[RE_MAX_BINS];
+    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lmap[k] = bmap[k];
+    for (u32 k = threadIdx.x; k < nbins; k += RDF_BLOCK) lh[k] = SCATTER ? ghist[(u64)k * gridDim.x + blockIdx.x] : 0u;
+    __syncthreads();
+    JoinSel all = own;
+    all.lo = 0u;
+    all.hi = JOIN_ALL_HI;
+    const u64 per = (n + gridDim.x - 1) / gridDim.x;
+    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
+        const u32 v[3] = {s[i], p[i], o[i]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (!((proj >> a) & 1) || !all.take(v[a])) continue;
+            const u32 bin = 3u * lmap[v[a] >> jshift] + (u32)a;
+            const u32 pos = atomicAdd(&lh[bin], 1u);
+            if (SCATTER) out[pos] = (u32)i;
+        }
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < nbins; k += RDF_BLOCK) ghist[(u64)k * gridDim.x + blockIdx.x] = lh[k];
     }
 }
 
@@ -657,7 +850,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_key_offsets(const u64* __restrict
 
 // records per join bucket (join >> jshift, JH_BUCKETS buckets): the K3 count pass's per-triple record counts split by
 // their join value (o, p or s of the triple), LDS-privatised
-static constexpr u32 JH_BUCKETS = 1u << 14;
 __global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_hist(const u32* __restrict__ s, const u32* __restrict__ p,
                                                               const u32* __restrict__ o, u64 n, u32 V, u32 twoU,
                                                               const u32* __restrict__ frank, const u64* __restrict__ lkeys,
@@ -666,7 +858,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_hist(const u32* __restr
     __shared__ u32 lh[JH_BUCKETS];
     for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lh[k] = 0;
     __syncthreads();
-    const JoinSel all = {own.rank, own.nranks, 0u, JOIN_ALL_HI};  // this rank's join values (sharded), every range
+    JoinSel all = own;  // this rank's join values (sharded: hash or hot-table owner), every range
+    all.lo = 0u;
+    all.hi = JOIN_ALL_HI;
     const u64 jmask = (1ull << joinbits) - 1;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         u64 rec[9];

@@ -9,6 +9,7 @@
 #include <vector>
 #include <utility>
 #include <initializer_list>
+#include <unordered_map>
 
 #include "../../include/rdfind_hip.h"
 #include "primitives.hpp"
@@ -66,10 +67,20 @@ struct rdf_ctx {
     struct JoinRange { u32 lo, hi; u64 recs; };
     std::vector<JoinRange> jranges;  // the current build's join ranges (pass 1 -> pass 2)
     u64 jr_cap_rec = 1;              // records of the largest range (the range scratch's size)
+    // per range (triple, attribute) entry lists (g_range_entries): a range's emissions read only its own triples
+    DevBuf jrmap, jrhist, jent;      // join bucket -> range, per (bin, block) counts, the entries (bin-major)
+    std::vector<u64> jr_bin;         // first entry of bin 3 range + attribute (+ the total)
+    bool jr_lists = false;           // the current range build emits from the entry lists
+    bool range_lists = false;        // RDFIND_RANGE_LISTS=1: emit each range from its entry lists (measured slower:
+                                     // the lists' triple gathers cost more than reading every triple)
     bool sh_ranged = false;          // the sharded build of this run goes in join ranges (sh_phase14 -> sh_phase1)
     u64 sh_m = 0;                    // sharded: triples received for this rank's join shard (wts / wtp / wto)
     std::string test_fail_launch;    // RDFIND_TEST_FAIL_LAUNCH: a kernel launched with an invalid configuration (test hook)
     int holder_qbits = 2;            // RDFIND_HOLDER_Q: pivot-holder election on log-size buckets (holder_key; 0: exact)
+    bool hot_balance = true;         // RDFIND_HOT_BALANCE=0: every join value's owner by hash (no hot table)
+    DevBuf hot, hotc;                // hot join values' owners (open-addressing table), this owner's candidates
+    u32 hot_mask = 0;                // table slots - 1 (0 with hot_n == 0: no table)
+    u64 hot_n = 0, sh_Bu = 0;        // hot values in the table; this owner's frequent unary keys (phase 16 -> 18)
     u64 group_range_records = 0;  // RDFIND_GROUP_RANGE test hook: records per join range (0: automatic)
     u64 n_group_ranges = 1;
     u64 J = 0, Jf = 0, G = 0, J_emit = 0;  // J: distinct-within-iteration records sorted; J_emit: records emitted
@@ -233,8 +244,8 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
 // every step cost seconds: c4 at 10^9 triples spent 4.3 of 6.4 s per step outside its kernels) and are released
 // only when an allocation of a later stage would otherwise fail.
 static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
-    DevBuf* fc_scratch[] = {&c->brkeys, &c->brkeys2, &c->tkeys, &c->urecs};
-    DevBuf* grp_scratch[] = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp};
+    const std::vector<DevBuf*> fc_scratch = {&c->brkeys, &c->brkeys2, &c->tkeys, &c->urecs};
+    const std::vector<DevBuf*> grp_scratch = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->jent};
     bool any = false;
     for (int k = 0; k < 2; ++k) {
         if (!(k == 0 ? c->spare_fc : c->spare_groups)) continue;
@@ -389,7 +400,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
                       &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
                       &c->gcap, &c->gmap, &c->csup,
-                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->lsup, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
+                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->lsup, &c->hot, &c->hotc, &c->jrmap, &c->jrhist, &c->jent, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
@@ -437,6 +448,8 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
         if (atoll(dm) > 0) c->dense_min = (u64)atoll(dm);
     if (const char* hq = getenv("RDFIND_HOLDER_Q")) c->holder_qbits = std::max(0, std::min(atoi(hq), 8));
     if (const char* tf = getenv("RDFIND_TEST_FAIL_LAUNCH")) c->test_fail_launch = tf;
+    if (const char* hb = getenv("RDFIND_HOT_BALANCE")) c->hot_balance = atoi(hb) != 0;
+    if (const char* rl = getenv("RDFIND_RANGE_LISTS")) c->range_lists = atoi(rl) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -1268,12 +1281,24 @@ static rdf_status g_record_bits(rdf_ctx* c) {
     return RDF_OK;
 }
 
+// this rank's join shard (sharded build; one GPU: every join value): the hash owner, or the hot table's
+static JoinSel shard_sel(const rdf_ctx* c) {
+    JoinSel js{c->rank, c->nranks, 0u, JOIN_ALL_HI};
+    if (c->nranks > 1 && c->hot_n) {
+        js.hot = c->hot.as<u64>();
+        js.hmask = c->hot_mask;
+    }
+    return js;
+}
+
 // K3 emission of the selected join values (record buffers of cap_rec slots), K4 sort by (capture, join), K5 run
 // bounds (cstart), fresh-record scan (fpos) and the records' supports -> sup[ncap].  The sorted records are left in
 // c->rec_sorted; *Jout = their number.  Adds to c->J_emit and c->sort_passes_records.
 // Join ranges (g_build_ranges) emit every range twice with the same selection: the first emission (cache = +1 + k,
 // range k) keeps the scanned per-block offsets and the slot count, the second (cache = -1 - k) reuses them instead of
 // re-running the count pass and its scan and read-back.  cache = 0: no reuse.
+// a range's cached block offsets: one fixed-size slot per range (the grid follows a range's entry count, <= kGrid)
+static constexpr u64 ECACHE_STRIDE = kGrid + 1ull;
 static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u32* sup, u64* Jout, int cache = 0) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
@@ -1284,39 +1309,71 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     ENSURE(c, rec, std::max<u64>(cap_rec, 1) * 8);
     ENSURE(c, rec_tmp, std::max<u64>(cap_rec, 1) * 8);
     tbegin(c, RDF_T_EMIT);
-    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
-    const u64 per = n ? (n + eg - 1) / eg : 0;
-    ENSURE(c, eblk, (eg + 1ull) * 8);
     const int slot = cache > 0 ? cache - 1 : cache < 0 ? -cache - 1 : -1;
+    // work units: every triple (js selects the join values), or the range's (triple, attribute) entries
+    const bool lists = c->jr_lists && slot >= 0 && 3 * (u64)slot + 3 < c->jr_bin.size();
+    u64 units = n, m_s = 0, m_sp = 0;
+    const u32* ent = nullptr;
+    if (lists) {
+        const u64 base = c->jr_bin[3 * slot];
+        units = c->jr_bin[3 * slot + 3] - base;
+        m_s = c->jr_bin[3 * slot + 1] - base;
+        m_sp = c->jr_bin[3 * slot + 2] - base;
+        ent = c->jent.as<u32>() + base;
+    }
+    const unsigned eg = grid_for(units, RDF_BLOCK, kGrid);
+    const u64 per = units ? (units + eg - 1) / eg : 0;
+    ENSURE(c, eblk, (eg + 1ull) * 8);
     const bool reuse = cache < 0 && slot < (int)c->ecache_je.size();
+    u64 je_early = ~0ull;  // the slot count, when read before the write pass
     if (cache > 0) {
         if ((int)c->ecache_je.size() <= slot) c->ecache_je.resize(slot + 1);
-        HIP_TRY(c, c->ecache.grow_keep((size_t)(slot + 1) * (eg + 1ull) * 8, st));
+        HIP_TRY(c, c->ecache.grow_keep((size_t)(slot + 1) * ECACHE_STRIDE * 8, st));
     }
-    if (n) {
+    if (units) {
         if (reuse) {
-            HIP_TRY(c, hipMemcpyAsync(c->eblk.p, c->ecache.as<u64>() + (u64)slot * (eg + 1ull), eg * 8ull,
+            HIP_TRY(c, hipMemcpyAsync(c->eblk.p, c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, eg * 8ull,
                                       hipMemcpyDeviceToDevice, st));
         } else {
-            hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
-                               c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
+            if (lists)
+                hipLaunchKernelGGL((k_emit_entries<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, ent, units, m_s,
+                                   m_sp, per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(),
+                                   c->lcap - 1, joinbits, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr,
+                                   capbits + joinbits);
+            else
+                hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                                   2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
+                                   joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
             HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
             if (cache > 0)
-                HIP_TRY(c, hipMemcpyAsync(c->ecache.as<u64>() + (u64)slot * (eg + 1ull), c->eblk.p, eg * 8ull,
+                HIP_TRY(c, hipMemcpyAsync(c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, c->eblk.p, eg * 8ull,
                                           hipMemcpyDeviceToDevice, st));
+            if (cap_rec < 9 * n) {  // a join range's buffers: the slot count is checked before the write pass
+                TRY(read_scalars(c, 1));
+                je_early = c->hscal[0];
+                if (je_early > cap_rec)
+                    return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
+            }
         }
-        hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                           c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
-                           (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+        if (lists)
+            hipLaunchKernelGGL((k_emit_entries<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, ent, units, m_s, m_sp,
+                               per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1,
+                               joinbits, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+        else
+            hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
+                               (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
     }
     tend(c, RDF_T_EMIT);
     u64 Je = 0;  // emitted record slots (repeats within an emission iteration are padding)
     if (reuse) {
         Je = c->ecache_je[slot];
     } else {
-        TRY(read_scalars(c, 1));
-        Je = c->hscal[0];
+        if (je_early == ~0ull) {
+            TRY(read_scalars(c, 1));
+            je_early = c->hscal[0];
+        }
+        Je = je_early;
         if (cache > 0) c->ecache_je[slot] = Je;
     }
     if (Je > cap_rec) return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
@@ -1353,7 +1410,7 @@ static rdf_status g_emit_sort_support(rdf_ctx* c, int proj) {
     c->sort_passes_records = 0;
     ENSURE(c, support, std::max<u64>(c->ncap, 1) * 4);
     u64 J = 0;
-    TRY(g_emit_range(c, proj, JoinSel{c->rank, c->nranks, 0u, JOIN_ALL_HI}, 9 * c->n, c->support.as<u32>(), &J));
+    TRY(g_emit_range(c, proj, shard_sel(c), 9 * c->n, c->support.as<u32>(), &J));
     c->J = J;
     return RDF_OK;
 }
@@ -1477,6 +1534,46 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
 //     join order, so goff / gcap / gmap / dgrp are exactly the one-pass build's.
 // One GPU runs the passes back to back (g_build_ranges).  A rank of a sharded run (own = its join shard) runs pass 1
 // on the triples it received, all-reduces the supports, and runs pass 2 (sh_phase14 -> sh_phase1).
+// The (triple, attribute) entries of every join range (k_range_entries: a count pass, a scan, a scatter pass over the
+// triples' join values only), so that each range's two emissions read its own triples instead of all of them: c4 at
+// 10^9 triples in 4 ranges read every triple 8 times.  12 B of entries per triple at most (3 attributes).
+static rdf_status g_range_entries(rdf_ctx* c, int proj, JoinSel own, int jshift) {
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
+    const u32 nr = (u32)ranges.size(), nbins = 3 * nr;
+    std::vector<uint16_t> bm(JH_BUCKETS);
+    u32 r = 0;
+    for (u32 b = 0; b < JH_BUCKETS; ++b) {
+        const u64 j0 = (u64)b << jshift;
+        while (r + 1 < nr && j0 >= ranges[r].hi) ++r;
+        bm[b] = (uint16_t)r;
+    }
+    ENSURE(c, jrmap, JH_BUCKETS * 2);
+    HIP_TRY(c, ctx_copy(c, c->jrmap.p, bm.data(), JH_BUCKETS * 2, hipMemcpyHostToDevice));
+    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>(2048, (n + 16383) / 16384));
+    const u64 nh = (u64)nbins * G;
+    ENSURE(c, jrhist, (nh + 1) * 4);
+    tbegin(c, RDF_T_EMIT);
+    hipLaunchKernelGGL((k_range_entries<false>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, proj, own, jshift,
+                       c->jrmap.as<uint16_t>(), nbins, c->jrhist.as<u32>(), (u32*)nullptr);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->jrhist.as<u32>(), c->jrhist.as<u32>(), nh, c->jrhist.as<u32>() + nh, st));
+    std::vector<u32> h(nh + 1);
+    HIP_TRY(c, ctx_copy(c, h.data(), c->jrhist.p, (nh + 1) * 4, hipMemcpyDeviceToHost));
+    const u64 total = h[nh];
+    ENSURE(c, jent, std::max<u64>(total, 1) * 4);
+    hipLaunchKernelGGL((k_range_entries<true>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, proj, own, jshift,
+                       c->jrmap.as<uint16_t>(), nbins, c->jrhist.as<u32>(), c->jent.as<u32>());
+    HIP_TRY(c, hipGetLastError());
+    tend(c, RDF_T_EMIT);
+    c->jr_bin.resize(nbins + 1);
+    for (u32 b = 0; b < nbins; ++b) c->jr_bin[b] = h[(u64)b * G];
+    c->jr_bin[nbins] = total;
+    c->jr_lists = true;
+    return RDF_OK;
+}
+
 static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel own) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
@@ -1520,6 +1617,9 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
         return fail(c, RDF_ERR_LIMIT, "one join bucket holds >= 2^32 capture records");
     c->jr_cap_rec = cap_rec;
     c->n_group_ranges = ranges.size();
+    c->jr_lists = false;
+    if (c->range_lists && ranges.size() > 1 && 3 * ranges.size() <= RE_MAX_BINS && n)
+        TRY(g_range_entries(c, proj, own, jshift));
     // 2. supports
     ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
     ENSURE(c, rsup, std::max<u64>(ncap, 1) * 4);
@@ -1529,7 +1629,10 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     for (size_t k = 0; k < ranges.size(); ++k) {
         const rdf_ctx::JoinRange& r = ranges[k];
         u64 J = 0;
-        TRY(g_emit_range(c, proj, JoinSel{own.rank, own.nranks, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
+        JoinSel js = own;
+        js.lo = r.lo;
+        js.hi = r.hi;
+        TRY(g_emit_range(c, proj, js, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
         Jtot += J;
         if (ncap)
             hipLaunchKernelGGL(k_add_u32, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->support.as<u32>(),
@@ -1584,7 +1687,10 @@ static rdf_status g_ranges_groups(rdf_ctx* c, int proj, JoinSel own, const u32* 
     for (size_t k = 0; k < ranges.size(); ++k) {
         const rdf_ctx::JoinRange& r = ranges[k];
         u64 J = 0;
-        TRY(g_emit_range(c, proj, JoinSel{own.rank, own.nranks, r.lo, r.hi}, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
+        JoinSel js = own;
+        js.lo = r.lo;
+        js.hi = r.hi;
+        TRY(g_emit_range(c, proj, js, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
         u64* keys = c->rec_sorted;
         tbegin(c, RDF_T_SUPPORT);
         ENSURE(c, flags, std::max<u64>(std::max<u64>(J, ncap), 1) * 4);
@@ -1655,13 +1761,17 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
 
 // records per join range of the automatic g_build_ranges: the range scratch (two record buffers, fresh flags + scan,
 // kept keys and their sort buffer, group flags + scan: <= 48 B per record) in the free HBM left after the stage's
-// global arrays (gcap + dgrp, <= 8 B per record overall), at most 2^31 (u32 scans inside a range)
+// global arrays (gcap + dgrp, <= 8 B per record overall), at most 2^31.  This sizes the ranges only: a range is
+// consecutive 2^(joinbits-14)-value join buckets, so one bucket larger than this (hot join values) makes a larger
+// range; the hard bound is the u32 record offsets inside a range (cstart, fpos: < 2^32 - 1 records, checked with
+// RDF_ERR_LIMIT), and a range's buffers are sized by the largest range (an allocation failure is RDF_ERR_OOM)
 static u64 auto_range_records(rdf_ctx* c) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1ull << 30;
     const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap;  // released by g_build_ranges
     const u64 avail = (u64)free_b + held;
-    const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30);  // ~4.5 records per triple kept
+    // ~4.5 records per triple kept; the ranges' entry lists (g_range_entries) up to 12 B per triple
+    const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30) + (c->range_lists ? 12 * c->n : 0);
     const u64 r = avail > global ? (avail - global) / 48 : 0;
     return std::max<u64>(std::min<u64>(r, 1ull << 31), 1ull << 24);
 }
@@ -3025,13 +3135,98 @@ static rdf_status sh_phase10(rdf_ctx* c, rdf_exchange* req) {
 }
 
 // received unary partials of this rank's keys -> summed -> frequent keys -> all-gather
+// hot join values (sharded): a value is hot with >= 1 / HOT_DIV of a rank's expected occurrences (so at most
+// HOT_DIV * N of them); an owner submits at most HOT_CAP candidate keys
+static constexpr u64 HOT_DIV = 4096;
+static constexpr u64 HOT_CAP = 32768;
+
 static rdf_status sh_phase16(rdf_ctx* c, rdf_exchange* req) {
+    hipStream_t st = c->stream;
     tbegin(c, RDF_T_UNARY);
     u64 Bu = 0, nk = 0;
-    TRY(fc_sum_pairs(c, c->xrecv.as<u64>(), nullptr, c->x_recv_count, &Bu, &nk, true, &c->ukeys));
+    const u64 m = c->x_recv_count;
+    TRY(fc_sum_pairs(c, c->xrecv.as<u64>(), nullptr, m, &Bu, &nk, true, &c->ukeys));
     tend(c, RDF_T_UNARY);
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ukeys.p, Bu, 11);
+    c->sh_Bu = Bu;
+    c->hot_n = 0;
+    c->hot_mask = 0;
+    if (!c->hot_balance || c->sh_nranks <= 1) {
+        HIP_TRY(c, hipStreamSynchronize(st));
+        return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ukeys.p, Bu, 11);
+    }
+    // hot join value candidates: this owner's summed keys of projected positions with >= |proj| n_local / HOT_DIV
+    // occurrences (a rank's share of the load is ~|proj| n_local), then all-gathered with every rank's slice size
+    // (phase 18 builds the same owner table on every rank from the same gathered words)
+    const u32 *s, *p, *o;
+    u64 n;
+    sh_slice(c, &s, &p, &o, &n);
+    const int np = __builtin_popcount((unsigned)c->sh_proj & 7u);
+    const u64 thr = std::max<u64>(1, (u64)np * n / (3 * HOT_DIV));  // a hot value may spread over 3 positions
+    const u64 tcap = next_pow2(std::max<u64>(1024, 2 * m));  // fc_sum_pairs' table (lkeys / lvals)
+    ENSURE(c, hotc, (HOT_CAP + 2) * 8);
+    HIP_TRY(c, hipMemsetAsync(c->hotc.as<u64>() + HOT_CAP + 1, 0, 8, st));
+    hipLaunchKernelGGL(k_hot_candidates, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->lkeys.as<u64>(),
+                       c->lvals.as<u32>(), tcap, c->V ? c->V : 1u, c->sh_proj, (u32)std::min<u64>(thr, 0xffffffffu),
+                       (u32)HOT_CAP, c->hotc.as<u64>() + 1, (u32*)(c->hotc.as<u64>() + HOT_CAP + 1));
+    HIP_TRY(c, hipGetLastError());
+    u32 k = 0;
+    TRY(read_u32(c, c->hotc.as<u64>() + HOT_CAP + 1, &k));
+    k = std::min<u32>(k, HOT_CAP);
+    c->hscal[14] = (0xffffffffull << 32) | n;  // marker word: this rank's slice size
+    HIP_TRY(c, ctx_copy(c, c->hotc.p, c->hscal + 14, 8, hipMemcpyHostToDevice));
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->hotc.p, 1ull + k, 18);
+}
+
+// every rank's hot candidates -> the hot join values' owners, identical on every rank: occurrences per value summed over
+// its positions, values with >= |proj| n_total / (N HOT_DIV) occurrences assigned largest first to the least loaded
+// rank (each rank starting from its expected share of the hashed rest; ties to the lower rank) -> c->hot; then the
+// frequent unary keys are all-gathered as before (phase 11)
+static rdf_status sh_phase18(rdf_ctx* c, rdf_exchange* req) {
+    const u64 cnt = c->x_recv_count;
+    const u32 V = c->V ? c->V : 1;
+    const u32 R = c->sh_nranks;
+    std::vector<u64> w(cnt);
+    if (cnt) HIP_TRY(c, ctx_copy(c, w.data(), c->xrecv.p, cnt * 8, hipMemcpyDeviceToHost));
+    u64 n_total = 0;
+    std::unordered_map<u32, u64> occ;
+    for (u64 x : w) {
+        const u64 key = x >> 32;
+        if (key == 0xffffffffull) {
+            n_total += (u32)x;
+            continue;
+        }
+        occ[(u32)(key % V)] += (u32)x;
+    }
+    const int np = __builtin_popcount((unsigned)c->sh_proj & 7u);
+    const double total = (double)np * (double)n_total;
+    const u64 thr = std::max<u64>(1, (u64)(total / ((double)R * HOT_DIV)));
+    std::vector<std::pair<u64, u32>> hot;  // (occurrences, value)
+    for (const auto& kv : occ)
+        if (kv.second >= thr) hot.push_back({kv.second, kv.first});
+    std::sort(hot.begin(), hot.end(), [](const std::pair<u64, u32>& a, const std::pair<u64, u32>& b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    c->hot_n = hot.size();
+    if (!hot.empty()) {
+        double hot_total = 0;
+        for (const auto& h : hot) hot_total += (double)h.first;
+        std::vector<double> load(R, std::max(0.0, total - hot_total) / R);
+        const u64 slots = next_pow2(std::max<u64>(64, 2 * hot.size()));
+        std::vector<u64> table(slots, EMPTY64);
+        for (const auto& h : hot) {
+            u32 r = 0;
+            for (u32 q = 1; q < R; ++q)
+                if (load[q] < load[r]) r = q;
+            load[r] += (double)h.first;
+            u32 slot = hot_slot(h.second, (u32)(slots - 1));
+            while (table[slot] != EMPTY64) slot = (slot + 1) & (u32)(slots - 1);
+            table[slot] = ((u64)h.second << 32) | r;
+        }
+        ENSURE(c, hot, slots * 8);
+        HIP_TRY(c, ctx_copy(c, c->hot.p, table.data(), slots * 8, hipMemcpyHostToDevice));
+        c->hot_mask = (u32)(slots - 1);
+    }
+    return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ukeys.p, c->sh_Bu, 11);
 }
 
 // every owner's frequent unary keys -> global ranks; local binary (key, count) partials -> all-to-all to the keys' owners
@@ -3113,10 +3308,11 @@ static rdf_status sh_route_triples(rdf_ctx* c, rdf_exchange* req) {
     ENSURE(c, uhist, ((u64)R * G + 1) * 4);
     ENSURE(c, xsend, std::max<u64>(6 * n, 1) * 8);  // <= 3 copies of 2 words
     tbegin(c, RDF_T_EMIT);
-    hipLaunchKernelGGL((k_route_triples<false>), dim3(G), dim3(RDF_BLOCK), 0, st, s, p, o, n, c->sh_proj, R,
+    const u64* hot = c->hot_n ? c->hot.as<u64>() : nullptr;
+    hipLaunchKernelGGL((k_route_triples<false>), dim3(G), dim3(RDF_BLOCK), 0, st, s, p, o, n, c->sh_proj, R, hot, c->hot_mask,
                        c->uhist.as<u32>(), (u64*)nullptr);
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), (u64)R * G, c->uhist.as<u32>() + (u64)R * G, st));
-    hipLaunchKernelGGL((k_route_triples<true>), dim3(G), dim3(RDF_BLOCK), 0, st, s, p, o, n, c->sh_proj, R,
+    hipLaunchKernelGGL((k_route_triples<true>), dim3(G), dim3(RDF_BLOCK), 0, st, s, p, o, n, c->sh_proj, R, hot, c->hot_mask,
                        c->uhist.as<u32>(), c->xsend.as<u64>());
     tend(c, RDF_T_EMIT);
     std::vector<u32> h((u64)R * G + 1);
@@ -3199,7 +3395,7 @@ static rdf_status sh_phase14(rdf_ctx* c, rdf_exchange* req) {
         ReceivedTriples rt(c);  // K3 reads the received triples; the resident input stays this rank's slice
         if (c->sh_ranged) {
             TRY(g_ranges_supports(c, c->sh_proj, c->group_range_records ? c->group_range_records : auto_range_records(c),
-                                  JoinSel{c->rank, c->nranks, 0u, JOIN_ALL_HI}));
+                                  shard_sel(c)));
             // this rank's supports, kept for pass 2 (the all-reduce brings the global ones)
             ENSURE(c, lsup, std::max<u64>(c->ncap, 1) * 4);
             HIP_TRY(c, hipMemcpyAsync(c->lsup.p, c->support.p, std::max<u64>(c->ncap, 1) * 4, hipMemcpyDeviceToDevice, st));
@@ -3215,7 +3411,7 @@ static rdf_status sh_phase1(rdf_ctx* c, rdf_exchange* req) {
     HIP_TRY(c, hipMemcpyAsync(c->support.p, c->xrecv.p, c->ncap * 4, hipMemcpyDeviceToDevice, c->stream));
     if (c->sh_ranged) {  // pass 2 of the join-range build, on the received triples again
         ReceivedTriples rt(c);
-        TRY(g_ranges_groups(c, c->sh_proj, JoinSel{c->rank, c->nranks, 0u, JOIN_ALL_HI}, c->lsup.as<u32>()));
+        TRY(g_ranges_groups(c, c->sh_proj, shard_sel(c), c->lsup.as<u32>()));
     } else {
         TRY(g_compact_groups(c));
     }
@@ -3886,7 +4082,7 @@ static rdf_status sh_phase32(rdf_ctx* c, rdf_exchange* req) {
 // phase that follows a collective
 static bool sh_phase_valid(int ph, bool pending) {
     if (ph >= 1 && ph <= 8) return true;
-    if (ph >= 11 && ph <= 17) return true;
+    if (ph >= 11 && ph <= 18) return true;
     if (ph >= 21 && ph <= 24) return true;
     if (ph >= 31 && ph <= 32) return true;
     return !pending && (ph == 10 || ph == 20 || ph == 30);
@@ -3988,6 +4184,7 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
         case 15: r = sh_phase15(c, req); break;
         case 16: r = sh_phase16(c, req); break;
         case 17: r = sh_phase17(c, req); break;
+        case 18: r = sh_phase18(c, req); break;
         case 20: r = sh_phase20(c, req); break;
         case 21: r = sh_phase21(c, req); break;
         case 22: r = sh_phase22(c, req); break;

@@ -9,13 +9,13 @@
 __device__ inline u32 key_owner(u64 key, u32 nranks) { return (u32)((mix64(key) & 0xffffffffull) % nranks); }
 
 // destinations of a triple: the distinct owners of its projected join values (at most 3)
-__device__ inline int triple_dests(u32 ts, u32 tp, u32 to, int proj, u32 nranks, u32 (&d)[3]) {
+__device__ inline int triple_dests(u32 ts, u32 tp, u32 to, int proj, u32 nranks, const u64* hot, u32 hmask, u32 (&d)[3]) {
     int k = 0;
     const u32 v[3] = {ts, tp, to};
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
         if (!(proj & (1 << t))) continue;
-        const u32 r = shard_of(v[t], nranks);
+        const u32 r = join_owner(v[t], nranks, hot, hmask);
         bool seen = false;
         for (int j = 0; j < k; ++j) seen |= d[j] == r;
         if (!seen) d[k++] = r;
@@ -28,7 +28,8 @@ __device__ inline int triple_dests(u32 ts, u32 tp, u32 to, int proj, u32 nranks,
 template <bool SCATTER>
 __global__ __launch_bounds__(RDF_BLOCK) void k_route_triples(const u32* __restrict__ s, const u32* __restrict__ p,
                                                              const u32* __restrict__ o, u64 n, int proj, u32 nranks,
-                                                             u32* ghist, u64* __restrict__ out) {
+                                                             const u64* __restrict__ hot, u32 hmask, u32* ghist,
+                                                             u64* __restrict__ out) {
     __shared__ u32 lh[RDF_MAX_RANKS];
     for (u32 i = threadIdx.x; i < nranks; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
     __syncthreads();
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_route_triples(const u32* __restri
     for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
         const u32 ts = s[i], tp = p[i], to = o[i];
         u32 d[3];
-        const int k = triple_dests(ts, tp, to, proj, nranks, d);
+        const int k = triple_dests(ts, tp, to, proj, nranks, hot, hmask, d);
         for (int j = 0; j < k; ++j) {
             const u32 pos = atomicAdd(&lh[d[j]], 1u);
             if (SCATTER) {
@@ -132,3 +133,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_ranks_from_keys(const u64* __rest
     }
 }
 
+
+// Hot join value candidates of this owner rank: its summed unary (key, count) table entries (key = pos * V + value)
+// whose position is projected and whose count reaches thr, as key << 32 | count (at most cap; *n counts them all)
+__global__ __launch_bounds__(RDF_BLOCK) void k_hot_candidates(const u64* __restrict__ tkeys, const u32* __restrict__ tcnt,
+                                                              u64 tcap, u32 V, int proj, u32 thr, u32 cap, u64* out, u32* n) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < tcap; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = tkeys[i];
+        if (k == EMPTY64) continue;
+        const u32 c = tcnt[i];
+        if (c < thr || !((proj >> (int)(k / V)) & 1)) continue;
+        const u32 slot = atomicAdd(n, 1u);
+        if (slot < cap) out[slot] = (k << 32) | c;
+    }
+}

@@ -304,28 +304,45 @@ def _gz_size(path):
     return n, last
 
 
-def _gz_slice(path, a, b):
-    """Decompressed bytes [a, b) of a .gz file, streamed: the bytes before a are discarded as they come."""
-    out, pos = [], 0
-    with gzip.open(path, "rb") as f:
-        while pos < b:
-            chunk = f.read(_GZ_STEP)
-            if not chunk:
-                break
-            lo, hi = max(a - pos, 0), min(b - pos, len(chunk))
-            if lo < hi:
-                out.append(chunk[lo:hi])
-            pos += len(chunk)
-    return b"".join(out)
+def _stream_from(files, start):
+    """(absolute offset, chunk) pairs of the concatenated input stream from byte `start` on: plain files are seeked,
+    a .gz file is decompressed once from its beginning (the bytes before `start` discarded as they come), and a file
+    without a final line break is followed by one."""
+    base = 0
+    for path, sz, gz in files:
+        if base + sz <= start:
+            base += sz
+            continue
+        skip = max(start - base, 0)
+        got = 0  # bytes of this file's stream part produced so far (from its byte `skip` on)
+        if gz:
+            pos = 0
+            with gzip.open(path, "rb") as f:
+                while chunk := f.read(_GZ_STEP):
+                    lo = max(skip - pos, 0)
+                    if lo < len(chunk):
+                        yield base + pos + lo, chunk[lo:]
+                        got += len(chunk) - lo
+                    pos += len(chunk)
+        else:
+            with open(path, "rb") as f:
+                f.seek(skip)
+                while chunk := f.read(_GZ_STEP):
+                    yield base + skip + got, chunk
+                    got += len(chunk)
+        if skip + got < sz:  # the virtual line break after a file without one
+            yield base + skip + got, b"\n"
+        base += sz
 
 
 def read_byte_range(paths, rank: int, nranks: int) -> bytes:
     """This rank's part of the input for the sharded ingest: the bytes of the whole lines that start in
     [T * rank / nranks, T * (rank + 1) / nranks) of the concatenated input of T bytes (read_bytes' stream: a line
     break after a file without one).  A line belongs to the rank its first byte falls to, so the parts partition the
-    lines (the reference's input splits, FLK/persistence/MultiFileTextInputFormat.java:49-100).  Plain files are
-    read by seeking to the range; a .gz file cannot be split, so it is stream-decompressed (once for its size, then up
-    to the end of the range) and only the range is kept: no rank holds a whole compressed input."""
+    lines (the reference's input splits, FLK/persistence/MultiFileTextInputFormat.java:49-100).  One forward pass from
+    the byte before the range finds its first line start, collects the range and stops at the first line start at or
+    after its end: plain files are seeked, a .gz file (which cannot be split) is decompressed once for its size and once
+    up to the end of the range, and only the range is kept: no rank holds a whole compressed input."""
     files = []  # (path, size of its stream part, gz)
     for path in paths:
         path = _plain_path(path)
@@ -340,45 +357,35 @@ def read_byte_range(paths, rank: int, nranks: int) -> bytes:
                     last = f.read(1)
                 else:
                     last = b"\n"
-            files.append((path, size + (0 if last == b"\n" else 1), None))
+            files.append((path, size + (0 if last == b"\n" else 1), False))
     total = sum(sz for _, sz, _ in files)
     lo, hi = total * rank // nranks, total * (rank + 1) // nranks
-
-    def read(a, b):  # stream bytes [a, b)
-        out, base = [], 0
-        for path, sz, data in files:
-            s0, s1 = max(a, base), min(b, base + sz)
-            if s0 < s1:
-                if data:
-                    chunk = _gz_slice(path, s0 - base, s1 - base)
-                    if len(chunk) < s1 - s0:  # the virtual line break after a file without one
-                        chunk += b"\n"
-                    out.append(chunk)
-                else:
-                    with open(path, "rb") as f:
-                        f.seek(s0 - base)
-                        chunk = f.read(s1 - s0)
-                    if len(chunk) < s1 - s0:  # the virtual line break after a file without one
-                        chunk += b"\n"
-                    out.append(chunk)
-            base += sz
-        return b"".join(out)
-
-    def line_start_at_or_after(x):  # first line start >= x (a line starts at 0 or right after a "\n")
-        if x <= 0:
-            return 0
-        pos = x - 1
-        step = 1 << 16
-        while pos < total:
-            chunk = read(pos, min(pos + step, total))
-            k = chunk.find(b"\n")
+    if lo >= total:
+        return b""
+    # a line starts at 0 or right after a "\n": the range's first line start is the first one >= lo, found from the
+    # byte before lo on; its end is the first line start >= hi (the total when hi reaches it)
+    b0 = 0 if lo == 0 else None
+    b1 = total if hi >= total else None
+    out = []
+    for pos, chunk in _stream_from(files, max(lo - 1, 0)):
+        if b0 is None:
+            k = chunk.find(b"\n", max(lo - 1 - pos, 0))
+            if k < 0:
+                continue
+            b0 = pos + k + 1
+        if b1 is None:
+            k = chunk.find(b"\n", max(hi - 1 - pos, 0))
             if k >= 0:
-                return pos + k + 1
-            pos += len(chunk)
-        return total
-
-    b0, b1 = line_start_at_or_after(lo), line_start_at_or_after(hi)
-    return read(b0, b1) if b0 < b1 else b""
+                b1 = pos + k + 1
+        end = len(chunk) if b1 is None else min(len(chunk), b1 - pos)
+        begin = max(b0 - pos, 0)
+        if begin < end:
+            out.append(chunk[begin:end])
+        if b1 is not None and pos + len(chunk) >= b1:
+            break
+    if b0 is None or b1 is None or b0 >= b1:
+        return b""
+    return b"".join(out)
 
 
 class HeapDictionary:

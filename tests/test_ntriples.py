@@ -114,3 +114,29 @@ def test_read_byte_range_partitions_lines(tmp_path):
         parts = [ntriples.read_byte_range(paths, r, nranks) for r in range(nranks)]
         assert b"".join(parts) == full, nranks
         assert all(not p or p.endswith(b"\n") for p in parts)
+
+
+def test_read_byte_range_small_chunks(tmp_path, monkeypatch):
+    """The one-pass range reader across chunk boundaries (chunks of 7 bytes), empty files, long lines and files
+    without a final line break: the ranks' parts still partition the stream's lines."""
+    import gzip
+    import random
+
+    monkeypatch.setattr(ntriples, "_GZ_STEP", 7)
+    rng = random.Random(3)
+    paths = []
+    for k in range(6):
+        lines = [b"<s%d> <p> \"%s\" ." % (i, b"x" * rng.randrange(0, 90)) for i in range(rng.randrange(0, 40))]
+        data = b"\n".join(lines) + (b"\n" if lines and rng.random() < 0.5 else b"")
+        path = tmp_path / (f"f{k}.nt.gz" if k % 2 else f"f{k}.nt")
+        if k % 2:
+            with gzip.open(path, "wb") as f:
+                f.write(data)
+        else:
+            path.write_bytes(data)
+        paths.append(str(path))
+    full = ntriples.read_bytes(paths)
+    for nranks in (1, 2, 3, 7, 13, 50, 400):
+        parts = [ntriples.read_byte_range(paths, r, nranks) for r in range(nranks)]
+        assert b"".join(parts) == full, nranks
+        assert all(not p or p.endswith(b"\n") for p in parts)
