@@ -18,6 +18,12 @@ result.  Default weak scaling: N GPUs run the config at N x scale (c2: LUBM-(100
 LUBM-100-sized share; `value` = all triples / max-over-ranks step time.  `roofline` is computed for the dominant
 kernel family from HIP events recorded on the library's stream; `cpu_baseline` times the C restatement
 (oracle/, OpenMP) on rank 0.
+
+`c4_strong` (default with the c2 workload; `--c4-strong off` skips it): BASELINE configs[3], c4 at 10^9 triples,
+split over the same N GPUs (strong scaling, the north-star scaling config), after the main leg: each rank draws only
+its 1/N of the rows, a rank whose join shard holds >= 2^32/9 triples builds its groups in join ranges, and the step is
+the same T_disc with every rank's result handed over.  It reports ms per step, triples/s, the ranks' work balance
+(max / mean) and the one-GPU c4 step of round 4 (1.616 s) as its reference; `value` stays the c2 leg's.
 """
 from __future__ import annotations
 

@@ -382,7 +382,14 @@ static constexpr int B2_SUB_MAX = 4;
 __device__ inline u32 b2_sub(u64 rec, int bits, int sub) {
     return (u32)(mix64(rec & ~B2_CBITS) >> (64 - bits - sub)) & ((1u << sub) - 1);
 }
-static constexpr int B2_SPLIT_R = 8;  // records per lane in flight in k_b2_split
+#ifndef RDF_B2_SPLIT_R
+#define RDF_B2_SPLIT_R 8
+#endif
+static constexpr int B2_SPLIT_R = RDF_B2_SPLIT_R;  // records per lane in flight in k_b2_split
+#ifndef RDF_B2_SPLIT_GRID
+#define RDF_B2_SPLIT_GRID 4096
+#endif
+static constexpr unsigned B2_SPLIT_GRID = RDF_B2_SPLIT_GRID;  // k_b2_split blocks (each loops over buckets)
 
 // lanes of the wave with the same sub-bucket j (j < 2^sub; inactive lanes pass j = 1 << sub and get 0)
 __device__ inline u64 sub_peers(u32 j, int sub) {

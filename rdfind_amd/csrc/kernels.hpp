@@ -48,7 +48,7 @@ static constexpr u64 LIGHT_PACK_MAXG = 32;  // dependents with at most this many
 static constexpr u64 LIGHT_PACK_MAXG2 = RDF_PACK_MAXG2;  // ... and those with at most this many groups of
 static constexpr u32 LIGHT_PACK_NL = RDF_PACK_NL;        // which at most this many are light
 #ifndef RDF_LIGHT_BATCH
-#define RDF_LIGHT_BATCH 8
+#define RDF_LIGHT_BATCH 4  // 8 before round 5: c2 light 2.52 -> 2.21 ms, c3 at 0.5 7.33 -> 7.12, c4 at 0.4 64.2 -> 60.1 (profiles/r05_light_ab_batch.log)
 #endif
 static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched together in k_light
 #ifndef RDF_LIGHT_SERIAL

@@ -186,6 +186,7 @@ struct rdf_ctx {
     bool pend_fc = false, pend_groups = false;
     bool pend_heavy = false;
     bool spare_fc = false, spare_groups = false;  // reclaim_spare may release these stages' scratch
+    bool spare_x = false;  // ... and the exchange buffers, from the routing of the triples to the end of the group build
     DevBuf ecache;                   // join ranges: each range's scanned K3 block offsets from its first emission
     std::vector<u64> ecache_je;      // ... and its record-slot count  // heavy threshold / count of the last group build still on the device (hist + 256, + 258)
     // per kernel-family device timers (events on the context stream)
@@ -246,10 +247,11 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
 static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
     const std::vector<DevBuf*> fc_scratch = {&c->brkeys, &c->brkeys2, &c->tkeys, &c->urecs};
     const std::vector<DevBuf*> grp_scratch = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->jent};
+    const std::vector<DevBuf*> x_scratch = {&c->xsend, &c->xrecv};
     bool any = false;
-    for (int k = 0; k < 2; ++k) {
-        if (!(k == 0 ? c->spare_fc : c->spare_groups)) continue;
-        for (DevBuf* b : (k == 0 ? fc_scratch : grp_scratch)) {
+    for (int k = 0; k < 3; ++k) {
+        if (!(k == 0 ? c->spare_fc : k == 1 ? c->spare_groups : c->spare_x)) continue;
+        for (DevBuf* b : (k == 0 ? fc_scratch : k == 1 ? grp_scratch : x_scratch)) {
             if (b == keep || !b->p) continue;
             if (!any) (void)hipStreamSynchronize(c->stream);  // queued kernels may still read them
             b->release();
@@ -981,7 +983,7 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
         ENSURE(c, bstart2, ((u64)NBc + 1) * 4);
         // RDFIND_TEST_FAIL_LAUNCH=k_b2_split (test hook): launched with an invalid block size, so the launch fails
         const unsigned sblock = c->test_fail_launch == "k_b2_split" ? 4 * 1024 : RDF_BLOCK;
-        hipLaunchKernelGGL(k_b2_split, dim3(std::min<u32>(NB2, 4096)), dim3(sblock), 0, st, c->brkeys.as<u64>(),
+        hipLaunchKernelGGL(k_b2_split, dim3(std::min<u32>(NB2, B2_SPLIT_GRID)), dim3(sblock), 0, st, c->brkeys.as<u64>(),
                            c->uhist.as<u32>(), NB2, G2, bits, sub, c->brkeys2.as<u64>(), c->bstart2.as<u32>());
         // bstart2 (the sub-bucket starts) is consumed as record offsets by k_b2_slices and k_b2_count: a launch that
         // did not run must stop here (the round-4 aperture violation in rdf_frequent_conditions was a count kernel
@@ -1768,7 +1770,9 @@ static rdf_status g_build_ranges(rdf_ctx* c, int proj, u64 max_range) {
 static u64 auto_range_records(rdf_ctx* c) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1ull << 30;
-    const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap;  // released by g_build_ranges
+    // spare buffers an allocation of the build may release (reclaim_spare)
+    const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap +
+                     (c->spare_x ? (u64)c->xsend.cap + c->xrecv.cap : 0ull);
     const u64 avail = (u64)free_b + held;
     // ~4.5 records per triple kept; the ranges' entry lists (g_range_entries) up to 12 B per triple
     const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30) + (c->range_lists ? 12 * c->n : 0);
@@ -3384,6 +3388,10 @@ static rdf_status sh_phase14(rdf_ctx* c, rdf_exchange* req) {
     if (m)
         hipLaunchKernelGGL(k_unpack_triples, dim3(grid_for(m, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->xrecv.as<u64>(), m,
                            c->wts.as<u32>(), c->wtp.as<u32>(), c->wto.as<u32>());
+    // the routing's exchange buffers (16 B per received copy, 48 B per slice triple: ~45 GB per rank for c4 at 10^9
+    // triples over 2 ranks) hold nothing the group build reads: spare until the build ends (phase 1), released only
+    // if one of its allocations would fail (re-allocating them every step would cost more than keeping them)
+    c->spare_x = true;
     c->rank = c->sh_rank;
     c->nranks = c->sh_nranks;
     c->sh_m = m;
@@ -3415,6 +3423,7 @@ static rdf_status sh_phase1(rdf_ctx* c, rdf_exchange* req) {
     } else {
         TRY(g_compact_groups(c));
     }
+    c->spare_x = false;  // the exchange buffers carry the collectives again
     if (c->ar_on) TRY(g_ar_refs(c));
     TRY(g_size_hist(c, c->h_hist_local));
     ENSURE(c, xsend, 256 * 8);
@@ -4103,6 +4112,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
     c->sh_flags = flags;
     c->sh_phase = 10;
     c->x_imported = true;
+    c->spare_x = false;  // (a run that failed between phases 14 and 1 left them marked)
     c->stage = std::min(c->stage, 1);
     c->paged = false;
     return RDF_OK;

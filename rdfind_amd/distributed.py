@@ -5,6 +5,8 @@ the library requests one at a time (``rdf_shard_step``):
 
   a. all-to-all       unary (key, count) partials of the slices to the key's owner rank, which sums them
                       (FrequentConditionPlanner.scala:293-309)
+  a''. all-gather     (world > 1) each owner's hot join value candidates and every rank's slice size: every rank
+                      derives the same owner table for the hottest join values (balanced, largest first)
   a'. all-gather      the frequent unary keys of every owner (sorted afterwards: global ranks)
   b. all-to-all       binary (key, count) partials to the key's owner rank, which sums them (:381-393)
   c. all-gather       the frequent binary keys of every owner (sorted afterwards: deterministic ids)
@@ -145,9 +147,18 @@ def exchange_device(group=None) -> torch.device:
     return torch.device("cpu")
 
 
+_BIG_EXCHANGE_BYTES = 1 << 30  # a collective above this (the triples' routing at 10^9-triple scale) is not cached
+
+
 def _send_buffer(machine, n, dtype, device):
     """The rank's send buffer for one collective: a view of a persistent buffer per (dtype, device), grown by half
-    again when a collective needs more (the 14 collectives of a run reuse it instead of allocating each time)."""
+    again when a collective needs more (the collectives of a run reuse it instead of allocating each time).  A send of
+    more than _BIG_EXCHANGE_BYTES gets a buffer of its own, released after the collective, so the one large exchange of a
+    run (the triples to their join owners: ~21 GB per rank for c4 at 10^9 triples over 2 ranks) does not stay allocated
+    through the group build that follows it."""
+    elem = torch.empty(0, dtype=dtype).element_size()
+    if n * elem > _BIG_EXCHANGE_BYTES:
+        return torch.empty(n, dtype=dtype, device=device)
     bufs = machine.__dict__.setdefault("_x_send", {})
     key = (dtype, device.type, device.index)
     b = bufs.get(key)
@@ -184,6 +195,10 @@ def run_protocol(machine, group=None, device=None):
         sent += send.numel() * send.element_size()
         received += recv.numel() * recv.element_size()
         machine.shard_import(recv.data_ptr(), recv.numel())
+        big = max(send.numel() * send.element_size(), recv.numel() * recv.element_size()) > _BIG_EXCHANGE_BYTES
+        del send, recv
+        if big and device.type == "cuda":  # give the large exchange's HBM back to the library's allocations
+            torch.cuda.empty_cache()
         n += 1
 
 
