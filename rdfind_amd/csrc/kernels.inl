@@ -400,21 +400,31 @@ __device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u
 // splitAndCollectUnaryCaptures).  Record = capture << joinbits | join: sorted, a capture's records are
 // contiguous, so its support is a run length (no atomics) and its join list is the dependent -> groups CSR.
 
-// records of triple i (at most 9); returns the count
+// records of triple i (at most 9); returns the count.  LAZY: load only the condition ranks the taken join values'
+// records need (join ranges, shards: a selection takes a fraction of the join values, and the random rank loads bound
+// the emission: c4 at 10^9 triples 457 -> 401 ms); without it all three are loaded up front (one GPU, one pass: the
+// lazy form cost c2's emission 0.80 -> 0.91 ms)
 // rep (optional): bit k set for the records that repeat across triples of one subject or one (predicate, object) pair
 // (p[s], s[p], o[p], p[o]: the same predicate twice for a subject, the same typed object for many subjects); the others
 // (o[s], s[o] and the binary captures) practically never repeat within an emission iteration
+template <bool LAZY>
 __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
                                      u32 V, u32 twoU, const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                      const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, JoinSel js,
                                      u64 (&rec)[9], u32* rep = nullptr) {
     u32 c = 0, rp_mask = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
-    // the join values this selection takes; only the condition ranks their records need are loaded (a join range
-    // takes a fraction of the join values: the random frank loads, not the coalesced triple reads, bound its emission)
     const bool jo = (proj & 4) && js.take(to), jp = (proj & 2) && js.take(tp), js_ = (proj & 1) && js.take(ts);
-    const u32 rs = jo || jp ? frank[ts] : NONE32, rp = jo || js_ ? frank[(u64)V + tp] : NONE32,
-              ro = jp || js_ ? frank[2ull * V + to] : NONE32;  // global condition ranks (or NONE)
+    u32 rs, rp, ro;  // global condition ranks (or NONE)
+    if (LAZY) {
+        rs = jo || jp ? frank[ts] : NONE32;
+        rp = jo || js_ ? frank[(u64)V + tp] : NONE32;
+        ro = jp || js_ ? frank[2ull * V + to] : NONE32;
+    } else {
+        rs = frank[ts];
+        rp = frank[(u64)V + tp];
+        ro = frank[2ull * V + to];
+    }
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
     if (jo) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
         if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
@@ -499,7 +509,7 @@ __device__ inline void emit_records_body(const u32* __restrict__ s, const u32* _
     const u64 e = b + per < n ? b + per : n;
 #define RDF_UNIT_RECORDS(i, rec, rep)                                                                                  \
     (ENTRIES ? entry_records(i, ent, m_s, m_sp, s, p, o, V, twoU, frank, lkeys, lvals, lmask, joinbits, rec, rep)        \
-             : triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, rep))
+             : triple_records<false>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, rep))
     if (!WRITE) {  // the block's record count: per-thread sums, one block reduction at the end
         u32 mine = 0;
         for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
@@ -585,7 +595,7 @@ __device__ inline void emit_records_body(const u32* __restrict__ s, const u32* _
 // two passes over contiguous per-block chunks of triples: COUNT writes each block's record count, the
 // write pass places records at the scanned block offset + block-local prefix (no shared counter, and the
 // record order is deterministic)
-template <bool WRITE>
+template <bool WRITE, bool LAZY>
 __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restrict__ s, const u32* __restrict__ p,
                                                             const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
                                                             const u32* __restrict__ frank, const u64* __restrict__ lkeys,
@@ -600,7 +610,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         u32 mine = 0;
         for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
             u64 rec[9];
-            mine += triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec);
+            mine += triple_records<LAZY>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec);
         }
         u32 total;
         block_exclusive_scan_u32(mine, lds_wave, &total);
@@ -621,7 +631,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
         u32 c = 0, rep = 0;
-        if (i < e) c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, &rep);
+        if (i < e) c = triple_records<LAZY>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, &rep);
         // Records repeated within the iteration's 256 triples (the same subject's predicate, the same (predicate,
         // object) pair: ~23 % of c2's records; only the kinds flagged by triple_records are looked up) are written
         // once; the count pass's region stays as it is and its tail is padded with EMIT_PAD, which the record sort's
@@ -737,14 +747,32 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_range_entries(const u32* __restri
 // Sorted (capture << joinbits | join) records: fresh[i] = keys[i] differs from keys[i - 1] (a distinct
 // (capture, join) pair), and the capture runs' bounds: cstart[c] = first record of capture c, for every
 // c in [0, ncap] (captures without records get the next run's start; cstart[ncap] = n).
+// Streaming kernels over the sorted records take STREAM_U elements per thread per step, their loads issued together
+// (element step * U * T + u * T + thread: every load instruction stays coalesced).  One element per thread per step
+// kept ~16 KB in flight per CU, which at 10^9-triple sizes (arrays far beyond the MALL) held these kernels near
+// 1.5-2 TB/s.
+static constexpr int STREAM_U = 4;
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_fresh_bounds(const u64* __restrict__ keys, u64 n, u64 ncap, int joinbits,
                                                             u32* fresh, u32* cstart) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= n; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 k = i < n ? keys[i] : 0ull, kp = i ? keys[i - 1] : 0ull;
-        if (i < n) fresh[i] = (i == 0 || kp != k) ? 1u : 0u;
-        const u64 c = i < n ? k >> joinbits : ncap;
-        const u64 cp = i ? (kp >> joinbits) + 1 : 0;
-        for (u64 x = cp; x <= c; ++x) cstart[x] = (u32)i;
+    const u64 T = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 i0 = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i0 <= n; i0 += T * STREAM_U) {
+        u64 k[STREAM_U], kp[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            k[u] = i < n ? keys[i] : 0ull;
+            kp[u] = i && i <= n ? keys[i - 1] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            if (i > n) break;
+            if (i < n) fresh[i] = (i == 0 || kp[u] != k[u]) ? 1u : 0u;
+            const u64 c = i < n ? k[u] >> joinbits : ncap;
+            const u64 cp = i ? (kp[u] >> joinbits) + 1 : 0;
+            for (u64 x = cp; x <= c; ++x) cstart[x] = (u32)i;
+        }
     }
 }
 
@@ -796,21 +824,45 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_keep_scatter(const u64* __restric
                                                             const u32* __restrict__ support, u32 ms,
                                                             const u32* __restrict__ fidx, u64* dk, u64* fk) {
     const u64 jmask = (1ull << joinbits) - 1;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 k = keys[i];
-        if (i && keys[i - 1] == k) continue;
-        const u64 cap = k >> joinbits;
-        if (support[cap] < ms) continue;
-        const u64 p = fpos[i] - skip[cap];
-        const u64 c = fidx[cap], j = k & jmask;
-        dk[p] = (c << 32) | j;
-        fk[p] = (j << 32) | c;
+    const u64 T = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 i0 = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i0 < n; i0 += T * STREAM_U) {
+        u64 k[STREAM_U], kp[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            k[u] = i < n ? keys[i] : 0ull;
+            kp[u] = i && i < n ? keys[i - 1] : ~k[u];
+        }
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            if (i >= n || kp[u] == k[u]) continue;
+            const u64 cap = k[u] >> joinbits;
+            if (support[cap] < ms) continue;
+            const u64 p = fpos[i] - skip[cap];
+            const u64 c = fidx[cap], j = k[u] & jmask;
+            dk[p] = (c << 32) | j;
+            fk[p] = (j << 32) | c;
+        }
     }
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_group_flags(const u64* __restrict__ fk, u64 n, u32* flags) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
-        flags[i] = (i == 0 || (fk[i - 1] >> 32) != (fk[i] >> 32)) ? 1u : 0u;
+    const u64 T = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 i0 = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i0 < n; i0 += T * STREAM_U) {
+        u64 a[STREAM_U], b[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            a[u] = i < n ? fk[i] >> 32 : 0ull;
+            b[u] = i && i < n ? fk[i - 1] >> 32 : ~a[u];
+        }
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            if (i < n) flags[i] = a[u] != b[u] ? 1u : 0u;
+        }
+    }
 }
 
 // groups: goff[g] = first record; gcap[i] = compact capture id; gmap[join] = g (fk = join << 32 | capture)
@@ -830,8 +882,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_build(const u64* __restrict
 // dependent -> groups: dgrp[i] = group of the join value of dk[i].  A capture's joins ascend and group ids
 // are assigned in join order, so every dependent's group list comes out sorted.
 __global__ __launch_bounds__(RDF_BLOCK) void k_dgrp(const u64* __restrict__ dk, u64 n, const u32* __restrict__ gmap, u32* dgrp) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK)
-        dgrp[i] = gmap[(u32)dk[i]];
+    const u64 T = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 i0 = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i0 < n; i0 += T * STREAM_U) {
+        u32 j[STREAM_U], g[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) j[u] = i0 + (u64)u * T < n ? (u32)dk[i0 + (u64)u * T] : 0u;
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) g[u] = i0 + (u64)u * T < n ? gmap[j[u]] : 0u;
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u)
+            if (i0 + (u64)u * T < n) dgrp[i0 + (u64)u * T] = g[u];
+    }
 }
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_info_support_u32(const CapInfo* __restrict__ info, u32 C, u32* out) {
@@ -864,7 +925,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_hist(const u32* __restr
     const u64 jmask = (1ull << joinbits) - 1;
     for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
         u64 rec[9];
-        const u32 c = triple_records(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, all, rec);
+        const u32 c = triple_records<false>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, all, rec);
         // a triple's records are grouped by join value (o, then p, then s): one LDS atomic per run
         u32 k = 0;
         while (k < c) {
@@ -900,10 +961,23 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_build_at(const u64* __restr
 __global__ __launch_bounds__(RDF_BLOCK) void k_dgrp_range(const u64* __restrict__ dk, u64 n, const u64* __restrict__ offp,
                                                           const u64* __restrict__ doff, const u32* __restrict__ dcur,
                                                           const u32* __restrict__ gmap, u32* dgrp) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 k = dk[i];
-        const u32 d = (u32)(k >> 32);
-        dgrp[doff[d] + dcur[d] + (i - offp[d])] = gmap[(u32)k];
+    const u64 T = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 i0 = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i0 < n; i0 += T * STREAM_U) {
+        u64 k[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) k[u] = i0 + (u64)u * T < n ? dk[i0 + (u64)u * T] : 0ull;
+        u32 g[STREAM_U];
+        u64 at[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            const u32 d = (u32)(k[u] >> 32);
+            g[u] = i < n ? gmap[(u32)k[u]] : 0u;
+            at[u] = i < n ? doff[d] + dcur[d] + (i - offp[d]) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u)
+            if (i0 + (u64)u * T < n) dgrp[at[u]] = g[u];
     }
 }
 

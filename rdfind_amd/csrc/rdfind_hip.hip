@@ -420,6 +420,26 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
             &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout};
 }
 
+// RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout"};
+static void mem_report(rdf_ctx* c) {
+    static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
+    if (!on) return;
+    std::vector<DevBuf*> bufs = ctx_buffers(c);
+    std::vector<std::pair<size_t, const char*>> big;
+    size_t total = 0;
+    for (size_t i = 0; i < bufs.size(); ++i) {
+        total += bufs[i]->cap;
+        if (bufs[i]->cap >= (256ull << 20)) big.push_back({bufs[i]->cap, i < sizeof(kBufNames) / sizeof(kBufNames[0]) ? kBufNames[i] : "?"});
+    }
+    std::sort(big.begin(), big.end(), [](const std::pair<size_t, const char*>& x, const std::pair<size_t, const char*>& y) {
+        return x.first > y.first;
+    });
+    fprintf(stderr, "MEM total %.2f GiB (workspace %.2f GiB):", total / 1073741824.0, c->ws.bytes() / 1073741824.0);
+    for (const auto& b : big) fprintf(stderr, " %s=%.2f", b.second, b.first / 1073741824.0);
+    fprintf(stderr, "\n");
+}
+
 extern "C" {
 
 const char* rdf_version(void) { return RDF_VERSION; }
@@ -1312,6 +1332,8 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     ENSURE(c, rec_tmp, std::max<u64>(cap_rec, 1) * 8);
     tbegin(c, RDF_T_EMIT);
     const int slot = cache > 0 ? cache - 1 : cache < 0 ? -cache - 1 : -1;
+    // the selection takes a part of the join values (a join range, or a rank's shard): lazy condition-rank loads
+    const bool lazy = js.nranks > 1 || js.lo != 0u || js.hi != JOIN_ALL_HI;
     // work units: every triple (js selects the join values), or the range's (triple, attribute) entries
     const bool lists = c->jr_lists && slot >= 0 && 3 * (u64)slot + 3 < c->jr_bin.size();
     u64 units = n, m_s = 0, m_sp = 0;
@@ -1342,8 +1364,12 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
                                    m_sp, per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(),
                                    c->lcap - 1, joinbits, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr,
                                    capbits + joinbits);
+            else if (lazy)
+                hipLaunchKernelGGL((k_emit_records<false, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                                   2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
+                                   joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
             else
-                hipLaunchKernelGGL((k_emit_records<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                hipLaunchKernelGGL((k_emit_records<false, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                    2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
                                    joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
             HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
@@ -1361,10 +1387,14 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
             hipLaunchKernelGGL((k_emit_entries<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, ent, units, m_s, m_sp,
                                per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1,
                                joinbits, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+        else if (lazy)
+            hipLaunchKernelGGL((k_emit_records<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                               2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
+                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
         else
-            hipLaunchKernelGGL((k_emit_records<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
-                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, js,
-                               (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+            hipLaunchKernelGGL((k_emit_records<true, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                               2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
+                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
     }
     tend(c, RDF_T_EMIT);
     u64 Je = 0;  // emitted record slots (repeats within an emission iteration are padding)
@@ -3063,6 +3093,7 @@ rdf_status rdf_run(rdf_ctx* c, uint32_t min_support, const char* projection, uin
     if (r) return r;
     TRY(settle_group_stats(c));
     if (gs) *gs = c->gstats;
+    mem_report(c);
     return RDF_OK;
 }
 
@@ -3836,6 +3867,7 @@ static rdf_status sh_phase8(rdf_ctx* c, rdf_exchange* req) {
     memset(req, 0, sizeof(*req));
     req->op = RDF_X_DONE;
     c->sh_phase = 9;
+    mem_report(c);
     return RDF_OK;
 }
 

@@ -10,3 +10,6 @@ RDFIND_AB_LIBS=librdfind_hip.so,librdfind_hip_sg32k.so,librdfind_hip_sr16.so,lib
 echo done
 RDFIND_AB_LIBS=librdfind_hip.so,librdfind_hip_ps8.so,librdfind_hip_ps2.so,librdfind_hip_ser8.so,librdfind_hip_ser2.so timeout -k 10 600 python -u tools/light_ab.py c2:1.0 c3:0.5 c4:0.4 c5:0.1 > gpurun_out/light_ab2_r05i.log 2>&1 || { tail -20 gpurun_out/light_ab2_r05i.log; exit 1; }
 echo done2
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r05i_c2only -o run --output-format csv -- python3 bench.py --no-cpu-baseline --c4-strong off > gpurun_out/prof_r05i_c2only.log 2>&1 || { tail -20 gpurun_out/prof_r05i_c2only.log; exit 1; }
+find gpurun_out/prof_r05i_c2only -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_r05i_c2only.kernel_stats.csv \;
+echo done3
