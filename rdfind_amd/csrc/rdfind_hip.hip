@@ -76,6 +76,7 @@ struct rdf_ctx {
     bool sh_ranged = false;          // the sharded build of this run goes in join ranges (sh_phase14 -> sh_phase1)
     u64 sh_m = 0;                    // sharded: triples received for this rank's join shard (wts / wtp / wto)
     std::string test_fail_launch;    // RDFIND_TEST_FAIL_LAUNCH: a kernel launched with an invalid configuration (test hook)
+    bool test_oom_discovery = false; // RDFIND_TEST_OOM_DISCOVERY: rdf_discover_cinds fails with RDF_ERR_OOM (test hook)
     int holder_qbits = 2;            // RDFIND_HOLDER_Q: pivot-holder election on log-size buckets (holder_key; 0: exact)
     bool hot_balance = true;         // RDFIND_HOT_BALANCE=0: every join value's owner by hash (no hot table)
     DevBuf hot, hotc;                // hot join values' owners (open-addressing table), this owner's candidates
@@ -470,6 +471,7 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
         if (atoll(dm) > 0) c->dense_min = (u64)atoll(dm);
     if (const char* hq = getenv("RDFIND_HOLDER_Q")) c->holder_qbits = std::max(0, std::min(atoi(hq), 8));
     if (const char* tf = getenv("RDFIND_TEST_FAIL_LAUNCH")) c->test_fail_launch = tf;
+    if (const char* to = getenv("RDFIND_TEST_OOM_DISCOVERY")) c->test_oom_discovery = atoi(to) != 0;
     if (const char* hb = getenv("RDFIND_HOT_BALANCE")) c->hot_balance = atoi(hb) != 0;
     if (const char* rl = getenv("RDFIND_RANGE_LISTS")) c->range_lists = atoi(rl) != 0;
     hipError_t e = hipSetDevice(device);
@@ -2786,6 +2788,9 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
     c->paged = false;
+    // test hook (RDFIND_TEST_OOM_DISCOVERY=1): the unpaged discovery reports RDF_ERR_OOM at once, so a caller's
+    // fallback to pages runs on small inputs
+    if (c->test_oom_discovery) return fail(c, RDF_ERR_OOM, "test hook: the unpaged discovery runs out of memory");
     hipStream_t st = c->stream;
     CindView v = make_view(c, flags);
     TRY(d_pivot_local(c, v));

@@ -88,3 +88,22 @@ def test_program_pages_written_lines_vs_oracle(tmp_path):
     want = lines_of(rows, d.terms.term)
     assert len(got) == len(want) == 2698238
     assert sorted(got) == want
+
+
+@pytest.mark.timeout(300)
+def test_program_oom_fallback_writes_output(tmp_path, monkeypatch):
+    """The driver's RDF_ERR_OOM fallback with --output: the unpaged discovery fails (RDFIND_TEST_OOM_DISCOVERY, read when
+    the context is created), the driver continues in pages and writes the same lines as a run without the hook.  Only
+    the discovery is inside the fallback's try: the output is written once (no truncated-then-rewritten file)."""
+    d = synth.config("c1", 0.05)
+    nt = tmp_path / "c1.nt"
+    write_text(d, nt)
+    common = ["--use-fis", "--clean-implied", "--support", str(d.min_support)]
+    a, b = tmp_path / "fallback.txt", tmp_path / "plain.txt"
+    run_program(common + ["--output", f"file://{b}", str(nt)])
+    monkeypatch.setenv("RDFIND_TEST_OOM_DISCOVERY", "1")
+    prog, out = run_program(common + ["--debug-level", "1", "--output", f"file://{a}", str(nt)])
+    assert prog.stats["pages"] >= 1
+    la, lb = a.read_text().splitlines(), b.read_text().splitlines()
+    assert len(la) == len(lb) > 1000
+    assert sorted(la) == sorted(lb)
