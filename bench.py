@@ -261,7 +261,7 @@ def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):
         gs = ctx.groups
         kt = {k: v / steps for k, v in kt_sum.items()}
         mine = {"triples": n_local, "records": gs["n_records"], "join_ranges": gs.get("n_join_ranges", 1),
-                "groups": gs["n_groups"], "light_chunks": cs["n_light_chunks"], "explicit_raw": cs["n_explicit_raw"],
+                "ranges_kept": gs.get("n_ranges_kept", 0), "groups": gs["n_groups"], "light_chunks": cs["n_light_chunks"], "explicit_raw": cs["n_explicit_raw"],
                 "cinds": cs["n_cinds"], "light_ms": round(kt.get("light", 0.0), 3),
                 "kernel_ms": round(sum(kt.values()), 3), "hbm_held_gib": round(ctx.device_bytes() / 2**30, 1),
                 **{k: v for k, v in (getattr(ctx, "x_stats", None) or {}).items() if k in ("bytes_sent", "bytes_received")}}
@@ -574,7 +574,7 @@ def main():
             **({"c4_strong": c4} if c4 else {}),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
-                     "join_ranges": gs.get("n_join_ranges", 1),
+                     "join_ranges": gs.get("n_join_ranges", 1), "ranges_kept": gs.get("n_ranges_kept", 0),
                      "heavy_groups": gs["n_heavy_groups"], "light_chunks": cs["n_light_chunks"],
                      "explicit_raw": cs["n_explicit_raw"], "heavy_chunks": cs["n_heavy_chunks"],
                      "heavy_candidates": cs["n_heavy_candidates"], "class_members": cs["n_class_members"],

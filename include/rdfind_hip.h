@@ -74,6 +74,8 @@ typedef struct {
                                        repeats dropped) */
     uint64_t n_join_ranges;         /* join-value ranges the groups were built in (1; more for inputs of >= 2^32/9
                                        triples, whose records exceed one sort: Flink's spilling groupBy, RDFind.scala:339-345) */
+    uint64_t n_ranges_kept;         /* join ranges whose sorted records the second pass read back instead of emitting
+                                       and sorting them again (0: none kept) */
 } rdf_group_stats;
 
 typedef struct {

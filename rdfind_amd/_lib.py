@@ -57,7 +57,7 @@ class GroupStats(ctypes.Structure):
                 ("n_groups", ctypes.c_uint64), ("n_captures", ctypes.c_uint64),
                 ("n_unary_captures", ctypes.c_uint64), ("n_heavy_groups", ctypes.c_uint64),
                 ("heavy_threshold", ctypes.c_uint64), ("n_sorted_records", ctypes.c_uint64),
-                ("n_join_ranges", ctypes.c_uint64)]
+                ("n_join_ranges", ctypes.c_uint64), ("n_ranges_kept", ctypes.c_uint64)]
 
 
 class CindStats(ctypes.Structure):

@@ -411,7 +411,7 @@ template <bool LAZY>
 __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
                                      u32 V, u32 twoU, const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                      const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, JoinSel js,
-                                     u64 (&rec)[9], u32* rep = nullptr) {
+                                     u64 (&rec)[9], u32* rep = nullptr, u32* grp = nullptr) {
     u32 c = 0, rp_mask = 0;
     const u32 ts = s[i], tp = p[i], to = o[i];
     const bool jo = (proj & 4) && js.take(to), jp = (proj & 2) && js.take(tp), js_ = (proj & 1) && js.take(ts);
@@ -434,6 +434,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
         }
     }
+    const u32 co = c;
     if (jp) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
         if (fs) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
         if (fo) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
@@ -442,6 +443,7 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
             if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
         }
     }
+    if (grp) *grp = co | ((c - co) << 2);  // records joined on the object, on the predicate (the rest: the subject)
     if (js_) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
         if (fo) rec[c++] = ((2ull * ro) << joinbits) | ts;
@@ -684,6 +686,112 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
         for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
         run += total;
+    }
+}
+
+// K3 of every join range at once (the kept range build, g_emit_all_ranges): the records go to their range's region of
+// rstore.  The count pass writes per (range, block) counts -> block_counts[r * gridDim.x + block]; the write pass places
+// a triple's records joined on one attribute (one join value, so one range) at that range's scanned block offset + an
+// LDS cursor.  The order inside a block's region is free (every range is sorted afterwards), so the cursors need no
+// scan.  Ranges: nr <= EMIT_MAX_RANGES ascending first join values rlo[0..nr), rlo[0] = 0.
+static constexpr u32 EMIT_MAX_RANGES = 256;
+__device__ inline u32 range_of(const u32* rlo, u32 nr, u32 j) {  // last k with rlo[k] <= j
+    u32 a = 0, b = nr - 1;
+    while (a < b) {
+        const u32 m = (a + b + 1) >> 1;
+        if (rlo[m] <= j) a = m;
+        else b = m - 1;
+    }
+    return a;
+}
+template <bool WRITE, bool LAZY>
+__global__ __launch_bounds__(RDF_BLOCK) void k_emit_ranges(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                           const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
+                                                           const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                                           const u32* __restrict__ lvals, u64 lmask, int proj,
+                                                           int joinbits, JoinSel js, const u32* __restrict__ rlo_g, u32 nr,
+                                                           u64* block_counts, const u64* __restrict__ block_offsets,
+                                                           u64* out, int recbits) {
+    __shared__ u32 rlo[EMIT_MAX_RANGES];
+    __shared__ u32 cur[EMIT_MAX_RANGES];
+    __shared__ u64 base[WRITE ? EMIT_MAX_RANGES : 1];
+    __shared__ u64 htab[WRITE ? EMIT_DEDUP_SLOTS : 1];  // the iteration's distinct records (write pass)
+    for (u32 k = threadIdx.x; k < nr; k += RDF_BLOCK) {
+        rlo[k] = rlo_g[k];
+        cur[k] = 0;
+        if (WRITE) base[k] = block_offsets[(u64)k * gridDim.x + blockIdx.x];
+    }
+    const bool dedup = WRITE && RDF_EMIT_DEDUP && recbits <= 48;
+    if (dedup)
+        for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;  // tag 0: empty
+    __syncthreads();
+    const u64 b = (u64)blockIdx.x * per;
+    const u64 e = b + per < n ? b + per : n;
+    u32 tag = 0;
+    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
+        const u64 i = i0 + threadIdx.x;
+        u64 rec[9];
+        u32 c = 0, rep = 0, grp = 0;
+        if (i < e) c = triple_records<LAZY>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, &rep, &grp);
+        const u32 co = grp & 3u, cp = (grp >> 2) & 3u, cs = c - co - cp;
+        u32 keep = (1u << c) - 1u;
+        if (dedup) {  // as k_emit_records: the repeating kinds through the iteration's LDS table, the others kept
+            ++tag;
+            if (tag == (1u << 15)) {
+                for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;
+                __syncthreads();
+                tag = 1;
+            }
+            keep = ((1u << c) - 1u) & ~rep;
+            for (int k = 0; k < 9; ++k) {
+                if ((u32)k >= c) break;
+                if (!((rep >> k) & 1u)) continue;
+                const u64 want = rec[k] | ((u64)tag << 48);
+                u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
+                u64 cur_h = htab[h];
+                while (true) {
+                    if ((u32)(cur_h >> 48) != tag) {
+                        const u64 prev = atomicCAS((unsigned long long*)&htab[h], (unsigned long long)cur_h,
+                                                   (unsigned long long)want);
+                        if (prev == cur_h) {
+                            keep |= 1u << k;
+                            break;
+                        }
+                        cur_h = prev;
+                        continue;
+                    }
+                    if (cur_h == want) break;
+                    h = (h + 1) & (EMIT_DEDUP_SLOTS - 1);
+                    cur_h = htab[h];
+                }
+            }
+        }
+        // one LDS cursor claim per attribute group (its join value: o, p or s of the triple)
+        u32 ro = 0, rp = 0, rs = 0;
+        u64 qo = 0, qp = 0, qs = 0;
+        if (co) ro = range_of(rlo, nr, o[i]);
+        if (cp) rp = range_of(rlo, nr, p[i]);
+        if (cs) rs = range_of(rlo, nr, s[i]);
+        if (!WRITE) {
+            if (co) atomicAdd(&cur[ro], co);
+            if (cp) atomicAdd(&cur[rp], cp);
+            if (cs) atomicAdd(&cur[rs], cs);
+        } else {
+            if (co) qo = base[ro] + atomicAdd(&cur[ro], co);
+            if (cp) qp = base[rp] + atomicAdd(&cur[rp], cp) - co;
+            if (cs) qs = base[rs] + atomicAdd(&cur[rs], cs) - co - cp;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                if ((u32)k >= c) break;
+                const u64 q = (u32)k < co ? qo : (u32)k < co + cp ? qp : qs;
+                out[q + k] = ((keep >> k) & 1u) ? rec[k] : EMIT_PAD;
+            }
+        }
+        if (dedup) __syncthreads();  // the next iteration's tag reuses the table's slots
+    }
+    if (!WRITE) {
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < nr; k += RDF_BLOCK) block_counts[(u64)k * gridDim.x + blockIdx.x] = cur[k];
     }
 }
 

@@ -67,6 +67,11 @@ struct rdf_ctx {
     struct JoinRange { u32 lo, hi; u64 recs; };
     std::vector<JoinRange> jranges;  // the current build's join ranges (pass 1 -> pass 2)
     u64 jr_cap_rec = 1;              // records of the largest range (the range scratch's size)
+    // pass 1's sorted records of every range, kept for pass 2 when they fit next to the range scratch (pass 2 then
+    // neither re-emits nor re-sorts a range); RDFIND_RANGE_KEEP=0: always re-emit
+    DevBuf rstore;
+    std::vector<u64> jr_seg, jr_J;   // range k's slots in rstore start at jr_seg[k]; its sorted records
+    bool jr_keep = false, range_keep = true;
     // per range (triple, attribute) entry lists (g_range_entries): a range's emissions read only its own triples
     DevBuf jrmap, jrhist, jent;      // join bucket -> range, per (bin, block) counts, the entries (bin-major)
     std::vector<u64> jr_bin;         // first entry of bin 3 range + attribute (+ the total)
@@ -247,7 +252,7 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
 // only when an allocation of a later stage would otherwise fail.
 static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
     const std::vector<DevBuf*> fc_scratch = {&c->brkeys, &c->brkeys2, &c->tkeys, &c->urecs};
-    const std::vector<DevBuf*> grp_scratch = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->jent};
+    const std::vector<DevBuf*> grp_scratch = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->jent, &c->rstore};
     const std::vector<DevBuf*> x_scratch = {&c->xsend, &c->xrecv};
     bool any = false;
     for (int k = 0; k < 3; ++k) {
@@ -418,11 +423,11 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
-            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout};
+            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore};
 }
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
-static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout"};
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore"};
 static void mem_report(rdf_ctx* c) {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
     if (!on) return;
@@ -474,6 +479,7 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (const char* to = getenv("RDFIND_TEST_OOM_DISCOVERY")) c->test_oom_discovery = atoi(to) != 0;
     if (const char* hb = getenv("RDFIND_HOT_BALANCE")) c->hot_balance = atoi(hb) != 0;
     if (const char* rl = getenv("RDFIND_RANGE_LISTS")) c->range_lists = atoi(rl) != 0;
+    if (const char* rk = getenv("RDFIND_RANGE_KEEP")) c->range_keep = atoi(rk) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
@@ -1293,6 +1299,7 @@ static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj
 // record key layout of this run's K3 records: capture << joinbits | join
 static rdf_status g_record_bits(rdf_ctx* c) {
     c->spare_groups = false;  // a group build starts: its record buffers are in use
+    c->jr_keep = false;
     const u32 V = c->V ? c->V : 1;
     const u64 ncap = 2ull * c->U + c->B;  // compact candidate captures (k_frank_final)
     const int capbits = bits_for(ncap ? ncap - 1 : 0);
@@ -1323,6 +1330,7 @@ static JoinSel shard_sel(const rdf_ctx* c) {
 // re-running the count pass and its scan and read-back.  cache = 0: no reuse.
 // a range's cached block offsets: one fixed-size slot per range (the grid follows a range's entry count, <= kGrid)
 static constexpr u64 ECACHE_STRIDE = kGrid + 1ull;
+static rdf_status g_sort_support(rdf_ctx* c, u64* keys, u64* tmp, u64 Je, u32* sup, u64* Jout, u64* keep_out);
 static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u32* sup, u64* Jout, int cache = 0) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
@@ -1332,6 +1340,8 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
     ENSURE(c, rec, std::max<u64>(cap_rec, 1) * 8);
     ENSURE(c, rec_tmp, std::max<u64>(cap_rec, 1) * 8);
+    u64* ebuf = c->rec.as<u64>();
+    const u64 slot_cap = cap_rec;
     tbegin(c, RDF_T_EMIT);
     const int slot = cache > 0 ? cache - 1 : cache < 0 ? -cache - 1 : -1;
     // the selection takes a part of the join values (a join range, or a rank's shard): lazy condition-rank loads
@@ -1378,25 +1388,25 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
             if (cache > 0)
                 HIP_TRY(c, hipMemcpyAsync(c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, c->eblk.p, eg * 8ull,
                                           hipMemcpyDeviceToDevice, st));
-            if (cap_rec < 9 * n) {  // a join range's buffers: the slot count is checked before the write pass
+            if (slot_cap < 9 * n) {  // a join range's buffers: the slot count is checked before the write pass
                 TRY(read_scalars(c, 1));
                 je_early = c->hscal[0];
-                if (je_early > cap_rec)
+                if (je_early > slot_cap)
                     return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
             }
         }
         if (lists)
             hipLaunchKernelGGL((k_emit_entries<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, ent, units, m_s, m_sp,
                                per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1,
-                               joinbits, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+                               joinbits, (u64*)nullptr, c->eblk.as<u64>(), ebuf, capbits + joinbits);
         else if (lazy)
             hipLaunchKernelGGL((k_emit_records<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
-                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), ebuf, capbits + joinbits);
         else
             hipLaunchKernelGGL((k_emit_records<true, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
-                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), c->rec.as<u64>(), capbits + joinbits);
+                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), ebuf, capbits + joinbits);
     }
     tend(c, RDF_T_EMIT);
     u64 Je = 0;  // emitted record slots (repeats within an emission iteration are padding)
@@ -1410,13 +1420,25 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
         Je = je_early;
         if (cache > 0) c->ecache_je[slot] = Je;
     }
-    if (Je > cap_rec) return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
+    if (Je > slot_cap) return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
+    return g_sort_support(c, ebuf, c->rec_tmp.as<u64>(), Je, sup, Jout, nullptr);
+}
+
+// K4 sort of Je emitted record slots (keys, with tmp as the other buffer; padding dropped) and K5 supports -> sup.
+// keep_out: the sorted records must end there (keys == keep_out: a range of rstore, copied back after an odd number of
+// passes).  Sets c->rec_sorted, *Jout.
+static rdf_status g_sort_support(rdf_ctx* c, u64* keys, u64* tmp, u64 Je, u32* sup, u64* Jout, u64* keep_out) {
+    hipStream_t st = c->stream;
+    const u64 ncap = c->ncap;
+    const int capbits = c->capbits, joinbits = c->joinbits;
     c->J_emit += Je;
-    u64* keys = c->rec.as<u64>();
-    u64* tmp = c->rec_tmp.as<u64>();
     u64 J = 0;
     tbegin(c, RDF_T_SORT);
     HIP_TRY(c, radix_sort_u64_drop(c->ws, keys, tmp, Je, capbits + joinbits, (u32*)dscal(c, 1), &J, st));
+    if (keep_out && keys != keep_out) {  // an odd number of passes ended in tmp
+        if (J) HIP_TRY(c, hipMemcpyAsync(keep_out, keys, J * 8, hipMemcpyDeviceToDevice, st));
+        keys = keep_out;
+    }
     tend(c, RDF_T_SORT);
     *Jout = J;
     c->rec_sorted = keys;
@@ -1608,6 +1630,100 @@ static rdf_status g_range_entries(rdf_ctx* c, int proj, JoinSel own, int jshift)
     return RDF_OK;
 }
 
+// Keep pass 1's sorted records of every range (rstore: the ranges' record counts, 8 B each) when they fit beside the
+// range scratch and the build's global arrays (the bound of auto_range_records): pass 2 then reads them instead of
+// emitting and sorting every range a second time (c4 at 10^9 triples: 47 GB kept, one emission and one sort saved
+// per range).  Otherwise, or when the allocation fails, pass 2 re-emits.
+static rdf_status g_range_keep_plan(rdf_ctx* c) {
+    const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
+    c->jr_keep = false;
+    if (!c->range_keep || ranges.size() < 2 || ranges.size() > EMIT_MAX_RANGES) return RDF_OK;
+    u64 total = 0;
+    c->jr_seg.assign(ranges.size() + 1, 0);
+    c->jr_J.assign(ranges.size(), 0);
+    for (size_t k = 0; k < ranges.size(); ++k) {
+        c->jr_seg[k] = total;
+        total += ranges[k].recs;
+    }
+    c->jr_seg[ranges.size()] = total;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return RDF_OK;
+    // held by this context and reusable here: the spare stages' scratch and the range buffers of an earlier build
+    const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap +
+                     (c->spare_x ? (u64)c->xsend.cap + c->xrecv.cap : 0ull) + c->rec.cap + c->rec_tmp.cap + c->fk.cap +
+                     c->fk_tmp.cap + c->rstore.cap;
+    const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30);
+    const u64 need = 8 * total + 40 * c->jr_cap_rec + global;  // rec_tmp (8 B per record) is not used when keeping
+    if ((u64)free_b + held < need) {
+        (void)hipStreamSynchronize(c->stream);
+        c->rstore.release();  // an earlier build's: the range buffers may need the room
+        return RDF_OK;
+    }
+    (void)hipStreamSynchronize(c->stream);
+    c->rec_tmp.release();  // not used by a kept build (an earlier build's)
+    hipError_t e = c->rstore.ensure(std::max<u64>(total, 1) * 8);
+    if (e == hipErrorOutOfMemory && reclaim_spare(c, &c->rstore)) e = c->rstore.ensure(std::max<u64>(total, 1) * 8);
+    (void)hipGetLastError();
+    c->jr_keep = e == hipSuccess;
+    return RDF_OK;
+}
+
+// K3 of every range in one emission into its rstore region (k_emit_ranges: a count pass per (range, block), one scan,
+// the write pass): each triple is read twice for all ranges instead of twice per range.  The regions' sizes are the
+// join histogram's range counts; the scanned counts must agree with them.
+static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
+    hipStream_t st = c->stream;
+    const u64 n = c->n;
+    const u32 V = c->V ? c->V : 1;
+    const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
+    const u32 nr = (u32)ranges.size();
+    ENSURE(c, rec, std::max<u64>(c->jr_cap_rec, 1) * 8);  // the ranges' sort buffer
+    std::vector<u32> lo(nr);
+    for (u32 k = 0; k < nr; ++k) lo[k] = ranges[k].lo;
+    ENSURE(c, jrmap, nr * 4ull);
+    HIP_TRY(c, ctx_copy(c, c->jrmap.p, lo.data(), nr * 4ull, hipMemcpyHostToDevice));
+    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const u64 per = n ? (n + eg - 1) / eg : 0;
+    const u64 nb = (u64)nr * eg;
+    ENSURE(c, eblk, (nb + 1) * 8);
+    HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
+    const bool lazy = own.nranks > 1;
+    const int recbits = c->capbits + c->joinbits;
+    const u32 twoU = 2u * c->U;
+    tbegin(c, RDF_T_EMIT);
+    if (n) {
+        if (lazy)
+            hipLaunchKernelGGL((k_emit_ranges<false, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
+                               c->jrmap.as<u32>(), nr, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, recbits);
+        else
+            hipLaunchKernelGGL((k_emit_ranges<false, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
+                               c->jrmap.as<u32>(), nr, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, recbits);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), nb, c->eblk.as<u64>() + nb, st));
+    }
+    // the regions must be the histogram's: each range's first block offset = its rstore offset
+    std::vector<u64> off(nb + 1, 0);
+    if (n) HIP_TRY(c, ctx_copy(c, off.data(), c->eblk.p, (nb + 1) * 8, hipMemcpyDeviceToHost));
+    for (u32 k = 0; k <= nr; ++k)
+        if ((n ? off[(u64)k * eg] : 0) != c->jr_seg[k])
+            return fail(c, RDF_ERR_LIMIT, "K3 records per join range disagree with the join histogram");
+    if (n) {
+        if (lazy)
+            hipLaunchKernelGGL((k_emit_ranges<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
+                               c->jrmap.as<u32>(), nr, (u64*)nullptr, c->eblk.as<u64>(), c->rstore.as<u64>(), recbits);
+        else
+            hipLaunchKernelGGL((k_emit_ranges<true, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
+                               c->jrmap.as<u32>(), nr, (u64*)nullptr, c->eblk.as<u64>(), c->rstore.as<u64>(), recbits);
+        HIP_TRY(c, hipGetLastError());
+    }
+    tend(c, RDF_T_EMIT);
+    return RDF_OK;
+}
+
 static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel own) {
     hipStream_t st = c->stream;
     const u64 n = c->n;
@@ -1652,7 +1768,8 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     c->jr_cap_rec = cap_rec;
     c->n_group_ranges = ranges.size();
     c->jr_lists = false;
-    if (c->range_lists && ranges.size() > 1 && 3 * ranges.size() <= RE_MAX_BINS && n)
+    TRY(g_range_keep_plan(c));
+    if (!c->jr_keep && c->range_lists && ranges.size() > 1 && 3 * ranges.size() <= RE_MAX_BINS && n)
         TRY(g_range_entries(c, proj, own, jshift));
     // 2. supports
     ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
@@ -1660,19 +1777,45 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     HIP_TRY(c, hipMemsetAsync(c->support.p, 0, std::max<u64>(ncap, 1) * 4, st));
     u64 Jtot = 0;
     c->ecache_je.clear();
+    if (c->jr_keep) TRY(g_emit_all_ranges(c, proj, own));
     for (size_t k = 0; k < ranges.size(); ++k) {
         const rdf_ctx::JoinRange& r = ranges[k];
         u64 J = 0;
         JoinSel js = own;
         js.lo = r.lo;
         js.hi = r.hi;
-        TRY(g_emit_range(c, proj, js, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
+        if (c->jr_keep) {  // range k's records are emitted (g_emit_all_ranges): its sort in place
+            u64* seg = c->rstore.as<u64>() + c->jr_seg[k];
+            TRY(g_sort_support(c, seg, c->rec.as<u64>(), c->jr_seg[k + 1] - c->jr_seg[k], c->rsup.as<u32>(), &J, seg));
+            c->jr_J[k] = J;
+        } else {
+            TRY(g_emit_range(c, proj, js, cap_rec, c->rsup.as<u32>(), &J, 1 + (int)k));
+        }
         Jtot += J;
         if (ncap)
             hipLaunchKernelGGL(k_add_u32, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->support.as<u32>(),
                                c->rsup.as<u32>(), ncap);
     }
     c->J = Jtot;
+    return RDF_OK;
+}
+
+// pass 2 of a kept range: its sorted records from rstore, their run bounds (cstart) and fresh-record scan (fpos)
+static rdf_status g_restore_range(rdf_ctx* c, size_t k, u64* Jout) {
+    hipStream_t st = c->stream;
+    const u64 J = c->jr_J[k], ncap = c->ncap;
+    u64* keys = c->rstore.as<u64>() + c->jr_seg[k];
+    ENSURE(c, flags, std::max<u64>(J, 1) * 4);
+    ENSURE(c, fpos, (J + 1) * 4);
+    ENSURE(c, cstart, (ncap + 1) * 4);
+    ENSURE(c, rec, std::max<u64>(c->jr_cap_rec, 1) * 8);  // the kept records' destination (dk) in pass 2
+    tbegin(c, RDF_T_SUPPORT);
+    hipLaunchKernelGGL(k_fresh_bounds, dim3(grid_for(J + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, ncap,
+                       c->joinbits, c->flags.as<u32>(), c->cstart.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), J, c->fpos.as<u32>() + J, st));
+    tend(c, RDF_T_SUPPORT);
+    c->rec_sorted = keys;
+    *Jout = J;
     return RDF_OK;
 }
 
@@ -1724,7 +1867,8 @@ static rdf_status g_ranges_groups(rdf_ctx* c, int proj, JoinSel own, const u32* 
         JoinSel js = own;
         js.lo = r.lo;
         js.hi = r.hi;
-        TRY(g_emit_range(c, proj, js, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
+        if (c->jr_keep) TRY(g_restore_range(c, k, &J));
+        else TRY(g_emit_range(c, proj, js, cap_rec, c->rsup.as<u32>(), &J, -1 - (int)k));
         u64* keys = c->rec_sorted;
         tbegin(c, RDF_T_SUPPORT);
         ENSURE(c, flags, std::max<u64>(std::max<u64>(J, ncap), 1) * 4);
@@ -1804,7 +1948,7 @@ static u64 auto_range_records(rdf_ctx* c) {
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1ull << 30;
     // spare buffers an allocation of the build may release (reclaim_spare)
     const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap +
-                     (c->spare_x ? (u64)c->xsend.cap + c->xrecv.cap : 0ull);
+                     (c->spare_x ? (u64)c->xsend.cap + c->xrecv.cap : 0ull) + c->rstore.cap;
     const u64 avail = (u64)free_b + held;
     // ~4.5 records per triple kept; the ranges' entry lists (g_range_entries) up to 12 B per triple
     const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30) + (c->range_lists ? 12 * c->n : 0);
@@ -1912,6 +2056,7 @@ static void fill_group_stats(rdf_ctx* c) {
     s.n_heavy_groups = c->nheavy;
     s.heavy_threshold = c->heavy_threshold;
     s.n_join_ranges = c->n_group_ranges;
+    s.n_ranges_kept = c->jr_keep ? c->n_group_ranges : 0;
 }
 
 // the heavy threshold and count of a device-threshold build -> gstats (one host read; at the run's end for rdf_run)
@@ -2825,6 +2970,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     TRY(d_heavy_count(c, v, WH, &H));
     TRY(d_emit(c, v, E, WH, H, HC, NT));
     if (stats) *stats = c->cstats;
+    mem_report(c);
     return RDF_OK;
 }
 
@@ -3098,7 +3244,6 @@ rdf_status rdf_run(rdf_ctx* c, uint32_t min_support, const char* projection, uin
     if (r) return r;
     TRY(settle_group_stats(c));
     if (gs) *gs = c->gstats;
-    mem_report(c);
     return RDF_OK;
 }
 

@@ -346,15 +346,18 @@ def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
         g.close()
 
 
-@pytest.mark.parametrize("range_records,lists", [(1, 1), (7, 1), (300, 1), (7, 0)])
-def test_join_range_groups_parity(monkeypatch, range_records, lists):
+@pytest.mark.parametrize("range_records,lists,keep", [(1, 1, 1), (7, 0, 1), (300, 0, 1), (7, 1, 0), (7, 0, 0)])
+def test_join_range_groups_parity(monkeypatch, range_records, lists, keep):
     """Capture groups built in join-value ranges (the path of inputs with >= 2^32/9 triples; RDFIND_GROUP_RANGE forces
     ranges of at most that many K3 records, a single join value's records may exceed it): every mode gives the oracle's
     set, and the stage statistics equal the one-pass build's.  Each range's emissions read its (triple, attribute) entry
-    lists (g_range_entries), or with RDFIND_RANGE_LISTS=0 every triple."""
+    lists (g_range_entries), or with RDFIND_RANGE_LISTS=0 every triple.  RDFIND_RANGE_KEEP=1 (the default, up to 256
+    ranges): every range is emitted at once into its region of the kept store (k_emit_ranges), and the second pass reads
+    the first pass's sorted records instead of emitting and sorting every range again."""
     ref = _lib.Context(0)
     monkeypatch.setenv("RDFIND_GROUP_RANGE", str(range_records))
     monkeypatch.setenv("RDFIND_RANGE_LISTS", str(lists))
+    monkeypatch.setenv("RDFIND_RANGE_KEEP", str(keep))
     g = _lib.Context(0)
     try:
         rng = random.Random(900 + range_records)
@@ -378,13 +381,16 @@ def test_join_range_groups_parity(monkeypatch, range_records, lists):
             assert (g.cind_count(), g.checksum()) == (ref.cind_count(), ref.checksum())
             if range_records == 1 and n > 50:
                 assert g.groups["n_join_ranges"] > 1
+            nr = g.groups["n_join_ranges"]
+            assert g.groups["n_ranges_kept"] == (nr if keep and 1 < nr <= 256 else 0)
         for cfg, scale in (("c1", 0.05), ("c5", 0.01), ("c4", 0.0003)):
             d = dataset(cfg, scale)
             g.set_triples(d.s, d.p, d.o, d.num_terms)
             g.run(d.min_support)
             st = assert_stream_matches(g, cfg, scale, what=range_records)["stats"]
             assert g.groups["n_records"] == st["n_records"] and g.groups["n_captures"] == st["n_freq_captures"]
-            assert g.groups["n_join_ranges"] > 1
+            nr = g.groups["n_join_ranges"]
+            assert nr > 1 and g.groups["n_ranges_kept"] == (nr if keep and nr <= 256 else 0)
     finally:
         g.close()
         ref.close()
