@@ -34,6 +34,8 @@ static constexpr int B2_SLOTS = 4096;          // LDS hash slots of a K2 countin
 static constexpr u64 B2_BIG = 64ull << 20;     // above 3n = 64M keys, one more bucket bit per doubling (fewer
                                                // multi-slice buckets, which go to the spill table)
 static constexpr int B2_PBLOCK = 1024;         // threads of a K2 histogram / scatter block
+static constexpr u64 B2_RADIX_MIN = 1ull << 27;  // 3n from which K2 groups compact records with the radix passes
+                                                 // (k_b2_emit; RDFIND_B2_RADIX_MIN overrides)
 
 // global rank of unary condition i (= pos * V + value) among all frequent conditions, or NONE
 __device__ inline u32 frank_at(const u32* __restrict__ frank, const u32* __restrict__ boff, u64 i) {
@@ -459,6 +461,76 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_b2_split(const u64* __restrict__ 
             }
         }
         __syncthreads();  // cnt is reused by the next bucket
+    }
+}
+
+// K2 for large inputs (fc_binary_part, 3n >= B2_RADIX_MIN): the records written compactly, then grouped by the top
+// bits of their key hash with the tile-staged radix passes (radix_partition_hashed) instead of k_b2_part's scatter into
+// 2^15 buckets and k_b2_split's second level (at c4 scale both write 8-B records to tens of thousands of open buckets
+// per block: partial-line writes).  k_b2_emit: PART_U triples per thread, their merged records (b2_keys) at one
+// claim per block iteration (the order of the records is free: the counting slices aggregate in hash tables).
+__global__ __launch_bounds__(RDF_BLOCK) void k_b2_emit(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                       const u32* __restrict__ o, u64 n, u32 V, const u64* __restrict__ fbits,
+                                                       u64* __restrict__ out, u64* counter) {
+    __shared__ u32 s_wave[RDF_WAVES_PER_BLOCK];
+    __shared__ u64 s_base;
+    const int lane = lane_id(), wave = threadIdx.x / RDF_WAVE;
+    constexpr u64 TILE = (u64)RDF_BLOCK * PART_U;
+    for (u64 i0 = (u64)blockIdx.x * TILE; i0 < n; i0 += (u64)gridDim.x * TILE) {  // block-uniform trip count
+        u32 ts[PART_U], tp[PART_U], to[PART_U];
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            const u64 i = i0 + (u64)u * RDF_BLOCK + threadIdx.x;
+            ts[u] = i < n ? s[i] : 0u;
+            tp[u] = i < n ? p[i] : 0u;
+            to[u] = i < n ? o[i] : 0u;
+        }
+        bool fs[PART_U], fp[PART_U], fo[PART_U];
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            const bool act = i0 + (u64)u * RDF_BLOCK + threadIdx.x < n;
+            fs[u] = act && fbit(fbits, ts[u]);
+            fp[u] = act && fbit(fbits, (u64)V + tp[u]);
+            fo[u] = act && fbit(fbits, 2ull * V + to[u]);
+        }
+        u64 key[PART_U][3];
+        u32 cnt[PART_U][3];
+        u32 mine = 0;
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u) {
+            b2_keys(ts[u], tp[u], to[u], fs[u], fp[u], fo[u], key[u], cnt[u]);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) mine += cnt[u][t] != 0;
+        }
+        const u32 incl = wave_inclusive_scan(mine);
+        if (lane == RDF_WAVE - 1) s_wave[wave] = incl;
+        __syncthreads();
+        u32 woff = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < RDF_WAVES_PER_BLOCK; ++w) {
+            woff += w < wave ? s_wave[w] : 0u;
+            tot += s_wave[w];
+        }
+        if (threadIdx.x == 0) s_base = tot ? atomicAdd((unsigned long long*)counter, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        u64 q = s_base + woff + incl - mine;
+#pragma unroll
+        for (int u = 0; u < PART_U; ++u)
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                if (cnt[u][t]) out[q++] = b2_pack(key[u][t], cnt[u][t]);
+        __syncthreads();  // s_wave / s_base are reused by the next iteration
+    }
+}
+
+// bucket starts of hash-grouped records: bstart[b] = first record whose bucket (top `bits` of the key hash) is >= b,
+// b in [0, 2^bits]
+__global__ __launch_bounds__(RDF_BLOCK) void k_b2_hbounds(const u64* __restrict__ rec, u64 n, int bits, u32* bstart) {
+    const u64 NB = 1ull << bits;
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= n; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 b = i < n ? b2_bucket(rec[i] & ~B2_CBITS, bits) : NB;
+        const u64 bp = i ? (u64)b2_bucket(rec[i - 1] & ~B2_CBITS, bits) + 1 : 0;
+        for (u64 x = bp; x <= b; ++x) bstart[x] = (u32)i;
     }
 }
 

@@ -1018,35 +1018,55 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_key_offsets(const u64* __restrict
 // members of each group and every dependent's group list come out exactly as the one-pass build makes them.
 
 // records per join bucket (join >> jshift, JH_BUCKETS buckets): the K3 count pass's per-triple record counts split by
-// their join value (o, p or s of the triple), LDS-privatised
-__global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_hist(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                              const u32* __restrict__ o, u64 n, u32 V, u32 twoU,
-                                                              const u32* __restrict__ frank, const u64* __restrict__ lkeys,
-                                                              const u32* __restrict__ lvals, u64 lmask, int proj,
-                                                              int joinbits, JoinSel own, int jshift, u64* hist) {
+// their join value (o, p or s of the triple), LDS-privatised per block of contiguous triples (the blocks of
+// k_emit_ranges: per = ceil(n / gridDim.x)): the block's bucket counts -> bh[block * JH_BUCKETS + bucket], the totals
+// -> hist.  A triple's records joined on one attribute share a join value: one LDS atomic per attribute
+// (triple_records' group counts).
+template <bool LAZY>
+__global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_bhist(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                               const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
+                                                               const u32* __restrict__ frank, const u64* __restrict__ lkeys,
+                                                               const u32* __restrict__ lvals, u64 lmask, int proj,
+                                                               int joinbits, JoinSel own, int jshift, u32* bh, u64* hist) {
     __shared__ u32 lh[JH_BUCKETS];
     for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lh[k] = 0;
     __syncthreads();
     JoinSel all = own;  // this rank's join values (sharded: hash or hot-table owner), every range
     all.lo = 0u;
     all.hi = JOIN_ALL_HI;
-    const u64 jmask = (1ull << joinbits) - 1;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+    const u64 b = (u64)blockIdx.x * per;
+    const u64 e = b + per < n ? b + per : n;
+    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
         u64 rec[9];
-        const u32 c = triple_records<false>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, all, rec);
-        // a triple's records are grouped by join value (o, then p, then s): one LDS atomic per run
-        u32 k = 0;
-        while (k < c) {
-            const u64 j = rec[k] & jmask;
-            u32 r = 1;
-            while (k + r < c && (rec[k + r] & jmask) == j) ++r;
-            atomicAdd(&lh[(u32)(j >> jshift)], r);
-            k += r;
-        }
+        u32 grp = 0;
+        const u32 c = triple_records<LAZY>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, all, rec,
+                                           nullptr, &grp);
+        const u32 co = grp & 3u, cp = (grp >> 2) & 3u, cs = c - co - cp;
+        if (co) atomicAdd(&lh[o[i] >> jshift], co);
+        if (cp) atomicAdd(&lh[p[i] >> jshift], cp);
+        if (cs) atomicAdd(&lh[s[i] >> jshift], cs);
     }
     __syncthreads();
-    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK)
-        if (lh[k]) atomicAdd(&hist[k], (u64)lh[k]);
+    u32* row = bh + (u64)blockIdx.x * JH_BUCKETS;
+    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) {
+        const u32 x = lh[k];
+        row[k] = x;
+        if (x) atomicAdd(&hist[k], (u64)x);
+    }
+}
+
+// per (range, block) record counts from the blocks' bucket histograms: one wave per pair sums the range's buckets
+// [blo[r], blo[r + 1]) of the block's row -> counts[r * nblk + block] (the layout k_emit_ranges' count pass writes)
+__global__ __launch_bounds__(RDF_BLOCK) void k_range_block_counts(const u32* __restrict__ bh, u32 nblk,
+                                                                  const u32* __restrict__ blo, u32 nr, u64* counts) {
+    const u64 wv = ((u64)blockIdx.x * RDF_BLOCK + threadIdx.x) / RDF_WAVE;
+    if (wv >= (u64)nr * nblk) return;
+    const u32 r = (u32)(wv / nblk), blk = (u32)(wv % nblk);
+    const u32* row = bh + (u64)blk * JH_BUCKETS;
+    u32 acc = 0;  // a block's records: <= 9 per triple of its chunk, far below 2^32
+    for (u32 k = blo[r] + lane_id(); k < blo[r + 1]; k += RDF_WAVE) acc += row[k];
+    acc = wave_sum(acc);
+    if (lane_id() == 0) counts[wv] = acc;
 }
 
 // a range's groups: goff[gbase + g] = rbase + first member, gcap[rbase + i], gmap[join] = gbase + g

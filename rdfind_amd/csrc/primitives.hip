@@ -336,9 +336,15 @@ __device__ inline void load_tile_pairs(const u64* __restrict__ keys, u64 n, u64 
 // Digits of DB bits (the pass's width w <= DB is masked at run time: DB only sizes the LDS counters)
 // drop: keys equal to ~0 (padding) are left out of the histogram and of the scattered output (first pass of a sort
 // whose input carries padding; the output then holds only the other keys)
-template <int DB>
+// HASH: the digits are those of mix64(key & hmask) (a hash partition: K2's records grouped by the top bits of their
+// key hash, radix_partition_hashed); the keys themselves are moved unchanged
+template <bool HASH>
+__device__ inline u32 radix_digit(u64 k, int shift, u32 dmask, u64 hmask) {
+    return (u32)((HASH ? mix64(k & hmask) : k) >> shift) & dmask;
+}
+template <int DB, bool HASH = false>
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict__ keys, u64 n, int shift, int w,
-                                                           u32* __restrict__ hist, u32 num_tiles, int drop) {
+                                                           u32* __restrict__ hist, u32 num_tiles, int drop, u64 hmask) {
     constexpr u32 NBIN = 1u << DB;
     __shared__ u32 wcnt[RDF_WAVES_PER_BLOCK][NBIN];
     const int lane = lane_id();
@@ -353,7 +359,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
     for (int r = 0; r < RS_ITEMS; ++r) {
         const u64 idx = tbase + 2ull * ((u64)(r / 2) * RDF_BLOCK + threadIdx.x) + (r & 1);
         const bool valid = idx < n && !(drop && k[r] == ~0ull);
-        const u32 d = (u32)(k[r] >> shift) & dmask;
+        const u32 d = radix_digit<HASH>(k[r], shift, dmask, hmask);
         const u64 peers = digit_peers<DB>(d, valid);
         if (valid && ((peers >> lane) >> 1) == 0) wcnt[wave][d] += (u32)__popcll(peers);
     }
@@ -366,10 +372,10 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
     }
 }
 
-template <int DB>
+template <int DB, bool HASH = false>
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
                                                              int shift, int w, const u32* __restrict__ offs,
-                                                             u32 num_tiles, int drop) {
+                                                             u32 num_tiles, int drop, u64 hmask) {
     constexpr u32 NBIN = 1u << DB;
     constexpr u32 PER = NBIN / RDF_BLOCK;  // digits per thread in the tile scan (1, 2 or 4)
     static_assert(NBIN % RDF_BLOCK == 0, "digit bins must be a multiple of the block");
@@ -405,7 +411,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == ~0ull);
-        const u32 d = (u32)(k[r] >> shift) & dmask;
+        const u32 d = radix_digit<HASH>(k[r], shift, dmask, hmask);
         const u64 peers = digit_peers<DB>(d, valid);
         const u32 before = (u32)__popcll(peers & lt);
         const u32 old = valid ? wcount[wave][d] : 0;
@@ -442,7 +448,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         if (wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == ~0ull)) {
-            const u32 d = (u32)(k[r] >> shift) & dmask;
+            const u32 d = radix_digit<HASH>(k[r], shift, dmask, hmask);
             skeys[tstart[d] + wcount[wave][d] + rank[r]] = k[r];
         }
     }
@@ -453,21 +459,23 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
         const u32 p = (u32)i * RDF_BLOCK + threadIdx.x;
         if (p < tv) {
             const u64 key = skeys[p];
-            const u32 d = (u32)(key >> shift) & dmask;
+            const u32 d = radix_digit<HASH>(key, shift, dmask, hmask);
             out[(u64)gbase[d] + (p - tstart[d])] = key;
         }
     }
 }
 
-template <int DB>
+template <int DB, bool HASH = false>
 static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, int shift, int w, u32* hist, u32 tiles,
-                             hipStream_t st, u32* d_kept = nullptr) {
+                             hipStream_t st, u32* d_kept = nullptr, u64 hmask = 0) {
     const u64 hn = (u64)tiles << w;
     const int drop = d_kept ? 1 : 0;
-    hipLaunchKernelGGL(k_radix_count<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, tiles, drop);
+    hipLaunchKernelGGL((k_radix_count<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, tiles, drop,
+                       hmask);
     hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, d_kept, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_radix_scatter<DB>, dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, tiles, drop);
+    hipLaunchKernelGGL((k_radix_scatter<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, tiles,
+                       drop, hmask);
     return hipSuccess;
 }
 
@@ -522,6 +530,28 @@ hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int 
 
 hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, hipStream_t st) {
     return radix_sort_u64_bits(ws, keys, tmp, n, 0, bits, st);
+}
+
+// Keys grouped by bits [64 - bits, 64) of mix64(key & hmask), ascending (LSD passes of <= 10 bits over those hash bits;
+// within a group the order is the passes' stable order).  keys / tmp swap like radix_sort_u64_bits.
+hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u64 hmask, hipStream_t st) {
+    if (n < 2 || bits <= 0) return hipSuccess;
+    if (n >= (1ull << 32) || bits > 30) return hipErrorInvalidValue;
+    const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
+    const int passes = (bits + 9) / 10;
+    u32* hist = (u32*)ws.scratch(((u64)tiles << 10) * sizeof(u32), 1);
+    if (!hist) return hipErrorOutOfMemory;
+    int shift = 64 - bits;
+    for (int p = 0; p < passes; ++p) {
+        const int w = bits / passes + (p < bits % passes ? 1 : 0);
+        hipError_t e = w <= 8 ? radix_pass<8, true>(ws, keys, tmp, n, shift, w, hist, tiles, st, nullptr, hmask)
+                     : w == 9 ? radix_pass<9, true>(ws, keys, tmp, n, shift, w, hist, tiles, st, nullptr, hmask)
+                              : radix_pass<10, true>(ws, keys, tmp, n, shift, w, hist, tiles, st, nullptr, hmask);
+        if (e != hipSuccess) return e;
+        std::swap(keys, tmp);
+        shift += w;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace rdf

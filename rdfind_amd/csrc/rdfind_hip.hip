@@ -63,6 +63,7 @@ struct rdf_ctx {
     DevBuf rec, rec_tmp, support, fidx, fcap, info, fk, fk_tmp, fpos, cstart, skip, gflag, gexcl, goff, gcap, gmap, csup, doff, dcur, dgrp;
     DevBuf hist, heavy_list, hbit, bcomp, bkeyc, pcnt, poff, pcur, plist;
     DevBuf jhist, rsup, offp;  // capture groups built in join-value ranges (g_build_ranges)
+    DevBuf jbh;                // ... the emission blocks' join-bucket histograms (k_emit_join_bhist)
     DevBuf lsup;               // sharded join ranges: this rank's supports (the all-reduce replaces c->support)
     struct JoinRange { u32 lo, hi; u64 recs; };
     std::vector<JoinRange> jranges;  // the current build's join ranges (pass 1 -> pass 2)
@@ -423,11 +424,11 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
-            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore};
+            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore, &c->jbh};
 }
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
-static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore"};
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh"};
 static void mem_report(rdf_ctx* c) {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
     if (!on) return;
@@ -960,6 +961,8 @@ static rdf_status fc_sum_pairs(rdf_ctx* c, const u64* keys, const u32* cnt, u64 
 // partials = false: frequent keys -> bkeys[0, *B), distinct count -> *nkeys (multi-slice buckets summed by
 // fc_sum_pairs).  partials = true (sharded input): every local (key, count) partial -> the spill list
 // (c->tkeys keys, c->pos counts), *S entries.
+static rdf_status fc_binary_count(rdf_ctx* c, const u64* recs, const u32* bstart, u32 NBc, u32 Gc, bool partials, u64* B,
+                                  u64* nkeys, u64* S);
 static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u32* o, u64 n, bool partials, u64* B,
                                  u64* nkeys, u64* S) {
     hipStream_t st = c->stream;
@@ -980,6 +983,30 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
     ENSURE(c, pos, maxrec * 4);    // spill list: counts
     const u64 bmax = maxrec / std::max<u32>(c->ms, 1) + 1;  // frequent keys: each counts >= ms of <= 3n records
     ENSURE(c, bkeys, bmax * 8);
+    static const int split_mode = getenv("RDFIND_B2_SPLIT") ? atoi(getenv("RDFIND_B2_SPLIT")) : 1;
+    // large inputs: compact records grouped by hash prefix with the radix passes (k_b2_emit, radix_partition_hashed)
+    static const u64 radix_min = getenv("RDFIND_B2_RADIX_MIN") ? strtoull(getenv("RDFIND_B2_RADIX_MIN"), nullptr, 10)
+                                                               : B2_RADIX_MIN;
+    if (split_mode != 0 && 3 * n >= radix_min && maxrec < (1ull << 32)) {
+        ENSURE(c, brkeys2, maxrec * 8);
+        HIP_TRY(c, hipMemsetAsync(dscal(c, 2), 0, 8, st));
+        hipLaunchKernelGGL(k_b2_emit, dim3(grid_for(n, RDF_BLOCK * PART_U, kGrid)), dim3(RDF_BLOCK), 0, st, s, p, o, n, V,
+                           c->fbits.as<u64>(), c->brkeys.as<u64>(), dscal(c, 2));
+        HIP_TRY(c, hipGetLastError());
+        TRY(read_scalars(c, 3));
+        const u64 R = c->hscal[2];
+        int T = 1;  // hash-prefix buckets of about 0.9 counting slice each
+        while (T < 20 && R > ((u64)1 << T) * (B2_SLICE * 9 / 10)) ++T;
+        u64* keys = c->brkeys.as<u64>();
+        u64* tmp = c->brkeys2.as<u64>();
+        HIP_TRY(c, radix_partition_hashed(c->ws, keys, tmp, R, T, ~B2_CBITS, st));
+        const u32 NBh = 1u << T;
+        ENSURE(c, bstart2, ((u64)NBh + 1) * 4);
+        hipLaunchKernelGGL(k_b2_hbounds, dim3(grid_for(R + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, R, T,
+                           c->bstart2.as<u32>());
+        HIP_TRY(c, hipGetLastError());
+        return fc_binary_count(c, keys, c->bstart2.as<u32>(), NBh, 1, partials, B, nkeys, S);
+    }
     const size_t lds = (size_t)NB2 * 4;
     hipLaunchKernelGGL((k_b2_part<false>), dim3(G2), dim3(B2_PBLOCK), lds, st, s, p, o, n, V, c->fbits.as<u64>(), bits,
                        c->uhist.as<u32>(), (u64*)nullptr);
@@ -990,7 +1017,6 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
     // into sub-buckets of about 0.9 slice each (smaller ones pay the counting block's per-slice table setup for
     // nothing); decided on the actual record count, read back only when the 3n bound says it may be needed
     // (RDFIND_B2_SPLIT=2: at least one split bit whatever the size, a test hook for the split path on small inputs)
-    static const int split_mode = getenv("RDFIND_B2_SPLIT") ? atoi(getenv("RDFIND_B2_SPLIT")) : 1;
     // a failed launch would leave uhist stale for the scan and the split below: caught here, not as a fault in a
     // consumer of garbage offsets
     HIP_TRY(c, hipGetLastError());
@@ -1020,6 +1046,14 @@ static rdf_status fc_binary_part(rdf_ctx* c, const u32* s, const u32* p, const u
         recs = c->brkeys2.as<u64>();
         bstart = c->bstart2.as<u32>();
     }
+    return fc_binary_count(c, recs, bstart, NBc, Gc, partials, B, nkeys, S);
+}
+
+// K2 counting of bucketed records (bucket b = recs[bstart[b * G], bstart[(b + 1) * G])): (bucket, slice) list, LDS
+// hash aggregation per slice, spill list summed in one global table
+static rdf_status fc_binary_count(rdf_ctx* c, const u64* recs, const u32* bstart, u32 NBc, u32 Gc, bool partials, u64* B,
+                                  u64* nkeys, u64* S) {
+    hipStream_t st = c->stream;
     ENSURE(c, usl, ((u64)NBc + 1) * 4);
     hipLaunchKernelGGL(k_b2_slices, dim3(grid_for(NBc, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, bstart, NBc, Gc,
                        c->usl.as<u32>());
@@ -1579,7 +1613,7 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
 // offsets of K4/K5: n >= 2^32 / 9 triples; c4 at full size emits ~5.8·10^9 records) or the memory of one pass.  The
 // reference has no such ceiling: Flink's sort-based groupBy("joinValue") spills (ALG/programs/RDFind.scala:339-345).
 // Pass 1 (g_ranges_supports):
-//  1. records per join bucket (k_emit_join_hist) -> consecutive bucket ranges of at most max_range records each;
+//  1. records per join bucket (k_emit_join_bhist) -> consecutive bucket ranges of at most max_range records each;
 //  2. per range: K3-K5 (g_emit_range), its supports summed into c->support (a join value's records are all in one
 //     range, so the ranges' distinct (capture, join) counts add up).
 // Pass 2 (g_ranges_groups):
@@ -1678,10 +1712,16 @@ static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
     const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
     const u32 nr = (u32)ranges.size();
     ENSURE(c, rec, std::max<u64>(c->jr_cap_rec, 1) * 8);  // the ranges' sort buffer
-    std::vector<u32> lo(nr);
-    for (u32 k = 0; k < nr; ++k) lo[k] = ranges[k].lo;
-    ENSURE(c, jrmap, nr * 4ull);
-    HIP_TRY(c, ctx_copy(c, c->jrmap.p, lo.data(), nr * 4ull, hipMemcpyHostToDevice));
+    // the ranges' first join values, then their first join buckets (+ the end)
+    const int jshift = c->joinbits > 14 ? c->joinbits - 14 : 0;
+    std::vector<u32> lo(2 * nr + 1);
+    for (u32 k = 0; k < nr; ++k) {
+        lo[k] = ranges[k].lo;
+        lo[nr + k] = ranges[k].lo >> jshift;
+    }
+    lo[2 * nr] = JH_BUCKETS;
+    ENSURE(c, jrmap, (2 * nr + 1) * 4ull);
+    HIP_TRY(c, ctx_copy(c, c->jrmap.p, lo.data(), (2 * nr + 1) * 4ull, hipMemcpyHostToDevice));
     const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
     const u64 per = n ? (n + eg - 1) / eg : 0;
     const u64 nb = (u64)nr * eg;
@@ -1691,15 +1731,19 @@ static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
     const int recbits = c->capbits + c->joinbits;
     const u32 twoU = 2u * c->U;
     tbegin(c, RDF_T_EMIT);
-    if (n) {
-        if (lazy)
+    if (n) {  // per (range, block) counts from the histogram pass's block rows (RDFIND_RANGE_COUNT=1: a count pass)
+        static const bool count_pass = getenv("RDFIND_RANGE_COUNT") && atoi(getenv("RDFIND_RANGE_COUNT")) != 0;
+        if (count_pass && lazy)
             hipLaunchKernelGGL((k_emit_ranges<false, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
                                c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
                                c->jrmap.as<u32>(), nr, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, recbits);
-        else
+        else if (count_pass)
             hipLaunchKernelGGL((k_emit_ranges<false, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
                                c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
                                c->jrmap.as<u32>(), nr, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, recbits);
+        else
+            hipLaunchKernelGGL(k_range_block_counts, dim3(grid_for(nb * RDF_WAVE, RDF_BLOCK, 1u << 30)), dim3(RDF_BLOCK), 0, st,
+                               c->jbh.as<u32>(), eg, c->jrmap.as<u32>() + nr, nr, c->eblk.as<u64>());
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), nb, c->eblk.as<u64>() + nb, st));
     }
@@ -1740,11 +1784,22 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     const int jshift = joinbits > 14 ? joinbits - 14 : 0;
     ENSURE(c, jhist, JH_BUCKETS * 8);
     HIP_TRY(c, hipMemsetAsync(c->jhist.p, 0, JH_BUCKETS * 8, st));
+    // the blocks of the emission (g_emit_all_ranges): their bucket histograms give its per-range block offsets
+    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const u64 per = n ? (n + eg - 1) / eg : 0;
+    ENSURE(c, jbh, (u64)eg * JH_BUCKETS * 4);
     tbegin(c, RDF_T_EMIT);
-    if (n)
-        hipLaunchKernelGGL(k_emit_join_hist, dim3(grid_for(n, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, V,
-                           2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits,
-                           own, jshift, c->jhist.as<u64>());
+    if (n) {
+        if (own.nranks > 1)
+            hipLaunchKernelGGL(k_emit_join_bhist<true>, dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, own,
+                               jshift, c->jbh.as<u32>(), c->jhist.as<u64>());
+        else
+            hipLaunchKernelGGL(k_emit_join_bhist<false>, dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, own,
+                               jshift, c->jbh.as<u32>(), c->jhist.as<u64>());
+        HIP_TRY(c, hipGetLastError());
+    }
     tend(c, RDF_T_EMIT);
     std::vector<u64> h(JH_BUCKETS);
     HIP_TRY(c, hipMemcpyAsync(h.data(), c->jhist.p, JH_BUCKETS * 8, hipMemcpyDeviceToHost, st));

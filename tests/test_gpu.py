@@ -411,9 +411,12 @@ def test_binary_keys_right_after_frequent_conditions(ctx):
         assert (early[1:] > early[:-1]).all()  # sorted, unpacked keys
 
 
-def test_k2_split_forced_small_inputs(monkeypatch):
-    """The K2 sub-bucket split (k_b2_split, which large inputs take: c3 / c4) forced on small inputs (RDFIND_B2_SPLIT=2,
-    read once per process: a child process) gives the oracle's sets in every mode and c1/c5 samples' checksums."""
+@pytest.mark.parametrize("env", [{"RDFIND_B2_SPLIT": "2"}, {"RDFIND_B2_RADIX_MIN": "1"}], ids=["split", "radix"])
+def test_k2_split_forced_small_inputs(monkeypatch, env):
+    """The K2 paths of large inputs forced on small ones (read once per process: a child process): the sub-bucket split
+    (k_b2_split, RDFIND_B2_SPLIT=2) and the hash-prefix radix grouping of compact records (k_b2_emit +
+    radix_partition_hashed, which inputs of 3n >= 2^27 records take: c3, c4; RDFIND_B2_RADIX_MIN=1) give the oracle's
+    sets in every mode and c1/c5 samples' checksums."""
     import json
     import subprocess
     import sys
@@ -446,7 +449,7 @@ with _lib.Context(0) as g:
             bad.append(cfg)
 print(json.dumps({"bad": bad}))
 """
-    r = subprocess.run([sys.executable, "-c", child, root], env=dict(os.environ, RDFIND_B2_SPLIT="2"), capture_output=True,
+    r = subprocess.run([sys.executable, "-c", child, root], env=dict(os.environ, **env), capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1])["bad"] == []
