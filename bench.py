@@ -41,6 +41,15 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip-level parameters)
 RADIX_MAX_BITS = 9     # widest radix digit of the library's sorts (rdfind_amd/csrc/primitives.hip RS_MAX_BITS)
 
+
+def sort_passes(bits):
+    """Digit passes of a library sort of `bits` key bits (primitives.hip sort_digit_bits: 10-bit digits when that saves
+    a pass, unless RDFIND_SORT10=0)."""
+    rs = RADIX_MAX_BITS
+    if os.environ.get("RDFIND_SORT10", "1") != "0" and -(-bits // 10) < -(-bits // rs):
+        rs = 10
+    return -(-bits // rs)
+
 # timer family -> its kernels, whose rocprofv3 PMC traffic (profiles/pmc_<config>.json, tools/pmc.sh) is summed
 FAMILY_KERNELS = {
     "unary": ["k_u2_part", "k_u2_slices", "k_u2_count", "k_u2_finish", "k_u2_fval"],
@@ -459,10 +468,9 @@ def main():
     V = d.num_terms
     capbits = int(2 * sum(fc["n_frequent_unary"]) + fc["n_frequent_binary"] - 1).bit_length()  # compact capture ids
     joinbits = max(int(V - 1).bit_length(), 1)
-    rs = RADIX_MAX_BITS  # digits of <= 10 bits (primitives.hip RS_MAX_BITS)
     # the first pass reads every emitted record slot, the others only the records it kept (repeats dropped)
-    counts = {"sort_passes_records": gs["n_records"] + ((capbits + joinbits + rs - 1) // rs - 1) * gs["n_sorted_records"],
-              "group_passes": (joinbits + rs - 1) // rs}
+    counts = {"sort_passes_records": gs["n_records"] + (sort_passes(capbits + joinbits) - 1) * gs["n_sorted_records"],
+              "group_passes": sort_passes(joinbits)}
     fams = family_rooflines(d, fc, gs, cs, kt, counts)
     if total_scale == 1.0 and world == 1:  # HBM bytes per step from the committed PMC summary of this config
         for name, f in fams.items():

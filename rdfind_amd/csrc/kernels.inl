@@ -813,7 +813,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_entries(const u32* __restric
 // value this rank takes, its range from the bucket -> range map (join >> jshift, JH_BUCKETS buckets).  Pass 1 counts
 // per (bin, block) -> ghist[bin * G + block]; pass 2 writes the triple indices at the scanned offsets (LDS cursors).
 // Each block takes one contiguous chunk of triples, so the entries of a bin ascend by block.
-static constexpr u32 JH_BUCKETS = 1u << 14;  // join buckets of the join-range build (join >> jshift)
+#ifndef RDF_JH_BITS
+#define RDF_JH_BITS 14
+#endif
+static constexpr int JH_BITS = RDF_JH_BITS;
+static constexpr u32 JH_BUCKETS = 1u << JH_BITS;  // join buckets of the join-range build (join >> jshift)
 static constexpr u32 RE_MAX_BINS = 3 * 1024;
 template <bool SCATTER>
 __global__ __launch_bounds__(RDF_BLOCK) void k_range_entries(const u32* __restrict__ s, const u32* __restrict__ p,
@@ -2304,8 +2308,8 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     if (lane == 0 && (alive0 & ~alive)) atomicOr(&dead[oct0], alive0 & ~alive);
 }
 // Occupancy per variant (waves per SIMD; the register budget follows): the staging variant (small groups, c2) is
-// fastest unconstrained (151 VGPRs, 3 waves); the plain variant (large groups, c4) at RDF_LIGHT_PLAIN_WAVES
-// (profiles/r04_light_ab_occupancy.log)
+// fastest unconstrained (122 VGPRs, 4 waves; 5 waves with spills measured no better: profiles/r05_light_ab_occupancy.log);
+// the plain variant (large groups, c4) at RDF_LIGHT_PLAIN_WAVES (profiles/r04_light_ab_occupancy.log)
 #ifdef RDF_LIGHT_STAGE_WAVES
 #define RDF_LIGHT_STAGE_ATTR __attribute__((amdgpu_waves_per_eu(RDF_LIGHT_STAGE_WAVES)))
 #else

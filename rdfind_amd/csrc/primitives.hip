@@ -479,6 +479,19 @@ static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, in
     return hipSuccess;
 }
 
+// Widest digit of a sort of `bits` bits: RS_MAX_BITS, or 10 when that saves a whole pass (c4 at 10^9 triples: 50-bit
+// records in 5 passes instead of 6; RDFIND_SORT10=0: never)
+static hipError_t radix_sort_dmax(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, int dmax, hipStream_t st);
+static int sort_digit_bits(int bits) {
+    static const bool ten = !(getenv("RDFIND_SORT10") && atoi(getenv("RDFIND_SORT10")) == 0);
+    return ten && RS_MAX_BITS < 10 && (bits + 9) / 10 < (bits + RS_MAX_BITS - 1) / RS_MAX_BITS ? 10 : RS_MAX_BITS;
+}
+
+int radix_sort_passes(int bits) {
+    const int d = sort_digit_bits(bits);
+    return bits > 0 ? (bits + d - 1) / d : 0;
+}
+
 // Sort of keys some of which are padding (~0): the first pass drops them, *n_out (host) = the other keys, which the
 // remaining passes sort.  One host read-back between the first and the second pass.
 hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u32* d_kept, u64* n_out,
@@ -486,10 +499,11 @@ hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int 
     *n_out = 0;
     if (n == 0 || bits <= 0) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;
-    const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
+    const int dmax = sort_digit_bits(bits);
+    const int passes = (bits + dmax - 1) / dmax;
     const int w0 = bits / passes + (0 < bits % passes ? 1 : 0);
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
-    u32* hist = (u32*)ws.scratch(((u64)tiles << RS_MAX_BITS) * sizeof(u32), 1);
+    u32* hist = (u32*)ws.scratch(((u64)tiles << dmax) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
     hipError_t e = w0 <= 8 ? radix_pass<8>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept)
                  : w0 == 9 ? radix_pass<9>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept)
@@ -501,17 +515,22 @@ hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int 
     if (e != hipSuccess) return e;
     std::swap(keys, tmp);
     *n_out = kept;
-    return radix_sort_u64_bits(ws, keys, tmp, kept, w0, bits, st);
+    return radix_sort_dmax(ws, keys, tmp, kept, w0, bits, dmax, st);
 }
 
-// Passes of at most RS_MAX_BITS bits, as even as possible (43 bits: 9+9+9+8+8 instead of six 8-bit passes)
+// Passes of at most RS_MAX_BITS bits (10 when that saves a pass), as even as possible (43 bits: 9+9+9+8+8 instead of
+// six 8-bit passes)
 hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st) {
+    return radix_sort_dmax(ws, keys, tmp, n, lo, hi, sort_digit_bits(hi - lo), st);
+}
+
+static hipError_t radix_sort_dmax(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, int dmax, hipStream_t st) {
     if (n < 2 || hi <= lo) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
     const int bits = hi - lo;
-    const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
-    u32* hist = (u32*)ws.scratch(((u64)tiles << RS_MAX_BITS) * sizeof(u32), 1);
+    const int passes = (bits + dmax - 1) / dmax;
+    u32* hist = (u32*)ws.scratch(((u64)tiles << dmax) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
     int shift = lo;
     for (int p = 0; p < passes; ++p) {

@@ -101,6 +101,7 @@ static_assert(RS_MAX_BITS >= 8 && RS_MAX_BITS <= 10, "digit kernels exist for 8,
 hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u32* d_kept, u64* n_out,
                                hipStream_t st);
 hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st);
+int radix_sort_passes(int bits);  // passes of a sort of `bits` key bits
 hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u64 hmask, hipStream_t st);
 
 }  // namespace rdf

@@ -73,6 +73,7 @@ struct rdf_ctx {
     DevBuf rstore;
     std::vector<u64> jr_seg, jr_J;   // range k's slots in rstore start at jr_seg[k]; its sorted records
     bool jr_keep = false, range_keep = true;
+    u64 peak_bytes = 0;              // RDFIND_MEM_REPORT: the largest sum of the buffers' sizes so far
     // per range (triple, attribute) entry lists (g_range_entries): a range's emissions read only its own triples
     DevBuf jrmap, jrhist, jent;      // join bucket -> range, per (bin, block) counts, the entries (bin-major)
     std::vector<u64> jr_bin;         // first entry of bin 3 range + attribute (+ the total)
@@ -268,9 +269,12 @@ static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
     (void)hipGetLastError();
     return any;
 }
+static void mem_track(rdf_ctx* c);
 static rdf_status ensure_buf(rdf_ctx* c, DevBuf* b, size_t bytes, const char* what) {
+    const size_t cap0 = b->cap;
     hipError_t e = b->ensure(bytes);
     if (e == hipErrorOutOfMemory && reclaim_spare(c, b)) e = b->ensure(bytes);
+    if (e == hipSuccess && b->cap != cap0) mem_track(c);
     if (e != hipSuccess)
         return fail(c, e == hipErrorOutOfMemory ? RDF_ERR_OOM : RDF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
     return RDF_OK;
@@ -429,9 +433,19 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
 static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh"};
-static void mem_report(rdf_ctx* c) {
+static bool mem_report_on() {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
-    if (!on) return;
+    return on;
+}
+// the context's peak of buffer bytes (RDFIND_MEM_REPORT only: summed at every allocation that changes a buffer)
+static void mem_track(rdf_ctx* c) {
+    if (!mem_report_on()) return;
+    size_t total = c->ws.bytes();
+    for (DevBuf* b : ctx_buffers(c)) total += b->cap;
+    c->peak_bytes = std::max<u64>(c->peak_bytes, total);
+}
+static void mem_report(rdf_ctx* c) {
+    if (!mem_report_on()) return;
     std::vector<DevBuf*> bufs = ctx_buffers(c);
     std::vector<std::pair<size_t, const char*>> big;
     size_t total = 0;
@@ -442,7 +456,8 @@ static void mem_report(rdf_ctx* c) {
     std::sort(big.begin(), big.end(), [](const std::pair<size_t, const char*>& x, const std::pair<size_t, const char*>& y) {
         return x.first > y.first;
     });
-    fprintf(stderr, "MEM total %.2f GiB (workspace %.2f GiB):", total / 1073741824.0, c->ws.bytes() / 1073741824.0);
+    fprintf(stderr, "MEM total %.2f GiB, peak %.2f GiB (workspace %.2f GiB):", total / 1073741824.0,
+            std::max<u64>(c->peak_bytes, total) / 1073741824.0, c->ws.bytes() / 1073741824.0);
     for (const auto& b : big) fprintf(stderr, " %s=%.2f", b.second, b.first / 1073741824.0);
     fprintf(stderr, "\n");
 }
@@ -1476,7 +1491,7 @@ static rdf_status g_sort_support(rdf_ctx* c, u64* keys, u64* tmp, u64 Je, u32* s
     tend(c, RDF_T_SORT);
     *Jout = J;
     c->rec_sorted = keys;
-    c->sort_passes_records += Je + (u64)((capbits + joinbits + RS_MAX_BITS - 1) / RS_MAX_BITS - 1) * J;
+    c->sort_passes_records += Je + (u64)(radix_sort_passes(capbits + joinbits) - 1) * J;
     // supports = distinct join values per capture: fresh (capture, join) records counted per key run
     ENSURE(c, flags, std::max<u64>(J, 1) * 4);
     ENSURE(c, fpos, (J + 1) * 4);
@@ -1713,7 +1728,7 @@ static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
     const u32 nr = (u32)ranges.size();
     ENSURE(c, rec, std::max<u64>(c->jr_cap_rec, 1) * 8);  // the ranges' sort buffer
     // the ranges' first join values, then their first join buckets (+ the end)
-    const int jshift = c->joinbits > 14 ? c->joinbits - 14 : 0;
+    const int jshift = c->joinbits > JH_BITS ? c->joinbits - JH_BITS : 0;
     std::vector<u32> lo(2 * nr + 1);
     for (u32 k = 0; k < nr; ++k) {
         lo[k] = ranges[k].lo;
@@ -1781,7 +1796,7 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     // the frequent-condition stage's record scratch (up to 84 GB at 10^9 triples) is spare from here on: reclaimed
     // by the range buffers' allocation if they need the room
     // 1. ranges
-    const int jshift = joinbits > 14 ? joinbits - 14 : 0;
+    const int jshift = joinbits > JH_BITS ? joinbits - JH_BITS : 0;
     ENSURE(c, jhist, JH_BUCKETS * 8);
     HIP_TRY(c, hipMemsetAsync(c->jhist.p, 0, JH_BUCKETS * 8, st));
     // the blocks of the emission (g_emit_all_ranges): their bucket histograms give its per-range block offsets
@@ -2716,7 +2731,7 @@ static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorte
     hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                        c->epairs.as<u64>(), E, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
     tend(c, RDF_T_ESORT);
-    c->sort_passes_pairs = presorted ? 0 : (u64)((32 + bits_for(C ? C - 1 : 0) + RS_MAX_BITS - 1) / RS_MAX_BITS) * E;
+    c->sort_passes_pairs = presorted ? 0 : (u64)radix_sort_passes(32 + bits_for(C ? C - 1 : 0)) * E;
     v.eoff = c->eoff.as<u64>();
     v.epairs = c->epairs.as<u64>();
     v.ebin = c->ebin.as<u64>();
