@@ -44,9 +44,9 @@ RADIX_MAX_BITS = 9     # widest radix digit of the library's sorts (rdfind_amd/c
 
 def sort_passes(bits):
     """Digit passes of a library sort of `bits` key bits (primitives.hip sort_digit_bits: 10-bit digits when that saves
-    a pass, unless RDFIND_SORT10=0)."""
+    a pass, with RDFIND_SORT10=1 only)."""
     rs = RADIX_MAX_BITS
-    if os.environ.get("RDFIND_SORT10", "1") != "0" and -(-bits // 10) < -(-bits // rs):
+    if os.environ.get("RDFIND_SORT10", "0") not in ("", "0") and -(-bits // 10) < -(-bits // rs):
         rs = 10
     return -(-bits // rs)
 

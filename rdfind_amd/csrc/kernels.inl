@@ -865,6 +865,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_range_entries(const u32* __restri
 // 1.5-2 TB/s.
 static constexpr int STREAM_U = 4;
 
+static constexpr u64 CSTART_GAP = 64;  // run starts a k_fresh_bounds thread writes per gap of absent captures
 __global__ __launch_bounds__(RDF_BLOCK) void k_fresh_bounds(const u64* __restrict__ keys, u64 n, u64 ncap, int joinbits,
                                                             u32* fresh, u32* cstart) {
     const u64 T = (u64)gridDim.x * RDF_BLOCK;
@@ -883,9 +884,19 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_fresh_bounds(const u64* __restric
             if (i < n) fresh[i] = (i == 0 || kp[u] != k[u]) ? 1u : 0u;
             const u64 c = i < n ? k[u] >> joinbits : ncap;
             const u64 cp = i ? (kp[u] >> joinbits) + 1 : 0;
-            for (u64 x = cp; x <= c; ++x) cstart[x] = (u32)i;
+            // the captures in (previous record's, this record's]: at most CSTART_GAP of them here (the gap's end);
+            // the rest of a longer gap keeps the caller's fill and k_cstart_fix finds it (a thread looping over a
+            // gap of millions of absent captures -- a join range holding only high capture ids -- took 20 ms)
+            for (u64 x = c + 1 > cp + CSTART_GAP ? c + 1 - CSTART_GAP : cp; x <= c; ++x) cstart[x] = (u32)i;
         }
     }
+}
+
+// run starts k_fresh_bounds left unwritten (cstart filled with ~0 before it): the first record of capture >= x
+__global__ __launch_bounds__(RDF_BLOCK) void k_cstart_fix(const u64* __restrict__ keys, u64 n, u64 ncap, int joinbits,
+                                                          u32* cstart) {
+    for (u64 x = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; x <= ncap; x += (u64)gridDim.x * RDF_BLOCK)
+        if (cstart[x] == ~0u) cstart[x] = (u32)(x == ncap ? n : lower_bound_u64(keys, n, x << joinbits));
 }
 
 // support of capture c = distinct join values among its records = fresh records of its run; fpos = exclusive
@@ -1026,21 +1037,24 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_key_offsets(const u64* __restrict
 // k_emit_ranges: per = ceil(n / gridDim.x)): the block's bucket counts -> bh[block * JH_BUCKETS + bucket], the totals
 // -> hist.  A triple's records joined on one attribute share a join value: one LDS atomic per attribute
 // (triple_records' group counts).
+// 1024 threads per block: the 64-KB LDS histogram allows two blocks per CU, so the block is what sets the waves in
+// flight for the gathers (256 threads: 2 waves per SIMD)
+static constexpr int JH_BLOCK = 1024;
 template <bool LAZY>
-__global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_bhist(const u32* __restrict__ s, const u32* __restrict__ p,
+__global__ __launch_bounds__(JH_BLOCK) void k_emit_join_bhist(const u32* __restrict__ s, const u32* __restrict__ p,
                                                                const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
                                                                const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                                const u32* __restrict__ lvals, u64 lmask, int proj,
                                                                int joinbits, JoinSel own, int jshift, u32* bh, u64* hist) {
     __shared__ u32 lh[JH_BUCKETS];
-    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lh[k] = 0;
+    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += JH_BLOCK) lh[k] = 0;
     __syncthreads();
     JoinSel all = own;  // this rank's join values (sharded: hash or hot-table owner), every range
     all.lo = 0u;
     all.hi = JOIN_ALL_HI;
     const u64 b = (u64)blockIdx.x * per;
     const u64 e = b + per < n ? b + per : n;
-    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
+    for (u64 i = b + threadIdx.x; i < e; i += JH_BLOCK) {
         u64 rec[9];
         u32 grp = 0;
         const u32 c = triple_records<LAZY>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, all, rec,
@@ -1052,7 +1066,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_join_bhist(const u32* __rest
     }
     __syncthreads();
     u32* row = bh + (u64)blockIdx.x * JH_BUCKETS;
-    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) {
+    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += JH_BLOCK) {
         const u32 x = lh[k];
         row[k] = x;
         if (x) atomicAdd(&hist[k], (u64)x);

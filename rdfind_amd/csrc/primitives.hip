@@ -479,11 +479,12 @@ static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, in
     return hipSuccess;
 }
 
-// Widest digit of a sort of `bits` bits: RS_MAX_BITS, or 10 when that saves a whole pass (c4 at 10^9 triples: 50-bit
-// records in 5 passes instead of 6; RDFIND_SORT10=0: never)
+// Widest digit of a sort of `bits` bits: RS_MAX_BITS; with RDFIND_SORT10=1, 10 when that saves a whole pass (measured
+// slower: c4 at 10^9 triples sorts its 50-bit records in 5 passes of 10 bits in 362 ms against 234 ms for 6 passes of
+// <= 9 bits, c3 21.8 vs 19.0 ms: 1,024 bins leave ~4 keys per bin of a 4096-key tile; profiles/r05_sort10_ab.log)
 static hipError_t radix_sort_dmax(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, int dmax, hipStream_t st);
 static int sort_digit_bits(int bits) {
-    static const bool ten = !(getenv("RDFIND_SORT10") && atoi(getenv("RDFIND_SORT10")) == 0);
+    static const bool ten = getenv("RDFIND_SORT10") && atoi(getenv("RDFIND_SORT10")) != 0;
     return ten && RS_MAX_BITS < 10 && (bits + 9) / 10 < (bits + RS_MAX_BITS - 1) / RS_MAX_BITS ? 10 : RS_MAX_BITS;
 }
 
@@ -557,7 +558,8 @@ hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, i
     if (n < 2 || bits <= 0) return hipSuccess;
     if (n >= (1ull << 32) || bits > 30) return hipErrorInvalidValue;
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
-    const int passes = (bits + 9) / 10;
+    static const int pdig = getenv("RDFIND_PART_DIGIT") ? std::max(8, std::min(10, atoi(getenv("RDFIND_PART_DIGIT")))) : 10;
+    const int passes = (bits + pdig - 1) / pdig;
     u32* hist = (u32*)ws.scratch(((u64)tiles << 10) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
     int shift = 64 - bits;

@@ -1384,7 +1384,6 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     hipStream_t st = c->stream;
     const u64 n = c->n;
     const u32 V = c->V ? c->V : 1;
-    const u64 ncap = c->ncap;
     const int capbits = c->capbits, joinbits = c->joinbits;
     HIP_TRY(c, hipMemsetAsync(c->scal.p, 0, 16 * sizeof(u64), st));
     ENSURE(c, rec, std::max<u64>(cap_rec, 1) * 8);
@@ -1473,6 +1472,17 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     return g_sort_support(c, ebuf, c->rec_tmp.as<u64>(), Je, sup, Jout, nullptr);
 }
 
+// fresh-record flags (c->flags) and capture run starts (c->cstart[0, ncap]) of J sorted records
+static rdf_status g_fresh_bounds(rdf_ctx* c, const u64* keys, u64 J) {
+    hipStream_t st = c->stream;
+    HIP_TRY(c, hipMemsetAsync(c->cstart.p, 0xff, (c->ncap + 1) * 4, st));
+    hipLaunchKernelGGL(k_fresh_bounds, dim3(grid_for(J + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, c->ncap,
+                       c->joinbits, c->flags.as<u32>(), c->cstart.as<u32>());
+    hipLaunchKernelGGL(k_cstart_fix, dim3(grid_for(c->ncap + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, c->ncap,
+                       c->joinbits, c->cstart.as<u32>());
+    return RDF_OK;
+}
+
 // K4 sort of Je emitted record slots (keys, with tmp as the other buffer; padding dropped) and K5 supports -> sup.
 // keep_out: the sorted records must end there (keys == keep_out: a range of rstore, copied back after an odd number of
 // passes).  Sets c->rec_sorted, *Jout.
@@ -1497,8 +1507,7 @@ static rdf_status g_sort_support(rdf_ctx* c, u64* keys, u64* tmp, u64 Je, u32* s
     ENSURE(c, fpos, (J + 1) * 4);
     ENSURE(c, cstart, (ncap + 1) * 4);
     tbegin(c, RDF_T_SUPPORT);
-    hipLaunchKernelGGL(k_fresh_bounds, dim3(grid_for(J + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, ncap, joinbits,
-                       c->flags.as<u32>(), c->cstart.as<u32>());
+    TRY(g_fresh_bounds(c, keys, J));
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), J, c->fpos.as<u32>() + J, st));
     if (ncap)
         hipLaunchKernelGGL(k_run_support, dim3(grid_for(ncap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->cstart.as<u32>(),
@@ -1806,11 +1815,11 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     tbegin(c, RDF_T_EMIT);
     if (n) {
         if (own.nranks > 1)
-            hipLaunchKernelGGL(k_emit_join_bhist<true>, dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+            hipLaunchKernelGGL(k_emit_join_bhist<true>, dim3(eg), dim3(JH_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
                                c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, own,
                                jshift, c->jbh.as<u32>(), c->jhist.as<u64>());
         else
-            hipLaunchKernelGGL(k_emit_join_bhist<false>, dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
+            hipLaunchKernelGGL(k_emit_join_bhist<false>, dim3(eg), dim3(JH_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, 2u * c->U,
                                c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, joinbits, own,
                                jshift, c->jbh.as<u32>(), c->jhist.as<u64>());
         HIP_TRY(c, hipGetLastError());
@@ -1880,8 +1889,7 @@ static rdf_status g_restore_range(rdf_ctx* c, size_t k, u64* Jout) {
     ENSURE(c, cstart, (ncap + 1) * 4);
     ENSURE(c, rec, std::max<u64>(c->jr_cap_rec, 1) * 8);  // the kept records' destination (dk) in pass 2
     tbegin(c, RDF_T_SUPPORT);
-    hipLaunchKernelGGL(k_fresh_bounds, dim3(grid_for(J + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, J, ncap,
-                       c->joinbits, c->flags.as<u32>(), c->cstart.as<u32>());
+    TRY(g_fresh_bounds(c, keys, J));
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->flags.as<u32>(), c->fpos.as<u32>(), J, c->fpos.as<u32>() + J, st));
     tend(c, RDF_T_SUPPORT);
     c->rec_sorted = keys;
