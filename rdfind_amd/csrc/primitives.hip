@@ -298,7 +298,10 @@ hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32
 //            LDS, then written out as contiguous per-digit runs (coalesced stores instead of 8-byte
 //            scattered ones).
 
-static constexpr int RS_ITEMS = 16;                              // keys per lane per tile
+#ifndef RDF_RS_ITEMS
+#define RDF_RS_ITEMS 16
+#endif
+static constexpr int RS_ITEMS = RDF_RS_ITEMS;                    // keys per lane per tile
 static constexpr int RS_TILE = RDF_BLOCK * RS_ITEMS;             // 4096 keys per tile
 static constexpr int RS_WAVE_KEYS = RDF_WAVE * RS_ITEMS;         // 1024 keys per wave
 
@@ -552,13 +555,15 @@ hipError_t radix_sort_u64(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits,
     return radix_sort_u64_bits(ws, keys, tmp, n, 0, bits, st);
 }
 
-// Keys grouped by bits [64 - bits, 64) of mix64(key & hmask), ascending (LSD passes of <= 10 bits over those hash bits;
+// Keys grouped by bits [64 - bits, 64) of mix64(key & hmask), ascending (LSD passes of <= 9 bits over those hash bits;
 // within a group the order is the passes' stable order).  keys / tmp swap like radix_sort_u64_bits.
 hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u64 hmask, hipStream_t st) {
     if (n < 2 || bits <= 0) return hipSuccess;
     if (n >= (1ull << 32) || bits > 30) return hipErrorInvalidValue;
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
-    static const int pdig = getenv("RDFIND_PART_DIGIT") ? std::max(8, std::min(10, atoi(getenv("RDFIND_PART_DIGIT")))) : 10;
+    // digits of <= 9 bits (c4 at 10^9 triples: 20 bits in 3 passes 89.6 ms of K2, in 2 passes of 10 bits 96.0 ms: a
+    // 1,024-bin digit leaves ~4 keys per bin of a tile; RDFIND_PART_DIGIT overrides, 8..10)
+    static const int pdig = getenv("RDFIND_PART_DIGIT") ? std::max(8, std::min(10, atoi(getenv("RDFIND_PART_DIGIT")))) : 9;
     const int passes = (bits + pdig - 1) / pdig;
     u32* hist = (u32*)ws.scratch(((u64)tiles << 10) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
