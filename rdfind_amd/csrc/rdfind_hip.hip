@@ -1695,7 +1695,7 @@ static rdf_status g_range_entries(rdf_ctx* c, int proj, JoinSel own, int jshift)
 static rdf_status g_range_keep_plan(rdf_ctx* c) {
     const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
     c->jr_keep = false;
-    if (!c->range_keep || ranges.size() < 2 || ranges.size() > EMIT_MAX_RANGES) return RDF_OK;
+    if (!c->range_keep || ranges.empty() || ranges.size() > EMIT_MAX_RANGES) return RDF_OK;
     u64 total = 0;
     c->jr_seg.assign(ranges.size() + 1, 0);
     c->jr_J.assign(ranges.size(), 0);
