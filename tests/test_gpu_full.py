@@ -196,7 +196,7 @@ print(json.dumps(out))
                                  {"RDFIND_SWEEP_F": "1000000000", "RDFIND_LIGHT2": "1", "RDFIND_DENSE": "0"},
                                  {"RDFIND_LIGHT_HIOCC": "1"}, {"RDFIND_LIGHT_HIOCC": "0"}, {"RDFIND_PIVX": "0"},
                                  {"RDFIND_PIVX_N": "2"}, {"RDFIND_PIVX_PACKED": "1"}])
-def test_light_variants_full_size(env):
+def test_light_variants_full_size(ctx, env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
     paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
     verify passes forced instead of one light pass, pass B group-major for every dependent or none, window range sweeps
@@ -207,6 +207,7 @@ def test_light_variants_full_size(env):
     import subprocess
     import sys
 
+    ctx.release_scratch()  # the module context's buffers from the full-size runs (c5 at 0.3: ~100 GB) would starve the child
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     keys = ["c1@1.0/s1_clean", "c2@1.0/s1_clean"]
     if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N",
@@ -276,7 +277,7 @@ print(json.dumps({"bad": bad}))
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("heavy_min,gm", [("64", "1"), ("2", "1"), ("64", "2"), ("2", "2")])
-def test_two_light_passes_random(heavy_min, gm):
+def test_two_light_passes_random(ctx, heavy_min, gm):
     """The filter + verify light passes forced on random inputs (RDFIND_LIGHT2=1; LIGHT_PRE_MAX defers every chunk of
     a multi-chunk dependent) against the C oracle in three modes, with and without lowered heavy columns, pass B
     choosing group-major per dependent (RDFIND_LIGHT_GM=1) or group-major for every dependent (2).  In its own
@@ -284,6 +285,7 @@ def test_two_light_passes_random(heavy_min, gm):
     import subprocess
     import sys
 
+    ctx.release_scratch()  # the module context's pages of c5 at full size stay allocated otherwise
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, RDFIND_LIGHT2="1", RDFIND_HEAVY_MIN=heavy_min, RDFIND_LIGHT_GM=gm)
     r = subprocess.run([sys.executable, "-c", _TWO_PASS_CHILD, root, "71" + heavy_min], env=env, capture_output=True,
