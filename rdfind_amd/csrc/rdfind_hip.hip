@@ -118,6 +118,8 @@ struct rdf_ctx {
     int pivx_kept = 0;  // extra pivots the pivot pass computed this run (PIV_EXTRA_PLAIN or PIV_EXTRA)
     int light_npx = 0;  // ... and how many k_light checks
     DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
+    u32* dbits_p = nullptr;      // the bitmaps in use: dbits, or the idle kept store (rstore_lent)
+    bool rstore_lent = false;    // rstore holds the discovery's dense bitmaps (not reclaimable) until the next build
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
     int dense_div = -1;                   // RDFIND_DENSE (0: no bitmaps; -1: by input, d_dense_flags)
@@ -260,7 +262,7 @@ static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
     for (int k = 0; k < 3; ++k) {
         if (!(k == 0 ? c->spare_fc : k == 1 ? c->spare_groups : c->spare_x)) continue;
         for (DevBuf* b : (k == 0 ? fc_scratch : k == 1 ? grp_scratch : x_scratch)) {
-            if (b == keep || !b->p) continue;
+            if (b == keep || !b->p || (b == &c->rstore && c->rstore_lent)) continue;
             if (!any) (void)hipStreamSynchronize(c->stream);  // queued kernels may still read them
             b->release();
             any = true;
@@ -573,6 +575,7 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next, bool always = false) {
         if (!kept(b)) b->release();
     c->ws.release();
     c->dense_on = false;
+    c->rstore_lent = false;
     c->class_pending = false;
     c->h_runs_valid = false;
     c->h_bkeys_valid = false;
@@ -1349,6 +1352,8 @@ static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj
 static rdf_status g_record_bits(rdf_ctx* c) {
     c->spare_groups = false;  // a group build starts: its record buffers are in use
     c->jr_keep = false;
+    c->rstore_lent = false;   // (the previous discovery's bitmaps in rstore are not read again)
+    c->dense_on = false;
     const u32 V = c->V ? c->V : 1;
     const u64 ncap = 2ull * c->U + c->B;  // compact candidate captures (k_frank_final)
     const int capbits = bits_for(ncap ? ncap - 1 : 0);
@@ -2218,7 +2223,7 @@ static CindView make_view(rdf_ctx* c, uint32_t flags) {
     v.pivx = c->pivx_on ? c->pivx.as<u32>() : nullptr;
     v.npx = 0;  // set per k_light launch (d_light_kernels)
     v.gdrow = c->dense_on ? c->gdrow.as<u32>() : nullptr;
-    v.dbits = c->dense_on ? c->dbits.as<u32>() : nullptr;
+    v.dbits = c->dense_on ? c->dbits_p : nullptr;
     v.dwords = c->dwords;
     v.prefilter = 0;
     v.p2done = 0;
@@ -2265,6 +2270,14 @@ static rdf_status d_dense_build(rdf_ctx* c, CindView& v, u64 nrows) {
     size_t hfree = 0, htotal = 0;
     if (hipMemGetInfo(&hfree, &htotal) == hipSuccess) budget = std::min<u64>(budget, std::max<u64>(c->dbits.cap, hfree / 2));
     (void)hipGetLastError();
+    // RDFIND_DENSE_LEND=1: the kept store of a join-range build (c4 at 10^9 triples: 43.6 GiB, idle until the next
+    // build) holds the bitmaps when it has room for more rows than the budget.  Measured slower: c4 at 10^9 with all
+    // 79,141 wanted rows (25 GB) 156 ms of light pass against 141 ms with the 8-GiB budget's 27,213 rows (the extra
+    // rows' probes are single 4-B reads in 315-KB rows, each a cache miss; profiles/r05_dense_lend_ab.log)
+    static const bool lend_ok = getenv("RDFIND_DENSE_LEND") && atoi(getenv("RDFIND_DENSE_LEND")) != 0;
+    const bool lend = lend_ok && c->spare_groups && c->rstore.p && !getenv("RDFIND_DENSE_BYTES") &&
+                      c->rstore.cap / (dwords * 4) > budget / (dwords * 4);
+    if (lend) budget = c->rstore.cap;
     const u64 rows = std::min<u64>(nrows, budget / (dwords * 4));
     if (getenv("RDFIND_DEBUG_LIGHT"))
         fprintf(stderr, "dense: C %llu G %llu rows %llu of %llu, %.1f MB\n", (unsigned long long)C, (unsigned long long)G,
@@ -2273,18 +2286,24 @@ static rdf_status d_dense_build(rdf_ctx* c, CindView& v, u64 nrows) {
     ENSURE(c, dlist, rows * 4);
     // the bitmaps only speed the light pass up: without the memory for them the member lists serve (no reclaim of the
     // spare scratch for them either: the next run would allocate that again)
-    if (c->dbits.ensure(rows * dwords * 4) != hipSuccess) return RDF_OK;
+    if (lend) {
+        c->rstore_lent = true;
+        c->dbits_p = c->rstore.as<u32>();
+    } else {
+        if (c->dbits.ensure(rows * dwords * 4) != hipSuccess) return RDF_OK;
+        c->dbits_p = c->dbits.as<u32>();
+    }
     tbegin(c, RDF_T_LIGHT);
     hipLaunchKernelGGL(k_dense_rows, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gflag.as<u32>(),
                        c->gexcl.as<u32>(), G, (u32)rows, c->gdrow.as<u32>(), c->dlist.as<u32>());
     hipLaunchKernelGGL(k_dense_build, dim3((unsigned)std::min<u64>(rows, 4096)), dim3(RDF_BLOCK), 0, st,
                        c->dlist.as<u32>(), c->gexcl.as<u32>() + G, rows, c->goff.as<u64>(), c->gcap.as<u32>(),
-                       dwords, c->dbits.as<u32>());
+                       dwords, c->dbits_p);
     tend(c, RDF_T_LIGHT);
     c->dense_on = true;
     c->dwords = dwords;
     v.gdrow = c->gdrow.as<u32>();
-    v.dbits = c->dbits.as<u32>();
+    v.dbits = c->dbits_p;
     v.dwords = dwords;
     return RDF_OK;
 }
