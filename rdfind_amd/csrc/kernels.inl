@@ -2172,6 +2172,35 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         { u32 x = gszv[0] + (u32)gbv[0]; asm volatile("" : : "v"(x)); }  // stats: the metadata loads have arrived
 #endif
         LSTAT_TOC(1);
+        // Few candidates left (a dependent with a small pivot and many groups: c2's multi-segment items, 28 % of the
+        // light cycles): one candidate at a time, each lane searching all LIGHT_IT of its groups at once, so a level of
+        // the LIGHT_IT windows' searches is one round trip instead of one per window.  Off (RDF_LIGHT_FEW 0): measured
+        // no faster on c2 and slower on c3 / c4 than the windows' own paths (LDS-staged rows, serial groups)
+        if (LIGHT_FEW && __popcll(alive) <= LIGHT_FEW) {
+            if (nseg > 1 && s0 != b)
+                alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8 - ob], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u64 todo = alive;
+            while (todo) {
+                const int l = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const u32 key = __shfl(cand, l, RDF_WAVE);
+                const u32* ga[LIGHT_IT];
+                u64 gn[LIGHT_IT];
+#pragma unroll
+                for (int it = 0; it < LIGHT_IT; ++it) {
+                    ga[it] = v.gcap + gbv[it];
+                    gn[it] = gg[it] != NONE32 && !gdr[it] ? gszv[it] : 0;
+                }
+                bool f[LIGHT_IT];
+                multi_search<LIGHT_IT>(ga, gn, key, f);
+                bool ok = true;
+#pragma unroll
+                for (int it = 0; it < LIGHT_IT; ++it)
+                    ok = ok && (gg[it] == NONE32 || (gdr[it] ? dense_has(gdr[it], key) : f[it]));
+                if (!__all(ok)) alive &= ~(1ull << l);
+            }
+            continue;
+        }
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it) {
             if (s0 + (u64)it * RDF_WAVE >= e) break;
