@@ -51,6 +51,10 @@ static constexpr u32 LIGHT_PACK_NL = RDF_PACK_NL;        // which at most this m
 #define RDF_LIGHT_BATCH 4  // 8 before round 5: c2 light 2.52 -> 2.21 ms, c3 at 0.5 7.33 -> 7.12, c4 at 0.4 64.2 -> 60.1 (profiles/r05_light_ab_batch.log)
 #endif
 static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched together in k_light
+#ifndef RDF_LIGHT_ORDER_MIN
+#define RDF_LIGHT_ORDER_MIN 128
+#endif
+static constexpr u64 LIGHT_ORDER_MIN = RDF_LIGHT_ORDER_MIN;  // light-group entries from which a dependent's items go first
 #ifndef RDF_LIGHT_FEW
 #define RDF_LIGHT_FEW 0  // 2: c2 2.22 -> 2.22 ms, c3 17.0 -> 18.1, c4 at 0.4 60.2 -> 61.9 (profiles/r05_light_few_ab.log)
 #endif

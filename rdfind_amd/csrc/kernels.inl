@@ -2079,12 +2079,13 @@ template <bool STAGE>
 __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict__ pivot,
                                     const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
                                     const u64* __restrict__ choff, u64 w0, u64 W, u64 ob, u64* dead, u64* slots,
-                                    u32* counts) {
+                                    u32* counts, const u32* __restrict__ order) {
     // a staged group, or (STAGE) the lanes' small-group rows.  The larger buffer is only allocated by the variant
     // that uses it: on c3 (large light groups) 31.7 KB per block cost 30 % of the kernel even with the path unused
     __shared__ u32 s_light[RDF_WAVES_PER_BLOCK][STAGE ? LIGHT_BUF : LIGHT_LDS];
-    const u64 wl = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (wl >= W) return;
+    const u64 wq = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    if (wq >= W) return;
+    const u64 wl = order ? order[wq] : wq;  // the long items first (k_light_order), so none starts last
     const u64 w = w0 + wl;  // work items [w0, w0 + W); octets relative to ob (paged runs)
     const int lane = lane_id();
     const u32 d = item_dep[w];
@@ -2366,20 +2367,37 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
 #define RDF_LIGHT_ARGS                                                                                                     \
     u64 nvblk, CindView v, const u32 *__restrict__ pivot, const u64 *__restrict__ itemoff,                               \
         const u32 *__restrict__ item_dep, const u64 *__restrict__ choff, u64 w0, u64 W, u64 ob, u64 *dead, u64 *slots,  \
-        u32 *counts
+        u32 *counts, const u32 *__restrict__ order
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_STAGE_ATTR void k_light_stage(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<true>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
+        k_light_body<true>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_PLAIN_ATTR void k_light_plain(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
+        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
+// Work items in issue order, the items of dependents with >= thr light-group entries (many windows: c2's 6 % of
+// items that hold 45 % of the cycles) first: blocks are dispatched in index order, and a 10^6-cycle item issued near
+// the end set the kernel's tail.  flags -> excl (exclusive scan) -> order (a stable two-way partition).
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_long_flags(const u32* __restrict__ item_dep, const u64* __restrict__ doff,
+                                                                u64 w0, u64 W, u64 thr, u32* flags) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < W; i += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 d = item_dep[w0 + i];
+        flags[i] = doff[d + 1] - doff[d] >= thr ? 1u : 0u;
+    }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_light_order(const u32* __restrict__ flags, const u32* __restrict__ excl, u64 W,
+                                                           u32* order) {
+    const u32 nlong = excl[W];
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < W; i += (u64)gridDim.x * RDF_BLOCK)
+        order[flags[i] ? excl[i] : nlong + (u32)i - excl[i]] = (u32)i;
+}
+
 // the plain variant at 6 waves per SIMD (84 VGPRs, some spills): inputs whose light groups are very large (c4: the
 // searches and sweeps are latency-bound, more waves hide more of it), chosen by LIGHT_HIOCC_AVG
 __global__ __launch_bounds__(RDF_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_light_plain_hi(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts);
+        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 
 
