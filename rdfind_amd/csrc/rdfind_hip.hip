@@ -120,6 +120,8 @@ struct rdf_ctx {
     DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
     u32* dbits_p = nullptr;      // the bitmaps in use: dbits, or the idle kept store (rstore_lent)
     DevBuf iflag, iexcl, iorder; // k_light's issue order (k_light_long_flags / k_light_order)
+    hipStream_t side = nullptr;  // k_light_packed beside k_light (their slots are disjoint), joined before the compaction
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool rstore_lent = false;    // rstore holds the discovery's dense bitmaps (not reclaimable) until the next build
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
@@ -501,6 +503,9 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (const char* rk = getenv("RDFIND_RANGE_KEEP")) c->range_keep = atoi(rk) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hread, 16 * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent);
@@ -519,6 +524,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     for (DevBuf* b : ctx_buffers(c)) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -527,6 +533,9 @@ void rdf_ctx_destroy(rdf_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->tev)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2540,10 +2549,19 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
     const bool pivx_packed = pxp ? atoi(pxp) != 0 : !c->light_stage && c->light_wmean >= PIVX_WMEAN;
     vp.npx = pivx_packed && c->pivx_kept ? 1 : 0;
     if (!vp.npx) vp.pivx = nullptr;
+    // the packed dependents on the side stream, beside k_light (disjoint output octets): their blocks fill the SIMDs
+    // k_light's long items leave idle (RDFIND_LIGHT_SIDE=0: one stream)
+    static const bool side_ok = !(getenv("RDFIND_LIGHT_SIDE") && atoi(getenv("RDFIND_LIGHT_SIDE")) == 0);
+    const bool side = side_ok && WP && WI;
+    if (side) {
+        HIP_TRY(c, hipEventRecord(c->ev_fork, st));
+        HIP_TRY(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    }
     if (WP)
-        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, st, (u64)thread_blocks(WP * 8), vp,
-                           pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP, c->choffl.as<u64>(), ob,
-                           slots.as<u64>(), counts.as<u32>());
+        hipLaunchKernelGGL(k_light_packed, dim3(vgrid(thread_blocks(WP * 8))), dim3(RDF_BLOCK), 0, side ? c->side : st,
+                           (u64)thread_blocks(WP * 8), vp, pivot, c->pkoff.as<u64>(), c->pk_dep.as<u32>(), r.q0, WP,
+                           c->choffl.as<u64>(), ob, slots.as<u64>(), counts.as<u32>());
+    if (side) HIP_TRY(c, hipEventRecord(c->ev_join, c->side));
     if (WI) {
         auto kl = c->light_stage ? k_light_stage : c->light_hiocc ? k_light_plain_hi : k_light_plain;
         CindView vl = v;
@@ -2569,6 +2587,7 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
                            0, st, (u64)wave_blocks(WI), vl, pivot, c->itoffl.as<u64>(), c->item_dep.as<u32>(), c->choffl.as<u64>(),
                            r.i0, WI, ob, c->dead.as<u64>(), slots.as<u64>(), counts.as<u32>(), order);
     }
+    if (side) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_join, 0));
     if (WM)
         hipLaunchKernelGGL(k_light_mseg_emit, dim3(vgrid(wave_blocks(WM))),
                            dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WM), v, pivot, c->mchoff.as<u64>(), c->mch_dep.as<u32>(), r.m0,
