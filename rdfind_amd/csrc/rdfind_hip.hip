@@ -2568,7 +2568,9 @@ static rdf_status d_light_kernels(rdf_ctx* c, const CindView& v, const u32* pivo
         vl.npx = c->light_npx;
         // issue order: the items of dependents with many light-group entries first (RDFIND_LIGHT_ORDER=<entries>, 0: off).
         // By default for the staging variant only: c2 light 2.22 -> 2.03 ms, while the plain variant's inputs lose a
-        // little (c3 17.0 -> 17.2, c4 at 0.4 60.4 -> 61.1; profiles/r05_light_order_ab.log)
+        // little (c3 17.0 -> 17.2, c4 at 0.4 60.4 -> 61.1; profiles/r05_light_order_ab.log).  The partition is stable:
+        // an octave-class order whose slots came from atomics measured 2.23 ms on c2 (consecutive items of one
+        // dependent share its groups in L2; profiles/r05_light_order_classes_ab.log)
         static const char* oenv = getenv("RDFIND_LIGHT_ORDER");
         const u64 order_thr = oenv ? strtoull(oenv, nullptr, 10) : c->light_stage ? LIGHT_ORDER_MIN : 0;
         const u32* order = nullptr;
