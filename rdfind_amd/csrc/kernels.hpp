@@ -55,10 +55,18 @@ static constexpr int LIGHT_BATCH = RDF_LIGHT_BATCH;  // candidates searched toge
 #define RDF_LIGHT_ORDER_MIN 128
 #endif
 static constexpr u64 LIGHT_ORDER_MIN = RDF_LIGHT_ORDER_MIN;  // light-group entries from which a dependent's items go first
+#ifndef RDF_LIGHT_DENSE_BATCH
+#define RDF_LIGHT_DENSE_BATCH 8
+#endif
+static constexpr int LIGHT_DENSE_BATCH = RDF_LIGHT_DENSE_BATCH;  // dense groups' bitmap words in flight per lane (k_light)
 #ifndef RDF_LIGHT_FEW
 #define RDF_LIGHT_FEW 0  // 2: c2 2.22 -> 2.22 ms, c3 17.0 -> 18.1, c4 at 0.4 60.2 -> 61.9 (profiles/r05_light_few_ab.log)
 #endif
 static constexpr int LIGHT_FEW = RDF_LIGHT_FEW;  // alive candidates up to which k_light searches LIGHT_IT windows at once
+#ifndef RDF_LIGHT_FEW_GROUPS
+#define RDF_LIGHT_FEW_GROUPS 1024
+#endif
+static constexpr u64 LIGHT_FEW_GROUPS = RDF_LIGHT_FEW_GROUPS;  // ... in segments of at least this many group entries
 #ifndef RDF_LIGHT_SERIAL
 #define RDF_LIGHT_SERIAL 4
 #endif

@@ -1886,9 +1886,12 @@ __device__ inline void k_light_packed_body(u64 vblk, CindView v, const u32* __re
             ga[i] = v.gcap + gb;
         }
         bool f[PACK_STEP];
+        u32 dw[PACK_STEP];  // the dense groups' bitmap words, loaded together (not behind each other's test)
+#pragma unroll
+        for (int i = 0; i < PACK_STEP; ++i) dw[i] = dr[i] ? dr[i][cand >> 5] : ~0u;
         multi_search<PACK_STEP>(ga, gn, cand, f);
 #pragma unroll
-        for (int i = 0; i < PACK_STEP; ++i) ok = ok && (dr[i] ? dense_has(dr[i], cand) : (gn[i] == 0 || f[i]));
+        for (int i = 0; i < PACK_STEP; ++i) ok = ok && (dr[i] ? ((dw[i] >> (cand & 31)) & 1u) != 0 : (gn[i] == 0 || f[i]));
     }
     const u64 alive = __ballot(ok);
     const int lane = lane_id(), o = lane >> 3, jj = lane & 7;
@@ -2177,7 +2180,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         // light cycles): one candidate at a time, each lane searching all LIGHT_IT of its groups at once, so a level of
         // the LIGHT_IT windows' searches is one round trip instead of one per window.  Off (RDF_LIGHT_FEW 0): measured
         // no faster on c2 and slower on c3 / c4 than the windows' own paths (LDS-staged rows, serial groups)
-        if (LIGHT_FEW && __popcll(alive) <= LIGHT_FEW) {
+        if (LIGHT_FEW && e - b >= LIGHT_FEW_GROUPS && __popcll(alive) <= LIGHT_FEW) {
             if (nseg > 1 && s0 != b)
                 alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8 - ob], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             u64 todo = alive;
@@ -2216,21 +2219,24 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
             if (dm && __popcll(alive) >= LIGHT_DENSE_SER) {
                 // many candidates alive: the dense groups one at a time with the lanes over the candidates.  The
                 // candidates are ascending pivot members, so a group's 64 tests hit a few lines of its bitmap row
-                // (lanes over groups would touch 64 rows per candidate).  Four groups' loads in flight.
+                // (lanes over groups would touch 64 rows per candidate).  LIGHT_DENSE_BATCH groups' bitmap words are
+                // loaded unconditionally before any is tested, so they are in flight together (a short-circuit test
+                // per group would make each load wait for the previous one's result)
                 u64 t = dm;
                 while (t && alive) {
-                    const u32* dr[4];
+                    const bool mine = (alive >> lane) & 1ull;
+                    u32 wv[LIGHT_DENSE_BATCH];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
+                    for (int k = 0; k < LIGHT_DENSE_BATCH; ++k) {
                         const int l = t ? __ffsll((long long)t) - 1 : -1;
                         t &= t - 1;
-                        dr[k] = l < 0 ? nullptr : (const u32*)__shfl((unsigned long long)gdr[it], l, RDF_WAVE);
+                        const u32* dr = l < 0 ? nullptr : (const u32*)__shfl((unsigned long long)gdr[it], l, RDF_WAVE);
+                        wv[k] = mine && dr ? dr[cand >> 5] : ~0u;
                     }
-                    const bool mine = (alive >> lane) & 1ull;
-                    bool f = true;
+                    u32 all = ~0u;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) f = f && (!mine || !dr[k] || dense_has(dr[k], cand));
-                    alive &= __ballot(f);
+                    for (int k = 0; k < LIGHT_DENSE_BATCH; ++k) all &= wv[k];
+                    alive &= __ballot(!mine || ((all >> (cand & 31)) & 1u));
                 }
                 if (gdr[it]) g = NONE32;  // what is left: the sparse light groups of the window
                 lm = __ballot(g != NONE32);
