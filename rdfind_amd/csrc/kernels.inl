@@ -379,14 +379,34 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_bin_lookup_build(const u64* __res
     }
 }
 
-__device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u64 key) {
-    u64 h = mix64(key) & mask;
+__device__ inline u32 bin_lookup_from(const u64* lkeys, const u32* lvals, u64 mask, u64 key, u64 h) {
     for (;;) {
         u64 k = lkeys[h];
         if (k == key) return lvals[h];
         if (k == EMPTY64) return NONE32;
         h = (h + 1) & mask;
     }
+}
+__device__ inline u32 bin_lookup(const u64* lkeys, const u32* lvals, u64 mask, u64 key) {
+    return bin_lookup_from(lkeys, lvals, mask, key, mix64(key) & mask);
+}
+
+// a triple's (up to) three binary lookups together: the three first probes' key loads are issued at once, then the
+// hits' value loads at once; a probe that meets another key continues alone (rare: the table is at most half full).
+// One lookup after the other made K3 wait for up to six dependent round trips per triple.
+__device__ inline void bin_lookup3(const u64* __restrict__ lkeys, const u32* __restrict__ lvals, u64 mask,
+                                   const u64 (&key)[3], const bool (&need)[3], u32 (&out)[3]) {
+    u64 h[3], k[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        h[t] = mix64(key[t]) & mask;
+        k[t] = need[t] ? lkeys[h[t]] : EMPTY64;
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) out[t] = need[t] && k[t] == key[t] ? lvals[h[t]] : NONE32;
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+        if (need[t] && k[t] != key[t] && k[t] != EMPTY64) out[t] = bin_lookup_from(lkeys, lvals, mask, key[t], (h[t] + 1) & mask);
 }
 
 #include "ars.inl"
@@ -426,31 +446,35 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
         ro = frank[2ull * V + to];
     }
     const bool fs = rs != NONE32, fp = rp != NONE32, fo = ro != NONE32;
+    // the binary captures o[s,p], p[s,o], s[p,o]: their lookups in flight together (bin_lookup3)
+    const u64 bkey[3] = {bin_key(2, ts, tp), bin_key(1, ts, to), bin_key(0, tp, to)};
+    const bool bneed[3] = {jo && fs && fp, jp && fs && fo, js_ && fp && fo};
+    u32 bval[3];
+#ifndef RDF_K3_LOOKUP3  // 1: bin_lookup3 (measured slower: c4 at 0.4 emit 54.1 -> 57.8 ms, c3 8.44 -> 8.88; its registers
+#define RDF_K3_LOOKUP3 0   // cost the write pass an occupancy step; profiles/r05_k3_lookup3_ab.log)
+#endif
+    if (RDF_K3_LOOKUP3) {
+        bin_lookup3(lkeys, lvals, lmask, bkey, bneed, bval);
+    } else {  // one lookup after the other (A/B switch)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) bval[t] = bneed[t] ? bin_lookup(lkeys, lvals, lmask, bkey[t]) : NONE32;
+    }
     if (jo) {  // project objects: o[s] (t4), o[p] (t5), o[s,p]
         if (fs) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp + 1) << joinbits) | to; }
-        if (fs && fp) {
-            u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
-            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
-        }
+        if (bval[0] != NONE32) rec[c++] = (((u64)twoU + bval[0]) << joinbits) | to;
     }
     const u32 co = c;
     if (jp) {  // project predicates: p[s] (t2), p[o] (t3), p[s,o]
         if (fs) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
         if (fo) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
-        if (fs && fo) {
-            u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
-            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
-        }
+        if (bval[1] != NONE32) rec[c++] = (((u64)twoU + bval[1]) << joinbits) | tp;
     }
     if (grp) *grp = co | ((c - co) << 2);  // records joined on the object, on the predicate (the rest: the subject)
     if (js_) {  // project subjects: s[p] (t0), s[o] (t1), s[p,o]
         if (fp) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
         if (fo) rec[c++] = ((2ull * ro) << joinbits) | ts;
-        if (fp && fo) {
-            u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
-            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | ts;
-        }
+        if (bval[2] != NONE32) rec[c++] = (((u64)twoU + bval[2]) << joinbits) | ts;
     }
     if (rep) *rep = rp_mask;
     return c;
@@ -989,17 +1013,38 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_group_flags(const u64* __restrict
 }
 
 // groups: goff[g] = first record; gcap[i] = compact capture id; gmap[join] = g (fk = join << 32 | capture)
-__global__ __launch_bounds__(RDF_BLOCK) void k_group_build(const u64* __restrict__ fk, u64 n, const u32* __restrict__ gflag,
-                                                           const u32* __restrict__ gexcl, u64* goff, u32* gcap, u32* gmap) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 k = fk[i];
-        gcap[i] = (u32)(k & 0xffffffffu);
-        if (gflag[i]) {
-            const u32 g = gexcl[i];
-            goff[g] = i;
-            gmap[k >> 32] = g;
+// STREAM_U elements per thread with their loads in flight together (a one-element grid-stride loop keeps one load per
+// lane in flight and is latency-bound at ~2 TB/s)
+__device__ inline void group_build_body(const u64* __restrict__ fk, u64 n, const u32* __restrict__ gflag,
+                                        const u32* __restrict__ gexcl, u64 rbase, u32 gbase, u64* goff, u32* gcap,
+                                        u32* gmap) {
+    const u64 T = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 i0 = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i0 < n; i0 += T * STREAM_U) {
+        u64 k[STREAM_U];
+        u32 f[STREAM_U], x[STREAM_U];
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            k[u] = i < n ? fk[i] : 0ull;
+            f[u] = i < n ? gflag[i] : 0u;
+            x[u] = i < n ? gexcl[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < STREAM_U; ++u) {
+            const u64 i = i0 + (u64)u * T;
+            if (i >= n) break;
+            gcap[rbase + i] = (u32)(k[u] & 0xffffffffu);
+            if (f[u]) {
+                const u32 g = gbase + x[u];
+                goff[g] = rbase + i;
+                gmap[k[u] >> 32] = g;
+            }
         }
     }
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_group_build(const u64* __restrict__ fk, u64 n, const u32* __restrict__ gflag,
+                                                           const u32* __restrict__ gexcl, u64* goff, u32* gcap, u32* gmap) {
+    group_build_body(fk, n, gflag, gexcl, 0, 0u, goff, gcap, gmap);
 }
 
 // dependent -> groups: dgrp[i] = group of the join value of dk[i].  A capture's joins ascend and group ids
@@ -1091,15 +1136,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_range_block_counts(const u32* __r
 __global__ __launch_bounds__(RDF_BLOCK) void k_group_build_at(const u64* __restrict__ fk, u64 n, const u32* __restrict__ gflag,
                                                               const u32* __restrict__ gexcl, u64 rbase, u32 gbase, u64* goff,
                                                               u32* gcap, u32* gmap) {
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
-        const u64 k = fk[i];
-        gcap[rbase + i] = (u32)(k & 0xffffffffu);
-        if (gflag[i]) {
-            const u32 g = gbase + gexcl[i];
-            goff[g] = rbase + i;
-            gmap[k >> 32] = g;
-        }
-    }
+    group_build_body(fk, n, gflag, gexcl, rbase, gbase, goff, gcap, gmap);
 }
 
 // a range's dependent -> group entries: dk (compact capture << 32 | join, (capture, join) order) with this range's
@@ -1371,6 +1408,10 @@ __device__ inline void extra_pivots(u64 best, const u64 (&l)[NP], u32* pivx, u64
     }
 }
 
+#ifndef RDF_PIVOT_U
+#define RDF_PIVOT_U 4
+#endif
+static constexpr int PIVOT_U = RDF_PIVOT_U;  // group entries per lane whose loads are in flight together (pivot pass)
 template <int EX>
 __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp_tag, u64* best_out, u32* nlight_out,
                                                            u64* sig, u32* piv2, u32* pivx) {
@@ -1384,19 +1425,28 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_pivot_short(CindView v, u32* dgrp
         for (int k = 0; k < NPIV; ++k) l[k] = ~0ull;
         u32 nlight = 0;
         u64 sg[SIG_W] = {};
-        for (u64 j = b; j < e; ++j) {
-            const u32 raw = v.dgrp[j], g = raw & ~DGRP_HEAVY;
-            const u32 gi = v.ginfo[g];
-            const u64 key = ((u64)(gi & ~GINFO_HEAVY) << 32) | g;
-            best = key < best ? key : best;
-            const bool light = !(gi & GINFO_HEAVY);
-            nlight += light;
-            if (light) {
-                sig_add(sg, g);
-                smallest_k(l, key);
+        for (u64 j0 = b; j0 < e; j0 += PIVOT_U) {  // PIVOT_U entries' loads, then their gathers, in flight together
+            u32 raw[PIVOT_U], gi[PIVOT_U];
+#pragma unroll
+            for (int u = 0; u < PIVOT_U; ++u) raw[u] = j0 + u < e ? v.dgrp[j0 + u] : 0u;
+#pragma unroll
+            for (int u = 0; u < PIVOT_U; ++u) gi[u] = j0 + u < e ? v.ginfo[raw[u] & ~DGRP_HEAVY] : 0u;
+#pragma unroll
+            for (int u = 0; u < PIVOT_U; ++u) {
+                const u64 j = j0 + u;
+                if (j >= e) break;
+                const u32 g = raw[u] & ~DGRP_HEAVY;
+                const u64 key = ((u64)(gi[u] & ~GINFO_HEAVY) << 32) | g;
+                best = key < best ? key : best;
+                const bool light = !(gi[u] & GINFO_HEAVY);
+                nlight += light;
+                if (light) {
+                    sig_add(sg, g);
+                    smallest_k(l, key);
+                }
+                const u32 tagged = light ? g : (g | DGRP_HEAVY);
+                if (tagged != raw[u]) dgrp_tag[j] = tagged;  // in place: light entries stay as they are (no rewrite)
             }
-            const u32 tagged = light ? g : (g | DGRP_HEAVY);
-            if (tagged != raw) dgrp_tag[j] = tagged;  // in place: light entries stay as they are (no rewrite)
         }
         best_out[d] = best;
         nlight_out[d] = nlight;
@@ -1425,19 +1475,32 @@ __device__ inline void k_pivot_seg_body(u64 vblk, CindView v, u32* dgrp_tag, con
     for (int k = 0; k < NPIV; ++k) l[k] = ~0ull;
     u32 nlight = 0;
     u64 sg[SIG_W] = {};
-    for (u64 j = b + lane; j < e; j += RDF_WAVE) {
-        const u32 raw = v.dgrp[j], g = raw & ~DGRP_HEAVY;
-        const u32 gi = v.ginfo[g];
-        const u64 key = ((u64)(gi & ~GINFO_HEAVY) << 32) | g;
-        best = key < best ? key : best;
-        const bool light = !(gi & GINFO_HEAVY);
-        nlight += light;
-        if (light) {
-            sig_add(sg, g);
-            smallest_k(l, key);
+    // PIVOT_U entries per lane at a time: their dgrp loads, then their ginfo gathers, each batch in flight together
+    for (u64 j0 = b + lane; j0 < e; j0 += (u64)RDF_WAVE * PIVOT_U) {
+        u32 raw[PIVOT_U], gi[PIVOT_U];
+#pragma unroll
+        for (int u = 0; u < PIVOT_U; ++u) {
+            const u64 j = j0 + (u64)u * RDF_WAVE;
+            raw[u] = j < e ? v.dgrp[j] : 0u;
         }
-        const u32 tagged = light ? g : (g | DGRP_HEAVY);
-        if (tagged != raw) dgrp_tag[j] = tagged;
+#pragma unroll
+        for (int u = 0; u < PIVOT_U; ++u) gi[u] = j0 + (u64)u * RDF_WAVE < e ? v.ginfo[raw[u] & ~DGRP_HEAVY] : 0u;
+#pragma unroll
+        for (int u = 0; u < PIVOT_U; ++u) {
+            const u64 j = j0 + (u64)u * RDF_WAVE;
+            if (j >= e) break;
+            const u32 g = raw[u] & ~DGRP_HEAVY;
+            const u64 key = ((u64)(gi[u] & ~GINFO_HEAVY) << 32) | g;
+            best = key < best ? key : best;
+            const bool light = !(gi[u] & GINFO_HEAVY);
+            nlight += light;
+            if (light) {
+                sig_add(sg, g);
+                smallest_k(l, key);
+            }
+            const u32 tagged = light ? g : (g | DGRP_HEAVY);
+            if (tagged != raw[u]) dgrp_tag[j] = tagged;
+        }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
