@@ -23,7 +23,7 @@ kernel family from HIP events recorded on the library's stream; `cpu_baseline` t
 split over the same N GPUs (strong scaling, the north-star scaling config), after the main leg: each rank draws only
 its 1/N of the rows, a rank whose join shard holds >= 2^32/9 triples builds its groups in join ranges, and the step is
 the same T_disc with every rank's result handed over.  It reports ms per step, triples/s, the ranks' work balance
-(max / mean) and the one-GPU c4 step of round 5 (0.881 s; round 4: 1.616 s) as its reference; `value` stays the c2 leg's.
+(max / mean) and the one-GPU c4 step of round 5 (0.852 s; round 4: 1.616 s) as its reference; `value` stays the c2 leg's.
 """
 from __future__ import annotations
 
@@ -218,9 +218,9 @@ def per_rank_balance(dist, world, mine):
                               for k in mine if all(isinstance(r.get(k), (int, float)) for r in allr)}}
 
 
-# the one-GPU c4 step this leg is compared with: round 5 (kept join ranges, K2 radix path), profiles/r05_cfg_c4_1.0.json
-# (round 4: 1616 ms)
-C4_ONE_GPU_MS = 881.0
+# the one-GPU c4 step this leg is compared with: round 5 (kept join ranges, K2 radix path, light load chains), the
+# c4_strong leg of profiles/r05_bench_c2.json (round 4: 1616 ms)
+C4_ONE_GPU_MS = 852.0
 
 
 def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):

@@ -59,6 +59,10 @@ static constexpr u64 LIGHT_ORDER_MIN = RDF_LIGHT_ORDER_MIN;  // light-group entr
 #define RDF_LIGHT_DENSE_BATCH 8
 #endif
 static constexpr int LIGHT_DENSE_BATCH = RDF_LIGHT_DENSE_BATCH;  // dense groups' bitmap words in flight per lane (k_light)
+#ifndef RDF_LIGHT_P2X
+#define RDF_LIGHT_P2X 0
+#endif
+static constexpr int LIGHT_P2X = RDF_LIGHT_P2X;  // second and first extra pivot searched together (plain variant)
 #ifndef RDF_LIGHT_FEW
 #define RDF_LIGHT_FEW 0  // 2: c2 2.22 -> 2.22 ms, c3 17.0 -> 18.1, c4 at 0.4 60.2 -> 61.9 (profiles/r05_light_few_ab.log)
 #endif

@@ -2183,7 +2183,31 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // second pivot is not verified here; its survivors go out tagged (item seg 0) and pass B verifies them compacted
     const bool multi = v.prefilter && itemoff[d + 1] - itemoff[d] > nseg;
     LSTAT_TIC();
-    if (p2 != NONE32 && alive && !v.p2done) {
+    int k_px = 0;  // extra pivots already checked
+    // RDF_LIGHT_P2X: the second pivot and the first extra pivot searched at once (two chains per lane) when both are
+    // groups the lanes search in global memory (dense rows or > LIGHT_LDS members), instead of one after the other
+    bool p2_done_here = false;
+    if (LIGHT_P2X && pxs && p2 != NONE32 && alive && !v.p2done) {
+        const u32 pk0 = pxs[0];
+        if (pk0 != NONE32) {
+            const u64 gb2 = v.goff[p2], ge2 = v.goff[p2 + 1], gb3 = v.goff[pk0], ge3 = v.goff[pk0 + 1];
+            const u32 *d2 = dense_row(v, p2), *d3 = dense_row(v, pk0);
+            if ((d2 || ge2 - gb2 > LIGHT_LDS) && (d3 || ge3 - gb3 > LIGHT_LDS)) {
+                const bool mine = (alive >> lane) & 1ull;
+                const u32* ga[2] = {v.gcap + gb2, v.gcap + gb3};
+                const u64 gn[2] = {mine && !d2 ? ge2 - gb2 : 0, mine && !d3 ? ge3 - gb3 : 0};
+                const u32 w2 = mine && d2 ? d2[cand >> 5] : ~0u, w3 = mine && d3 ? d3[cand >> 5] : ~0u;
+                bool f[2];
+                multi_search<2>(ga, gn, cand, f);
+                const bool ok = !mine || ((d2 ? ((w2 >> (cand & 31)) & 1u) != 0 : f[0]) &&
+                                          (d3 ? ((w3 >> (cand & 31)) & 1u) != 0 : f[1]));
+                alive &= __ballot(ok);
+                p2_done_here = true;
+                k_px = 1;
+            }
+        }
+    }
+    if (!p2_done_here && p2 != NONE32 && alive && !v.p2done) {
         const u64 gb2 = v.goff[p2];
         alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
                             dense_row(v, p2));
@@ -2192,7 +2216,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // window's searches (c3: half of the light cycles), one targeted check each (lanes over candidates) before it
     if (pxs && !v.p2done) {
 #pragma unroll 1
-        for (int k = 0; k < v.npx && alive; ++k) {
+        for (int k = k_px; k < v.npx && alive; ++k) {
             const u32 pk = pxs[k];
             if (pk == NONE32) break;  // ascending: no more light groups
             const u64 gb3 = v.goff[pk];
