@@ -60,7 +60,7 @@ static constexpr u64 LIGHT_ORDER_MIN = RDF_LIGHT_ORDER_MIN;  // light-group entr
 #endif
 static constexpr int LIGHT_DENSE_BATCH = RDF_LIGHT_DENSE_BATCH;  // dense groups' bitmap words in flight per lane (k_light)
 #ifndef RDF_LIGHT_P2X
-#define RDF_LIGHT_P2X 0
+#define RDF_LIGHT_P2X 0  // 1: c3 15.75 -> 16.05 ms, c4 at 0.4 49.6 -> 50.0 (profiles/r05_light_p2x_ab.log)
 #endif
 static constexpr int LIGHT_P2X = RDF_LIGHT_P2X;  // second and first extra pivot searched together (plain variant)
 #ifndef RDF_LIGHT_FEW
