@@ -146,7 +146,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* in, TO* out,
     if (threadIdx.x == 0 && grand_total) *grand_total = carry;
 }
 
-static constexpr u64 SCAN_SMALL_TILES = 4;
+static constexpr u64 SCAN_SMALL_TILES = 4;  // one 1024-thread block up to 8 or 32 tiles measured no faster (c1 groups 0.23 -> 0.39 ms at 32;
+                                           // profiles/r05_scan_small_ab.log)
 
 // Single-pass exclusive scan (chained, decoupled look-back): one launch reads the input once.  Tiles take their ids
 // from a counter in launch order, publish their aggregate at once, then wave 0 looks back over the 64 nearest
