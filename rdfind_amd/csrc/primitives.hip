@@ -307,6 +307,19 @@ static constexpr int RS_TILE = RDF_BLOCK * RS_ITEMS;             // 4096 keys pe
 static constexpr int RS_WAVE_KEYS = RDF_WAVE * RS_ITEMS;         // 1024 keys per wave
 
 
+// Tile of a radix block.  RDF_RS_XCD=1: consecutive tiles on one XCD (blocks are dealt round-robin over the 8 XCDs,
+// MI355X_MICROARCH.md "Workgroup dispatch"): tile t's digit runs end where tile t+1's begin (a 4096-key tile averages
+// 8 keys = 64 B per digit at 9 bits), and the (digit, tile) histogram words of neighbouring tiles share lines, so
+// partial lines written by neighbours meet in one L2 instead of leaving eight L2s separately
+#ifndef RDF_RS_XCD
+#define RDF_RS_XCD 1
+#endif
+__device__ inline u32 rs_tile() {
+    if (!RDF_RS_XCD) return blockIdx.x;
+    const u32 b = blockIdx.x, n = gridDim.x, x = b % 8u, q = n / 8u, r = n % 8u;
+    return x * q + (x < r ? x : r) + b / 8u;  // XCD x holds tiles [x q + min(x, r), + q + (x < r))
+}
+
 // lanes of the wave whose key is valid and has the same DB-bit digit as this lane (0 for invalid lanes)
 template <int DB>
 __device__ inline u64 digit_peers(u32 d, bool valid) {
@@ -356,7 +369,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
     const u32 dmask = (1u << w) - 1u;
     for (u32 i = threadIdx.x; i < RDF_WAVES_PER_BLOCK * NBIN; i += RDF_BLOCK) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const u64 tbase = (u64)blockIdx.x * RS_TILE;
+    const u32 tile = rs_tile();
+    const u64 tbase = (u64)tile * RS_TILE;
     u64 k[RS_ITEMS];
     load_tile_pairs(keys, n, tbase, k);  // counting is order-free: any assignment of keys to lanes works
 #pragma unroll
@@ -372,7 +386,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
         u32 sum = 0;
 #pragma unroll
         for (int ww = 0; ww < RDF_WAVES_PER_BLOCK; ++ww) sum += wcnt[ww][b];
-        hist[(u64)b * num_tiles + blockIdx.x] = sum;
+        hist[(u64)b * num_tiles + tile] = sum;
     }
 }
 
@@ -393,8 +407,9 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     const int wave = threadIdx.x / RDF_WAVE;
     const u32 nbin = 1u << w, dmask = nbin - 1u;
     for (u32 i = threadIdx.x; i < RDF_WAVES_PER_BLOCK * NBIN; i += RDF_BLOCK) (&wcount[0][0])[i] = 0;
-    for (u32 b = threadIdx.x; b < nbin; b += RDF_BLOCK) gbase[b] = offs[(u64)b * num_tiles + blockIdx.x];
-    const u64 tbase = (u64)blockIdx.x * RS_TILE;
+    const u32 tile = rs_tile();
+    for (u32 b = threadIdx.x; b < nbin; b += RDF_BLOCK) gbase[b] = offs[(u64)b * num_tiles + tile];
+    const u64 tbase = (u64)tile * RS_TILE;
     const u64 tn = n - tbase < (u64)RS_TILE ? n - tbase : (u64)RS_TILE;
     {   // stage the tile through LDS: 16-byte global loads, then each wave reads its contiguous sub-range
         u64 kin[RS_ITEMS];
