@@ -89,6 +89,15 @@ __device__ inline u32 hash32(u32 x) {
 __device__ inline int lane_id() { return (int)(threadIdx.x & (RDF_WAVE - 1)); }
 __device__ inline u64 lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// blockIdx.x renumbered so that consecutive numbers share an XCD (blocks are dealt round-robin over the 8 XCDs,
+// MI355X_MICROARCH.md "Workgroup dispatch"): XCD x runs numbers [x q + min(x, r), + q + (x < r)), q = n / 8, r = n % 8.
+// For kernels whose neighbouring blocks write neighbouring bytes (per-(bin, block) runs of a partition pass, their
+// histogram columns): the partial lines the neighbours share meet in one L2.
+__device__ inline u32 xcd_block() {
+    const u32 b = blockIdx.x, n = gridDim.x, x = b % 8u, q = n / 8u, r = n % 8u;
+    return x * q + (x < r ? x : r) + b / 8u;
+}
+
 // Wave-wide inclusive scan (u32) with DPP-free shuffles.
 __device__ inline u32 wave_inclusive_scan(u32 v) {
     const int lane = lane_id();

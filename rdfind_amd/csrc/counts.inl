@@ -81,16 +81,22 @@ __device__ inline u32 bucket_slot(u32* lh, u32 bk, bool active) {
 #define RDF_PART_U 4
 #endif
 static constexpr int PART_U = RDF_PART_U;  // triples per thread whose loads are in flight together (partition passes)
+// RDF_PART_XCD=1: the K1/K2 partition passes number their blocks with xcd_block (a block's run per bucket is a few
+// records: neighbouring blocks' runs share lines)
+#ifndef RDF_PART_XCD
+#define RDF_PART_XCD 1
+#endif
+__device__ inline u32 part_block() { return RDF_PART_XCD ? xcd_block() : blockIdx.x; }
 
 template <bool SCATTER>
 __global__ __launch_bounds__(RDF_BLOCK) void k_u2_part(const u32* __restrict__ s, const u32* __restrict__ p,
                                                        const u32* __restrict__ o, u64 n, u32 V, u32 NB, int bits,
                                                        u32* ghist, uint16_t* __restrict__ recs) {
     extern __shared__ u32 lh[];
-    for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
+    for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + part_block()] : 0u;
     __syncthreads();
     const u64 per = (n + gridDim.x - 1) / gridDim.x;
-    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    const u64 b = (u64)part_block() * per, e = b + per < n ? b + per : n;
     const u64 lmask = (1ull << bits) - 1;
     // PART_U rows per thread loaded before any is used: the chunk is read with PART_U x 3 loads in flight per lane
     // instead of one round trip per 256 rows (the slot reservations below are LDS work)
@@ -116,7 +122,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_u2_part(const u32* __restrict__ s
     }
     if (!SCATTER) {
         __syncthreads();
-        for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
+        for (u32 i = threadIdx.x; i < NB; i += RDF_BLOCK) ghist[(u64)i * gridDim.x + part_block()] = lh[i];
     }
 }
 
@@ -334,10 +340,10 @@ __global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s
                                                        int bits, u32* ghist, u64* __restrict__ rkeys) {
     extern __shared__ u32 lh[];
     const u32 NB = 1u << bits;
-    for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + blockIdx.x] : 0u;
+    for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) lh[i] = SCATTER ? ghist[(u64)i * gridDim.x + part_block()] : 0u;
     __syncthreads();
     const u64 per = (n + gridDim.x - 1) / gridDim.x;
-    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
+    const u64 b = (u64)part_block() * per, e = b + per < n ? b + per : n;
     // PART_U rows per thread: their triple loads, then their frequency-bit loads, each batch in flight together
     for (u64 i0 = b; i0 < e; i0 += (u64)B2_PBLOCK * PART_U) {
         u32 ts[PART_U], tp[PART_U], to[PART_U];
@@ -371,7 +377,7 @@ __global__ __launch_bounds__(B2_PBLOCK) void k_b2_part(const u32* __restrict__ s
     }
     if (!SCATTER) {
         __syncthreads();
-        for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) ghist[(u64)i * gridDim.x + blockIdx.x] = lh[i];
+        for (u32 i = threadIdx.x; i < NB; i += B2_PBLOCK) ghist[(u64)i * gridDim.x + part_block()] = lh[i];
     }
 }
 

@@ -307,18 +307,13 @@ static constexpr int RS_TILE = RDF_BLOCK * RS_ITEMS;             // 4096 keys pe
 static constexpr int RS_WAVE_KEYS = RDF_WAVE * RS_ITEMS;         // 1024 keys per wave
 
 
-// Tile of a radix block.  RDF_RS_XCD=1: consecutive tiles on one XCD (blocks are dealt round-robin over the 8 XCDs,
-// MI355X_MICROARCH.md "Workgroup dispatch"): tile t's digit runs end where tile t+1's begin (a 4096-key tile averages
-// 8 keys = 64 B per digit at 9 bits), and the (digit, tile) histogram words of neighbouring tiles share lines, so
-// partial lines written by neighbours meet in one L2 instead of leaving eight L2s separately
+// Tile of a radix block.  RDF_RS_XCD=1: consecutive tiles on one XCD (xcd_block): tile t's digit runs end where tile
+// t+1's begin (a 4096-key tile averages 8 keys = 64 B per digit at 9 bits), and the (digit, tile) histogram words of
+// neighbouring tiles share lines (c2 sort 1.90 -> 1.78 ms, c3 19.1 -> 17.4; profiles/r05_rs_xcd_ab.log)
 #ifndef RDF_RS_XCD
 #define RDF_RS_XCD 1
 #endif
-__device__ inline u32 rs_tile() {
-    if (!RDF_RS_XCD) return blockIdx.x;
-    const u32 b = blockIdx.x, n = gridDim.x, x = b % 8u, q = n / 8u, r = n % 8u;
-    return x * q + (x < r ? x : r) + b / 8u;  // XCD x holds tiles [x q + min(x, r), + q + (x < r))
-}
+__device__ inline u32 rs_tile() { return RDF_RS_XCD ? xcd_block() : blockIdx.x; }
 
 // lanes of the wave whose key is valid and has the same DB-bit digit as this lane (0 for invalid lanes)
 template <int DB>
