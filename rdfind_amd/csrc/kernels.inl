@@ -2461,13 +2461,27 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     u64 nvblk, CindView v, const u32 *__restrict__ pivot, const u64 *__restrict__ itemoff,                               \
         const u32 *__restrict__ item_dep, const u64 *__restrict__ choff, u64 w0, u64 W, u64 ob, u64 *dead, u64 *slots,  \
         u32 *counts, const u32 *__restrict__ order
+// RDF_LIGHT_XCD = K: runs of K consecutive virtual blocks (4 K consecutive work items in issue order) on one XCD
+// (virtual block vb runs on XCD vb % 8: the grid is all virtual blocks, or 2^20), so the items of one dependent,
+// which read the same group entries, meet in one L2; the runs keep the issue order at 8 K blocks.  0: off (K = 8 / 32
+// measured slower: c2 light 2.02 -> 2.07 / 2.08 ms, c3 and c4 unchanged; profiles/r05_light_xcd_ab.log)
+#ifndef RDF_LIGHT_XCD
+#define RDF_LIGHT_XCD 0
+#endif
+__device__ inline u64 light_vb(u64 vb, u64 nv) {
+    if (!RDF_LIGHT_XCD) return vb;
+    constexpr u64 K = RDF_LIGHT_XCD, C = 8 * K;
+    const u64 c = vb / C;
+    if ((c + 1) * C > nv) return vb;  // the last partial run: as issued
+    return c * C + (vb % 8) * K + (vb / 8) % K;
+}
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_STAGE_ATTR void k_light_stage(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<true>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
+        k_light_body<true>(light_vb(vb, nvblk), v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_PLAIN_ATTR void k_light_plain(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
+        k_light_body<false>(light_vb(vb, nvblk), v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 // Work items in issue order, the items of dependents with >= thr light-group entries (many windows: c2's 6 % of
 // items that hold 45 % of the cycles) first: blocks are dispatched in index order, and a 10^6-cycle item issued near
@@ -2490,7 +2504,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_order(const u32* __restrict
 // searches and sweeps are latency-bound, more waves hide more of it), chosen by LIGHT_HIOCC_AVG
 __global__ __launch_bounds__(RDF_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_light_plain_hi(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
+        k_light_body<false>(light_vb(vb, nvblk), v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 
 
