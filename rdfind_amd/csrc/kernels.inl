@@ -643,7 +643,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
         return;
     }
-    u64 run = block_offsets[blockIdx.x];
+    // region mode (block_offsets == nullptr, k_emit_compact after it): no count pass; the block writes its kept records
+    // from 9 x per x block on and its kept count to block_counts, no padding
+    const bool region = block_offsets == nullptr;
+    const u64 rbase = region ? 9ull * per * blockIdx.x : 0ull;
+    u64 run = region ? rbase : block_offsets[blockIdx.x];
 #ifndef RDF_EMIT_DEDUP
 #define RDF_EMIT_DEDUP 1
 #endif
@@ -707,9 +711,32 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
 #pragma unroll
         for (int k = 0; k < 9; ++k)
             if ((keep >> k) & 1u) out[q++] = rec[k];
+        if (region) {
+            run += kept;
+            continue;
+        }
         u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
         for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
         run += total;
+    }
+    if (region && threadIdx.x == 0) block_counts[blockIdx.x] = run - rbase;
+}
+
+// region mode's compaction: block b's kept records [9 x per x b, + cnt[b]) -> dst[off[b], + cnt[b]) (coalesced, 4 loads
+// in flight per lane)
+__global__ __launch_bounds__(RDF_BLOCK) void k_emit_compact(const u64* __restrict__ src, u64 region,
+                                                            const u64* __restrict__ cnt, const u64* __restrict__ off,
+                                                            u64* __restrict__ dst) {
+    const u64 b = blockIdx.x, m = cnt[b];
+    const u64* sp = src + b * region;
+    u64* dp = dst + off[b];
+    for (u64 i0 = threadIdx.x; i0 < m; i0 += 4ull * RDF_BLOCK) {
+        u64 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i0 + (u64)u * RDF_BLOCK < m ? sp[i0 + (u64)u * RDF_BLOCK] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + (u64)u * RDF_BLOCK < m) dp[i0 + (u64)u * RDF_BLOCK] = v[u];
     }
 }
 

@@ -1422,14 +1422,35 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     }
     const unsigned eg = grid_for(units, RDF_BLOCK, kGrid);
     const u64 per = units ? (units + eg - 1) / eg : 0;
-    ENSURE(c, eblk, (eg + 1ull) * 8);
+    ENSURE(c, eblk, 2 * (eg + 1ull) * 8);
     const bool reuse = cache < 0 && slot < (int)c->ecache_je.size();
+    // one pass (no count pass) when the record buffers hold 9 records per triple: every block writes its kept records
+    // into its own region of rec_tmp (9 x per slots), then k_emit_compact packs the regions into rec by the scanned
+    // block counts; no padding reaches the sort (RDFIND_EMIT_ONEPASS=1; default: count pass + write pass)
+    static const bool onepass_env = getenv("RDFIND_EMIT_ONEPASS") && atoi(getenv("RDFIND_EMIT_ONEPASS")) != 0;
+    const bool onepass = onepass_env && !lists && cache == 0 && slot_cap >= 9 * n && units == n;
+    if (onepass && units) {
+        u64* eoff = c->eblk.as<u64>() + (eg + 1ull);
+        if (lazy)
+            hipLaunchKernelGGL((k_emit_records<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                               2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
+                               joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, c->rec_tmp.as<u64>(), capbits + joinbits);
+        else
+            hipLaunchKernelGGL((k_emit_records<true, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
+                               2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
+                               joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, c->rec_tmp.as<u64>(), capbits + joinbits);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), eoff, eg, dscal(c, 0), st));
+        hipLaunchKernelGGL(k_emit_compact, dim3(eg), dim3(RDF_BLOCK), 0, st, c->rec_tmp.as<u64>(), 9 * per,
+                           c->eblk.as<u64>(), eoff, ebuf);
+        HIP_TRY(c, hipGetLastError());
+    }
     u64 je_early = ~0ull;  // the slot count, when read before the write pass
     if (cache > 0) {
         if ((int)c->ecache_je.size() <= slot) c->ecache_je.resize(slot + 1);
         HIP_TRY(c, c->ecache.grow_keep((size_t)(slot + 1) * ECACHE_STRIDE * 8, st));
     }
-    if (units) {
+    if (units && !onepass) {
         if (reuse) {
             HIP_TRY(c, hipMemcpyAsync(c->eblk.p, c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, eg * 8ull,
                                       hipMemcpyDeviceToDevice, st));
