@@ -648,6 +648,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
     const bool region = block_offsets == nullptr;
     const u64 rbase = region ? 9ull * per * blockIdx.x : 0ull;
     u64 run = region ? rbase : block_offsets[blockIdx.x];
+    u64 emitted = 0;  // region mode: records emitted, repeats included (the run's n_records)
 #ifndef RDF_EMIT_DEDUP
 #define RDF_EMIT_DEDUP 1
 #endif
@@ -713,13 +714,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
             if ((keep >> k) & 1u) out[q++] = rec[k];
         if (region) {
             run += kept;
+            emitted += total;
             continue;
         }
         u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
         for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
         run += total;
     }
-    if (region && threadIdx.x == 0) block_counts[blockIdx.x] = run - rbase;
+    if (region && threadIdx.x == 0) {
+        block_counts[blockIdx.x] = run - rbase;
+        atomicAdd((unsigned long long*)(block_counts + gridDim.x), (unsigned long long)emitted);
+    }
 }
 
 // region mode's compaction: block b's kept records [9 x per x b, + cnt[b]) -> dst[off[b], + cnt[b]) (coalesced, 4 loads

@@ -1426,11 +1426,13 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     const bool reuse = cache < 0 && slot < (int)c->ecache_je.size();
     // one pass (no count pass) when the record buffers hold 9 records per triple: every block writes its kept records
     // into its own region of rec_tmp (9 x per slots), then k_emit_compact packs the regions into rec by the scanned
-    // block counts; no padding reaches the sort (RDFIND_EMIT_ONEPASS=1; default: count pass + write pass)
-    static const bool onepass_env = getenv("RDFIND_EMIT_ONEPASS") && atoi(getenv("RDFIND_EMIT_ONEPASS")) != 0;
+    // block counts; no padding reaches the sort.  c2 emit 0.86 -> 0.73 ms, sort 1.79 -> 1.71, c3 step 72.4 -> 69.9 ms
+    // (profiles/r05_emit_onepass_ab.log).  RDFIND_EMIT_ONEPASS=0: the count pass + write pass with padding
+    static const bool onepass_env = !getenv("RDFIND_EMIT_ONEPASS") || atoi(getenv("RDFIND_EMIT_ONEPASS")) != 0;
     const bool onepass = onepass_env && !lists && cache == 0 && slot_cap >= 9 * n && units == n;
     if (onepass && units) {
         u64* eoff = c->eblk.as<u64>() + (eg + 1ull);
+        HIP_TRY(c, hipMemsetAsync(c->eblk.as<u64>() + eg, 0, 8, st));  // records emitted, repeats included
         if (lazy)
             hipLaunchKernelGGL((k_emit_records<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
@@ -1444,6 +1446,7 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
         hipLaunchKernelGGL(k_emit_compact, dim3(eg), dim3(RDF_BLOCK), 0, st, c->rec_tmp.as<u64>(), 9 * per,
                            c->eblk.as<u64>(), eoff, ebuf);
         HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipMemcpyAsync(dscal(c, 3), c->eblk.as<u64>() + eg, 8, hipMemcpyDeviceToDevice, st));
     }
     u64 je_early = ~0ull;  // the slot count, when read before the write pass
     if (cache > 0) {
@@ -1498,8 +1501,10 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
         Je = c->ecache_je[slot];
     } else {
         if (je_early == ~0ull) {
-            TRY(read_scalars(c, 1));
+            TRY(read_scalars(c, onepass ? 4 : 1));
             je_early = c->hscal[0];
+            // one pass: the kept records are sorted, the emitted ones (repeats included) count as n_records
+            if (onepass && units && c->hscal[3] >= je_early) c->J_emit += c->hscal[3] - je_early;
         }
         Je = je_early;
         if (cache > 0) c->ecache_je[slot] = Je;
