@@ -221,7 +221,7 @@ def per_rank_balance(dist, world, mine):
 # the one-GPU c4 step this leg is compared with: round 5 (kept join ranges, K2 radix path, light load chains, XCD-local
 # radix tiles), the
 # c4_strong leg of profiles/r05_bench_c2.json (round 4: 1616 ms)
-C4_ONE_GPU_MS = 834.4
+C4_ONE_GPU_MS = 830.8
 
 
 def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):
