@@ -224,6 +224,13 @@ def per_rank_balance(dist, world, mine):
 C4_ONE_GPU_MS = 830.8
 
 
+def c4_golden(scale):
+    """The committed golden entry (count, set checksum) of c4 at this scale, strategy 1 --clean-implied, or None."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "full_size.json")))
+    key = "c4@1.0/s1_clean" if scale == 1.0 else f"c4@{scale}/s1_clean"
+    return g.get(key)
+
+
 def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):
     """BASELINE configs[3] (c4 at 10^9 triples, support 100) split over the N ranks -- strong scaling, the north-star
     scaling config.  Each rank draws and holds only its 1/N of the rows (synth.config_slice); a rank whose join shard
@@ -269,6 +276,7 @@ def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
         steps = max(args.c4_steps, 1)
+        checksum = ctx.checksum()  # this rank's set checksum (rdf_cind_checksum; the ranks' sets are disjoint)
         gs = ctx.groups
         kt = {k: v / steps for k, v in kt_sum.items()}
         mine = {"triples": n_local, "records": gs["n_records"], "join_ranges": gs.get("n_join_ranges", 1),
@@ -277,15 +285,26 @@ def c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks):
                 "kernel_ms": round(sum(kt.values()), 3), "hbm_held_gib": round(ctx.device_bytes() / 2**30, 1),
                 **{k: v for k, v in (getattr(ctx, "x_stats", None) or {}).items() if k in ("bytes_sent", "bytes_received")}}
     total_cinds = cs["n_cinds"]
+    total_checksum = checksum
     bal = None
     if dist is not None:
         bal = per_rank_balance(dist, world, mine)
         total_cinds = sum(r["cinds"] for r in bal["per_rank"])
+        sums = [None] * world
+        dist.all_gather_object(sums, checksum)
+        total_checksum = sum(sums) % (1 << 64)
     ms_step = elapsed * 1000.0 / steps
+    golden = c4_golden(scale)
     return {"workload": f"c4 (Freebase-shaped) scale {scale}: {total_n} triples split over {world} GPU(s), support {ms}, "
                         "strategy 1 --use-fis --clean-implied",
             "scaling": "strong", "n_gpus": world, "steps": args.c4_steps, "warmup": args.c4_warmup,
             "ms_per_step": round(ms_step, 3), "triples_per_s": round(total_n * steps / elapsed, 1), "cinds": total_cinds,
+            "checksum": str(total_checksum),
+            # the ranks' summed CIND count and set checksum against the committed golden of the streamed C oracle
+            # (tests/golden/full_size.json, read as data): the same set at every N
+            "matches_golden": None if golden is None else bool(total_cinds == golden["n_cinds"] and
+                                                               total_checksum == int(golden["checksum"])),
+            "golden": None if golden is None else f"tests/golden/full_size.json c4@{scale}/s1_clean",
             "one_gpu_ms_ref": C4_ONE_GPU_MS if scale == 1.0 else None,
             "speedup_vs_one_gpu_ref": round(C4_ONE_GPU_MS / ms_step, 3) if scale == 1.0 else None,
             "kernel_ms_rank0": {k: round(v, 3) for k, v in kt.items()}, "rank0": mine,
@@ -321,6 +340,10 @@ def main():
     ap.add_argument("--c4-scale", type=float, default=1.0, help="scale of the c4_strong leg (1.0 = 10^9 triples)")
     ap.add_argument("--c4-steps", type=int, default=2)
     ap.add_argument("--c4-warmup", type=int, default=1)
+    ap.add_argument("--c4-deadline", type=float, default=420.0,
+                    help="seconds the c4_strong leg may take; past it rank 0 prints the line with the c2 leg's "
+                         "measurement and c4_strong.error, and every rank exits (the line is never lost to a hang)")
+    ap.add_argument("--pg-timeout", type=float, default=300.0, help="process-group timeout (seconds) for N > 1")
     ap.add_argument("--page-bytes", type=int, default=None,
                     help="paged discovery (rdf_discover_cinds_paged) with this working memory per page, 0 = "
                          "automatic; every page is handed over in turn.  Default: unpaged, or automatic pages when the "
@@ -343,7 +366,11 @@ def main():
 
         local_rank %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group(args.backend)
+        import datetime
+        # a rank lost inside a collective ends the run after this long (gloo raises; RCCL's watchdog aborts the
+        # process) instead of leaving its peers waiting; failures outside collectives are agreed on at once
+        # (rdfind_amd/distributed.py run_protocol)
+        dist.init_process_group(args.backend, timeout=datetime.timedelta(seconds=args.pg_timeout))
 
     from rdfind_amd import _lib, synth
 
@@ -549,15 +576,7 @@ def main():
         ranks = per_rank_balance(dist, world, mine)
 
     ctx.close()
-    c4 = None
-    want_c4 = args.c4_strong == "on" or (args.c4_strong == "auto" and args.config == "c2"
-                                         and (world == 1 or args.backend == "nccl"))
-    if want_c4:
-        try:
-            c4 = c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks)
-        except Exception as e:  # reported in the line; the main leg's measurement stands
-            c4 = {"error": f"{type(e).__name__}: {e}"[:500]}
-
+    line = None
     if rank == 0:
         per = "per GPU" if args.scaling == "weak" else "total"
         wl = {"c2": "LUBM-shaped"}.get(args.config, args.config)
@@ -581,7 +600,6 @@ def main():
                                 "note": "the same steps with the result left in HBM"},
             "roofline": roof, "count_kernels": count_roof, "families": fams,
             "cpu_baseline": cpu, "ingest": ingest, **({"ranks": ranks} if ranks else {}),
-            **({"c4_strong": c4} if c4 else {}),
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "work": {"records": gs["n_records"], "groups": gs["n_groups"], "captures": gs["n_captures"],
                      "join_ranges": gs.get("n_join_ranges", 1), "ranges_kept": gs.get("n_ranges_kept", 0),
@@ -591,6 +609,32 @@ def main():
                      "classes": cs["n_classes"], "class_cinds": cs["n_class_cinds"],
                      **({"exchange_rank0": getattr(ctx, "x_stats", None)} if world > 1 else {})},
         }
+    want_c4 = args.c4_strong == "on" or (args.c4_strong == "auto" and args.config == "c2"
+                                         and (world == 1 or args.backend == "nccl"))
+    if want_c4:
+        if line is not None:  # the main leg's measurement, on record before the c4 leg starts (stderr)
+            print("bench.py: main leg: " + json.dumps(line), file=sys.stderr, flush=True)
+        import threading
+
+        def expire():  # the c4 leg hangs (a rank lost inside a collective): the line goes out without it
+            if line is not None:
+                line["c4_strong"] = {"error": f"the c4_strong leg exceeded --c4-deadline {args.c4_deadline:.0f} s; "
+                                              "every rank stopped"}
+                print(json.dumps(line), flush=True)
+            sys.stderr.flush()
+            os._exit(0)
+
+        timer = threading.Timer(args.c4_deadline, expire)
+        timer.daemon = True
+        timer.start()
+        try:
+            c4 = c4_strong_leg(args, dist, rank, world, local_rank, barrier, max_over_ranks)
+        except Exception as e:  # reported in the line; the main leg's measurement stands
+            c4 = {"error": f"{type(e).__name__}: {e}"[:500]}
+        timer.cancel()
+        if line is not None:
+            line["c4_strong"] = c4
+    if line is not None:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

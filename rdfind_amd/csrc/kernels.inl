@@ -480,147 +480,13 @@ __device__ inline u32 triple_records(u64 i, const u32* __restrict__ s, const u32
     return c;
 }
 
-// One join range's (triple, attribute) entries: the triples whose subject (entries [0, m_s)), predicate ([m_s, m_sp))
-// or object ([m_sp, m)) is a join value of the range, ascending triple index per attribute.  The records of entry e are
-// those triple_records makes for that attribute (at most 3), in the same order; the join value needs no selection test.
-__device__ inline u32 entry_records(u64 e, const u32* __restrict__ ent, u64 m_s, u64 m_sp, const u32* __restrict__ s,
-                                    const u32* __restrict__ p, const u32* __restrict__ o, u32 V, u32 twoU,
-                                    const u32* __restrict__ frank, const u64* __restrict__ lkeys,
-                                    const u32* __restrict__ lvals, u64 lmask, int joinbits, u64 (&rec)[9], u32* rep) {
-    const u64 i = ent[e];
-    const u32 ts = s[i], tp = p[i], to = o[i];
-    u32 c = 0, rp_mask = 0;
-    if (e >= m_sp) {  // o[s] (t4), o[p] (t5), o[s,p]
-        const u32 rs = frank[ts], rp = frank[(u64)V + tp];
-        if (rs != NONE32) rec[c++] = ((2ull * rs + 1) << joinbits) | to;
-        if (rp != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp + 1) << joinbits) | to; }
-        if (rs != NONE32 && rp != NONE32) {
-            const u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(2, ts, tp));
-            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | to;
-        }
-    } else if (e >= m_s) {  // p[s] (t2), p[o] (t3), p[s,o]
-        const u32 rs = frank[ts], ro = frank[2ull * V + to];
-        if (rs != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * rs) << joinbits) | tp; }
-        if (ro != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * ro + 1) << joinbits) | tp; }
-        if (rs != NONE32 && ro != NONE32) {
-            const u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(1, ts, to));
-            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | tp;
-        }
-    } else {  // s[p] (t0), s[o] (t1), s[p,o]
-        const u32 rp = frank[(u64)V + tp], ro = frank[2ull * V + to];
-        if (rp != NONE32) { rp_mask |= 1u << c; rec[c++] = ((2ull * rp) << joinbits) | ts; }
-        if (ro != NONE32) rec[c++] = ((2ull * ro) << joinbits) | ts;
-        if (rp != NONE32 && ro != NONE32) {
-            const u32 b = bin_lookup(lkeys, lvals, lmask, bin_key(0, tp, to));
-            if (b != NONE32) rec[c++] = (((u64)twoU + b) << joinbits) | ts;
-        }
-    }
-    if (rep) *rep = rp_mask;
-    return c;
-}
-
-// k_emit_records' two passes over a join range's entries (ENTRIES; the triple form below is k_emit_records itself,
-// kept as its own kernel: folded into this body it compiled to 45 instead of 75 VGPRs and c2's emission went from
-// 0.79 to 1.01 ms)
-template <bool WRITE, bool ENTRIES>
-__device__ inline void emit_records_body(const u32* __restrict__ s, const u32* __restrict__ p, const u32* __restrict__ o,
-                                         const u32* __restrict__ ent, u64 m_s, u64 m_sp, u64 n, u64 per, u32 V, u32 twoU,
-                                         const u32* __restrict__ frank, const u64* __restrict__ lkeys,
-                                         const u32* __restrict__ lvals, u64 lmask, int proj, int joinbits, JoinSel js,
-                                         u64* __restrict__ block_counts, const u64* __restrict__ block_offsets,
-                                         u64* __restrict__ out, int recbits) {
-    __shared__ u32 lds_wave[RDF_WAVES_PER_BLOCK];
-    __shared__ u64 htab[WRITE ? EMIT_DEDUP_SLOTS : 1];  // the iteration's distinct records (write pass)
-    const u64 b = (u64)blockIdx.x * per;
-    const u64 e = b + per < n ? b + per : n;
-#define RDF_UNIT_RECORDS(i, rec, rep)                                                                                  \
-    (ENTRIES ? entry_records(i, ent, m_s, m_sp, s, p, o, V, twoU, frank, lkeys, lvals, lmask, joinbits, rec, rep)        \
-             : triple_records<false>(i, s, p, o, V, twoU, frank, lkeys, lvals, lmask, proj, joinbits, js, rec, rep))
-    if (!WRITE) {  // the block's record count: per-thread sums, one block reduction at the end
-        u32 mine = 0;
-        for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
-            u64 rec[9];
-            mine += RDF_UNIT_RECORDS(i, rec, nullptr);
-        }
-        u32 total;
-        block_exclusive_scan_u32(mine, lds_wave, &total);
-        if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
-        return;
-    }
-    u64 run = block_offsets[blockIdx.x];
-#ifndef RDF_EMIT_DEDUP
-#define RDF_EMIT_DEDUP 1
-#endif
-    const bool dedup = RDF_EMIT_DEDUP && recbits <= 48;
-    u32 tag = 0;
-    if (dedup) {
-        for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;  // tag 0: empty
-        __syncthreads();
-    }
-    for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
-        const u64 i = i0 + threadIdx.x;
-        u64 rec[9];
-        u32 c = 0, rep = 0;
-        if (i < e) c = RDF_UNIT_RECORDS(i, rec, &rep);
-        // Records repeated within the iteration's 256 units (the same subject's predicate, the same (predicate,
-        // object) pair: ~23 % of c2's records; only the kinds flagged by the source are looked up) are written
-        // once; the count pass's region stays as it is and its tail is padded with EMIT_PAD, which the record sort's
-        // first pass drops.  The LDS table slots carry the iteration's tag in bits 48.. (records have <= 48 bits
-        // here), so it is cleared only when the tag wraps; the previous iteration's insertions finished before its
-        // scan's barriers.
-        u32 keep = (1u << c) - 1u;
-        if (dedup) {
-            ++tag;
-            if (tag == (1u << 15)) {  // tags wrap: clear the table once
-                __syncthreads();
-                for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;
-                __syncthreads();
-                tag = 1;
-            }
-            keep = ((1u << c) - 1u) & ~rep;  // only the repeating kinds go through the table
-            for (int k = 0; k < 9; ++k) {
-                if ((u32)k >= c) break;
-                if (!((rep >> k) & 1u)) continue;
-                const u64 want = rec[k] | ((u64)tag << 48);
-                u32 h = (u32)(mix64(rec[k]) >> 40) & (EMIT_DEDUP_SLOTS - 1);
-                u64 cur = htab[h];
-                while (true) {
-                    if ((u32)(cur >> 48) != tag) {  // a slot of an earlier iteration: free
-                        const u64 prev = atomicCAS((unsigned long long*)&htab[h], (unsigned long long)cur,
-                                                   (unsigned long long)want);
-                        if (prev == cur) {  // the first copy of the record: kept
-                            keep |= 1u << k;
-                            break;
-                        }
-                        cur = prev;
-                        continue;
-                    }
-                    if (cur == want) break;  // a copy is kept by another record
-                    h = (h + 1) & (EMIT_DEDUP_SLOTS - 1);
-                    cur = htab[h];
-                }
-            }
-        }
-        // one scan of (kept, emitted) packed in 16-bit halves (each <= 9 x 256): this thread's kept records go to the
-        // front of the iteration's region, its dropped ones become padding behind all kept records
-        const u32 nk = (u32)__popc(keep);
-        u32 tot;
-        const u32 off = block_exclusive_scan_u32(nk | (c << 16), lds_wave, &tot);
-        const u32 kept = tot & 0xffffu, total = tot >> 16;
-        u64 q = run + (off & 0xffffu);
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-            if ((keep >> k) & 1u) out[q++] = rec[k];
-        u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
-        for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
-        run += total;
-    }
-}
-#undef RDF_UNIT_RECORDS
-
 // two passes over contiguous per-block chunks of triples: COUNT writes each block's record count, the
 // write pass places records at the scanned block offset + block-local prefix (no shared counter, and the
-// record order is deterministic)
+// record order is deterministic).  The write pass is bounded by construction: block b writes only below
+// block_offsets[b + 1] (the scan's eg + 1 entries, the last one the total), so offsets that do not match this
+// emission (a join range's second emission reusing its first's scanned offsets) cannot write past the buffer; a record
+// that does not fit sets *block_counts (the overflow word of the write pass) and the host fails the build with
+// RDF_ERR_LIMIT (g_emit_range)
 template <bool WRITE, bool LAZY>
 __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restrict__ s, const u32* __restrict__ p,
                                                             const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
@@ -648,6 +514,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
     const bool region = block_offsets == nullptr;
     const u64 rbase = region ? 9ull * per * blockIdx.x : 0ull;
     u64 run = region ? rbase : block_offsets[blockIdx.x];
+    const u64 lim = region ? rbase + 9ull * per : block_offsets[blockIdx.x + 1];
+    bool over = false;
     u64 emitted = 0;  // region mode: records emitted, repeats included (the run's n_records)
 #ifndef RDF_EMIT_DEDUP
 #define RDF_EMIT_DEDUP 1
@@ -711,20 +579,28 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_records(const u32* __restric
         u64 q = run + (off & 0xffffu);
 #pragma unroll
         for (int k = 0; k < 9; ++k)
-            if ((keep >> k) & 1u) out[q++] = rec[k];
+            if ((keep >> k) & 1u) {
+                if (q < lim) out[q] = rec[k];
+                else over = true;
+                ++q;
+            }
         if (region) {
             run += kept;
             emitted += total;
             continue;
         }
         u64 pq = run + kept + ((off >> 16) - (off & 0xffffu));
-        for (u32 k = nk; k < c; ++k) out[pq++] = EMIT_PAD;
+        for (u32 k = nk; k < c; ++k, ++pq) {
+            if (pq < lim) out[pq] = EMIT_PAD;
+            else over = true;
+        }
         run += total;
     }
     if (region && threadIdx.x == 0) {
         block_counts[blockIdx.x] = run - rbase;
         atomicAdd((unsigned long long*)(block_counts + gridDim.x), (unsigned long long)emitted);
     }
+    if (!region && over) atomicOr((unsigned long long*)block_counts, 1ull);
 }
 
 // region mode's compaction: block b's kept records [9 x per x b, + cnt[b]) -> dst[off[b], + cnt[b]) (coalesced, 4 loads
@@ -746,10 +622,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_compact(const u64* __restric
 }
 
 // K3 of every join range at once (the kept range build, g_emit_all_ranges): the records go to their range's region of
-// rstore.  The count pass writes per (range, block) counts -> block_counts[r * gridDim.x + block]; the write pass places
-// a triple's records joined on one attribute (one join value, so one range) at that range's scanned block offset + an
-// LDS cursor.  The order inside a block's region is free (every range is sorted afterwards), so the cursors need no
-// scan.  Ranges: nr <= EMIT_MAX_RANGES ascending first join values rlo[0..nr), rlo[0] = 0.
+// rstore.  The per (range, block) counts come from the join histogram pass's block rows (k_range_block_counts), scanned
+// into block_offsets (nr x gridDim.x + 1 entries, the last the total); a triple's records joined on one attribute (one
+// join value, so one range) go to that range's block offset + an LDS cursor.  The order inside a block's region is free
+// (every range is sorted afterwards), so the cursors need no scan.  A (range, block) region ends at the next offset:
+// records past it are not written and set *overflow (the host fails the build: the histogram and this emission
+// disagree).  Ranges: nr <= EMIT_MAX_RANGES ascending first join values rlo[0..nr), rlo[0] = 0.
 static constexpr u32 EMIT_MAX_RANGES = 256;
 __device__ inline u32 range_of(const u32* rlo, u32 nr, u32 j) {  // last k with rlo[k] <= j
     u32 a = 0, b = nr - 1;
@@ -760,30 +638,33 @@ __device__ inline u32 range_of(const u32* rlo, u32 nr, u32 j) {  // last k with 
     }
     return a;
 }
-template <bool WRITE, bool LAZY>
+template <bool LAZY>
 __global__ __launch_bounds__(RDF_BLOCK) void k_emit_ranges(const u32* __restrict__ s, const u32* __restrict__ p,
                                                            const u32* __restrict__ o, u64 n, u64 per, u32 V, u32 twoU,
                                                            const u32* __restrict__ frank, const u64* __restrict__ lkeys,
                                                            const u32* __restrict__ lvals, u64 lmask, int proj,
                                                            int joinbits, JoinSel js, const u32* __restrict__ rlo_g, u32 nr,
-                                                           u64* block_counts, const u64* __restrict__ block_offsets,
+                                                           u64* overflow, const u64* __restrict__ block_offsets,
                                                            u64* out, int recbits) {
     __shared__ u32 rlo[EMIT_MAX_RANGES];
     __shared__ u32 cur[EMIT_MAX_RANGES];
-    __shared__ u64 base[WRITE ? EMIT_MAX_RANGES : 1];
-    __shared__ u64 htab[WRITE ? EMIT_DEDUP_SLOTS : 1];  // the iteration's distinct records (write pass)
+    __shared__ u64 base[EMIT_MAX_RANGES];
+    __shared__ u64 lim[EMIT_MAX_RANGES];
+    __shared__ u64 htab[EMIT_DEDUP_SLOTS];  // the iteration's distinct records
     for (u32 k = threadIdx.x; k < nr; k += RDF_BLOCK) {
         rlo[k] = rlo_g[k];
         cur[k] = 0;
-        if (WRITE) base[k] = block_offsets[(u64)k * gridDim.x + blockIdx.x];
+        base[k] = block_offsets[(u64)k * gridDim.x + blockIdx.x];
+        lim[k] = block_offsets[(u64)k * gridDim.x + blockIdx.x + 1];
     }
-    const bool dedup = WRITE && RDF_EMIT_DEDUP && recbits <= 48;
+    const bool dedup = RDF_EMIT_DEDUP && recbits <= 48;
     if (dedup)
         for (u32 k = threadIdx.x; k < (u32)EMIT_DEDUP_SLOTS; k += RDF_BLOCK) htab[k] = 0;  // tag 0: empty
     __syncthreads();
     const u64 b = (u64)blockIdx.x * per;
     const u64 e = b + per < n ? b + per : n;
     u32 tag = 0;
+    bool over = false;
     for (u64 i0 = b; i0 < e; i0 += RDF_BLOCK) {
         const u64 i = i0 + threadIdx.x;
         u64 rec[9];
@@ -828,84 +709,27 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_emit_ranges(const u32* __restrict
         if (co) ro = range_of(rlo, nr, o[i]);
         if (cp) rp = range_of(rlo, nr, p[i]);
         if (cs) rs = range_of(rlo, nr, s[i]);
-        if (!WRITE) {
-            if (co) atomicAdd(&cur[ro], co);
-            if (cp) atomicAdd(&cur[rp], cp);
-            if (cs) atomicAdd(&cur[rs], cs);
-        } else {
-            if (co) qo = base[ro] + atomicAdd(&cur[ro], co);
-            if (cp) qp = base[rp] + atomicAdd(&cur[rp], cp) - co;
-            if (cs) qs = base[rs] + atomicAdd(&cur[rs], cs) - co - cp;
+        if (co) qo = base[ro] + atomicAdd(&cur[ro], co);
+        if (cp) qp = base[rp] + atomicAdd(&cur[rp], cp) - co;
+        if (cs) qs = base[rs] + atomicAdd(&cur[rs], cs) - co - cp;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                if ((u32)k >= c) break;
-                const u64 q = (u32)k < co ? qo : (u32)k < co + cp ? qp : qs;
-                out[q + k] = ((keep >> k) & 1u) ? rec[k] : EMIT_PAD;
-            }
+        for (int k = 0; k < 9; ++k) {
+            if ((u32)k >= c) break;
+            const bool ko = (u32)k < co, kp = !ko && (u32)k < co + cp;
+            const u64 q = (ko ? qo : kp ? qp : qs) + k;
+            if (q < lim[ko ? ro : kp ? rp : rs]) out[q] = ((keep >> k) & 1u) ? rec[k] : EMIT_PAD;
+            else over = true;
         }
         if (dedup) __syncthreads();  // the next iteration's tag reuses the table's slots
     }
-    if (!WRITE) {
-        __syncthreads();
-        for (u32 k = threadIdx.x; k < nr; k += RDF_BLOCK) block_counts[(u64)k * gridDim.x + blockIdx.x] = cur[k];
-    }
+    if (over) atomicOr((unsigned long long*)overflow, 1ull);
 }
 
-// K3 over one join range's entry lists (m entries, entry_records)
-template <bool WRITE>
-__global__ __launch_bounds__(RDF_BLOCK) void k_emit_entries(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                            const u32* __restrict__ o, const u32* __restrict__ ent, u64 m,
-                                                            u64 m_s, u64 m_sp, u64 per, u32 V, u32 twoU,
-                                                            const u32* __restrict__ frank, const u64* __restrict__ lkeys,
-                                                            const u32* __restrict__ lvals, u64 lmask, int joinbits,
-                                                            u64* block_counts, const u64* __restrict__ block_offsets,
-                                                            u64* out, int recbits) {
-    const JoinSel all{0u, 1u, 0u, JOIN_ALL_HI};
-    emit_records_body<WRITE, true>(s, p, o, ent, m_s, m_sp, m, per, V, twoU, frank, lkeys, lvals, lmask, 7, joinbits, all,
-                                   block_counts, block_offsets, out, recbits);
-}
-
-// (triple, attribute) entries of the join ranges: bin = range * 3 + attribute (0 s, 1 p, 2 o) of each projected join
-// value this rank takes, its range from the bucket -> range map (join >> jshift, JH_BUCKETS buckets).  Pass 1 counts
-// per (bin, block) -> ghist[bin * G + block]; pass 2 writes the triple indices at the scanned offsets (LDS cursors).
-// Each block takes one contiguous chunk of triples, so the entries of a bin ascend by block.
 #ifndef RDF_JH_BITS
 #define RDF_JH_BITS 14
 #endif
 static constexpr int JH_BITS = RDF_JH_BITS;
 static constexpr u32 JH_BUCKETS = 1u << JH_BITS;  // join buckets of the join-range build (join >> jshift)
-static constexpr u32 RE_MAX_BINS = 3 * 1024;
-template <bool SCATTER>
-__global__ __launch_bounds__(RDF_BLOCK) void k_range_entries(const u32* __restrict__ s, const u32* __restrict__ p,
-                                                             const u32* __restrict__ o, u64 n, int proj, JoinSel own,
-                                                             int jshift, const uint16_t* __restrict__ bmap, u32 nbins,
-                                                             u32* ghist, u32* __restrict__ out) {
-    __shared__ uint16_t lmap[JH_BUCKETS];
-    __shared__ u32 lh[RE_MAX_BINS];
-    for (u32 k = threadIdx.x; k < JH_BUCKETS; k += RDF_BLOCK) lmap[k] = bmap[k];
-    for (u32 k = threadIdx.x; k < nbins; k += RDF_BLOCK) lh[k] = SCATTER ? ghist[(u64)k * gridDim.x + blockIdx.x] : 0u;
-    __syncthreads();
-    JoinSel all = own;
-    all.lo = 0u;
-    all.hi = JOIN_ALL_HI;
-    const u64 per = (n + gridDim.x - 1) / gridDim.x;
-    const u64 b = (u64)blockIdx.x * per, e = b + per < n ? b + per : n;
-    for (u64 i = b + threadIdx.x; i < e; i += RDF_BLOCK) {
-        const u32 v[3] = {s[i], p[i], o[i]};
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            if (!((proj >> a) & 1) || !all.take(v[a])) continue;
-            const u32 bin = 3u * lmap[v[a] >> jshift] + (u32)a;
-            const u32 pos = atomicAdd(&lh[bin], 1u);
-            if (SCATTER) out[pos] = (u32)i;
-        }
-    }
-    if (!SCATTER) {
-        __syncthreads();
-        for (u32 k = threadIdx.x; k < nbins; k += RDF_BLOCK) ghist[(u64)k * gridDim.x + blockIdx.x] = lh[k];
-    }
-}
-
 // ================================================================================================
 // K4/K5: capture groups  (UnionJoinCandidates.combine / UnionCombinedJoinCandidates.reduce,
 //     ALG/operators/UnionJoinCandidates.scala:27-44, UnionCombinedJoinCandidates.scala:21-31: distinct

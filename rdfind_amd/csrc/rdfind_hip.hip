@@ -74,16 +74,13 @@ struct rdf_ctx {
     std::vector<u64> jr_seg, jr_J;   // range k's slots in rstore start at jr_seg[k]; its sorted records
     bool jr_keep = false, range_keep = true;
     u64 peak_bytes = 0;              // RDFIND_MEM_REPORT: the largest sum of the buffers' sizes so far
-    // per range (triple, attribute) entry lists (g_range_entries): a range's emissions read only its own triples
-    DevBuf jrmap, jrhist, jent;      // join bucket -> range, per (bin, block) counts, the entries (bin-major)
-    std::vector<u64> jr_bin;         // first entry of bin 3 range + attribute (+ the total)
-    bool jr_lists = false;           // the current range build emits from the entry lists
-    bool range_lists = false;        // RDFIND_RANGE_LISTS=1: emit each range from its entry lists (measured slower:
-                                     // the lists' triple gathers cost more than reading every triple)
+    DevBuf jrmap;                    // the kept range build: the ranges' first join values and first join buckets
     bool sh_ranged = false;          // the sharded build of this run goes in join ranges (sh_phase14 -> sh_phase1)
     u64 sh_m = 0;                    // sharded: triples received for this rank's join shard (wts / wtp / wto)
     std::string test_fail_launch;    // RDFIND_TEST_FAIL_LAUNCH: a kernel launched with an invalid configuration (test hook)
     bool test_oom_discovery = false; // RDFIND_TEST_OOM_DISCOVERY: rdf_discover_cinds fails with RDF_ERR_OOM (test hook)
+    int test_fail_rank = -1, test_fail_phase = -1;  // RDFIND_TEST_FAIL_SHARD=rank:phase: that rank's rdf_shard_step fails
+                                                    // with RDF_ERR_OOM at that phase (test hook: cross-rank failure agreement)
     int holder_qbits = 2;            // RDFIND_HOLDER_Q: pivot-holder election on log-size buckets (holder_key; 0: exact)
     bool hot_balance = true;         // RDFIND_HOT_BALANCE=0: every join value's owner by hash (no hot table)
     DevBuf hot, hotc;                // hot join values' owners (open-addressing table), this owner's candidates
@@ -259,7 +256,7 @@ static rdf_status fail(rdf_ctx* c, rdf_status code, const std::string& msg) {
 // only when an allocation of a later stage would otherwise fail.
 static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
     const std::vector<DevBuf*> fc_scratch = {&c->brkeys, &c->brkeys2, &c->tkeys, &c->urecs};
-    const std::vector<DevBuf*> grp_scratch = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->jent, &c->rstore};
+    const std::vector<DevBuf*> grp_scratch = {&c->rec, &c->rec_tmp, &c->fk, &c->fk_tmp, &c->rstore};
     const std::vector<DevBuf*> x_scratch = {&c->xsend, &c->xrecv};
     bool any = false;
     for (int k = 0; k < 3; ++k) {
@@ -418,7 +415,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->lkeys, &c->lvals, &c->flags, &c->pos, &c->rec, &c->rec_tmp, &c->support, &c->fidx,
                       &c->fcap, &c->frank, &c->fval, &c->fext, &c->info, &c->fk, &c->fk_tmp, &c->fpos, &c->cstart, &c->skip, &c->gflag, &c->gexcl, &c->goff,
                       &c->gcap, &c->gmap, &c->csup,
-                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->lsup, &c->hot, &c->hotc, &c->jrmap, &c->jrhist, &c->jent, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
+                      &c->doff, &c->dcur, &c->dgrp, &c->jhist, &c->rsup, &c->lsup, &c->hot, &c->hotc, &c->jrmap, &c->offp, &c->hist, &c->heavy_list, &c->hbit, &c->bcomp, &c->bkeyc,
                       &c->pcnt, &c->poff, &c->pcur, &c->plist, &c->pivot, &c->nchl, &c->nchh, &c->choffl,
                       &c->choffh, &c->epairs, &c->epairs_tmp, &c->eoff, &c->hcounts, &c->hoff, &c->hbits, &c->cbits, &c->hown, &c->cown, &c->sbase, &c->dcls, &c->crep, &c->out,
                       &c->stage_rows, &c->nitl, &c->itoffl, &c->dead, &c->ebin,
@@ -437,7 +434,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
 }
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
-static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "jrhist", "jent", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder"};
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder"};
 static bool mem_report_on() {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
     return on;
@@ -498,8 +495,10 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (const char* hq = getenv("RDFIND_HOLDER_Q")) c->holder_qbits = std::max(0, std::min(atoi(hq), 8));
     if (const char* tf = getenv("RDFIND_TEST_FAIL_LAUNCH")) c->test_fail_launch = tf;
     if (const char* to = getenv("RDFIND_TEST_OOM_DISCOVERY")) c->test_oom_discovery = atoi(to) != 0;
+    if (const char* tf = getenv("RDFIND_TEST_FAIL_SHARD")) {
+        if (sscanf(tf, "%d:%d", &c->test_fail_rank, &c->test_fail_phase) != 2) c->test_fail_rank = c->test_fail_phase = -1;
+    }
     if (const char* hb = getenv("RDFIND_HOT_BALANCE")) c->hot_balance = atoi(hb) != 0;
-    if (const char* rl = getenv("RDFIND_RANGE_LISTS")) c->range_lists = atoi(rl) != 0;
     if (const char* rk = getenv("RDFIND_RANGE_KEEP")) c->range_keep = atoi(rk) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -1409,28 +1408,18 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     const int slot = cache > 0 ? cache - 1 : cache < 0 ? -cache - 1 : -1;
     // the selection takes a part of the join values (a join range, or a rank's shard): lazy condition-rank loads
     const bool lazy = js.nranks > 1 || js.lo != 0u || js.hi != JOIN_ALL_HI;
-    // work units: every triple (js selects the join values), or the range's (triple, attribute) entries
-    const bool lists = c->jr_lists && slot >= 0 && 3 * (u64)slot + 3 < c->jr_bin.size();
-    u64 units = n, m_s = 0, m_sp = 0;
-    const u32* ent = nullptr;
-    if (lists) {
-        const u64 base = c->jr_bin[3 * slot];
-        units = c->jr_bin[3 * slot + 3] - base;
-        m_s = c->jr_bin[3 * slot + 1] - base;
-        m_sp = c->jr_bin[3 * slot + 2] - base;
-        ent = c->jent.as<u32>() + base;
-    }
-    const unsigned eg = grid_for(units, RDF_BLOCK, kGrid);
-    const u64 per = units ? (units + eg - 1) / eg : 0;
+    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const u64 per = n ? (n + eg - 1) / eg : 0;
     ENSURE(c, eblk, 2 * (eg + 1ull) * 8);
     const bool reuse = cache < 0 && slot < (int)c->ecache_je.size();
+    u64* overflow = (u64*)dscal(c, 8);  // the write pass's overflow word (zeroed above)
     // one pass (no count pass) when the record buffers hold 9 records per triple: every block writes its kept records
     // into its own region of rec_tmp (9 x per slots), then k_emit_compact packs the regions into rec by the scanned
     // block counts; no padding reaches the sort.  c2 emit 0.86 -> 0.73 ms, sort 1.79 -> 1.71, c3 step 72.4 -> 69.9 ms
     // (profiles/r05_emit_onepass_ab.log).  RDFIND_EMIT_ONEPASS=0: the count pass + write pass with padding
     static const bool onepass_env = !getenv("RDFIND_EMIT_ONEPASS") || atoi(getenv("RDFIND_EMIT_ONEPASS")) != 0;
-    const bool onepass = onepass_env && !lists && cache == 0 && slot_cap >= 9 * n && units == n;
-    if (onepass && units) {
+    const bool onepass = onepass_env && cache == 0 && slot_cap >= 9 * n;
+    if (onepass && n) {
         u64* eoff = c->eblk.as<u64>() + (eg + 1ull);
         HIP_TRY(c, hipMemsetAsync(c->eblk.as<u64>() + eg, 0, 8, st));  // records emitted, repeats included
         if (lazy)
@@ -1453,17 +1442,13 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
         if ((int)c->ecache_je.size() <= slot) c->ecache_je.resize(slot + 1);
         HIP_TRY(c, c->ecache.grow_keep((size_t)(slot + 1) * ECACHE_STRIDE * 8, st));
     }
-    if (units && !onepass) {
+    if (n && !onepass) {
+        // the write pass's block offsets: eg + 1 entries (the last one the slot count), each block bounded by the next
         if (reuse) {
-            HIP_TRY(c, hipMemcpyAsync(c->eblk.p, c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, eg * 8ull,
+            HIP_TRY(c, hipMemcpyAsync(c->eblk.p, c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, (eg + 1ull) * 8ull,
                                       hipMemcpyDeviceToDevice, st));
         } else {
-            if (lists)
-                hipLaunchKernelGGL((k_emit_entries<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, ent, units, m_s,
-                                   m_sp, per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(),
-                                   c->lcap - 1, joinbits, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr,
-                                   capbits + joinbits);
-            else if (lazy)
+            if (lazy)
                 hipLaunchKernelGGL((k_emit_records<false, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                    2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
                                    joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
@@ -1471,9 +1456,11 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
                 hipLaunchKernelGGL((k_emit_records<false, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                    2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
                                    joinbits, js, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, capbits + joinbits);
-            HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, dscal(c, 0), st));
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), eg, c->eblk.as<u64>() + eg, st));
+            HIP_TRY(c, hipMemcpyAsync(dscal(c, 0), c->eblk.as<u64>() + eg, 8, hipMemcpyDeviceToDevice, st));
             if (cache > 0)
-                HIP_TRY(c, hipMemcpyAsync(c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, c->eblk.p, eg * 8ull,
+                HIP_TRY(c, hipMemcpyAsync(c->ecache.as<u64>() + (u64)slot * ECACHE_STRIDE, c->eblk.p, (eg + 1ull) * 8ull,
                                           hipMemcpyDeviceToDevice, st));
             if (slot_cap < 9 * n) {  // a join range's buffers: the slot count is checked before the write pass
                 TRY(read_scalars(c, 1));
@@ -1482,21 +1469,27 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
                     return fail(c, RDF_ERR_LIMIT, "K3 emitted more records than the join range was sized for");
             }
         }
-        if (lists)
-            hipLaunchKernelGGL((k_emit_entries<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, ent, units, m_s, m_sp,
-                               per, V, 2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1,
-                               joinbits, (u64*)nullptr, c->eblk.as<u64>(), ebuf, capbits + joinbits);
-        else if (lazy)
+        if (lazy)
             hipLaunchKernelGGL((k_emit_records<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
-                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), ebuf, capbits + joinbits);
+                               joinbits, js, overflow, c->eblk.as<u64>(), ebuf, capbits + joinbits);
         else
             hipLaunchKernelGGL((k_emit_records<true, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V,
                                2u * c->U, c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj,
-                               joinbits, js, (u64*)nullptr, c->eblk.as<u64>(), ebuf, capbits + joinbits);
+                               joinbits, js, overflow, c->eblk.as<u64>(), ebuf, capbits + joinbits);
+        HIP_TRY(c, hipGetLastError());
     }
     tend(c, RDF_T_EMIT);
     u64 Je = 0;  // emitted record slots (repeats within an emission iteration are padding)
+    if (n && !onepass) {
+        // every block of the write pass stayed inside its region [off[b], off[b + 1]) (k_emit_records bounds it); the
+        // overflow word says whether a block had more records than its region (a join range's second emission reusing
+        // its first's offsets, if the two ever differed): an error, never a write past the buffer
+        TRY(read_u64(c, overflow, &c->hscal[8]));
+        if (c->hscal[8])
+            return fail(c, RDF_ERR_LIMIT, "K3: a block emitted more records than its scanned region (records past it "
+                                          "were not written)");
+    }
     if (reuse) {
         Je = c->ecache_je[slot];
     } else {
@@ -1504,7 +1497,7 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
             TRY(read_scalars(c, onepass ? 4 : 1));
             je_early = c->hscal[0];
             // one pass: the kept records are sorted, the emitted ones (repeats included) count as n_records
-            if (onepass && units && c->hscal[3] >= je_early) c->J_emit += c->hscal[3] - je_early;
+            if (onepass && n && c->hscal[3] >= je_early) c->J_emit += c->hscal[3] - je_early;
         }
         Je = je_early;
         if (cache > 0) c->ecache_je[slot] = Je;
@@ -1689,46 +1682,6 @@ static rdf_status g_compact_groups(rdf_ctx* c) {
 //     join order, so goff / gcap / gmap / dgrp are exactly the one-pass build's.
 // One GPU runs the passes back to back (g_build_ranges).  A rank of a sharded run (own = its join shard) runs pass 1
 // on the triples it received, all-reduces the supports, and runs pass 2 (sh_phase14 -> sh_phase1).
-// The (triple, attribute) entries of every join range (k_range_entries: a count pass, a scan, a scatter pass over the
-// triples' join values only), so that each range's two emissions read its own triples instead of all of them: c4 at
-// 10^9 triples in 4 ranges read every triple 8 times.  12 B of entries per triple at most (3 attributes).
-static rdf_status g_range_entries(rdf_ctx* c, int proj, JoinSel own, int jshift) {
-    hipStream_t st = c->stream;
-    const u64 n = c->n;
-    const std::vector<rdf_ctx::JoinRange>& ranges = c->jranges;
-    const u32 nr = (u32)ranges.size(), nbins = 3 * nr;
-    std::vector<uint16_t> bm(JH_BUCKETS);
-    u32 r = 0;
-    for (u32 b = 0; b < JH_BUCKETS; ++b) {
-        const u64 j0 = (u64)b << jshift;
-        while (r + 1 < nr && j0 >= ranges[r].hi) ++r;
-        bm[b] = (uint16_t)r;
-    }
-    ENSURE(c, jrmap, JH_BUCKETS * 2);
-    HIP_TRY(c, ctx_copy(c, c->jrmap.p, bm.data(), JH_BUCKETS * 2, hipMemcpyHostToDevice));
-    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>(2048, (n + 16383) / 16384));
-    const u64 nh = (u64)nbins * G;
-    ENSURE(c, jrhist, (nh + 1) * 4);
-    tbegin(c, RDF_T_EMIT);
-    hipLaunchKernelGGL((k_range_entries<false>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, proj, own, jshift,
-                       c->jrmap.as<uint16_t>(), nbins, c->jrhist.as<u32>(), (u32*)nullptr);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, exclusive_scan_u32(c->ws, c->jrhist.as<u32>(), c->jrhist.as<u32>(), nh, c->jrhist.as<u32>() + nh, st));
-    std::vector<u32> h(nh + 1);
-    HIP_TRY(c, ctx_copy(c, h.data(), c->jrhist.p, (nh + 1) * 4, hipMemcpyDeviceToHost));
-    const u64 total = h[nh];
-    ENSURE(c, jent, std::max<u64>(total, 1) * 4);
-    hipLaunchKernelGGL((k_range_entries<true>), dim3(G), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, proj, own, jshift,
-                       c->jrmap.as<uint16_t>(), nbins, c->jrhist.as<u32>(), c->jent.as<u32>());
-    HIP_TRY(c, hipGetLastError());
-    tend(c, RDF_T_EMIT);
-    c->jr_bin.resize(nbins + 1);
-    for (u32 b = 0; b < nbins; ++b) c->jr_bin[b] = h[(u64)b * G];
-    c->jr_bin[nbins] = total;
-    c->jr_lists = true;
-    return RDF_OK;
-}
-
 // Keep pass 1's sorted records of every range (rstore: the ranges' record counts, 8 B each) when they fit beside the
 // range scratch and the build's global arrays (the bound of auto_range_records): pass 2 then reads them instead of
 // emitting and sorting every range a second time (c4 at 10^9 triples: 47 GB kept, one emission and one sort saved
@@ -1796,19 +1749,9 @@ static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
     const int recbits = c->capbits + c->joinbits;
     const u32 twoU = 2u * c->U;
     tbegin(c, RDF_T_EMIT);
-    if (n) {  // per (range, block) counts from the histogram pass's block rows (RDFIND_RANGE_COUNT=1: a count pass)
-        static const bool count_pass = getenv("RDFIND_RANGE_COUNT") && atoi(getenv("RDFIND_RANGE_COUNT")) != 0;
-        if (count_pass && lazy)
-            hipLaunchKernelGGL((k_emit_ranges<false, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
-                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
-                               c->jrmap.as<u32>(), nr, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, recbits);
-        else if (count_pass)
-            hipLaunchKernelGGL((k_emit_ranges<false, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
-                               c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
-                               c->jrmap.as<u32>(), nr, c->eblk.as<u64>(), (const u64*)nullptr, (u64*)nullptr, recbits);
-        else
-            hipLaunchKernelGGL(k_range_block_counts, dim3(grid_for(nb * RDF_WAVE, RDF_BLOCK, 1u << 30)), dim3(RDF_BLOCK), 0, st,
-                               c->jbh.as<u32>(), eg, c->jrmap.as<u32>() + nr, nr, c->eblk.as<u64>());
+    if (n) {  // per (range, block) counts from the histogram pass's block rows
+        hipLaunchKernelGGL(k_range_block_counts, dim3(grid_for(nb * RDF_WAVE, RDF_BLOCK, 1u << 30)), dim3(RDF_BLOCK), 0, st,
+                           c->jbh.as<u32>(), eg, c->jrmap.as<u32>() + nr, nr, c->eblk.as<u64>());
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, exclusive_scan_u64(c->ws, c->eblk.as<u64>(), c->eblk.as<u64>(), nb, c->eblk.as<u64>() + nb, st));
     }
@@ -1819,15 +1762,20 @@ static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
         if ((n ? off[(u64)k * eg] : 0) != c->jr_seg[k])
             return fail(c, RDF_ERR_LIMIT, "K3 records per join range disagree with the join histogram");
     if (n) {
+        u64* overflow = (u64*)dscal(c, 8);  // zeroed above
         if (lazy)
-            hipLaunchKernelGGL((k_emit_ranges<true, true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
+            hipLaunchKernelGGL((k_emit_ranges<true>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
                                c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
-                               c->jrmap.as<u32>(), nr, (u64*)nullptr, c->eblk.as<u64>(), c->rstore.as<u64>(), recbits);
+                               c->jrmap.as<u32>(), nr, overflow, c->eblk.as<u64>(), c->rstore.as<u64>(), recbits);
         else
-            hipLaunchKernelGGL((k_emit_ranges<true, false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
+            hipLaunchKernelGGL((k_emit_ranges<false>), dim3(eg), dim3(RDF_BLOCK), 0, st, c->s, c->p, c->o, n, per, V, twoU,
                                c->frank.as<u32>(), c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1, proj, c->joinbits, own,
-                               c->jrmap.as<u32>(), nr, (u64*)nullptr, c->eblk.as<u64>(), c->rstore.as<u64>(), recbits);
+                               c->jrmap.as<u32>(), nr, overflow, c->eblk.as<u64>(), c->rstore.as<u64>(), recbits);
         HIP_TRY(c, hipGetLastError());
+        // every (range, block) region ends at the next offset; records past it were not written
+        TRY(read_u64(c, overflow, &c->hscal[8]));
+        if (c->hscal[8])
+            return fail(c, RDF_ERR_LIMIT, "K3 records per (join range, block) disagree with the join histogram");
     }
     tend(c, RDF_T_EMIT);
     return RDF_OK;
@@ -1887,10 +1835,7 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
         return fail(c, RDF_ERR_LIMIT, "one join bucket holds >= 2^32 capture records");
     c->jr_cap_rec = cap_rec;
     c->n_group_ranges = ranges.size();
-    c->jr_lists = false;
     TRY(g_range_keep_plan(c));
-    if (!c->jr_keep && c->range_lists && ranges.size() > 1 && 3 * ranges.size() <= RE_MAX_BINS && n)
-        TRY(g_range_entries(c, proj, own, jshift));
     // 2. supports
     ENSURE(c, support, std::max<u64>(ncap, 1) * 4);
     ENSURE(c, rsup, std::max<u64>(ncap, 1) * 4);
@@ -2069,8 +2014,8 @@ static u64 auto_range_records(rdf_ctx* c) {
     const u64 held = (u64)c->brkeys.cap + c->brkeys2.cap + c->tkeys.cap + c->urecs.cap +
                      (c->spare_x ? (u64)c->xsend.cap + c->xrecv.cap : 0ull) + c->rstore.cap;
     const u64 avail = (u64)free_b + held;
-    // ~4.5 records per triple kept; the ranges' entry lists (g_range_entries) up to 12 B per triple
-    const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30) + (c->range_lists ? 12 * c->n : 0);
+    // ~4.5 records per triple kept
+    const u64 global = 8 * 9 * c->n / 2 + 16ull * (c->V ? c->V : 1) + (4ull << 30);
     const u64 r = avail > global ? (avail - global) / 48 : 0;
     return std::max<u64>(std::min<u64>(r, 1ull << 31), 1ull << 24);
 }
@@ -3497,7 +3442,9 @@ static rdf_status sh_phase16(rdf_ctx* c, rdf_exchange* req) {
     c->sh_Bu = Bu;
     c->hot_n = 0;
     c->hot_mask = 0;
-    if (!c->hot_balance || c->sh_nranks <= 1) {
+    // (hot balancing packs a key as key << 32 | count with 0xffffffff as the slice-size marker: dictionaries whose 3V
+    // keys reach it keep the hash owners)
+    if (!c->hot_balance || c->sh_nranks <= 1 || 3ull * (c->V ? c->V : 1) >= 0xffffffffull) {
         HIP_TRY(c, hipStreamSynchronize(st));
         return x_request(c, req, RDF_X_ALLGATHERV_U64, c->ukeys.p, Bu, 11);
     }
@@ -3518,6 +3465,25 @@ static rdf_status sh_phase16(rdf_ctx* c, rdf_exchange* req) {
     HIP_TRY(c, hipGetLastError());
     u32 k = 0;
     TRY(read_u32(c, c->hotc.as<u64>() + HOT_CAP + 1, &k));
+    if (k > HOT_CAP) {
+        // more candidates than the cap (an owner whose slice is small against the summed counts it owns): all of them
+        // again, and the HOT_CAP largest by (count desc, key asc), so the submitted set does not depend on the order of
+        // the device's atomics and keeps the hottest values
+        const u64 kk = k;
+        ENSURE(c, hotc, (kk + 2) * 8);
+        HIP_TRY(c, hipMemsetAsync(c->hotc.as<u64>() + kk + 1, 0, 8, st));
+        hipLaunchKernelGGL(k_hot_candidates, dim3(grid_for(tcap, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->lkeys.as<u64>(), c->lvals.as<u32>(), tcap, c->V ? c->V : 1u, c->sh_proj,
+                           (u32)std::min<u64>(thr, 0xffffffffu), (u32)kk, c->hotc.as<u64>() + 1,
+                           (u32*)(c->hotc.as<u64>() + kk + 1));
+        HIP_TRY(c, hipGetLastError());
+        std::vector<u64> cand(kk);
+        HIP_TRY(c, ctx_copy(c, cand.data(), c->hotc.as<u64>() + 1, kk * 8, hipMemcpyDeviceToHost));
+        std::partial_sort(cand.begin(), cand.begin() + HOT_CAP, cand.end(), [](u64 a, u64 b) {
+            return (u32)a != (u32)b ? (u32)a > (u32)b : (a >> 32) < (b >> 32);
+        });
+        HIP_TRY(c, ctx_copy(c, c->hotc.as<u64>() + 1, cand.data(), HOT_CAP * 8, hipMemcpyHostToDevice));
+    }
     k = std::min<u32>(k, HOT_CAP);
     c->hscal[14] = (0xffffffffull << 32) | n;  // marker word: this rank's slice size
     HIP_TRY(c, ctx_copy(c, c->hotc.p, c->hscal + 14, 8, hipMemcpyHostToDevice));
@@ -4528,6 +4494,8 @@ rdf_status rdf_shard_step(rdf_ctx* c, rdf_exchange* req) {
     if (!sh_phase_valid(c->sh_phase, false)) return fail(c, RDF_ERR_STATE, "rdf_shard_begin must be called first");
     if (!c->x_imported) return fail(c, RDF_ERR_STATE, "rdf_shard_import must supply the pending exchange first");
     HIP_TRY(c, hipSetDevice(c->device));
+    if ((int)c->sh_rank == c->test_fail_rank && c->sh_phase == c->test_fail_phase)
+        return fail(c, RDF_ERR_OOM, "RDFIND_TEST_FAIL_SHARD: this rank fails at phase " + std::to_string(c->sh_phase));
     rdf_status r = RDF_OK;
     switch (c->sh_phase) {
         case 1: r = sh_phase1(c, req); break;

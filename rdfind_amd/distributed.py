@@ -36,6 +36,13 @@ Each rank then emits the CINDs of its own dependents; the union over ranks is th
 
 ``run_sharded`` drives any object with ``shard_begin/shard_step/shard_export/shard_import`` (the HIP
 ``Context``); ``run_protocol`` is the backend-neutral loop, also used by the CPU protocol tests.
+
+Failure agreement.  Every collective starts with one small all-gather of a header per rank -- (status, op, count,
+send counts) -- which also carries the counts allgatherv / alltoallv need, and the run ends with one more header (op
+DONE).  A rank whose library step, export or import fails joins the next header with a failure status and raises; every
+other rank sees it there and raises ``PeerFailure`` instead of waiting in a collective the failed rank never enters
+(the reference's job fails as a whole on any task's exception, FLK/jobs/AbstractProgram.java:119-126).  A rank that
+dies inside a collective is covered by the process group's timeout (``init_process_group(timeout=...)``).
 """
 from __future__ import annotations
 
@@ -74,18 +81,19 @@ def _compact_in_place(buf: torch.Tensor, counts, mx: int) -> int:
     return off
 
 
-def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
-    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order.  One all-gather of the counts,
-    then, unless the contributions are very skewed, one all-gather of padded slices into a single preallocated tensor
-    (world x the largest slice) that is compacted in place, so the peak is that tensor (+ one padded copy of this
-    rank's slice and a 64 MiB staging chunk), not a second result-sized copy.  When padding would exceed 4x the payload
-    and 64 MiB, one broadcast per rank into its exact slice of the result instead (no padding)."""
+def allgatherv(send: torch.Tensor, group=None, counts=None) -> torch.Tensor:
+    """Variable-length all-gather: concatenation of every rank's ``send`` in rank order.  The counts (from the header
+    exchange, or one all-gather of them), then, unless the contributions are very skewed, one all-gather of padded slices
+    into a single preallocated tensor (world x the largest slice) that is compacted in place, so the peak is that tensor
+    (+ one padded copy of this rank's slice and a 64 MiB staging chunk), not a second result-sized copy.  When padding
+    would exceed 4x the payload and 64 MiB, one broadcast per rank into its exact slice of the result instead."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
-    counts_t = torch.empty(world, dtype=torch.int64, device=send.device)
-    dist.all_gather_into_tensor(counts_t, n, group=group)
-    counts = [int(c) for c in counts_t.tolist()]
+    if counts is None:
+        n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
+        counts_t = torch.empty(world, dtype=torch.int64, device=send.device)
+        dist.all_gather_into_tensor(counts_t, n, group=group)
+        counts = [int(c) for c in counts_t.tolist()]
     mx, tot = max(counts), sum(counts)
     if not tot:
         return send.new_empty(0)
@@ -111,21 +119,24 @@ def allgatherv(send: torch.Tensor, group=None) -> torch.Tensor:
     return out
 
 
-def alltoallv(send: torch.Tensor, send_counts, group=None) -> torch.Tensor:
-    """Variable-length all-to-all: ``send`` holds consecutive slices for ranks 0..R-1."""
+def alltoallv(send: torch.Tensor, send_counts, group=None, recv_counts=None) -> torch.Tensor:
+    """Variable-length all-to-all: ``send`` holds consecutive slices for ranks 0..R-1.  recv_counts: from the header
+    exchange (else one all-to-all of the counts)."""
     world = dist.get_world_size(group)
-    sc = torch.tensor(list(send_counts) + [0] * (world - len(send_counts)), dtype=torch.int64, device=send.device)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(x) for x in rc.tolist()]
+    sc = [int(x) for x in send_counts] + [0] * (world - len(send_counts))
+    if recv_counts is None:
+        sct = torch.tensor(sc, dtype=torch.int64, device=send.device)
+        rc = torch.empty_like(sct)
+        dist.all_to_all_single(rc, sct, group=group)
+        recv_counts = [int(x) for x in rc.tolist()]
     out = send.new_empty(sum(recv_counts))
-    dist.all_to_all_single(out, send, output_split_sizes=recv_counts, input_split_sizes=[int(x) for x in sc.tolist()],
-                           group=group)
+    dist.all_to_all_single(out, send, output_split_sizes=list(recv_counts), input_split_sizes=sc, group=group)
     return out
 
 
-def exchange(req: _lib.ExchangeRequest, send: torch.Tensor, group=None) -> torch.Tensor:
-    """Perform the collective ``req`` describes on ``send`` and return the result tensor."""
+def exchange(req: _lib.ExchangeRequest, send: torch.Tensor, group=None, header=None) -> torch.Tensor:
+    """Perform the collective ``req`` describes on ``send`` and return the result tensor.  header: the agreed per-rank
+    header rows (``agree``), whose counts replace the count exchanges of allgatherv / alltoallv."""
     op = req.op
     if op in (_lib.X_ALLREDUCE_SUM_U32, _lib.X_ALLREDUCE_SUM_U64):
         dist.all_reduce(send, op=dist.ReduceOp.SUM, group=group)  # two's-complement sums == unsigned sums
@@ -134,10 +145,38 @@ def exchange(req: _lib.ExchangeRequest, send: torch.Tensor, group=None) -> torch
         dist.all_reduce(send, op=dist.ReduceOp.MIN, group=group)  # values < 2^63 by contract
         return send
     if op == _lib.X_ALLGATHERV_U64:
-        return allgatherv(send, group)
+        return allgatherv(send, group, None if header is None else [h[2] for h in header])
     if op == _lib.X_ALLTOALLV_U64:
-        return alltoallv(send, req.send_counts, group)
+        me = dist.get_rank(group)
+        return alltoallv(send, req.send_counts, group, None if header is None else [h[3 + me] for h in header])
     raise ValueError(f"unknown exchange op {op}")
+
+
+class PeerFailure(RuntimeError):
+    """Another rank of the sharded run failed; this rank stops at the same collective instead of waiting in it."""
+
+
+_ST_OK, _ST_FAILED = 0, 1
+_OP_DONE = -1
+
+
+def agree(status: int, op: int, count: int, send_counts, group=None, device=None):
+    """One all-gather of (status, op, count, send counts[world]) per rank: returns every rank's header row.  Raises
+    PeerFailure when another rank reports a failure, RuntimeError when the ranks disagree on the collective (a protocol
+    bug: the collective itself would hang or mix data)."""
+    world = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    sc = [int(x) for x in (send_counts or [])][:world]
+    row = torch.tensor([status, op, count] + sc + [0] * (world - len(sc)), dtype=torch.int64, device=device)
+    allrows = torch.empty(world * (3 + world), dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(allrows, row, group=group)
+    rows = [[int(x) for x in allrows[r * (3 + world):(r + 1) * (3 + world)].tolist()] for r in range(world)]
+    failed = [r for r in range(world) if rows[r][0] != _ST_OK and r != me]
+    if failed:
+        raise PeerFailure(f"rank {me}: sharded run stopped, rank(s) {failed} failed")
+    if status == _ST_OK and any(rows[r][1] != op for r in range(world)):
+        raise RuntimeError(f"rank {me}: ranks disagree on the collective: ops {[rows[r][1] for r in range(world)]}")
+    return rows
 
 
 def exchange_device(group=None) -> torch.device:
@@ -171,30 +210,52 @@ def _send_buffer(machine, n, dtype, device):
 def run_protocol(machine, group=None, device=None):
     """Drive a shard machine to completion.  ``machine.shard_step()`` returns an ExchangeRequest;
     ``machine.shard_export(ptr)`` fills ``count`` elements at ``ptr``; ``machine.shard_import(ptr, n)``
-    takes the result.  Returns the number of collectives performed."""
+    takes the result.  Every collective is preceded by the header agreement (``agree``): a failure of this rank's step,
+    export or import is announced in the next header and re-raised here; a peer's failure raises PeerFailure.  Returns
+    the number of collectives performed."""
     device = device or exchange_device(group)
+    world = dist.get_world_size(group)
     n = 0
     sent = received = 0
     while True:
-        req = machine.shard_step()
+        try:
+            req = machine.shard_step()
+            send = None
+            if req.op != _lib.X_DONE:
+                send = _send_buffer(machine, req.count, _dtype(req.op), device)
+                machine.shard_export(send.data_ptr())
+        except Exception:
+            # this rank failed before its collective: the peers wait in (or are about to start) the next header
+            try:
+                agree(_ST_FAILED, 0, 0, None, group, device)
+            except Exception:
+                pass
+            raise
+        op = _OP_DONE if req.op == _lib.X_DONE else int(req.op)
+        sc = list(req.send_counts)[:world] if req.op == _lib.X_ALLTOALLV_U64 else None
+        header = agree(_ST_OK, op, int(req.count), sc, group, device)
         if req.op == _lib.X_DONE:
             # this rank's exchange volume (elements x element size), kept on the machine for the bench's work counters
             machine.x_stats = {"collectives": n, "bytes_sent": sent, "bytes_received": received}
             return n
-        send = _send_buffer(machine, req.count, _dtype(req.op), device)
-        machine.shard_export(send.data_ptr())
         if req.count == 0 and req.op in (_lib.X_ALLREDUCE_SUM_U32, _lib.X_ALLREDUCE_SUM_U64, _lib.X_ALLREDUCE_MIN_U64):
-            machine.shard_import(send.data_ptr(), 0)  # an all-reduce has the same count on every rank: all skip it
-            n += 1
-            continue
-        # shard_export returns once the library's stream has written `send`, so the collective (on torch's stream)
-        # may start at once; the library reads `recv` on its own stream, so torch's stream must have finished it
-        recv = exchange(req, send, group).contiguous()
-        if device.type == "cuda":
-            torch.cuda.current_stream(device).synchronize()
-        sent += send.numel() * send.element_size()
-        received += recv.numel() * recv.element_size()
-        machine.shard_import(recv.data_ptr(), recv.numel())
+            recv = send  # an all-reduce has the same count on every rank: all skip it
+        else:
+            # shard_export returns once the library's stream has written `send`, so the collective (on torch's stream)
+            # may start at once; the library reads `recv` on its own stream, so torch's stream must have finished it
+            recv = exchange(req, send, group, header).contiguous()
+            if device.type == "cuda":
+                torch.cuda.current_stream(device).synchronize()
+            sent += send.numel() * send.element_size()
+            received += recv.numel() * recv.element_size()
+        try:
+            machine.shard_import(recv.data_ptr(), recv.numel())
+        except Exception:
+            try:  # the peers are at the next step's header
+                agree(_ST_FAILED, 0, 0, None, group, device)
+            except Exception:
+                pass
+            raise
         big = max(send.numel() * send.element_size(), recv.numel() * recv.element_size()) > _BIG_EXCHANGE_BYTES
         del send, recv
         if big and device.type == "cuda":  # give the large exchange's HBM back to the library's allocations

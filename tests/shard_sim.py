@@ -2,11 +2,13 @@
 
 ``ShardSim`` answers the same ``shard_begin / shard_step / shard_export / shard_import`` calls as the HIP
 ``Context`` in sharded mode, with the same sequence of collectives and message layouts
-(rdfind_amd/distributed.py, rdfind_hip.hip sh_phase10, 16, 11-14 and 1-8), but computes each rank's part with
+(rdfind_amd/distributed.py, rdfind_hip.hip sh_phase10, 16, 18, 11-14 and 1-8), but computes each rank's part with
 the Python oracle: unary and binary (key, count) partials of the rank's slice routed to the key's owner
-(all-to-all, same key hash as shard.inl key_owner), the frequent keys all-gathered, every
-triple routed to the owners of its join values (all-to-all, two words per copy), join lines of the join
-values this rank owns, local intersections, owner-side multiplicity check, then minimality on the gathered
+(all-to-all, same key hash as shard.inl key_owner), the hot join value candidates and slice sizes all-gathered and
+turned into the same balanced owner table as sh_phase18 on every rank, the frequent keys all-gathered, every
+triple routed to the owners of its join values (all-to-all, two words per copy; join_owner: the hot table, else the
+hash), join lines of the join values this rank owns, local intersections, owner-side multiplicity check, then
+minimality on the gathered
 explicit set (every rank's unary dependents' pairs + its own binary ones).  It treats every group as light (no bitmask columns), so the class exchange is empty.
 It lets the CPU suite run the real collectives (gloo, world size 2 and 3) and check that the decomposition
 reproduces the single-process oracle result.
@@ -39,6 +41,37 @@ def mix64(x: int) -> int:
     x = (x * 0xC4CEB9FE1A85EC53) & M64
     x ^= x >> 33
     return x
+
+
+HOT_DIV, HOT_CAP = 4096, 32768  # rdfind_hip.hip sh_phase16 / sh_phase18
+
+
+def hot_owner_table(words, V: int, nranks: int, nproj: int) -> dict:
+    """rdfind_hip.hip sh_phase18: every rank's gathered hot candidates (key << 32 | count, key = pos * V + value) and
+    slice-size markers (0xffffffff << 32 | n) -> {join value: owner rank}, identical on every rank: occurrences summed
+    per value, values with >= nproj * n_total / (R * HOT_DIV) of them assigned largest first (ties: smaller value) to the
+    least loaded rank (ties: lower rank), each rank starting from its share of the hashed rest."""
+    n_total, occ = 0, {}
+    for w in words:
+        w &= M64
+        key, cnt = w >> 32, w & 0xFFFFFFFF
+        if key == 0xFFFFFFFF:
+            n_total += cnt
+            continue
+        occ[key % V] = occ.get(key % V, 0) + cnt
+    total = float(nproj * n_total)
+    thr = max(1, int(total / (float(nranks) * HOT_DIV)))
+    hot = sorted(((c, v) for v, c in occ.items() if c >= thr), key=lambda x: (-x[0], x[1]))
+    if not hot:
+        return {}
+    hot_total = float(sum(c for c, _ in hot))
+    load = [max(0.0, total - hot_total) / nranks] * nranks
+    table = {}
+    for c, v in hot:
+        r = min(range(nranks), key=lambda q: (load[q], q))
+        load[r] += c
+        table[v] = r
+    return table
 
 
 def key_owner(key: int, nranks: int) -> int:
@@ -87,6 +120,11 @@ class ShardSim:
         self.slice = self.triples if self.local_slice else self.triples[n * rank // nranks: n * (rank + 1) // nranks]
         self.phase = 10
         self.pending = None
+        self.hot = {}
+
+    def join_owner(self, v: int) -> int:
+        """common.hpp join_owner: the hot table's owner, else the hash"""
+        return self.hot.get(v, shard_of(v, self.R))
 
     # -- machine ----------------------------------------------------------------------------
     def shard_step(self):
@@ -120,11 +158,24 @@ class ShardSim:
         send = np.array([x for o in out for x in o], np.int64)
         return self._req(_lib.X_ALLTOALLV_U64, send, 16, [len(o) for o in out])
 
-    def _phase16(self):  # summed partials of the owned unary keys -> frequent keys -> all-gather
-        tot = {}
+    def _phase16(self):  # summed partials of the owned unary keys -> hot join value candidates + slice size
+        V = self.V
+        self.tot = {}
         for w in self.recv.astype(np.int64).tolist():
-            tot[w >> 32] = tot.get(w >> 32, 0) + (w & 0xFFFFFFFF)
-        return self._req(_lib.X_ALLGATHERV_U64, np.array(sorted(k for k, c in tot.items() if c >= self.ms), np.int64), 11)
+            self.tot[w >> 32] = self.tot.get(w >> 32, 0) + (w & 0xFFFFFFFF)
+        pbits = sum(1 << i for i, c in enumerate("spo") if c in self.proj)
+        nproj = bin(pbits).count("1")
+        thr = max(1, nproj * len(self.slice) // (3 * HOT_DIV))
+        cand = sorted(((c, k) for k, c in self.tot.items() if c >= thr and (pbits >> (k // V)) & 1),
+                      key=lambda x: (-x[0], x[1]))[:HOT_CAP]  # the top HOT_CAP by count (ties: smaller key)
+        words = [(0xFFFFFFFF << 32) | len(self.slice)] + [(k << 32) | c for c, k in cand]
+        return self._req(_lib.X_ALLGATHERV_U64, np.array([_i64(w) for w in words], np.int64), 18)
+
+    def _phase18(self):  # the hot join values' owners (same table on every rank); frequent unary keys -> all-gather
+        nproj = sum(1 for c in "spo" if c in self.proj)
+        self.hot = hot_owner_table(self.recv.tolist(), self.V, self.R, nproj)
+        return self._req(_lib.X_ALLGATHERV_U64,
+                         np.array(sorted(k for k, c in self.tot.items() if c >= self.ms), np.int64), 11)
 
     def _phase11(self):  # frequent unary conditions (every owner's keys); binary partials -> owners
         V = self.V
@@ -156,8 +207,8 @@ class ShardSim:
         for s, p, o in self.slice:
             dests = []
             for pos, v in (("s", s), ("p", p), ("o", o)):
-                if pos in self.proj and shard_of(v, self.R) not in dests:
-                    dests.append(shard_of(v, self.R))
+                if pos in self.proj and self.join_owner(v) not in dests:
+                    dests.append(self.join_owner(v))
             for d in dests:
                 out[d] += [(s << 32) | p, o]
         send = np.array([x for o in out for x in o], np.int64)
@@ -169,7 +220,7 @@ class ShardSim:
         lines = R.join_lines(tr, self.uf, self.bf, self.proj)
         self.local = []
         for jv, line in lines.items():
-            if shard_of(jv, self.R) == self.rank:
+            if self.join_owner(jv) == self.rank:
                 u, b = R.line_captures(line)
                 self.local.append(u | b)
         caps = set()

@@ -83,7 +83,7 @@ def test_sharded_protocol_matches_oracle(world, local_slice):
         else:
             expected = R.cind_set(R.rdfind(tr, ms, strategy, clean))
         parts = [set(res[r][k][1]) for r in range(world)]
-        assert all(res[r][k][0] == 14 for r in range(world))  # the library's fourteen collectives
+        assert all(res[r][k][0] == 15 for r in range(world))  # the library's fifteen collectives (world > 1)
         union = set().union(*parts)
         assert sum(len(p) for p in parts) == len(union)      # every dependent has one owner
         assert union == expected, (k, ms, strategy, clean)
@@ -192,3 +192,58 @@ def test_allgatherv_skewed_contributions_gloo(world):
     sizes = [6, 7, 0, 5][:world]
     want = [100 * r + i for r in range(world) for i in range(sizes[r])]
     assert all(got[r] == want for r in range(world))
+
+
+def _fail_worker(rank, world, port, q, fail_phase, where):
+    import time
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import distributed
+    from tests.shard_sim import ShardSim
+
+    class Failing(ShardSim):  # rank 1 fails in its step, export or import at one phase
+        def shard_step(self):
+            if rank == 1 and where == "step" and self.phase == fail_phase:
+                raise RuntimeError("test: step failed")
+            return super().shard_step()
+
+        def shard_import(self, ptr, n):
+            if rank == 1 and where == "import" and self.phase == fail_phase:
+                raise RuntimeError("test: import failed")
+            return super().shard_import(ptr, n)
+
+    t0 = time.perf_counter()
+    try:
+        arr = _cases(7, 1)[0][0]
+        sim = Failing(arr, 1 + max(max(t) for t in arr))
+        sim.shard_begin(rank, world, 2, "spo", True, 1)
+        distributed.run_protocol(sim)
+        q.put((rank, ("ok", time.perf_counter() - t0)))
+    except Exception as e:
+        q.put((rank, (f"{type(e).__name__}: {e}", time.perf_counter() - t0)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_phase,where", [(2, 14, "step"), (3, 5, "step"), (2, 6, "import"), (2, 8, "import")])
+def test_rank_failure_agreement_gloo(world, fail_phase, where):
+    """Cross-rank failure agreement of run_protocol (the header all-gather before each collective and at the end): a
+    rank whose step or import raises announces it in the next header; every other rank raises PeerFailure there instead
+    of waiting in a collective the failed rank never enters (import at phase 8: the last collective, caught by the final
+    DONE header)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, q, fail_phase, where)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert got[1][0].startswith("RuntimeError: test:"), got
+    for r in range(world):
+        if r != 1:
+            assert got[r][0].startswith("PeerFailure") and "[1]" in got[r][0], got
+    assert max(v[1] for v in got.values()) < 60, got

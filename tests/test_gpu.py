@@ -346,17 +346,16 @@ def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
         g.close()
 
 
-@pytest.mark.parametrize("range_records,lists,keep", [(1, 1, 1), (7, 0, 1), (300, 0, 1), (7, 1, 0), (7, 0, 0)])
-def test_join_range_groups_parity(monkeypatch, range_records, lists, keep):
+@pytest.mark.parametrize("range_records,keep", [(1, 1), (7, 1), (300, 1), (1, 0), (7, 0), (300, 0)])
+def test_join_range_groups_parity(monkeypatch, range_records, keep):
     """Capture groups built in join-value ranges (the path of inputs with >= 2^32/9 triples; RDFIND_GROUP_RANGE forces
     ranges of at most that many K3 records, a single join value's records may exceed it): every mode gives the oracle's
-    set, and the stage statistics equal the one-pass build's.  Each range's emissions read its (triple, attribute) entry
-    lists (g_range_entries), or with RDFIND_RANGE_LISTS=0 every triple.  RDFIND_RANGE_KEEP=1 (the default, up to 256
-    ranges): every range is emitted at once into its region of the kept store (k_emit_ranges), and the second pass reads
-    the first pass's sorted records instead of emitting and sorting every range again."""
+    set, and the stage statistics equal the one-pass build's.  RDFIND_RANGE_KEEP=1 (the default, up to 256 ranges):
+    every range is emitted at once into its region of the kept store (k_emit_ranges), and the second pass reads the first
+    pass's sorted records; RDFIND_RANGE_KEEP=0: every range is emitted twice, the second emission writing at the first's
+    cached block offsets (each block bounded by the next offset)."""
     ref = _lib.Context(0)
     monkeypatch.setenv("RDFIND_GROUP_RANGE", str(range_records))
-    monkeypatch.setenv("RDFIND_RANGE_LISTS", str(lists))
     monkeypatch.setenv("RDFIND_RANGE_KEEP", str(keep))
     g = _lib.Context(0)
     try:
@@ -373,10 +372,7 @@ def test_join_range_groups_parity(monkeypatch, range_records, lists, keep):
                 assert compact_matches(g, nv)
             gpu_set(ref, arr, nv, ms, 1, True)
             gpu_set(g, arr, nv, ms, 1, True)
-            # (n_sorted_records counts the records left after each emission iteration drops its repeats: entry lists
-            # group a subject's or object's records differently, so only the one-pass-equal counts are compared then)
-            keys = ("n_records", "n_frequent_records", "n_groups", "n_captures", "n_heavy_groups") + \
-                (() if lists else ("n_sorted_records",))
+            keys = ("n_records", "n_frequent_records", "n_groups", "n_captures", "n_heavy_groups", "n_sorted_records")
             assert {k: g.groups[k] for k in keys} == {k: ref.groups[k] for k in keys}
             assert (g.cind_count(), g.checksum()) == (ref.cind_count(), ref.checksum())
             if range_records == 1 and n > 50:

@@ -38,11 +38,16 @@ def _worker(rank, world, port, cases, q, local_slice=False, backend="gloo", env=
         for case in cases:
             s, p, o, nv, ms, strategy, clean = case[:7]
             use_ars = len(case) > 7 and case[7]
-            if local_slice:  # this rank holds only its slice (interleaved rows: slices need not be contiguous)
+            if local_slice == "uneven":  # rank 0 holds 10 rows, the others split the rest
+                cut = [0] + [10 + (len(s) - 10) * r // (world - 1) for r in range(world)]
+                lo, hi = cut[rank], cut[rank + 1]
+                ctx.set_triples(s[lo:hi], p[lo:hi], o[lo:hi], nv)
+            elif local_slice:  # this rank holds only its slice (interleaved rows: slices need not be contiguous)
                 ctx.set_triples(s[rank::world], p[rank::world], o[rank::world], nv)
             else:
                 ctx.set_triples(s, p, o, nv)
-            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy, local_slice=local_slice, use_ars=use_ars)
+            gs, cs = distributed.run_sharded(ctx, ms, "spo", clean, strategy, local_slice=bool(local_slice),
+                                             use_ars=use_ars)
             n = ctx.cind_count()
             rows = ctx.copy_cinds() if n <= 2_000_000 else None
             item = {"n": n, "checksum": ctx.checksum(), "rows": rows, "heavy": gs["n_heavy_groups"],
@@ -287,7 +292,8 @@ def _config_worker(rank, world, port, cfg, scale, q, env=None):
             ctx.set_triples(d.s, d.p, d.o, d.num_terms)
             del d
             gs, _ = distributed.run_sharded(ctx, 100 if cfg == "c4" else 10, local_slice=True)
-            q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum(), "ranges": gs["n_join_ranges"]}))
+            q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum(), "ranges": gs["n_join_ranges"],
+                         "kept": gs["n_ranges_kept"]}))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
     finally:
@@ -333,13 +339,18 @@ def test_sharded_c4_at_scale_vs_golden():
 
 
 @pytest.mark.timeout(300)
-def test_sharded_c4_join_ranges_vs_golden():
+@pytest.mark.parametrize("keep", [1, 0])
+def test_sharded_c4_join_ranges_vs_golden(keep):
     """A rank's join shard built in join-value ranges (sh_phase14 -> sh_phase1: the path of shards of >= 2^32/9
     received triples, e.g. c4 at 10^9 triples over 2 or 4 ranks; RDFIND_GROUP_RANGE forces it here): c4 at 0.1 over 2
-    ranks, each rank's ~2.8·10^8 records in ranges of <= 6·10^7, sums to the golden count and checksum."""
+    ranks, each rank's ~2.8·10^8 records in ranges of <= 6·10^7, sums to the golden count and checksum.  keep=1: the
+    ranges' records kept between phase 14 and phase 1 (rstore); keep=0 (RDFIND_RANGE_KEEP=0, the path when the kept
+    store does not fit): phase 1 emits every range again at the block offsets phase 14 cached -- the write whose round-5
+    fault DESIGN.md section 9 records; every block is now bounded by its cached region."""
     g = _golden("c4@0.1/s1_clean")
-    res = _run_config(2, "c4", 0.1, env={"RDFIND_GROUP_RANGE": str(60_000_000)})
+    res = _run_config(2, "c4", 0.1, env={"RDFIND_GROUP_RANGE": str(60_000_000), "RDFIND_RANGE_KEEP": str(keep)})
     assert all(res[r]["ranges"] >= 4 for r in range(2)), res
+    assert all((res[r]["kept"] > 0) == bool(keep) for r in range(2)), res
     assert sum(res[r]["n"] for r in range(2)) == g["n_cinds"]
     assert sum(res[r]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"])
 
@@ -351,3 +362,68 @@ def test_sharded_join_ranges_random(range_records):
     res = _check(2, _random_cases(400 + range_records, 24), local_slice=True,
                  env={"RDFIND_GROUP_RANGE": str(range_records)})
     assert any(res[r][k]["ranges"] > 1 for r in range(2) for k in range(24))
+
+
+def test_hot_candidates_uneven_slices_deterministic():
+    """An owner whose slice is tiny against the summed counts it owns (rank 0 holds 10 rows) submits more hot join value
+    candidates than HOT_CAP (32768): it keeps the HOT_CAP largest by (count, key), not the first to arrive, so every
+    rank's share of the result is the same from run to run, and the union equals the single-GPU result."""
+    rng = np.random.default_rng(12)
+    n, nv = 200_000, 100_000
+    s_, p_, o_ = (rng.integers(0, nv, n, dtype=np.uint32) for _ in range(3))
+    p_ %= 400
+    cases = [(s_, p_, o_, nv, 2, 1, True)] * 2
+    res = _check(2, cases, local_slice="uneven")
+    assert [res[r][0]["n"] for r in range(2)] == [res[r][1]["n"] for r in range(2)]
+    assert [res[r][0]["checksum"] for r in range(2)] == [res[r][1]["checksum"] for r in range(2)]
+
+
+def _fail_worker(rank, world, port, q, env):
+    import time
+
+    os.environ.update(env)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    from rdfind_amd import _lib, distributed, synth
+
+    t0 = time.perf_counter()
+    try:
+        d = synth.config("c1", 0.02)
+        with _lib.Context(0) as ctx:
+            ctx.set_triples(d.s[rank::world], d.p[rank::world], d.o[rank::world], d.num_terms)
+            distributed.run_sharded(ctx, d.min_support, local_slice=True)
+        q.put((rank, ("ok", time.perf_counter() - t0)))
+    except Exception as e:
+        q.put((rank, (f"{type(e).__name__}: {e}", time.perf_counter() - t0)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("phase", [14, 6])
+def test_rank_failure_ends_every_rank(phase):
+    """Cross-rank failure agreement: rank 1's rdf_shard_step fails mid-protocol (RDFIND_TEST_FAIL_SHARD test hook, an
+    RDF_ERR_OOM at phase 14 -- the group build -- or phase 6 -- the light exchange); rank 1 raises the library's error,
+    rank 0 raises PeerFailure at the same collective's header instead of waiting in it, both well under 60 s."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env = {"RDFIND_TEST_FAIL_SHARD": f"1:{phase}"}
+    procs = [ctx.Process(target=_fail_worker, args=(r, 2, port, q, env)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in procs:
+            r, item = q.get(timeout=90)
+            got[r] = item
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+    assert "RDFIND_TEST_FAIL_SHARD" in got[1][0], got
+    assert got[0][0].startswith("PeerFailure") and "rank(s) [1] failed" in got[0][0], got
+    assert max(got[0][1], got[1][1]) < 60, got
