@@ -43,12 +43,8 @@ RADIX_MAX_BITS = 9     # widest radix digit of the library's sorts (rdfind_amd/c
 
 
 def sort_passes(bits):
-    """Digit passes of a library sort of `bits` key bits (primitives.hip sort_digit_bits: 10-bit digits when that saves
-    a pass, with RDFIND_SORT10=1 only)."""
-    rs = RADIX_MAX_BITS
-    if os.environ.get("RDFIND_SORT10", "0") not in ("", "0") and -(-bits // 10) < -(-bits // rs):
-        rs = 10
-    return -(-bits // rs)
+    """Digit passes of a library sort of `bits` key bits (primitives.hip: digits of <= RS_MAX_BITS bits)."""
+    return -(-bits // RADIX_MAX_BITS)
 
 # timer family -> its kernels, whose rocprofv3 PMC traffic (profiles/pmc_<config>.json, tools/pmc.sh) is summed
 FAMILY_KERNELS = {

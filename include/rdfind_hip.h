@@ -8,7 +8,7 @@
  *                              (ALG/programs/RDFind.scala:220-237, RDFTriple ALG/data/RDFTriple.scala:7),
  *                              dictionary-encoded: one uint32 id space for s, p and o.
  *   rdf_frequent_conditions    FrequentConditionPlanner.constructFrequentConditionPlan
- *                              (ALG/plan/FrequentConditionPlanner.scala:230-319), called at
+ *                              (ALG/plan/FrequentConditionPlanner.scala:33-122), called at
  *                              ALG/programs/RDFind.scala:290-296 (--use-fis).
  *   rdf_build_capture_groups   CreateJoinPartners (RichFlatMapFunction, ALG/operators/CreateJoinPartners.scala:23-147)
  *                              -> UnionJoinCandidates (ALG/operators/UnionJoinCandidates.scala:19-44)
@@ -153,7 +153,7 @@ rdf_status rdf_copy_triples(rdf_ctx* ctx, uint32_t* s, uint32_t* p, uint32_t* o,
 
 rdf_status rdf_frequent_conditions(rdf_ctx* ctx, uint32_t min_support, rdf_fc_stats* stats);
 /* --use-ars: exact association rules between frequent conditions (FrequentConditionPlanner.findAssociationRules,
- * ALG/plan/FrequentConditionPlanner.scala:129-193).  Call between rdf_frequent_conditions and
+ * ALG/plan/FrequentConditionPlanner.scala:130-194).  Call between rdf_frequent_conditions and
  * rdf_build_capture_groups: the AR-implied binary conditions then produce no captures (CreateJoinPartners.scala:
  * 99-141), and rdf_discover_cinds leaves out the CINDs the reference does not produce with the rules
  * (CreateAllCindCandidates.scala:108-115 for strategy 0; SmallToLargeTraversalStrategy.scala:80-85 and the

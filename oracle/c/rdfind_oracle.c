@@ -10,10 +10,10 @@
  *
  * Abbreviation: ALG/ = rdfind-algorithm/src/main/scala/de/hpi/isg/sodap/rdfind/
  * Stages (each follows the cited reference code):
- *   1. unary condition counts            ALG/plan/FrequentConditionPlanner.scala:488-508
+ *   1. unary condition counts            ALG/plan/FrequentConditionPlanner.scala:291-311
  *   2. binary condition counts           ALG/operators/candidate_extraction/CreatedReducedDoubleConditionCounts.scala:45-86
  *   3. join partners (capture records)   ALG/operators/CreateJoinPartners.scala:86-147 (+ binary split,
- *                                        CreateDependencyCandidates.scala:157-186)
+ *                                        CreateDependencyCandidates.scala:90-105)
  *   4. capture groups = distinct (join, capture) grouped by join value
  *                                        ALG/operators/UnionJoinCandidates.scala:27-44, UnionCombinedJoinCandidates.scala:21-31
  *   5. AllAtOnce candidates + intersection per dependent
@@ -210,7 +210,7 @@ static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_
     int proj_p = strchr(projection, 'p') != NULL;
     int proj_o = strchr(projection, 'o') != NULL;
 
-    /* 1. unary condition counts (FrequentConditionPlanner.scala:488-508) */
+    /* 1. unary condition counts (FrequentConditionPlanner.scala:291-311) */
     uint32_t *cnt = (uint32_t *)calloc((size_t)3 * V + 1, sizeof(uint32_t));
     for (uint64_t i = 0; i < n; ++i) { cnt[s[i]]++; cnt[(uint64_t)V + p[i]]++; cnt[2ull * V + o[i]]++; }
     uint8_t *freq = (uint8_t *)calloc((size_t)V + 1, 1); /* bit0 s, bit1 p, bit2 o */
@@ -279,7 +279,7 @@ static int prep(const uint32_t *s, const uint32_t *p, const uint32_t *o, uint64_
     for (uint64_t b = 0; b < nb; ++b) *map_slot(&bidx, bkeys[b], 1) = (uint32_t)b;
 
     /* 3. join partners (CreateJoinPartners.scala:86-147), binary captures split into their unary
-     *    components as every consumer does (CreateDependencyCandidates.scala:157-186), as records
+     *    components as every consumer does (CreateDependencyCandidates.scala:90-105), as records
      *    join << capbits | capture.  Inputs whose records exceed range_records (0: no limit) are processed in ranges
      *    of join values (the reference's sort-based groupBy("joinValue") spills instead, RDFind.scala:339-345): a
      *    join value's records all fall in one range, so each range's groups are whole. */

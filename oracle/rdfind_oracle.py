@@ -327,7 +327,7 @@ def split_binary(cond: Cond):
 
 
 def line_captures(line):
-    """``CreateDependencyCandidates.flatMap`` gathering (CreateDependencyCandidates.scala:157-186):
+    """``CreateDependencyCandidates.flatMap`` gathering (CreateDependencyCandidates.scala:90-105):
     unary captures (direct + split binaries) and binary captures."""
     unary, binary = set(), set()
     for c in line:
@@ -435,7 +435,7 @@ def split_by_arity(cinds):
 
 def trivially_implied(dep: Cond, ref: Cond) -> bool:
     """Semantic triviality: ``ref`` is ``dep`` itself or a unary sub-capture of binary ``dep`` with
-    the same value (what S2L excludes: ``dep != ref`` in ExtractBinaryBinaryCindCandidates.scala:249,
+    the same value (what S2L excludes: ``dep != ref`` in ExtractBinaryBinaryCindCandidates.scala:67,
     ``!binaryCapture.implies(unaryCapture)`` in CreateBinaryUnaryCindCandidates.scala:76)."""
     if dep == ref:
         return True

@@ -1,6 +1,6 @@
 // --use-ars: exact association rules between frequent conditions (included by kernels.inl).
 //
-// FrequentConditionPlanner.findAssociationRules (ALG/plan/FrequentConditionPlanner.scala:129-193): a frequent binary
+// FrequentConditionPlanner.findAssociationRules (ALG/plan/FrequentConditionPlanner.scala:130-194): a frequent binary
 // condition (a=va, c=vc) whose triple count equals the count of its unary condition a=va yields the rule
 // a=va -> c=vc (confidence 1, the only rules kept, :186-190).  Binary keys: bt 0 = (p, o), 1 = (s, o), 2 = (s, p),
 // v1 the value at the lower position, so every key can give the rule lower -> upper and upper -> lower.

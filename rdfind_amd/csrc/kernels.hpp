@@ -59,18 +59,6 @@ static constexpr u64 LIGHT_ORDER_MIN = RDF_LIGHT_ORDER_MIN;  // light-group entr
 #define RDF_LIGHT_DENSE_BATCH 8
 #endif
 static constexpr int LIGHT_DENSE_BATCH = RDF_LIGHT_DENSE_BATCH;  // dense groups' bitmap words in flight per lane (k_light)
-#ifndef RDF_LIGHT_P2X
-#define RDF_LIGHT_P2X 0  // 1: c3 15.75 -> 16.05 ms, c4 at 0.4 49.6 -> 50.0 (profiles/r05_light_p2x_ab.log)
-#endif
-static constexpr int LIGHT_P2X = RDF_LIGHT_P2X;  // second and first extra pivot searched together (plain variant)
-#ifndef RDF_LIGHT_FEW
-#define RDF_LIGHT_FEW 0  // 2: c2 2.22 -> 2.22 ms, c3 17.0 -> 18.1, c4 at 0.4 60.2 -> 61.9 (profiles/r05_light_few_ab.log)
-#endif
-static constexpr int LIGHT_FEW = RDF_LIGHT_FEW;  // alive candidates up to which k_light searches LIGHT_IT windows at once
-#ifndef RDF_LIGHT_FEW_GROUPS
-#define RDF_LIGHT_FEW_GROUPS 1024
-#endif
-static constexpr u64 LIGHT_FEW_GROUPS = RDF_LIGHT_FEW_GROUPS;  // ... in segments of at least this many group entries
 #ifndef RDF_LIGHT_SERIAL
 #define RDF_LIGHT_SERIAL 4
 #endif

@@ -18,7 +18,7 @@ __device__ inline u64 lower_bound_u64(const u64* a, u64 n, u64 key) {
 
 // ================================================================================================
 // K1: unary condition counts  (FrequentConditionPlanner.findFrequentSingleConditions,
-//     ALG/plan/FrequentConditionPlanner.scala:488-508: flatMap 3 x (type, value, 1) -> groupBy.sum)
+//     ALG/plan/FrequentConditionPlanner.scala:291-311: flatMap 3 x (type, value, 1) -> groupBy.sum)
 // Keys are type*V + value.  Per-block LDS hash table pre-aggregates hot keys (Zipf predicates /
 // classes) so only one global atomic per distinct key per block remains; table misses go global.
 
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_external_ids(const u32* __restric
 // ================================================================================================
 // K2: binary condition counts  (CreatedReducedDoubleConditionCounts.flatMap,
 //     ALG/operators/candidate_extraction/CreatedReducedDoubleConditionCounts.scala:45-86, + groupBy.sum
-//     FrequentConditionPlanner.scala:571-591).  Only triples with >= 2 frequent values emit sp/so/po.
+//     FrequentConditionPlanner.scala:374-394).  Only triples with >= 2 frequent values emit sp/so/po.
 
 __device__ inline void freq_flags(const u32* frank, const u32* boff, u32 V, u32 s, u32 p, u32 o, bool& fs, bool& fp,
                                   bool& fo) {
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_binary_count(const u32* __restric
         if (lkey[i] != EMPTY64) global_hash_add(tkeys, tcnt, tmask, lkey[i], lcnt[i]);
 }
 
-// frequent binary conditions: filter >= minSupport (FrequentConditionPlanner.scala:587-589); *nonempty =
+// frequent binary conditions: filter >= minSupport (FrequentConditionPlanner.scala:390-392); *nonempty =
 // number of distinct binary keys (stats)
 __global__ __launch_bounds__(RDF_BLOCK) void k_bin_freq_flags(const u64* __restrict__ tkeys, const u32* __restrict__ tcnt,
                                                               u64 cap, u32 ms, u32* flags, u64* nonempty) {
@@ -416,7 +416,7 @@ __device__ inline void bin_lookup3(const u64* __restrict__ lkeys, const u32* __r
 // K3: join partners  (CreateJoinPartners.flatMap, ALG/operators/CreateJoinPartners.scala:86-147)
 // Per triple and projection: unary captures of the frequent condition values and, when the binary
 // condition is frequent, the binary capture.  Binary captures are emitted together with both unary
-// components, which is what every consumer reconstructs (CreateDependencyCandidates.scala:157-186,
+// components, which is what every consumer reconstructs (CreateDependencyCandidates.scala:90-105,
 // splitAndCollectUnaryCaptures).  Record = capture << joinbits | join: sorted, a capture's records are
 // contiguous, so its support is a run length (no atomics) and its join list is the dependent -> groups CSR.
 
@@ -2039,31 +2039,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // second pivot is not verified here; its survivors go out tagged (item seg 0) and pass B verifies them compacted
     const bool multi = v.prefilter && itemoff[d + 1] - itemoff[d] > nseg;
     LSTAT_TIC();
-    int k_px = 0;  // extra pivots already checked
-    // RDF_LIGHT_P2X: the second pivot and the first extra pivot searched at once (two chains per lane) when both are
-    // groups the lanes search in global memory (dense rows or > LIGHT_LDS members), instead of one after the other
-    bool p2_done_here = false;
-    if (LIGHT_P2X && pxs && p2 != NONE32 && alive && !v.p2done) {
-        const u32 pk0 = pxs[0];
-        if (pk0 != NONE32) {
-            const u64 gb2 = v.goff[p2], ge2 = v.goff[p2 + 1], gb3 = v.goff[pk0], ge3 = v.goff[pk0 + 1];
-            const u32 *d2 = dense_row(v, p2), *d3 = dense_row(v, pk0);
-            if ((d2 || ge2 - gb2 > LIGHT_LDS) && (d3 || ge3 - gb3 > LIGHT_LDS)) {
-                const bool mine = (alive >> lane) & 1ull;
-                const u32* ga[2] = {v.gcap + gb2, v.gcap + gb3};
-                const u64 gn[2] = {mine && !d2 ? ge2 - gb2 : 0, mine && !d3 ? ge3 - gb3 : 0};
-                const u32 w2 = mine && d2 ? d2[cand >> 5] : ~0u, w3 = mine && d3 ? d3[cand >> 5] : ~0u;
-                bool f[2];
-                multi_search<2>(ga, gn, cand, f);
-                const bool ok = !mine || ((d2 ? ((w2 >> (cand & 31)) & 1u) != 0 : f[0]) &&
-                                          (d3 ? ((w3 >> (cand & 31)) & 1u) != 0 : f[1]));
-                alive &= __ballot(ok);
-                p2_done_here = true;
-                k_px = 1;
-            }
-        }
-    }
-    if (!p2_done_here && p2 != NONE32 && alive && !v.p2done) {
+    if (p2 != NONE32 && alive && !v.p2done) {
         const u64 gb2 = v.goff[p2];
         alive = check_group(v, gb2, (u32)(v.goff[p2 + 1] - gb2), cand, alive, s_light[threadIdx.x / RDF_WAVE],
                             dense_row(v, p2));
@@ -2072,7 +2048,7 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     // window's searches (c3: half of the light cycles), one targeted check each (lanes over candidates) before it
     if (pxs && !v.p2done) {
 #pragma unroll 1
-        for (int k = k_px; k < v.npx && alive; ++k) {
+        for (int k = 0; k < v.npx && alive; ++k) {
             const u32 pk = pxs[k];
             if (pk == NONE32) break;  // ascending: no more light groups
             const u64 gb3 = v.goff[pk];
@@ -2119,35 +2095,6 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
         { u32 x = gszv[0] + (u32)gbv[0]; asm volatile("" : : "v"(x)); }  // stats: the metadata loads have arrived
 #endif
         LSTAT_TOC(1);
-        // Few candidates left (a dependent with a small pivot and many groups: c2's multi-segment items, 28 % of the
-        // light cycles): one candidate at a time, each lane searching all LIGHT_IT of its groups at once, so a level of
-        // the LIGHT_IT windows' searches is one round trip instead of one per window.  Off (RDF_LIGHT_FEW 0): measured
-        // no faster on c2 and slower on c3 / c4 than the windows' own paths (LDS-staged rows, serial groups)
-        if (LIGHT_FEW && e - b >= LIGHT_FEW_GROUPS && __popcll(alive) <= LIGHT_FEW) {
-            if (nseg > 1 && s0 != b)
-                alive &= ~__hip_atomic_load(&dead[choff[d] + chunk * 8 - ob], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            u64 todo = alive;
-            while (todo) {
-                const int l = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                const u32 key = __shfl(cand, l, RDF_WAVE);
-                const u32* ga[LIGHT_IT];
-                u64 gn[LIGHT_IT];
-#pragma unroll
-                for (int it = 0; it < LIGHT_IT; ++it) {
-                    ga[it] = v.gcap + gbv[it];
-                    gn[it] = gg[it] != NONE32 && !gdr[it] ? gszv[it] : 0;
-                }
-                bool f[LIGHT_IT];
-                multi_search<LIGHT_IT>(ga, gn, key, f);
-                bool ok = true;
-#pragma unroll
-                for (int it = 0; it < LIGHT_IT; ++it)
-                    ok = ok && (gg[it] == NONE32 || (gdr[it] ? dense_has(gdr[it], key) : f[it]));
-                if (!__all(ok)) alive &= ~(1ull << l);
-            }
-            continue;
-        }
 #pragma unroll
         for (int it = 0; it < LIGHT_IT; ++it) {
             if (s0 + (u64)it * RDF_WAVE >= e) break;
@@ -2317,27 +2264,13 @@ __device__ inline void k_light_body(u64 vblk, CindView v, const u32* __restrict_
     u64 nvblk, CindView v, const u32 *__restrict__ pivot, const u64 *__restrict__ itemoff,                               \
         const u32 *__restrict__ item_dep, const u64 *__restrict__ choff, u64 w0, u64 W, u64 ob, u64 *dead, u64 *slots,  \
         u32 *counts, const u32 *__restrict__ order
-// RDF_LIGHT_XCD = K: runs of K consecutive virtual blocks (4 K consecutive work items in issue order) on one XCD
-// (virtual block vb runs on XCD vb % 8: the grid is all virtual blocks, or 2^20), so the items of one dependent,
-// which read the same group entries, meet in one L2; the runs keep the issue order at 8 K blocks.  0: off (K = 8 / 32
-// measured slower: c2 light 2.02 -> 2.07 / 2.08 ms, c3 and c4 unchanged; profiles/r05_light_xcd_ab.log)
-#ifndef RDF_LIGHT_XCD
-#define RDF_LIGHT_XCD 0
-#endif
-__device__ inline u64 light_vb(u64 vb, u64 nv) {
-    if (!RDF_LIGHT_XCD) return vb;
-    constexpr u64 K = RDF_LIGHT_XCD, C = 8 * K;
-    const u64 c = vb / C;
-    if ((c + 1) * C > nv) return vb;  // the last partial run: as issued
-    return c * C + (vb % 8) * K + (vb / 8) % K;
-}
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_STAGE_ATTR void k_light_stage(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<true>(light_vb(vb, nvblk), v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
+        k_light_body<true>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 __global__ __launch_bounds__(RDF_BLOCK) RDF_LIGHT_PLAIN_ATTR void k_light_plain(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<false>(light_vb(vb, nvblk), v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
+        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 // Work items in issue order, the items of dependents with >= thr light-group entries (many windows: c2's 6 % of
 // items that hold 45 % of the cycles) first: blocks are dispatched in index order, and a 10^6-cycle item issued near
@@ -2360,7 +2293,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_light_order(const u32* __restrict
 // searches and sweeps are latency-bound, more waves hide more of it), chosen by LIGHT_HIOCC_AVG
 __global__ __launch_bounds__(RDF_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_light_plain_hi(RDF_LIGHT_ARGS) {
     for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_light_body<false>(light_vb(vb, nvblk), v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
+        k_light_body<false>(vb, v, pivot, itemoff, item_dep, choff, w0, W, ob, dead, slots, counts, order);
 }
 
 
@@ -3230,231 +3163,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_clear_bits(u64* words, u64 n, u64
 }
 
 // verify pass plan: candidates = the verify pairs of d, groups = all local light groups of d (no pivot skipped)
-// ---- light pass B, group-major (IntersectCindCandidates.scala:40-43: a ref survives iff it is in every group of the
-// dependent).  Pass B's candidate-major verification searches every surviving candidate in every light group of its
-// dependent: (survivors x groups x log2 n) divergent loads.  For a dependent with many survivors that are mostly true
-// refs (c4: 1,570 survivors of a 2,229-member pivot through ~800 light groups of ~8k members) one coalesced sweep of each
-// light group's members, marking the candidates it holds (an LDS hash of the dependent's survivors), reads ~Σ n_g words
-// instead.  k_gm_select picks, per dependent, the cheaper of the two by their estimated lines read; k_light_gm verifies
-// the chosen ones, one block per (dependent, chunk of <= GM_CAND survivors, segment of GM_SEG group entries), and flags
-// the survivors some light group lacks (gdead, one byte per survivor of vpairs).
-static constexpr u32 GM_CAND = 4096;   // survivors per block (LDS: hash keys 32 KB + indices 16 KB + bitmaps)
-static constexpr u32 GM_HASH = 8192;   // LDS hash slots (load <= 1/2)
-static constexpr u64 GM_SEG = 256;     // group entries of the dependent per block (64 per wave)
-static constexpr u32 GM_MIN_SURV = 16; // fewer survivors: candidate-major always
-
-__device__ inline u32 gm_hash(u32 x) { return hash32(x) & (GM_HASH - 1); }
-
-// per dependent with pass-B survivors: light groups, their members, the survivors -> gm (1: group-major), its k_light_gm
-// items, and the candidate-major plan of the group-major dependents cleared (one wave per dependent)
-__device__ inline void k_gm_select_body(u64 vblk, CindView v, const u32* __restrict__ pivot, int mode, u32* gm,
-                                        u32* gmitems, u32* nchunk_light, u32* nitem_light, u32* npacked) {
-    const u64 w = (u64)vblk * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
-    if (w >= v.C) return;
-    const u32 d = (u32)w;
-    const int lane = lane_id();
-    const u64 S = v.vcoff[d + 1] - v.vcoff[d];
-    const u64 b = v.doff[d], e = v.doff[d + 1];
-    bool pick = false;
-    if (mode && S >= (mode == 2 ? 1u : GM_MIN_SURV) && e > b) {
-        const u32 piv = pivot[d], p2 = v.piv2 ? v.piv2[d] : NONE32;
-        u64 m = 0, sum = 0, lg = 0;
-        for (u64 j = b + lane; j < e; j += RDF_WAVE) {
-            const u32 g = v.dgrp[j];
-            if ((g & DGRP_HEAVY) || g == piv || g == p2) continue;
-            const u32 n = v.ginfo[g] & ~GINFO_HEAVY;
-            ++m;
-            sum += n;
-            lg += n > 1 ? 32 - __clz(n - 1) : 1;  // search levels
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            m += __shfl_xor(m, off, RDF_WAVE);
-            sum += __shfl_xor(sum, off, RDF_WAVE);
-            lg += __shfl_xor(lg, off, RDF_WAVE);
-        }
-        // lines read: candidate-major ~ one 64-B sector per search level per (survivor, group); group-major ~ the
-        // members (16 per sector) + two 64-lane bound probes per group
-        const u64 cm = S * lg, gmc = sum / 16 + 2 * RDF_WAVE * m;
-        pick = m && (mode == 2 || gmc < cm);
-    }
-    if (lane == 0) {
-        gm[d] = pick ? 1u : 0u;
-        gmitems[d] = pick ? (u32)(((S + GM_CAND - 1) / GM_CAND) * ((e - b + GM_SEG - 1) / GM_SEG)) : 0u;
-        if (pick) nchunk_light[d] = nitem_light[d] = npacked[d] = 0;
-    }
-}
-__global__ __launch_bounds__(RDF_BLOCK) void k_gm_select(u64 nvblk, CindView v, const u32* __restrict__ pivot, int mode,
-                                                         u32* gm, u32* gmitems, u32* nchunk_light, u32* nitem_light,
-                                                         u32* npacked) {
-    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x)
-        k_gm_select_body(vb, v, pivot, mode, gm, gmitems, nchunk_light, nitem_light, npacked);
-}
-
-// lower_bound(lo_key) and upper_bound(hi_key) in the sorted a[0, n) by 64-ary probes: per level every lane loads one of
-// 64 splitters of the remaining interval (both bounds from one pair of ballots), so ~8k members take three levels instead
-// of thirteen dependent steps of a binary search; the last interval of <= 64 members is read whole
-__device__ inline u64 gm_pos(u64 b, u64 len, int l) { return b + (len * (u64)(l + 1)) / 65; }
-__device__ inline void gm_bounds(const u32* __restrict__ a, u64 n, u32 lo_key, u32 hi_key, u64* lo, u64* hi) {
-    const int lane = lane_id();
-    u64 b0 = 0, e0 = n, b1 = 0, e1 = n;  // the bound lies in [b, e]
-    bool done0 = false, done1 = false;
-    while (!(done0 && done1)) {
-        const u64 l0 = e0 - b0, l1 = e1 - b1;
-        bool t0 = false, t1 = false;
-        if (!done0) t0 = l0 <= RDF_WAVE ? ((u64)lane < l0 && a[b0 + lane] < lo_key) : a[gm_pos(b0, l0, lane)] < lo_key;
-        if (!done1) t1 = l1 <= RDF_WAVE ? ((u64)lane < l1 && a[b1 + lane] <= hi_key) : a[gm_pos(b1, l1, lane)] <= hi_key;
-        const int k0 = __popcll(__ballot(t0)), k1 = __popcll(__ballot(t1));  // splitters below the key (a prefix)
-        if (!done0) {
-            if (l0 <= RDF_WAVE) {
-                b0 += k0;
-                done0 = true;
-            } else {
-                const u64 nb = k0 ? gm_pos(b0, l0, k0 - 1) + 1 : b0;
-                e0 = k0 < RDF_WAVE ? gm_pos(b0, l0, k0) : e0;
-                b0 = nb;
-            }
-        }
-        if (!done1) {
-            if (l1 <= RDF_WAVE) {
-                b1 += k1;
-                done1 = true;
-            } else {
-                const u64 nb = k1 ? gm_pos(b1, l1, k1 - 1) + 1 : b1;
-                e1 = k1 < RDF_WAVE ? gm_pos(b1, l1, k1) : e1;
-                b1 = nb;
-            }
-        }
-    }
-    *lo = b0;
-    *hi = b1 > b0 ? b1 : b0;
-}
-
-__device__ inline void k_light_gm_body(u64 vblk, CindView v, const u32* __restrict__ pivot, const u64* __restrict__ itemoff,
-                                       const u32* __restrict__ item_dep, u64 W, uint8_t* gdead, u32* s_key,
-                                       uint16_t* s_idx, u32* s_alive, u32* s_found) {
-    if (vblk >= W) return;
-    const u32 d = item_dep[vblk];
-    const u64 b0 = v.doff[d], e0 = v.doff[d + 1];
-    const u64 nseg = (e0 - b0 + GM_SEG - 1) / GM_SEG;
-    const u64 item = vblk - itemoff[d];
-    const u64 q = item / nseg, seg = item % nseg;
-    const u64 c0 = v.vcoff[d] + q * GM_CAND;
-    const u64 c1 = c0 + GM_CAND < v.vcoff[d + 1] ? c0 + GM_CAND : v.vcoff[d + 1];
-    const u32 S = (u32)(c1 - c0);
-    const u32 NW = (S + 31) / 32;
-    const int lane = lane_id(), wv = threadIdx.x / RDF_WAVE;
-    u32* found = s_found + wv * (GM_CAND / 32);
-    for (u32 k = threadIdx.x; k < GM_HASH; k += RDF_BLOCK) s_key[k] = EMPTY32;
-    for (u32 k = threadIdx.x; k < GM_CAND / 32; k += RDF_BLOCK) s_alive[k] = k < NW ? (k + 1 < NW || !(S & 31) ? ~0u : (1u << (S & 31)) - 1u) : 0u;
-    for (u32 k = threadIdx.x; k < RDF_WAVES_PER_BLOCK * (GM_CAND / 32); k += RDF_BLOCK) s_found[k] = 0;
-    __syncthreads();
-    for (u32 k = threadIdx.x; k < S; k += RDF_BLOCK) {
-        const u32 x = (u32)v.vpairs[c0 + k];
-        u32 h = gm_hash(x);
-        while (atomicCAS(&s_key[h], EMPTY32, x) != EMPTY32) h = (h + 1) & (GM_HASH - 1);
-        s_idx[h] = (uint16_t)k;
-    }
-    __syncthreads();
-    const u32 cmin = (u32)v.vpairs[c0], cmax = (u32)v.vpairs[c1 - 1];  // the survivors ascend
-    const u32 piv = pivot[d], p2 = v.piv2 ? v.piv2[d] : NONE32;
-    const u64 jb = b0 + seg * GM_SEG, je = jb + GM_SEG < e0 ? jb + GM_SEG : e0;
-    for (u64 j = jb + wv; j < je; j += RDF_WAVES_PER_BLOCK) {
-        const u32 g = v.dgrp[j];
-        if ((g & DGRP_HEAVY) || g == piv || g == p2) continue;
-        // anything left to verify?  (other waves clear bits concurrently: a stale word only costs a sweep)
-        bool any = false;
-        for (u32 k = lane; k < NW; k += RDF_WAVE) any |= s_alive[k] != 0;
-        if (!__any(any)) break;
-        const u32* dr = dense_row(v, g);
-        if (dr) {  // dense group: one bitmap word per alive candidate (lanes over candidates)
-            for (u32 k = lane; k < S; k += RDF_WAVE) {
-                const u32 bit = 1u << (k & 31);
-                if ((s_alive[k >> 5] & bit) && !dense_has(dr, (u32)v.vpairs[c0 + k])) atomicAnd(&s_alive[k >> 5], ~bit);
-            }
-            continue;
-        }
-        const u64 gb = v.goff[g], n = v.goff[g + 1] - gb;
-        u64 lo, hi;
-        gm_bounds(v.gcap + gb, n, cmin, cmax, &lo, &hi);
-        // sweep the members in [cmin, cmax]: 4 coalesced loads in flight per lane, each member looked up in the hash
-        for (u64 i0 = gb + lo; i0 < gb + hi; i0 += 4 * RDF_WAVE) {
-            u32 x[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const u64 i = i0 + (u64)t * RDF_WAVE + lane;
-                x[t] = i < gb + hi ? v.gcap[i] : EMPTY32;
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (x[t] == EMPTY32) continue;
-                u32 h = gm_hash(x[t]);
-                for (;;) {
-                    const u32 k = s_key[h];
-                    if (k == x[t]) {
-                        const u32 idx = s_idx[h];
-                        atomicOr(&found[idx >> 5], 1u << (idx & 31));
-                        break;
-                    }
-                    if (k == EMPTY32) break;
-                    h = (h + 1) & (GM_HASH - 1);
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (u32 k = lane; k < NW; k += RDF_WAVE) {
-            const u32 f = found[k];
-            if (~f & s_alive[k]) atomicAnd(&s_alive[k], f);
-            found[k] = 0;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    __syncthreads();
-    for (u32 k = threadIdx.x; k < S; k += RDF_BLOCK)
-        if (!((s_alive[k >> 5] >> (k & 31)) & 1u)) gdead[c0 + k] = 1;  // several segments may write the same 1
-}
-__global__ __launch_bounds__(RDF_BLOCK) void k_light_gm(u64 nvblk, CindView v, const u32* __restrict__ pivot,
-                                                        const u64* __restrict__ itemoff, const u32* __restrict__ item_dep,
-                                                        u64 W, uint8_t* gdead) {
-    __shared__ u32 s_key[GM_HASH];
-    __shared__ uint16_t s_idx[GM_HASH];
-    __shared__ u32 s_alive[GM_CAND / 32];
-    __shared__ u32 s_found[RDF_WAVES_PER_BLOCK * (GM_CAND / 32)];
-    for (u64 vb = blockIdx.x; vb < nvblk; vb += gridDim.x) {
-        k_light_gm_body(vb, v, pivot, itemoff, item_dep, W, gdead, s_key, s_idx, s_alive, s_found);
-        __syncthreads();  // the block's LDS is reused by its next item
-    }
-}
-
-// pass A's tagged slots after pass B: candidate-major dependents keep the pairs pass B verified (bpairs / boff), group-
-// major ones the survivors k_light_gm did not flag (vpairs / voff / gdead)
-__global__ __launch_bounds__(RDF_BLOCK) void k_tag_fix_gm(u64* slots, u32* counts, const u32* __restrict__ flags, u64 W,
-                                                          const u64* __restrict__ bpairs, const u64* __restrict__ boff,
-                                                          const u32* __restrict__ gm, const u64* __restrict__ vpairs,
-                                                          const u64* __restrict__ voff, const uint8_t* __restrict__ gdead) {
-    for (u64 o = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; o < W; o += (u64)gridDim.x * RDF_BLOCK) {
-        const u32 n = flags[o];
-        if (!n) continue;
-        u32 k = 0;
-        for (u32 j = 0; j < n; ++j) {
-            const u64 x = slots[o * 8 + j] & ~(u64)PRE_TAG;
-            const u64 d = x >> 32;
-            bool keep;
-            if (gm[d]) {
-                const u64 p = lower_bound_u64(vpairs + voff[d], voff[d + 1] - voff[d], x);
-                keep = !gdead[voff[d] + p];
-            } else {
-                keep = bsearch_u64(bpairs + boff[d], boff[d + 1] - boff[d], x);
-            }
-            if (keep) slots[o * 8 + k++] = x;
-        }
-        counts[o] = k;
-    }
-}
 
 __global__ __launch_bounds__(RDF_BLOCK) void k_verify_plan(CindView v, const u32* __restrict__ nlight_in, u32* nchunk_light,
                                                            u32* nitem_light, u32* npacked) {

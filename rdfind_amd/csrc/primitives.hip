@@ -149,106 +149,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* in, TO* out,
 static constexpr u64 SCAN_SMALL_TILES = 4;  // one 1024-thread block up to 8 or 32 tiles measured no faster (c1 groups 0.23 -> 0.39 ms at 32;
                                            // profiles/r05_scan_small_ab.log)
 
-// Single-pass exclusive scan (chained, decoupled look-back): one launch reads the input once.  Tiles take their ids
-// from a counter in launch order, publish their aggregate at once, then wave 0 looks back over the 64 nearest
-// predecessors per step (one state word per lane) until it meets an inclusive prefix, and publishes its own.  A tile
-// waits only on tiles that took their ids earlier, so every word it waits for is written by a running or finished
-// block.  State word: flag (63..62: 1 aggregate, 2 inclusive) | the call's epoch (61..48) | value (47..0); the word is
-// the whole hand-off (value and flag in one 8-B relaxed agent-scope store / load: MI355X_MICROARCH.md, R2 granule).
-// Values (partial sums) must stay below 2^48.
-static constexpr u64 CS_VAL = (1ull << 48) - 1;
-static constexpr u64 CS_AGG = 1ull << 62, CS_INC = 2ull << 62;
-static constexpr unsigned CS_EPOCHS = 1u << 14;
-
-template <typename T>
-__device__ inline T wave_sum_t(T v) {
-#pragma unroll
-    for (int off = RDF_WAVE / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off, RDF_WAVE);
-    return v;
-}
-
-template <typename TI, typename TO>
-__global__ __launch_bounds__(RDF_BLOCK) void k_scan_chained(const TI* in, TO* out, u64 n, u64* state, u32 epoch,
-                                                            TO* __restrict__ grand_total) {
-    __shared__ TO lds[SCAN_TILE];
-    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
-    __shared__ u32 s_tile;
-    __shared__ TO s_prefix;
-    u32* ctr = (u32*)state;  // state[0]: the tile counter; tile t's word is state[1 + t]
-    if (threadIdx.x == 0) s_tile = atomicAdd(ctr, 1u);
-    __syncthreads();
-    const u32 tile = s_tile;
-    const u64 base = (u64)tile * SCAN_TILE;
-#pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
-        lds[i * RDF_BLOCK + threadIdx.x] = (idx < n) ? (TO)in[idx] : (TO)0;
-    }
-    __syncthreads();
-    TO v[SCAN_ITEMS];
-    TO local = 0;
-#pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        v[i] = lds[threadIdx.x * SCAN_ITEMS + i];
-        local += v[i];
-    }
-    TO agg;
-    TO off = block_exclusive_scan<TO>(local, lds_wave, &agg);
-    const u64 tag = (u64)epoch << 48;
-    if (threadIdx.x == 0)
-        __hip_atomic_store(&state[1 + tile], (tile ? CS_AGG : CS_INC) | tag | ((u64)agg & CS_VAL), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (tile && threadIdx.x < RDF_WAVE) {
-        const int lane = threadIdx.x;
-        long long t = (long long)tile - 1;
-        TO acc = 0;
-        for (;;) {
-            const long long q = t - lane;
-            u64 w = 0;
-            if (q >= 0) {
-                do {
-                    w = __hip_atomic_load(&state[1 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } while ((w >> 62) == 0 || ((w >> 48) & (CS_EPOCHS - 1)) != epoch);
-            }
-            const u64 incm = __ballot(q >= 0 && (w >> 62) == 2);
-            const int stop = incm ? __ffsll((long long)incm) - 1 : RDF_WAVE;  // nearest inclusive predecessor
-            acc += wave_sum_t<TO>((q >= 0 && lane <= stop) ? (TO)(w & CS_VAL) : (TO)0);
-            if (incm) break;  // tile 0 publishes an inclusive word, so every look-back ends
-            t -= RDF_WAVE;
-        }
-        if (lane == 0) {
-            __hip_atomic_store(&state[1 + tile], CS_INC | tag | (((u64)acc + (u64)agg) & CS_VAL), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            s_prefix = acc;
-        }
-    }
-    __syncthreads();
-    const TO prefix = tile ? s_prefix : (TO)0;
-    off += prefix;
-#pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        lds[threadIdx.x * SCAN_ITEMS + i] = off;
-        off += v[i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
-        if (idx < n) out[idx] = lds[i * RDF_BLOCK + threadIdx.x];
-    }
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) {  // the last id handed out: every block has taken its id
-        if (grand_total) *grand_total = prefix + agg;
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// RDFIND_SCAN=1: the chained scan above instead of reduce-then-scan (off by default: on c2 the step's scans took
-// ~0.2 ms longer with it, record sort 1.93 -> 2.00 ms, groups 1.33 -> 1.40; profiles/r05_scan_ab.log)
-static bool chained_scans() {
-    static const bool on = getenv("RDFIND_SCAN") && atoi(getenv("RDFIND_SCAN")) == 1;
-    return on;
-}
-
 template <typename TI, typename TO>
 static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 n, TO* d_total, hipStream_t st) {
     if (n == 0) {
@@ -258,18 +158,6 @@ static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 
     u64 tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (tiles <= SCAN_SMALL_TILES) {
         hipLaunchKernelGGL((k_scan_small<TI, TO>), dim3(1), dim3(RDF_BLOCK), 0, st, in, out, n, d_total);
-        return hipGetLastError();
-    }
-    if (chained_scans()) {
-        const size_t need = (tiles + 1) * sizeof(u64);
-        if (ws.cs_state.cap < need || ++ws.cs_epoch >= CS_EPOCHS) {  // fresh words: zero them, restart the epochs
-            if (ws.cs_state.ensure(need) != hipSuccess) return hipErrorOutOfMemory;
-            const hipError_t e = hipMemsetAsync(ws.cs_state.p, 0, ws.cs_state.cap, st);
-            if (e != hipSuccess) return e;
-            ws.cs_epoch = 1;
-        }
-        hipLaunchKernelGGL((k_scan_chained<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n,
-                           ws.cs_state.as<u64>(), (u32)ws.cs_epoch, d_total);
         return hipGetLastError();
     }
     TO* sums = (TO*)ws.scratch(tiles * sizeof(TO), 0);
@@ -493,14 +381,11 @@ static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, in
     return hipSuccess;
 }
 
-// Widest digit of a sort of `bits` bits: RS_MAX_BITS; with RDFIND_SORT10=1, 10 when that saves a whole pass (measured
-// slower: c4 at 10^9 triples sorts its 50-bit records in 5 passes of 10 bits in 362 ms against 234 ms for 6 passes of
-// <= 9 bits, c3 21.8 vs 19.0 ms: 1,024 bins leave ~4 keys per bin of a 4096-key tile; profiles/r05_sort10_ab.log)
+// Widest digit of a sort: RS_MAX_BITS (9).  10-bit digits saving a pass measured slower (c4 at 10^9 triples sorts its
+// 50-bit records in 5 passes of 10 bits in 362 ms against 234 ms for 6 passes of <= 9 bits, c3 21.8 vs 19.0 ms: 1,024
+// bins leave ~4 keys per bin of a 4096-key tile; profiles/r05_sort10_ab.log)
 static hipError_t radix_sort_dmax(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, int dmax, hipStream_t st);
-static int sort_digit_bits(int bits) {
-    static const bool ten = getenv("RDFIND_SORT10") && atoi(getenv("RDFIND_SORT10")) != 0;
-    return ten && RS_MAX_BITS < 10 && (bits + 9) / 10 < (bits + RS_MAX_BITS - 1) / RS_MAX_BITS ? 10 : RS_MAX_BITS;
-}
+static int sort_digit_bits(int) { return RS_MAX_BITS; }
 
 int radix_sort_passes(int bits) {
     const int d = sort_digit_bits(bits);

@@ -62,10 +62,6 @@ struct DevBuf {
 struct Workspace {
     static constexpr int kSlots = 8;
     DevBuf slot[kSlots];
-    // single-pass (chained) scans: tile counter + one state word per tile, tagged with the call's epoch so that the
-    // words never need clearing between calls (zeroed when the buffer grows or the 14-bit epoch wraps)
-    DevBuf cs_state;
-    unsigned cs_epoch = 0;
     void* scratch(size_t bytes, int s) {
         if (s < 0 || s >= kSlots) return nullptr;
         if (slot[s].ensure(bytes) != hipSuccess) return nullptr;
@@ -73,11 +69,9 @@ struct Workspace {
     }
     void release() {
         for (auto& b : slot) b.release();
-        cs_state.release();
-        cs_epoch = 0;
     }
     size_t bytes() const {
-        size_t t = cs_state.cap;
+        size_t t = 0;
         for (const auto& b : slot) t += b.cap;
         return t;
     }

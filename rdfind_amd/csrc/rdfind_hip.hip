@@ -115,11 +115,10 @@ struct rdf_ctx {
     int pivx_kept = 0;  // extra pivots the pivot pass computed this run (PIV_EXTRA_PLAIN or PIV_EXTRA)
     int light_npx = 0;  // ... and how many k_light checks
     DevBuf gdrow, dlist, dbits;  // dense light groups: group -> bitmap row, row -> group, the bitmaps
-    u32* dbits_p = nullptr;      // the bitmaps in use: dbits, or the idle kept store (rstore_lent)
+    u32* dbits_p = nullptr;      // the bitmaps in use (dbits)
     DevBuf iflag, iexcl, iorder; // k_light's issue order (k_light_long_flags / k_light_order)
     hipStream_t side = nullptr;  // k_light_packed beside k_light (their slots are disjoint), joined before the compaction
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool rstore_lent = false;    // rstore holds the discovery's dense bitmaps (not reclaimable) until the next build
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
     int dense_div = -1;                   // RDFIND_DENSE (0: no bitmaps; -1: by input, d_dense_flags)
@@ -168,8 +167,6 @@ struct rdf_ctx {
     DevBuf lmask, hrep, vpairs, vcoff, vpiv;  // holder-first light exchange (sh_phase5 / sh_phase15)
     DevBuf ebown, segb, sege, seglen;         // this rank's binary dependents' final pairs; dependent segments
     DevBuf bslots, bcounts;                   // light pass B's output slots (pass A's stay in epairs_tmp / lslot)
-    DevBuf gmflag, gmitems, gmioff, gmdep, gdead, voff2;  // light pass B, group-major (k_gm_select / k_light_gm)
-    u64 n_gm_deps = 0, n_gm_items = 0;
     DevBuf ukeys, ukeys_tmp;                  // sharded: frequent unary keys (owned, then every rank's, sorted)
     // sharded ingest (rdf_shard_parse_begin): local terms routed to their owners, the owner's dictionary, global ids
     DevBuf ithv, ikeys, ikeys_tmp, iwords, iwoff, ihdr, ipay, ibnd, iwb, rhdr, rlen, rwords, rwoff, rts, rhv, rvalid, rtab,
@@ -262,7 +259,7 @@ static bool reclaim_spare(rdf_ctx* c, const DevBuf* keep) {
     for (int k = 0; k < 3; ++k) {
         if (!(k == 0 ? c->spare_fc : k == 1 ? c->spare_groups : c->spare_x)) continue;
         for (DevBuf* b : (k == 0 ? fc_scratch : k == 1 ? grp_scratch : x_scratch)) {
-            if (b == keep || !b->p || (b == &c->rstore && c->rstore_lent)) continue;
+            if (b == keep || !b->p) continue;
             if (!any) (void)hipStreamSynchronize(c->stream);  // queued kernels may still read them
             b->release();
             any = true;
@@ -426,7 +423,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
                       &c->fbits, &c->brkeys, &c->xsend, &c->xrecv, &c->gbest, &c->nrl, &c->smask, &c->smask_tmp, &c->cpairs, &c->cpairs_tmp,
                       &c->obounds, &c->lmask, &c->hrep, &c->vpairs, &c->vcoff, &c->vpiv, &c->runoff, &c->rundep, &c->dheap, &c->dtoff, &c->cslen, &c->csoff,
                       &c->cstr, &c->flen, &c->floff, &c->fbuf, &c->drows, &c->ppart, &c->wts, &c->wtp,
-            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->bslots, &c->bcounts, &c->gmflag, &c->gmitems, &c->gmioff, &c->gmdep, &c->gdead, &c->voff2, &c->segb, &c->sege, &c->seglen, &c->ukeys,
+            &c->wto, &c->arcnt, &c->ar_bits, &c->ar_rules, &c->arref, &c->loff, &c->gdrow, &c->dlist, &c->dbits, &c->ebown, &c->bslots, &c->bcounts, &c->segb, &c->sege, &c->seglen, &c->ukeys,
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
@@ -434,7 +431,7 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
 }
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
-static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "gmflag", "gmitems", "gmioff", "gmdep", "gdead", "voff2", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder"};
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder"};
 static bool mem_report_on() {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
     return on;
@@ -584,7 +581,6 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next, bool always = false) {
         if (!kept(b)) b->release();
     c->ws.release();
     c->dense_on = false;
-    c->rstore_lent = false;
     c->class_pending = false;
     c->h_runs_valid = false;
     c->h_bkeys_valid = false;
@@ -1361,7 +1357,6 @@ static rdf_status parse_projection(rdf_ctx* c, const char* projection, int* proj
 static rdf_status g_record_bits(rdf_ctx* c) {
     c->spare_groups = false;  // a group build starts: its record buffers are in use
     c->jr_keep = false;
-    c->rstore_lent = false;   // (the previous discovery's bitmaps in rstore are not read again)
     c->dense_on = false;
     const u32 V = c->V ? c->V : 1;
     const u64 ncap = 2ull * c->U + c->B;  // compact candidate captures (k_frank_final)
@@ -2251,14 +2246,6 @@ static rdf_status d_dense_build(rdf_ctx* c, CindView& v, u64 nrows) {
     size_t hfree = 0, htotal = 0;
     if (hipMemGetInfo(&hfree, &htotal) == hipSuccess) budget = std::min<u64>(budget, std::max<u64>(c->dbits.cap, hfree / 2));
     (void)hipGetLastError();
-    // RDFIND_DENSE_LEND=1: the kept store of a join-range build (c4 at 10^9 triples: 43.6 GiB, idle until the next
-    // build) holds the bitmaps when it has room for more rows than the budget.  Measured slower: c4 at 10^9 with all
-    // 79,141 wanted rows (25 GB) 156 ms of light pass against 141 ms with the 8-GiB budget's 27,213 rows (the extra
-    // rows' probes are single 4-B reads in 315-KB rows, each a cache miss; profiles/r05_dense_lend_ab.log)
-    static const bool lend_ok = getenv("RDFIND_DENSE_LEND") && atoi(getenv("RDFIND_DENSE_LEND")) != 0;
-    const bool lend = lend_ok && c->spare_groups && c->rstore.p && !getenv("RDFIND_DENSE_BYTES") &&
-                      c->rstore.cap / (dwords * 4) > budget / (dwords * 4);
-    if (lend) budget = c->rstore.cap;
     const u64 rows = std::min<u64>(nrows, budget / (dwords * 4));
     if (getenv("RDFIND_DEBUG_LIGHT"))
         fprintf(stderr, "dense: C %llu G %llu rows %llu of %llu, %.1f MB\n", (unsigned long long)C, (unsigned long long)G,
@@ -2267,13 +2254,11 @@ static rdf_status d_dense_build(rdf_ctx* c, CindView& v, u64 nrows) {
     ENSURE(c, dlist, rows * 4);
     // the bitmaps only speed the light pass up: without the memory for them the member lists serve (no reclaim of the
     // spare scratch for them either: the next run would allocate that again)
-    if (lend) {
-        c->rstore_lent = true;
-        c->dbits_p = c->rstore.as<u32>();
-    } else {
-        if (c->dbits.ensure(rows * dwords * 4) != hipSuccess) return RDF_OK;
-        c->dbits_p = c->dbits.as<u32>();
+    if (c->dbits.ensure(rows * dwords * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        return RDF_OK;
     }
+    c->dbits_p = c->dbits.as<u32>();
     tbegin(c, RDF_T_LIGHT);
     hipLaunchKernelGGL(k_dense_rows, dim3(grid_for(G, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->gflag.as<u32>(),
                        c->gexcl.as<u32>(), G, (u32)rows, c->gdrow.as<u32>(), c->dlist.as<u32>());
@@ -2689,41 +2674,6 @@ static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL
             hipLaunchKernelGGL(k_verify_plan, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, vb, c->pnl.as<u32>(),
                                c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>());
         tend(c, RDF_T_LIGHT);
-        // dependents with many survivors: group-major sweeps of their light groups instead (k_gm_select picks them and
-        // clears their candidate-major plan); RDFIND_LIGHT_GM=0 keeps every dependent candidate-major, 2 none
-        // default off: on c4 the window range sweeps of k_light (light_sweep) verify these dependents faster (c4 at 0.4:
-        // light 281.7 ms candidate-major, 701 ms with this group-major pass B, 188.8 ms with sweeps in one light pass)
-        static const int gm_mode = getenv("RDFIND_LIGHT_GM") ? atoi(getenv("RDFIND_LIGHT_GM")) : 0;
-        u64 WG = 0;
-        c->n_gm_items = 0;
-        if (gm_mode && C) {
-            tbegin(c, RDF_T_LIGHT);
-            ENSURE(c, gmflag, (u64)C * 4);
-            ENSURE(c, gmitems, (u64)C * 4);
-            ENSURE(c, gmioff, (C + 1ull) * 8);
-            ENSURE(c, voff2, (C + 1ull) * 8);
-            HIP_TRY(c, hipMemcpyAsync(c->voff2.p, c->vcoff.p, (C + 1ull) * 8, hipMemcpyDeviceToDevice, st));
-            vb.vcoff = c->voff2.as<u64>();  // the survivors' offsets (vcoff is rewritten for pass B's pairs below)
-            hipLaunchKernelGGL(k_gm_select, dim3(vgrid(wave_blocks(C))), dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(C), vb,
-                               pivot, gm_mode, c->gmflag.as<u32>(), c->gmitems.as<u32>(), c->nchl.as<u32>(),
-                               c->nitl.as<u32>(), c->npk.as<u32>());
-            HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->gmitems.as<u32>(), c->gmioff.as<u64>(), C, c->gmioff.as<u64>() + C, st));
-            tend(c, RDF_T_LIGHT);
-            TRY(read_u64(c, c->gmioff.as<u64>() + C, &WG));
-            c->n_gm_items = WG;
-            if (WG) {
-                tbegin(c, RDF_T_LIGHT);
-                ENSURE(c, gmdep, WG * 4);
-                ENSURE(c, gdead, T);
-                HIP_TRY(c, hipMemsetAsync(c->gdead.p, 0, T, st));
-                hipLaunchKernelGGL(k_expand_owner, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                                   c->gmioff.as<u64>(), C, c->gmdep.as<u32>());
-                hipLaunchKernelGGL(k_light_gm, dim3(vgrid(WG)), dim3(RDF_BLOCK), 0, st, WG, vb, pivot, c->gmioff.as<u64>(),
-                                   c->gmdep.as<u32>(), WG, c->gdead.as<uint8_t>());
-                tend(c, RDF_T_LIGHT);
-            }
-            vb.vcoff = c->vcoff.as<u64>();
-        }
         const u64 hc = c->heavy_candidates, lc = c->light_candidates, le = c->light_entries;
         u64 WL2 = 0, WH2 = 0, WI2 = 0, WP2 = 0, WM2 = 0, EB = 0;
         TRY(d_chunks(c, &WL2, &WH2, &WI2, &WP2));
@@ -2737,13 +2687,7 @@ static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL
         tbegin(c, RDF_T_LIGHT);
         hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->cpairs.as<u64>(), EB, C, c->Cu, c->vcoff.as<u64>(), c->ebin.as<u64>());
-        if (WG)
-            hipLaunchKernelGGL(k_tag_fix_gm, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                               c->epairs_tmp.as<u64>(), c->lslot.as<u32>(), c->flags.as<u32>(), WL, c->cpairs.as<u64>(),
-                               c->vcoff.as<u64>(), c->gmflag.as<u32>(), c->vpairs.as<u64>(), c->voff2.as<u64>(),
-                               c->gdead.as<uint8_t>());
-        else
-            hipLaunchKernelGGL(k_tag_fix, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
+        hipLaunchKernelGGL(k_tag_fix, dim3(grid_for(WL, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs_tmp.as<u64>(),
                                c->lslot.as<u32>(), c->flags.as<u32>(), WL, c->cpairs.as<u64>(), c->vcoff.as<u64>());
         tend(c, RDF_T_LIGHT);
     }
@@ -3064,9 +3008,9 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (two) TRY(d_light_two_pass(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     else TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     if (getenv("RDFIND_LIGHT2_LOG"))
-        fprintf(stderr, "LIGHT2 two=%d items=%llu multi_chunk_items=%llu survivors=%llu gm_items=%llu explicit=%llu\n",
+        fprintf(stderr, "LIGHT2 two=%d items=%llu multi_chunk_items=%llu survivors=%llu explicit=%llu\n",
                 (int)two, (unsigned long long)WI, (unsigned long long)c->n_multi_items,
-                (unsigned long long)c->n_light_survivors, (unsigned long long)c->n_gm_items, (unsigned long long)E);
+                (unsigned long long)c->n_light_survivors, (unsigned long long)E);
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));

@@ -11,7 +11,7 @@ the library requests one at a time (``rdf_shard_step``):
   b. all-to-all       binary (key, count) partials to the key's owner rank, which sums them (:381-393)
   c. all-gather       the frequent binary keys of every owner (sorted afterwards: deterministic ids)
   (c'. all-reduce     --use-ars only: the slices' triple counts of the frequent conditions, for the rules,
-                      FrequentConditionPlanner.scala:129-193)
+                      FrequentConditionPlanner.scala:130-194)
   d. all-to-all       every triple to the ranks owning its join values (RDFind.scala:339-345 groupBy(joinValue)),
                       so rank r builds the capture groups of its join-value hash shard
   1. all-reduce(sum)  capture supports (distinct join values per capture)

@@ -190,8 +190,7 @@ print(json.dumps(out))
 @pytest.mark.parametrize("env", [{"RDFIND_STAGE": "0"}, {"RDFIND_STAGE": "1"},
                                  {"RDFIND_SIG": "0", "RDFIND_PIV2": "0"}, {"RDFIND_SIG": "1", "RDFIND_PIV2": "2"},
                                  {"RDFIND_DENSE": "0"}, {"RDFIND_DENSE": "256"}, {"RDFIND_LIGHT2": "1"},
-                                 {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "2"}, {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "0"},
-                                 {"RDFIND_LIGHT2": "1", "RDFIND_LIGHT_GM": "2", "RDFIND_DENSE": "0"},
+                                 {"RDFIND_LIGHT2": "1", "RDFIND_DENSE": "0"},
                                  {"RDFIND_SWEEP_F": "0"}, {"RDFIND_SWEEP_F": "1000000000"},
                                  {"RDFIND_SWEEP_F": "1000000000", "RDFIND_LIGHT2": "1", "RDFIND_DENSE": "0"},
                                  {"RDFIND_LIGHT_HIOCC": "1"}, {"RDFIND_LIGHT_HIOCC": "0"}, {"RDFIND_PIVX": "0"},
@@ -199,9 +198,9 @@ print(json.dumps(out))
 def test_light_variants_full_size(ctx, env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
     paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
-    verify passes forced instead of one light pass, pass B group-major for every dependent or none, window range sweeps
+    verify passes forced instead of one light pass (with and without bitmaps), window range sweeps
     never / whenever many candidates are alive, the plain variant at 6 waves per SIMD forced on / off, no extra pivots /
-    two) each reproduce the c1 and c2 golden vectors (and c4 at 0.1 for the sweep, group-major, occupancy and pivot
+    two) each reproduce the c1 and c2 golden vectors (and c4 at 0.1 for the sweep, two-pass, occupancy and pivot
     switches).  The switches are read
     once per process, so each combination runs in its own child process."""
     import subprocess
@@ -210,7 +209,7 @@ def test_light_variants_full_size(ctx, env):
     ctx.release_scratch()  # the module context's buffers from the full-size runs (c5 at 0.3: ~100 GB) would starve the child
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     keys = ["c1@1.0/s1_clean", "c2@1.0/s1_clean"]
-    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT_GM", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N",
+    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT2", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N",
             "RDFIND_PIVX_PACKED"} & set(env):  # c4 runs these
         keys.append("c4@0.1/s1_clean")
     jobs = [(GOLD[key], dataset_npz(GOLD[key]["config"], GOLD[key]["scale"])) for key in keys]
@@ -276,18 +275,17 @@ print(json.dumps({"bad": bad}))
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("heavy_min,gm", [("64", "1"), ("2", "1"), ("64", "2"), ("2", "2")])
-def test_two_light_passes_random(ctx, heavy_min, gm):
+@pytest.mark.parametrize("heavy_min", ["64", "2"])
+def test_two_light_passes_random(ctx, heavy_min):
     """The filter + verify light passes forced on random inputs (RDFIND_LIGHT2=1; LIGHT_PRE_MAX defers every chunk of
-    a multi-chunk dependent) against the C oracle in three modes, with and without lowered heavy columns, pass B
-    choosing group-major per dependent (RDFIND_LIGHT_GM=1) or group-major for every dependent (2).  In its own
+    a multi-chunk dependent) against the C oracle in three modes, with and without lowered heavy columns.  In its own
     process: the switch is read once per process."""
     import subprocess
     import sys
 
     ctx.release_scratch()  # the module context's pages of c5 at full size stay allocated otherwise
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RDFIND_LIGHT2="1", RDFIND_HEAVY_MIN=heavy_min, RDFIND_LIGHT_GM=gm)
+    env = dict(os.environ, RDFIND_LIGHT2="1", RDFIND_HEAVY_MIN=heavy_min)
     r = subprocess.run([sys.executable, "-c", _TWO_PASS_CHILD, root, "71" + heavy_min], env=env, capture_output=True,
                        text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]

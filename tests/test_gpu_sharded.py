@@ -290,8 +290,9 @@ def _config_worker(rank, world, port, cfg, scale, q, env=None):
         d, _ = synth.config_slice(cfg, scale, rank, world)
         with _lib.Context(0) as ctx:
             ctx.set_triples(d.s, d.p, d.o, d.num_terms)
+            ms = d.min_support
             del d
-            gs, _ = distributed.run_sharded(ctx, 100 if cfg == "c4" else 10, local_slice=True)
+            gs, _ = distributed.run_sharded(ctx, ms, local_slice=True)
             q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum(), "ranges": gs["n_join_ranges"],
                          "kept": gs["n_ranges_kept"]}))
     except Exception as e:  # report instead of hanging the parent
@@ -326,6 +327,68 @@ def _golden(key):
 
     from tests.conftest import GOLDEN
     return json.load(open(os.path.join(GOLDEN, "full_size.json")))[key]
+
+
+def _npz_worker(rank, world, port, path, q, env=None):
+    """One rank of a sharded run on a saved BASELINE input (tests/parity.py dataset_npz): the rank takes only its
+    contiguous slice of the rows (memory-mapped), as synth.config_slice would cut them."""
+    os.environ.update(env or {})
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rdfind_amd import _lib, distributed
+    from tests.parity import load_npz
+
+    try:
+        s, p, o, nv, ms = load_npz(path)
+        lo, hi = len(s) * rank // world, len(s) * (rank + 1) // world
+        with _lib.Context(0) as ctx:
+            ctx.set_triples(np.ascontiguousarray(s[lo:hi]), np.ascontiguousarray(p[lo:hi]),
+                            np.ascontiguousarray(o[lo:hi]), nv)
+            gs, cs = distributed.run_sharded(ctx, ms, local_slice=True)
+            q.put((rank, {"n": ctx.cind_count(), "checksum": ctx.checksum(), "explicit": cs["n_explicit_raw"],
+                          "hbm_gib": round(ctx.device_bytes() / 2**30, 1)}))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_npz(world, path, env=None, timeout=600):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_npz_worker, args=(r, world, port, path, q, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r, item = q.get(timeout=timeout)
+            assert not isinstance(item, str), f"rank {r}: {item}"
+            res[r] = item
+    finally:
+        for p in procs:
+            p.join(timeout=5 if len(res) < world else 60)
+            if p.is_alive():
+                p.terminate()
+    return res
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("key", ["c3@1.0/s1_clean", "c5@0.3/s1_clean"])
+def test_sharded_full_configs_vs_golden(key):
+    """BASELINE configs[2] (c3, DBpedia-shaped, 10^8 triples, support 25) at full size and configs[4] (c5, the skewed
+    pair-explosion shape, support 2) at the largest scale two ranks hold on the box's one GPU (0.3: 1.7·10^10 CINDs),
+    each over 2 ranks holding half of the rows: the ranks' CINDs sum to the streamed C oracle's golden count and set
+    checksum (tests/golden/full_size.json)."""
+    from tests.parity import dataset_npz
+
+    g = _golden(key)
+    path = dataset_npz(g["config"], g["scale"])
+    res = _run_npz(2, path)
+    assert sum(res[r]["n"] for r in range(2)) == g["n_cinds"], res
+    assert sum(res[r]["checksum"] for r in range(2)) % (1 << 64) == int(g["checksum"]), res
 
 
 @pytest.mark.timeout(300)
