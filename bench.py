@@ -139,12 +139,21 @@ class CompactSink:
 
     STREAM_REFS = 1 << 28  # 1 GiB of u32 refs
 
-    def __init__(self):
+    def __init__(self, early=True):
         self.bufs, self.cap, self.pinned, self._keep = None, {}, True, []
+        self.early = early  # register the pinned buffers for the library's early hand-over (rdf_set_handover)
+
+    def register(self, ctx):
+        """The unpaged discoveries that follow fill the refs and the capture table of these buffers while they still
+        compute (rdf_set_handover); copy() then moves only the rest."""
+        if self.early and self.pinned and self.bufs is not None:
+            ctx.set_handover(self.bufs["refs"], self.cap["refs"], self.bufs["capture_ids"], self.bufs["supports"],
+                             min(self.cap["capture_ids"], self.cap["supports"]))
 
     def ensure(self, ctx):
         from rdfind_amd import _lib
         L = ctx.result_layout()
+        grown = False
         if self.bufs is None:
             self.bufs, self._keep = {}, {}
         for name, dt, count in _lib.COMPACT_PARTS:  # only a part that outgrew its buffer is re-allocated
@@ -168,6 +177,9 @@ class CompactSink:
                 self._keep[name] = a
                 self.bufs[name] = a.ctypes.data
             self.cap[name] = need
+            grown = True
+        if grown:
+            self.register(ctx)
         return L
 
     def copy(self, ctx):
@@ -328,6 +340,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (gloo: host-staged "
                     "exchanges, to rehearse several ranks on one GPU)")
     ap.add_argument("--no-resident", action="store_true", help="skip the device-resident repeat of the steps")
+    ap.add_argument("--no-early-handover", action="store_true", help="hand the whole result over after each run "
+                    "(no rdf_set_handover: the refs and the capture table are not copied while the run computes)")
     ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
     ap.add_argument("--c4-strong", choices=("auto", "on", "off"), default="auto",
                     help="also time BASELINE configs[3] (c4, Freebase-shaped, 10^9 triples, support 100) split over the "
@@ -379,7 +393,7 @@ def main():
     ms = d.min_support
     ctx = _lib.Context(local_rank)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
-    sink = CompactSink()
+    sink = CompactSink(early=not args.no_early_handover)
 
     paged = dist is None and args.page_bytes is not None
     if dist is None and not paged:  # a result larger than HBM: the unpaged run fails with RDF_ERR_OOM -> pages
@@ -468,6 +482,7 @@ def main():
     # the same steps without the hand-over (results left in HBM): the device-resident rate
     elapsed_dev = None
     if not args.no_resident:
+        ctx.set_handover()  # results stay in HBM: no early copies either
         barrier()
         t1 = time.perf_counter()
         for _ in range(args.steps):
@@ -588,7 +603,8 @@ def main():
             "step": "T_disc (SURVEY.md 8(d)): dictionary-encoded triples resident in HBM -> compact CindSet-shaped "
                     "id-records (rdf_copy_result_compact) in pinned host memory, every rank" +
                     (" (paged: every page handed over in turn)" if paged else ""),
-            "handover": {"bytes_all_ranks": total_bytes, "pinned": sink.pinned, "n_refs": L["n_refs"],
+            "handover": {"bytes_all_ranks": total_bytes, "pinned": sink.pinned, "early": sink.early and sink.pinned,
+                         "n_refs": L["n_refs"],
                          "n_list_refs": L["n_list_refs"], "n_members": L["n_members"], "n_runs": L["n_runs"]},
             "device_resident": None if elapsed_dev is None else
                                {"ms_per_step": round(elapsed_dev * 1000.0 / steps, 3),

@@ -119,6 +119,16 @@ struct rdf_ctx {
     DevBuf iflag, iexcl, iorder; // k_light's issue order (k_light_long_flags / k_light_order)
     hipStream_t side = nullptr;  // k_light_packed beside k_light (their slots are disjoint), joined before the compaction
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // early hand-over (rdf_set_handover): pinned host buffers the unpaged discovery fills on a copy stream while it still
+    // computes -- the capture table as the discovery starts, the explicit refs once the rules have run (before the
+    // class stage); rdf_copy_result_compact then copies only the rest
+    hipStream_t hstream = nullptr;
+    hipEvent_t hv_ev = nullptr;
+    uint32_t *hv_refs = nullptr, *hv_capid = nullptr, *hv_sup = nullptr;
+    u64 hv_refs_cap = 0, hv_cap_cap = 0;
+    u64 hv_refs_n = ~0ull;       // refs copied early by the current result (~0: none)
+    bool hv_caps_done = false;   // capture ids and supports copied early
+    bool hv_pending = false;     // copies queued on hstream not yet waited for
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
     int dense_div = -1;                   // RDFIND_DENSE (0: no bitmaps; -1: by input, d_dense_flags)
@@ -279,6 +289,19 @@ static rdf_status ensure_buf(rdf_ctx* c, DevBuf* b, size_t bytes, const char* wh
     return RDF_OK;
 }
 #define ENSURE(ctx, buf, bytes) TRY(ensure_buf(ctx, &(ctx)->buf, (size_t)(bytes), "allocating " #buf))
+// the early hand-over's copies (rdf_set_handover) must finish before the device buffers they read are rewritten or
+// freed by the next stage, and before the caller reads its host buffers; a new result forgets them
+static rdf_status hv_wait(rdf_ctx* c, bool forget) {
+    if (c->hv_pending) {
+        c->hv_pending = false;
+        HIP_TRY(c, hipStreamSynchronize(c->hstream));
+    }
+    if (forget) {
+        c->hv_refs_n = ~0ull;
+        c->hv_caps_done = false;
+    }
+    return RDF_OK;
+}
 #define ENSURE_KEEP(ctx, buf, bytes) HIP_TRY(ctx, (ctx)->buf.grow_keep((size_t)(bytes), (ctx)->stream))
 
 static int bits_for(u64 maxval) {  // bits needed to represent values in [0, maxval]
@@ -501,6 +524,8 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hv_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
@@ -521,6 +546,7 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->hstream) (void)hipStreamSynchronize(c->hstream);
     for (DevBuf* b : ctx_buffers(c)) b->release();
     c->ws.release();
     if (c->hscal) (void)hipHostFree(c->hscal);
@@ -530,6 +556,8 @@ void rdf_ctx_destroy(rdf_ctx* c) {
     for (auto& e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->hstream) (void)hipStreamDestroy(c->hstream);
+    if (c->hv_ev) (void)hipEventDestroy(c->hv_ev);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -590,6 +618,7 @@ static void release_run_buffers(rdf_ctx* c, u64 n_next, bool always = false) {
 rdf_status rdf_release_scratch(rdf_ctx* c) {
     if (!c) return RDF_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     release_run_buffers(c, 0, true);
     (void)hipGetLastError();  // an out-of-memory failure before this call is not the next call's error
     c->paged = false;
@@ -603,6 +632,7 @@ rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, con
     rdf_status st = check_terms(c, n, num_terms);
     if (st) return st;
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     release_run_buffers(c, n);
     ENSURE(c, ts, n * 4);
     ENSURE(c, tp, n * 4);
@@ -628,6 +658,7 @@ rdf_status rdf_set_triples(rdf_ctx* c, const uint32_t* s, const uint32_t* p, con
 rdf_status rdf_set_triples_device(rdf_ctx* c, const uint32_t* s, const uint32_t* p, const uint32_t* o, uint64_t n,
                                   uint32_t num_terms) {
     if (!c || (n && (!s || !p || !o))) return fail(c, RDF_ERR_ARG, "null triple arrays");
+    if (c) TRY(hv_wait(c, true));
     rdf_status st = check_terms(c, n, num_terms);
     if (st) return st;
     c->s = s;
@@ -649,6 +680,7 @@ rdf_status rdf_distinct_triples(rdf_ctx* c, uint64_t* n_distinct, float* ms) {
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     hipStream_t st = c->stream;
     const u64 n = c->n;
     HIP_TRY(c, hipEventRecord(c->ev[6], st));
@@ -715,6 +747,7 @@ rdf_status rdf_parse_ntriples(rdf_ctx* c, const char* text, uint64_t nbytes, uin
                               uint32_t* num_terms, float* ms) {
     if (!c || (nbytes && !text)) return fail(c, RDF_ERR_ARG, "null text");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     hipStream_t st = c->stream;
     const unsigned char* dtext = nullptr;
     ENSURE(c, ntext, nbytes + 16);  // 16-B loads of the last tile stay inside the buffer
@@ -1204,6 +1237,7 @@ rdf_status rdf_frequent_conditions(rdf_ctx* c, uint32_t min_support, rdf_fc_stat
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     TRY(fc_begin(c, min_support));
     u64 nfreq[3] = {0, 0, 0};
     tbegin(c, RDF_T_UNARY);
@@ -2149,6 +2183,7 @@ rdf_status rdf_build_capture_groups(rdf_ctx* c, const char* projection, rdf_grou
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 2) return fail(c, RDF_ERR_STATE, "rdf_frequent_conditions must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     int proj = 0;
     TRY(parse_projection(c, projection, &proj));
     c->rank = 0;
@@ -2896,9 +2931,10 @@ static rdf_status d_class_bin(rdf_ctx* c, const CindView& v, u64* WH) {
 }
 
 // K7 minimality on the (owned) explicit pairs, heavy-only binary write pass, class emission -> out
-static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
+// minimality rules on the explicit pairs and their kept refs compacted into out[0, *K) (out sized for E refs + `extra`)
+static rdf_status d_emit_rules(rdf_ctx* c, const CindView& v, u64 E, u64 extra, u64* Kout) {
     hipStream_t st = c->stream;
-    ENSURE(c, out, std::max<u64>(E + H, 1) * 4);  // the class part is expanded behind it on demand (materialize)
+    ENSURE(c, out, std::max<u64>(E + extra, 1) * 4);  // the class part is expanded behind it on demand (materialize)
     ENSURE(c, flags, std::max<u64>(E, 1) * 4);
     ENSURE(c, pos, (E + 1) * 8);
     tbegin(c, RDF_T_RULES);
@@ -2913,8 +2949,24 @@ static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u6
         hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->epairs.as<u64>(), E,
                            c->flags.as<u32>(), c->pos.as<u64>(), c->out.as<u32>());
     tend(c, RDF_T_RULES);
+    return read_u64(c, c->pos.as<u64>() + E, Kout);
+}
+
+static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 WH, u64 H, u64 HC, u64 NT);
+static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
     u64 K = 0;
-    TRY(read_u64(c, c->pos.as<u64>() + E, &K));
+    TRY(d_emit_rules(c, v, E, H, &K));
+    return d_emit_rest(c, v, E, K, WH, H, HC, NT);
+}
+
+// the heavy-only refs behind the K explicit ones, the class lists' offsets, the run table, the stage's statistics
+static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 WH, u64 H, u64 HC, u64 NT) {
+    hipStream_t st = c->stream;
+    (void)E;
+    if ((u64)c->out.cap < std::max<u64>(K + H, 1) * 4) {  // the early rules sized `out` before H was known
+        TRY(hv_wait(c, false));
+        HIP_TRY(c, c->out.grow_keep(std::max<u64>(K + H, 1) * 4, st));
+    }
     tbegin(c, RDF_T_HWRITE);
     if (WH)
         hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(WH))),
@@ -2983,11 +3035,20 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     c->paged = false;
     // test hook (RDFIND_TEST_OOM_DISCOVERY=1): the unpaged discovery reports RDF_ERR_OOM at once, so a caller's
     // fallback to pages runs on small inputs
     if (c->test_oom_discovery) return fail(c, RDF_ERR_OOM, "test hook: the unpaged discovery runs out of memory");
     hipStream_t st = c->stream;
+    if (c->hv_capid && c->hv_sup && c->C && (u64)c->C <= c->hv_cap_cap) {  // the capture table is final: early copy
+        HIP_TRY(c, hipEventRecord(c->hv_ev, st));
+        HIP_TRY(c, hipStreamWaitEvent(c->hstream, c->hv_ev, 0));
+        HIP_TRY(c, hipMemcpyAsync(c->hv_capid, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, c->hstream));
+        HIP_TRY(c, hipMemcpyAsync(c->hv_sup, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, c->hstream));
+        c->hv_caps_done = true;
+        c->hv_pending = true;
+    }
     CindView v = make_view(c, flags);
     TRY(d_pivot_local(c, v));
     tbegin(c, RDF_T_PIVOT);
@@ -3014,12 +3075,23 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
     TRY(d_explicit_index(c, v, E, true));
+    // the explicit pairs' rules first: their refs are final before the class stage, so an early hand-over copies them
+    // while the classes and the heavy-only dependents are computed
+    u64 K = 0;
+    TRY(d_emit_rules(c, v, E, 0, &K));
+    if (c->hv_refs && K <= c->hv_refs_cap) {
+        HIP_TRY(c, hipEventRecord(c->hv_ev, st));
+        HIP_TRY(c, hipStreamWaitEvent(c->hstream, c->hv_ev, 0));
+        if (K) HIP_TRY(c, hipMemcpyAsync(c->hv_refs, c->out.p, K * 4, hipMemcpyDeviceToHost, c->hstream));
+        c->hv_refs_n = K;
+        c->hv_pending = true;
+    }
     // strategy 0's quirk filter is per dependent: keep the pivot scan there (RDFIND_HCLASS=0: test hook)
     c->hclassed = !v.literal && c->allow_hclass && !v.ar;
     TRY(d_classes_single(c, v, &HC, &NT));
     if (c->hclassed) TRY(d_class_bin(c, v, &WH));
     TRY(d_heavy_count(c, v, WH, &H));
-    TRY(d_emit(c, v, E, WH, H, HC, NT));
+    TRY(d_emit_rest(c, v, E, K, WH, H, HC, NT));
     if (stats) *stats = c->cstats;
     mem_report(c);
     return RDF_OK;
@@ -3156,6 +3228,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
     hipStream_t st = c->stream;
     if (!page_bytes) {  // an eighth of the free HBM, at most 32 GB: the resident unary pairs need the rest
         size_t fr = 0, tot = 0;
@@ -4354,6 +4427,7 @@ static bool sh_phase_valid(int ph, bool pending) {
 rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t min_support, const char* projection,
                            uint32_t flags) {
     if (!c) return RDF_ERR_ARG;
+    if (c) TRY(hv_wait(c, true));
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
     c->hclassed = false;
@@ -4375,6 +4449,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
 rdf_status rdf_shard_parse_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, const char* text, uint64_t nbytes,
                                  uint32_t flags, uint64_t* n_triples) {
     if (!c) return RDF_ERR_ARG;
+    if (c) TRY(hv_wait(c, true));
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     uint64_t n = 0;
     u32 Vl = 0;
@@ -4505,6 +4580,7 @@ static rdf_status materialize(rdf_ctx* c) {
     if (!c->class_pending) return RDF_OK;
     hipStream_t st = c->stream;
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, false));  // an early refs copy may still read `out`
     HIP_TRY(c, c->out.grow_keep((size_t)std::max<u64>(c->n_out, 1) * 4, st));
     c->tn[RDF_T_CEMIT] = 0;
     tbegin(c, RDF_T_CEMIT);
@@ -4553,7 +4629,12 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     hipStream_t st = c->stream;
     const u64 nrefs = c->n_out - c->n_class_out, R = c->n_runs_explicit;
     const u64 nmem = c->n_class_out ? c->n_class_members : 0;
-    if (refs && nrefs) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr, nrefs * 4, hipMemcpyDeviceToHost, st));
+    // parts the early hand-over already copied into these same buffers: only their tails (heavy-only refs behind the
+    // explicit ones) or nothing
+    const u64 r0 = refs && refs == c->hv_refs && c->hv_refs_n != ~0ull ? std::min<u64>(c->hv_refs_n, nrefs) : 0;
+    const bool caps_done = c->hv_caps_done && capture_ids == c->hv_capid && supports == c->hv_sup;
+    if (refs && nrefs > r0)
+        HIP_TRY(c, hipMemcpyAsync(refs + r0, c->out_ptr + r0, (nrefs - r0) * 4, hipMemcpyDeviceToHost, st));
     if (runoff) HIP_TRY(c, hipMemcpyAsync(runoff, c->runoff.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
     if (rundep && R) HIP_TRY(c, hipMemcpyAsync(rundep, c->rundep.p, R * 4, hipMemcpyDeviceToHost, st));
     if (c->n_lists) {
@@ -4564,9 +4645,25 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
         list_off[0] = 0;
     }
     if (members && nmem) HIP_TRY(c, hipMemcpyAsync(members, c->ckeys.p, nmem * 8, hipMemcpyDeviceToHost, st));
-    if (capture_ids && c->C) HIP_TRY(c, hipMemcpyAsync(capture_ids, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
-    if (supports && c->C) HIP_TRY(c, hipMemcpyAsync(supports, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
+    if (capture_ids && c->C && !caps_done)
+        HIP_TRY(c, hipMemcpyAsync(capture_ids, c->fext.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
+    if (supports && c->C && !caps_done)
+        HIP_TRY(c, hipMemcpyAsync(supports, c->csup.p, (u64)c->C * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(c, hipStreamSynchronize(st));
+    TRY(hv_wait(c, false));
+    return RDF_OK;
+}
+
+rdf_status rdf_set_handover(rdf_ctx* c, uint32_t* refs, uint64_t refs_cap, uint32_t* capture_ids, uint32_t* supports,
+                            uint64_t capture_cap) {
+    if (!c) return RDF_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, true));
+    c->hv_refs = refs_cap ? refs : nullptr;
+    c->hv_refs_cap = refs ? refs_cap : 0;
+    c->hv_capid = capture_cap ? capture_ids : nullptr;
+    c->hv_sup = capture_cap ? supports : nullptr;
+    c->hv_cap_cap = capture_ids && supports ? capture_cap : 0;
     return RDF_OK;
 }
 

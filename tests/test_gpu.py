@@ -793,3 +793,41 @@ def test_parse_scratch_released(ctx):
         assert c.cind_count() > 0
     finally:
         c.close()
+
+
+def test_early_handover_matches_plain_copy():
+    """rdf_set_handover: the explicit refs and the capture table copied into registered page-locked buffers while the
+    discovery still computes, the rest by rdf_copy_result_compact, equal the plain hand-over into fresh arrays (random
+    inputs in every mode, a refs buffer too small for some results -- those go the plain way --, and re-runs into the
+    same buffers), and the checker expands them to the device's own count and checksum."""
+    import ctypes
+
+    from bench import CompactSink
+
+    g = _lib.Context(0)
+    try:
+        sink = CompactSink(early=True)
+        rng = random.Random(31)
+        seen_early = 0
+        for it in range(30):
+            n = rng.randrange(1, 500)
+            nv = rng.randrange(2, 60)
+            ms = rng.randrange(1, 4)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            for strategy, clean in MODES:
+                g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+                g.run(ms, "spo", clean, strategy)
+                L = sink.copy(g)
+                plain = g.copy_result_compact()
+                for name, dt, count in _lib.COMPACT_PARTS:
+                    k = count(L)
+                    got = np.ctypeslib.as_array(ctypes.cast(sink.bufs[name], ctypes.POINTER(
+                        ctypes.c_uint32 if dt == np.uint32 else ctypes.c_uint64)), shape=(max(k, 1),))[:k]
+                    assert np.array_equal(got, plain[name][:k]), (it, strategy, clean, name)
+                cnt, h, _ = C.checksum_compact(plain, nv)
+                assert (cnt, h) == (g.cind_count(), g.checksum()), (it, strategy, clean)
+                seen_early += L["n_refs"] <= sink.cap["refs"]
+        assert seen_early > 0
+    finally:
+        g.close()
