@@ -147,8 +147,9 @@ class CompactSink:
         """The unpaged discoveries that follow fill the refs and the capture table of these buffers while they still
         compute (rdf_set_handover); copy() then moves only the rest."""
         if self.early and self.pinned and self.bufs is not None:
-            ctx.set_handover(self.bufs["refs"], self.cap["refs"], self.bufs["capture_ids"], self.bufs["supports"],
-                             min(self.cap["capture_ids"], self.cap["supports"]))
+            ctx.set_handover(self.bufs["refs"], self.cap["refs"], self.bufs["runoff"], self.bufs["rundep"],
+                             min(self.cap["runoff"] - 1, self.cap["rundep"]), self.bufs["capture_ids"],
+                             self.bufs["supports"], min(self.cap["capture_ids"], self.cap["supports"]))
 
     def ensure(self, ctx):
         from rdfind_amd import _lib

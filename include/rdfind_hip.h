@@ -229,12 +229,13 @@ rdf_status rdf_copy_result_compact(rdf_ctx* ctx, uint32_t* refs, uint64_t* runof
 /* Early hand-over (optional; pipelining of the sink with the computation).  Registers page-locked host buffers that
  * every later unpaged single-GPU rdf_discover_cinds / rdf_run may fill on a copy stream while it still computes: the
  * capture table (capture_ids, supports: up to capture_cap entries) when the discovery starts, the explicit refs (up to
- * refs_cap) once their minimality rules have run, before the class stage.  A later rdf_copy_result_compact given the
+ * refs_cap) and the explicit dependents' runs (runoff / rundep [0, n_captures), runs_cap >= n_captures) once their
+ * minimality rules have run, before the class stage.  A later rdf_copy_result_compact given the
  * same pointers copies only what is left and returns when everything has arrived; the buffers must not be read before
  * it returns.  Parts that do not fit are copied by rdf_copy_result_compact as before.  Null pointers / zero capacities
  * unregister.  The reference's sink likewise consumes results while the job still runs (ALG/programs/RDFind.scala:507-520). */
-rdf_status rdf_set_handover(rdf_ctx* ctx, uint32_t* refs, uint64_t refs_cap, uint32_t* capture_ids, uint32_t* supports,
-                            uint64_t capture_cap);
+rdf_status rdf_set_handover(rdf_ctx* ctx, uint32_t* refs, uint64_t refs_cap, uint64_t* runoff, uint32_t* rundep,
+                            uint64_t runs_cap, uint32_t* capture_ids, uint32_t* supports, uint64_t capture_cap);
 
 /* refs[offset, offset + count) of the compact result (the explicit ref part, n_refs in all) -> refs; *n_copied = the
  * refs copied (fewer at the end).  A streaming sink hands a large page over through one bounded staging buffer

@@ -164,7 +164,7 @@ def load():
         "rdf_get_result_layout": (i32, [P, ctypes.POINTER(ResultLayout)]),
         "rdf_copy_result_compact": (i32, [P, P, P, P, P, P, P, P, P]),
         "rdf_copy_result_refs": (i32, [P, u64, u64, P, ctypes.POINTER(u64)]),
-        "rdf_set_handover": (i32, [P, P, u64, P, P, u64]),
+        "rdf_set_handover": (i32, [P, P, u64, P, P, u64, P, P, u64]),
         "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
         "rdf_format_cinds": (i32, [P, u64, u64, P, u64, ctypes.POINTER(u64)]),
@@ -535,12 +535,14 @@ class Context:
         self._check(self.lib.rdf_copy_result_compact(self.ptr, *ptrs), "rdf_copy_result_compact")
         return bufs
 
-    def set_handover(self, refs=None, refs_cap: int = 0, capture_ids=None, supports=None, capture_cap: int = 0):
+    def set_handover(self, refs=None, refs_cap: int = 0, runoff=None, rundep=None, runs_cap: int = 0, capture_ids=None,
+                     supports=None, capture_cap: int = 0):
         """rdf_set_handover: page-locked buffers (raw pointers or numpy arrays) the next unpaged discoveries fill early;
         rdf_copy_result_compact with the same buffers then copies only the rest.  No arguments: unregister."""
-        p = [0 if x is None else (x if isinstance(x, int) else x.ctypes.data) for x in (refs, capture_ids, supports)]
-        self._check(self.lib.rdf_set_handover(self.ptr, p[0] or None, refs_cap, p[1] or None, p[2] or None, capture_cap),
-                    "rdf_set_handover")
+        p = [None if x is None else (x if isinstance(x, int) else x.ctypes.data)
+             for x in (refs, runoff, rundep, capture_ids, supports)]
+        self._check(self.lib.rdf_set_handover(self.ptr, p[0] or None, refs_cap, p[1] or None, p[2] or None, runs_cap,
+                                              p[3] or None, p[4] or None, capture_cap), "rdf_set_handover")
 
     def copy_result_refs(self, offset: int, count: int, ptr) -> int:
         """rdf_copy_result_refs: refs[offset, offset + count) of the compact result into ``ptr`` (numpy array or raw

@@ -2905,9 +2905,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_output_runs(u32 C, const u64* __r
                                                            u64 WH, const u64* __restrict__ choffh, const u64* __restrict__ hoff,
                                                            u64 K, u64 nmem, const u64* __restrict__ ckeys,
                                                            const u64* __restrict__ cobase, u64 H, u64 n_out, u64* runoff,
-                                                           u32* rundep) {
+                                                           u32* rundep, u64 i0, u64 i1) {
+    // runs [i0, i1] of the table (the explicit runs [0, C) are final once the rules have run: the early hand-over
+    // writes and copies them before the class stage, the rest at the end)
     const u64 R = (u64)C + WH + nmem;
-    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= R; i += (u64)gridDim.x * RDF_BLOCK) {
+    for (u64 i = i0 + (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i <= i1 && i <= R; i += (u64)gridDim.x * RDF_BLOCK) {
         if (i == R) {
             runoff[i] = n_out;
         } else if (i < C) {

@@ -124,8 +124,10 @@ struct rdf_ctx {
     // class stage); rdf_copy_result_compact then copies only the rest
     hipStream_t hstream = nullptr;
     hipEvent_t hv_ev = nullptr;
-    uint32_t *hv_refs = nullptr, *hv_capid = nullptr, *hv_sup = nullptr;
-    u64 hv_refs_cap = 0, hv_cap_cap = 0;
+    uint32_t *hv_refs = nullptr, *hv_capid = nullptr, *hv_sup = nullptr, *hv_rundep = nullptr;
+    uint64_t* hv_runoff = nullptr;
+    u64 hv_refs_cap = 0, hv_cap_cap = 0, hv_runs_cap = 0;
+    u64 hv_runs_n = ~0ull;       // explicit runs [0, hv_runs_n) copied early (runoff and rundep; ~0: none)
     u64 hv_refs_n = ~0ull;       // refs copied early by the current result (~0: none)
     bool hv_caps_done = false;   // capture ids and supports copied early
     bool hv_pending = false;     // copies queued on hstream not yet waited for
@@ -298,6 +300,7 @@ static rdf_status hv_wait(rdf_ctx* c, bool forget) {
     }
     if (forget) {
         c->hv_refs_n = ~0ull;
+        c->hv_runs_n = ~0ull;
         c->hv_caps_done = false;
     }
     return RDF_OK;
@@ -2952,15 +2955,16 @@ static rdf_status d_emit_rules(rdf_ctx* c, const CindView& v, u64 E, u64 extra, 
     return read_u64(c, c->pos.as<u64>() + E, Kout);
 }
 
-static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 WH, u64 H, u64 HC, u64 NT);
+static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 WH, u64 H, u64 HC, u64 NT, u64 runs0);
 static rdf_status d_emit(rdf_ctx* c, const CindView& v, u64 E, u64 WH, u64 H, u64 HC, u64 NT) {
     u64 K = 0;
     TRY(d_emit_rules(c, v, E, H, &K));
-    return d_emit_rest(c, v, E, K, WH, H, HC, NT);
+    return d_emit_rest(c, v, E, K, WH, H, HC, NT, 0);
 }
 
-// the heavy-only refs behind the K explicit ones, the class lists' offsets, the run table, the stage's statistics
-static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 WH, u64 H, u64 HC, u64 NT) {
+// the heavy-only refs behind the K explicit ones, the class lists' offsets, the run table from run runs0 on (the
+// explicit runs [0, runs0) were written early), the stage's statistics
+static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 WH, u64 H, u64 HC, u64 NT, u64 runs0) {
     hipStream_t st = c->stream;
     (void)E;
     if ((u64)c->out.cap < std::max<u64>(K + H, 1) * 4) {  // the early rules sized `out` before H was known
@@ -2991,11 +2995,19 @@ static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 W
     // run table: the dependent of every output ref (CindSet-shaped result, ALG/data/CindSet.scala:9-13)
     const u64 nmem = HC ? c->n_class_members : 0;
     const u64 R = (u64)c->C + WH + nmem;
-    ENSURE(c, runoff, (R + 1) * 8);
-    ENSURE(c, rundep, std::max<u64>(R, 1) * 4);
-    hipLaunchKernelGGL(k_output_runs, dim3(grid_for(R + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->C, v.eoff,
+    if (runs0) {  // the explicit runs are in place (and may be on their way to the host): grow keeping them
+        if ((u64)c->runoff.cap < (R + 1) * 8 || (u64)c->rundep.cap < std::max<u64>(R, 1) * 4) {
+            TRY(hv_wait(c, false));
+            HIP_TRY(c, c->runoff.grow_keep((R + 1) * 8, st));
+            HIP_TRY(c, c->rundep.grow_keep(std::max<u64>(R, 1) * 4, st));
+        }
+    } else {
+        ENSURE(c, runoff, (R + 1) * 8);
+        ENSURE(c, rundep, std::max<u64>(R, 1) * 4);
+    }
+    hipLaunchKernelGGL(k_output_runs, dim3(grid_for(R + 1 - runs0, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->C, v.eoff,
                        c->pos.as<u64>(), WH, c->choffh.as<u64>(), c->hoff.as<u64>(), K, nmem, c->ckeys.as<u64>(),
-                       c->cobase.as<u64>(), H, K + H + HC, c->runoff.as<u64>(), c->rundep.as<u32>());
+                       c->cobase.as<u64>(), H, K + H + HC, c->runoff.as<u64>(), c->rundep.as<u32>(), runs0, R);
     c->n_runs = R;
     c->n_runs_explicit = (u64)c->C + WH;
     c->h_runs_valid = false;
@@ -3079,11 +3091,29 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     // while the classes and the heavy-only dependents are computed
     u64 K = 0;
     TRY(d_emit_rules(c, v, E, 0, &K));
-    if (c->hv_refs && K <= c->hv_refs_cap) {
+    u64 runs0 = 0;  // explicit runs written early
+    if (c->hv_runoff && c->hv_rundep && (u64)c->C <= c->hv_runs_cap) {
+        ENSURE(c, runoff, (c->C + 1ull) * 8);
+        ENSURE(c, rundep, std::max<u64>(c->C, 1) * 4);
+        if (c->C)
+            hipLaunchKernelGGL(k_output_runs, dim3(grid_for(c->C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->C, v.eoff,
+                               c->pos.as<u64>(), 0ull, c->choffh.as<u64>(), c->hoff.as<u64>(), K, 0ull, c->ckeys.as<u64>(),
+                               c->cobase.as<u64>(), 0ull, K, c->runoff.as<u64>(), c->rundep.as<u32>(), 0ull,
+                               (u64)c->C - 1);
+        runs0 = c->C;
+    }
+    if ((c->hv_refs && K <= c->hv_refs_cap) || runs0) {
         HIP_TRY(c, hipEventRecord(c->hv_ev, st));
         HIP_TRY(c, hipStreamWaitEvent(c->hstream, c->hv_ev, 0));
-        if (K) HIP_TRY(c, hipMemcpyAsync(c->hv_refs, c->out.p, K * 4, hipMemcpyDeviceToHost, c->hstream));
-        c->hv_refs_n = K;
+        if (c->hv_refs && K <= c->hv_refs_cap) {
+            if (K) HIP_TRY(c, hipMemcpyAsync(c->hv_refs, c->out.p, K * 4, hipMemcpyDeviceToHost, c->hstream));
+            c->hv_refs_n = K;
+        }
+        if (runs0) {
+            HIP_TRY(c, hipMemcpyAsync(c->hv_runoff, c->runoff.p, runs0 * 8, hipMemcpyDeviceToHost, c->hstream));
+            HIP_TRY(c, hipMemcpyAsync(c->hv_rundep, c->rundep.p, runs0 * 4, hipMemcpyDeviceToHost, c->hstream));
+            c->hv_runs_n = runs0;
+        }
         c->hv_pending = true;
     }
     // strategy 0's quirk filter is per dependent: keep the pivot scan there (RDFIND_HCLASS=0: test hook)
@@ -3091,7 +3121,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     TRY(d_classes_single(c, v, &HC, &NT));
     if (c->hclassed) TRY(d_class_bin(c, v, &WH));
     TRY(d_heavy_count(c, v, WH, &H));
-    TRY(d_emit_rest(c, v, E, K, WH, H, HC, NT));
+    TRY(d_emit_rest(c, v, E, K, WH, H, HC, NT, runs0));
     if (stats) *stats = c->cstats;
     mem_report(c);
     return RDF_OK;
@@ -4635,8 +4665,12 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     const bool caps_done = c->hv_caps_done && capture_ids == c->hv_capid && supports == c->hv_sup;
     if (refs && nrefs > r0)
         HIP_TRY(c, hipMemcpyAsync(refs + r0, c->out_ptr + r0, (nrefs - r0) * 4, hipMemcpyDeviceToHost, st));
-    if (runoff) HIP_TRY(c, hipMemcpyAsync(runoff, c->runoff.p, (R + 1) * 8, hipMemcpyDeviceToHost, st));
-    if (rundep && R) HIP_TRY(c, hipMemcpyAsync(rundep, c->rundep.p, R * 4, hipMemcpyDeviceToHost, st));
+    const u64 q0 = runoff && rundep && runoff == c->hv_runoff && rundep == c->hv_rundep && c->hv_runs_n != ~0ull
+                       ? std::min<u64>(c->hv_runs_n, R) : 0;
+    if (runoff)
+        HIP_TRY(c, hipMemcpyAsync(runoff + q0, c->runoff.as<u64>() + q0, (R + 1 - q0) * 8, hipMemcpyDeviceToHost, st));
+    if (rundep && R > q0)
+        HIP_TRY(c, hipMemcpyAsync(rundep + q0, c->rundep.as<u32>() + q0, (R - q0) * 4, hipMemcpyDeviceToHost, st));
     if (c->n_lists) {
         if (list_refs && c->n_list_refs)
             HIP_TRY(c, hipMemcpyAsync(list_refs, c->clists.p, c->n_list_refs * 4, hipMemcpyDeviceToHost, st));
@@ -4654,13 +4688,16 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     return RDF_OK;
 }
 
-rdf_status rdf_set_handover(rdf_ctx* c, uint32_t* refs, uint64_t refs_cap, uint32_t* capture_ids, uint32_t* supports,
-                            uint64_t capture_cap) {
+rdf_status rdf_set_handover(rdf_ctx* c, uint32_t* refs, uint64_t refs_cap, uint64_t* runoff, uint32_t* rundep,
+                            uint64_t runs_cap, uint32_t* capture_ids, uint32_t* supports, uint64_t capture_cap) {
     if (!c) return RDF_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     TRY(hv_wait(c, true));
     c->hv_refs = refs_cap ? refs : nullptr;
     c->hv_refs_cap = refs ? refs_cap : 0;
+    c->hv_runoff = runs_cap && rundep ? runoff : nullptr;
+    c->hv_rundep = runs_cap && runoff ? rundep : nullptr;
+    c->hv_runs_cap = runoff && rundep ? runs_cap : 0;
     c->hv_capid = capture_cap ? capture_ids : nullptr;
     c->hv_sup = capture_cap ? supports : nullptr;
     c->hv_cap_cap = capture_ids && supports ? capture_cap : 0;
