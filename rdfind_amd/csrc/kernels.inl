@@ -1621,6 +1621,221 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_dense_build(const u32* __restrict
     }
 }
 
+// ---- light dependents with identical group lists -------------------------------------------------------------
+// Two captures that occur with exactly the same join values (LUBM: s[o=X] and s[p=P,o=X] when X only occurs as the
+// object of P; 22 % of c2's light group entries belong to such dependents) have the same groups, support, heavy mask
+// and light-group signature, so the light pass would verify the same candidates against the same groups twice.  The
+// smallest compact id of such a class (its representative) is verified; every other member m takes the
+// representative r's verified refs V(r) = out(r) + {r} + triv(r) (r itself and r's trivially implied components pass
+// every test for m: their join sets contain r's), minus m and m's own trivially implied components, which are in V(r)
+// for the same reason (IntersectCindCandidates.scala:40-43 intersects the same groups for both).
+// key of a light dependent (its support, heavy mask, signature words and group count; 0: not a light dependent) -> key,
+// and an open-addressing table (slots 2^k >= 2 C, EMPTY64 = free) of tag << 32 | the smallest dependent of the key: the
+// slot comes from the low bits of the key's hash and the tag from its high 32, so one atomic claims or lowers a slot
+// (two keys sharing a slot and a tag merge; k_dup_verify then finds their lists differ).  Members are often
+// consecutive ids (the same join value under consecutive capture codes): a dependent whose predecessor in the wave has
+// its key leaves the table alone (the predecessor is smaller), which keeps a large class off one slot.
+__device__ inline u64 dup_key(const CindView& v, u32 d) {
+    const CapInfo id = v.info[d];
+    u64 h = mix64(((u64)id.support << 32) ^ (v.doff[d + 1] - v.doff[d])) ^ mix64(id.hmask + 0x9E3779B97F4A7C15ull);
+    if (v.sig) {
+        const u64* sd = v.sig + (u64)d * SIG_W;
+#pragma unroll
+        for (int k = 0; k < SIG_W; ++k) h = mix64(h ^ (sd[k] + (u64)k));
+    }
+    return h ? h : 1;
+}
+__device__ inline u64 dup_tag(u64 hk) {
+    const u64 t = hk >> 32;
+    return (t == 0xffffffffull ? 0xfffffffeull : t) << 32;
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_insert(CindView v, const u32* __restrict__ nchunk_light, u64* key,
+                                                          u64* tab, u64 tmask, u64 min_entries) {
+    const u64 stride = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 d0 = (u64)blockIdx.x * RDF_BLOCK + (threadIdx.x & ~(RDF_WAVE - 1)); d0 < v.C; d0 += stride) {
+        const u64 d = d0 + lane_id();
+        // (only lists of >= min_entries groups, 256 by default: c2's classes average ~2,200 entries per member, and
+        // the short lists' atomics cost more than their light work)
+        const u64 k = d < v.C && nchunk_light[d] && v.doff[d + 1] - v.doff[d] >= min_entries ? dup_key(v, (u32)d) : 0;
+        if (d < v.C) key[d] = k;
+        const u64 kp = __shfl_up(k, 1, RDF_WAVE);
+        if (!k || (lane_id() && kp == k)) continue;
+        const u64 hk = mix64(k), tag = dup_tag(hk), want = tag | d;
+        u64 h = hk & tmask;
+        for (;;) {
+            u64 cur = tab[h];  // a smaller id already there needs no atomic
+            if (cur == EMPTY64)
+                cur = atomicCAS((unsigned long long*)&tab[h], (unsigned long long)EMPTY64, (unsigned long long)want);
+            if (cur == EMPTY64) break;
+            if ((cur & 0xffffffff00000000ull) == tag) {
+                if (want < cur) atomicMin((unsigned long long*)&tab[h], (unsigned long long)want);
+                break;
+            }
+            h = (h + 1) & tmask;
+        }
+    }
+}
+// every light dependent's candidate representative (the smallest id of its key; crep[d] = d when none is smaller) and
+// the 4096-entry chunks of its group list to compare with the representative's (0: nothing to compare)
+static constexpr u64 DUP_CHUNK = 4096;
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_rep(CindView v, const u64* __restrict__ key, const u64* __restrict__ tab,
+                                                       u64 tmask, u32* crep, u32* nchunk, u32* bad) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = key[d];
+        u32 r = (u32)d;
+        if (k) {
+            const u64 hk = mix64(k), tag = dup_tag(hk);
+            u64 h = hk & tmask;
+            while ((tab[h] & 0xffffffff00000000ull) != tag) h = (h + 1) & tmask;
+            r = (u32)tab[h];
+        }
+        const u64 n = v.doff[d + 1] - v.doff[d];
+        if (r != (u32)d && v.doff[r + 1] - v.doff[r] != n) r = (u32)d;  // (the key covers the length; a collision)
+        crep[d] = r;
+        nchunk[d] = r != (u32)d ? (u32)((n + DUP_CHUNK - 1) / DUP_CHUNK) : 0u;
+        bad[d] = 0;
+    }
+}
+// one wave per chunk of a candidate member's group list: any entry that differs from the representative's -> bad[d]
+// (the lists are equal entry for entry exactly when the two captures have the same join values)
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_verify(CindView v, const u32* __restrict__ crep,
+                                                          const u64* __restrict__ ckoff, u32* bad) {
+    const u64 W = ckoff[v.C];
+    const u64 nw = (u64)gridDim.x * RDF_WAVES_PER_BLOCK;
+    for (u64 w = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE; w < W; w += nw) {
+        u32 lo = 0, hi = v.C;  // the member: last d with ckoff[d] <= w
+        while (lo < hi) {
+            const u32 mid = (lo + hi + 1) >> 1;
+            if (ckoff[mid] <= w) lo = mid;
+            else hi = mid - 1;
+        }
+        const u32 d = lo, r = crep[d];
+        const u64 n = v.doff[d + 1] - v.doff[d];
+        const u64 j0 = (w - ckoff[d]) * DUP_CHUNK, j1 = j0 + DUP_CHUNK < n ? j0 + DUP_CHUNK : n;
+        const u32* a = v.dgrp + v.doff[d];
+        const u32* b = v.dgrp + v.doff[r];
+        bool diff = false;
+        for (u64 j = j0 + lane_id(); j < j1; j += 8 * RDF_WAVE) {
+            u32 x[8], y[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const u64 jj = j + (u64)u * RDF_WAVE;
+                x[u] = jj < j1 ? a[jj] : 0u;
+                y[u] = jj < j1 ? b[jj] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) diff |= x[u] != y[u];
+        }
+        if (__any(diff) && lane_id() == 0) bad[d] = 1;
+    }
+}
+// verified members do no light work of their own (a member with a differing list is its own representative); the
+// members are listed in `members` (in any order: their output offsets come from a scan) and counted in *nmembers
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_unplan(u32* crep, const u32* __restrict__ bad, u32 C, u32* nchunk_light,
+                                                          u32* nitem_light, u32* npacked, u32* nmembers, u32* members) {
+    const u64 stride = (u64)gridDim.x * RDF_BLOCK;
+    for (u64 d0 = (u64)blockIdx.x * RDF_BLOCK + (threadIdx.x & ~(RDF_WAVE - 1)); d0 < C; d0 += stride) {
+        const u64 d = d0 + lane_id();
+        bool mem = false;
+        if (d < C) {
+            const u32 r = crep[d];
+            if (r != (u32)d && bad[d]) crep[d] = (u32)d;
+            mem = r != (u32)d && !bad[d];
+            if (mem) nchunk_light[d] = nitem_light[d] = npacked[d] = 0;
+        }
+        const u64 mask = __ballot(mem);
+        if (!mask) continue;
+        u32 base = 0;
+        if (lane_id() == 0) base = atomicAdd(nmembers, (u32)__popcll(mask));
+        base = __shfl(base, 0, RDF_WAVE);
+        if (mem) members[base + __popcll(mask & ((1ull << lane_id()) - 1))] = (u32)d;
+    }
+}
+__device__ inline u32 ntriv(const CindView& v, u32 x) { return x >= v.Cu ? 2u : 0u; }
+// explicit pairs per dependent after the expansion: its own (eoff) or its representative's + 1 + triv(r) - 1 - triv(m)
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_counts(CindView v, const u32* __restrict__ crep, const u64* __restrict__ eoff,
+                                                          u32* cnt) {
+    for (u64 d = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; d < v.C; d += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 r = crep[d];
+        cnt[d] = (u32)(eoff[r + 1] - eoff[r]) + (r != (u32)d ? ntriv(v, r) - ntriv(v, (u32)d) : 0u);
+    }
+}
+// non-members' pairs moved to their new offsets, and their ebin shifted by the same amount
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_move(const u64* __restrict__ pairs, u64 E, u32 C, const u32* __restrict__ crep,
+                                                        const u64* __restrict__ eoff, const u64* __restrict__ ebin,
+                                                        const u64* __restrict__ noff, u64* out, u64* nbin) {
+    for (u64 j = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; j < E || j < C; j += (u64)gridDim.x * RDF_BLOCK) {
+        if (j < E) {
+            const u64 x = pairs[j];
+            const u32 d = (u32)(x >> 32);
+            out[noff[d] + (j - eoff[d])] = x;
+        }
+        if (j < C && crep[j] == (u32)j) nbin[j] = noff[j] + (ebin[j] - eoff[j]);
+    }
+}
+// one wave per member m (representative r): V(r) = out(r) + {r} + triv(r), ascending, without m and triv(m), written at
+// noff[m]; nbin[m] = noff[m] + #{refs < Cu}
+__global__ __launch_bounds__(RDF_BLOCK) void k_dup_expand(u64 nwaves, u64 nm, CindView v, const u32* __restrict__ members,
+                                                          const u32* __restrict__ crep, const u64* __restrict__ pairs,
+                                                          const u64* __restrict__ eoff, const u64* __restrict__ ebin,
+                                                          const u64* __restrict__ noff, u64* out, u64* nbin) {
+    const u64 w0 = (u64)blockIdx.x * RDF_WAVES_PER_BLOCK + threadIdx.x / RDF_WAVE;
+    for (u64 w = w0; w < nm; w += nwaves) {
+        const u64 m = members[w];
+        const u32 r = crep[m];
+        // the extras (r and its components) and the exclusions (m and its components): at most 3 each
+        u32 ex[3], ne = 0, xs[3], nx = 0;
+        ex[ne++] = r;
+        if (r >= v.Cu) {
+            ex[ne++] = v.bcomp[2ull * (r - v.Cu)];
+            ex[ne++] = v.bcomp[2ull * (r - v.Cu) + 1];
+        }
+        xs[nx++] = (u32)m;
+        if (m >= v.Cu) {
+            xs[nx++] = v.bcomp[2ull * (m - v.Cu)];
+            xs[nx++] = v.bcomp[2ull * (m - v.Cu) + 1];
+        }
+        const u64 b = eoff[r], n = eoff[r + 1] - b;
+        const u64 base = noff[m];
+        const u64 hi = m << 32;
+        // a ref x of V(r) goes to rank(x) = #{V(r) < x} - #{exclusions < x}
+        for (u64 i = lane_id(); i < n; i += RDF_WAVE) {
+            const u32 x = (u32)pairs[b + i];
+            bool drop = false;
+            u32 below = (u32)i;
+            for (u32 k = 0; k < ne; ++k) below += ex[k] < x;
+            for (u32 k = 0; k < nx; ++k) {
+                below -= xs[k] < x;
+                drop |= xs[k] == x;
+            }
+            if (!drop) out[base + below] = hi | x;
+        }
+        if (lane_id() < ne) {
+            const u32 x = ex[lane_id()];
+            bool drop = false;
+            u32 lo = 0, h2 = (u32)n;  // #out(r) < x
+            while (lo < h2) {
+                const u32 mid = (lo + h2) >> 1;
+                if ((u32)pairs[b + mid] < x) lo = mid + 1;
+                else h2 = mid;
+            }
+            u32 below = lo;
+            for (u32 k = 0; k < ne; ++k) below += ex[k] < x;
+            for (u32 k = 0; k < nx; ++k) {
+                below -= xs[k] < x;
+                drop |= xs[k] == x;
+            }
+            if (!drop) out[base + below] = hi | x;
+        }
+        if (lane_id() == 0) {  // refs below Cu: V(r)'s minus the exclusions'
+            u32 below = (u32)(ebin[r] - b);
+            for (u32 k = 0; k < ne; ++k) below += ex[k] < v.Cu;
+            for (u32 k = 0; k < nx; ++k) below -= xs[k] < v.Cu;
+            nbin[m] = base + below;
+        }
+    }
+}
+
 // candidate filter: the i-th member of the pivot group (or NONE)
 __device__ inline u32 pivot_candidate(const CindView& v, u32 d, const CapInfo& id, u32 piv, u64 i) {
     if (v.vcoff) {  // sharded verify pass: the candidates are given (already filtered by the pivot holder)

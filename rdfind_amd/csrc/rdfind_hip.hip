@@ -75,6 +75,13 @@ struct rdf_ctx {
     bool jr_keep = false, range_keep = true;
     u64 peak_bytes = 0;              // RDFIND_MEM_REPORT: the largest sum of the buffers' sizes so far
     DevBuf jrmap;                    // the kept range build: the ranges' first join values and first join buckets
+    // light dependents with identical group lists (d_light_dedup): keys, key table, class representatives, counts
+    DevBuf ukey, utab, urep, ucnt, unoff, uebin, umem;
+    u32 dup_min = 256;               // RDFIND_DUP_MIN: the shortest group list that looks for an equal one
+    int light_dedup = -1;            // RDFIND_LIGHT_DEDUP: 0 every light dependent verified on its own, 1 once per class
+                                     // of equal group lists, unset: classes where the light pass stages (c2-like inputs)
+    u64 n_dedup_members = 0;         // light dependents that took their representative's refs (last discovery)
+    bool dedup_pending = false;      // d_light_dedup ran: d_dedup_expand reads the member count
     bool sh_ranged = false;          // the sharded build of this run goes in join ranges (sh_phase14 -> sh_phase1)
     u64 sh_m = 0;                    // sharded: triples received for this rank's join shard (wts / wtp / wto)
     std::string test_fail_launch;    // RDFIND_TEST_FAIL_LAUNCH: a kernel launched with an invalid configuration (test hook)
@@ -453,11 +460,11 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
-            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore, &c->jbh, &c->iflag, &c->iexcl, &c->iorder};
+            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore, &c->jbh, &c->iflag, &c->iexcl, &c->iorder, &c->ukey, &c->utab, &c->urep, &c->ucnt, &c->unoff, &c->uebin, &c->umem};
 }
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
-static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder"};
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder", "ukey", "utab", "urep", "ucnt", "unoff", "uebin", "umem"};
 static bool mem_report_on() {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
     return on;
@@ -523,6 +530,8 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     }
     if (const char* hb = getenv("RDFIND_HOT_BALANCE")) c->hot_balance = atoi(hb) != 0;
     if (const char* rk = getenv("RDFIND_RANGE_KEEP")) c->range_keep = atoi(rk) != 0;
+    if (const char* ld = getenv("RDFIND_LIGHT_DEDUP")) c->light_dedup = atoi(ld) != 0 ? 1 : 0;
+    if (const char* dm = getenv("RDFIND_DUP_MIN")) c->dup_min = (u32)std::max(1, atoi(dm));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
@@ -2733,8 +2742,9 @@ static rdf_status d_light_two_pass(rdf_ctx* c, const CindView& v, u64 WI, u64 WL
 }
 
 // sort the explicit pairs (epairs[0, E)) and index them: v.eoff / v.ebin / v.epairs
-// (presorted: the single-GPU light pass already emits them in (dep, ref) order, chunk by chunk)
-static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorted) {
+// (presorted: the single-GPU light pass already emits them in (dep, ref) order, chunk by chunk; indexed: eoff / ebin
+// are already those of epairs[0, E), d_dedup_expand)
+static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorted, bool indexed = false) {
     hipStream_t st = c->stream;
     const u32 C = c->C;
     if (!presorted) ENSURE(c, epairs_tmp, std::max<u64>(E, 1) * 8);
@@ -2747,8 +2757,9 @@ static rdf_status d_explicit_index(rdf_ctx* c, CindView& v, u64 E, bool presorte
     }
     ENSURE(c, eoff, (C + 1ull) * 8);
     ENSURE(c, ebin, std::max<u64>(C, 1) * 8);
-    hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
-                       c->epairs.as<u64>(), E, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
+    if (!indexed)
+        hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                           c->epairs.as<u64>(), E, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
     tend(c, RDF_T_ESORT);
     c->sort_passes_pairs = presorted ? 0 : (u64)radix_sort_passes(32 + bits_for(C ? C - 1 : 0)) * E;
     v.eoff = c->eoff.as<u64>();
@@ -3042,6 +3053,102 @@ static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 W
     return RDF_OK;
 }
 
+// Light dependents with identical group lists (k_dup_*, kernels.inl): after the pivot pass the members of every class
+// lose their light items (only the representative, the class's smallest compact id, is verified); after the light pass
+// their explicit pairs are derived from the representative's (d_dedup_expand).  Strategy 1 without association rules
+// (the strategy-0 quirk and the rules' per-pair drop are per dependent), one GPU, unpaged.
+static rdf_status d_light_dedup(rdf_ctx* c, const CindView& v) {
+    c->n_dedup_members = 0;
+    c->dedup_pending = false;
+    const u32 C = c->C;
+    // automatic: only inputs whose light pass takes the LDS-staging variant (small light groups) have enough such
+    // classes to pay for finding them (c2: 22 % of the light group entries, light 2.02 -> 1.80 ms, step -0.08 ms; c3
+    // and c4 at 0.4: ~2.5 %, no gain; profiles/r06_light_dedup_ab.log).  The member count waits in scalar slot 9
+    // (which no light-pass stage uses) until d_dedup_expand reads it with the pair count
+    const bool on = c->light_dedup < 0 ? c->light_stage : c->light_dedup != 0;
+    if (!on || v.literal || v.ar || c->nranks != 1 || !C) return RDF_OK;
+    hipStream_t st = c->stream;
+    const u64 tcap = next_pow2(2ull * C + 16);
+    ENSURE(c, ukey, (u64)C * 8);
+    ENSURE(c, utab, tcap * 8);
+    ENSURE(c, urep, (u64)C * 4);
+    tbegin(c, RDF_T_PIVOT);
+    HIP_TRY(c, hipMemsetAsync(c->utab.p, 0xff, tcap * 8, st));
+    HIP_TRY(c, hipMemsetAsync(dscal(c, 9), 0, 8, st));
+    const dim3 g(grid_for(C, RDF_BLOCK, kGrid));
+    hipLaunchKernelGGL(k_dup_insert, g, dim3(RDF_BLOCK), 0, st, v, c->nchl.as<u32>(), c->ukey.as<u64>(), c->utab.as<u64>(),
+                       tcap - 1, (u64)c->dup_min);
+    ENSURE(c, ucnt, (u64)C * 4);
+    ENSURE(c, unoff, (C + 1ull) * 8);
+    ENSURE(c, eoff, (C + 1ull) * 8);  // (scratch here: the members' chunk offsets; the explicit index rewrites it)
+    hipLaunchKernelGGL(k_dup_rep, g, dim3(RDF_BLOCK), 0, st, v, c->ukey.as<u64>(), c->utab.as<u64>(), tcap - 1,
+                       c->urep.as<u32>(), c->ucnt.as<u32>(), (u32*)c->unoff.p);
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ucnt.as<u32>(), c->eoff.as<u64>(), C, c->eoff.as<u64>() + C, st));
+    // (the chunk count stays on the device: a grid-stride verify pass instead of a read-back)
+    hipLaunchKernelGGL(k_dup_verify, dim3(kGrid), dim3(RDF_BLOCK), 0, st, v, c->urep.as<u32>(), c->eoff.as<u64>(),
+                       (u32*)c->unoff.p);
+    ENSURE(c, umem, (u64)C * 4);
+    hipLaunchKernelGGL(k_dup_unplan, g, dim3(RDF_BLOCK), 0, st, c->urep.as<u32>(), (const u32*)c->unoff.p, C,
+                       c->nchl.as<u32>(), c->nitl.as<u32>(), c->npk.as<u32>(), (u32*)dscal(c, 9), c->umem.as<u32>());
+    HIP_TRY(c, hipGetLastError());
+    tend(c, RDF_T_PIVOT);
+    c->dedup_pending = true;  // the member count is read with the expansion's pair count (d_dedup_expand)
+    return RDF_OK;
+}
+
+// the members' explicit pairs from their representatives' (V(r) minus the member and its components), every pair in
+// (dependent, ref) order again; *E grows by the members' pairs.  The new index (eoff = the scanned counts, ebin shifted
+// by the same offsets) is written here, so d_explicit_index need not search the pairs again (*indexed)
+static rdf_status d_dedup_expand(rdf_ctx* c, const CindView& v, u64* E, bool* indexed) {
+    *indexed = false;
+    if (!c->dedup_pending) return RDF_OK;
+    c->dedup_pending = false;
+    hipStream_t st = c->stream;
+    const u32 C = c->C;
+    const u64 E0 = *E;
+    ENSURE(c, eoff, (C + 1ull) * 8);
+    ENSURE(c, ebin, std::max<u64>(C, 1) * 8);
+    ENSURE(c, ucnt, (u64)C * 4);
+    ENSURE(c, unoff, (C + 1ull) * 8);
+    ENSURE(c, uebin, std::max<u64>(C, 1) * 8);
+    tbegin(c, RDF_T_ESORT);
+    hipLaunchKernelGGL(k_pair_offsets, dim3(grid_for(C + 1ull, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->epairs.as<u64>(), E0, C, c->Cu, c->eoff.as<u64>(), c->ebin.as<u64>());
+    hipLaunchKernelGGL(k_dup_counts, dim3(grid_for(C, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, v, c->urep.as<u32>(),
+                       c->eoff.as<u64>(), c->ucnt.as<u32>());
+    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->ucnt.as<u32>(), c->unoff.as<u64>(), C, c->unoff.as<u64>() + C, st));
+    tend(c, RDF_T_ESORT);
+    ScalarGather sg = {};  // one read-back: the expanded pair count and the member count
+    sg.p[0] = c->unoff.as<u64>() + C;
+    sg.bytes[0] = 8;
+    sg.p[1] = dscal(c, 9);
+    sg.bytes[1] = 4;
+    sg.n = 2;
+    u64 rb[2] = {0, 0};
+    TRY(gather_read(c, sg, rb));
+    const u64 E1 = rb[0];
+    c->n_dedup_members = rb[1];
+    if (!c->n_dedup_members) return RDF_OK;  // (E1 == E0: nothing moves)
+    ENSURE(c, epairs_tmp, std::max<u64>(E1, 1) * 8);
+    tbegin(c, RDF_T_ESORT);
+    hipLaunchKernelGGL(k_dup_move, dim3(grid_for(std::max<u64>(E0, C), RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
+                       c->epairs.as<u64>(), E0, C, c->urep.as<u32>(), c->eoff.as<u64>(), c->ebin.as<u64>(),
+                       c->unoff.as<u64>(), c->epairs_tmp.as<u64>(), c->uebin.as<u64>());
+    const u64 nm = c->n_dedup_members;
+    const unsigned eg = grid_for(nm, RDF_WAVES_PER_BLOCK, 4 * kGrid);
+    hipLaunchKernelGGL(k_dup_expand, dim3(eg), dim3(RDF_BLOCK), 0, st, (u64)eg * RDF_WAVES_PER_BLOCK, nm, v,
+                       c->umem.as<u32>(), c->urep.as<u32>(), c->epairs.as<u64>(), c->eoff.as<u64>(), c->ebin.as<u64>(),
+                       c->unoff.as<u64>(), c->epairs_tmp.as<u64>(), c->uebin.as<u64>());
+    HIP_TRY(c, hipGetLastError());
+    tend(c, RDF_T_ESORT);
+    std::swap(c->epairs, c->epairs_tmp);
+    std::swap(c->eoff, c->unoff);
+    std::swap(c->ebin, c->uebin);
+    *E = E1;
+    *indexed = true;
+    return RDF_OK;
+}
+
 rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats) {
     if (!c) return RDF_ERR_ARG;
     if (c->stage < 3) return fail(c, RDF_ERR_STATE, "rdf_build_capture_groups must be called first");
@@ -3073,6 +3180,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
         hipLaunchKernelGGL(k_sum_partials3, dim3(1), dim3(RDF_BLOCK), 0, st, c->ppart.as<u64>(), gp, dscal(c, 2));
     }
     tend(c, RDF_T_PIVOT);
+    TRY(d_light_dedup(c, v));
     u64 WL = 0, WH = 0, WI = 0, WP = 0, E = 0, H = 0, HC = 0, NT = 0;
     TRY(d_multi_items(c));
     TRY(d_chunks(c, &WL, &WH, &WI, &WP));
@@ -3080,13 +3188,15 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     const bool two = use_two_pass(c, WI);
     if (two) TRY(d_light_two_pass(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
     else TRY(d_light(c, v, WI, WL, WP, &E, c->pivot.as<u32>()));
+    bool indexed = false;
+    TRY(d_dedup_expand(c, v, &E, &indexed));
     if (getenv("RDFIND_LIGHT2_LOG"))
         fprintf(stderr, "LIGHT2 two=%d items=%llu multi_chunk_items=%llu survivors=%llu explicit=%llu\n",
                 (int)two, (unsigned long long)WI, (unsigned long long)c->n_multi_items,
                 (unsigned long long)c->n_light_survivors, (unsigned long long)E);
     c->n_explicit_raw = E;
     c->n_light_chunks = WL;
-    TRY(d_explicit_index(c, v, E, true));
+    TRY(d_explicit_index(c, v, E, true, indexed));
     // the explicit pairs' rules first: their refs are final before the class stage, so an early hand-over copies them
     // while the classes and the heavy-only dependents are computed
     u64 K = 0;

@@ -831,3 +831,36 @@ def test_early_handover_matches_plain_copy():
         assert seen_early > 0
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("dedup,dup_min", [("0", "256"), ("1", "1"), ("1", "256")])
+def test_light_dedup_parity(monkeypatch, dedup, dup_min):
+    """Light dependents with identical group lists verified once per class (RDFIND_LIGHT_DEDUP=1; members take their
+    representative's refs minus themselves and their trivially implied components) or each on its own (0): random
+    inputs with many equal join sets in every mode, with the heavy columns lowered too, and c1 / c5 samples, equal the
+    oracle.  The strategy-0 quirk and --use-ars keep per-dependent verification (the filters are per dependent).
+    RDFIND_DUP_MIN=1 lets every light dependent look for an equal list (the default, 256 groups, leaves the random
+    inputs' short lists alone)."""
+    monkeypatch.setenv("RDFIND_LIGHT_DEDUP", dedup)
+    monkeypatch.setenv("RDFIND_DUP_MIN", dup_min)
+    for heavy_min in ("64", "2"):
+        monkeypatch.setenv("RDFIND_HEAVY_MIN", heavy_min)
+        g = _lib.Context(0)
+        try:
+            rng = random.Random(600 + int(heavy_min))
+            for _ in range(30):
+                n = rng.randrange(1, 400)
+                nv = rng.randrange(2, 40)
+                ms = rng.randrange(1, 4)
+                arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
+                               dtype=np.uint32)
+                for strategy, clean in MODES:
+                    assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean), \
+                        (n, nv, ms, strategy, clean, dedup, heavy_min)
+            for cfg, scale in (("c1", 0.05), ("c5", 0.01), ("c2", 0.02)):
+                d = dataset(cfg, scale)
+                g.set_triples(d.s, d.p, d.o, d.num_terms)
+                g.run(d.min_support)
+                assert_stream_matches(g, cfg, scale, what=(dedup, heavy_min))
+        finally:
+            g.close()

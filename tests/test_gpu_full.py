@@ -194,13 +194,16 @@ print(json.dumps(out))
                                  {"RDFIND_SWEEP_F": "0"}, {"RDFIND_SWEEP_F": "1000000000"},
                                  {"RDFIND_SWEEP_F": "1000000000", "RDFIND_LIGHT2": "1", "RDFIND_DENSE": "0"},
                                  {"RDFIND_LIGHT_HIOCC": "1"}, {"RDFIND_LIGHT_HIOCC": "0"}, {"RDFIND_PIVX": "0"},
+                                 {"RDFIND_LIGHT_DEDUP": "0"}, {"RDFIND_LIGHT_DEDUP": "1"},
+                                 {"RDFIND_LIGHT_DEDUP": "1", "RDFIND_DUP_MIN": "1"},
                                  {"RDFIND_PIVX_N": "2"}, {"RDFIND_PIVX_PACKED": "1"}])
 def test_light_variants_full_size(ctx, env):
     """The light pass's alternative code paths (LDS-staged small groups or not, signature filter off / on both
     paths, second pivot off / k_light only, dense-group bitmaps off / for groups of >= C/256 members, the filter and
     verify passes forced instead of one light pass (with and without bitmaps), window range sweeps
     never / whenever many candidates are alive, the plain variant at 6 waves per SIMD forced on / off, no extra pivots /
-    two) each reproduce the c1 and c2 golden vectors (and c4 at 0.1 for the sweep, two-pass, occupancy and pivot
+    two, every light dependent verified on its own instead of once per class of equal group lists, or every list of
+    any length looking for an equal one) each reproduce the c1 and c2 golden vectors (and c4 at 0.1 for the sweep, two-pass, occupancy and pivot
     switches).  The switches are read
     once per process, so each combination runs in its own child process."""
     import subprocess
@@ -209,7 +212,7 @@ def test_light_variants_full_size(ctx, env):
     ctx.release_scratch()  # the module context's buffers from the full-size runs (c5 at 0.3: ~100 GB) would starve the child
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     keys = ["c1@1.0/s1_clean", "c2@1.0/s1_clean"]
-    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT2", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N",
+    if {"RDFIND_SWEEP_F", "RDFIND_LIGHT2", "RDFIND_LIGHT_HIOCC", "RDFIND_PIVX", "RDFIND_PIVX_N", "RDFIND_LIGHT_DEDUP",
             "RDFIND_PIVX_PACKED"} & set(env):  # c4 runs these
         keys.append("c4@0.1/s1_clean")
     jobs = [(GOLD[key], dataset_npz(GOLD[key]["config"], GOLD[key]["scale"])) for key in keys]
