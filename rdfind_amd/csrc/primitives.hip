@@ -119,6 +119,47 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply(const TI* in, TO* out,
     }
 }
 
+// up to SCAN_FOLD_TILES tiles: each apply block sums the tile totals before it itself (<= 1024 L2 loads shared by the
+// block) instead of a k_scan_single launch between reduce and apply; the last block writes the grand total
+static constexpr u64 SCAN_FOLD_TILES = 1024;
+template <typename TI, typename TO>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply_fold(const TI* in, TO* out, u64 n, const TO* __restrict__ tile_sums,
+                                                               TO* __restrict__ grand_total) {
+    __shared__ TO lds[SCAN_TILE];
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        lds[i * RDF_BLOCK + threadIdx.x] = (idx < n) ? (TO)in[idx] : (TO)0;
+    }
+    TO before = 0;
+    for (u32 t = threadIdx.x; t < blockIdx.x; t += RDF_BLOCK) before += tile_sums[t];
+    TO prior;
+    block_exclusive_scan<TO>(before, lds_wave, &prior);  // (the block's sum of the earlier tiles' totals)
+    TO v[SCAN_ITEMS];
+    TO local = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        v[i] = lds[threadIdx.x * SCAN_ITEMS + i];
+        local += v[i];
+    }
+    TO total;
+    TO off = block_exclusive_scan<TO>(local, lds_wave, &total) + prior;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        lds[threadIdx.x * SCAN_ITEMS + i] = off;
+        off += v[i];
+    }
+    if (grand_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *grand_total = prior + total;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        if (idx < n) out[idx] = lds[i * RDF_BLOCK + threadIdx.x];
+    }
+}
+
 // small inputs (a few tiles): one block scans in -> out with a running carry (one launch instead of three)
 template <typename TI, typename TO>
 __global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* in, TO* out, u64 n,
@@ -163,6 +204,11 @@ static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 
     TO* sums = (TO*)ws.scratch(tiles * sizeof(TO), 0);
     if (!sums) return hipErrorOutOfMemory;
     hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, n, sums);
+    if (tiles <= SCAN_FOLD_TILES) {
+        hipLaunchKernelGGL((k_scan_apply_fold<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n, sums,
+                           d_total);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((k_scan_single<TO>), dim3(1), dim3(RDF_BLOCK), 0, st, sums, tiles, d_total);
     hipLaunchKernelGGL((k_scan_apply<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n, sums);
     return hipGetLastError();
@@ -276,7 +322,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
 template <int DB, bool HASH = false>
 __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
                                                              int shift, int w, const u32* __restrict__ offs,
-                                                             u32 num_tiles, int drop, u64 hmask) {
+                                                             const u32* __restrict__ rowtot, u32 num_tiles, int drop,
+                                                             u64 hmask, u32* d_kept) {
     constexpr u32 NBIN = 1u << DB;
     constexpr u32 PER = NBIN / RDF_BLOCK;  // digits per thread in the tile scan (1, 2 or 4)
     static_assert(NBIN % RDF_BLOCK == 0, "digit bins must be a multiple of the block");
@@ -291,12 +338,28 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     const u32 nbin = 1u << w, dmask = nbin - 1u;
     for (u32 i = threadIdx.x; i < RDF_WAVES_PER_BLOCK * NBIN; i += RDF_BLOCK) (&wcount[0][0])[i] = 0;
     const u32 tile = rs_tile();
-    for (u32 b = threadIdx.x; b < nbin; b += RDF_BLOCK) gbase[b] = offs[(u64)b * num_tiles + tile];
     const u64 tbase = (u64)tile * RS_TILE;
     const u64 tn = n - tbase < (u64)RS_TILE ? n - tbase : (u64)RS_TILE;
-    {   // stage the tile through LDS: 16-byte global loads, then each wave reads its contiguous sub-range
+    {   // stage the tile through LDS: 16-byte global loads, then each wave reads its contiguous sub-range; while they
+        // are in flight, the digits' bases (exclusive scan of the row totals, PER digits a thread) + the row prefixes
         u64 kin[RS_ITEMS];
         load_tile_pairs(keys, n, tbase, kin);
+        u32 rt[PER], ro[PER], local = 0;
+#pragma unroll
+        for (u32 q = 0; q < PER; ++q) {
+            const u32 dg = threadIdx.x * PER + q;
+            rt[q] = dg < nbin ? rowtot[dg] : 0u;
+            ro[q] = dg < nbin ? offs[(u64)dg * num_tiles + tile] : 0u;
+            local += rt[q];
+        }
+        u32 total;
+        u32 off = block_exclusive_scan<u32>(local, lds_wave, &total);
+#pragma unroll
+        for (u32 q = 0; q < PER; ++q) {
+            gbase[threadIdx.x * PER + q] = off + ro[q];
+            off += rt[q];
+        }
+        if (d_kept && tile == 0 && threadIdx.x == 0) *d_kept = total;
 #pragma unroll
         for (int r = 0; r < RS_ITEMS / 2; ++r) {
             const u32 p = 2u * ((u32)r * RDF_BLOCK + threadIdx.x);
@@ -367,18 +430,82 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     }
 }
 
+// The digit-major histogram's rows scanned in place, one 1024-thread block per digit (exclusive within the row: the
+// digit's keys in earlier tiles; c2's rows of 14.4k tiles in one step), each row's total to rowtot[digit].  The scatter
+// blocks scan the totals into the digits' bases themselves (a few hundred L2 loads, issued behind the tile's key
+// loads), so a pass is three launches instead of the five of a device-wide scan (c2: 21 passes per step spent ~35 us
+// each in reduce / single / apply)
+static constexpr int RS_SCAN_THREADS = 1024;
+static constexpr int RS_SCAN_ITEMS = 16;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(RS_SCAN_THREADS) void k_radix_rowscan(u32* __restrict__ hist, u32 row_stride, u32 num_tiles,
+                                                                   u32* rowtot) {
+    constexpr int NW = RS_SCAN_THREADS / RDF_WAVE;
+    constexpr u32 STEP = RS_SCAN_THREADS * RS_SCAN_ITEMS;
+    __shared__ u32 lds_wave[NW];
+    const int lane = lane_id(), wave = threadIdx.x / RDF_WAVE;
+    u32* row = hist + (u64)blockIdx.x * row_stride;  // (rows 16-B aligned: the stride is a multiple of 4)
+    u32 carry = 0;
+    for (u32 b0 = 0; b0 < num_tiles; b0 += STEP) {
+        u32 v[RS_SCAN_ITEMS];
+        u32 local = 0;
+        const u32 tb = b0 + threadIdx.x * RS_SCAN_ITEMS;
+#pragma unroll
+        for (int i = 0; i < RS_SCAN_ITEMS; i += 4) {
+            u32x4_t x = tb + i < row_stride ? *(const u32x4_t*)(row + tb + i) : u32x4_t{0u, 0u, 0u, 0u};
+            v[i] = tb + i < num_tiles ? x.x : 0u;  // (the padding past num_tiles reads as 0)
+            v[i + 1] = tb + i + 1 < num_tiles ? x.y : 0u;
+            v[i + 2] = tb + i + 2 < num_tiles ? x.z : 0u;
+            v[i + 3] = tb + i + 3 < num_tiles ? x.w : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < RS_SCAN_ITEMS; ++i) local += v[i];
+        u32 incl = local;
+#pragma unroll
+        for (int off = 1; off < RDF_WAVE; off <<= 1) {
+            const u32 t = __shfl_up(incl, off, RDF_WAVE);
+            if (lane >= off) incl += t;
+        }
+        if (lane == RDF_WAVE - 1) lds_wave[wave] = incl;
+        __syncthreads();
+        u32 woff = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const u32 x = lds_wave[w];
+            woff += w < wave ? x : 0u;
+            total += x;
+        }
+        __syncthreads();
+        u32 off = carry + woff + incl - local;
+#pragma unroll
+        for (int i = 0; i < RS_SCAN_ITEMS; i += 4) {
+            u32x4_t x;
+            x.x = off;
+            x.y = off + v[i];
+            x.z = x.y + v[i + 1];
+            x.w = x.z + v[i + 2];
+            off = x.w + v[i + 3];
+            if (tb + i < row_stride) *(u32x4_t*)(row + tb + i) = x;
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) rowtot[blockIdx.x] = carry;
+}
+
+static inline u32 hist_stride(u32 tiles) { return (tiles + 3u) & ~3u; }
 template <int DB, bool HASH = false>
 static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, int shift, int w, u32* hist, u32 tiles,
                              hipStream_t st, u32* d_kept = nullptr, u64 hmask = 0) {
-    const u64 hn = (u64)tiles << w;
     const int drop = d_kept ? 1 : 0;
-    hipLaunchKernelGGL((k_radix_count<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, tiles, drop,
+    u32* rowtot = (u32*)ws.scratch(1024 * sizeof(u32), 2);
+    if (!rowtot) return hipErrorOutOfMemory;
+    const u32 rs = hist_stride(tiles);  // the histogram's digit rows, 16-B aligned
+    hipLaunchKernelGGL((k_radix_count<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, rs, drop,
                        hmask);
-    hipError_t e = exclusive_scan_u32(ws, hist, hist, hn, d_kept, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_radix_scatter<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, tiles,
-                       drop, hmask);
-    return hipSuccess;
+    hipLaunchKernelGGL(k_radix_rowscan, dim3(1u << w), dim3(RS_SCAN_THREADS), 0, st, hist, rs, tiles, rowtot);
+    hipLaunchKernelGGL((k_radix_scatter<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, rowtot,
+                       rs, drop, hmask, d_kept);
+    return hipGetLastError();
 }
 
 // Widest digit of a sort: RS_MAX_BITS (9).  10-bit digits saving a pass measured slower (c4 at 10^9 triples sorts its
@@ -403,7 +530,7 @@ hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int 
     const int passes = (bits + dmax - 1) / dmax;
     const int w0 = bits / passes + (0 < bits % passes ? 1 : 0);
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
-    u32* hist = (u32*)ws.scratch(((u64)tiles << dmax) * sizeof(u32), 1);
+    u32* hist = (u32*)ws.scratch(((u64)hist_stride(tiles) << dmax) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
     hipError_t e = w0 <= 8 ? radix_pass<8>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept)
                  : w0 == 9 ? radix_pass<9>(ws, keys, tmp, n, 0, w0, hist, tiles, st, d_kept)
@@ -430,7 +557,7 @@ static hipError_t radix_sort_dmax(Workspace& ws, u64*& keys, u64*& tmp, u64 n, i
     const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
     const int bits = hi - lo;
     const int passes = (bits + dmax - 1) / dmax;
-    u32* hist = (u32*)ws.scratch(((u64)tiles << dmax) * sizeof(u32), 1);
+    u32* hist = (u32*)ws.scratch(((u64)hist_stride(tiles) << dmax) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
     int shift = lo;
     for (int p = 0; p < passes; ++p) {
@@ -461,7 +588,7 @@ hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, i
     // 1,024-bin digit leaves ~4 keys per bin of a tile; RDFIND_PART_DIGIT overrides, 8..10)
     static const int pdig = getenv("RDFIND_PART_DIGIT") ? std::max(8, std::min(10, atoi(getenv("RDFIND_PART_DIGIT")))) : 9;
     const int passes = (bits + pdig - 1) / pdig;
-    u32* hist = (u32*)ws.scratch(((u64)tiles << 10) * sizeof(u32), 1);
+    u32* hist = (u32*)ws.scratch(((u64)hist_stride(tiles) << 10) * sizeof(u32), 1);
     if (!hist) return hipErrorOutOfMemory;
     int shift = 64 - bits;
     for (int p = 0; p < passes; ++p) {
