@@ -150,7 +150,8 @@ def test_c4_full_size_one_gpu(ctx):
     records exceed one sort's u32 offsets, so the capture groups are built in join-value ranges (the reference's
     sort-based groupBy spills instead, ALG/programs/RDFind.scala:339-345).  One run, checked against the streamed
     oracle's golden vector (stage counts, count, checksum), through the compact hand-over expanded by the checker, and
-    by sampled CINDs verified on the triples.  Other range splits are parity-tested at c4 at 0.1
+    by sampled CINDs verified on the triples; then run again in the same context, which must give the same ranges,
+    records, count and checksum.  Other range splits are parity-tested at c4 at 0.1
     (test_join_ranges_full_size_vs_oracle) and on random inputs (test_gpu.py::test_join_range_groups_parity)."""
     from oracle import c_oracle as C
 
@@ -168,6 +169,11 @@ def test_c4_full_size_one_gpu(ctx):
     n, h, kind = C.checksum_compact(ctx.copy_result_compact(), d.num_terms)
     assert (n, h, kind) == (g["n_cinds"], int(g["checksum"]), g["n_kind"])
     _sample_verify(ctx, d, 10, 4)
+    # determinism at the scale where the records exceed 2^32: a second run in the same context (kept-store ranges, the
+    # buffers of the first run reused) gives the same ranges, records and result
+    first = (ctx.groups["n_join_ranges"], ctx.groups["n_records"], ctx.cind_count(), ctx.checksum())
+    ctx.run(d.min_support)
+    assert (ctx.groups["n_join_ranges"], ctx.groups["n_records"], ctx.cind_count(), ctx.checksum()) == first
 
 
 _VARIANT_CHILD = r"""
