@@ -51,11 +51,12 @@ FAMILY_KERNELS = {
     "unary": ["k_u2_part", "k_u2_slices", "k_u2_count", "k_u2_finish", "k_u2_fval"],
     "binary": ["k_b2_part", "k_b2_slices", "k_b2_count", "k_spill_insert", "k_bin_freq_flags", "k_bin_freq_scatter",
                "k_bin_lookup_build"],
-    "emit": ["k_emit_records"],
-    "support": ["k_fresh_bounds", "k_run_support", "k_support_flags", "k_compact_captures", "k_skip_counts",
-                "k_keep_scatter"],
+    "emit": ["k_emit_records", "k_emit_compact"],
+    "support": ["k_fresh_bounds", "k_cstart_fix", "k_run_support", "k_support_flags", "k_compact_captures",
+                "k_skip_counts", "k_keep_scatter"],
     "groups": ["k_key_offsets", "k_group_flags", "k_group_build", "k_dgrp"],
-    "pivot": ["k_group_info", "k_pivot_nseg", "k_pivot_short", "k_pivot_seg", "k_pivot_final"],
+    "pivot": ["k_group_info", "k_pivot_nseg", "k_pivot_short", "k_pivot_seg", "k_pivot_final", "k_dup_insert", "k_dup_rep",
+              "k_dup_verify", "k_dup_unplan"],
     "light": ["k_light", "k_light_stage", "k_light_plain", "k_light_packed", "k_light_mseg_emit", "k_mseg_chunks", "k_slot_compact"],
     "rules": ["k_rules_explicit", "k_rules_mark", "k_compact_refs"],
     "cemit": ["k_class_emit"],

@@ -34,6 +34,8 @@ static constexpr int B2_SLOTS = 4096;          // LDS hash slots of a K2 countin
 static constexpr u64 B2_BIG = 64ull << 20;     // above 3n = 64M keys, one more bucket bit per doubling (fewer
                                                // multi-slice buckets, which go to the spill table)
 static constexpr int B2_PBLOCK = 1024;         // threads of a K2 histogram / scatter block
+static constexpr u64 U1_RADIX_MIN = 1ull << 27;  // K1 groups u32 keys with radix passes (k_u1_keys) from 3n keys
+static constexpr u64 U1_RADIX_LDS = 80u << 10;   // ... when the partition passes' bucket counters exceed this LDS
 static constexpr u64 B2_RADIX_MIN = 1ull << 27;  // 3n from which K2 groups compact records with the radix passes
                                                  // (k_b2_emit; RDFIND_B2_RADIX_MIN overrides)
 
@@ -192,9 +194,10 @@ __device__ inline void u2_ranks(const u32* lc, u32 lim, u32 ms, u64 base, u64 V,
 }
 
 // one block per (bucket, slice) of the compact slice list soff (exclusive scan of nsl); ghist = scanned
-// bucket-major histogram (G blocks per bucket)
-template <int BITS>
-__global__ __launch_bounds__(U2_CBLOCK) void k_u2_count(const uint16_t* __restrict__ recs, const u32* __restrict__ ghist,
+// bucket-major histogram (G blocks per bucket).  Records: the u16 low key bits of the partition passes, or (RT = u32,
+// large inputs, fc_unary_part's radix form) whole keys grouped by bucket, G = 1
+template <int BITS, typename RT = uint16_t>
+__global__ __launch_bounds__(U2_CBLOCK) void k_u2_count(const RT* __restrict__ recs, const u32* __restrict__ ghist,
                                                         const u32* __restrict__ soff, u32 NB, u32 G, u64 K, u32 V, u32 ms,
                                                         u32* frank, u32* bfreq, u32* fstage, u64* fbits, u64* nbound,
                                                         u32* cntg, int counts_only) {
@@ -215,24 +218,29 @@ __global__ __launch_bounds__(U2_CBLOCK) void k_u2_count(const uint16_t* __restri
     const u64 s0 = start + len * j / nsl, s1 = start + len * (j + 1) / nsl;
     for (u32 i = threadIdx.x; i < R; i += U2_CBLOCK) lc[i] = 0;
     __syncthreads();
-    // records in 16-B vectors (8 per lane) between the unaligned head and tail
-    const u64 a0 = (s0 + 7) & ~7ull, a1 = s1 & ~7ull;
+    // records in 16-B vectors (8 or 4 per lane) between the unaligned head and tail
+    constexpr u64 PV = 16 / sizeof(RT);
+    const u64 a0 = (s0 + PV - 1) & ~(PV - 1), a1 = s1 & ~(PV - 1);
     if (a0 < a1) {
-        for (u64 i = s0 + threadIdx.x; i < a0; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
+        for (u64 i = s0 + threadIdx.x; i < a0; i += U2_CBLOCK) atomicAdd(&lc[recs[i] & (R - 1)], 1u);
         const uint4* v = (const uint4*)(recs + a0);
-        const u64 nq = (a1 - a0) / 8;
+        const u64 nq = (a1 - a0) / PV;
         for (u64 q = threadIdx.x; q < nq; q += U2_CBLOCK) {
             const uint4 w = v[q];
             const u32 ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                atomicAdd(&lc[ww[h] & 0xffffu], 1u);
-                atomicAdd(&lc[ww[h] >> 16], 1u);
+                if (sizeof(RT) == 2) {
+                    atomicAdd(&lc[ww[h] & 0xffffu], 1u);
+                    atomicAdd(&lc[ww[h] >> 16], 1u);
+                } else {
+                    atomicAdd(&lc[ww[h] & (R - 1)], 1u);
+                }
             }
         }
-        for (u64 i = a1 + threadIdx.x; i < s1; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
+        for (u64 i = a1 + threadIdx.x; i < s1; i += U2_CBLOCK) atomicAdd(&lc[recs[i] & (R - 1)], 1u);
     } else {
-        for (u64 i = s0 + threadIdx.x; i < s1; i += U2_CBLOCK) atomicAdd(&lc[recs[i]], 1u);
+        for (u64 i = s0 + threadIdx.x; i < s1; i += U2_CBLOCK) atomicAdd(&lc[recs[i] & (R - 1)], 1u);
     }
     __syncthreads();
     const u64 base = (u64)bk << BITS;
@@ -244,6 +252,31 @@ __global__ __launch_bounds__(U2_CBLOCK) void k_u2_count(const uint16_t* __restri
     } else {  // several slices share the bucket: sum into its zeroed global counters, ranked by k_u2_finish
         for (u32 i = threadIdx.x; i < lim; i += U2_CBLOCK)
             if (lc[i]) atomicAdd(&cntg[base + i], lc[i]);
+    }
+}
+
+// K1 of large inputs (fc_unary_part, 3n >= U1_RADIX_MIN): the keys pos * V + value of every triple as u32, one
+// position after the other (coalesced), for the radix partition by bucket; instead of the partition passes' scatter
+// of 2-B records into 2^15 open buckets per block (c4 at 10^9 triples: 28 ms for 6 GB of partial-line writes)
+__global__ __launch_bounds__(RDF_BLOCK) void k_u1_keys(const u32* __restrict__ s, const u32* __restrict__ p,
+                                                       const u32* __restrict__ o, u64 n, u32 V, u32* keys) {
+    for (u64 i = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; i < n; i += (u64)gridDim.x * RDF_BLOCK) {
+        keys[i] = s[i];
+        keys[n + i] = V + p[i];
+        keys[2 * n + i] = 2 * V + o[i];
+    }
+}
+// bucket starts of keys grouped by bucket (key >> bits): ghist[b] = first key of bucket >= b, b in [0, NB]
+__global__ __launch_bounds__(RDF_BLOCK) void k_u1_bucket_starts(const u32* __restrict__ keys, u64 m, int bits, u32 NB,
+                                                                u32* ghist) {
+    for (u64 b = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; b <= NB; b += (u64)gridDim.x * RDF_BLOCK) {
+        u64 lo = 0, hi = m;
+        while (lo < hi) {
+            const u64 mid = (lo + hi) >> 1;
+            if (((u64)keys[mid] >> bits) < b) lo = mid + 1;
+            else hi = mid;
+        }
+        ghist[b] = (u32)lo;
     }
 }
 

@@ -262,14 +262,21 @@ __device__ inline u64 digit_peers(u32 d, bool valid) {
 }
 
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <typename KT> struct KeyPair;
+template <> struct KeyPair<u64> { typedef u64x2_t type; };
+template <> struct KeyPair<u32> { typedef u32x2_t type; };
 
-// 16-byte loads of a tile (two consecutive keys per lane and row); out-of-range keys read as 0
-__device__ inline void load_tile_pairs(const u64* __restrict__ keys, u64 n, u64 tbase, u64 (&k)[RS_ITEMS]) {
+// 16-byte (u64 keys) or 8-byte (u32 keys, K1's partition) loads of a tile: two consecutive keys per lane and row;
+// out-of-range keys read as 0
+template <typename KT>
+__device__ inline void load_tile_pairs(const KT* __restrict__ keys, u64 n, u64 tbase, KT (&k)[RS_ITEMS]) {
+    typedef typename KeyPair<KT>::type KT2;
 #pragma unroll
     for (int r = 0; r < RS_ITEMS / 2; ++r) {
         const u64 idx = tbase + 2ull * ((u64)r * RDF_BLOCK + threadIdx.x);
         if (idx + 1 < n) {
-            const u64x2_t v = *(const u64x2_t*)(keys + idx);
+            const KT2 v = *(const KT2*)(keys + idx);
             k[2 * r] = v.x;
             k[2 * r + 1] = v.y;
         } else {
@@ -288,8 +295,8 @@ template <bool HASH>
 __device__ inline u32 radix_digit(u64 k, int shift, u32 dmask, u64 hmask) {
     return (u32)((HASH ? mix64(k & hmask) : k) >> shift) & dmask;
 }
-template <int DB, bool HASH = false>
-__global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict__ keys, u64 n, int shift, int w,
+template <int DB, bool HASH = false, typename KT = u64>
+__global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const KT* __restrict__ keys, u64 n, int shift, int w,
                                                            u32* __restrict__ hist, u32 num_tiles, int drop, u64 hmask) {
     constexpr u32 NBIN = 1u << DB;
     __shared__ u32 wcnt[RDF_WAVES_PER_BLOCK][NBIN];
@@ -300,12 +307,12 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
     __syncthreads();
     const u32 tile = rs_tile();
     const u64 tbase = (u64)tile * RS_TILE;
-    u64 k[RS_ITEMS];
-    load_tile_pairs(keys, n, tbase, k);  // counting is order-free: any assignment of keys to lanes works
+    KT k[RS_ITEMS];
+    load_tile_pairs<KT>(keys, n, tbase, k);  // counting is order-free: any assignment of keys to lanes works
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         const u64 idx = tbase + 2ull * ((u64)(r / 2) * RDF_BLOCK + threadIdx.x) + (r & 1);
-        const bool valid = idx < n && !(drop && k[r] == ~0ull);
+        const bool valid = idx < n && !(drop && k[r] == (KT)~0ull);
         const u32 d = radix_digit<HASH>(k[r], shift, dmask, hmask);
         const u64 peers = digit_peers<DB>(d, valid);
         if (valid && ((peers >> lane) >> 1) == 0) wcnt[wave][d] += (u32)__popcll(peers);
@@ -319,15 +326,15 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_count(const u64* __restrict
     }
 }
 
-template <int DB, bool HASH = false>
-__global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restrict__ keys, u64* __restrict__ out, u64 n,
+template <int DB, bool HASH = false, typename KT = u64>
+__global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const KT* __restrict__ keys, KT* __restrict__ out, u64 n,
                                                              int shift, int w, const u32* __restrict__ offs,
                                                              const u32* __restrict__ rowtot, u32 num_tiles, int drop,
                                                              u64 hmask, u32* d_kept) {
     constexpr u32 NBIN = 1u << DB;
     constexpr u32 PER = NBIN / RDF_BLOCK;  // digits per thread in the tile scan (1, 2 or 4)
     static_assert(NBIN % RDF_BLOCK == 0, "digit bins must be a multiple of the block");
-    __shared__ __align__(16) u64 skeys[RS_TILE];
+    __shared__ __align__(16) KT skeys[RS_TILE];
     __shared__ u32 wcount[RDF_WAVES_PER_BLOCK][NBIN];
     __shared__ u32 tstart[NBIN];
     __shared__ u32 gbase[NBIN];
@@ -342,8 +349,8 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     const u64 tn = n - tbase < (u64)RS_TILE ? n - tbase : (u64)RS_TILE;
     {   // stage the tile through LDS: 16-byte global loads, then each wave reads its contiguous sub-range; while they
         // are in flight, the digits' bases (exclusive scan of the row totals, PER digits a thread) + the row prefixes
-        u64 kin[RS_ITEMS];
-        load_tile_pairs(keys, n, tbase, kin);
+        KT kin[RS_ITEMS];
+        load_tile_pairs<KT>(keys, n, tbase, kin);
         u32 rt[PER], ro[PER], local = 0;
 #pragma unroll
         for (u32 q = 0; q < PER; ++q) {
@@ -363,11 +370,11 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
 #pragma unroll
         for (int r = 0; r < RS_ITEMS / 2; ++r) {
             const u32 p = 2u * ((u32)r * RDF_BLOCK + threadIdx.x);
-            *(u64x2_t*)(skeys + p) = u64x2_t{kin[2 * r], kin[2 * r + 1]};
+            *(typename KeyPair<KT>::type*)(skeys + p) = typename KeyPair<KT>::type{kin[2 * r], kin[2 * r + 1]};
         }
     }
     __syncthreads();
-    u64 k[RS_ITEMS];
+    KT k[RS_ITEMS];
     u32 rank[RS_ITEMS];
     const u64 lt = lanemask_lt();
     const u32 wofs = (u32)wave * RS_WAVE_KEYS;
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     for (int r = 0; r < RS_ITEMS; ++r) k[r] = skeys[wofs + (u32)r * RDF_WAVE + lane];
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == ~0ull);
+        const bool valid = wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == (KT)~0ull);
         const u32 d = radix_digit<HASH>(k[r], shift, dmask, hmask);
         const u64 peers = digit_peers<DB>(d, valid);
         const u32 before = (u32)__popcll(peers & lt);
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        if (wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == ~0ull)) {
+        if (wofs + (u32)r * RDF_WAVE + lane < tn && !(drop && k[r] == (KT)~0ull)) {
             const u32 d = radix_digit<HASH>(k[r], shift, dmask, hmask);
             skeys[tstart[d] + wcount[wave][d] + rank[r]] = k[r];
         }
@@ -423,7 +430,7 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const u64* __restri
     for (int i = 0; i < RS_ITEMS; ++i) {
         const u32 p = (u32)i * RDF_BLOCK + threadIdx.x;
         if (p < tv) {
-            const u64 key = skeys[p];
+            const KT key = skeys[p];
             const u32 d = radix_digit<HASH>(key, shift, dmask, hmask);
             out[(u64)gbase[d] + (p - tstart[d])] = key;
         }
@@ -493,17 +500,17 @@ __global__ __launch_bounds__(RS_SCAN_THREADS) void k_radix_rowscan(u32* __restri
 }
 
 static inline u32 hist_stride(u32 tiles) { return (tiles + 3u) & ~3u; }
-template <int DB, bool HASH = false>
-static hipError_t radix_pass(Workspace& ws, const u64* keys, u64* tmp, u64 n, int shift, int w, u32* hist, u32 tiles,
+template <int DB, bool HASH = false, typename KT = u64>
+static hipError_t radix_pass(Workspace& ws, const KT* keys, KT* tmp, u64 n, int shift, int w, u32* hist, u32 tiles,
                              hipStream_t st, u32* d_kept = nullptr, u64 hmask = 0) {
     const int drop = d_kept ? 1 : 0;
     u32* rowtot = (u32*)ws.scratch(1024 * sizeof(u32), 2);
     if (!rowtot) return hipErrorOutOfMemory;
     const u32 rs = hist_stride(tiles);  // the histogram's digit rows, 16-B aligned
-    hipLaunchKernelGGL((k_radix_count<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, rs, drop,
+    hipLaunchKernelGGL((k_radix_count<DB, HASH, KT>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, n, shift, w, hist, rs, drop,
                        hmask);
     hipLaunchKernelGGL(k_radix_rowscan, dim3(1u << w), dim3(RS_SCAN_THREADS), 0, st, hist, rs, tiles, rowtot);
-    hipLaunchKernelGGL((k_radix_scatter<DB, HASH>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, rowtot,
+    hipLaunchKernelGGL((k_radix_scatter<DB, HASH, KT>), dim3(tiles), dim3(RDF_BLOCK), 0, st, keys, tmp, n, shift, w, hist, rowtot,
                        rs, drop, hmask, d_kept);
     return hipGetLastError();
 }
@@ -596,6 +603,27 @@ hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, i
         hipError_t e = w <= 8 ? radix_pass<8, true>(ws, keys, tmp, n, shift, w, hist, tiles, st, nullptr, hmask)
                      : w == 9 ? radix_pass<9, true>(ws, keys, tmp, n, shift, w, hist, tiles, st, nullptr, hmask)
                               : radix_pass<10, true>(ws, keys, tmp, n, shift, w, hist, tiles, st, nullptr, hmask);
+        if (e != hipSuccess) return e;
+        std::swap(keys, tmp);
+        shift += w;
+    }
+    return hipGetLastError();
+}
+
+// u32 keys ordered by bits [lo, hi) (LSD passes of <= 8 bits, stable; bits below lo keep the input's order): K1's
+// records of large inputs grouped by their 2^14 / 2^15-key bucket (fc_unary_radix).  keys / tmp swap like
+// radix_sort_u64_bits.
+hipError_t radix_partition_u32(Workspace& ws, u32*& keys, u32*& tmp, u64 n, int lo, int hi, hipStream_t st) {
+    if (n < 2 || hi <= lo) return hipSuccess;
+    if (n >= (1ull << 32) || hi > 32) return hipErrorInvalidValue;
+    const u32 tiles = (u32)((n + RS_TILE - 1) / RS_TILE);
+    const int bits = hi - lo, passes = (bits + 7) / 8;
+    u32* hist = (u32*)ws.scratch(((u64)hist_stride(tiles) << 8) * sizeof(u32), 1);
+    if (!hist) return hipErrorOutOfMemory;
+    int shift = lo;
+    for (int p = 0; p < passes; ++p) {
+        const int w = bits / passes + (p < bits % passes ? 1 : 0);
+        hipError_t e = radix_pass<8, false, u32>(ws, keys, tmp, n, shift, w, hist, tiles, st);
         if (e != hipSuccess) return e;
         std::swap(keys, tmp);
         shift += w;

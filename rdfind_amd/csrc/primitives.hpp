@@ -97,5 +97,7 @@ hipError_t radix_sort_u64_drop(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int 
 hipError_t radix_sort_u64_bits(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int lo, int hi, hipStream_t st);
 int radix_sort_passes(int bits);  // passes of a sort of `bits` key bits
 hipError_t radix_partition_hashed(Workspace& ws, u64*& keys, u64*& tmp, u64 n, int bits, u64 hmask, hipStream_t st);
+// u32 keys ordered by bits [lo, hi) (stable LSD passes of <= 8 bits); keys / tmp swap so that `keys` holds the result
+hipError_t radix_partition_u32(Workspace& ws, u32*& keys, u32*& tmp, u64 n, int lo, int hi, hipStream_t st);
 
 }  // namespace rdf

@@ -78,6 +78,7 @@ struct rdf_ctx {
     // light dependents with identical group lists (d_light_dedup): keys, key table, class representatives, counts
     DevBuf ukey, utab, urep, ucnt, unoff, uebin, umem;
     u32 dup_min = 256;               // RDFIND_DUP_MIN: the shortest group list that looks for an equal one
+    u64 u1_radix_min = 0;            // RDFIND_U1_RADIX_MIN: 3n from which K1 takes its radix form (0: the rule)
     int light_dedup = -1;            // RDFIND_LIGHT_DEDUP: 0 every light dependent verified on its own, 1 once per class
                                      // of equal group lists, unset: classes where the light pass stages (c2-like inputs)
     u64 n_dedup_members = 0;         // light dependents that took their representative's refs (last discovery)
@@ -532,6 +533,7 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (const char* rk = getenv("RDFIND_RANGE_KEEP")) c->range_keep = atoi(rk) != 0;
     if (const char* ld = getenv("RDFIND_LIGHT_DEDUP")) c->light_dedup = atoi(ld) != 0 ? 1 : 0;
     if (const char* dm = getenv("RDFIND_DUP_MIN")) c->dup_min = (u32)std::max(1, atoi(dm));
+    if (const char* um = getenv("RDFIND_U1_RADIX_MIN")) c->u1_radix_min = strtoull(um, nullptr, 10);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
@@ -872,39 +874,68 @@ static rdf_status fc_unary_part(rdf_ctx* c, const u32* s, const u32* p, const u3
     hipStream_t st = c->stream;
     const u32 V = c->V ? c->V : 1;
     const u64 K = 3ull * V;
-    const unsigned G = (unsigned)std::max<u64>(1, std::min<u64>({1024, (n + 2047) / 2048, (1ull << 25) / NB}));
-    const u64 nh = NB * G;
-    ENSURE(c, uhist, (nh + 1) * 4);
-    ENSURE(c, urecs, 3 * n * 2 + 16);
     ENSURE(c, usl, (NB + 1) * 4);
-    const size_t lds = NB * 4;
-    hipLaunchKernelGGL((k_u2_part<false>), dim3(G), dim3(RDF_BLOCK), lds, st, s, p, o, n, V, (u32)NB, ubits,
-                       c->uhist.as<u32>(), (uint16_t*)nullptr);
-    HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
-    hipLaunchKernelGGL((k_u2_part<true>), dim3(G), dim3(RDF_BLOCK), lds, st, s, p, o, n, V, (u32)NB, ubits,
-                       c->uhist.as<u32>(), c->urecs.as<uint16_t>());
+    // large inputs whose bucket counters leave one partition block per CU (NB x 4 B of LDS > 80 KB): the keys as u32,
+    // grouped by bucket with two stable radix passes over the bucket bits, bucket starts by binary search (G = 1); the
+    // keys live in K2's record buffers, which the next stage needs anyway.  c4 at 10^9 triples (22,891 buckets of 2^15
+    // keys): K1 53.1 -> 42.9 ms; c4 at 0.4 (18,313 buckets, two blocks per CU) 14.1 -> 16.8 and c3 2.4 -> 4.6 lose, so
+    // they keep the partition passes (profiles/r06_k1_radix_ab.log).  RDFIND_U1_RADIX_MIN=<3n> replaces the rule
+    const bool radix_rule = c->u1_radix_min ? 3 * n >= c->u1_radix_min : 3 * n >= U1_RADIX_MIN && NB * 4 > U1_RADIX_LDS;
+    const bool radix = radix_rule && 3 * n < (1ull << 32) && K <= 0xffffffffull;
+    const void* recs = nullptr;
+    unsigned G = 1;
+    if (radix) {
+        const u64 m = 3 * n;
+        ENSURE(c, brkeys, m * 4);
+        ENSURE(c, brkeys2, m * 4);
+        ENSURE(c, uhist, (NB + 1) * 4);
+        u32* keys = c->brkeys.as<u32>();
+        u32* tmp = c->brkeys2.as<u32>();
+        hipLaunchKernelGGL(k_u1_keys, dim3(grid_for(n, RDF_BLOCK, 8 * kGrid)), dim3(RDF_BLOCK), 0, st, s, p, o, n, V, keys);
+        HIP_TRY(c, radix_partition_u32(c->ws, keys, tmp, m, ubits, ubits + bits_for(NB - 1), st));
+        hipLaunchKernelGGL(k_u1_bucket_starts, dim3(grid_for(NB + 1, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, keys, m,
+                           ubits, (u32)NB, c->uhist.as<u32>());
+        recs = keys;
+    } else {
+        G = (unsigned)std::max<u64>(1, std::min<u64>({1024, (n + 2047) / 2048, (1ull << 25) / NB}));
+        const u64 nh = NB * G;
+        ENSURE(c, uhist, (nh + 1) * 4);
+        ENSURE(c, urecs, 3 * n * 2 + 16);
+        const size_t lds = NB * 4;
+        hipLaunchKernelGGL((k_u2_part<false>), dim3(G), dim3(RDF_BLOCK), lds, st, s, p, o, n, V, (u32)NB, ubits,
+                           c->uhist.as<u32>(), (uint16_t*)nullptr);
+        HIP_TRY(c, exclusive_scan_u32(c->ws, c->uhist.as<u32>(), c->uhist.as<u32>(), nh, c->uhist.as<u32>() + nh, st));
+        hipLaunchKernelGGL((k_u2_part<true>), dim3(G), dim3(RDF_BLOCK), lds, st, s, p, o, n, V, (u32)NB, ubits,
+                           c->uhist.as<u32>(), c->urecs.as<uint16_t>());
+        recs = c->urecs.p;
+    }
+    HIP_TRY(c, hipGetLastError());
     hipLaunchKernelGGL(k_u2_slices, dim3((unsigned)NB), dim3(RDF_BLOCK), 0, st, c->uhist.as<u32>(), (u32)NB, G, ubits, K,
                        c->usl.as<u32>(), c->cntg.as<u32>());
     HIP_TRY(c, exclusive_scan_u32(c->ws, c->usl.as<u32>(), c->usl.as<u32>(), NB, c->usl.as<u32>() + NB, st));
     const u64 max_slices = NB + 3 * n / U2_SLICE + 1;  // >= sum over buckets of max(1, ceil(len / U2_SLICE))
     const int co = counts_only ? 1 : 0;
+#define RDF_U2_COUNT(BITS, RT)                                                                                           \
+    hipLaunchKernelGGL((k_u2_count<BITS, RT>), dim3((unsigned)max_slices), dim3(U2_CBLOCK), 0, st, (const RT*)recs,     \
+                       c->uhist.as<u32>(), c->usl.as<u32>(), (u32)NB, G, K, V, c->ms, c->frank.as<u32>(),                \
+                       c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0), c->cntg.as<u32>(), co)
     if (ubits == 14) {
-        hipLaunchKernelGGL(k_u2_count<14>, dim3((unsigned)max_slices), dim3(U2_CBLOCK), 0, st, c->urecs.as<uint16_t>(),
-                           c->uhist.as<u32>(), c->usl.as<u32>(), (u32)NB, G, K, V, c->ms, c->frank.as<u32>(),
-                           c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0), c->cntg.as<u32>(), co);
+        if (radix) RDF_U2_COUNT(14, u32);
+        else RDF_U2_COUNT(14, uint16_t);
         if (!counts_only)
             hipLaunchKernelGGL(k_u2_finish<14>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, st, c->usl.as<u32>(), (u32)NB, K, V,
                                c->ms, c->cntg.as<u32>(), c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(),
                                c->fbits.as<u64>(), dscal(c, 0));
     } else {
-        hipLaunchKernelGGL(k_u2_count<15>, dim3((unsigned)max_slices), dim3(U2_CBLOCK), 0, st, c->urecs.as<uint16_t>(),
-                           c->uhist.as<u32>(), c->usl.as<u32>(), (u32)NB, G, K, V, c->ms, c->frank.as<u32>(),
-                           c->bfreq.as<u32>(), c->fstage.as<u32>(), c->fbits.as<u64>(), dscal(c, 0), c->cntg.as<u32>(), co);
+        if (radix) RDF_U2_COUNT(15, u32);
+        else RDF_U2_COUNT(15, uint16_t);
         if (!counts_only)
             hipLaunchKernelGGL(k_u2_finish<15>, dim3((unsigned)NB), dim3(U2_CBLOCK), 0, st, c->usl.as<u32>(), (u32)NB, K, V,
                                c->ms, c->cntg.as<u32>(), c->frank.as<u32>(), c->bfreq.as<u32>(), c->fstage.as<u32>(),
                                c->fbits.as<u64>(), dscal(c, 0));
     }
+#undef RDF_U2_COUNT
+    HIP_TRY(c, hipGetLastError());
     return RDF_OK;
 }
 

@@ -191,6 +191,34 @@ def test_global_count_paths(ctx, monkeypatch):
         g.close()
 
 
+def test_unary_radix_path_parity(ctx, monkeypatch):
+    """K1's radix form (u32 keys grouped by bucket with stable radix passes, bucket starts by binary search, the same
+    counting blocks; the default from 3n >= 2^27) forced on every input by RDFIND_U1_RADIX_MIN=1: random inputs in two
+    modes equal the oracle, and c1 / c5 / c2 samples give the partition passes' condition statistics and checksum."""
+    monkeypatch.setenv("RDFIND_U1_RADIX_MIN", "1")
+    g = _lib.Context(0)
+    try:
+        rng = random.Random(61)
+        for _ in range(30):
+            n = rng.randrange(1, 400)
+            nv = rng.randrange(2, 60)
+            ms = rng.randrange(1, 5)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 3 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            for strategy, clean in ((1, True), (0, False)):
+                assert gpu_set(g, arr, nv, ms, strategy, clean) == expected_set(arr, nv, ms, strategy, clean)
+        for cfg, scale in (("c1", 0.2), ("c5", 0.01), ("c2", 0.05)):
+            d = dataset(cfg, scale)
+            stats = []
+            for c in (g, ctx):
+                c.set_triples(d.s, d.p, d.o, d.num_terms)
+                c.run(d.min_support)
+                stats.append((dict(c.fc), c.cind_count(), c.checksum()))
+            assert stats[0] == stats[1], cfg
+    finally:
+        g.close()
+
+
 def _capture_joins(d, code, v1, v2):
     """Distinct join values of a capture, straight from the triples (the definition of its groups)."""
     cols = {1: d.s, 2: d.p, 4: d.o}

@@ -427,6 +427,13 @@ def test_sharded_join_ranges_random(range_records):
     assert any(res[r][k]["ranges"] > 1 for r in range(2) for k in range(24))
 
 
+def test_sharded_unary_radix_path():
+    """Each rank's K1 partial counts (counts_only, summed by the unary key owners) in the radix form forced on
+    (RDFIND_U1_RADIX_MIN=1; by default only inputs like a c4 at 10^9 rank slice take it): random inputs in all four
+    modes over 2 ranks with local slices equal the single-GPU result."""
+    _check(2, _random_cases(500, 16), local_slice=True, env={"RDFIND_U1_RADIX_MIN": "1"})
+
+
 def test_hot_candidates_uneven_slices_deterministic():
     """An owner whose slice is tiny against the summed counts it owns (rank 0 holds 10 rows) submits more hot join value
     candidates than HOT_CAP (32768): it keeps the HOT_CAP largest by (count, key), not the first to arrive, so every
