@@ -214,6 +214,88 @@ static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 
     return hipGetLastError();
 }
 
+// k scans of equal length in one pass (blockIdx.y = the array): d_chunks' four per-dependent counts on c2 took eight
+// launches, now two
+struct ScanBatch {
+    const u32* in[SCAN_BATCH_MAX];
+    u64* out[SCAN_BATCH_MAX];
+};
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_reduce_batch(ScanBatch b, u64 n, u64* __restrict__ tile_sums) {
+    __shared__ u64 lds_wave[RDF_WAVES_PER_BLOCK];
+    const u32* in = b.in[blockIdx.y];
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    u64 acc = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        if (idx < n) acc += in[idx];
+    }
+    u64 total;
+    block_exclusive_scan<u64>(acc, lds_wave, &total);
+    if (threadIdx.x == 0) tile_sums[(u64)blockIdx.y * gridDim.x + blockIdx.x] = total;
+}
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply_fold_batch(ScanBatch b, u64 n, const u64* __restrict__ tile_sums) {
+    __shared__ u64 lds[SCAN_TILE];
+    __shared__ u64 lds_wave[RDF_WAVES_PER_BLOCK];
+    const u32* in = b.in[blockIdx.y];
+    u64* out = b.out[blockIdx.y];
+    const u64* sums = tile_sums + (u64)blockIdx.y * gridDim.x;
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        lds[i * RDF_BLOCK + threadIdx.x] = idx < n ? (u64)in[idx] : 0ull;
+    }
+    u64 before = 0;
+    for (u32 t = threadIdx.x; t < blockIdx.x; t += RDF_BLOCK) before += sums[t];
+    u64 prior;
+    block_exclusive_scan<u64>(before, lds_wave, &prior);
+    u64 v[SCAN_ITEMS];
+    u64 local = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        v[i] = lds[threadIdx.x * SCAN_ITEMS + i];
+        local += v[i];
+    }
+    u64 total;
+    u64 off = block_exclusive_scan<u64>(local, lds_wave, &total) + prior;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        lds[threadIdx.x * SCAN_ITEMS + i] = off;
+        off += v[i];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = prior + total;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+        if (idx < n) out[idx] = lds[i * RDF_BLOCK + threadIdx.x];
+    }
+}
+
+hipError_t exclusive_scan_u32_u64_batch(Workspace& ws, const u32* const* in, u64* const* out, int k, u64 n,
+                                        hipStream_t st) {
+    const u64 tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (k < 1 || k > SCAN_BATCH_MAX) return hipErrorInvalidValue;
+    if (n == 0 || tiles <= SCAN_SMALL_TILES || tiles > SCAN_FOLD_TILES) {  // (one launch each already, or large)
+        for (int j = 0; j < k; ++j) {
+            hipError_t e = exclusive_scan_u32_u64(ws, in[j], out[j], n, out[j] + n, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    ScanBatch b = {};
+    for (int j = 0; j < k; ++j) {
+        b.in[j] = in[j];
+        b.out[j] = out[j];
+    }
+    u64* sums = (u64*)ws.scratch(tiles * k * sizeof(u64), 0);
+    if (!sums) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL(k_scan_reduce_batch, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
+    hipLaunchKernelGGL(k_scan_apply_fold_batch, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
+    return hipGetLastError();
+}
+
 hipError_t exclusive_scan_u32_u64(Workspace& ws, const u32* in, u64* out, u64 n, u64* d_total, hipStream_t st) {
     return exclusive_scan_impl<u32, u64>(ws, in, out, n, d_total, st);
 }

@@ -79,6 +79,10 @@ struct Workspace {
 
 // out[i] = sum_{j<i} in[j]; *d_total (device, optional) = sum of all.  In-place allowed.
 hipError_t exclusive_scan_u32_u64(Workspace& ws, const u32* in, u64* out, u64 n, u64* d_total, hipStream_t st);
+// k <= SCAN_BATCH_MAX scans of n elements each in one pass; out[j][n] = the total of in[j]
+static constexpr int SCAN_BATCH_MAX = 4;
+hipError_t exclusive_scan_u32_u64_batch(Workspace& ws, const u32* const* in, u64* const* out, int k, u64 n,
+                                        hipStream_t st);
 hipError_t exclusive_scan_u64(Workspace& ws, const u64* in, u64* out, u64 n, u64* d_total, hipStream_t st);
 hipError_t exclusive_scan_u32(Workspace& ws, const u32* in, u32* out, u64 n, u32* d_total, hipStream_t st);
 

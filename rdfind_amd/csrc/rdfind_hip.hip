@@ -2477,10 +2477,11 @@ static rdf_status d_pivot_local(rdf_ctx* c, CindView& v) {
 static rdf_status d_chunks(rdf_ctx* c, u64* WL, u64* WH, u64* WI, u64* WP) {
     hipStream_t st = c->stream;
     const u32 C = c->C;
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchl.as<u32>(), c->choffl.as<u64>(), C, c->choffl.as<u64>() + C, st));
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nitl.as<u32>(), c->itoffl.as<u64>(), C, c->itoffl.as<u64>() + C, st));
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->nchh.as<u32>(), c->choffh.as<u64>(), C, c->choffh.as<u64>() + C, st));
-    HIP_TRY(c, exclusive_scan_u32_u64(c->ws, c->npk.as<u32>(), c->pkoff.as<u64>(), C, c->pkoff.as<u64>() + C, st));
+    {
+        const u32* in[4] = {c->nchl.as<u32>(), c->nitl.as<u32>(), c->nchh.as<u32>(), c->npk.as<u32>()};
+        u64* out[4] = {c->choffl.as<u64>(), c->itoffl.as<u64>(), c->choffh.as<u64>(), c->pkoff.as<u64>()};
+        HIP_TRY(c, exclusive_scan_u32_u64_batch(c->ws, in, out, 4, C, st));
+    }
     u64 v[8];  // [7]: k_multi_items' sum when rdf_discover_cinds launched it (else stale, unused)
     TRY(read_multi(c, {{c->choffl.as<u64>() + C, 8}, {c->pkoff.as<u64>() + C, 8}, {c->choffh.as<u64>() + C, 8},
                        {dscal(c, 2), 8}, {c->itoffl.as<u64>() + C, 8}, {dscal(c, 3), 8}, {dscal(c, 4), 8},
