@@ -345,6 +345,8 @@ def main():
     ap.add_argument("--no-early-handover", action="store_true", help="hand the whole result over after each run "
                     "(no rdf_set_handover: the refs and the capture table are not copied while the run computes)")
     ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
+    ap.add_argument("--no-numa-bind", action="store_true", help="leave the process on every CPU (default: bound to the "
+                    "GPU's NUMA node before any host buffer is allocated, rdfind_amd/numa.py)")
     ap.add_argument("--c4-strong", choices=("auto", "on", "off"), default="auto",
                     help="also time BASELINE configs[3] (c4, Freebase-shaped, 10^9 triples, support 100) split over the "
                          "N GPUs (strong scaling; the north-star scaling config) and report it as `c4_strong` (auto: "
@@ -372,11 +374,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    import torch
+
+    local_rank %= max(torch.cuda.device_count(), 1)
+    if not args.no_numa_bind:  # host buffers on the GPU's NUMA node (rdfind_amd/numa.py)
+        from rdfind_amd import numa
+
+        numa.bind_to_device_node(local_rank)
     if world > 1:
-        import torch
         import torch.distributed as dist
 
-        local_rank %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
         import datetime
         # a rank lost inside a collective ends the run after this long (gloo raises; RCCL's watchdog aborts the

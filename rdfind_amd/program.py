@@ -131,6 +131,9 @@ class RDFind:
                 torch.cuda.set_device(device)
         else:
             device = a.device
+        if os.environ.get("RDFIND_NUMA_BIND", "1") != "0":  # host buffers next to the GPU (rdfind_amd/numa.py)
+            from . import numa
+            numa.bind_to_device_node(device)
         t0 = time.time()
         paths = ntriples.resolve_paths(a.inputs)
         if not paths:
