@@ -184,15 +184,20 @@ class CompactSink:
             self.register(ctx)
         return L
 
-    def copy(self, ctx):
+    def copy(self, ctx, overlap=False):
+        """overlap (pages): the refs are queued on the library's copy stream (rdf_copy_result_refs_async) and leave
+        while the next page computes; the caller ends with ctx.handover_wait()."""
         L = self.ensure(ctx)
-        if L["n_refs"] <= self.cap["refs"]:
+        if L["n_refs"] <= self.cap["refs"] and not (overlap and self.pinned):
             ctx.copy_result_compact(self.bufs)
             return L
         ctx.copy_result_compact(dict(self.bufs, refs=0))  # everything but the refs, which stream in chunks
         off = 0
         while off < L["n_refs"]:
-            off += ctx.copy_result_refs(off, self.cap["refs"], self.bufs["refs"])
+            if overlap and self.pinned:
+                off += ctx.copy_result_refs_async(off, self.cap["refs"], self.bufs["refs"])
+            else:
+                off += ctx.copy_result_refs(off, self.cap["refs"], self.bufs["refs"])
         return L
 
 
@@ -345,6 +350,8 @@ def main():
     ap.add_argument("--no-early-handover", action="store_true", help="hand the whole result over after each run "
                     "(no rdf_set_handover: the refs and the capture table are not copied while the run computes)")
     ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
+    ap.add_argument("--no-page-overlap", action="store_true", help="paged runs: hand each page's refs over before the "
+                    "next page starts (default: queued on the copy stream while the next page computes)")
     ap.add_argument("--no-numa-bind", action="store_true", help="leave the process on every CPU (default: bound to the "
                     "GPU's NUMA node before any host buffer is allocated, rdfind_amd/numa.py)")
     ap.add_argument("--c4-strong", choices=("auto", "on", "off"), default="auto",
@@ -431,8 +438,8 @@ def main():
             for i, _ in enumerate(ctx.pages(True, 1, args.page_bytes or 0)):
                 n += ctx.cind_count()
                 t_copy = time.perf_counter()
-                if hand_over:
-                    sink.copy(ctx)
+                if hand_over:  # a page's refs leave while the next page computes (--no-page-overlap: in turn)
+                    sink.copy(ctx, overlap=not args.no_page_overlap)
                 if args.page_log:
                     _, pcs = ctx.last_stats()
                     t_end = time.perf_counter()
@@ -440,6 +447,7 @@ def main():
                           f"HBM held {ctx.device_bytes() / 2**30:.1f} GiB, page {t_copy - t_page:.2f} s, "
                           f"hand-over {t_end - t_copy:.2f} s", file=sys.stderr, flush=True)
                     t_page = time.perf_counter()
+            ctx.handover_wait()  # the last page's refs are in host memory
             _, cs = ctx.last_stats()
             return dict(cs, n_cinds=n, pages=ctx_pages(ctx))
     else:

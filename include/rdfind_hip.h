@@ -242,6 +242,16 @@ rdf_status rdf_set_handover(rdf_ctx* ctx, uint32_t* refs, uint64_t refs_cap, uin
  * (the reference's sink consumes its output as it comes, ALG/programs/RDFind.scala:507-520). */
 rdf_status rdf_copy_result_refs(rdf_ctx* ctx, uint64_t offset, uint64_t count, uint32_t* refs, uint64_t* n_copied);
 
+/* The same copy, queued on the context's copy stream instead of waiting for it: the refs of a page leave while the
+ * next rdf_next_page computes (its emission waits on the GPU for the copy before it overwrites them; only a page that
+ * needs a larger output buffer waits on the host).  `refs` must be page-locked (rdf_host_alloc) and stay untouched
+ * until rdf_handover_wait, or until another copy call, returns.  Copies queued this way into one buffer complete in
+ * order.  Replaces the page-by-page synchronous sink of ALG/programs/RDFind.scala:507-520 with an overlapped one. */
+rdf_status rdf_copy_result_refs_async(rdf_ctx* ctx, uint64_t offset, uint64_t count, uint32_t* refs, uint64_t* n_copied);
+
+/* Wait until every queued asynchronous copy (rdf_copy_result_refs_async, the early hand-over) has reached the host. */
+rdf_status rdf_handover_wait(rdf_ctx* ctx);
+
 /* Page-locked host memory (hipHostMalloc) for hand-over buffers: the copies above then run at the link rate.
  * Returns null on failure; free with rdf_host_free. */
 void* rdf_host_alloc(uint64_t bytes);

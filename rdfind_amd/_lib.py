@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
     "rdf_discover_cinds_paged", "rdf_next_page", "rdf_shard_parse_begin", "rdf_shard_dictionary_begin", "rdf_num_terms",
     "rdf_dictionary_terms", "rdf_copy_result_refs", "rdf_release_scratch", "rdf_set_handover",
+    "rdf_copy_result_refs_async", "rdf_handover_wait",
 )
 RDF_NT_TABS = 1
 
@@ -164,6 +165,8 @@ def load():
         "rdf_get_result_layout": (i32, [P, ctypes.POINTER(ResultLayout)]),
         "rdf_copy_result_compact": (i32, [P, P, P, P, P, P, P, P, P]),
         "rdf_copy_result_refs": (i32, [P, u64, u64, P, ctypes.POINTER(u64)]),
+        "rdf_copy_result_refs_async": (i32, [P, u64, u64, P, ctypes.POINTER(u64)]),
+        "rdf_handover_wait": (i32, [P]),
         "rdf_set_handover": (i32, [P, P, u64, P, P, u64, P, P, u64]),
         "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
@@ -551,6 +554,18 @@ class Context:
         p = ptr if isinstance(ptr, int) else ptr.ctypes.data
         self._check(self.lib.rdf_copy_result_refs(self.ptr, offset, count, p, ctypes.byref(copied)), "rdf_copy_result_refs")
         return copied.value
+
+    def copy_result_refs_async(self, offset: int, count: int, ptr: int) -> int:
+        """rdf_copy_result_refs_async: the same copy queued on the context's copy stream (``ptr``: page-locked, untouched
+        until handover_wait); returns the refs queued."""
+        copied = ctypes.c_uint64()
+        self._check(self.lib.rdf_copy_result_refs_async(self.ptr, offset, count, ptr, ctypes.byref(copied)),
+                    "rdf_copy_result_refs_async")
+        return copied.value
+
+    def handover_wait(self) -> None:
+        """rdf_handover_wait: every queued copy has reached the host."""
+        self._check(self.lib.rdf_handover_wait(self.ptr), "rdf_handover_wait")
 
     def copy_cinds_decoded(self, offset: int = 0, count: int | None = None) -> np.ndarray:
         """Cind-shaped rows decoded on the device (rdf_copy_cinds_decoded), ROW_DTYPE."""

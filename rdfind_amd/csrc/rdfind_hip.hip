@@ -139,6 +139,10 @@ struct rdf_ctx {
     u64 hv_refs_n = ~0ull;       // refs copied early by the current result (~0: none)
     bool hv_caps_done = false;   // capture ids and supports copied early
     bool hv_pending = false;     // copies queued on hstream not yet waited for
+    // paged hand-over (rdf_copy_result_refs_async): a page's refs leave on hstream while the next page computes; the
+    // next page's emission waits for hv_done on the GPU before it writes `out` (a growing `out` waits on the host)
+    hipEvent_t hv_done = nullptr;
+    bool hv_gpu_wait = false;
     bool dense_on = false;
     u64 dwords = 0, n_dense = 0;
     int dense_div = -1;                   // RDFIND_DENSE (0: no bitmaps; -1: by input, d_dense_flags)
@@ -304,6 +308,7 @@ static rdf_status ensure_buf(rdf_ctx* c, DevBuf* b, size_t bytes, const char* wh
 static rdf_status hv_wait(rdf_ctx* c, bool forget) {
     if (c->hv_pending) {
         c->hv_pending = false;
+        c->hv_gpu_wait = false;
         HIP_TRY(c, hipStreamSynchronize(c->hstream));
     }
     if (forget) {
@@ -540,6 +545,7 @@ rdf_status rdf_ctx_create(int device, rdf_ctx** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hv_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hv_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = c->scal.ensure(16 * sizeof(u64));
     if (e == hipSuccess) e = hipHostMalloc((void**)&c->hscal, 16 * sizeof(u64), hipHostMallocDefault);
@@ -583,7 +589,7 @@ const char* rdf_last_error(const rdf_ctx* c) { return c ? c->err.c_str() : "null
 rdf_status rdf_sync(rdf_ctx* c) {
     if (!c) return RDF_ERR_ARG;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return RDF_OK;
+    return hv_wait(c, false);  // (and the copies queued on the copy stream)
 }
 
 rdf_status rdf_device_bytes(rdf_ctx* c, uint64_t* bytes) {
@@ -3325,6 +3331,10 @@ static rdf_status d_page_emit(rdf_ctx* c, const CindView& v, u32 d0, u32 d1, u64
     u64 kh[2];
     TRY(read_multi(c, {{c->pos.as<u64>() + E, 8}, {c->hoff.as<u64>() + WHr, 8}}, kh));
     const u64 K = kh[0], H = kh[1];
+    if (c->hv_gpu_wait) {  // the previous page's refs may still be on their way to the host (rdf_copy_result_refs_async)
+        if (c->out.cap < std::max<u64>(K + H, 1) * 4) TRY(hv_wait(c, false));  // (growing frees what the copy reads)
+        else HIP_TRY(c, hipStreamWaitEvent(c->stream, c->hv_done, 0));
+    }
     ENSURE(c, out, std::max<u64>(K + H, 1) * 4);
     if (E)
         hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
@@ -4850,12 +4860,37 @@ rdf_status rdf_copy_result_refs(rdf_ctx* c, uint64_t offset, uint64_t count, uin
     if (!c || (count && !refs)) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, false));  // (an asynchronous copy may still write the same host buffer)
     const u64 nrefs = c->n_out - c->n_class_out;
     const u64 n = offset < nrefs ? std::min<u64>(count, nrefs - offset) : 0;
     if (n) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr + offset, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (n_copied) *n_copied = n;
     return RDF_OK;
+}
+
+rdf_status rdf_copy_result_refs_async(rdf_ctx* c, uint64_t offset, uint64_t count, uint32_t* refs, uint64_t* n_copied) {
+    if (!c || (count && !refs)) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 nrefs = c->n_out - c->n_class_out;
+    const u64 n = offset < nrefs ? std::min<u64>(count, nrefs - offset) : 0;
+    if (n) {  // after everything queued so far on the compute stream, on the copy stream
+        HIP_TRY(c, hipEventRecord(c->hv_ev, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->hstream, c->hv_ev, 0));
+        HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr + offset, n * 4, hipMemcpyDeviceToHost, c->hstream));
+        HIP_TRY(c, hipEventRecord(c->hv_done, c->hstream));
+        c->hv_pending = true;
+        c->hv_gpu_wait = true;
+    }
+    if (n_copied) *n_copied = n;
+    return RDF_OK;
+}
+
+rdf_status rdf_handover_wait(rdf_ctx* c) {
+    if (!c) return RDF_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    return hv_wait(c, false);
 }
 
 rdf_status rdf_last_stats(rdf_ctx* c, rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs) {

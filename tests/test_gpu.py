@@ -374,6 +374,47 @@ def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
         g.close()
 
 
+def test_paged_async_refs_survive_the_next_page():
+    """rdf_copy_result_refs_async: page k's refs are queued on the copy stream into page-locked memory and the next
+    page is computed before anyone waits; after rdf_handover_wait each page's refs equal a synchronous copy of the same
+    page (the next page's emission waits for the copy on the GPU before it overwrites `out`).  Small pages of c5 and c1
+    samples, the two host buffers alternating, one of them in two chunks."""
+    g = _lib.Context(0)
+    try:
+        for cfg, scale, budget in (("c5", 0.01, 1 << 16), ("c1", 0.05, 1 << 14)):
+            d = dataset(cfg, scale)
+            g.set_triples(d.s, d.p, d.o, d.num_terms)
+            g.frequent_conditions(d.min_support)
+            g.build_capture_groups("spo")
+            bufs = [None, None]
+            pending = []  # (buffer, expected refs) of the page whose copy is in flight
+            pages = checked = 0
+            for k, _ in enumerate(g.pages(True, 1, budget)):
+                n = g.result_layout()["n_refs"]
+                exp = np.empty(max(n, 1), np.uint32)
+                assert g.copy_result_refs(0, n, exp) == n  # (waits for the previous page's queued copy first)
+                for buf, want in pending:  # that copy is complete now: its page's refs arrived intact
+                    assert np.array_equal(buf.array[:len(want)], want), (cfg, k)
+                    checked += 1
+                pending = []
+                b = bufs[k % 2]
+                if b is None or b.array.size < n:
+                    b = bufs[k % 2] = _lib.PinnedBuffer(max(n, 1), np.uint32)
+                half = n // 2
+                q = g.copy_result_refs_async(0, half, b.ptr)
+                q += g.copy_result_refs_async(half, n - half, b.ptr + 4 * half)
+                assert q == n
+                pending.append((b, exp[:n].copy()))
+                pages += 1
+            g.handover_wait()
+            for buf, want in pending:
+                assert np.array_equal(buf.array[:len(want)], want), cfg
+                checked += 1
+            assert pages > 2 and checked == pages, (cfg, pages, checked)
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("range_records,keep", [(1, 1), (7, 1), (300, 1), (1, 0), (7, 0), (300, 0)])
 def test_join_range_groups_parity(monkeypatch, range_records, keep):
     """Capture groups built in join-value ranges (the path of inputs with >= 2^32/9 triples; RDFIND_GROUP_RANGE forces
