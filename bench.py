@@ -143,6 +143,7 @@ class CompactSink:
     def __init__(self, early=True):
         self.bufs, self.cap, self.pinned, self._keep = None, {}, True, []
         self.early = early  # register the pinned buffers for the library's early hand-over (rdf_set_handover)
+        self.heavy, self.heavy_cap, self.heavy_chunks = {}, 0, 0  # the heavy-bits form's chunks (rdf_copy_result_heavy)
 
     def register(self, ctx):
         """The unpaged discoveries that follow fill the refs and the capture table of these buffers while they still
@@ -184,10 +185,27 @@ class CompactSink:
             self.register(ctx)
         return L
 
+    def copy_heavy(self, ctx):
+        """The heavy-bits form's part: one (dependent, list position, survivor word) per chunk of 64 class-list
+        candidates (rdf_copy_result_heavy), into pinned buffers grown like the others."""
+        from rdfind_amd import _lib
+        nh = ctx.heavy_chunk_count()
+        self.heavy_chunks = nh
+        if not nh:
+            return
+        if nh > self.heavy_cap:
+            need = max(nh, self.heavy_cap + self.heavy_cap // 2)
+            self.heavy = {}
+            for name, dt in (("deps", np.uint32), ("pos", np.uint64), ("bits", np.uint64)):
+                self.heavy[name] = _lib.PinnedBuffer(need, dt)
+            self.heavy_cap = need
+        ctx.copy_result_heavy(self.heavy["deps"].ptr, self.heavy["pos"].ptr, self.heavy["bits"].ptr)
+
     def copy(self, ctx, overlap=False):
         """overlap (pages): the refs are queued on the library's copy stream (rdf_copy_result_refs_async) and leave
         while the next page computes; the caller ends with ctx.handover_wait()."""
         L = self.ensure(ctx)
+        self.copy_heavy(ctx)
         if L["n_refs"] <= self.cap["refs"] and not (overlap and self.pinned):
             ctx.copy_result_compact(self.bufs)
             return L
@@ -201,9 +219,9 @@ class CompactSink:
         return L
 
 
-def layout_bytes(L):
+def layout_bytes(L, heavy_chunks=0):
     return (4 * L["n_refs"] + 12 * L["n_runs"] + 8 + 4 * L["n_list_refs"] + 8 * (L["n_lists"] + 1) +
-            8 * L["n_members"] + 8 * L["n_captures"])
+            8 * L["n_members"] + 8 * L["n_captures"] + 20 * heavy_chunks)
 
 
 def ctx_pages(ctx):
@@ -350,6 +368,8 @@ def main():
     ap.add_argument("--no-early-handover", action="store_true", help="hand the whole result over after each run "
                     "(no rdf_set_handover: the refs and the capture table are not copied while the run computes)")
     ap.add_argument("--page-log", action="store_true", help="one progress line per page on stderr (paged runs)")
+    ap.add_argument("--expanded-heavy", action="store_true", help="hand the heavy-only dependents' CINDs over as one "
+                    "u32 ref each (default: RDF_FORM_HEAVY_BITS, a survivor word per 64 class-list candidates)")
     ap.add_argument("--no-page-overlap", action="store_true", help="paged runs: hand each page's refs over before the "
                     "next page starts (default: queued on the copy stream while the next page computes)")
     ap.add_argument("--no-numa-bind", action="store_true", help="leave the process on every CPU (default: bound to the "
@@ -410,6 +430,9 @@ def main():
     ctx = _lib.Context(local_rank)
     ctx.set_triples(d.s, d.p, d.o, d.num_terms)  # inputs resident in HBM before the timed region
     sink = CompactSink(early=not args.no_early_handover)
+    # the heavy-only binary dependents' CINDs hand over as survivor words over their class lists (rdf_set_result_form;
+    # --expanded-heavy: one u32 ref each)
+    ctx.set_result_form(not args.expanded_heavy)
 
     paged = dist is None and args.page_bytes is not None
     if dist is None and not paged:  # a result larger than HBM: the unpaged run fails with RDF_ERR_OOM -> pages
@@ -510,11 +533,11 @@ def main():
     if dist is not None:
         import torch
         dev = f"cuda:{local_rank}" if args.backend == "nccl" else "cpu"
-        tot = torch.tensor([cs["n_cinds"], layout_bytes(L)], device=dev, dtype=torch.int64)
+        tot = torch.tensor([cs["n_cinds"], layout_bytes(L, sink.heavy_chunks)], device=dev, dtype=torch.int64)
         dist.all_reduce(tot)
         total_cinds, total_bytes = (int(x) for x in tot.tolist())
     else:
-        total_cinds, total_bytes = cs["n_cinds"], layout_bytes(L)
+        total_cinds, total_bytes = cs["n_cinds"], layout_bytes(L, sink.heavy_chunks)
     steps = max(args.steps, 1)
     ms_per_step = elapsed * 1000.0 / steps
     value = float(total_n) * steps / elapsed
@@ -621,7 +644,7 @@ def main():
                     "id-records (rdf_copy_result_compact) in pinned host memory, every rank" +
                     (" (paged: every page handed over in turn)" if paged else ""),
             "handover": {"bytes_all_ranks": total_bytes, "pinned": sink.pinned, "early": sink.early and sink.pinned,
-                         "n_refs": L["n_refs"],
+                         "n_refs": L["n_refs"], "heavy_chunks": sink.heavy_chunks,
                          "n_list_refs": L["n_list_refs"], "n_members": L["n_members"], "n_runs": L["n_runs"]},
             "device_resident": None if elapsed_dev is None else
                                {"ms_per_step": round(elapsed_dev * 1000.0 / steps, 3),

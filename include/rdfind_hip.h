@@ -252,6 +252,20 @@ rdf_status rdf_copy_result_refs_async(rdf_ctx* ctx, uint64_t offset, uint64_t co
 /* Wait until every queued asynchronous copy (rdf_copy_result_refs_async, the early hand-over) has reached the host. */
 rdf_status rdf_handover_wait(rdf_ctx* ctx);
 
+/* Result form of the compact hand-over, from the next discovery on.  RDF_FORM_EXPANDED (default): every non-class ref
+ * is an explicit ref.  RDF_FORM_HEAVY_BITS: the refs of the heavy-only binary dependents (checked against their mask
+ * class's shared list, K6d) leave as one 64-bit survivor word per chunk of 64 list candidates instead of one u32 per
+ * CIND: rdf_get_result_layout then counts only the explicit refs and runs, and rdf_copy_result_heavy hands over the
+ * chunks (dependent, position in the class lists `list_refs`, bits: bit b set = the CIND dependent ⊆ list_refs[pos + b]).
+ * Paged results send the class lists with the first page only; the later pages' chunks index them.  The device-side
+ * result (row accessors, checksums, formatting) is unchanged.  A CindSet per dependent either way
+ * (ALG/data/CindSet.scala:9-13). */
+#define RDF_FORM_EXPANDED 0u
+#define RDF_FORM_HEAVY_BITS 1u
+rdf_status rdf_set_result_form(rdf_ctx* ctx, uint32_t form);
+rdf_status rdf_heavy_chunk_count(rdf_ctx* ctx, uint64_t* n_chunks);
+rdf_status rdf_copy_result_heavy(rdf_ctx* ctx, uint32_t* deps, uint64_t* pos, uint64_t* bits);
+
 /* Page-locked host memory (hipHostMalloc) for hand-over buffers: the copies above then run at the link rate.
  * Returns null on failure; free with rdf_host_free. */
 void* rdf_host_alloc(uint64_t bytes);

@@ -816,6 +816,29 @@ uint64_t orc_checksum_compact(const uint32_t *refs, const uint64_t *runoff, cons
     return acc;
 }
 
+/* The heavy-bits part of a compact result (rdf_copy_result_heavy): chunk w of 64 class-list candidates of dependent
+ * deps[w] starting at list position pos[w]; bit b of bits[w] set = the CIND deps[w] < list_refs[pos[w] + b]. */
+uint64_t orc_checksum_heavy(const uint32_t *deps, const uint64_t *pos, const uint64_t *bits, uint64_t nchunks,
+                            const uint32_t *list_refs, const uint32_t *capture_ids, const uint32_t *supports, uint32_t V,
+                            uint64_t *count, uint64_t kind[4]) {
+    const uint64_t U = 6ull * V;
+    uint64_t acc = 0, cnt = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+#pragma omp parallel for reduction(+ : acc, cnt, k0, k1, k2, k3) schedule(static, 4096)
+    for (uint64_t w = 0; w < nchunks; ++w) {
+        const uint32_t d = deps[w], dx = capture_ids[d], sup = supports[d];
+        for (uint64_t m = bits[w]; m; m &= m - 1) {
+            const uint32_t rx = capture_ids[list_refs[pos[w] + (uint64_t)__builtin_ctzll(m)]];
+            acc += row_hash(dx, rx, sup);
+            cnt++;
+            const int k = (dx >= U) * 2 + (rx >= U);
+            k0 += k == 0; k1 += k == 1; k2 += k == 2; k3 += k == 3;
+        }
+    }
+    *count = cnt;
+    kind[0] = k0; kind[1] = k1; kind[2] = k2; kind[3] = k3;
+    return acc;
+}
+
 void orc_free(void *ptr) { free(ptr); }
 
 /* threads stages 4-6 use (OMP_NUM_THREADS, else all cores) */

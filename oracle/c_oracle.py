@@ -165,6 +165,21 @@ def checksum_compact(parts, num_terms):
                                  L["n_runs"], arr["list_refs"].ctypes.data, arr["list_off"].ctypes.data,
                                  arr["members"].ctypes.data, L["n_members"], arr["capture_ids"].ctypes.data,
                                  arr["supports"].ctypes.data, num_terms, ctypes.byref(cnt), kind.ctypes.data)
+    nh = int(parts.get("n_heavy_chunks", 0) or 0)
+    if nh:  # the heavy-bits form (rdf_copy_result_heavy): chunks of class-list candidates as survivor words
+        lib.orc_checksum_heavy.restype = ctypes.c_uint64
+        lib.orc_checksum_heavy.argtypes = ([ctypes.c_void_p] * 3 + [ctypes.c_uint64] + [ctypes.c_void_p] * 3 +
+                                           [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p])
+        lists = np.ascontiguousarray(parts.get("heavy_lists", parts["list_refs"]))  # (a later page: the first page's)
+        hv = {k: np.ascontiguousarray(parts[k]) for k in ("heavy_deps", "heavy_pos", "heavy_bits")}
+        hc = ctypes.c_uint64()
+        hk = np.zeros(4, np.uint64)
+        h2 = lib.orc_checksum_heavy(hv["heavy_deps"].ctypes.data, hv["heavy_pos"].ctypes.data,
+                                    hv["heavy_bits"].ctypes.data, nh, lists.ctypes.data, arr["capture_ids"].ctypes.data,
+                                    arr["supports"].ctypes.data, num_terms, ctypes.byref(hc), hk.ctypes.data)
+        h = (int(h) + int(h2)) % (1 << 64)
+        cnt.value += hc.value
+        kind += hk
     return int(cnt.value), int(h), [int(x) for x in kind]
 
 

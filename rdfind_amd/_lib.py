@@ -34,7 +34,8 @@ EXPORTED_SYMBOLS = (
     "rdf_copy_result_compact", "rdf_association_rule_count", "rdf_host_alloc", "rdf_host_free",
     "rdf_discover_cinds_paged", "rdf_next_page", "rdf_shard_parse_begin", "rdf_shard_dictionary_begin", "rdf_num_terms",
     "rdf_dictionary_terms", "rdf_copy_result_refs", "rdf_release_scratch", "rdf_set_handover",
-    "rdf_copy_result_refs_async", "rdf_handover_wait",
+    "rdf_copy_result_refs_async", "rdf_handover_wait", "rdf_set_result_form", "rdf_heavy_chunk_count",
+    "rdf_copy_result_heavy",
 )
 RDF_NT_TABS = 1
 
@@ -167,6 +168,9 @@ def load():
         "rdf_copy_result_refs": (i32, [P, u64, u64, P, ctypes.POINTER(u64)]),
         "rdf_copy_result_refs_async": (i32, [P, u64, u64, P, ctypes.POINTER(u64)]),
         "rdf_handover_wait": (i32, [P]),
+        "rdf_set_result_form": (i32, [P, u32]),
+        "rdf_heavy_chunk_count": (i32, [P, ctypes.POINTER(u64)]),
+        "rdf_copy_result_heavy": (i32, [P, P, P, P]),
         "rdf_set_handover": (i32, [P, P, u64, P, P, u64, P, P, u64]),
         "rdf_set_dictionary": (i32, [P, P, u64, P, u64]),
         "rdf_format_size": (i32, [P, u64, u64, ctypes.POINTER(u64)]),
@@ -530,12 +534,21 @@ class Context:
     def copy_result_compact(self, bufs: dict | None = None) -> dict:
         """rdf_copy_result_compact into ``bufs`` (name -> numpy array or raw pointer, e.g. pinned memory sized from
         :meth:`result_layout`), or into fresh numpy arrays; returns the name -> buffer dict."""
-        if bufs is None:
+        fresh = bufs is None
+        if fresh:
             L = self.result_layout()
             bufs = {name: np.empty(max(count(L), 1), dt) for name, dt, count in COMPACT_PARTS}
             bufs["layout"] = L
         ptrs = [bufs[name] if isinstance(bufs[name], int) else bufs[name].ctypes.data for name, _, _ in COMPACT_PARTS]
         self._check(self.lib.rdf_copy_result_compact(self.ptr, *ptrs), "rdf_copy_result_compact")
+        if fresh:  # the heavy-bits form's chunks (rdf_set_result_form), when the result has them
+            nh = self.heavy_chunk_count()
+            bufs["n_heavy_chunks"] = nh
+            if nh:
+                bufs["heavy_deps"] = np.empty(nh, np.uint32)
+                bufs["heavy_pos"] = np.empty(nh, np.uint64)
+                bufs["heavy_bits"] = np.empty(nh, np.uint64)
+                self.copy_result_heavy(bufs["heavy_deps"], bufs["heavy_pos"], bufs["heavy_bits"])
         return bufs
 
     def set_handover(self, refs=None, refs_cap: int = 0, runoff=None, rundep=None, runs_cap: int = 0, capture_ids=None,
@@ -562,6 +575,21 @@ class Context:
         self._check(self.lib.rdf_copy_result_refs_async(self.ptr, offset, count, ptr, ctypes.byref(copied)),
                     "rdf_copy_result_refs_async")
         return copied.value
+
+    def set_result_form(self, heavy_bits: bool) -> None:
+        """rdf_set_result_form: RDF_FORM_HEAVY_BITS (the heavy-only refs as survivor words over the class lists) or
+        the expanded form, from the next discovery on."""
+        self._check(self.lib.rdf_set_result_form(self.ptr, 1 if heavy_bits else 0), "rdf_set_result_form")
+
+    def heavy_chunk_count(self) -> int:
+        n = ctypes.c_uint64()
+        self._check(self.lib.rdf_heavy_chunk_count(self.ptr, ctypes.byref(n)), "rdf_heavy_chunk_count")
+        return int(n.value)
+
+    def copy_result_heavy(self, deps, pos, bits) -> None:
+        """rdf_copy_result_heavy into three buffers (numpy arrays or raw pointers) of heavy_chunk_count() elements."""
+        ptrs = [b if isinstance(b, int) else b.ctypes.data for b in (deps, pos, bits)]
+        self._check(self.lib.rdf_copy_result_heavy(self.ptr, *ptrs), "rdf_copy_result_heavy")
 
     def handover_wait(self) -> None:
         """rdf_handover_wait: every queued copy has reached the host."""

@@ -3142,6 +3142,17 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_output_runs(u32 C, const u64* __r
     }
 }
 
+// heavy-bits form (rdf_copy_result_heavy): the class-list position of the first candidate of heavy work items
+// [h0, h0 + W) (dependent deps[w] from the run table; its chunks are consecutive from choffh[dep])
+__global__ __launch_bounds__(RDF_BLOCK) void k_heavy_pos(u32 C, u64 h0, u64 W, const u64* __restrict__ choffh,
+                                                         const u32* __restrict__ deps, const u64* __restrict__ sbase,
+                                                         u64* pos) {
+    for (u64 w = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; w < W; w += (u64)gridDim.x * RDF_BLOCK) {
+        const u32 d = deps[w];
+        pos[w] = sbase[d] + (h0 + w - choffh[d]) * RDF_WAVE;
+    }
+}
+
 // run table of one page of a paged run: explicit runs of dependents [d0, d1) (their pairs start at e0 of the explicit
 // array; epos = the page's compaction offsets), heavy work items [h0, h0 + WH), then the class members (page 0)
 __global__ __launch_bounds__(RDF_BLOCK) void k_output_runs_range(u32 C, u32 d0, u32 d1, const u64* __restrict__ eoff, u64 e0,

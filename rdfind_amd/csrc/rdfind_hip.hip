@@ -158,6 +158,13 @@ struct rdf_ctx {
     // compact result: the class part (members x shared lists) is expanded into `out` only on demand
     bool class_pending = false;
     u64 pend_NT = 0, pend_base = 0, n_lists = 0, n_list_refs = 0, n_runs_explicit = 0;
+    // compact form of the heavy-only refs (rdf_set_result_form(RDF_FORM_HEAVY_BITS)): the current result's K explicit
+    // refs, its explicit runs [0, res_nx) and heavy work items (chunks of 64 class-list candidates) [0, res_wh) of the
+    // work-item range starting at res_h0; res_bits: the form applies to this result (classed heavy-only dependents)
+    u32 result_form = 0;
+    u64 res_K = 0, res_nx = 0, res_wh = 0, res_h0 = 0;
+    bool res_bits = false;
+    DevBuf hpos;
     DevBuf loff;  // list offsets of the shared (class) ref lists
     // paged discovery (rdf_discover_cinds_paged / rdf_next_page): dependents in ranges, one page at a time
     bool paged = false, pg_unary_done = false;
@@ -466,11 +473,11 @@ static std::vector<DevBuf*> ctx_buffers(rdf_ctx* c) {
             &c->ukeys_tmp, &c->ithv, &c->ikeys, &c->ikeys_tmp, &c->iwords, &c->iwoff, &c->ihdr, &c->ipay, &c->ibnd, &c->iwb,
             &c->rhdr, &c->rlen, &c->rwords, &c->rwoff, &c->rts, &c->rhv, &c->rvalid, &c->rtab, &c->rslot, &c->rrep, &c->rfirst,
             &c->rfid, &c->rhist, &c->rreply, &c->own_text, &c->own_off, &c->own_len, &c->gmapv, &c->dneed, &c->dnpos, &c->dwn,
-            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore, &c->jbh, &c->iflag, &c->iexcl, &c->iorder, &c->ukey, &c->utab, &c->urep, &c->ucnt, &c->unoff, &c->uebin, &c->umem};
+            &c->dwo, &c->dhdr, &c->dlen, &c->dlwords, &c->dwoff, &c->tids, &c->tlenv, &c->toffv, &c->tout, &c->rstore, &c->jbh, &c->iflag, &c->iexcl, &c->iorder, &c->ukey, &c->utab, &c->urep, &c->ucnt, &c->unoff, &c->uebin, &c->umem, &c->hpos};
 }
 
 // RDFIND_MEM_REPORT=1: after each rdf_run, the context's buffers of >= 256 MiB (name, GiB) on stderr, largest first
-static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder", "ukey", "utab", "urep", "ucnt", "unoff", "uebin", "umem"};
+static const char* const kBufNames[] = {"scal", "ts", "tp", "to", "cnt", "tkeys", "tcnt", "bkeys", "bkeys_tmp", "lkeys", "lvals", "flags", "pos", "rec", "rec_tmp", "support", "fidx", "fcap", "frank", "fval", "fext", "info", "fk", "fk_tmp", "fpos", "cstart", "skip", "gflag", "gexcl", "goff", "gcap", "gmap", "csup", "doff", "dcur", "dgrp", "jhist", "rsup", "lsup", "hot", "hotc", "jrmap", "offp", "hist", "heavy_list", "hbit", "bcomp", "bkeyc", "pcnt", "poff", "pcur", "plist", "pivot", "nchl", "nchh", "choffl", "choffh", "epairs", "epairs_tmp", "eoff", "hcounts", "hoff", "hbits", "cbits", "hown", "cown", "sbase", "dcls", "crep", "out", "stage_rows", "nitl", "itoffl", "dead", "ebin", "pseg", "psegoff", "pbest", "pnl", "lsig", "brkeys2", "bstart2", "ginfo", "gsums", "piv2", "pivx", "ecache", "ctab", "cflag", "ccid", "ckeys", "ckeys_tmp", "coff", "cmask", "cpiv", "cnch", "cchoff", "ccnt", "lwoff", "clists", "cself", "cmcnt", "cobase", "ctiles", "ctoff", "pedges", "pedges_tmp", "item_dep", "eblk", "lslot", "npk", "pkoff", "pk_dep", "nmch", "mchoff", "mch_dep", "uhist", "urecs", "usl", "cntg", "fstage", "bfreq", "boff", "fbits", "brkeys", "xsend", "xrecv", "gbest", "nrl", "smask", "smask_tmp", "cpairs", "cpairs_tmp", "obounds", "lmask", "hrep", "vpairs", "vcoff", "vpiv", "runoff", "rundep", "dheap", "dtoff", "cslen", "csoff", "cstr", "flen", "floff", "fbuf", "drows", "ppart", "wts", "wtp", "wto", "arcnt", "ar_bits", "ar_rules", "arref", "loff", "gdrow", "dlist", "dbits", "ebown", "bslots", "bcounts", "segb", "sege", "seglen", "ukeys", "ukeys_tmp", "ithv", "ikeys", "ikeys_tmp", "iwords", "iwoff", "ihdr", "ipay", "ibnd", "iwb", "rhdr", "rlen", "rwords", "rwoff", "rts", "rhv", "rvalid", "rtab", "rslot", "rrep", "rfirst", "rfid", "rhist", "rreply", "own_text", "own_off", "own_len", "gmapv", "dneed", "dnpos", "dwn", "dwo", "dhdr", "dlen", "dlwords", "dwoff", "tids", "tlenv", "toffv", "tout", "rstore", "jbh", "iflag", "iexcl", "iorder", "ukey", "utab", "urep", "ucnt", "unoff", "uebin", "umem", "hpos"};
 static bool mem_report_on() {
     static const bool on = getenv("RDFIND_MEM_REPORT") && atoi(getenv("RDFIND_MEM_REPORT")) != 0;
     return on;
@@ -3033,8 +3040,13 @@ static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 W
     c->class_pending = NT > 0;
     c->pend_NT = NT;
     c->pend_base = K + H;
+    c->res_bits = c->result_form == RDF_FORM_HEAVY_BITS && c->hclassed && WH;
+    c->res_K = K;
+    c->res_nx = c->C;
+    c->res_wh = WH;
+    c->res_h0 = 0;
     const u32 ncls = (u32)c->n_classes;
-    c->n_lists = HC ? ncls : 0;
+    c->n_lists = HC || c->res_bits ? ncls : 0;  // (the heavy bits index the class lists)
     c->n_list_refs = 0;
     if (c->n_lists) {
         ENSURE(c, loff, (ncls + 1ull) * 8);
@@ -3193,6 +3205,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
     TRY(hv_wait(c, true));
+    c->res_bits = false;  // (the heavy-bits form applies to the result of d_emit_rest / d_page_emit only)
     c->paged = false;
     // test hook (RDFIND_TEST_OOM_DISCOVERY=1): the unpaged discovery reports RDF_ERR_OOM at once, so a caller's
     // fallback to pages runs on small inputs
@@ -3349,8 +3362,15 @@ static rdf_status d_page_emit(rdf_ctx* c, const CindView& v, u32 d0, u32 d1, u64
     c->class_pending = NT > 0;
     c->pend_NT = NT;
     c->pend_base = K + H;
+    c->res_bits = c->result_form == RDF_FORM_HEAVY_BITS && c->hclassed && c->n_classes;
+    c->res_K = K;
+    c->res_nx = nd;
+    c->res_wh = WHr;
+    c->res_h0 = h0;
     const u32 ncls = (u32)c->n_classes;
-    c->n_lists = HC ? ncls : 0;
+    // the class lists go with the first page (the class part; in the heavy-bits form also the lists every later page's
+    // heavy bits index: a consumer keeps them)
+    c->n_lists = HC || (c->res_bits && d0 == 0) ? ncls : 0;
     c->n_list_refs = 0;
     if (c->n_lists) {
         ENSURE(c, loff, (ncls + 1ull) * 8);
@@ -3411,6 +3431,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
     TRY(hv_wait(c, true));
+    c->res_bits = false;  // (the heavy-bits form applies to the result of d_emit_rest / d_page_emit only)
     hipStream_t st = c->stream;
     if (!page_bytes) {  // an eighth of the free HBM, at most 32 GB: the resident unary pairs need the rest
         size_t fr = 0, tot = 0;
@@ -3521,6 +3542,7 @@ rdf_status rdf_next_page(rdf_ctx* c, uint32_t* done, uint64_t* first_dep, uint64
     } else {
         *done = 1;
         c->n_out = c->n_class_out = c->n_runs = c->n_runs_explicit = c->n_lists = c->n_list_refs = 0;
+        c->res_bits = false;
         c->class_pending = false;
         HIP_TRY(c, c->runoff.ensure(8));
         HIP_TRY(c, hipMemsetAsync(c->runoff.p, 0, 8, c->stream));
@@ -4610,6 +4632,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
                            uint32_t flags) {
     if (!c) return RDF_ERR_ARG;
     if (c) TRY(hv_wait(c, true));
+    c->res_bits = false;  // (the heavy-bits form applies to the result of d_emit_rest / d_page_emit only)
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
     c->hclassed = false;
@@ -4787,12 +4810,17 @@ void rdf_host_free(void* p) {
     if (p) (void)hipHostFree(p);
 }
 
+// explicit refs and runs of the compact result: all of the non-class refs, or (heavy-bits form) the explicit ones only,
+// the heavy-only ones leaving as bits (rdf_copy_result_heavy)
+static u64 compact_refs(const rdf_ctx* c) { return c->res_bits ? c->res_K : c->n_out - c->n_class_out; }
+static u64 compact_runs(const rdf_ctx* c) { return c->res_bits ? c->res_nx : c->n_runs_explicit; }
+
 rdf_status rdf_get_result_layout(rdf_ctx* c, rdf_result_layout* L) {
     if (!c || !L) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     L->n_cinds = c->n_out;
-    L->n_refs = c->n_out - c->n_class_out;
-    L->n_runs = c->n_runs_explicit;
+    L->n_refs = compact_refs(c);
+    L->n_runs = compact_runs(c);
     L->n_lists = c->n_lists;
     L->n_list_refs = c->n_list_refs;
     L->n_members = c->n_class_out ? c->n_class_members : 0;
@@ -4809,7 +4837,7 @@ rdf_status rdf_copy_result_compact(rdf_ctx* c, uint32_t* refs, uint64_t* runoff,
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    const u64 nrefs = c->n_out - c->n_class_out, R = c->n_runs_explicit;
+    const u64 nrefs = compact_refs(c), R = compact_runs(c);
     const u64 nmem = c->n_class_out ? c->n_class_members : 0;
     // parts the early hand-over already copied into these same buffers: only their tails (heavy-only refs behind the
     // explicit ones) or nothing
@@ -4861,7 +4889,7 @@ rdf_status rdf_copy_result_refs(rdf_ctx* c, uint64_t offset, uint64_t count, uin
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
     TRY(hv_wait(c, false));  // (an asynchronous copy may still write the same host buffer)
-    const u64 nrefs = c->n_out - c->n_class_out;
+    const u64 nrefs = compact_refs(c);
     const u64 n = offset < nrefs ? std::min<u64>(count, nrefs - offset) : 0;
     if (n) HIP_TRY(c, hipMemcpyAsync(refs, c->out_ptr + offset, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -4873,7 +4901,7 @@ rdf_status rdf_copy_result_refs_async(rdf_ctx* c, uint64_t offset, uint64_t coun
     if (!c || (count && !refs)) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
-    const u64 nrefs = c->n_out - c->n_class_out;
+    const u64 nrefs = compact_refs(c);
     const u64 n = offset < nrefs ? std::min<u64>(count, nrefs - offset) : 0;
     if (n) {  // after everything queued so far on the compute stream, on the copy stream
         HIP_TRY(c, hipEventRecord(c->hv_ev, c->stream));
@@ -4891,6 +4919,38 @@ rdf_status rdf_handover_wait(rdf_ctx* c) {
     if (!c) return RDF_ERR_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     return hv_wait(c, false);
+}
+
+rdf_status rdf_set_result_form(rdf_ctx* c, uint32_t form) {
+    if (!c || form > RDF_FORM_HEAVY_BITS) return RDF_ERR_ARG;
+    c->result_form = form;  // (from the next discovery on)
+    return RDF_OK;
+}
+
+rdf_status rdf_heavy_chunk_count(rdf_ctx* c, uint64_t* n) {
+    if (!c || !n) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    *n = c->res_bits ? c->res_wh : 0;
+    return RDF_OK;
+}
+
+rdf_status rdf_copy_result_heavy(rdf_ctx* c, uint32_t* deps, uint64_t* pos, uint64_t* bits) {
+    if (!c) return RDF_ERR_ARG;
+    if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const u64 W = c->res_bits ? c->res_wh : 0;
+    if (!W) return RDF_OK;
+    if (!deps || !pos || !bits) return RDF_ERR_ARG;
+    hipStream_t st = c->stream;
+    ENSURE(c, hpos, W * 8);
+    hipLaunchKernelGGL(k_heavy_pos, dim3(grid_for(W, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st, c->C, c->res_h0, W,
+                       c->choffh.as<u64>(), c->rundep.as<u32>() + c->res_nx, c->sbase.as<u64>(), c->hpos.as<u64>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(deps, c->rundep.as<u32>() + c->res_nx, W * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(pos, c->hpos.p, W * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(bits, c->hbits.p, W * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    return RDF_OK;
 }
 
 rdf_status rdf_last_stats(rdf_ctx* c, rdf_fc_stats* fc, rdf_group_stats* gs, rdf_cind_stats* cs) {

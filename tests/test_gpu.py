@@ -346,6 +346,68 @@ def _paged(g, ms, strategy, clean, page_bytes, keep_rows=True):
 
 
 @pytest.mark.parametrize("heavy_min", [64, 2])
+def test_heavy_bits_form_parity(monkeypatch, heavy_min):
+    """rdf_set_result_form(RDF_FORM_HEAVY_BITS): the heavy-only binary dependents' CINDs leave as survivor words over the
+    class lists (rdf_copy_result_heavy) instead of explicit refs.  The compact parts, expanded by the checker, give the
+    device's count and checksum and the oracle's, unpaged (random inputs in the classed mode, c5 / c1 / c2 samples) and
+    paged (later pages index the first page's lists); the expanded form's explicit refs are the explicit part plus the
+    heavy chunks' refs."""
+    monkeypatch.setenv("RDFIND_HEAVY_MIN", str(heavy_min))
+    g = _lib.Context(0)
+    e = _lib.Context(0)
+    try:
+        g.set_result_form(True)
+        rng = random.Random(900 + heavy_min)
+        chunks = 0
+        for _ in range(12):
+            n = rng.randrange(20, 400)
+            nv = rng.randrange(4, 40)
+            ms = rng.randrange(1, 4)
+            arr = np.array([(rng.randrange(nv), rng.randrange(nv // 4 + 1), rng.randrange(nv)) for _ in range(n)],
+                           dtype=np.uint32)
+            g.set_triples(arr[:, 0], arr[:, 1], arr[:, 2], nv)
+            g.run(ms)
+            parts = g.copy_result_compact()
+            chunks += parts["n_heavy_chunks"]
+            assert C.checksum_compact(parts, nv)[:2] == (g.cind_count(), g.checksum()), (n, nv, ms)
+        for cfg, scale in (("c5", 0.01), ("c1", 0.05), ("c2", 0.02)):
+            d = dataset(cfg, scale)
+            exp = oracle_stream(cfg, scale)
+            for c in (g, e):
+                c.set_triples(d.s, d.p, d.o, d.num_terms)
+                c.run(d.min_support)
+            parts, full = g.copy_result_compact(), e.copy_result_compact()
+            chunks += parts["n_heavy_chunks"]
+            assert C.checksum_compact(parts, d.num_terms)[:2] == (exp["n_cinds"], exp["checksum"]), cfg
+            assert C.checksum_compact(full, d.num_terms)[:2] == (exp["n_cinds"], exp["checksum"]), cfg
+            if parts["n_heavy_chunks"]:
+                assert parts["layout"]["n_refs"] < full["layout"]["n_refs"], cfg
+        assert chunks > 0  # the form was exercised
+        # paged: each page's parts (heavy chunks indexing the first page's class lists)
+        d = dataset("c5", 0.01)
+        exp = oracle_stream("c5", 0.01)
+        g.set_triples(d.s, d.p, d.o, d.num_terms)
+        g.frequent_conditions(d.min_support)
+        g.build_capture_groups("spo")
+        n = h = pages = 0
+        lists = None
+        for _ in g.pages(True, 1, 1 << 16):
+            parts = g.copy_result_compact()
+            if lists is None:
+                lists = parts["list_refs"].copy()
+            parts["heavy_lists"] = lists
+            cnt, hh, _ = C.checksum_compact(parts, d.num_terms)
+            assert (cnt, hh) == (g.cind_count(), g.checksum())
+            n += cnt
+            h = (h + hh) % (1 << 64)
+            pages += 1
+        assert (n, h) == (exp["n_cinds"], exp["checksum"]) and pages > 2
+    finally:
+        g.close()
+        e.close()
+
+
+@pytest.mark.parametrize("heavy_min", [64, 2])
 def test_paged_discovery_matches_unpaged(monkeypatch, heavy_min):
     """rdf_discover_cinds_paged with a one-byte page budget (every binary dependent is its own page) partitions the
     unpaged result, in every mode, with and without bitmask columns and classes."""
