@@ -165,6 +165,10 @@ struct rdf_ctx {
     u64 res_K = 0, res_nx = 0, res_wh = 0, res_h0 = 0;
     bool res_bits = false;
     DevBuf hpos;
+    // ... and their expansion into `out` (k_heavy_write) deferred to the first row accessor, like the class part:
+    // work items [hp_h0, hp_h0 + hp_W) at output offset hp_K
+    bool heavy_pending = false;
+    u64 hp_W = 0, hp_h0 = 0, hp_K = 0;
     DevBuf loff;  // list offsets of the shared (class) ref lists
     // paged discovery (rdf_discover_cinds_paged / rdf_next_page): dependents in ranges, one page at a time
     bool paged = false, pg_unary_done = false;
@@ -3027,12 +3031,20 @@ static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 W
         TRY(hv_wait(c, false));
         HIP_TRY(c, c->out.grow_keep(std::max<u64>(K + H, 1) * 4, st));
     }
+    c->res_bits = c->result_form == RDF_FORM_HEAVY_BITS && c->hclassed && WH;
+    c->heavy_pending = false;
     tbegin(c, RDF_T_HWRITE);
-    if (WH)
+    if (WH && c->res_bits) {  // (handed over as bits; expanded in `out` only when a row accessor needs it)
+        c->heavy_pending = true;
+        c->hp_W = WH;
+        c->hp_h0 = 0;
+        c->hp_K = K;
+    } else if (WH) {
         hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(WH))),
                            dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WH), v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), 0ull, WH,
                            c->hbits.as<u64>(), c->hclassed ? c->clists.as<u32>() : c->gcap.as<u32>(),
                            c->hclassed ? c->sbase.as<u64>() : (const u64*)nullptr, c->hoff.as<u64>(), K, c->out.as<u32>());
+    }
     tend(c, RDF_T_HWRITE);
     // The class part stays compact: each member's refs are its class's shared list minus itself (a CindSet whose
     // ref list is shared, ALG/data/CindSet.scala:9-13).  rdf_copy_result_compact hands it over as is; the expanded
@@ -3040,7 +3052,6 @@ static rdf_status d_emit_rest(rdf_ctx* c, const CindView& v, u64 E, u64 K, u64 W
     c->class_pending = NT > 0;
     c->pend_NT = NT;
     c->pend_base = K + H;
-    c->res_bits = c->result_form == RDF_FORM_HEAVY_BITS && c->hclassed && WH;
     c->res_K = K;
     c->res_nx = c->C;
     c->res_wh = WH;
@@ -3205,7 +3216,7 @@ rdf_status rdf_discover_cinds(rdf_ctx* c, uint32_t flags, rdf_cind_stats* stats)
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
     TRY(hv_wait(c, true));
-    c->res_bits = false;  // (the heavy-bits form applies to the result of d_emit_rest / d_page_emit only)
+    c->res_bits = c->heavy_pending = false;  // (the heavy-bits form: results of d_emit_rest / d_page_emit only)
     c->paged = false;
     // test hook (RDFIND_TEST_OOM_DISCOVERY=1): the unpaged discovery reports RDF_ERR_OOM at once, so a caller's
     // fallback to pages runs on small inputs
@@ -3352,17 +3363,24 @@ static rdf_status d_page_emit(rdf_ctx* c, const CindView& v, u32 d0, u32 d1, u64
     if (E)
         hipLaunchKernelGGL(k_compact_refs, dim3(grid_for(E, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->epairs.as<u64>() + e0, E, c->flags.as<u32>(), c->pos.as<u64>(), c->out.as<u32>());
+    c->res_bits = c->result_form == RDF_FORM_HEAVY_BITS && c->hclassed && c->n_classes;
+    c->heavy_pending = false;  // (the previous page's, if nobody asked for its rows)
     tbegin(c, RDF_T_HWRITE);
-    if (WHr)
+    if (WHr && c->res_bits) {  // (handed over as bits; expanded in `out` only when a row accessor needs it)
+        c->heavy_pending = true;
+        c->hp_W = WHr;
+        c->hp_h0 = h0;
+        c->hp_K = K;
+    } else if (WHr) {
         hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(WHr))), dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(WHr), v,
                            c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), h0, WHr, c->hbits.as<u64>(),
                            c->hclassed ? c->clists.as<u32>() : c->gcap.as<u32>(),
                            c->hclassed ? c->sbase.as<u64>() : (const u64*)nullptr, c->hoff.as<u64>(), K, c->out.as<u32>());
+    }
     tend(c, RDF_T_HWRITE);
     c->class_pending = NT > 0;
     c->pend_NT = NT;
     c->pend_base = K + H;
-    c->res_bits = c->result_form == RDF_FORM_HEAVY_BITS && c->hclassed && c->n_classes;
     c->res_K = K;
     c->res_nx = nd;
     c->res_wh = WHr;
@@ -3431,7 +3449,7 @@ rdf_status rdf_discover_cinds_paged(rdf_ctx* c, uint32_t flags, uint64_t page_by
     if (c->nranks != 1) return fail(c, RDF_ERR_STATE, "capture groups were built in sharded mode");
     HIP_TRY(c, hipSetDevice(c->device));
     TRY(hv_wait(c, true));
-    c->res_bits = false;  // (the heavy-bits form applies to the result of d_emit_rest / d_page_emit only)
+    c->res_bits = c->heavy_pending = false;  // (the heavy-bits form: results of d_emit_rest / d_page_emit only)
     hipStream_t st = c->stream;
     if (!page_bytes) {  // an eighth of the free HBM, at most 32 GB: the resident unary pairs need the rest
         size_t fr = 0, tot = 0;
@@ -3542,7 +3560,7 @@ rdf_status rdf_next_page(rdf_ctx* c, uint32_t* done, uint64_t* first_dep, uint64
     } else {
         *done = 1;
         c->n_out = c->n_class_out = c->n_runs = c->n_runs_explicit = c->n_lists = c->n_list_refs = 0;
-        c->res_bits = false;
+        c->res_bits = c->heavy_pending = false;
         c->class_pending = false;
         HIP_TRY(c, c->runoff.ensure(8));
         HIP_TRY(c, hipMemsetAsync(c->runoff.p, 0, 8, c->stream));
@@ -4632,7 +4650,7 @@ rdf_status rdf_shard_begin(rdf_ctx* c, uint32_t rank, uint32_t nranks, uint32_t 
                            uint32_t flags) {
     if (!c) return RDF_ERR_ARG;
     if (c) TRY(hv_wait(c, true));
-    c->res_bits = false;  // (the heavy-bits form applies to the result of d_emit_rest / d_page_emit only)
+    c->res_bits = c->heavy_pending = false;  // (the heavy-bits form: results of d_emit_rest / d_page_emit only)
     if (nranks < 1 || nranks > RDF_MAX_RANKS || rank >= nranks) return fail(c, RDF_ERR_ARG, "invalid rank / nranks");
     if (c->stage < 1) return fail(c, RDF_ERR_STATE, "rdf_set_triples must be called first");
     c->hclassed = false;
@@ -4781,7 +4799,25 @@ rdf_status rdf_shard_import(rdf_ctx* c, const void* src, uint64_t count) {
 
 // Expands the class part of the result (members x shared lists) into per-dependent runs behind the explicit refs:
 // needed by every row-level accessor (copy, decode, checksum, formatting), not by rdf_copy_result_compact.
+// the heavy-bits form's refs written into `out` behind the explicit ones (k_heavy_write, deferred by d_emit_rest /
+// d_page_emit): row accessors and the device checksum read them there
+static rdf_status materialize_heavy(rdf_ctx* c) {
+    if (!c->heavy_pending) return RDF_OK;
+    hipStream_t st = c->stream;
+    HIP_TRY(c, hipSetDevice(c->device));
+    TRY(hv_wait(c, false));
+    CindView v = {};  // (the classed write reads only the class lists through sbase)
+    hipLaunchKernelGGL(k_heavy_write, dim3(vgrid(wave_blocks(c->hp_W))), dim3(RDF_BLOCK), 0, st, (u64)wave_blocks(c->hp_W),
+                       v, c->pivot.as<u32>(), c->choffh.as<u64>(), c->hown.as<u32>(), c->hp_h0, c->hp_W, c->hbits.as<u64>(),
+                       c->clists.as<u32>(), c->sbase.as<u64>(), c->hoff.as<u64>(), c->hp_K, c->out.as<u32>());
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+    c->heavy_pending = false;
+    return RDF_OK;
+}
+
 static rdf_status materialize(rdf_ctx* c) {
+    TRY(materialize_heavy(c));
     if (!c->class_pending) return RDF_OK;
     hipStream_t st = c->stream;
     HIP_TRY(c, hipSetDevice(c->device));
@@ -5090,6 +5126,7 @@ rdf_status rdf_cind_checksum(rdf_ctx* c, uint64_t* checksum) {
     if (!c || !checksum) return RDF_ERR_ARG;
     if (c->stage < 4) return fail(c, RDF_ERR_STATE, "rdf_discover_cinds must be called first");
     HIP_TRY(c, hipSetDevice(c->device));
+    TRY(materialize_heavy(c));
     HIP_TRY(c, hipMemsetAsync(dscal(c, 7), 0, 8, c->stream));
     // a pending class part is summed from the compact form (no expansion: 4 B per row of HBM it would need)
     const u64 nrows = c->class_pending ? c->n_out - c->n_class_out : c->n_out;

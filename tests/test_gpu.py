@@ -382,6 +382,10 @@ def test_heavy_bits_form_parity(monkeypatch, heavy_min):
             assert C.checksum_compact(full, d.num_terms)[:2] == (exp["n_cinds"], exp["checksum"]), cfg
             if parts["n_heavy_chunks"]:
                 assert parts["layout"]["n_refs"] < full["layout"]["n_refs"], cfg
+            # the device-side result (the heavy refs expanded on first use) equals the expanded form's
+            assert (g.cind_count(), g.checksum()) == (e.cind_count(), e.checksum()) == (exp["n_cinds"], exp["checksum"])
+            if cfg != "c2":  # every row (external ids) against the materializing C oracle
+                assert_rows_equal(g, d)
         assert chunks > 0  # the form was exercised
         # paged: each page's parts (heavy chunks indexing the first page's class lists)
         d = dataset("c5", 0.01)
