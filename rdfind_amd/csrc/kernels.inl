@@ -363,6 +363,26 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_bkey_repack(u64* __restrict__ key
     }
 }
 
+// the same keys packed by the global ranks of their two frequent unary conditions (strictly increasing in the value for
+// a fixed position, and the positions are fixed per key type), so the order is the same in fewer bits: c2's keys
+// 2 + 2 x 23 -> 2 + 2 x 19 bits, five radix passes instead of six.  bt 0: (p, o), 1: (s, o), 2: (s, p)
+__global__ __launch_bounds__(RDF_BLOCK) void k_bkey_rank_repack(u64* __restrict__ keys, u64 B, int rb, u32 V,
+                                                                const u32* __restrict__ frank, const u32* __restrict__ fval,
+                                                                int unpack) {
+    const u64 m = (1ull << rb) - 1;
+    for (u64 b = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; b < B; b += (u64)gridDim.x * RDF_BLOCK) {
+        const u64 k = keys[b];
+        if (unpack) {
+            keys[b] = bin_key(k >> (2 * rb), fval[(k >> rb) & m], fval[k & m]);
+        } else {
+            const int bt = bin_key_type(k);
+            const u64 pa = bt == 0 ? 1 : 0, pb = bt == 2 ? 1 : 2;
+            const u64 r1 = frank[pa * V + bin_key_v1(k)], r2 = frank[pb * V + bin_key_v2(k)];
+            keys[b] = ((u64)bt << (2 * rb)) | (r1 << rb) | r2;
+        }
+    }
+}
+
 __global__ __launch_bounds__(RDF_BLOCK) void k_bin_lookup_build(const u64* __restrict__ bkeys, u64 B, u64* lkeys, u32* lvals,
                                                                 u64 mask) {
     for (u64 b = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; b < B; b += (u64)gridDim.x * RDF_BLOCK) {

@@ -1230,11 +1230,22 @@ static rdf_status fc_binary_index(rdf_ctx* c, u64 B) {
         u64* t = c->bkeys_tmp.as<u64>();
         const int jb = c->V ? bits_for(c->V - 1) : 31;
         const bool dense = B && jb < 31;
+        // one GPU: the keys by their conditions' global ranks when that saves a radix pass (frank / fval are final)
+        const int rb = c->U ? bits_for(c->U - 1) : 31;
+        const bool ranked = dense && c->nranks == 1 && radix_sort_passes(2 + 2 * rb) < radix_sort_passes(2 + 2 * jb);
         const dim3 g(grid_for(B, RDF_BLOCK, kGrid));
-        if (dense) hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, k, B, jb, 0);
-        HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, dense ? 2 + 2 * jb : 64, st));
+        if (ranked)
+            hipLaunchKernelGGL(k_bkey_rank_repack, g, dim3(RDF_BLOCK), 0, st, k, B, rb, c->V, c->frank.as<u32>(),
+                               c->fval.as<u32>(), 0);
+        else if (dense)
+            hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, k, B, jb, 0);
+        HIP_TRY(c, radix_sort_u64(c->ws, k, t, B, ranked ? 2 + 2 * rb : dense ? 2 + 2 * jb : 64, st));
         if (k != c->bkeys.as<u64>()) std::swap(c->bkeys, c->bkeys_tmp);
-        if (dense) hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, jb, 1);
+        if (ranked)
+            hipLaunchKernelGGL(k_bkey_rank_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, rb, c->V,
+                               c->frank.as<u32>(), c->fval.as<u32>(), 1);
+        else if (dense)
+            hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, jb, 1);
     }
     c->lcap = next_pow2(2 * B + 16);
     ENSURE(c, lkeys, c->lcap * 8);
