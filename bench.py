@@ -251,10 +251,9 @@ def per_rank_balance(dist, world, mine):
                               for k in mine if all(isinstance(r.get(k), (int, float)) for r in allr)}}
 
 
-# the one-GPU c4 step this leg is compared with: round 5 (kept join ranges, K2 radix path, light load chains, XCD-local
-# radix tiles), the
-# c4_strong leg of profiles/r05_bench_c2.json (round 4: 1616 ms)
-C4_ONE_GPU_MS = 830.8
+# the one-GPU c4 step this leg is compared with: round 6 (digit-row scans, K1's radix form), the c4_strong leg of
+# profiles/r06_bench_c2.json (round 5: 830.8 ms, round 4: 1616 ms)
+C4_ONE_GPU_MS = 819.6
 
 
 def c4_golden(scale):
