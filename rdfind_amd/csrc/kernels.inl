@@ -383,15 +383,23 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_bkey_rank_repack(u64* __restrict_
     }
 }
 
+// binary-condition lookup table (open addressing, at most half full).  SLOT16: key and value side by side in one
+// 16-byte slot, so a probe is one load; 0: separate key / value arrays (the value a second, dependent load)
+#ifndef RDF_LOOKUP_SLOT16
+#define RDF_LOOKUP_SLOT16 1
+#endif
 __global__ __launch_bounds__(RDF_BLOCK) void k_bin_lookup_build(const u64* __restrict__ bkeys, u64 B, u64* lkeys, u32* lvals,
                                                                 u64 mask) {
     for (u64 b = (u64)blockIdx.x * RDF_BLOCK + threadIdx.x; b < B; b += (u64)gridDim.x * RDF_BLOCK) {
         u64 key = bkeys[b];
         u64 h = mix64(key) & mask;
         for (;;) {
-            u64 prev = atomicCAS(&lkeys[h], EMPTY64, key);
+            u64 prev = atomicCAS(&lkeys[RDF_LOOKUP_SLOT16 ? 2 * h : h], EMPTY64, key);
             if (prev == EMPTY64) {
-                lvals[h] = (u32)b;
+                if (RDF_LOOKUP_SLOT16)
+                    lkeys[2 * h + 1] = b;
+                else
+                    lvals[h] = (u32)b;
                 break;
             }
             h = (h + 1) & mask;
@@ -399,11 +407,20 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_bin_lookup_build(const u64* __res
     }
 }
 
+struct alignas(16) LookupSlot {
+    u64 key, val;
+};
 __device__ inline u32 bin_lookup_from(const u64* lkeys, const u32* lvals, u64 mask, u64 key, u64 h) {
     for (;;) {
-        u64 k = lkeys[h];
-        if (k == key) return lvals[h];
-        if (k == EMPTY64) return NONE32;
+        if (RDF_LOOKUP_SLOT16) {
+            const LookupSlot sl = ((const LookupSlot*)lkeys)[h];
+            if (sl.key == key) return (u32)sl.val;
+            if (sl.key == EMPTY64) return NONE32;
+        } else {
+            u64 k = lkeys[h];
+            if (k == key) return lvals[h];
+            if (k == EMPTY64) return NONE32;
+        }
         h = (h + 1) & mask;
     }
 }
@@ -420,10 +437,11 @@ __device__ inline void bin_lookup3(const u64* __restrict__ lkeys, const u32* __r
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
         h[t] = mix64(key[t]) & mask;
-        k[t] = need[t] ? lkeys[h[t]] : EMPTY64;
+        k[t] = need[t] ? lkeys[RDF_LOOKUP_SLOT16 ? 2 * h[t] : h[t]] : EMPTY64;
     }
 #pragma unroll
-    for (int t = 0; t < 3; ++t) out[t] = need[t] && k[t] == key[t] ? lvals[h[t]] : NONE32;
+    for (int t = 0; t < 3; ++t)
+        out[t] = need[t] && k[t] == key[t] ? (RDF_LOOKUP_SLOT16 ? (u32)lkeys[2 * h[t] + 1] : lvals[h[t]]) : NONE32;
 #pragma unroll
     for (int t = 0; t < 3; ++t)
         if (need[t] && k[t] != key[t] && k[t] != EMPTY64) out[t] = bin_lookup_from(lkeys, lvals, mask, key[t], (h[t] + 1) & mask);

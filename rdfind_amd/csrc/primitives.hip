@@ -6,7 +6,9 @@
 // digits as cover them (43 bits: 9+9+9+8+8).  Per pass: (1) per-tile digit histogram in LDS, (2) device exclusive
 // scan of the digit-major histogram, (3) stable scatter where each key's in-tile rank comes from wave ballots (one
 // ballot per digit bit gives the peer mask of lanes with the same digit) plus per-wave running digit counters in LDS.
+#include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "primitives.hpp"
 
@@ -14,6 +16,9 @@ namespace rdf {
 
 // ------------------------------------------------------------------------------------------------
 // Block-level helpers
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 
 template <typename T>
 __device__ inline T block_exclusive_scan(T v, T* lds_wave, T* total) {
@@ -187,6 +192,96 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_scan_small(const TI* in, TO* out,
     if (threadIdx.x == 0 && grand_total) *grand_total = carry;
 }
 
+// u32 inputs, 16-B aligned in and out: each lane scans 16 consecutive items it loads and stores as 16-B vectors, so the
+// tile needs no LDS transposition (the strided LDS reads of k_scan_apply conflict) and a wave's accesses are 4x fewer
+#ifndef RDF_SCAN_VEC
+#define RDF_SCAN_VEC 1
+#endif
+__device__ inline void scan_load16(const u32* __restrict__ in, u64 n, u64 tb, u32 (&v)[SCAN_ITEMS]) {
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; i += 4) {
+        if (tb + i + 4 <= n) {
+            const u32x4_t x = *(const u32x4_t*)(in + tb + i);
+            v[i] = x.x;
+            v[i + 1] = x.y;
+            v[i + 2] = x.z;
+            v[i + 3] = x.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[i + j] = tb + i + j < n ? in[tb + i + j] : 0u;
+        }
+    }
+}
+// out[tb + i] = off + (v[0] + .. + v[i-1])
+__device__ inline void scan_store16(u32* __restrict__ out, u64 n, u64 tb, const u32 (&v)[SCAN_ITEMS], u32 off) {
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; i += 4) {
+        u32x4_t x;
+        x.x = off;
+        x.y = x.x + v[i];
+        x.z = x.y + v[i + 1];
+        x.w = x.z + v[i + 2];
+        off = x.w + v[i + 3];
+        if (tb + i + 4 <= n) {
+            *(u32x4_t*)(out + tb + i) = x;
+        } else {
+            if (tb + i < n) out[tb + i] = x.x;
+            if (tb + i + 1 < n) out[tb + i + 1] = x.y;
+            if (tb + i + 2 < n) out[tb + i + 2] = x.z;
+        }
+    }
+}
+__device__ inline void scan_store16(u64* __restrict__ out, u64 n, u64 tb, const u32 (&v)[SCAN_ITEMS], u64 off) {
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; i += 2) {
+        u64x2_t x;
+        x.x = off;
+        x.y = off + v[i];
+        off = x.y + v[i + 1];
+        if (tb + i + 2 <= n) *(u64x2_t*)(out + tb + i) = x;
+        else if (tb + i < n) out[tb + i] = x.x;
+    }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_reduce_v(const u32* __restrict__ in, u64 n, TO* __restrict__ tile_sums) {
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    u32 v[SCAN_ITEMS];
+    scan_load16(in, n, (u64)blockIdx.x * SCAN_TILE + (u64)threadIdx.x * SCAN_ITEMS, v);
+    TO acc = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) acc += v[i];
+    TO total;
+    block_exclusive_scan<TO>(acc, lds_wave, &total);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+// FOLD: tile_sums are the tiles' totals (each block adds the ones before it; the last writes the grand total);
+// otherwise they are the tiles' offsets
+template <typename TO, bool FOLD>
+__global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply_v(const u32* in, TO* out, u64 n, const TO* __restrict__ tile_sums,
+                                                            TO* __restrict__ grand_total) {
+    __shared__ TO lds_wave[RDF_WAVES_PER_BLOCK];
+    const u64 tb = (u64)blockIdx.x * SCAN_TILE + (u64)threadIdx.x * SCAN_ITEMS;
+    u32 v[SCAN_ITEMS];
+    scan_load16(in, n, tb, v);
+    TO prior;
+    if (FOLD) {
+        TO before = 0;
+        for (u32 t = threadIdx.x; t < blockIdx.x; t += RDF_BLOCK) before += tile_sums[t];
+        block_exclusive_scan<TO>(before, lds_wave, &prior);
+    } else {
+        prior = tile_sums[blockIdx.x];
+    }
+    TO local = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) local += v[i];
+    TO total;
+    const TO off = block_exclusive_scan<TO>(local, lds_wave, &total) + prior;
+    if (FOLD && grand_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *grand_total = prior + total;
+    scan_store16(out, n, tb, v, off);
+}
+
 static constexpr u64 SCAN_SMALL_TILES = 4;  // one 1024-thread block up to 8 or 32 tiles measured no faster (c1 groups 0.23 -> 0.39 ms at 32;
                                            // profiles/r05_scan_small_ab.log)
 
@@ -203,6 +298,20 @@ static hipError_t exclusive_scan_impl(Workspace& ws, const TI* in, TO* out, u64 
     }
     TO* sums = (TO*)ws.scratch(tiles * sizeof(TO), 0);
     if (!sums) return hipErrorOutOfMemory;
+    if constexpr (std::is_same<TI, u32>::value) {
+        if (RDF_SCAN_VEC && (((uintptr_t)in | (uintptr_t)out) & 15) == 0) {
+            hipLaunchKernelGGL((k_scan_reduce_v<TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, n, sums);
+            if (tiles <= SCAN_FOLD_TILES) {
+                hipLaunchKernelGGL((k_scan_apply_v<TO, true>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n, sums,
+                                   d_total);
+                return hipGetLastError();
+            }
+            hipLaunchKernelGGL((k_scan_single<TO>), dim3(1), dim3(RDF_BLOCK), 0, st, sums, tiles, d_total);
+            hipLaunchKernelGGL((k_scan_apply_v<TO, false>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n, sums,
+                               (TO*)nullptr);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, n, sums);
     if (tiles <= SCAN_FOLD_TILES) {
         hipLaunchKernelGGL((k_scan_apply_fold<TI, TO>), dim3((unsigned)tiles), dim3(RDF_BLOCK), 0, st, in, out, n, sums,
@@ -220,51 +329,70 @@ struct ScanBatch {
     const u32* in[SCAN_BATCH_MAX];
     u64* out[SCAN_BATCH_MAX];
 };
+template <bool VEC>
 __global__ __launch_bounds__(RDF_BLOCK) void k_scan_reduce_batch(ScanBatch b, u64 n, u64* __restrict__ tile_sums) {
     __shared__ u64 lds_wave[RDF_WAVES_PER_BLOCK];
     const u32* in = b.in[blockIdx.y];
     const u64 base = (u64)blockIdx.x * SCAN_TILE;
     u64 acc = 0;
+    if (VEC) {
+        u32 v[SCAN_ITEMS];
+        scan_load16(in, n, base + (u64)threadIdx.x * SCAN_ITEMS, v);
 #pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
-        if (idx < n) acc += in[idx];
+        for (int i = 0; i < SCAN_ITEMS; ++i) acc += v[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+            if (idx < n) acc += in[idx];
+        }
     }
     u64 total;
     block_exclusive_scan<u64>(acc, lds_wave, &total);
     if (threadIdx.x == 0) tile_sums[(u64)blockIdx.y * gridDim.x + blockIdx.x] = total;
 }
+template <bool VEC>
 __global__ __launch_bounds__(RDF_BLOCK) void k_scan_apply_fold_batch(ScanBatch b, u64 n, const u64* __restrict__ tile_sums) {
-    __shared__ u64 lds[SCAN_TILE];
+    __shared__ u64 lds[VEC ? 1 : SCAN_TILE];
     __shared__ u64 lds_wave[RDF_WAVES_PER_BLOCK];
     const u32* in = b.in[blockIdx.y];
     u64* out = b.out[blockIdx.y];
     const u64* sums = tile_sums + (u64)blockIdx.y * gridDim.x;
     const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    const u64 tb = base + (u64)threadIdx.x * SCAN_ITEMS;
+    u32 vv[SCAN_ITEMS];
+    if (VEC) {
+        scan_load16(in, n, tb, vv);
+    } else {
 #pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
-        lds[i * RDF_BLOCK + threadIdx.x] = idx < n ? (u64)in[idx] : 0ull;
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            u64 idx = base + (u64)i * RDF_BLOCK + threadIdx.x;
+            lds[i * RDF_BLOCK + threadIdx.x] = idx < n ? (u64)in[idx] : 0ull;
+        }
     }
     u64 before = 0;
     for (u32 t = threadIdx.x; t < blockIdx.x; t += RDF_BLOCK) before += sums[t];
     u64 prior;
-    block_exclusive_scan<u64>(before, lds_wave, &prior);
+    block_exclusive_scan<u64>(before, lds_wave, &prior);  // (its barriers also order the LDS tile's stores)
     u64 v[SCAN_ITEMS];
     u64 local = 0;
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) {
-        v[i] = lds[threadIdx.x * SCAN_ITEMS + i];
+        v[i] = VEC ? (u64)vv[i] : lds[threadIdx.x * SCAN_ITEMS + i];
         local += v[i];
     }
     u64 total;
     u64 off = block_exclusive_scan<u64>(local, lds_wave, &total) + prior;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = prior + total;
+    if (VEC) {
+        scan_store16(out, n, tb, vv, off);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) {
         lds[threadIdx.x * SCAN_ITEMS + i] = off;
         off += v[i];
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = prior + total;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) {
@@ -291,8 +419,15 @@ hipError_t exclusive_scan_u32_u64_batch(Workspace& ws, const u32* const* in, u64
     }
     u64* sums = (u64*)ws.scratch(tiles * k * sizeof(u64), 0);
     if (!sums) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(k_scan_reduce_batch, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
-    hipLaunchKernelGGL(k_scan_apply_fold_batch, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
+    uintptr_t align = 0;
+    for (int j = 0; j < k; ++j) align |= (uintptr_t)in[j] | (uintptr_t)out[j];
+    if (RDF_SCAN_VEC && (align & 15) == 0) {
+        hipLaunchKernelGGL(k_scan_reduce_batch<true>, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
+        hipLaunchKernelGGL(k_scan_apply_fold_batch<true>, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_scan_reduce_batch<false>, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
+    hipLaunchKernelGGL(k_scan_apply_fold_batch<false>, dim3((unsigned)tiles, (unsigned)k), dim3(RDF_BLOCK), 0, st, b, n, sums);
     return hipGetLastError();
 }
 
@@ -526,7 +661,6 @@ __global__ __launch_bounds__(RDF_BLOCK) void k_radix_scatter(const KT* __restric
 // each in reduce / single / apply)
 static constexpr int RS_SCAN_THREADS = 1024;
 static constexpr int RS_SCAN_ITEMS = 16;
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(RS_SCAN_THREADS) void k_radix_rowscan(u32* __restrict__ hist, u32 row_stride, u32 num_tiles,
                                                                    u32* rowtot) {
     constexpr int NW = RS_SCAN_THREADS / RDF_WAVE;

@@ -1248,9 +1248,9 @@ static rdf_status fc_binary_index(rdf_ctx* c, u64 B) {
             hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, jb, 1);
     }
     c->lcap = next_pow2(2 * B + 16);
-    ENSURE(c, lkeys, c->lcap * 8);
-    ENSURE(c, lvals, c->lcap * 4);
-    HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, c->lcap * 8, st));
+    ENSURE(c, lkeys, c->lcap * (RDF_LOOKUP_SLOT16 ? 16 : 8));
+    ENSURE(c, lvals, RDF_LOOKUP_SLOT16 ? 4 : c->lcap * 4);
+    HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, c->lcap * (RDF_LOOKUP_SLOT16 ? 16 : 8), st));
     if (B)
         hipLaunchKernelGGL(k_bin_lookup_build, dim3(grid_for(B, RDF_BLOCK, kGrid)), dim3(RDF_BLOCK), 0, st,
                            c->bkeys.as<u64>(), B, c->lkeys.as<u64>(), c->lvals.as<u32>(), c->lcap - 1);
