@@ -781,7 +781,10 @@ static constexpr u32 JH_BUCKETS = 1u << JH_BITS;  // join buckets of the join-ra
 // (element step * U * T + u * T + thread: every load instruction stays coalesced).  One element per thread per step
 // kept ~16 KB in flight per CU, which at 10^9-triple sizes (arrays far beyond the MALL) held these kernels near
 // 1.5-2 TB/s.
-static constexpr int STREAM_U = 4;
+#ifndef RDF_STREAM_U
+#define RDF_STREAM_U 4
+#endif
+static constexpr int STREAM_U = RDF_STREAM_U;
 
 static constexpr u64 CSTART_GAP = 64;  // run starts a k_fresh_bounds thread writes per gap of absent captures
 __global__ __launch_bounds__(RDF_BLOCK) void k_fresh_bounds(const u64* __restrict__ keys, u64 n, u64 ncap, int joinbits,

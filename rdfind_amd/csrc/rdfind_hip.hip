@@ -449,7 +449,10 @@ static rdf_status load_bkeys(rdf_ctx* c) {
     return RDF_OK;
 }
 
-static const unsigned kGrid = 2048;  // grid-stride kernels: 8 blocks of 256 threads per CU
+#ifndef RDF_KGRID
+#define RDF_KGRID 2048
+#endif
+static const unsigned kGrid = RDF_KGRID;  // grid-stride kernels: 8 blocks of 256 threads per CU
 // work-item kernels loop over virtual blocks: a dispatch holds < 2^32 work-items in x, so grids are capped
 static const u64 kMaxBlocks = 1ull << 20;
 static inline unsigned vgrid(u64 blocks) { return (unsigned)std::min<u64>(std::max<u64>(blocks, 1), kMaxBlocks); }
@@ -1492,7 +1495,19 @@ static JoinSel shard_sel(const rdf_ctx* c) {
 // range k) keeps the scanned per-block offsets and the slot count, the second (cache = -1 - k) reuses them instead of
 // re-running the count pass and its scan and read-back.  cache = 0: no reuse.
 // a range's cached block offsets: one fixed-size slot per range (the grid follows a range's entry count, <= kGrid)
-static constexpr u64 ECACHE_STRIDE = kGrid + 1ull;
+// the emission kernels' grid (K3): 8192 blocks, 4x the grid-stride kernels' (c2 emit 0.72 -> 0.63 ms, c4 at 0.4
+// 40.8 -> 37.0 ms; a larger grid for every kernel cost K2 and the heavy mask as much; profiles/r06_emit_grid_ab.log)
+#ifndef RDF_EMIT_GRID
+#define RDF_EMIT_GRID 8192
+#endif
+static const unsigned kEmitGrid = RDF_EMIT_GRID;
+// the join-range emission's grid (k_emit_join_bhist + k_emit_ranges): each block keeps a JH_BUCKETS row of the
+// histogram (64 KB), so its grid stays at the grid-stride cap unless measured otherwise
+#ifndef RDF_RANGE_EMIT_GRID
+#define RDF_RANGE_EMIT_GRID 2048
+#endif
+static const unsigned kRangeEmitGrid = RDF_RANGE_EMIT_GRID;
+static constexpr u64 ECACHE_STRIDE = RDF_EMIT_GRID + 1ull;
 static rdf_status g_sort_support(rdf_ctx* c, u64* keys, u64* tmp, u64 Je, u32* sup, u64* Jout, u64* keep_out);
 static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u32* sup, u64* Jout, int cache = 0) {
     hipStream_t st = c->stream;
@@ -1508,7 +1523,7 @@ static rdf_status g_emit_range(rdf_ctx* c, int proj, JoinSel js, u64 cap_rec, u3
     const int slot = cache > 0 ? cache - 1 : cache < 0 ? -cache - 1 : -1;
     // the selection takes a part of the join values (a join range, or a rank's shard): lazy condition-rank loads
     const bool lazy = js.nranks > 1 || js.lo != 0u || js.hi != JOIN_ALL_HI;
-    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const unsigned eg = grid_for(n, RDF_BLOCK, kEmitGrid);
     const u64 per = n ? (n + eg - 1) / eg : 0;
     ENSURE(c, eblk, 2 * (eg + 1ull) * 8);
     const bool reuse = cache < 0 && slot < (int)c->ecache_je.size();
@@ -1840,7 +1855,7 @@ static rdf_status g_emit_all_ranges(rdf_ctx* c, int proj, JoinSel own) {
     lo[2 * nr] = JH_BUCKETS;
     ENSURE(c, jrmap, (2 * nr + 1) * 4ull);
     HIP_TRY(c, ctx_copy(c, c->jrmap.p, lo.data(), (2 * nr + 1) * 4ull, hipMemcpyHostToDevice));
-    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const unsigned eg = grid_for(n, RDF_BLOCK, kRangeEmitGrid);
     const u64 per = n ? (n + eg - 1) / eg : 0;
     const u64 nb = (u64)nr * eg;
     ENSURE(c, eblk, (nb + 1) * 8);
@@ -1898,7 +1913,7 @@ static rdf_status g_ranges_supports(rdf_ctx* c, int proj, u64 max_range, JoinSel
     ENSURE(c, jhist, JH_BUCKETS * 8);
     HIP_TRY(c, hipMemsetAsync(c->jhist.p, 0, JH_BUCKETS * 8, st));
     // the blocks of the emission (g_emit_all_ranges): their bucket histograms give its per-range block offsets
-    const unsigned eg = grid_for(n, RDF_BLOCK, kGrid);
+    const unsigned eg = grid_for(n, RDF_BLOCK, kRangeEmitGrid);
     const u64 per = n ? (n + eg - 1) / eg : 0;
     ENSURE(c, jbh, (u64)eg * JH_BUCKETS * 4);
     tbegin(c, RDF_T_EMIT);
