@@ -1250,7 +1250,10 @@ static rdf_status fc_binary_index(rdf_ctx* c, u64 B) {
         else if (dense)
             hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, jb, 1);
     }
-    c->lcap = next_pow2(2 * B + 16);
+#ifndef RDF_LCAP_QUARTERS  // lookup slots per key, in quarters (8: at most half full)
+#define RDF_LCAP_QUARTERS 8
+#endif
+    c->lcap = next_pow2(RDF_LCAP_QUARTERS * B / 4 + 16);
     ENSURE(c, lkeys, c->lcap * (RDF_LOOKUP_SLOT16 ? 16 : 8));
     ENSURE(c, lvals, RDF_LOOKUP_SLOT16 ? 4 : c->lcap * 4);
     HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, c->lcap * (RDF_LOOKUP_SLOT16 ? 16 : 8), st));
