@@ -252,8 +252,8 @@ def per_rank_balance(dist, world, mine):
 
 
 # the one-GPU c4 step this leg is compared with: round 6 (digit-row scans, K1's radix form, vectorized scans, the wider
-# emission grid), the c4_strong leg of profiles/r06_bench_c2.json (earlier in round 6: 819.6 ms, round 5: 830.8, round 4: 1616)
-C4_ONE_GPU_MS = 789.6
+# emission grid), the c4_strong leg of profiles/r06_bench_c2.json (earlier in round 6: 819.6 and 789.6 ms, round 5: 830.8, round 4: 1616)
+C4_ONE_GPU_MS = 787.9
 
 
 def c4_golden(scale):

@@ -1250,10 +1250,15 @@ static rdf_status fc_binary_index(rdf_ctx* c, u64 B) {
         else if (dense)
             hipLaunchKernelGGL(k_bkey_repack, g, dim3(RDF_BLOCK), 0, st, c->bkeys.as<u64>(), B, jb, 1);
     }
-#ifndef RDF_LCAP_QUARTERS  // lookup slots per key, in quarters (8: at most half full)
-#define RDF_LCAP_QUARTERS 8
+// lookup slots per key, in quarters: 16 = a table at most a quarter full.  Most K3 probes of a triple's pairs miss
+// (the pair is not frequent), and a linear-probing miss at load 1/2 reads ~2.5 slots: at most 1/4 full, c2 emit 0.63 ->
+// 0.58 ms, c3 5.90 -> 5.66, c4 at 0.4 36.5 -> 34.1 (at most 1/2: the old size; profiles/r06_lookup_load_ab.log).  Tables
+// past 2 GB keep the half-full size
+#ifndef RDF_LCAP_QUARTERS
+#define RDF_LCAP_QUARTERS 16
 #endif
     c->lcap = next_pow2(RDF_LCAP_QUARTERS * B / 4 + 16);
+    if (c->lcap * 16 > (2ull << 30)) c->lcap = next_pow2(2 * B + 16);
     ENSURE(c, lkeys, c->lcap * (RDF_LOOKUP_SLOT16 ? 16 : 8));
     ENSURE(c, lvals, RDF_LOOKUP_SLOT16 ? 4 : c->lcap * 4);
     HIP_TRY(c, hipMemsetAsync(c->lkeys.p, 0xff, c->lcap * (RDF_LOOKUP_SLOT16 ? 16 : 8), st));
